@@ -1,0 +1,182 @@
+// rl_cache.hpp — C++ mirror of the reference's backend plugin interface, implemented on
+// the HIP engine (include/rl_hip.h).
+//
+// The reference host code is Go; its toolchain is absent here, so this is the host side
+// above the C ABI, with the same names, argument meaning and error behaviour:
+//   limiter.RateLimitCache{DoLimit, Flush}            src/limiter/cache.go:15-33
+//   limiter.DoLimitResponse                            src/limiter/cache.go:9-12
+//   config.RateLimit / config.RateLimitStats           src/config/config.go:18-32
+//   redis.RedisError (thrown, Go panics)               src/redis/driver.go:6-10
+//   utils.TimeSource                                   src/utils/utilities.go:10-14
+//   redis.NewFixedRateLimitCacheImpl (constructor)     src/redis/fixed_cache_impl.go:128-135
+// DoLimit may be called concurrently from many threads (as grpc-go does); calls are
+// micro-batched by one submitter thread (REDIS_PIPELINE_WINDOW / _LIMIT analogue,
+// src/settings/settings.go:32-33), and the batch order is the serial order.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <future>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "rl_hip.h"
+
+namespace ratelimit {
+
+// pb.RateLimitResponse_RateLimit_Unit / _Code
+enum class Unit : uint32_t { UNKNOWN = 0, SECOND = 1, MINUTE = 2, HOUR = 3, DAY = 4 };
+enum class Code : uint32_t { UNKNOWN = 0, OK = 1, OVER_LIMIT = 2 };
+
+// gostats counter (additive only)
+class Counter {
+ public:
+  void Add(uint64_t d) { v_.fetch_add(d, std::memory_order_relaxed); }
+  uint64_t Value() const { return v_.load(std::memory_order_relaxed); }
+
+ private:
+  std::atomic<uint64_t> v_{0};
+};
+
+// config.RateLimitStats  src/config/config.go:18-23
+struct RateLimitStats {
+  Counter TotalHits, OverLimit, NearLimit, OverLimitWithLocalCache;
+};
+
+// Stats scope: counters are shared by name (`<FullKey>.total_hits` ...), like
+// statsScope.NewCounter returning the existing counter (config_impl.go:64-71,281-289).
+class StatsStore {
+ public:
+  std::shared_ptr<RateLimitStats> Get(const std::string& key);
+
+ private:
+  std::mutex mu_;
+  std::unordered_map<std::string, std::shared_ptr<RateLimitStats>> m_;
+};
+
+// pb.RateLimitResponse_RateLimit
+struct RateLimitLimit {
+  uint32_t RequestsPerUnit = 0;
+  Unit unit = Unit::UNKNOWN;
+};
+
+// config.RateLimit  src/config/config.go:26-32
+struct RateLimit {
+  std::string FullKey;
+  std::shared_ptr<RateLimitStats> Stats;
+  RateLimitLimit Limit;
+  bool SleepOnThrottle = false;
+  bool ReportDetails = false;
+};
+// config.NewRateLimit  src/config/config_impl.go:79-89
+std::shared_ptr<RateLimit> NewRateLimit(uint32_t requests_per_unit, Unit unit, const std::string& key,
+                                        StatsStore& scope, bool sleep_on_throttle, bool report_details);
+
+struct DescriptorEntry {
+  std::string Key, Value;
+};
+struct RateLimitDescriptor {
+  std::vector<DescriptorEntry> Entries;
+};
+// pb.RateLimitRequest
+struct RateLimitRequest {
+  std::string Domain;
+  std::vector<RateLimitDescriptor> Descriptors;
+  uint32_t HitsAddend = 0;
+};
+
+// pb.RateLimitResponse_DescriptorStatus
+struct DescriptorStatus {
+  Code code = Code::UNKNOWN;
+  const RateLimitLimit* CurrentLimit = nullptr;  // nil when no limit applies
+  uint32_t LimitRemaining = 0;
+  bool HasDurationUntilReset = false;
+  int64_t DurationUntilResetSeconds = 0;
+  bool operator==(const DescriptorStatus& o) const;
+};
+
+// limiter.DoLimitResponse  src/limiter/cache.go:9-12
+struct DoLimitResponse {
+  std::vector<DescriptorStatus> DescriptorStatuses;
+  uint32_t ThrottleMillis = 0;
+};
+
+// redis.RedisError — the only backend failure the service recovers
+// (src/service/ratelimit.go:276-281).
+class RedisError : public std::runtime_error {
+ public:
+  explicit RedisError(const std::string& m) : std::runtime_error(m) {}
+};
+
+// utils.TimeSource
+class TimeSource {
+ public:
+  virtual ~TimeSource() = default;
+  virtual int64_t UnixNow() = 0;
+};
+class SystemTimeSource : public TimeSource {
+ public:
+  int64_t UnixNow() override;
+};
+
+// limiter.RateLimitCache  src/limiter/cache.go:15-33
+class RateLimitCache {
+ public:
+  virtual ~RateLimitCache() = default;
+  virtual DoLimitResponse DoLimit(const RateLimitRequest& request,
+                                  const std::vector<std::shared_ptr<RateLimit>>& limits) = 0;
+  virtual void Flush() = 0;
+};
+
+// HIP_* settings (BACKEND_TYPE=hip)
+struct HipSettings {
+  int device = 0;                         // HIP_DEVICES
+  uint32_t log2_slots[4] = {20, 20, 20, 18};  // HIP_TABLE_SLOTS per unit
+  float near_limit_ratio = 0.8f;          // NEAR_LIMIT_RATIO
+  bool local_cache = false;               // LOCAL_CACHE_SIZE_IN_BYTES > 0
+  bool per_second_split = false;          // REDIS_PERSECOND
+  uint32_t batch_window_us = 75;          // HIP_BATCH_WINDOW
+  uint32_t batch_limit = 1u << 16;        // HIP_BATCH_LIMIT (descriptors)
+  uint64_t hash_seed = 0x5ee7ab1e5eedull;
+};
+
+// The HIP backend. Equivalent of redis.NewFixedRateLimitCacheImpl + fixedRateLimitCacheImpl.
+class HipRateLimitCache : public RateLimitCache {
+ public:
+  HipRateLimitCache(const HipSettings& s, std::shared_ptr<TimeSource> time_source);
+  ~HipRateLimitCache() override;
+  DoLimitResponse DoLimit(const RateLimitRequest& request,
+                          const std::vector<std::shared_ptr<RateLimit>>& limits) override;
+  // Flush() is a no-op for the Redis backend (fixed_cache_impl.go:125-126); here it
+  // waits until every enqueued call has been decided.
+  void Flush() override;
+
+ private:
+  struct Call;
+  void submitter();
+  uint32_t rule_id(const RateLimitLimit& l);
+  void run_batch(std::vector<std::shared_ptr<Call>>& calls);
+
+  HipSettings s_;
+  std::shared_ptr<TimeSource> ts_;
+  rl_engine* eng_ = nullptr;
+  std::mutex mu_;
+  std::condition_variable cv_, idle_cv_;
+  std::deque<std::shared_ptr<Call>> q_;
+  size_t inflight_ = 0;
+  bool stop_ = false;
+  std::thread thr_;
+  // rule registry (submitter thread only)
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> rule_ids_;
+  std::vector<rl_rule> rules_;
+  bool rules_dirty_ = false;
+};
+
+}  // namespace ratelimit

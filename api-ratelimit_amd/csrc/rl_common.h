@@ -1,0 +1,145 @@
+// rl_common.h — shared device/host definitions of the HIP rate-limit pipeline.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rl_hip.h"
+
+namespace rlhip {
+
+// ---------------------------------------------------------------------------
+// Key fingerprint. A key is the exact byte string of
+// GenerateCacheKey (src/limiter/cache_key.go:57-68) = prefix || decimal(window_start).
+// The prefix always ends in '_' and the decimal has none, so (prefix bytes,
+// window_start) <-> key string is a bijection; the fingerprint hashes exactly those
+// two parts, plus the unit (each unit has its own key space).
+// Two 64-bit lanes over 8-byte little-endian words (tail zero-padded, length folded
+// in). Each lane step is a bijection of the lane state for a fixed word, so two
+// equal-length prefixes that differ anywhere give different lane-a states.
+// ---------------------------------------------------------------------------
+constexpr uint64_t K0 = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t K1 = 0xC2B2AE3D27D4EB4Full;
+constexpr uint64_t K2 = 0x165667B19E3779F9ull;
+constexpr uint64_t K3 = 0xD6E8FEB86659FD93ull;
+constexpr uint64_t K4 = 0xFF51AFD7ED558CCDull;
+constexpr uint64_t K5 = 0xC4CEB9FE1A85EC53ull;
+
+__host__ __device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__host__ __device__ __forceinline__ uint64_t fmix64(uint64_t x) {
+  x ^= x >> 33; x *= K4; x ^= x >> 33; x *= K5; x ^= x >> 33;
+  return x;
+}
+struct FpState { uint64_t a, b; };
+__host__ __device__ __forceinline__ FpState fp_init(uint32_t len, uint32_t unit, uint64_t seed) {
+  return FpState{seed ^ K0, (seed + K1) ^ ((uint64_t)len << 32) ^ (uint64_t)unit};
+}
+__host__ __device__ __forceinline__ void fp_word(FpState& s, uint64_t w) {
+  s.a = rotl64((s.a ^ w) * K2, 31);
+  s.b = (s.b + w) * K3;
+  s.b ^= s.b >> 29;
+}
+__host__ __device__ __forceinline__ void fp_final(FpState s, uint64_t window_start, uint64_t& hi, uint64_t& lo) {
+  s.a ^= window_start * K1;
+  s.b = (s.b ^ window_start) * K2;
+  hi = fmix64(s.a + rotl64(s.b, 23));
+  lo = fmix64(s.b ^ (s.a * K5));
+}
+
+// Units (rl_hip.h RL_UNIT_*): divider = utils.UnitToDivider (src/utils/utilities.go:19-32)
+__host__ __device__ __forceinline__ uint32_t unit_div(uint32_t unit) {
+  return unit == RL_UNIT_SECOND ? 1u : unit == RL_UNIT_MINUTE ? 60u : unit == RL_UNIT_HOUR ? 3600u : 86400u;
+}
+
+// Sort key: [region:3 | fingerprint.hi >> 3]. region = (unit-1)*2 + (window_index & 1):
+// every (unit, window parity) owns one region of the counter table. ~0 marks nil-limit
+// descriptors, which sort last and are decided without the table.
+constexpr uint64_t NIL_KEY = ~0ull;
+__host__ __device__ __forceinline__ uint64_t make_sort_key(uint32_t region, uint64_t hi) {
+  uint64_t k = ((uint64_t)region << 61) | (hi >> 3);
+  return k == NIL_KEY ? NIL_KEY - 1 : k;
+}
+__host__ __device__ __forceinline__ uint32_t key_region(uint64_t k) { return (uint32_t)(k >> 61); }
+
+// Per-descriptor record written by the fingerprint kernel in arrival order (32 B).
+struct __attribute__((aligned(16))) ItemRec {
+  uint64_t fp_lo;    // low fingerprint lane (identity = (sort key, fp_lo))
+  uint32_t rule;     // rule id or RL_NIL_RULE
+  uint32_t req;      // request index
+  uint32_t h;        // max(1, hits_addend)
+  int32_t now_mod;   // now - window_start (CalculateReset: div - now % div)
+  uint32_t gen;      // window_index + 1 (0 = never-used slot)
+  uint32_t pad;
+};
+
+// Per-descriptor record in sorted order written by the scan kernel (32 B).
+struct __attribute__((aligned(16))) SortedRec {
+  uint64_t P;        // inclusive prefix sum of h within the key's segment
+  uint32_t head;     // sorted position of the segment head; bit31: rule changes within segment so far
+  uint32_t idx;      // arrival index
+  uint32_t rule;
+  uint32_t req;
+  uint32_t h;
+  int32_t now_mod;
+};
+constexpr uint32_t HEAD_MIXED_RULE = 0x80000000u;
+
+// Per-segment decision state written by the leader kernel at the segment head (16 B).
+struct __attribute__((aligned(16))) SegInfo {
+  uint64_t base;     // counter before this batch (INCRBY post-value = base + P)
+  uint32_t freeze;   // SEG_NO_FREEZE, SEG_FROZEN_BEFORE, or the request index R* that froze the key
+  uint32_t pad;
+};
+constexpr uint32_t SEG_NO_FREEZE = 0xFFFFFFFFu;
+constexpr uint32_t SEG_FROZEN_BEFORE = 0xFFFFFFFEu;
+
+// Counter-table slot (32 B). word0 = gen | (fp_lo low 32 bits) << 32 is the claim word.
+struct __attribute__((aligned(32))) Slot {
+  uint64_t ctrl;     // gen (low 32) | tag = (uint32)fp_lo (high 32)
+  uint64_t key;      // sort key (region | fp.hi >> 3)
+  uint32_t fp_lo_hi; // fp_lo >> 32
+  uint32_t flags;    // SLOT_FROZEN: local over-limit cache holds this key
+  uint64_t count;    // Redis counter value (INCRBY semantics, int64 in Redis)
+};
+constexpr uint32_t SLOT_FROZEN = 1u;
+
+// Rule table entry on the device.
+struct __attribute__((aligned(16))) DevRule {
+  uint32_t L;        // requests_per_unit
+  uint32_t near;     // uint32(floor(float64(float32(L) * ratio)))  base_limiter.go:86
+  uint32_t div;      // UnitToDivider
+  uint32_t unit;
+};
+
+// Device error flags (bitmask in EngineCtl.err).
+enum : uint32_t {
+  ERR_TABLE_FULL = 1u,
+  ERR_SPIN = 2u,
+  ERR_NEED_RESORT = 4u,  // a sort-prefix run holds two different fingerprints
+  ERR_BAD_TIME = 8u,
+  ERR_BAD_INPUT = 16u,    // rule id or request index out of range
+  ERR_WINDOW_SPAN = 32u,  // a region saw window generations more than one apart in one batch
+};
+
+// Small device control block, zeroed per batch.
+struct EngineCtl {
+  uint32_t err;
+  uint32_t n_nil;        // nil-limit descriptors (sorted to the tail)
+  uint32_t n_segments;   // unique keys in the batch (U)
+  uint32_t n_inserted;   // new keys inserted
+  uint32_t gen_min[8];   // per region: ~(min window generation) (max of complements; zero-init)
+  uint32_t gen_max[8];
+  uint32_t tile_ctr[32]; // dynamic tile counters per kernel launch slot
+};
+
+// Counter table: 8 regions (unit x window parity), region r has 2^region_log2[r] slots.
+struct TableDesc {
+  Slot* slots;
+  uint64_t region_base[8];  // slot offset of each region
+  uint32_t region_log2[8];
+};
+
+constexpr int RADIX_BITS = 8;
+constexpr int RADIX = 1 << RADIX_BITS;
+constexpr int MAX_PASSES = 16;
+
+}  // namespace rlhip

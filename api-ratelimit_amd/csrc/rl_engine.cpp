@@ -1,0 +1,598 @@
+// rl_engine.cpp — host runtime behind the C ABI in include/rl_hip.h.
+//
+// Owns the HBM counter table, the per-batch scratch, one HIP stream, and the launch
+// sequence of the decision pipeline (rl_kernels.hip). The host path mirrors what
+// fixedRateLimitCacheImpl.DoLimit does around redis PipeDo (src/redis/fixed_cache_impl.go:
+// 91-102): ship the batch, run it, bring the per-descriptor INCRBY outcomes back — except
+// that the decisions themselves are also computed on the device.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rl_common.h"
+#include "rl_hip.h"
+
+namespace rlhip {
+void launch_fingerprint(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint64_t*, ItemRec*,
+                        rl_status*, uint32_t*, int, int, EngineCtl*);
+void launch_histogram(hipStream_t, const uint64_t*, uint32_t, int, int, uint32_t*);
+void launch_hist_scan(hipStream_t, const uint32_t*, uint32_t*, int);
+void launch_fallback_lo_keys(hipStream_t, const ItemRec*, const uint64_t*, uint32_t, uint64_t*, uint32_t*);
+void launch_gather_keys(hipStream_t, const uint64_t*, const uint32_t*, uint32_t, uint64_t*);
+uint32_t sort_tiles(uint32_t n);
+uint32_t scan_tiles(uint32_t n);
+void launch_sort_pass(hipStream_t, const uint64_t*, const uint32_t*, uint64_t*, uint32_t*, uint32_t, int,
+                      const uint32_t*, uint32_t*, uint32_t*, EngineCtl*);
+void launch_scan(hipStream_t, const uint64_t*, const uint32_t*, const ItemRec*, uint32_t, int, int, SortedRec*,
+                 uint64_t*, uint64_t*, uint32_t*, EngineCtl*);
+void launch_leader(hipStream_t, const uint64_t*, const SortedRec*, const ItemRec*, const DevRule*, uint32_t,
+                   const TableDesc&, int, SegInfo*, EngineCtl*);
+void launch_decide(hipStream_t, const SortedRec*, const SegInfo*, const DevRule*, uint32_t, rl_status*, uint32_t*,
+                   EngineCtl*);
+}  // namespace rlhip
+
+using namespace rlhip;
+
+namespace {
+
+enum KernelId {
+  KT_FINGERPRINT, KT_HIST_SCAN, KT_SORT_PASS, KT_SCAN, KT_LEADER, KT_DECIDE, KT_FALLBACK, KT_MEMSET, KT_COUNT
+};
+const char* const kKernelNames[KT_COUNT] = {"k_fingerprint", "k_hist_scan", "k_sort_pass", "k_scan",
+                                            "k_leader",      "k_decide",    "fallback",    "memset"};
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct rl_engine {
+  rl_config cfg{};
+  int lo_bit = 16, npasses = 6;
+  hipStream_t stream = nullptr;
+  std::string err;
+
+  // counter table
+  Slot* table = nullptr;
+  size_t table_slots = 0;
+  TableDesc tab{};
+
+  // rules
+  DevRule* d_rules = nullptr;
+  uint32_t n_rules = 0, rules_cap = 0;
+
+  // host-path input staging (one contiguous region, same layout on host and device)
+  size_t in_bytes = 0;
+  uint8_t* d_in = nullptr;
+  uint8_t* h_in = nullptr;
+  rl_status* d_out = nullptr;
+  uint32_t* d_thr = nullptr;
+  rl_status* h_out = nullptr;
+  uint32_t* h_thr = nullptr;
+
+  // scratch
+  uint64_t *keys_orig = nullptr, *keys_a = nullptr, *keys_b = nullptr;
+  uint32_t *vals_a = nullptr, *vals_b = nullptr;
+  ItemRec* recs = nullptr;
+  SortedRec* srec = nullptr;
+  SegInfo* seg = nullptr;
+  uint32_t* offs = nullptr;
+  uint8_t* zero_block = nullptr;  // ctl | hist | lookbacks (zeroed per batch)
+  size_t zero_cap = 0;
+  EngineCtl* h_ctl = nullptr;     // pinned copy of the control block
+
+  // in-flight batch
+  bool in_flight = false;
+  bool host_path = false;
+  rl_batch dev_batch{};            // device pointers of the in-flight batch
+  rl_status* pend_out_dev = nullptr;
+  uint32_t* pend_thr_dev = nullptr;
+  rl_status* user_out = nullptr;   // host path destinations
+  uint32_t* user_thr = nullptr;
+
+  // timing
+  bool timing = false;
+  struct Mark { int kid; hipEvent_t a, b; };
+  std::vector<Mark> marks;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  double kt_ms[KT_COUNT] = {};
+  uint64_t kt_n[KT_COUNT] = {};
+
+  // stats
+  rl_engine_stats st{};
+  uint64_t last_unique = 0, last_n = 0, last_req = 0, last_blob = 0;
+
+  int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = buf;
+    return code;
+  }
+  int hip_fail(hipError_t e, const char* what) {
+    return fail(RL_EHIP, "%s: %s", what, hipGetErrorString(e));
+  }
+
+  hipEvent_t next_event() {
+    if (ev_used == ev_pool.size()) {
+      hipEvent_t e;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      ev_pool.push_back(e);
+    }
+    return ev_pool[ev_used++];
+  }
+  template <class F>
+  void timed(int kid, F f) {
+    if (!timing) { f(); return; }
+    hipEvent_t a = next_event(), b = next_event();
+    hipEventRecord(a, stream);
+    f();
+    hipEventRecord(b, stream);
+    marks.push_back({kid, a, b});
+  }
+
+  // Layout of the per-batch zero block for n descriptors; returns the bytes used.
+  struct ZLayout { size_t ctl, hist, lb_sort, lb_sum, lb_head, total; };
+  ZLayout zlayout(uint32_t n, int passes) const {
+    ZLayout z;
+    z.ctl = 0;
+    z.hist = align_up(sizeof(EngineCtl), 256);
+    z.lb_sort = z.hist + align_up((size_t)MAX_PASSES * RADIX * 4, 256);
+    z.lb_sum = z.lb_sort + align_up((size_t)passes * sort_tiles(n > 0 ? n : 1) * RADIX * 4, 256);
+    z.lb_head = z.lb_sum + align_up((size_t)scan_tiles(n > 0 ? n : 1) * 8, 256);
+    z.total = z.lb_head + align_up((size_t)scan_tiles(n > 0 ? n : 1) * 8, 256);
+    return z;
+  }
+
+  int run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bool full);
+  int finish();
+  int enqueue_d2h();
+};
+
+int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bool full) {
+  const uint32_t n = b.n_desc;
+  const int passes = full ? 16 : npasses;
+  const ZLayout z = zlayout(n, passes);
+  EngineCtl* ctl = reinterpret_cast<EngineCtl*>(zero_block + z.ctl);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(zero_block + z.hist);
+  uint32_t* lb_sort = reinterpret_cast<uint32_t*>(zero_block + z.lb_sort);
+  uint64_t* lb_sum = reinterpret_cast<uint64_t*>(zero_block + z.lb_sum);
+  uint64_t* lb_head = reinterpret_cast<uint64_t*>(zero_block + z.lb_head);
+  const size_t lb_pass_stride = (size_t)sort_tiles(n > 0 ? n : 1) * RADIX;
+  hipError_t e;
+  timed(KT_MEMSET, [&] {
+    hipMemsetAsync(zero_block, 0, z.total, stream);
+    if (b.n_req) hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
+  });
+  if (n == 0) {
+    e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpyAsync(ctl)");
+  }
+  const uint64_t* skeys;
+  const uint32_t* svals;
+  if (!full) {
+    timed(KT_FINGERPRINT, [&] {
+      launch_fingerprint(stream, b, d_rules, n_rules, cfg.hash_seed, keys_orig, recs, out, hist, lo_bit, npasses,
+                         ctl);
+    });
+    timed(KT_HIST_SCAN, [&] { launch_hist_scan(stream, hist, offs, npasses); });
+    const uint64_t* kin = keys_orig;
+    const uint32_t* vin = nullptr;
+    for (int p = 0; p < npasses; ++p) {
+      uint64_t* kout = (p & 1) ? keys_b : keys_a;
+      uint32_t* vout = (p & 1) ? vals_b : vals_a;
+      timed(KT_SORT_PASS, [&] {
+        launch_sort_pass(stream, kin, vin, kout, vout, n, lo_bit + 8 * p, offs + p * RADIX,
+                         lb_sort + p * lb_pass_stride, &ctl->tile_ctr[p], ctl);
+      });
+      kin = kout;
+      vin = vout;
+    }
+    skeys = kin;
+    svals = vin;
+  } else {
+    // Full-fingerprint order: stable sort by fp_lo, then by the 64-bit sort key.
+    timed(KT_FALLBACK, [&] {
+      launch_fingerprint(stream, b, d_rules, n_rules, cfg.hash_seed, keys_orig, recs, out, hist, 0, 0, ctl);
+      launch_fallback_lo_keys(stream, recs, keys_orig, n, keys_a, vals_a);
+      launch_histogram(stream, keys_a, n, 0, 8, hist);
+      launch_hist_scan(stream, hist, offs, 8);
+    });
+    const uint64_t* kin = keys_a;
+    const uint32_t* vin = vals_a;
+    for (int p = 0; p < 8; ++p) {
+      uint64_t* kout = (p & 1) ? keys_a : keys_b;
+      uint32_t* vout = (p & 1) ? vals_a : vals_b;
+      timed(KT_SORT_PASS, [&] {
+        launch_sort_pass(stream, kin, vin, kout, vout, n, 8 * p, offs + p * RADIX, lb_sort + p * lb_pass_stride,
+                         &ctl->tile_ctr[p], ctl);
+      });
+      kin = kout;
+      vin = vout;
+    }
+    // after 8 passes the result is in keys_a/vals_a; gather the sort keys in that order
+    timed(KT_FALLBACK, [&] {
+      launch_gather_keys(stream, keys_orig, vals_a, n, keys_b);
+      launch_histogram(stream, keys_b, n, 0, 8, hist + 8 * RADIX);
+      launch_hist_scan(stream, hist + 8 * RADIX, offs + 8 * RADIX, 8);
+    });
+    kin = keys_b;
+    vin = vals_a;
+    for (int p = 0; p < 8; ++p) {
+      uint64_t* kout = (p & 1) ? keys_b : keys_a;
+      uint32_t* vout = (p & 1) ? vals_a : vals_b;
+      timed(KT_SORT_PASS, [&] {
+        launch_sort_pass(stream, kin, vin, kout, vout, n, 8 * p, offs + (8 + p) * RADIX,
+                         lb_sort + (8 + p) * lb_pass_stride, &ctl->tile_ctr[8 + p], ctl);
+      });
+      kin = kout;
+      vin = vout;
+    }
+    skeys = kin;
+    svals = vin;
+  }
+  timed(KT_SCAN, [&] {
+    launch_scan(stream, skeys, svals, recs, n, full ? 0 : lo_bit, full ? 0 : 1, srec, lb_sum, lb_head,
+                &ctl->tile_ctr[31], ctl);
+  });
+  timed(KT_LEADER, [&] {
+    launch_leader(stream, skeys, srec, recs, d_rules, n, tab, cfg.local_cache ? 1 : 0, seg, ctl);
+  });
+  timed(KT_DECIDE, [&] { launch_decide(stream, srec, seg, d_rules, n, out, thr, ctl); });
+  e = hipGetLastError();
+  if (e != hipSuccess) return hip_fail(e, "kernel launch");
+  e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(ctl)");
+  return 0;
+}
+
+// Wait for the in-flight batch, run the full-fingerprint re-sort if needed, copy
+// host-path outputs back.
+int rl_engine::finish() {
+  hipError_t e = hipStreamSynchronize(stream);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  uint32_t errs = h_ctl->err;
+  if (errs & ERR_NEED_RESORT) {
+    // A sort-prefix run held two fingerprints: nothing touched the table (k_leader and
+    // k_decide return early), so re-run the batch on the full fingerprint order.
+    ++st.resorts;
+    int rc = run_pipeline(dev_batch, pend_out_dev, pend_thr_dev, true);
+    if (rc) return rc;
+    if (host_path && (rc = enqueue_d2h()) != 0) return rc;
+    e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    errs = h_ctl->err;
+  }
+  if (timing) {
+    for (auto& m : marks) {
+      float ms = 0;
+      hipEventElapsedTime(&ms, m.a, m.b);
+      kt_ms[m.kid] += ms;
+      kt_n[m.kid] += 1;
+    }
+    marks.clear();
+    ev_used = 0;
+  }
+  if (errs & ERR_BAD_INPUT) return fail(RL_EINVAL, "batch references an unknown rule id or request index");
+  if (errs & ERR_BAD_TIME) return fail(RL_EINVAL, "request time outside [0, 2^32) unix seconds");
+  if (errs & ERR_WINDOW_SPAN)
+    return fail(RL_EINVAL, "batch spans more than two windows of one unit; split it at window boundaries");
+  if (errs & ERR_TABLE_FULL) return fail(RL_ENOSPC, "counter table region full (raise log2_slots)");
+  if (errs & ERR_SPIN) return fail(RL_EDEVICE, "device look-back spin limit exceeded");
+  if (errs & ERR_NEED_RESORT) return fail(RL_EDEVICE, "full-fingerprint re-sort still found a mixed run");
+  last_unique = h_ctl->n_segments;
+  last_n = dev_batch.n_desc;
+  last_req = dev_batch.n_req;
+  last_blob = dev_batch.blob_bytes;
+  st.batches += 1;
+  st.descriptors += dev_batch.n_desc;
+  st.live_slots_hint += h_ctl->n_inserted;
+  if (host_path) {
+    if (dev_batch.n_desc) memcpy(user_out, h_out, (size_t)dev_batch.n_desc * sizeof(rl_status));
+    if (dev_batch.n_req) memcpy(user_thr, h_thr, (size_t)dev_batch.n_req * 4);
+  }
+  return 0;
+}
+
+int rl_engine::enqueue_d2h() {
+  hipError_t e;
+  if (dev_batch.n_desc) {
+    e = hipMemcpyAsync(h_out, d_out, (size_t)dev_batch.n_desc * sizeof(rl_status), hipMemcpyDeviceToHost, stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(D2H out)");
+  }
+  if (dev_batch.n_req) {
+    e = hipMemcpyAsync(h_thr, d_thr, (size_t)dev_batch.n_req * 4, hipMemcpyDeviceToHost, stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(D2H thr)");
+  }
+  return 0;
+}
+
+extern "C" {
+
+uint32_t rl_abi_version(void) { return RL_ABI_VERSION; }
+
+const char* rl_last_error(const rl_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+int rl_create(const rl_config* cfg_in, rl_engine** out) {
+  if (!cfg_in || !out) return RL_EINVAL;
+  *out = nullptr;
+  if (cfg_in->struct_size != sizeof(rl_config)) return RL_EINVAL;
+  auto* e = new rl_engine();
+  e->cfg = *cfg_in;
+  rl_config& c = e->cfg;
+  for (int u = 0; u < 4; ++u) {
+    if (c.log2_slots[u] == 0) c.log2_slots[u] = 20;
+    if (c.log2_slots[u] < 4 || c.log2_slots[u] > 34) {
+      delete e;
+      return RL_EINVAL;
+    }
+  }
+  if (c.max_batch_desc == 0) c.max_batch_desc = 1u << 20;
+  if (c.max_batch_req == 0) c.max_batch_req = c.max_batch_desc;
+  if (c.max_blob_bytes == 0) c.max_blob_bytes = c.max_batch_desc * 64u;
+  if (c.max_batch_desc > (1u << 28)) { delete e; return RL_EINVAL; }
+  if (c.sort_bits == 0) c.sort_bits = 48;
+  if (c.sort_bits % 8 || c.sort_bits < 8 || c.sort_bits > 64) { delete e; return RL_EINVAL; }
+  e->npasses = (int)c.sort_bits / 8;
+  e->lo_bit = 64 - (int)c.sort_bits;
+  hipError_t he = hipSetDevice(c.device);
+  if (he != hipSuccess) { delete e; return RL_EHIP; }
+  auto chk = [&](hipError_t x) { if (x != hipSuccess && he == hipSuccess) he = x; };
+  chk(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  // counter table: 8 regions (unit x window parity)
+  size_t off = 0;
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t lg = c.log2_slots[r / 2];
+    e->tab.region_base[r] = off;
+    e->tab.region_log2[r] = lg;
+    off += (size_t)1 << lg;
+  }
+  e->table_slots = off;
+  chk(hipMalloc(&e->table, off * sizeof(Slot)));
+  if (he == hipSuccess) chk(hipMemset(e->table, 0, off * sizeof(Slot)));
+  e->tab.slots = e->table;
+  const size_t N = c.max_batch_desc, R = c.max_batch_req, B = c.max_blob_bytes;
+  // input staging: blob | off | rule | req | now | hits
+  e->in_bytes = align_up(B + 16, 256) + align_up((N + 1) * 4, 256) + 2 * align_up(N * 4, 256) + align_up(R * 8, 256) +
+                align_up(R * 4, 256);
+  chk(hipMalloc(&e->d_in, e->in_bytes));
+  chk(hipHostMalloc(&e->h_in, e->in_bytes, hipHostMallocDefault));
+  chk(hipMalloc(&e->d_out, N * sizeof(rl_status)));
+  chk(hipMalloc(&e->d_thr, R * 4));
+  chk(hipHostMalloc(&e->h_out, N * sizeof(rl_status), hipHostMallocDefault));
+  chk(hipHostMalloc(&e->h_thr, R * 4, hipHostMallocDefault));
+  chk(hipMalloc(&e->keys_orig, N * 8));
+  chk(hipMalloc(&e->keys_a, N * 8));
+  chk(hipMalloc(&e->keys_b, N * 8));
+  chk(hipMalloc(&e->vals_a, N * 4));
+  chk(hipMalloc(&e->vals_b, N * 4));
+  chk(hipMalloc(&e->recs, N * sizeof(ItemRec)));
+  chk(hipMalloc(&e->srec, N * sizeof(SortedRec)));
+  chk(hipMalloc(&e->seg, N * sizeof(SegInfo)));
+  chk(hipMalloc(&e->offs, (size_t)MAX_PASSES * RADIX * 4));
+  e->zero_cap = e->zlayout((uint32_t)N, MAX_PASSES).total;
+  chk(hipMalloc(&e->zero_block, e->zero_cap));
+  chk(hipHostMalloc(&e->h_ctl, sizeof(EngineCtl), hipHostMallocDefault));
+  if (he == hipSuccess) chk(hipMemset(e->zero_block, 0, e->zero_cap));
+  if (he == hipSuccess) chk(hipDeviceSynchronize());
+  if (he != hipSuccess) {
+    rl_destroy(e);
+    return RL_EHIP;
+  }
+  *out = e;
+  return 0;
+}
+
+void rl_destroy(rl_engine* e) {
+  if (!e) return;
+  if (e->stream) hipStreamSynchronize(e->stream);
+  for (auto ev : e->ev_pool) hipEventDestroy(ev);
+  hipFree(e->table);
+  hipFree(e->d_rules);
+  hipFree(e->d_in);
+  hipHostFree(e->h_in);
+  hipFree(e->d_out);
+  hipFree(e->d_thr);
+  hipHostFree(e->h_out);
+  hipHostFree(e->h_thr);
+  hipFree(e->keys_orig);
+  hipFree(e->keys_a);
+  hipFree(e->keys_b);
+  hipFree(e->vals_a);
+  hipFree(e->vals_b);
+  hipFree(e->recs);
+  hipFree(e->srec);
+  hipFree(e->seg);
+  hipFree(e->offs);
+  hipFree(e->zero_block);
+  hipHostFree(e->h_ctl);
+  if (e->stream) hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int rl_load_rules(rl_engine* e, const rl_rule* rules, uint32_t n) {
+  if (!e) return RL_EINVAL;
+  if (e->in_flight) return e->fail(RL_ESTATE, "rl_load_rules while a batch is in flight");
+  std::vector<DevRule> h(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t u = rules[i].unit;
+    if (u < RL_UNIT_SECOND || u > RL_UNIT_DAY)
+      return e->fail(RL_EINVAL, "rule %u: unit %u is not SECOND/MINUTE/HOUR/DAY (utilities.go:31 panics)", i, u);
+    h[i].L = rules[i].requests_per_unit;
+    // nearLimitThreshold = uint32(math.Floor(float64(float32(L) * nearLimitRatio)))  base_limiter.go:86
+    const float p = (float)rules[i].requests_per_unit * e->cfg.near_limit_ratio;
+    h[i].near = (uint32_t)std::floor((double)p);
+    h[i].div = unit_div(u);
+    h[i].unit = u;
+  }
+  if (n > e->rules_cap) {
+    hipFree(e->d_rules);
+    e->d_rules = nullptr;
+    const uint32_t cap = n < 16 ? 16 : n;
+    hipError_t he = hipMalloc(&e->d_rules, (size_t)cap * sizeof(DevRule));
+    if (he != hipSuccess) return e->hip_fail(he, "hipMalloc(rules)");
+    e->rules_cap = cap;
+  }
+  if (!e->d_rules) {
+    hipError_t he = hipMalloc(&e->d_rules, 16 * sizeof(DevRule));
+    if (he != hipSuccess) return e->hip_fail(he, "hipMalloc(rules)");
+    e->rules_cap = 16;
+  }
+  if (n) {
+    hipError_t he = hipMemcpy(e->d_rules, h.data(), (size_t)n * sizeof(DevRule), hipMemcpyHostToDevice);
+    if (he != hipSuccess) return e->hip_fail(he, "hipMemcpy(rules)");
+  }
+  e->n_rules = n;
+  return 0;
+}
+
+int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_throttle_ms) {
+  if (!e || !b) return RL_EINVAL;
+  if (e->in_flight) return e->fail(RL_ESTATE, "rl_submit while a batch is in flight (call rl_wait)");
+  const rl_config& c = e->cfg;
+  if (b->n_desc > c.max_batch_desc || b->n_req > c.max_batch_req || b->blob_bytes > c.max_blob_bytes)
+    return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req, %u blob bytes)", c.max_batch_desc,
+                   c.max_batch_req, c.max_blob_bytes);
+  if (!e->d_rules) rl_load_rules(e, nullptr, 0);
+  // Host-side validation of the batch layout.
+  if (b->n_desc && (!b->prefix_off || !b->rule_id || !b->req_of || !out))
+    return e->fail(RL_EINVAL, "null descriptor array");
+  if (b->n_req && (!b->now || !b->hits_addend || !req_throttle_ms)) return e->fail(RL_EINVAL, "null request array");
+  if (b->n_desc) {
+    if (b->prefix_off[b->n_desc] > b->blob_bytes) return e->fail(RL_EINVAL, "prefix offsets exceed blob");
+    for (uint32_t i = 0; i < b->n_desc; ++i) {
+      if (b->prefix_off[i + 1] < b->prefix_off[i]) return e->fail(RL_EINVAL, "prefix offsets not monotone at %u", i);
+      if (b->req_of[i] >= b->n_req || (i && b->req_of[i] < b->req_of[i - 1]))
+        return e->fail(RL_EINVAL, "req_of not non-decreasing / in range at %u", i);
+      if (b->rule_id[i] != RL_NIL_RULE && b->rule_id[i] >= e->n_rules)
+        return e->fail(RL_EINVAL, "unknown rule id %u at %u", b->rule_id[i], i);
+    }
+  }
+  // Stage into pinned memory with the device layout, one H2D copy.
+  const size_t N = c.max_batch_desc, B = c.max_blob_bytes;
+  uint8_t* h = e->h_in;
+  size_t o_blob = 0, o_off = align_up(B + 16, 256), o_rule = o_off + align_up((N + 1) * 4, 256),
+         o_req = o_rule + align_up(N * 4, 256), o_now = o_req + align_up(N * 4, 256),
+         o_hits = o_now + align_up((size_t)c.max_batch_req * 8, 256);
+  if (b->blob_bytes) memcpy(h + o_blob, b->prefix_blob, b->blob_bytes);
+  memset(h + o_blob + b->blob_bytes, 0, 16);
+  if (b->n_desc) {
+    memcpy(h + o_off, b->prefix_off, ((size_t)b->n_desc + 1) * 4);
+    memcpy(h + o_rule, b->rule_id, (size_t)b->n_desc * 4);
+    memcpy(h + o_req, b->req_of, (size_t)b->n_desc * 4);
+  }
+  if (b->n_req) {
+    memcpy(h + o_now, b->now, (size_t)b->n_req * 8);
+    memcpy(h + o_hits, b->hits_addend, (size_t)b->n_req * 4);
+  }
+  hipError_t he;
+  // Copy only the used extents of each array.
+  struct Seg { size_t o, n; } segs[] = {{o_blob, (size_t)b->blob_bytes + 16},
+                                        {o_off, ((size_t)b->n_desc + 1) * 4},
+                                        {o_rule, (size_t)b->n_desc * 4},
+                                        {o_req, (size_t)b->n_desc * 4},
+                                        {o_now, (size_t)b->n_req * 8},
+                                        {o_hits, (size_t)b->n_req * 4}};
+  for (auto& s : segs) {
+    if (!s.n) continue;
+    he = hipMemcpyAsync(e->d_in + s.o, h + s.o, s.n, hipMemcpyHostToDevice, e->stream);
+    if (he != hipSuccess) return e->hip_fail(he, "hipMemcpyAsync(H2D)");
+  }
+  rl_batch d = *b;
+  d.prefix_blob = e->d_in + o_blob;
+  d.prefix_off = reinterpret_cast<const uint32_t*>(e->d_in + o_off);
+  d.rule_id = reinterpret_cast<const uint32_t*>(e->d_in + o_rule);
+  d.req_of = reinterpret_cast<const uint32_t*>(e->d_in + o_req);
+  d.now = reinterpret_cast<const int64_t*>(e->d_in + o_now);
+  d.hits_addend = reinterpret_cast<const uint32_t*>(e->d_in + o_hits);
+  int rc = e->run_pipeline(d, e->d_out, e->d_thr, false);
+  if (rc) return rc;
+  e->dev_batch = d;
+  e->pend_out_dev = e->d_out;
+  e->pend_thr_dev = e->d_thr;
+  e->user_out = out;
+  e->user_thr = req_throttle_ms;
+  e->host_path = true;
+  if ((rc = e->enqueue_d2h()) != 0) return rc;
+  e->in_flight = true;
+  return 0;
+}
+
+int rl_wait(rl_engine* e) {
+  if (!e) return RL_EINVAL;
+  if (!e->in_flight) return e->fail(RL_ESTATE, "rl_wait without a batch in flight");
+  e->in_flight = false;
+  return e->finish();
+}
+
+int rl_submit_device(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t* d_req_throttle_ms) {
+  if (!e || !b) return RL_EINVAL;
+  if (e->in_flight) return e->fail(RL_ESTATE, "rl_submit_device while a batch is in flight (call rl_wait)");
+  const rl_config& c = e->cfg;
+  if (b->n_desc > c.max_batch_desc || b->n_req > c.max_batch_req)
+    return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req)", c.max_batch_desc,
+                   c.max_batch_req);
+  if (!e->d_rules) rl_load_rules(e, nullptr, 0);
+  int rc = e->run_pipeline(*b, d_out, d_req_throttle_ms, false);
+  if (rc) return rc;
+  e->dev_batch = *b;
+  e->pend_out_dev = d_out;
+  e->pend_thr_dev = d_req_throttle_ms;
+  e->host_path = false;
+  e->in_flight = true;
+  return 0;
+}
+
+void* rl_stream(rl_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int rl_reset(rl_engine* e) {
+  if (!e) return RL_EINVAL;
+  if (e->in_flight) return e->fail(RL_ESTATE, "rl_reset while a batch is in flight");
+  hipError_t he = hipMemsetAsync(e->table, 0, e->table_slots * sizeof(Slot), e->stream);
+  if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+  return he == hipSuccess ? 0 : e->hip_fail(he, "rl_reset");
+}
+
+int rl_get_stats(rl_engine* e, rl_engine_stats* s) {
+  if (!e || !s) return RL_EINVAL;
+  *s = e->st;
+  return 0;
+}
+
+int rl_set_timing(rl_engine* e, int on) {
+  if (!e) return RL_EINVAL;
+  e->timing = on != 0;
+  for (int k = 0; k < KT_COUNT; ++k) { e->kt_ms[k] = 0; e->kt_n[k] = 0; }
+  return 0;
+}
+
+int rl_kernel_times(rl_engine* e, const char** names, double* total_ms, uint64_t* launches, uint32_t cap,
+                    uint32_t* n_out) {
+  if (!e) return RL_EINVAL;
+  uint32_t n = 0;
+  for (int k = 0; k < KT_COUNT && n < cap; ++k, ++n) {
+    if (names) names[n] = kKernelNames[k];
+    if (total_ms) total_ms[n] = e->kt_ms[k];
+    if (launches) launches[n] = e->kt_n[k];
+  }
+  if (n_out) *n_out = n;
+  return 0;
+}
+
+int rl_last_batch_info(rl_engine* e, uint64_t* unique_keys, uint64_t* n_desc, uint64_t* n_req, uint64_t* blob_bytes) {
+  if (!e) return RL_EINVAL;
+  if (unique_keys) *unique_keys = e->last_unique;
+  if (n_desc) *n_desc = e->last_n;
+  if (n_req) *n_req = e->last_req;
+  if (blob_bytes) *blob_bytes = e->last_blob;
+  return 0;
+}
+
+}  // extern "C"

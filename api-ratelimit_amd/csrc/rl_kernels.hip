@@ -1,0 +1,834 @@
+// rl_kernels.hip — CDNA4 (gfx950) kernels of the batched fixed-window decision path.
+//
+// One batch = descriptors of many RateLimitRequests in serial (enqueue) order. The
+// pipeline reproduces, per key, the counter value that a pipelined Redis INCRBY would
+// return in that order (src/redis/fixed_cache_impl.go:26-29,55-102) and the decisions
+// of BaseRateLimiter.GetResponseDescriptorStatus (src/limiter/base_limiter.go:70-177):
+//
+//   k_fingerprint  hash each key prefix + window start -> 128-bit fingerprint, sort key,
+//                  arrival-order record; radix histograms for every sort pass
+//   k_hist_scan    exclusive scan of the digit histograms
+//   k_sort_pass    stable LSD radix pass (8-bit digit) with decoupled look-back (xN)
+//   k_scan         segment heads + segmented inclusive prefix sum of hits_addend
+//                  (decoupled look-back), sorted-order record
+//   k_leader       one thread per unique key: probe/insert the HBM counter table,
+//                  find the local-cache freeze point, write the new counter
+//   k_decide       per descriptor: INCRBY post-value = base + prefix, status + stats
+//
+// Wave size is 64 everywhere; blocks are 256 threads (4 waves).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rl_common.h"
+
+namespace rlhip {
+
+#define RL_DEV __device__ __forceinline__
+
+RL_DEV uint32_t ld_relaxed(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+RL_DEV uint64_t ld_relaxed64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+RL_DEV void st_relaxed(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+RL_DEV void st_relaxed64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+RL_DEV uint64_t lanemask_lt() {
+  const uint32_t lane = __lane_id();
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+constexpr uint32_t SPIN_LIMIT = 1u << 24;
+
+// ---------------------------------------------------------------------------
+// k_fingerprint
+// ---------------------------------------------------------------------------
+struct DevBatch {
+  uint32_t n_desc, n_req, blob_bytes, pad;
+  const uint8_t* blob;
+  const uint32_t* off;
+  const uint32_t* rule;
+  const uint32_t* req_of;
+  const int64_t* now;
+  const uint32_t* hits;
+};
+
+// Unaligned little-endian 8-byte words of a byte string, read as aligned dwords and
+// funnel-shifted (v_alignbyte_b32). The blob has >= 16 bytes of slack past its end.
+RL_DEV void hash_prefix(const uint8_t* blob, uint32_t off, uint32_t len, FpState& s) {
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(blob + (off & ~3u));
+  const uint32_t sh = (off & 3u) * 8u;
+  uint32_t d0 = p[0];
+  uint32_t rem = len;
+  for (uint32_t k = 0; rem > 0; ++k) {
+    const uint32_t d1 = p[2 * k + 1];
+    const uint32_t d2 = p[2 * k + 2];
+    uint32_t lo = sh ? __builtin_amdgcn_alignbyte(d1, d0, sh / 8) : d0;
+    uint32_t hi = sh ? __builtin_amdgcn_alignbyte(d2, d1, sh / 8) : d1;
+    uint64_t w = ((uint64_t)hi << 32) | lo;
+    if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
+    fp_word(s, w);
+    d0 = d2;
+    rem = rem > 8 ? rem - 8 : 0;
+  }
+}
+
+RL_DEV int64_t div_const(int64_t now, uint32_t unit) {
+  switch (unit) {
+    case RL_UNIT_SECOND: return now;
+    case RL_UNIT_MINUTE: return now / 60;
+    case RL_UNIT_HOUR: return now / 3600;
+    default: return now / 86400;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
+                                                     uint64_t seed, uint64_t* __restrict__ keys_orig,
+                                                     ItemRec* __restrict__ recs, rl_status* __restrict__ out,
+                                                     uint32_t* __restrict__ hist, int lo_bit, int npasses,
+                                                     EngineCtl* ctl) {
+  __shared__ uint32_t sh_hist[8][RADIX];
+  __shared__ uint32_t sh_nil;
+  __shared__ uint32_t sh_err;
+  __shared__ uint32_t sh_gmin[8], sh_gmax[8];
+  const uint32_t tid = threadIdx.x;
+  for (int i = tid; i < 8 * RADIX; i += 256) (&sh_hist[0][0])[i] = 0;
+  if (tid < 8) { sh_gmin[tid] = 0; sh_gmax[tid] = 0; }  // gmin holds ~min (zero-init max)
+  if (tid == 0) { sh_nil = 0; sh_err = 0; }
+  __syncthreads();
+
+  const uint32_t i = blockIdx.x * 256 + tid;
+  uint32_t err = 0;
+  bool nil = true;
+  uint64_t key = NIL_KEY;
+  if (i < in.n_desc) {
+    const uint32_t r = in.rule[i];
+    const uint32_t q = in.req_of[i];
+    const bool q_ok = q < in.n_req;
+    const int64_t now = q_ok ? in.now[q] : 0;
+    const uint32_t ha = q_ok ? in.hits[q] : 1u;
+    ItemRec rec;
+    rec.rule = r;
+    rec.req = q;
+    rec.h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
+    rec.fp_lo = 0;
+    rec.now_mod = 0;
+    rec.gen = 0;
+    rec.pad = 0;
+    if (r != RL_NIL_RULE && (r >= n_rules || q >= in.n_req)) err |= ERR_BAD_INPUT;
+    if (r != RL_NIL_RULE && r < n_rules && q < in.n_req) {
+      if (now < 0 || now > 0xFFFFFFF0ll) {
+        err |= ERR_BAD_TIME;
+      } else {
+        const DevRule R = rules[r];
+        const int64_t widx = div_const(now, R.unit);
+        const int64_t ws = widx * (int64_t)R.div;  // (now/divider)*divider  cache_key.go:66-68
+        const uint32_t o0 = in.off[i], o1 = in.off[i + 1];
+        FpState s = fp_init(o1 - o0, R.unit, seed);
+        hash_prefix(in.blob, o0, o1 - o0, s);
+        uint64_t hi, lo;
+        fp_final(s, (uint64_t)ws, hi, lo);
+        const uint32_t region = (R.unit - 1u) * 2u + (uint32_t)(widx & 1);
+        key = make_sort_key(region, hi);
+        rec.fp_lo = lo;
+        rec.now_mod = (int32_t)(now - ws);
+        rec.gen = (uint32_t)widx + 1u;
+        atomicMax(&sh_gmin[region], ~rec.gen);
+        atomicMax(&sh_gmax[region], rec.gen);
+        nil = false;
+      }
+    }
+    recs[i] = rec;
+    keys_orig[i] = key;
+    if (nil) {
+      // GetResponseDescriptorStatus("" key) -> {OK, nil limit, 0}  base_limiter.go:72-75
+      rl_status st;
+      st.code_flags = RL_CODE_OK;
+      st.limit_remaining = 0;
+      st.reset_s = 0;
+      st.over_limit_delta = 0;
+      st.near_limit_delta = 0;
+      out[i] = st;
+      atomicAdd(&sh_nil, 1u);
+    }
+    for (int p = 0; p < npasses; ++p) atomicAdd(&sh_hist[p][(key >> (lo_bit + 8 * p)) & 0xFF], 1u);
+  }
+  if (err) atomicOr(&sh_err, err);
+  __syncthreads();
+  for (int p = 0; p < npasses; ++p) {
+    const uint32_t c = sh_hist[p][tid];
+    if (c) atomicAdd(&hist[p * RADIX + tid], c);
+  }
+  if (tid < 8 && sh_gmax[tid]) {
+    atomicMax(&ctl->gen_min[tid], sh_gmin[tid]);
+    atomicMax(&ctl->gen_max[tid], sh_gmax[tid]);
+  }
+  if (tid == 0) {
+    if (sh_nil) atomicAdd(&ctl->n_nil, sh_nil);
+    if (sh_err) atomicOr(&ctl->err, sh_err);
+  }
+}
+
+// Histogram of npasses 8-bit digits of a key array (full-fingerprint fallback sort).
+__global__ __launch_bounds__(256) void k_histogram(const uint64_t* __restrict__ keys, uint32_t n, int lo_bit,
+                                                   int npasses, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t sh_hist[8][RADIX];
+  const uint32_t tid = threadIdx.x;
+  for (int i = tid; i < 8 * RADIX; i += 256) (&sh_hist[0][0])[i] = 0;
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * 256 + tid; i < n; i += gridDim.x * 256) {
+    const uint64_t key = keys[i];
+    for (int p = 0; p < npasses; ++p) atomicAdd(&sh_hist[p][(key >> (lo_bit + 8 * p)) & 0xFF], 1u);
+  }
+  __syncthreads();
+  for (int p = 0; p < npasses; ++p) {
+    const uint32_t c = sh_hist[p][tid];
+    if (c) atomicAdd(&hist[p * RADIX + tid], c);
+  }
+}
+
+// Exclusive scan of each pass's 256-bin histogram (one block per pass).
+__global__ __launch_bounds__(256) void k_hist_scan(const uint32_t* __restrict__ hist, uint32_t* __restrict__ offs) {
+  __shared__ uint32_t sh[RADIX];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t p = blockIdx.x;
+  const uint32_t v = hist[p * RADIX + tid];
+  sh[tid] = v;
+  __syncthreads();
+  for (int d = 1; d < RADIX; d <<= 1) {
+    const uint32_t t = tid >= (uint32_t)d ? sh[tid - d] : 0u;
+    __syncthreads();
+    sh[tid] += t;
+    __syncthreads();
+  }
+  offs[p * RADIX + tid] = sh[tid] - v;
+}
+
+// Gather helpers for the full-fingerprint fallback sort.
+__global__ void k_fallback_lo_keys(const ItemRec* __restrict__ recs, const uint64_t* __restrict__ keys_orig,
+                                   uint32_t n, uint64_t* __restrict__ k_out, uint32_t* __restrict__ v_out) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  k_out[i] = keys_orig[i] == NIL_KEY ? 0ull : recs[i].fp_lo;
+  v_out[i] = i;
+}
+__global__ void k_gather_keys(const uint64_t* __restrict__ keys_orig, const uint32_t* __restrict__ vals, uint32_t n,
+                              uint64_t* __restrict__ k_out) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  k_out[i] = keys_orig[vals[i]];
+}
+
+// ---------------------------------------------------------------------------
+// k_sort_pass — one stable LSD pass over an 8-bit digit ("onesweep"): rank inside
+// the 4096-key tile with wave ballots, publish per-digit tile counts, decoupled
+// look-back over earlier tiles (tile ids come from an atomic ticket, so a tile only
+// ever waits on tiles already running), stage the tile in LDS in digit order and
+// write each digit run contiguously.
+// ---------------------------------------------------------------------------
+constexpr int SORT_IPT = 16;                // keys per thread
+constexpr int SORT_TILE = 256 * SORT_IPT;   // 4096
+constexpr uint32_t LB_AGG = 1u << 30;
+constexpr uint32_t LB_INC = 2u << 30;
+constexpr uint32_t LB_MASK = (1u << 30) - 1;
+
+__global__ __launch_bounds__(256) void k_sort_pass(const uint64_t* __restrict__ keys_in,
+                                                   const uint32_t* __restrict__ vals_in,
+                                                   uint64_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
+                                                   uint32_t n, int shift, const uint32_t* __restrict__ bin_off,
+                                                   uint32_t* __restrict__ lookback, uint32_t* tile_ctr,
+                                                   EngineCtl* ctl) {
+  __shared__ uint64_t s_keys[SORT_TILE];
+  __shared__ uint32_t s_vals[SORT_TILE];
+  __shared__ uint32_t s_wcnt[4][RADIX];   // per-wave digit counts -> per-wave exclusive offsets
+  __shared__ uint32_t s_tstart[RADIX];    // tile-local exclusive digit offsets
+  __shared__ uint32_t s_gbase[RADIX];     // global output base per digit for this tile
+  __shared__ uint32_t s_tile;
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wave = tid >> 6;
+  const uint32_t lane = tid & 63;
+  if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+  for (int i = tid; i < 4 * RADIX; i += 256) (&s_wcnt[0][0])[i] = 0;
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint32_t tbase = tile * SORT_TILE;
+
+  uint64_t key[SORT_IPT];
+  uint32_t val[SORT_IPT];
+  uint32_t rank[SORT_IPT];
+#pragma unroll
+  for (int k = 0; k < SORT_IPT; ++k) {
+    const uint32_t p = tbase + wave * (SORT_TILE / 4) + k * 64 + lane;
+    if (p < n) {
+      key[k] = keys_in[p];
+      val[k] = vals_in ? vals_in[p] : p;
+    } else {
+      key[k] = ~0ull;
+      val[k] = 0;
+    }
+  }
+  // Per-wave stable ranking, round by round in position order.
+  const uint64_t lt = lanemask_lt();
+#pragma unroll
+  for (int k = 0; k < SORT_IPT; ++k) {
+    const uint32_t p = tbase + wave * (SORT_TILE / 4) + k * 64 + lane;
+    const bool valid = p < n;
+    const uint32_t d = (uint32_t)(key[k] >> shift) & 0xFFu;
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < RADIX_BITS; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t bal = __ballot(bit);
+      m &= bit ? bal : ~bal;
+    }
+    uint32_t r = 0;
+    if (valid) {
+      const uint32_t before = s_wcnt[wave][d];
+      r = before + (uint32_t)__popcll(m & lt);
+      const uint32_t leader = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+      __builtin_amdgcn_wave_barrier();
+      if (lane == leader) s_wcnt[wave][d] = before + (uint32_t)__popcll(m);
+    }
+    __builtin_amdgcn_wave_barrier();
+    rank[k] = r;
+  }
+  __syncthreads();
+  // Thread tid owns digit tid: tile count, per-wave exclusive offsets.
+  uint32_t cnt = 0;
+  {
+    const uint32_t c0 = s_wcnt[0][tid], c1 = s_wcnt[1][tid], c2 = s_wcnt[2][tid], c3 = s_wcnt[3][tid];
+    s_wcnt[0][tid] = 0;
+    s_wcnt[1][tid] = c0;
+    s_wcnt[2][tid] = c0 + c1;
+    s_wcnt[3][tid] = c0 + c1 + c2;
+    cnt = c0 + c1 + c2 + c3;
+  }
+  // Publish this tile's aggregate for digit tid, then look back.
+  uint32_t* lb = lookback + (size_t)tile * RADIX;
+  if (tile == 0) {
+    st_relaxed(&lb[tid], LB_INC | cnt);
+  } else {
+    st_relaxed(&lb[tid], LB_AGG | cnt);
+  }
+  uint32_t excl = 0;
+  if (tile > 0) {
+    int32_t j = (int32_t)tile - 1;
+    uint32_t spins = 0;
+    while (j >= 0) {
+      const uint32_t v = ld_relaxed(&lookback[(size_t)j * RADIX + tid]);
+      const uint32_t f = v & ~LB_MASK;
+      if (f == 0) {
+        if (++spins > SPIN_LIMIT) { atomicOr(&ctl->err, ERR_SPIN); break; }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      excl += v & LB_MASK;
+      if (f == LB_INC) break;
+      --j;
+    }
+    st_relaxed(&lb[tid], LB_INC | (excl + cnt));
+  }
+  s_gbase[tid] = bin_off[tid] + excl;
+  // Tile-local exclusive scan of digit counts (block scan over 256 threads).
+  s_tstart[tid] = cnt;
+  __syncthreads();
+  for (int d = 1; d < RADIX; d <<= 1) {
+    const uint32_t t = tid >= (uint32_t)d ? s_tstart[tid - d] : 0u;
+    __syncthreads();
+    s_tstart[tid] += t;
+    __syncthreads();
+  }
+  s_tstart[tid] -= cnt;
+  __syncthreads();
+  // Stage the tile in digit order.
+#pragma unroll
+  for (int k = 0; k < SORT_IPT; ++k) {
+    const uint32_t p = tbase + wave * (SORT_TILE / 4) + k * 64 + lane;
+    if (p < n) {
+      const uint32_t d = (uint32_t)(key[k] >> shift) & 0xFFu;
+      const uint32_t pos = s_tstart[d] + s_wcnt[wave][d] + rank[k];
+      s_keys[pos] = key[k];
+      s_vals[pos] = val[k];
+    }
+  }
+  __syncthreads();
+  const uint32_t tvalid = n - tbase < (uint32_t)SORT_TILE ? n - tbase : (uint32_t)SORT_TILE;
+  for (uint32_t i = tid; i < tvalid; i += 256) {
+    const uint64_t k = s_keys[i];
+    const uint32_t d = (uint32_t)(k >> shift) & 0xFFu;
+    const uint32_t o = s_gbase[d] + (i - s_tstart[d]);
+    keys_out[o] = k;
+    vals_out[o] = s_vals[i];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_scan — segment heads + segmented inclusive prefix sum of h over the sorted batch.
+// Scan element (f, s, hp, o): f = segment starts inside, s = sum since the last head,
+// hp = last head position, o = rule changed within the segment. op(A,B) = B.f ? B :
+// (A.f, A.s+B.s, A.hp, A.o|B.o) — associative. Tiles chain through decoupled look-back
+// on two self-flagged 64-bit granules per tile (sum|o and head position).
+// ---------------------------------------------------------------------------
+constexpr int SCAN_IPT = 8;
+constexpr int SCAN_TILE = 256 * SCAN_IPT;  // 2048
+constexpr uint64_t LB64_AGG = 1ull << 62;
+constexpr uint64_t LB64_INC = 2ull << 62;
+constexpr uint64_t LB64_FLAGS = 3ull << 62;
+constexpr uint64_t LB64_O = 1ull << 61;
+constexpr uint64_t LB64_SUM = (1ull << 61) - 1;
+
+struct ScanEl {
+  uint32_t f;
+  uint32_t o;
+  uint32_t hp;
+  uint64_t s;
+};
+RL_DEV ScanEl scan_op(const ScanEl& a, const ScanEl& b) {
+  if (b.f) return b;
+  ScanEl r;
+  r.f = a.f;
+  r.s = a.s + b.s;
+  r.hp = a.hp;
+  r.o = a.o | b.o;
+  return r;
+}
+RL_DEV ScanEl shfl_up_el(const ScanEl& x, int d) {
+  ScanEl r;
+  r.f = __shfl_up(x.f, d, 64);
+  r.o = __shfl_up(x.o, d, 64);
+  r.hp = __shfl_up(x.hp, d, 64);
+  r.s = __shfl_up(x.s, d, 64);
+  return r;
+}
+
+__global__ __launch_bounds__(256) void k_scan(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ svals,
+                                              const ItemRec* __restrict__ recs, uint32_t n_all, int lo_bit,
+                                              int check_mixed, SortedRec* __restrict__ srec,
+                                              uint64_t* __restrict__ lb_sum, uint64_t* __restrict__ lb_head,
+                                              uint32_t* tile_ctr, EngineCtl* ctl) {
+  __shared__ ScanEl s_wagg[4];
+  __shared__ uint64_t s_lastkey[256];
+  __shared__ uint64_t s_lastlo[256];
+  __shared__ uint32_t s_lastrule[256];
+  __shared__ uint32_t s_tile;
+  __shared__ ScanEl s_carry;
+  __shared__ uint32_t s_heads;
+  __shared__ uint32_t s_mixed;
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t lane = tid & 63;
+  const uint32_t wave = tid >> 6;
+  if (tid == 0) {
+    s_tile = atomicAdd(tile_ctr, 1u);
+    s_heads = 0;
+    s_mixed = 0;
+  }
+  __syncthreads();
+  const uint32_t n = n_all - ld_relaxed(&ctl->n_nil);
+  const uint32_t tile = s_tile;
+  const uint32_t base = tile * SCAN_TILE + tid * SCAN_IPT;
+
+  uint64_t key[SCAN_IPT], lo[SCAN_IPT];
+  uint32_t idx[SCAN_IPT], rule[SCAN_IPT], req[SCAN_IPT], hh[SCAN_IPT];
+  int32_t nm[SCAN_IPT];
+#pragma unroll
+  for (int k = 0; k < SCAN_IPT; ++k) {
+    const uint32_t p = base + k;
+    if (p < n) {
+      key[k] = skeys[p];
+      idx[k] = svals[p];
+      const ItemRec r = recs[idx[k]];
+      lo[k] = r.fp_lo;
+      rule[k] = r.rule;
+      req[k] = r.req;
+      hh[k] = r.h;
+      nm[k] = r.now_mod;
+    } else {
+      key[k] = NIL_KEY;
+      idx[k] = 0;
+      lo[k] = 0;
+      rule[k] = 0;
+      req[k] = 0;
+      hh[k] = 0;
+      nm[k] = 0;
+    }
+  }
+  // Predecessor of this thread's first item.
+  s_lastkey[tid] = key[SCAN_IPT - 1];
+  s_lastlo[tid] = lo[SCAN_IPT - 1];
+  s_lastrule[tid] = rule[SCAN_IPT - 1];
+  __syncthreads();
+  uint64_t pkey, plo;
+  uint32_t prule;
+  if (tid > 0) {
+    pkey = s_lastkey[tid - 1];
+    plo = s_lastlo[tid - 1];
+    prule = s_lastrule[tid - 1];
+  } else if (base > 0 && base - 1 < n) {
+    pkey = skeys[base - 1];
+    const ItemRec r = recs[svals[base - 1]];
+    plo = r.fp_lo;
+    prule = r.rule;
+  } else {
+    pkey = NIL_KEY;
+    plo = 0;
+    prule = 0;
+  }
+  // Thread-local segmented reduction.
+  uint32_t head[SCAN_IPT];
+  uint32_t rchg[SCAN_IPT];
+  ScanEl t{0, 0, 0, 0};
+  uint32_t nheads = 0, mixed = 0;
+#pragma unroll
+  for (int k = 0; k < SCAN_IPT; ++k) {
+    const uint32_t p = base + k;
+    const bool valid = p < n;
+    const bool diff = (p == 0) || key[k] != pkey || lo[k] != plo;
+    head[k] = valid && diff;
+    rchg[k] = valid && !diff && rule[k] != prule;
+    if (valid && p > 0 && diff && check_mixed && ((key[k] ^ pkey) >> lo_bit) == 0) mixed = 1;
+    nheads += head[k];
+    ScanEl e{head[k], rchg[k], p, (uint64_t)hh[k]};
+    t = scan_op(t, e);
+    pkey = key[k];
+    plo = lo[k];
+    prule = rule[k];
+  }
+  // Wave inclusive scan of thread aggregates.
+  ScanEl incl = t;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const ScanEl y = shfl_up_el(incl, d);
+    if (lane >= (uint32_t)d) incl = scan_op(y, incl);
+  }
+  if (lane == 63) s_wagg[wave] = incl;
+  if (nheads) atomicAdd(&s_heads, nheads);
+  if (mixed) s_mixed = 1;
+  ScanEl wexcl = shfl_up_el(incl, 1);
+  if (lane == 0) wexcl = ScanEl{0, 0, 0, 0};
+  __syncthreads();
+  // Tile aggregate and this wave's offset.
+  ScanEl woff{0, 0, 0, 0};
+  ScanEl tagg{0, 0, 0, 0};
+  for (uint32_t w = 0; w < 4; ++w) {
+    if (w == wave) woff = tagg;
+    tagg = scan_op(tagg, s_wagg[w]);
+  }
+  // Decoupled look-back (thread 0).
+  if (tid == 0) {
+    ScanEl carry{0, 0, 0, 0};
+    if (tagg.f || tile == 0) {
+      // carry-out independent of predecessors for the part after the first head
+      if (tile == 0) {
+        st_relaxed64(&lb_head[tile], LB64_INC | tagg.hp);
+        st_relaxed64(&lb_sum[tile], LB64_INC | (tagg.o ? LB64_O : 0) | (tagg.s & LB64_SUM));
+      } else {
+        st_relaxed64(&lb_head[tile], LB64_INC | tagg.hp);
+        st_relaxed64(&lb_sum[tile], LB64_INC | (tagg.o ? LB64_O : 0) | (tagg.s & LB64_SUM));
+      }
+    } else {
+      st_relaxed64(&lb_sum[tile], LB64_AGG | (tagg.o ? LB64_O : 0) | (tagg.s & LB64_SUM));
+    }
+    if (tile > 0) {
+      ScanEl acc{0, 0, 0, 0};
+      int32_t j = (int32_t)tile - 1;
+      uint32_t spins = 0;
+      while (j >= 0) {
+        const uint64_t v = ld_relaxed64(&lb_sum[j]);
+        const uint64_t f = v & LB64_FLAGS;
+        if (f == 0) {
+          if (++spins > SPIN_LIMIT) { atomicOr(&ctl->err, ERR_SPIN); break; }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        if (f == LB64_AGG) {
+          ScanEl a{0, (uint32_t)((v & LB64_O) != 0), 0, v & LB64_SUM};
+          acc = scan_op(a, acc);
+          --j;
+          continue;
+        }
+        // inclusive: fetch its head position too
+        uint64_t hv;
+        while (((hv = ld_relaxed64(&lb_head[j])) & LB64_FLAGS) == 0) {
+          if (++spins > SPIN_LIMIT) { atomicOr(&ctl->err, ERR_SPIN); break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        ScanEl a{1, (uint32_t)((v & LB64_O) != 0), (uint32_t)(hv & 0xFFFFFFFFull), v & LB64_SUM};
+        acc = scan_op(a, acc);
+        break;
+      }
+      carry = acc;
+      if (!tagg.f) {
+        const ScanEl out = scan_op(carry, tagg);
+        st_relaxed64(&lb_head[tile], LB64_INC | out.hp);
+        st_relaxed64(&lb_sum[tile], LB64_INC | (out.o ? LB64_O : 0) | (out.s & LB64_SUM));
+      }
+    }
+    s_carry = carry;
+    if (s_heads) atomicAdd(&ctl->n_segments, s_heads);
+    if (s_mixed) atomicOr(&ctl->err, ERR_NEED_RESORT);
+  }
+  __syncthreads();
+  ScanEl run = scan_op(scan_op(s_carry, woff), wexcl);
+#pragma unroll
+  for (int k = 0; k < SCAN_IPT; ++k) {
+    const uint32_t p = base + k;
+    if (p >= n) break;
+    ScanEl e{head[k], rchg[k], p, (uint64_t)hh[k]};
+    run = scan_op(run, e);
+    SortedRec r;
+    r.P = run.s;
+    r.head = run.hp | (run.o ? HEAD_MIXED_RULE : 0u);
+    r.idx = idx[k];
+    r.rule = rule[k];
+    r.req = req[k];
+    r.h = hh[k];
+    r.now_mod = nm[k];
+    srec[p] = r;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_leader — one thread per unique key (segment tail).
+// ---------------------------------------------------------------------------
+constexpr uint32_t MAX_PROBE = 4096;
+
+__global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ skeys, const SortedRec* __restrict__ srec,
+                                                const ItemRec* __restrict__ recs, const DevRule* __restrict__ rules,
+                                                uint32_t n_all, TableDesc tab, int local_cache,
+                                                SegInfo* __restrict__ seg, EngineCtl* ctl) {
+  const uint32_t errs = ld_relaxed(&ctl->err);
+  if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_BAD_INPUT | ERR_WINDOW_SPAN)) return;
+  const uint32_t n = n_all - ld_relaxed(&ctl->n_nil);
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  if (j + 1 < n && (srec[j + 1].head & ~HEAD_MIXED_RULE) != j + 1) return;  // not a tail
+  const SortedRec tail = srec[j];
+  const uint32_t hp = tail.head & ~HEAD_MIXED_RULE;
+  const bool mixed_rule = (tail.head & HEAD_MIXED_RULE) != 0;
+  const uint64_t key = skeys[j];
+  const ItemRec rec = recs[tail.idx];
+  const uint32_t region = key_region(key);
+  // Two window generations of one region in one batch must be adjacent (a batch may
+  // straddle one window boundary); otherwise the older would read as empty.
+  if (ld_relaxed(&ctl->gen_max[region]) - ~ld_relaxed(&ctl->gen_min[region]) > 1u) {
+    atomicOr(&ctl->err, ERR_WINDOW_SPAN);
+    return;
+  }
+  const uint32_t lg = tab.region_log2[region];
+  const uint64_t mask = (1ull << lg) - 1ull;
+  Slot* rbase = tab.slots + tab.region_base[region];
+  uint64_t pos = (key << 3) >> (64 - lg);  // top lg bits below the region bits
+  const uint32_t G = rec.gen;
+  const uint32_t tag = (uint32_t)rec.fp_lo;
+  const uint32_t lohi = (uint32_t)(rec.fp_lo >> 32);
+  Slot* slot = nullptr;
+  bool existed = false;
+  for (uint32_t probe = 0; probe < MAX_PROBE;) {
+    Slot* s = rbase + (pos & mask);
+    const uint64_t c = ld_relaxed64(&s->ctrl);
+    const uint32_t g = (uint32_t)c;
+    if (g == G && (uint32_t)(c >> 32) == tag && s->key == key && s->fp_lo_hi == lohi) {
+      slot = s;
+      existed = true;
+      break;
+    }
+    if (g < G) {
+      // empty for this window generation: claim it
+      const unsigned long long want = ((unsigned long long)tag << 32) | G;
+      const unsigned long long old = atomicCAS((unsigned long long*)&s->ctrl, (unsigned long long)c, want);
+      if (old == c) {
+        slot = s;
+        break;
+      }
+      continue;  // lost the race: re-examine this slot
+    }
+    ++pos;
+    ++probe;
+  }
+  if (!slot) {
+    atomicOr(&ctl->err, ERR_TABLE_FULL);
+    return;
+  }
+  uint64_t base = 0;
+  bool frozen_pre = false;
+  if (existed) {
+    base = slot->count;
+    frozen_pre = (slot->flags & SLOT_FROZEN) != 0;
+  } else {
+    slot->key = key;
+    slot->fp_lo_hi = lohi;
+    atomicAdd(&ctl->n_inserted, 1u);
+  }
+  uint32_t freeze = SEG_NO_FREEZE;
+  uint64_t final_count = base + tail.P;
+  if (frozen_pre) {
+    // every descriptor is a local-cache hit: no INCRBY (fixed_cache_impl.go:61-65)
+    freeze = SEG_FROZEN_BEFORE;
+    final_count = base;
+  } else if (local_cache) {
+    // first descriptor whose INCRBY reply exceeds its limit (base_limiter.go:88,94-106);
+    // all later requests of this key are local-cache hits.
+    uint32_t jstar = 0xFFFFFFFFu;
+    const uint32_t L0 = rules[tail.rule].L;
+    if (!mixed_rule && base + tail.P < (1ull << 32)) {
+      // after = base + P is strictly increasing in the segment: binary search.
+      if ((uint64_t)(uint32_t)(base + tail.P) > L0) {
+        uint32_t lo_i = hp, hi_i = j;
+        while (lo_i < hi_i) {
+          const uint32_t mid = lo_i + (hi_i - lo_i) / 2;
+          if (base + srec[mid].P > (uint64_t)L0) hi_i = mid; else lo_i = mid + 1;
+        }
+        jstar = lo_i;
+      }
+    } else {
+      for (uint32_t k = hp; k <= j; ++k) {
+        const SortedRec r = srec[k];
+        if ((uint32_t)(base + r.P) > rules[r.rule].L) { jstar = k; break; }
+      }
+    }
+    if (jstar != 0xFFFFFFFFu) {
+      const uint32_t rstar = srec[jstar].req;
+      uint32_t last = jstar;
+      while (last < j && srec[last + 1].req == rstar) ++last;
+      freeze = rstar;
+      final_count = base + srec[last].P;
+    }
+  }
+  slot->count = final_count;
+  if (freeze != SEG_NO_FREEZE && freeze != SEG_FROZEN_BEFORE) slot->flags = slot->flags | SLOT_FROZEN;
+  if (!existed && freeze == SEG_NO_FREEZE) slot->flags = 0;
+  if (!existed && freeze != SEG_NO_FREEZE && freeze != SEG_FROZEN_BEFORE) slot->flags = SLOT_FROZEN;
+  SegInfo si;
+  si.base = base;
+  si.freeze = freeze;
+  si.pad = 0;
+  seg[hp] = si;
+}
+
+// ---------------------------------------------------------------------------
+// k_decide — per descriptor in sorted order.
+// GetResponseDescriptorStatus + checkOverLimitThreshold + checkNearLimitThreshold +
+// CalculateReset (base_limiter.go:70-195, utilities.go:34-38).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_decide(const SortedRec* __restrict__ srec, const SegInfo* __restrict__ seg,
+                                                const DevRule* __restrict__ rules, uint32_t n_all,
+                                                rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
+                                                EngineCtl* ctl) {
+  const uint32_t errs = ld_relaxed(&ctl->err);
+  if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_TABLE_FULL | ERR_BAD_INPUT | ERR_WINDOW_SPAN)) return;
+  const uint32_t n = n_all - ld_relaxed(&ctl->n_nil);
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  const SortedRec r = srec[j];
+  const SegInfo si = seg[r.head & ~HEAD_MIXED_RULE];
+  const DevRule R = rules[r.rule];
+  const uint32_t h = r.h;
+  const uint32_t reset = R.div - (uint32_t)r.now_mod;  // div - now % div
+  rl_status st;
+  st.reset_s = reset;
+  st.over_limit_delta = 0;
+  st.near_limit_delta = 0;
+  const bool local_hit = si.freeze == SEG_FROZEN_BEFORE || (si.freeze != SEG_NO_FREEZE && r.req > si.freeze);
+  uint32_t throttle = 0;
+  if (local_hit) {
+    st.code_flags = RL_CODE_OVER_LIMIT | ((RL_FLAG_HAS_LIMIT | RL_FLAG_LOCAL_CACHE_HIT) << 8);
+    st.limit_remaining = 0;
+    st.over_limit_delta = h;
+  } else {
+    const uint32_t after = (uint32_t)(si.base + r.P);
+    const uint32_t before = after - h;
+    const uint32_t L = R.L, near = R.near;
+    if (after > L) {
+      st.code_flags = RL_CODE_OVER_LIMIT | (RL_FLAG_HAS_LIMIT << 8);
+      st.limit_remaining = 0;
+      if (before >= L) {
+        st.over_limit_delta = h;
+      } else {
+        st.over_limit_delta = after - L;
+        st.near_limit_delta = L - (near > before ? near : before);
+      }
+    } else {
+      st.code_flags = RL_CODE_OK | (RL_FLAG_HAS_LIMIT << 8);
+      st.limit_remaining = L - after;
+      if (after > near) {
+        const uint32_t millis = reset * 1000u;  // uint32(end - now) * 1000
+        const uint32_t calls = (L - after) > 1u ? (L - after) : 1u;
+        throttle = millis / calls;
+        st.near_limit_delta = before >= near ? h : after - near;
+      }
+    }
+  }
+  out[r.idx] = st;
+  if (throttle) atomicMax(&req_thr[r.req], throttle);
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launchers (called from rl_engine.cpp).
+// ---------------------------------------------------------------------------
+void launch_fingerprint(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
+                        uint64_t* keys_orig, ItemRec* recs, rl_status* out,
+                        uint32_t* hist, int lo_bit, int npasses, EngineCtl* ctl) {
+  DevBatch d;
+  d.n_desc = b.n_desc;
+  d.n_req = b.n_req;
+  d.blob_bytes = b.blob_bytes;
+  d.pad = 0;
+  d.blob = b.prefix_blob;
+  d.off = b.prefix_off;
+  d.rule = b.rule_id;
+  d.req_of = b.req_of;
+  d.now = b.now;
+  d.hits = b.hits_addend;
+  const uint32_t grid = (b.n_desc + 255) / 256;
+  hipLaunchKernelGGL(k_fingerprint, dim3(grid), dim3(256), 0, st, d, rules, n_rules, seed, keys_orig, recs, out,
+                     hist, lo_bit, npasses, ctl);
+}
+void launch_histogram(hipStream_t st, const uint64_t* keys, uint32_t n, int lo_bit, int npasses, uint32_t* hist) {
+  uint32_t grid = (n + 255) / 256;
+  if (grid > 2048) grid = 2048;
+  if (grid == 0) grid = 1;
+  hipLaunchKernelGGL(k_histogram, dim3(grid), dim3(256), 0, st, keys, n, lo_bit, npasses, hist);
+}
+void launch_hist_scan(hipStream_t st, const uint32_t* hist, uint32_t* offs, int npasses) {
+  hipLaunchKernelGGL(k_hist_scan, dim3(npasses), dim3(256), 0, st, hist, offs);
+}
+void launch_fallback_lo_keys(hipStream_t st, const ItemRec* recs, const uint64_t* keys_orig, uint32_t n,
+                             uint64_t* k_out, uint32_t* v_out) {
+  hipLaunchKernelGGL(k_fallback_lo_keys, dim3((n + 255) / 256), dim3(256), 0, st, recs, keys_orig, n, k_out, v_out);
+}
+void launch_gather_keys(hipStream_t st, const uint64_t* keys_orig, const uint32_t* vals, uint32_t n, uint64_t* k_out) {
+  hipLaunchKernelGGL(k_gather_keys, dim3((n + 255) / 256), dim3(256), 0, st, keys_orig, vals, n, k_out);
+}
+uint32_t sort_tiles(uint32_t n) { return (n + SORT_TILE - 1) / SORT_TILE; }
+uint32_t scan_tiles(uint32_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE; }
+void launch_sort_pass(hipStream_t st, const uint64_t* kin, const uint32_t* vin, uint64_t* kout, uint32_t* vout,
+                      uint32_t n, int shift, const uint32_t* bin_off, uint32_t* lookback, uint32_t* tile_ctr,
+                      EngineCtl* ctl) {
+  hipLaunchKernelGGL(k_sort_pass, dim3(sort_tiles(n)), dim3(256), 0, st, kin, vin, kout, vout, n, shift, bin_off,
+                     lookback, tile_ctr, ctl);
+}
+void launch_scan(hipStream_t st, const uint64_t* skeys, const uint32_t* svals, const ItemRec* recs, uint32_t n,
+                 int lo_bit, int check_mixed, SortedRec* srec, uint64_t* lb_sum, uint64_t* lb_head,
+                 uint32_t* tile_ctr, EngineCtl* ctl) {
+  hipLaunchKernelGGL(k_scan, dim3(scan_tiles(n)), dim3(256), 0, st, skeys, svals, recs, n, lo_bit, check_mixed, srec,
+                     lb_sum, lb_head, tile_ctr, ctl);
+}
+void launch_leader(hipStream_t st, const uint64_t* skeys, const SortedRec* srec, const ItemRec* recs,
+                   const DevRule* rules, uint32_t n, const TableDesc& tab, int local_cache, SegInfo* seg,
+                   EngineCtl* ctl) {
+  hipLaunchKernelGGL(k_leader, dim3((n + 255) / 256), dim3(256), 0, st, skeys, srec, recs, rules, n, tab,
+                     local_cache, seg, ctl);
+}
+void launch_decide(hipStream_t st, const SortedRec* srec, const SegInfo* seg, const DevRule* rules, uint32_t n,
+                   rl_status* out, uint32_t* req_thr, EngineCtl* ctl) {
+  hipLaunchKernelGGL(k_decide, dim3((n + 255) / 256), dim3(256), 0, st, srec, seg, rules, n, out, req_thr, ctl);
+}
+
+}  // namespace rlhip

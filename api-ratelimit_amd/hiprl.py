@@ -1,0 +1,432 @@
+"""Python binding of the HIP rate-limit backend (include/rl_hip.h) and a Python mirror of
+the reference's backend interface, used by the parity tests and bench.py.
+
+The product is the C ABI in libratelimit_hip.so (HIP kernels + C++ host runtime); this
+module is a thin ctypes layer over it. It never falls back to a CPU implementation: if
+the shared library is missing, importing `Engine` raises.
+
+Reference interface mirrored here (for tests that read like the reference's own):
+  limiter.RateLimitCache.DoLimit / Flush     src/limiter/cache.go:15-33
+  limiter.DoLimitResponse                    src/limiter/cache.go:9-12
+  config.RateLimit / NewRateLimit            src/config/config.go:26-32, config_impl.go:79-89
+  redis.RedisError                           src/redis/driver.go:6-10
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from pathlib import Path
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "csrc" / "libratelimit_hip.so"
+
+NIL_RULE = 0xFFFFFFFF
+UNIT_UNKNOWN, SECOND, MINUTE, HOUR, DAY = 0, 1, 2, 3, 4
+UNIT_NAMES = {SECOND: "SECOND", MINUTE: "MINUTE", HOUR: "HOUR", DAY: "DAY"}
+UNIT_DIVIDER = {SECOND: 1, MINUTE: 60, HOUR: 3600, DAY: 86400}
+CODE_UNKNOWN, CODE_OK, CODE_OVER_LIMIT = 0, 1, 2
+FLAG_HAS_LIMIT, FLAG_LOCAL_CACHE_HIT = 1, 2
+
+RL_ERRORS = {-1: "RL_EINVAL", -2: "RL_EHIP", -3: "RL_ENOSPC", -4: "RL_ECAPACITY", -5: "RL_ESTATE", -6: "RL_EDEVICE"}
+
+STATUS_DTYPE = np.dtype([("code_flags", "<u4"), ("limit_remaining", "<u4"), ("reset_s", "<u4"),
+                         ("over_limit_delta", "<u4"), ("near_limit_delta", "<u4")])
+
+
+class RlConfig(C.Structure):
+    _fields_ = [("struct_size", C.c_uint32), ("device", C.c_int32), ("log2_slots", C.c_uint32 * 4),
+                ("near_limit_ratio", C.c_float), ("local_cache", C.c_uint32), ("per_second_split", C.c_uint32),
+                ("max_batch_desc", C.c_uint32), ("max_batch_req", C.c_uint32), ("max_blob_bytes", C.c_uint32),
+                ("sort_bits", C.c_uint32), ("hash_seed", C.c_uint64)]
+
+
+class RlRule(C.Structure):
+    _fields_ = [("requests_per_unit", C.c_uint32), ("unit", C.c_uint32)]
+
+
+class RlBatch(C.Structure):
+    _fields_ = [("n_desc", C.c_uint32), ("n_req", C.c_uint32), ("blob_bytes", C.c_uint32), ("reserved", C.c_uint32),
+                ("prefix_blob", C.c_void_p), ("prefix_off", C.c_void_p), ("rule_id", C.c_void_p),
+                ("req_of", C.c_void_p), ("now", C.c_void_p), ("hits_addend", C.c_void_p)]
+
+
+class RlEngineStats(C.Structure):
+    _fields_ = [("batches", C.c_uint64), ("descriptors", C.c_uint64), ("resorts", C.c_uint64),
+                ("live_slots_hint", C.c_uint64)]
+
+
+# (name, argtypes, restype) of every symbol include/rl_hip.h declares
+ABI = [
+    ("rl_create", [C.POINTER(RlConfig), C.POINTER(C.c_void_p)], C.c_int),
+    ("rl_destroy", [C.c_void_p], None),
+    ("rl_last_error", [C.c_void_p], C.c_char_p),
+    ("rl_abi_version", [], C.c_uint32),
+    ("rl_load_rules", [C.c_void_p, C.POINTER(RlRule), C.c_uint32], C.c_int),
+    ("rl_submit", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
+    ("rl_wait", [C.c_void_p], C.c_int),
+    ("rl_submit_device", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
+    ("rl_stream", [C.c_void_p], C.c_void_p),
+    ("rl_reset", [C.c_void_p], C.c_int),
+    ("rl_get_stats", [C.c_void_p, C.POINTER(RlEngineStats)], C.c_int),
+    ("rl_set_timing", [C.c_void_p, C.c_int], C.c_int),
+    ("rl_kernel_times", [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                         C.c_uint32, C.POINTER(C.c_uint32)], C.c_int),
+    ("rl_last_batch_info", [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                            C.POINTER(C.c_uint64)], C.c_int),
+]
+
+_lib = None
+
+
+def load_library(path: Optional[os.PathLike] = None) -> C.CDLL:
+    """Load libratelimit_hip.so; raises if it was not built (no silent fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else LIB_PATH
+    if not p.exists():
+        raise RuntimeError(f"HIP extension not built: {p} missing (run __graft_entry__.build())")
+    lib = C.CDLL(str(p))
+    for name, argt, rest in ABI:
+        f = getattr(lib, name)
+        f.argtypes = argt
+        f.restype = rest
+    if path is None:
+        _lib = lib
+    return lib
+
+
+class RedisError(RuntimeError):
+    """redis.RedisError — the backend's only recoverable failure (service/ratelimit.go:276-281)."""
+
+
+# ---------------------------------------------------------------------------
+# Flat batches (the C ABI's input layout)
+# ---------------------------------------------------------------------------
+@dataclass
+class Batch:
+    blob: np.ndarray      # uint8 key-prefix bytes
+    off: np.ndarray       # uint32 [n_desc + 1]
+    rule: np.ndarray      # uint32 [n_desc]
+    req_of: np.ndarray    # uint32 [n_desc]
+    now: np.ndarray       # int64 [n_req]
+    hits: np.ndarray      # uint32 [n_req]
+
+    @property
+    def n_desc(self) -> int:
+        return int(self.rule.shape[0])
+
+    @property
+    def n_req(self) -> int:
+        return int(self.now.shape[0])
+
+    def prefix(self, i: int) -> bytes:
+        return bytes(self.blob[self.off[i]:self.off[i + 1]])
+
+    def slice_requests(self, r0: int, r1: int) -> "Batch":
+        """Requests [r0, r1) as their own batch."""
+        d0 = int(np.searchsorted(self.req_of, r0, "left"))
+        d1 = int(np.searchsorted(self.req_of, r1, "left"))
+        b0, b1 = int(self.off[d0]), int(self.off[d1])
+        return Batch(self.blob[b0:b1].copy(), (self.off[d0:d1 + 1] - b0).astype(np.uint32),
+                     self.rule[d0:d1].copy(), (self.req_of[d0:d1] - r0).astype(np.uint32),
+                     self.now[r0:r1].copy(), self.hits[r0:r1].copy())
+
+
+def cache_key_prefix(domain: str, entries: Sequence[tuple]) -> bytes:
+    """GenerateCacheKey without the timestamp: domain '_' (key '_' value '_')*  (cache_key.go:57-65)."""
+    out = bytearray(domain.encode())
+    out += b"_"
+    for k, v in entries:
+        out += k.encode() + b"_" + v.encode() + b"_"
+    return bytes(out)
+
+
+def build_batch(requests: Sequence[tuple]) -> Batch:
+    """requests: [(domain, [entries | None...], [rule_id...], hits_addend, now)] where each
+    descriptor is a list of (key, value) and rule_id is NIL_RULE for a nil limit."""
+    blob = bytearray()
+    off, rule, req_of, now, hits = [0], [], [], [], []
+    for r, (domain, descs, rules, ha, t) in enumerate(requests):
+        assert len(descs) == len(rules)
+        for entries, rid in zip(descs, rules):
+            if rid != NIL_RULE:
+                blob += cache_key_prefix(domain, entries)
+            off.append(len(blob))
+            rule.append(rid)
+            req_of.append(r)
+        now.append(t)
+        hits.append(ha)
+    return Batch(np.frombuffer(bytes(blob), dtype=np.uint8).copy(), np.array(off, np.uint32),
+                 np.array(rule, np.uint32), np.array(req_of, np.uint32), np.array(now, np.int64),
+                 np.array(hits, np.uint32))
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a.size else 0
+
+
+def _batch_struct(b: Batch, ptrs=None) -> RlBatch:
+    s = RlBatch()
+    s.n_desc, s.n_req, s.blob_bytes, s.reserved = b.n_desc, b.n_req, int(b.blob.shape[0]), 0
+    if ptrs is None:
+        ptrs = [_ptr(b.blob), _ptr(b.off), _ptr(b.rule), _ptr(b.req_of), _ptr(b.now), _ptr(b.hits)]
+    s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+    return s
+
+
+# ---------------------------------------------------------------------------
+# Engine (C ABI wrapper)
+# ---------------------------------------------------------------------------
+class Engine:
+    def __init__(self, device: int = 0, log2_slots=(16, 16, 16, 14), near_limit_ratio: float = 0.8,
+                 local_cache: bool = False, per_second_split: bool = False, max_batch_desc: int = 1 << 16,
+                 max_batch_req: Optional[int] = None, max_blob_bytes: Optional[int] = None, sort_bits: int = 48,
+                 hash_seed: int = 0x5EE7AB1E5EED):
+        self.lib = load_library()
+        cfg = RlConfig()
+        cfg.struct_size = C.sizeof(RlConfig)
+        cfg.device = device
+        for i, v in enumerate(log2_slots):
+            cfg.log2_slots[i] = v
+        cfg.near_limit_ratio = near_limit_ratio
+        cfg.local_cache = int(local_cache)
+        cfg.per_second_split = int(per_second_split)
+        cfg.max_batch_desc = max_batch_desc
+        cfg.max_batch_req = max_batch_req or max_batch_desc
+        cfg.max_blob_bytes = max_blob_bytes or max_batch_desc * 64
+        cfg.sort_bits = sort_bits
+        cfg.hash_seed = hash_seed
+        self.cfg = cfg
+        h = C.c_void_p()
+        rc = self.lib.rl_create(C.byref(cfg), C.byref(h))
+        if rc:
+            raise RedisError(f"rl_create failed: {RL_ERRORS.get(rc, rc)}")
+        self.h = h
+        self.near_limit_ratio = near_limit_ratio
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.rl_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc:
+            msg = self.lib.rl_last_error(self.h).decode()
+            raise RedisError(f"{what}: {RL_ERRORS.get(rc, rc)}: {msg}")
+
+    def load_rules(self, rules: Sequence[tuple]):
+        arr = (RlRule * max(1, len(rules)))()
+        for i, (L, u) in enumerate(rules):
+            arr[i].requests_per_unit = L
+            arr[i].unit = u
+        self._check(self.lib.rl_load_rules(self.h, arr, len(rules)), "rl_load_rules")
+
+    def submit(self, b: Batch):
+        """Host batch -> (status[n_desc] structured array, throttle_ms[n_req])."""
+        out = np.zeros(b.n_desc, STATUS_DTYPE)
+        thr = np.zeros(b.n_req, np.uint32)
+        s = _batch_struct(b)
+        self._check(self.lib.rl_submit(self.h, C.byref(s), _ptr(out) or None, _ptr(thr) or None), "rl_submit")
+        self._check(self.lib.rl_wait(self.h), "rl_wait")
+        return out, thr
+
+    def submit_device_async(self, n_desc: int, n_req: int, blob_bytes: int, ptrs, out_ptr: int, thr_ptr: int):
+        s = RlBatch()
+        s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
+        s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        self._check(self.lib.rl_submit_device(self.h, C.byref(s), out_ptr, thr_ptr), "rl_submit_device")
+
+    def wait(self):
+        self._check(self.lib.rl_wait(self.h), "rl_wait")
+
+    def reset(self):
+        self._check(self.lib.rl_reset(self.h), "rl_reset")
+
+    def stats(self) -> dict:
+        s = RlEngineStats()
+        self._check(self.lib.rl_get_stats(self.h, C.byref(s)), "rl_get_stats")
+        return {k: getattr(s, k) for k, _ in RlEngineStats._fields_}
+
+    def set_timing(self, on: bool):
+        self._check(self.lib.rl_set_timing(self.h, int(on)), "rl_set_timing")
+
+    def kernel_times(self) -> dict:
+        cap = 16
+        names = (C.c_char_p * cap)()
+        ms = (C.c_double * cap)()
+        cnt = (C.c_uint64 * cap)()
+        n = C.c_uint32()
+        self._check(self.lib.rl_kernel_times(self.h, names, ms, cnt, cap, C.byref(n)), "rl_kernel_times")
+        return {names[i].decode(): (ms[i], cnt[i]) for i in range(n.value)}
+
+    def last_batch_info(self) -> dict:
+        v = [C.c_uint64() for _ in range(4)]
+        self._check(self.lib.rl_last_batch_info(self.h, *[C.byref(x) for x in v]), "rl_last_batch_info")
+        return dict(zip(["unique_keys", "n_desc", "n_req", "blob_bytes"], [x.value for x in v]))
+
+    def stream(self) -> int:
+        return self.lib.rl_stream(self.h) or 0
+
+
+# ---------------------------------------------------------------------------
+# Mirror of the reference's RateLimitCache contract (for reference-style tests)
+# ---------------------------------------------------------------------------
+class Counter:
+    def __init__(self):
+        self.v = 0
+
+    def Add(self, d: int):
+        self.v += int(d)
+
+    def Value(self) -> int:
+        return self.v
+
+
+@dataclass
+class RateLimitStats:
+    TotalHits: Counter = field(default_factory=Counter)
+    OverLimit: Counter = field(default_factory=Counter)
+    NearLimit: Counter = field(default_factory=Counter)
+    OverLimitWithLocalCache: Counter = field(default_factory=Counter)
+
+
+class StatsStore:
+    """Counters shared by name, like gostats' NewCounter (config_impl.go:64-71)."""
+
+    def __init__(self):
+        self.m = {}
+
+    def get(self, key: str) -> RateLimitStats:
+        return self.m.setdefault(key, RateLimitStats())
+
+
+@dataclass(frozen=True)
+class RateLimitLimit:
+    RequestsPerUnit: int
+    Unit: int
+
+
+@dataclass
+class RateLimit:
+    FullKey: str
+    Stats: RateLimitStats
+    Limit: RateLimitLimit
+    SleepOnThrottle: bool = False
+    ReportDetails: bool = False
+
+
+def NewRateLimit(requests_per_unit: int, unit: int, key: str, scope: StatsStore, sleep_on_throttle=False,
+                 report_details=False) -> RateLimit:
+    """config.NewRateLimit  src/config/config_impl.go:79-89"""
+    return RateLimit(key, scope.get(key), RateLimitLimit(requests_per_unit, unit), sleep_on_throttle, report_details)
+
+
+@dataclass
+class RateLimitRequest:
+    Domain: str
+    Descriptors: list  # list of list of (key, value)
+    HitsAddend: int = 1
+
+
+def NewRateLimitRequest(domain: str, descriptors, hits_addend: int) -> RateLimitRequest:
+    """test/common/common.go NewRateLimitRequest"""
+    return RateLimitRequest(domain, [list(d) for d in descriptors], hits_addend)
+
+
+@dataclass(frozen=True)
+class DescriptorStatus:
+    Code: int
+    CurrentLimit: Optional[RateLimitLimit]
+    LimitRemaining: int
+    DurationUntilReset: Optional[int] = None
+
+
+@dataclass
+class DoLimitResponse:
+    DescriptorStatuses: list
+    ThrottleMillis: int = 0
+
+
+def CalculateReset(limit: RateLimitLimit, now: int) -> int:
+    """utils.CalculateReset  src/utils/utilities.go:34-38"""
+    d = UNIT_DIVIDER[limit.Unit]
+    return d - now % d
+
+
+class HipRateLimitCache:
+    """limiter.RateLimitCache on the HIP engine. do_limit() is DoLimit for one request;
+    do_limit_batch() submits several requests as ONE device batch in serial order."""
+
+    def __init__(self, time_source, local_cache: bool = False, near_limit_ratio: float = 0.8,
+                 per_second_split: bool = False, **engine_kw):
+        self.time_source = time_source
+        self.engine = Engine(near_limit_ratio=near_limit_ratio, local_cache=local_cache,
+                             per_second_split=per_second_split, **engine_kw)
+        self.rule_ids = {}
+        self.rules = []
+        self.dirty = False
+
+    def _rule(self, lim: RateLimitLimit) -> int:
+        k = (lim.RequestsPerUnit, lim.Unit)
+        if k not in self.rule_ids:
+            self.rule_ids[k] = len(self.rules)
+            self.rules.append(k)
+            self.dirty = True
+        return self.rule_ids[k]
+
+    def DoLimit(self, request: RateLimitRequest, limits: list) -> DoLimitResponse:
+        return self.do_limit_batch([(request, limits)])[0]
+
+    def Flush(self):
+        pass
+
+    def do_limit_batch(self, calls) -> list:
+        reqs = []
+        nows = []
+        for request, limits in calls:
+            assert len(request.Descriptors) == len(limits), "assert: len(request.Descriptors) == len(limits)"
+            now = self.time_source()
+            nows.append(now)
+            h = max(1, request.HitsAddend)
+            rules = []
+            for lim in limits:
+                if lim is None:
+                    rules.append(NIL_RULE)
+                else:
+                    rules.append(self._rule(lim.Limit))
+                    lim.Stats.TotalHits.Add(h)  # base_limiter.go:49-51
+            reqs.append((request.Domain, request.Descriptors, rules, request.HitsAddend, now))
+        if self.dirty:
+            self.engine.load_rules(self.rules)
+            self.dirty = False
+        st, thr = self.engine.submit(build_batch(reqs))
+        out = []
+        d = 0
+        for r, (request, limits) in enumerate(calls):
+            sts = []
+            for lim in limits:
+                s = st[d]
+                d += 1
+                code = int(s["code_flags"]) & 0xFF
+                fl = int(s["code_flags"]) >> 8
+                if lim is None or not fl & FLAG_HAS_LIMIT:
+                    sts.append(DescriptorStatus(code, None, int(s["limit_remaining"])))
+                    continue
+                sts.append(DescriptorStatus(code, lim.Limit, int(s["limit_remaining"]), int(s["reset_s"])))
+                lim.Stats.OverLimit.Add(int(s["over_limit_delta"]))
+                if fl & FLAG_LOCAL_CACHE_HIT:
+                    lim.Stats.OverLimitWithLocalCache.Add(int(s["over_limit_delta"]))
+                lim.Stats.NearLimit.Add(int(s["near_limit_delta"]))
+            out.append(DoLimitResponse(sts, int(thr[r])))
+        return out

@@ -1,0 +1,157 @@
+/*
+ * rl_hip.h — C ABI of the MI355X-native fixed-window rate-limit backend.
+ *
+ * This is the drop-in boundary for the reference's hot path. It replaces
+ *   limiter.RateLimitCache.DoLimit / Flush         src/limiter/cache.go:15-33
+ * as implemented by the Redis backend
+ *   fixedRateLimitCacheImpl.DoLimit                src/redis/fixed_cache_impl.go:31-123
+ *   redis.Client.PipeAppend / PipeDo (INCRBY+EXPIRE pipeline)
+ *                                                  src/redis/driver.go:13-47, fixed_cache_impl.go:26-29
+ * A Go `src/hip` package binds these entry points over cgo; the C++
+ * mirror of the Go interface lives in api-ratelimit_amd/csrc/rl_cache.hpp.
+ *
+ * Plain C types only; no exceptions cross the ABI. Every call returns 0 on success or a
+ * negative RL_E* code; rl_last_error() then holds a message (the Go side turns a
+ * non-zero return into panic(redis.RedisError(msg)), src/redis/driver.go:6-10, so the
+ * service maps it to the redis_error stat exactly as for Redis, service/ratelimit.go:276-281).
+ * All calls on one engine must come from one thread (the batch submitter).
+ */
+#ifndef RL_HIP_H
+#define RL_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RL_ABI_VERSION 1u
+
+/* rule id of a descriptor whose limit is nil ("don't check", src/limiter/cache.go:19-22) */
+#define RL_NIL_RULE 0xFFFFFFFFu
+
+/* pb.RateLimitResponse_RateLimit_Unit (go-control-plane v0.9.7) */
+enum { RL_UNIT_UNKNOWN = 0, RL_UNIT_SECOND = 1, RL_UNIT_MINUTE = 2, RL_UNIT_HOUR = 3, RL_UNIT_DAY = 4 };
+/* pb.RateLimitResponse_Code */
+enum { RL_CODE_UNKNOWN = 0, RL_CODE_OK = 1, RL_CODE_OVER_LIMIT = 2 };
+/* rl_status.code_flags bits 8.. */
+enum {
+  RL_FLAG_HAS_LIMIT = 1u,       /* DescriptorStatus.CurrentLimit != nil and DurationUntilReset set */
+  RL_FLAG_LOCAL_CACHE_HIT = 2u  /* over limit via the local cache: add over_limit_delta to
+                                   OverLimitWithLocalCache too (base_limiter.go:76-81) */
+};
+
+/* error codes */
+enum {
+  RL_OK = 0,
+  RL_EINVAL = -1,    /* bad argument / malformed batch */
+  RL_EHIP = -2,      /* HIP runtime error */
+  RL_ENOSPC = -3,    /* a counter-table region is full (raise log2_slots) */
+  RL_ECAPACITY = -4, /* batch larger than the engine was created for */
+  RL_ESTATE = -5,    /* call out of order (e.g. rl_wait without rl_submit) */
+  RL_EDEVICE = -6    /* device-side fault detected (bounded spin expired) */
+};
+
+typedef struct rl_engine rl_engine;
+
+/* Engine configuration (REDIS_* settings analogues, src/settings/settings.go:10-48). */
+typedef struct rl_config {
+  uint32_t struct_size;        /* = sizeof(rl_config) */
+  int32_t device;              /* HIP device ordinal (HIP_DEVICES) */
+  uint32_t log2_slots[4];      /* per unit SECOND/MINUTE/HOUR/DAY: slots per window generation (HIP_TABLE_SLOTS) */
+  float near_limit_ratio;      /* NEAR_LIMIT_RATIO, default 0.8 (settings.go:44) */
+  uint32_t local_cache;        /* 1 = local over-limit cache on (LOCAL_CACHE_SIZE_IN_BYTES > 0, settings.go:45) */
+  uint32_t per_second_split;   /* REDIS_PERSECOND (settings.go:35). The HIP table keeps every unit in its own
+                                  key space, i.e. it always behaves like the split configuration. */
+  uint32_t max_batch_desc;     /* capacity: descriptors per batch (HIP_BATCH_LIMIT) */
+  uint32_t max_batch_req;      /* capacity: requests per batch */
+  uint32_t max_blob_bytes;     /* capacity: key-prefix bytes per batch */
+  uint32_t sort_bits;          /* fingerprint bits radix-sorted per batch (8..64, multiple of 8; 0 = 48) */
+  uint64_t hash_seed;          /* fingerprint seed (randomise per process against hash flooding) */
+} rl_config;
+
+/* One rate-limit rule: config.RateLimit.Limit (src/config/config.go:26-32). */
+typedef struct rl_rule {
+  uint32_t requests_per_unit;
+  uint32_t unit; /* RL_UNIT_SECOND..RL_UNIT_DAY; anything else is RL_EINVAL (utilities.go:31 panics) */
+} rl_rule;
+
+/* A batch of requests in serial (enqueue) order. Descriptor i belongs to request req_of[i]
+ * (non-decreasing). Its cache-key prefix is the exact byte string
+ *   domain '_' key1 '_' value1 '_' ... keyN '_' valueN '_'
+ * of GenerateCacheKey (src/limiter/cache_key.go:57-65) without the window timestamp, which
+ * the device appends (cache_key.go:66-68): bytes prefix_blob[prefix_off[i] .. prefix_off[i+1]).
+ * The same struct carries host pointers (rl_submit) or device pointers (rl_submit_device). */
+typedef struct rl_batch {
+  uint32_t n_desc;
+  uint32_t n_req;
+  uint32_t blob_bytes;
+  uint32_t reserved;
+  const uint8_t* prefix_blob;
+  const uint32_t* prefix_off;  /* n_desc + 1 entries */
+  const uint32_t* rule_id;     /* n_desc, RL_NIL_RULE for a nil limit */
+  const uint32_t* req_of;      /* n_desc */
+  const int64_t* now;          /* n_req: unix seconds, one per request (TimeSource.UnixNow) */
+  const uint32_t* hits_addend; /* n_req: RateLimitRequest.HitsAddend (0 means 1, fixed_cache_impl.go:39) */
+} rl_batch;
+
+/* One DescriptorStatus plus its stat increments (20 B). */
+typedef struct rl_status {
+  uint32_t code_flags;       /* RL_CODE_* | RL_FLAG_* << 8 */
+  uint32_t limit_remaining;  /* DescriptorStatus.LimitRemaining */
+  uint32_t reset_s;          /* DescriptorStatus.DurationUntilReset.Seconds (0 if no limit) */
+  uint32_t over_limit_delta; /* add to Stats.OverLimit (and OverLimitWithLocalCache if LOCAL_CACHE_HIT) */
+  uint32_t near_limit_delta; /* add to Stats.NearLimit */
+} rl_status;
+/* Stats.TotalHits is incremented by max(1, HitsAddend) for every non-nil limit on the host
+ * (base_limiter.go:49-51); it needs no device round trip. */
+
+typedef struct rl_engine_stats {
+  uint64_t batches;           /* batches completed */
+  uint64_t descriptors;       /* descriptors decided */
+  uint64_t resorts;           /* batches re-sorted on the full fingerprint after a sort-prefix collision */
+  uint64_t live_slots_hint;   /* keys inserted since creation (monotone; not a live count) */
+} rl_engine_stats;
+
+int rl_create(const rl_config* cfg, rl_engine** out);
+void rl_destroy(rl_engine* e);
+const char* rl_last_error(const rl_engine* e);
+uint32_t rl_abi_version(void);
+
+/* Load (replace) the rule table. Rule ids index it. Must not be called while a batch is in flight. */
+int rl_load_rules(rl_engine* e, const rl_rule* rules, uint32_t n);
+
+/* Host-memory batch: copies in, runs the pipeline, copies back into out[n_desc] and
+ * req_throttle_ms[n_req] (DoLimitResponse.ThrottleMillis, base_limiter.go:163-165).
+ * Asynchronous: outputs are valid after rl_wait(). */
+int rl_submit(rl_engine* e, const rl_batch* batch, rl_status* out, uint32_t* req_throttle_ms);
+int rl_wait(rl_engine* e);
+
+/* Device-memory batch (inputs already resident in HBM; outputs stay in HBM). Ordered on
+ * the engine's stream; rl_wait() or the stream synchronises. Used by the multi-GPU router
+ * and by the benchmark. */
+int rl_submit_device(rl_engine* e, const rl_batch* device_batch, rl_status* d_out, uint32_t* d_req_throttle_ms);
+
+/* The engine's HIP stream (hipStream_t), for ordering external work against it. */
+void* rl_stream(rl_engine* e);
+
+/* Clear the counter table and local-cache state (FLUSHALL analogue; tests and restarts). */
+int rl_reset(rl_engine* e);
+
+int rl_get_stats(rl_engine* e, rl_engine_stats* s);
+
+/* Per-kernel timing with HIP events on the engine stream (off by default). When on, each
+ * pipeline kernel is bracketed by an event pair; rl_kernel_times() returns the accumulated
+ * milliseconds and launch counts for up to `cap` kernels, their names in names[] (static strings). */
+int rl_set_timing(rl_engine* e, int on);
+int rl_kernel_times(rl_engine* e, const char** names, double* total_ms, uint64_t* launches, uint32_t cap,
+                    uint32_t* n_out);
+
+/* Algorithmic-byte accounting for the last completed batch: unique keys U
+ * (segments), descriptors, requests and prefix bytes, read back from the device. */
+int rl_last_batch_info(rl_engine* e, uint64_t* unique_keys, uint64_t* n_desc, uint64_t* n_req,
+                       uint64_t* blob_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RL_HIP_H */

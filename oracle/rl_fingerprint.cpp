@@ -1,0 +1,36 @@
+// rl_fingerprint.cpp — independent restatement of the product's key fingerprint
+//  so tests can check the fingerprint kernel bit-for-bit.
+// TEST INFRASTRUCTURE ONLY. Decisions in rl_oracle.cpp use exact key strings, never this.
+#include <cstring>
+
+#include "rl_oracle.h"
+
+namespace {
+inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+inline uint64_t fmix(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xFF51AFD7ED558CCDull;
+  x ^= x >> 33;
+  x *= 0xC4CEB9FE1A85EC53ull;
+  x ^= x >> 33;
+  return x;
+}
+}  // namespace
+
+extern "C" void rlo_fingerprint(const uint8_t* prefix, uint32_t len, uint64_t window_start, uint32_t region,
+                                uint64_t seed, uint64_t* hi, uint64_t* lo) {
+  // lanes: a = seed ^ K0, b = (seed + K1) ^ (len << 32) ^ unit
+  uint64_t a = seed ^ 0x9E3779B97F4A7C15ull;
+  uint64_t b = (seed + 0xC2B2AE3D27D4EB4Full) ^ ((uint64_t)len << 32) ^ (uint64_t)region;
+  for (uint32_t o = 0; o < len; o += 8) {
+    uint64_t w = 0;
+    for (uint32_t k = 0; k < 8 && o + k < len; ++k) w |= (uint64_t)prefix[o + k] << (8 * k);  // little-endian, zero pad
+    a = rotl((a ^ w) * 0x165667B19E3779F9ull, 31);
+    b = (b + w) * 0xD6E8FEB86659FD93ull;
+    b ^= b >> 29;
+  }
+  a ^= window_start * 0xC2B2AE3D27D4EB4Full;
+  b = (b ^ window_start) * 0x165667B19E3779F9ull;
+  *hi = fmix(a + rotl(b, 23));
+  *lo = fmix(b ^ (a * 0xC4CEB9FE1A85EC53ull));
+}

@@ -1,0 +1,338 @@
+// rl_oracle.cpp — CPU restatement of the reference DoLimit hot path.
+// TEST INFRASTRUCTURE ONLY: see rl_oracle.h. Never part of the product path.
+//
+// Every function cites the reference file:line it restates (paths relative to the
+// kentik/api-ratelimit tree). The Redis stand-in is a string-keyed map whose
+// INCRBY returns the post-increment int64 (Redis semantics; pinned by
+// test/redis/driver_impl_test.go:121-133, miniredis v2.11.4: INCRBY -> 1 then 2).
+// EXPIRE is modelled as "the key lives for the rest of its window": the key string
+// embeds the window start (cache_key.go:66-68), so with non-decreasing request time
+// a key is never referenced after its window ends and its TTL (div + jitter >= div,
+// fixed_cache_impl.go:69-72) never decides an outcome.
+#include "rl_oracle.h"
+
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <unordered_set>
+#include <vector>
+
+namespace {
+
+// utils.UnitToDivider — src/utils/utilities.go:19-32. Other units panic there; we
+// report them as bad input (-2) before touching state.
+int64_t unit_to_divider(uint32_t unit) {
+  switch (unit) {
+    case RLO_UNIT_SECOND: return 1;
+    case RLO_UNIT_MINUTE: return 60;
+    case RLO_UNIT_HOUR: return 60 * 60;
+    case RLO_UNIT_DAY: return 60 * 60 * 24;
+  }
+  return 0;
+}
+
+// utils.Max — src/utils/utilities.go:40-45
+inline uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
+// Go's int64 division truncates toward zero, like C++.
+inline int64_t window_start(int64_t now, int64_t div) { return (now / div) * div; }
+
+// strconv.FormatInt(v, 10)
+void append_dec(std::string& s, int64_t v) {
+  char buf[24];
+  int n = snprintf(buf, sizeof buf, "%lld", (long long)v);
+  s.append(buf, (size_t)n);
+}
+
+}  // namespace
+
+struct rlo_engine {
+  float near_ratio;
+  bool local_cache;       // localCache != nil (base_limiter.go:58, :94)
+  bool per_second_split;  // perSecondClient != nil (fixed_cache_impl.go:75)
+  std::vector<rlo_rule> rules;
+  std::vector<uint32_t> near_thr;  // per rule, base_limiter.go:86
+  // Redis stand-ins: main client and per-second client (fixed_cache_impl.go:74-85).
+  std::unordered_map<std::string, int64_t> redis[2];
+  // freecache stand-in: set of over-limit keys (base_limiter.go:94-106).
+  std::unordered_set<std::string> lcache;
+  uint64_t lc_hit = 0, lc_miss = 0;
+};
+
+// C linkage comes from the declarations in rl_oracle.h.
+
+rlo_engine* rlo_create(float near_limit_ratio, int local_cache, int per_second_split) {
+  auto* e = new rlo_engine();
+  e->near_ratio = near_limit_ratio;
+  e->local_cache = local_cache != 0;
+  e->per_second_split = per_second_split != 0;
+  return e;
+}
+
+void rlo_destroy(rlo_engine* e) { delete e; }
+
+int rlo_load_rules(rlo_engine* e, const rlo_rule* rules, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i)
+    if (unit_to_divider(rules[i].unit) == 0) return -2;
+  e->rules.assign(rules, rules + n);
+  e->near_thr.resize(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    // nearLimitThreshold = uint32(math.Floor(float64(float32(L) * ratio)))  base_limiter.go:86
+    float p = (float)rules[i].requests_per_unit * e->near_ratio;  // float32 * float32
+    e->near_thr[i] = (uint32_t)std::floor((double)p);
+  }
+  return 0;
+}
+
+uint32_t rlo_cache_key(const uint8_t* prefix, uint32_t len, uint32_t unit, int64_t now, char* out, uint32_t cap) {
+  // GenerateCacheKey: domain '_' (key '_' value '_')* FormatInt((now/div)*div)  cache_key.go:57-68
+  std::string k((const char*)prefix, len);
+  append_dec(k, window_start(now, unit_to_divider(unit)));
+  uint32_t n = (uint32_t)k.size();
+  memcpy(out, k.data(), n < cap ? n : cap);
+  return n;
+}
+
+// GetResponseDescriptorStatus + checkOverLimitThreshold + checkNearLimitThreshold +
+// generateResponseDescriptorStatus + CalculateReset.
+//   base_limiter.go:70-115 (status), :129-145 (over), :154-177 (near), :179-195 (reset),
+//   utilities.go:34-38 (DurationUntilReset = div - now % div).
+// `after` is the uint32 INCRBY reply (fixed_cache_impl.go:51,109); before = after - h
+// with uint32 wraparound (:110). The local-cache Set on OVER_LIMIT is done by the caller.
+static void decide(uint32_t L, uint32_t near, int64_t div, int64_t now, uint32_t h, uint32_t before,
+                   uint32_t after, bool local_hit, bool has_limit, rlo_status* o, uint32_t* throttle) {
+  *throttle = 0;
+  o->over_limit_delta = 0;
+  o->near_limit_delta = 0;
+  if (!has_limit) {  // key == "" -> {OK, nil, 0} without reset  :72-75, :189-193
+    o->code_flags = RLO_CODE_OK;
+    o->limit_remaining = 0;
+    o->reset_s = 0;
+    return;
+  }
+  const uint32_t reset = (uint32_t)(div - now % div);
+  if (local_hit) {  // :76-81
+    o->code_flags = RLO_CODE_OVER_LIMIT | ((RLO_FLAG_HAS_LIMIT | RLO_FLAG_LOCAL_CACHE_HIT) << 8);
+    o->limit_remaining = 0;
+    o->reset_s = reset;
+    o->over_limit_delta = h;  // OverLimit.Add(h) and OverLimitWithLocalCache.Add(h)
+    return;
+  }
+  o->reset_s = reset;
+  if (after > L) {  // :88
+    o->code_flags = RLO_CODE_OVER_LIMIT | (RLO_FLAG_HAS_LIMIT << 8);
+    o->limit_remaining = 0;
+    // checkOverLimitThreshold :129-145
+    if (before >= L) {
+      o->over_limit_delta = h;
+    } else {
+      o->over_limit_delta = after - L;
+      o->near_limit_delta = L - umax(near, before);
+    }
+  } else {
+    o->code_flags = RLO_CODE_OK | (RLO_FLAG_HAS_LIMIT << 8);
+    o->limit_remaining = L - after;  // :108-109
+    // checkNearLimitThreshold :154-177
+    if (after > near) {
+      const int64_t end = window_start(now, div) + div;
+      const uint32_t millis = (uint32_t)(end - now) * 1000u;
+      const uint32_t calls = umax(L - after, 1u);
+      *throttle = millis / calls;
+      o->near_limit_delta = (before >= near) ? h : after - near;
+    }
+  }
+}
+
+void rlo_decide(uint32_t requests_per_unit, uint32_t unit, float near_limit_ratio, int64_t now, uint32_t hits,
+                uint32_t before, uint32_t after, int local_cache_hit, int has_limit, rlo_status* out,
+                uint32_t* throttle_ms) {
+  const float p = (float)requests_per_unit * near_limit_ratio;
+  const uint32_t near = (uint32_t)std::floor((double)p);
+  int64_t div = unit_to_divider(unit);
+  if (div == 0) div = 1;
+  decide(requests_per_unit, near, div, now, hits, before, after, local_cache_hit != 0, has_limit != 0, out,
+         throttle_ms);
+}
+
+namespace {
+
+struct Desc {
+  uint32_t i;
+  std::string key;
+  bool per_second;
+};
+
+// Validate one batch; returns 0 or a negative error.
+int validate(const rlo_engine* e, uint32_t n_desc, const uint32_t* prefix_off, const uint32_t* rule_id,
+             const uint32_t* req_of, uint32_t n_req) {
+  for (uint32_t i = 0; i < n_desc; ++i) {
+    if (prefix_off[i + 1] < prefix_off[i]) return -1;
+    if (req_of[i] >= n_req) return -1;
+    if (i && req_of[i] < req_of[i - 1]) return -1;
+    if (rule_id[i] != RLO_NIL_RULE && rule_id[i] >= e->rules.size()) return -1;
+  }
+  return 0;
+}
+
+// One request: fixedRateLimitCacheImpl.DoLimit, fixed_cache_impl.go:31-123.
+// Descriptors [d0, d1) of the batch; `own` filters descriptors to a key shard
+// (nullptr = all). Returns the request's ThrottleMillis contribution.
+template <class Own>
+uint32_t do_limit(rlo_engine* e, uint32_t d0, uint32_t d1, const uint8_t* blob, const uint32_t* off,
+                  const uint32_t* rule_id, int64_t now, uint32_t hits_addend, rlo_status* out, Own own) {
+  // hitsAddend := utils.Max(1, request.HitsAddend)  :39
+  const uint32_t h = umax(1u, hits_addend);
+  // GenerateCacheKeys (one `now` per request, base_limiter.go:43) :42
+  std::vector<Desc> keys;
+  keys.reserve(d1 - d0);
+  for (uint32_t i = d0; i < d1; ++i) {
+    Desc d{i, std::string(), false};
+    const uint32_t r = rule_id[i];
+    if (r != RLO_NIL_RULE) {  // nil limit -> "" key (cache_key.go:46-51)
+      const rlo_rule& rule = e->rules[r];
+      d.key.assign((const char*)blob + off[i], off[i + 1] - off[i]);
+      append_dec(d.key, window_start(now, unit_to_divider(rule.unit)));
+      d.per_second = rule.unit == RLO_UNIT_SECOND;  // cache_key.go:33-35,70-72
+    }
+    keys.push_back(std::move(d));
+  }
+  // HOT LOOP 1 :55-86 — local-cache lookups for every descriptor precede any Set.
+  std::vector<char> local_hit(keys.size(), 0), skip(keys.size(), 0);
+  std::vector<uint32_t> results(keys.size(), 0);
+  for (size_t k = 0; k < keys.size(); ++k) {
+    if (!own(keys[k])) { skip[k] = 1; continue; }
+    if (keys[k].key.empty()) continue;
+    if (e->local_cache) {  // IsOverLimitWithLocalCache base_limiter.go:57-66
+      if (e->lcache.count(keys[k].key)) { ++e->lc_hit; local_hit[k] = 1; continue; }
+      ++e->lc_miss;
+    }
+    // INCRBY key h (post value, missing = 0) into results[i] as uint32; EXPIRE (TTL only).
+    const int store = (e->per_second_split && keys[k].per_second) ? 1 : 0;
+    int64_t& c = e->redis[store][keys[k].key];
+    c += (int64_t)h;
+    results[k] = (uint32_t)c;
+  }
+  // HOT LOOP 2 :108-117
+  uint32_t throttle_max = 0;
+  for (size_t k = 0; k < keys.size(); ++k) {
+    if (skip[k]) continue;
+    const uint32_t i = keys[k].i;
+    const uint32_t r = rule_id[i];
+    const bool has = !keys[k].key.empty();
+    uint32_t L = 0, near = 0;
+    int64_t div = 1;
+    if (has) {
+      L = e->rules[r].requests_per_unit;
+      near = e->near_thr[r];
+      div = unit_to_divider(e->rules[r].unit);
+    }
+    uint32_t thr = 0;
+    // limitBeforeIncrease := limitAfterIncrease - hitsAddend (uint32 wrap)  fixed_cache_impl.go:109-110
+    decide(L, near, div, now, h, results[k] - h, results[k], local_hit[k] != 0, has, &out[i], &thr);
+    // response.ThrottleMillis = max(...)  base_limiter.go:163-165
+    if (thr > throttle_max) throttle_max = thr;
+    // localCache.Set(key) on OVER_LIMIT from Redis  base_limiter.go:94-106
+    if (has && !local_hit[k] && e->local_cache && results[k] > L) e->lcache.insert(keys[k].key);
+  }
+  return throttle_max;
+}
+
+}  // namespace
+
+int rlo_submit(rlo_engine* e, uint32_t n_desc, const uint8_t* prefix_blob, const uint32_t* prefix_off,
+               const uint32_t* rule_id, const uint32_t* req_of, uint32_t n_req, const int64_t* now,
+               const uint32_t* hits_addend, rlo_status* out, uint32_t* req_throttle_ms) {
+  int rc = validate(e, n_desc, prefix_off, rule_id, req_of, n_req);
+  if (rc) return rc;
+  for (uint32_t r = 0; r < n_req; ++r) req_throttle_ms[r] = 0;
+  uint32_t d = 0;
+  for (uint32_t r = 0; r < n_req; ++r) {
+    uint32_t d1 = d;
+    while (d1 < n_desc && req_of[d1] == r) ++d1;
+    req_throttle_ms[r] = do_limit(e, d, d1, prefix_blob, prefix_off, rule_id, now[r], hits_addend[r], out,
+                                  [](const Desc&) { return true; });
+    d = d1;
+  }
+  return 0;
+}
+
+int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* prefix_blob,
+                  const uint32_t* prefix_off, const uint32_t* rule_id, const uint32_t* req_of, uint32_t n_req,
+                  const int64_t* now, const uint32_t* hits_addend, rlo_status* out, uint32_t* req_throttle_ms) {
+  if (n_threads <= 1)
+    return rlo_submit(e, n_desc, prefix_blob, prefix_off, rule_id, req_of, n_req, now, hits_addend, out,
+                      req_throttle_ms);
+  int rc = validate(e, n_desc, prefix_off, rule_id, req_of, n_req);
+  if (rc) return rc;
+  // Key-sharded: each thread owns keys with hash % n_threads == t and its own Redis /
+  // local-cache shard. Per-key serial order is kept, so outputs equal rlo_submit's.
+  const int T = n_threads;
+  std::vector<rlo_engine*> shard(T);
+  for (int t = 0; t < T; ++t) {
+    shard[t] = new rlo_engine();
+    shard[t]->near_ratio = e->near_ratio;
+    shard[t]->local_cache = e->local_cache;
+    shard[t]->per_second_split = e->per_second_split;
+    shard[t]->rules = e->rules;
+    shard[t]->near_thr = e->near_thr;
+  }
+  // Move existing state into shards.
+  std::hash<std::string> H;
+  for (int s = 0; s < 2; ++s)
+    for (auto& kv : e->redis[s]) shard[H(kv.first) % T]->redis[s].emplace(kv.first, kv.second);
+  for (auto& k : e->lcache) shard[H(k) % T]->lcache.insert(k);
+  std::vector<std::vector<uint32_t>> thr(T, std::vector<uint32_t>(n_req, 0));
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) {
+    th.emplace_back([&, t] {
+      uint32_t d = 0;
+      for (uint32_t r = 0; r < n_req; ++r) {
+        uint32_t d1 = d;
+        while (d1 < n_desc && req_of[d1] == r) ++d1;
+        // nil-limit descriptors (empty key) go to shard 0
+        thr[t][r] = do_limit(shard[t], d, d1, prefix_blob, prefix_off, rule_id, now[r], hits_addend[r], out,
+                             [&](const Desc& k) { return (int)(k.key.empty() ? 0 : H(k.key) % T) == t; });
+        d = d1;
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  e->redis[0].clear();
+  e->redis[1].clear();
+  e->lcache.clear();
+  for (int t = 0; t < T; ++t) {
+    for (int s = 0; s < 2; ++s) e->redis[s].insert(shard[t]->redis[s].begin(), shard[t]->redis[s].end());
+    e->lcache.insert(shard[t]->lcache.begin(), shard[t]->lcache.end());
+    e->lc_hit += shard[t]->lc_hit;
+    e->lc_miss += shard[t]->lc_miss;
+    delete shard[t];
+  }
+  for (uint32_t r = 0; r < n_req; ++r) {
+    uint32_t m = 0;
+    for (int t = 0; t < T; ++t) m = thr[t][r] > m ? thr[t][r] : m;
+    req_throttle_ms[r] = m;
+  }
+  return 0;
+}
+
+int64_t rlo_counter(rlo_engine* e, const char* key, uint32_t len, int per_second) {
+  const int s = (e->per_second_split && per_second) ? 1 : 0;
+  auto it = e->redis[s].find(std::string(key, len));
+  return it == e->redis[s].end() ? -1 : it->second;
+}
+
+int rlo_local_cached(rlo_engine* e, const char* key, uint32_t len) {
+  return e->lcache.count(std::string(key, len)) ? 1 : 0;
+}
+
+uint64_t rlo_num_keys(rlo_engine* e) { return e->redis[0].size() + e->redis[1].size(); }
+
+void rlo_local_cache_stats(rlo_engine* e, uint64_t* hit, uint64_t* miss, uint64_t* lookup, uint64_t* entries) {
+  *hit = e->lc_hit;
+  *miss = e->lc_miss;
+  *lookup = e->lc_hit + e->lc_miss;
+  *entries = e->lcache.size();
+}
+

@@ -1,0 +1,161 @@
+"""Differential parity: HIP path (C ABI) vs the CPU oracle on seeded request streams.
+
+Bit-exact on every descriptor status, stat delta and request throttle. Streams mix
+domains, 1-4 entry descriptors, nil limits, duplicate descriptors in one request,
+key-string collisions ("a_b","c" vs "a","b_c"), hits_addend 0..8, per-request limit
+overrides sharing one key (different L, same unit), every unit, window rollover, and the
+local over-limit cache on and off. Keys whose exact strings come from two different
+units are excluded (the device keeps unit key spaces apart).
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+import hiprl
+import oracle
+import streams
+
+pytestmark = pytest.mark.gpu
+
+UNITS = [hiprl.SECOND, hiprl.MINUTE, hiprl.HOUR, hiprl.DAY]
+LS = [1, 3, 10, 40]  # limits per unit -> rule id = u * len(LS) + l
+RULES = [(L, u) for u in UNITS for L in LS]
+
+
+def make_stream(seed, n_req, t0, keyspace=40, max_desc=4, nil_p=0.08, override_p=0.05, dt_max=2):
+    rng = np.random.default_rng(seed)
+    reqs = []
+    t = t0
+    for _ in range(n_req):
+        if rng.random() < 0.02:
+            t += int(rng.integers(1, dt_max + 1))
+        dom = ["dom", "a", "a_b"][int(rng.integers(0, 3))]
+        nd = int(rng.integers(1, max_desc + 1))
+        descs, rules = [], []
+        for _ in range(nd):
+            kind = rng.random()
+            if kind < 0.1:  # colliding entry splits: same key string
+                descs.append([("a_b", "c")] if rng.random() < 0.5 else [("a", "b_c")])
+            else:
+                ne = int(rng.integers(1, 4))
+                descs.append([(f"k{j}", f"v{int(rng.integers(0, keyspace))}") for j in range(ne)])
+            if rng.random() < nil_p:
+                rules.append(streams.NIL)
+                continue
+            prefix = hiprl.cache_key_prefix(dom, descs[-1])
+            hsh = zlib.crc32(prefix)
+            u = hsh % 4  # the unit is a function of the key string
+            li = (hsh >> 8) % len(LS)
+            if rng.random() < override_p:
+                li = int(rng.integers(0, len(LS)))
+            rules.append(u * len(LS) + li)
+        if rng.random() < 0.05 and nd > 0:  # duplicate a descriptor inside the request
+            descs.append(descs[0])
+            rules.append(rules[0])
+        reqs.append((dom, descs, rules, int(rng.integers(0, 9)), t))
+    return reqs
+
+
+def batch_sizes(reqs, rng, max_bs):
+    """Random batch cuts that keep each batch within two adjacent seconds."""
+    sizes, i = [], 0
+    while i < len(reqs):
+        bs = int(rng.integers(1, max_bs + 1))
+        j = i + 1
+        t_lo = reqs[i][4]
+        while j < len(reqs) and j - i < bs and reqs[j][4] - t_lo <= 1:
+            j += 1
+        sizes.append(j - i)
+        i = j
+    return sizes
+
+
+def run_both(reqs, sizes, local_cache, sort_bits=48, ratio=0.8):
+    o = oracle.Oracle(near_limit_ratio=ratio, local_cache=local_cache)
+    o.load_rules(RULES)
+    e = hiprl.Engine(near_limit_ratio=ratio, local_cache=local_cache, sort_bits=sort_bits, max_batch_desc=1 << 17)
+    e.load_rules(RULES)
+    a = streams.replay(o, reqs, sizes)
+    b = streams.replay(e, reqs, sizes)
+    return a, b, e
+
+
+@pytest.mark.parametrize("local_cache", [False, True])
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_streams(seed, local_cache):
+    reqs = make_stream(seed, 6000, t0=1_700_000_000 - 7 + seed * 3600 * 24 - 130)
+    sizes = batch_sizes(reqs, np.random.default_rng(seed + 100), 1500)
+    (ost, othr), (gst, gthr), _ = run_both(reqs, sizes, local_cache)
+    streams.assert_same(ost, othr, gst, gthr, f"seed={seed} local={local_cache}")
+
+
+@pytest.mark.parametrize("sort_bits", [8, 16, 64])
+def test_sort_prefix_widths_and_resort(sort_bits):
+    """Narrow sort prefixes make different keys share a sorted run; the engine must detect
+    it and re-sort on the full fingerprint (resorts > 0 at 8 bits) with identical output."""
+    reqs = make_stream(11, 4000, t0=1_600_000_000, keyspace=400)
+    sizes = batch_sizes(reqs, np.random.default_rng(5), 2000)
+    (ost, othr), (gst, gthr), eng = run_both(reqs, sizes, True, sort_bits=sort_bits)
+    streams.assert_same(ost, othr, gst, gthr, f"sort_bits={sort_bits}")
+    if sort_bits == 8:
+        assert eng.stats()["resorts"] > 0
+
+
+def test_hot_key_long_segments():
+    """One key hit thousands of times in one batch (segments span many scan tiles), with
+    the local cache freezing it mid-batch, and a second hot key under a large limit."""
+    reqs = []
+    t = 1_650_000_000
+    for i in range(30000):
+        if i % 3 == 0:
+            reqs.append(("hot", [[("k", "x")]], [2], 1, t))          # L=10 SECOND -> freezes early
+        elif i % 3 == 1:
+            reqs.append(("hot", [[("k", "y")]], [3 + 4 * 2], 2, t))  # L=40 HOUR
+        else:
+            reqs.append(("hot", [[("k", f"c{i % 997}")]], [1 + 4], 1, t))
+    for lc in (False, True):
+        (ost, othr), (gst, gthr), _ = run_both(reqs, [len(reqs)], lc)
+        streams.assert_same(ost, othr, gst, gthr, f"hot local={lc}")
+
+
+def test_window_rollover_across_batches():
+    """Counters reset at each window boundary; old-generation slots are reused."""
+    reqs = []
+    t = 1_700_003_595  # 5 s before an hour boundary
+    for s in range(12):
+        for i in range(200):
+            reqs.append(("roll", [[("k", str(i % 50))]], [(s + i) % 16], 1 + (i % 3), t + s))
+    sizes = [200] * 12
+    for lc in (False, True):
+        (ost, othr), (gst, gthr), _ = run_both(reqs, sizes, lc)
+        streams.assert_same(ost, othr, gst, gthr, f"rollover local={lc}")
+
+
+def test_large_hits_addend_and_counter_wrap():
+    """uint32 wraparound of INCRBY replies (fixed_cache_impl.go:109-110)."""
+    big = 0xFFFFFFF0
+    reqs = [("w", [[("k", "1")]], [3], big, 1000), ("w", [[("k", "1")]], [3], big, 1000),
+            ("w", [[("k", "1")]], [3], 40, 1000), ("w", [[("k", "2")]], [3], 0, 1000)]
+    for lc in (False, True):
+        (ost, othr), (gst, gthr), _ = run_both(reqs, [2, 2], lc)
+        streams.assert_same(ost, othr, gst, gthr, f"wrap local={lc}")
+
+
+def test_error_paths():
+    eng = hiprl.Engine()
+    eng.load_rules([(5, hiprl.SECOND)])
+    # rule id out of range is rejected before any device work
+    with pytest.raises(hiprl.RedisError):
+        eng.submit(hiprl.build_batch([("d", [[("a", "b")]], [7], 1, 10)]))
+    # a batch spanning three seconds of SECOND windows is rejected
+    with pytest.raises(hiprl.RedisError, match="window"):
+        eng.submit(hiprl.build_batch([("d", [[("a", "b")]], [0], 1, 10), ("d", [[("a", "b")]], [0], 1, 12)]))
+    # the engine keeps working afterwards
+    st, _ = eng.submit(hiprl.build_batch([("d", [[("a", "b")]], [0], 1, 13)]))
+    assert int(st["limit_remaining"][0]) == 4
+    # a full table region is reported, not silently dropped
+    small = hiprl.Engine(log2_slots=(4, 4, 4, 4))
+    small.load_rules([(5, hiprl.SECOND)])
+    with pytest.raises(hiprl.RedisError, match="full"):
+        small.submit(hiprl.build_batch([("d", [[("a", str(i))]], [0], 1, 10) for i in range(100)]))
