@@ -120,16 +120,21 @@ enum : uint32_t {
   ERR_WINDOW_SPAN = 32u,  // a region saw window generations more than one apart in one batch
 };
 
-// Small device control block, zeroed per batch.
+// Small device control block, zeroed per batch. Same-line atomics serialise at the L2
+// (~9 ns each on MI355X, measured), so every word that more than one block writes is
+// either written once by a single reducer block or lives on a 256-B line of its own.
 struct EngineCtl {
-  uint32_t err;
-  uint32_t n_nil;        // nil-limit descriptors (sorted to the tail)
-  uint32_t n_segments;   // unique keys in the batch (U)
-  uint32_t n_inserted;   // new keys inserted
-  uint32_t gen_min[8];   // per region: ~(min window generation) (max of complements; zero-init)
-  uint32_t gen_max[8];
-  uint32_t tile_ctr[32]; // dynamic tile counters per kernel launch slot
+  uint32_t err;          // atomicOr, only on an error
+  uint32_t n_nil;        // nil-limit descriptors (sorted to the tail); written by k_hist_scan
+  uint32_t n_segments;   // unique keys in the batch (U); written by k_leader block 0
+  uint32_t n_inserted;   // reserved
+  uint32_t gen_min[8];   // per region: min window generation in the batch (k_hist_scan)
+  uint32_t gen_max[8];   // per region: max window generation in the batch (k_hist_scan)
+  uint32_t pad0[64 - 20];
+  uint32_t tile_ctr[32][64];  // dynamic tile tickets, one 256-B line each
 };
+static_assert(sizeof(EngineCtl) == 256 + 32 * 256, "EngineCtl layout");
+constexpr int FP_PART_WORDS = 17;  // per fingerprint block: 8 x ~min gen, 8 x max gen, nil count
 
 // Counter table: 8 regions (unit x window parity), region r has 2^region_log2[r] slots.
 struct TableDesc {

@@ -19,9 +19,11 @@
 
 namespace rlhip {
 void launch_fingerprint(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint64_t*, ItemRec*,
-                        rl_status*, uint32_t*, int, int, EngineCtl*);
-void launch_histogram(hipStream_t, const uint64_t*, uint32_t, int, int, uint32_t*);
-void launch_hist_scan(hipStream_t, const uint32_t*, uint32_t*, int);
+                        rl_status*, uint32_t*, uint32_t*, EngineCtl*);
+void launch_histogram(hipStream_t, const uint64_t*, uint32_t, int, int, uint32_t*, const uint32_t*, uint32_t*);
+void launch_hist_scan(hipStream_t, const uint32_t*, uint32_t, uint32_t*, int, const uint32_t*, EngineCtl*);
+uint32_t hist_blocks(uint32_t n);
+uint32_t hist_sub_words();
 void launch_fallback_lo_keys(hipStream_t, const ItemRec*, const uint64_t*, uint32_t, uint64_t*, uint32_t*);
 void launch_gather_keys(hipStream_t, const uint64_t*, const uint32_t*, uint32_t, uint64_t*);
 uint32_t sort_tiles(uint32_t n);
@@ -29,9 +31,9 @@ uint32_t scan_tiles(uint32_t n);
 void launch_sort_pass(hipStream_t, const uint64_t*, const uint32_t*, uint64_t*, uint32_t*, uint32_t, int,
                       const uint32_t*, uint32_t*, uint32_t*, EngineCtl*);
 void launch_scan(hipStream_t, const uint64_t*, const uint32_t*, const ItemRec*, uint32_t, int, int, SortedRec*,
-                 uint64_t*, uint64_t*, uint32_t*, EngineCtl*);
+                 uint64_t*, uint64_t*, uint32_t*, uint32_t*, EngineCtl*);
 void launch_leader(hipStream_t, const uint64_t*, const SortedRec*, const ItemRec*, const DevRule*, uint32_t,
-                   const TableDesc&, int, SegInfo*, EngineCtl*);
+                   const TableDesc&, int, SegInfo*, const uint32_t*, EngineCtl*);
 void launch_decide(hipStream_t, const SortedRec*, const SegInfo*, const DevRule*, uint32_t, rl_status*, uint32_t*,
                    EngineCtl*);
 }  // namespace rlhip
@@ -41,9 +43,10 @@ using namespace rlhip;
 namespace {
 
 enum KernelId {
-  KT_FINGERPRINT, KT_HIST_SCAN, KT_SORT_PASS, KT_SCAN, KT_LEADER, KT_DECIDE, KT_FALLBACK, KT_MEMSET, KT_COUNT
+  KT_FINGERPRINT, KT_HISTOGRAM, KT_HIST_SCAN, KT_SORT_PASS, KT_SCAN, KT_LEADER, KT_DECIDE, KT_FALLBACK, KT_MEMSET,
+  KT_COUNT
 };
-const char* const kKernelNames[KT_COUNT] = {"k_fingerprint", "k_hist_scan", "k_sort_pass", "k_scan",
+const char* const kKernelNames[KT_COUNT] = {"k_fingerprint", "k_histogram", "k_hist_scan", "k_sort_pass", "k_scan",
                                             "k_leader",      "k_decide",    "fallback",    "memset"};
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -81,6 +84,10 @@ struct rl_engine {
   SortedRec* srec = nullptr;
   SegInfo* seg = nullptr;
   uint32_t* offs = nullptr;
+  uint32_t* hist_part = nullptr;  // per-block partial digit histograms
+  uint32_t* fp_part = nullptr;    // per-block fingerprint partials (generation range, nil count)
+  uint32_t* fp_part2 = nullptr;   // the same folded per histogram block
+  uint32_t* tile_heads = nullptr; // per-scan-tile segment-head counts
   uint8_t* zero_block = nullptr;  // ctl | hist | lookbacks (zeroed per batch)
   size_t zero_cap = 0;
   EngineCtl* h_ctl = nullptr;     // pinned copy of the control block
@@ -139,12 +146,11 @@ struct rl_engine {
   }
 
   // Layout of the per-batch zero block for n descriptors; returns the bytes used.
-  struct ZLayout { size_t ctl, hist, lb_sort, lb_sum, lb_head, total; };
+  struct ZLayout { size_t ctl, lb_sort, lb_sum, lb_head, total; };
   ZLayout zlayout(uint32_t n, int passes) const {
     ZLayout z;
     z.ctl = 0;
-    z.hist = align_up(sizeof(EngineCtl), 256);
-    z.lb_sort = z.hist + align_up((size_t)MAX_PASSES * RADIX * 4, 256);
+    z.lb_sort = align_up(sizeof(EngineCtl), 256);
     z.lb_sum = z.lb_sort + align_up((size_t)passes * sort_tiles(n > 0 ? n : 1) * RADIX * 4, 256);
     z.lb_head = z.lb_sum + align_up((size_t)scan_tiles(n > 0 ? n : 1) * 8, 256);
     z.total = z.lb_head + align_up((size_t)scan_tiles(n > 0 ? n : 1) * 8, 256);
@@ -161,15 +167,16 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bo
   const int passes = full ? 16 : npasses;
   const ZLayout z = zlayout(n, passes);
   EngineCtl* ctl = reinterpret_cast<EngineCtl*>(zero_block + z.ctl);
-  uint32_t* hist = reinterpret_cast<uint32_t*>(zero_block + z.hist);
+  uint32_t* hist = hist_part;
   uint32_t* lb_sort = reinterpret_cast<uint32_t*>(zero_block + z.lb_sort);
   uint64_t* lb_sum = reinterpret_cast<uint64_t*>(zero_block + z.lb_sum);
   uint64_t* lb_head = reinterpret_cast<uint64_t*>(zero_block + z.lb_head);
-  const size_t lb_pass_stride = (size_t)sort_tiles(n > 0 ? n : 1) * RADIX;
+  const size_t lb_pass_stride = (size_t)sort_tiles(n > 0 ? n : 1) * RADIX;  // per-digit look-back words
   hipError_t e;
   timed(KT_MEMSET, [&] {
     hipMemsetAsync(zero_block, 0, z.total, stream);
-    if (b.n_req) hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
+    // request throttles are zeroed by k_fingerprint; only an empty batch needs a memset
+    if (b.n_req && n == 0) hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
   });
   if (n == 0) {
     e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
@@ -179,18 +186,18 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bo
   const uint32_t* svals;
   if (!full) {
     timed(KT_FINGERPRINT, [&] {
-      launch_fingerprint(stream, b, d_rules, n_rules, cfg.hash_seed, keys_orig, recs, out, hist, lo_bit, npasses,
-                         ctl);
+      launch_fingerprint(stream, b, d_rules, n_rules, cfg.hash_seed, keys_orig, recs, out, thr, fp_part, ctl);
     });
-    timed(KT_HIST_SCAN, [&] { launch_hist_scan(stream, hist, offs, npasses); });
+    timed(KT_HISTOGRAM, [&] { launch_histogram(stream, keys_orig, n, lo_bit, npasses, hist, fp_part, fp_part2); });
+    timed(KT_HIST_SCAN, [&] { launch_hist_scan(stream, hist, n, offs, npasses, fp_part2, ctl); });
     const uint64_t* kin = keys_orig;
     const uint32_t* vin = nullptr;
     for (int p = 0; p < npasses; ++p) {
       uint64_t* kout = (p & 1) ? keys_b : keys_a;
       uint32_t* vout = (p & 1) ? vals_b : vals_a;
       timed(KT_SORT_PASS, [&] {
-        launch_sort_pass(stream, kin, vin, kout, vout, n, lo_bit + 8 * p, offs + p * RADIX,
-                         lb_sort + p * lb_pass_stride, &ctl->tile_ctr[p], ctl);
+        launch_sort_pass(stream, kin, vin, kout, vout, n, lo_bit + 8 * p, offs + p * hist_sub_words(),
+                         lb_sort + p * lb_pass_stride, &ctl->tile_ctr[p][0], ctl);
       });
       kin = kout;
       vin = vout;
@@ -200,10 +207,10 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bo
   } else {
     // Full-fingerprint order: stable sort by fp_lo, then by the 64-bit sort key.
     timed(KT_FALLBACK, [&] {
-      launch_fingerprint(stream, b, d_rules, n_rules, cfg.hash_seed, keys_orig, recs, out, hist, 0, 0, ctl);
+      launch_fingerprint(stream, b, d_rules, n_rules, cfg.hash_seed, keys_orig, recs, out, thr, fp_part, ctl);
       launch_fallback_lo_keys(stream, recs, keys_orig, n, keys_a, vals_a);
-      launch_histogram(stream, keys_a, n, 0, 8, hist);
-      launch_hist_scan(stream, hist, offs, 8);
+      launch_histogram(stream, keys_a, n, 0, 8, hist, fp_part, fp_part2);
+      launch_hist_scan(stream, hist, n, offs, 8, fp_part2, ctl);
     });
     const uint64_t* kin = keys_a;
     const uint32_t* vin = vals_a;
@@ -211,8 +218,8 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bo
       uint64_t* kout = (p & 1) ? keys_a : keys_b;
       uint32_t* vout = (p & 1) ? vals_a : vals_b;
       timed(KT_SORT_PASS, [&] {
-        launch_sort_pass(stream, kin, vin, kout, vout, n, 8 * p, offs + p * RADIX, lb_sort + p * lb_pass_stride,
-                         &ctl->tile_ctr[p], ctl);
+        launch_sort_pass(stream, kin, vin, kout, vout, n, 8 * p, offs + p * hist_sub_words(), lb_sort + p * lb_pass_stride,
+                         &ctl->tile_ctr[p][0], ctl);
       });
       kin = kout;
       vin = vout;
@@ -220,8 +227,8 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bo
     // after 8 passes the result is in keys_a/vals_a; gather the sort keys in that order
     timed(KT_FALLBACK, [&] {
       launch_gather_keys(stream, keys_orig, vals_a, n, keys_b);
-      launch_histogram(stream, keys_b, n, 0, 8, hist + 8 * RADIX);
-      launch_hist_scan(stream, hist + 8 * RADIX, offs + 8 * RADIX, 8);
+      launch_histogram(stream, keys_b, n, 0, 8, hist, nullptr, nullptr);
+      launch_hist_scan(stream, hist, n, offs + 8 * hist_sub_words(), 8, nullptr, ctl);
     });
     kin = keys_b;
     vin = vals_a;
@@ -229,8 +236,8 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bo
       uint64_t* kout = (p & 1) ? keys_b : keys_a;
       uint32_t* vout = (p & 1) ? vals_a : vals_b;
       timed(KT_SORT_PASS, [&] {
-        launch_sort_pass(stream, kin, vin, kout, vout, n, 8 * p, offs + (8 + p) * RADIX,
-                         lb_sort + (8 + p) * lb_pass_stride, &ctl->tile_ctr[8 + p], ctl);
+        launch_sort_pass(stream, kin, vin, kout, vout, n, 8 * p, offs + (8 + p) * hist_sub_words(),
+                         lb_sort + (8 + p) * lb_pass_stride, &ctl->tile_ctr[8 + p][0], ctl);
       });
       kin = kout;
       vin = vout;
@@ -240,10 +247,10 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bo
   }
   timed(KT_SCAN, [&] {
     launch_scan(stream, skeys, svals, recs, n, full ? 0 : lo_bit, full ? 0 : 1, srec, lb_sum, lb_head,
-                &ctl->tile_ctr[31], ctl);
+                &ctl->tile_ctr[31][0], tile_heads, ctl);
   });
   timed(KT_LEADER, [&] {
-    launch_leader(stream, skeys, srec, recs, d_rules, n, tab, cfg.local_cache ? 1 : 0, seg, ctl);
+    launch_leader(stream, skeys, srec, recs, d_rules, n, tab, cfg.local_cache ? 1 : 0, seg, tile_heads, ctl);
   });
   timed(KT_DECIDE, [&] { launch_decide(stream, srec, seg, d_rules, n, out, thr, ctl); });
   e = hipGetLastError();
@@ -376,7 +383,12 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   chk(hipMalloc(&e->recs, N * sizeof(ItemRec)));
   chk(hipMalloc(&e->srec, N * sizeof(SortedRec)));
   chk(hipMalloc(&e->seg, N * sizeof(SegInfo)));
-  chk(hipMalloc(&e->offs, (size_t)MAX_PASSES * RADIX * 4));
+  chk(hipMalloc(&e->offs, (size_t)MAX_PASSES * hist_sub_words() * 4));
+  chk(hipMalloc(&e->hist_part, (size_t)hist_blocks((uint32_t)N) * MAX_PASSES * RADIX * 4));
+  chk(hipMalloc(&e->fp_part2, (size_t)hist_blocks((uint32_t)N) * FP_PART_WORDS * 4 + 64));
+  chk(hipMalloc(&e->fp_part, ((N + 255) / 256) * FP_PART_WORDS * 4 + 64));
+  chk(hipMalloc(&e->tile_heads, (size_t)scan_tiles((uint32_t)N) * 4 + 64));
+
   e->zero_cap = e->zlayout((uint32_t)N, MAX_PASSES).total;
   chk(hipMalloc(&e->zero_block, e->zero_cap));
   chk(hipHostMalloc(&e->h_ctl, sizeof(EngineCtl), hipHostMallocDefault));
@@ -411,6 +423,11 @@ void rl_destroy(rl_engine* e) {
   hipFree(e->srec);
   hipFree(e->seg);
   hipFree(e->offs);
+  hipFree(e->hist_part);
+  hipFree(e->fp_part);
+  hipFree(e->fp_part2);
+  hipFree(e->tile_heads);
+
   hipFree(e->zero_block);
   hipHostFree(e->h_ctl);
   if (e->stream) hipStreamDestroy(e->stream);

@@ -45,6 +45,14 @@ RL_DEV uint64_t lanemask_lt() {
 
 constexpr uint32_t SPIN_LIMIT = 1u << 24;
 
+#ifdef RL_STAMPS
+// Diagnostic build only: per-block phase timestamps of the last sort pass (s_memtime).
+__device__ uint64_t g_stamps[4096][8];
+#define STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define STAMP(k) do { } while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // k_fingerprint
 // ---------------------------------------------------------------------------
@@ -87,18 +95,33 @@ RL_DEV int64_t div_const(int64_t now, uint32_t unit) {
   }
 }
 
+RL_DEV uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t o = __shfl_xor(v, d, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+RL_DEV uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t o = __shfl_xor(v, d, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
 __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
                                                      uint64_t seed, uint64_t* __restrict__ keys_orig,
                                                      ItemRec* __restrict__ recs, rl_status* __restrict__ out,
-                                                     uint32_t* __restrict__ hist, int lo_bit, int npasses,
+                                                     uint32_t* __restrict__ req_thr, uint32_t* __restrict__ fpart,
                                                      EngineCtl* ctl) {
-  __shared__ uint32_t sh_hist[8][RADIX];
   __shared__ uint32_t sh_nil;
   __shared__ uint32_t sh_err;
-  __shared__ uint32_t sh_gmin[8], sh_gmax[8];
+  __shared__ uint32_t sh_gmin[8], sh_gmax[8];  // gmin holds ~min (zero-init max)
   const uint32_t tid = threadIdx.x;
-  for (int i = tid; i < 8 * RADIX; i += 256) (&sh_hist[0][0])[i] = 0;
-  if (tid < 8) { sh_gmin[tid] = 0; sh_gmax[tid] = 0; }  // gmin holds ~min (zero-init max)
+  if (tid < 8) { sh_gmin[tid] = 0; sh_gmax[tid] = 0; }
   if (tid == 0) { sh_nil = 0; sh_err = 0; }
   __syncthreads();
 
@@ -106,12 +129,22 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
   uint32_t err = 0;
   bool nil = true;
   uint64_t key = NIL_KEY;
+  uint32_t region = 8, gen = 0;
   if (i < in.n_desc) {
     const uint32_t r = in.rule[i];
     const uint32_t q = in.req_of[i];
     const bool q_ok = q < in.n_req;
     const int64_t now = q_ok ? in.now[q] : 0;
     const uint32_t ha = q_ok ? in.hits[q] : 1u;
+    // Zero DoLimitResponse.ThrottleMillis of the requests this descriptor opens
+    // (k_decide max-reduces into it); the last descriptor also zeroes trailing requests.
+    if (q_ok) {
+      const uint32_t pq = i == 0 ? 0u : in.req_of[i - 1];
+      const uint32_t first = i == 0 ? 0u : (pq < q ? pq + 1u : q + 1u);
+      for (uint32_t rr = first; rr <= q; ++rr) req_thr[rr] = 0;
+      if (i + 1 == in.n_desc)
+        for (uint32_t rr = q + 1; rr < in.n_req; ++rr) req_thr[rr] = 0;
+    }
     ItemRec rec;
     rec.rule = r;
     rec.req = q;
@@ -120,8 +153,8 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
     rec.now_mod = 0;
     rec.gen = 0;
     rec.pad = 0;
-    if (r != RL_NIL_RULE && (r >= n_rules || q >= in.n_req)) err |= ERR_BAD_INPUT;
-    if (r != RL_NIL_RULE && r < n_rules && q < in.n_req) {
+    if (r != RL_NIL_RULE && (r >= n_rules || !q_ok)) err |= ERR_BAD_INPUT;
+    if (r != RL_NIL_RULE && r < n_rules && q_ok) {
       if (now < 0 || now > 0xFFFFFFF0ll) {
         err |= ERR_BAD_TIME;
       } else {
@@ -133,13 +166,12 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
         hash_prefix(in.blob, o0, o1 - o0, s);
         uint64_t hi, lo;
         fp_final(s, (uint64_t)ws, hi, lo);
-        const uint32_t region = (R.unit - 1u) * 2u + (uint32_t)(widx & 1);
+        region = (R.unit - 1u) * 2u + (uint32_t)(widx & 1);
         key = make_sort_key(region, hi);
         rec.fp_lo = lo;
         rec.now_mod = (int32_t)(now - ws);
         rec.gen = (uint32_t)widx + 1u;
-        atomicMax(&sh_gmin[region], ~rec.gen);
-        atomicMax(&sh_gmax[region], rec.gen);
+        gen = rec.gen;
         nil = false;
       }
     }
@@ -154,59 +186,131 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
       st.over_limit_delta = 0;
       st.near_limit_delta = 0;
       out[i] = st;
-      atomicAdd(&sh_nil, 1u);
     }
-    for (int p = 0; p < npasses; ++p) atomicAdd(&sh_hist[p][(key >> (lo_bit + 8 * p)) & 0xFF], 1u);
+  }
+  // Per-wave reductions, then one LDS op per wave.
+  const uint64_t nilmask = __ballot(i < in.n_desc && nil);
+  const uint32_t lane = __lane_id();
+  if (lane == 0 && nilmask) atomicAdd(&sh_nil, (uint32_t)__popcll(nilmask));
+  for (uint32_t rg = 0; rg < 8; ++rg) {
+    const bool mine = region == rg;
+    if (!__ballot(mine)) continue;
+    const uint32_t mn = wave_min_u32(mine ? gen : 0xFFFFFFFFu);
+    const uint32_t mx = wave_max_u32(mine ? gen : 0u);
+    if (lane == 0) {
+      atomicMax(&sh_gmin[rg], ~mn);
+      atomicMax(&sh_gmax[rg], mx);
+    }
   }
   if (err) atomicOr(&sh_err, err);
   __syncthreads();
-  for (int p = 0; p < npasses; ++p) {
-    const uint32_t c = sh_hist[p][tid];
-    if (c) atomicAdd(&hist[p * RADIX + tid], c);
-  }
-  if (tid < 8 && sh_gmax[tid]) {
-    atomicMax(&ctl->gen_min[tid], sh_gmin[tid]);
-    atomicMax(&ctl->gen_max[tid], sh_gmax[tid]);
-  }
-  if (tid == 0) {
-    if (sh_nil) atomicAdd(&ctl->n_nil, sh_nil);
-    if (sh_err) atomicOr(&ctl->err, sh_err);
-  }
+  // Block partials (plain stores); k_hist_scan's last block reduces them.
+  uint32_t* fp = fpart + (size_t)blockIdx.x * FP_PART_WORDS;
+  if (tid < 8) fp[tid] = sh_gmin[tid];
+  else if (tid < 16) fp[tid] = sh_gmax[tid - 8];
+  else if (tid == 16) fp[16] = sh_nil;
+  if (tid == 0 && sh_err) atomicOr(&ctl->err, sh_err);
 }
 
-// Histogram of npasses 8-bit digits of a key array (full-fingerprint fallback sort).
-__global__ __launch_bounds__(256) void k_histogram(const uint64_t* __restrict__ keys, uint32_t n, int lo_bit,
-                                                   int npasses, uint32_t* __restrict__ hist) {
+// Per-block partial histograms of npasses 8-bit digits (plain stores, no global atomics):
+// part[block][p][256]; block b covers keys [b*HIST_CHUNK, (b+1)*HIST_CHUNK). The same
+// block also folds the fingerprint partials of its items (generation range, nil count).
+constexpr int HIST_CHUNK = 4096;
+constexpr int HIST_SUB = 16;  // histogram partials are pre-reduced into HIST_SUB slices per pass
+__global__ __launch_bounds__(1024) void k_histogram(const uint64_t* __restrict__ keys, uint32_t n, int lo_bit,
+                                                     int npasses, uint32_t* __restrict__ part,
+                                                     const uint32_t* __restrict__ fpart, uint32_t* __restrict__ fpart2) {
   __shared__ uint32_t sh_hist[8][RADIX];
   const uint32_t tid = threadIdx.x;
-  for (int i = tid; i < 8 * RADIX; i += 256) (&sh_hist[0][0])[i] = 0;
+  for (int i = tid; i < 8 * RADIX; i += 1024) (&sh_hist[0][0])[i] = 0;
   __syncthreads();
-  for (uint32_t i = blockIdx.x * 256 + tid; i < n; i += gridDim.x * 256) {
+  const uint32_t b0 = blockIdx.x * HIST_CHUNK, b1 = min(n, b0 + HIST_CHUNK);
+  for (uint32_t i = b0 + tid; i < b1; i += 1024) {
     const uint64_t key = keys[i];
     for (int p = 0; p < npasses; ++p) atomicAdd(&sh_hist[p][(key >> (lo_bit + 8 * p)) & 0xFF], 1u);
   }
-  __syncthreads();
-  for (int p = 0; p < npasses; ++p) {
-    const uint32_t c = sh_hist[p][tid];
-    if (c) atomicAdd(&hist[p * RADIX + tid], c);
+  if (fpart && tid < FP_PART_WORDS) {
+    // fingerprint blocks are 256 items: this chunk covers HIST_CHUNK / 256 of them
+    const uint32_t f0 = b0 / 256, f1 = (b1 + 255) / 256;
+    uint32_t v = 0;
+    for (uint32_t f = f0; f < f1; ++f) {
+      const uint32_t x = fpart[(size_t)f * FP_PART_WORDS + tid];
+      v = tid < 16 ? (x > v ? x : v) : v + x;
+    }
+    fpart2[(size_t)blockIdx.x * FP_PART_WORDS + tid] = v;
   }
+  __syncthreads();
+  for (int i = tid; i < npasses * RADIX; i += 1024)
+    part[(size_t)blockIdx.x * MAX_PASSES * RADIX + i] = (&sh_hist[0][0])[i];
 }
 
-// Exclusive scan of each pass's 256-bin histogram (one block per pass).
-__global__ __launch_bounds__(256) void k_hist_scan(const uint32_t* __restrict__ hist, uint32_t* __restrict__ offs) {
-  __shared__ uint32_t sh[RADIX];
+// Block (p, q), q < HIST_SUB: sum slice q of pass p's partial histograms -> sub[p][q][256].
+// Last block (if fp_blocks): reduce the folded fingerprint partials into ctl (the only
+// writer of gen_min / gen_max / n_nil).
+__global__ __launch_bounds__(256) void k_hist_scan(const uint32_t* __restrict__ part, uint32_t nblocks,
+                                                   uint32_t* __restrict__ sub, int npasses,
+                                                   const uint32_t* __restrict__ fpart2, uint32_t fp_blocks,
+                                                   EngineCtl* ctl) {
   const uint32_t tid = threadIdx.x;
-  const uint32_t p = blockIdx.x;
-  const uint32_t v = hist[p * RADIX + tid];
-  sh[tid] = v;
+  if ((int)blockIdx.x == npasses * HIST_SUB) {
+    __shared__ uint32_t shm[FP_PART_WORDS][256];
+    for (int w = 0; w < FP_PART_WORDS; ++w) {
+      uint32_t v = 0;
+      for (uint32_t g = tid; g < fp_blocks; g += 256) {
+        const uint32_t x = fpart2[(size_t)g * FP_PART_WORDS + w];
+        v = w < 16 ? (x > v ? x : v) : v + x;
+      }
+      shm[w][tid] = v;
+    }
+    __syncthreads();
+    for (int d = 128; d > 0; d >>= 1) {
+      if (tid < (uint32_t)d)
+        for (int w = 0; w < FP_PART_WORDS; ++w) {
+          const uint32_t a = shm[w][tid], c = shm[w][tid + d];
+          shm[w][tid] = w < 16 ? (a > c ? a : c) : a + c;
+        }
+      __syncthreads();
+    }
+    if (tid < 8) ctl->gen_min[tid] = ~shm[tid][0];  // partials hold ~min
+    else if (tid < 16) ctl->gen_max[tid - 8] = shm[tid][0];
+    else if (tid == 16) ctl->n_nil = shm[16][0];
+    return;
+  }
+  const uint32_t p = blockIdx.x / HIST_SUB, q = blockIdx.x % HIST_SUB;
+  const uint32_t per = (nblocks + HIST_SUB - 1) / HIST_SUB;
+  const uint32_t g0 = q * per, g1 = min(nblocks, g0 + per);
+  const size_t stride = (size_t)MAX_PASSES * RADIX;
+  const uint32_t* b = part + p * RADIX + tid;
+  uint32_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+  uint32_t g = g0;
+  for (; g + 4 <= g1; g += 4) {
+    v0 += b[(g + 0) * stride];
+    v1 += b[(g + 1) * stride];
+    v2 += b[(g + 2) * stride];
+    v3 += b[(g + 3) * stride];
+  }
+  for (; g < g1; ++g) v0 += b[g * stride];
+  sub[((size_t)p * HIST_SUB + q) * RADIX + tid] = v0 + v1 + v2 + v3;
+}
+
+// Exclusive digit offsets of one pass from its HIST_SUB pre-reduced slices (block-wide scan);
+// every sort block recomputes this (16 loads per thread) instead of a separate launch.
+RL_DEV uint32_t bin_offset_from_sub(const uint32_t* __restrict__ sub_p, uint32_t* sh_scan) {
+  const uint32_t tid = threadIdx.x;
+  uint32_t v = 0;
+#pragma unroll
+  for (int q = 0; q < HIST_SUB; ++q) v += sub_p[q * RADIX + tid];
+  sh_scan[tid] = v;
   __syncthreads();
   for (int d = 1; d < RADIX; d <<= 1) {
-    const uint32_t t = tid >= (uint32_t)d ? sh[tid - d] : 0u;
+    const uint32_t t = tid >= (uint32_t)d ? sh_scan[tid - d] : 0u;
     __syncthreads();
-    sh[tid] += t;
+    sh_scan[tid] += t;
     __syncthreads();
   }
-  offs[p * RADIX + tid] = sh[tid] - v;
+  const uint32_t r = sh_scan[tid] - v;
+  __syncthreads();
+  return r;
 }
 
 // Gather helpers for the full-fingerprint fallback sort.
@@ -231,8 +335,15 @@ __global__ void k_gather_keys(const uint64_t* __restrict__ keys_orig, const uint
 // ever waits on tiles already running), stage the tile in LDS in digit order and
 // write each digit run contiguously.
 // ---------------------------------------------------------------------------
-constexpr int SORT_IPT = 16;                // keys per thread
-constexpr int SORT_TILE = 256 * SORT_IPT;   // 4096
+#ifndef RL_SORT_IPT
+#define RL_SORT_IPT 16
+#endif
+#ifndef RL_SORT_LB_WIN
+#define RL_SORT_LB_WIN 8
+#endif
+constexpr int SORT_IPT = RL_SORT_IPT;  // keys per thread
+constexpr int SORT_TILE = 256 * SORT_IPT;
+constexpr int SORT_LB_WIN = RL_SORT_LB_WIN;
 constexpr uint32_t LB_AGG = 1u << 30;
 constexpr uint32_t LB_INC = 2u << 30;
 constexpr uint32_t LB_MASK = (1u << 30) - 1;
@@ -240,7 +351,7 @@ constexpr uint32_t LB_MASK = (1u << 30) - 1;
 __global__ __launch_bounds__(256) void k_sort_pass(const uint64_t* __restrict__ keys_in,
                                                    const uint32_t* __restrict__ vals_in,
                                                    uint64_t* __restrict__ keys_out, uint32_t* __restrict__ vals_out,
-                                                   uint32_t n, int shift, const uint32_t* __restrict__ bin_off,
+                                                   uint32_t n, int shift, const uint32_t* __restrict__ sub_p,
                                                    uint32_t* __restrict__ lookback, uint32_t* tile_ctr,
                                                    EngineCtl* ctl) {
   __shared__ uint64_t s_keys[SORT_TILE];
@@ -250,10 +361,17 @@ __global__ __launch_bounds__(256) void k_sort_pass(const uint64_t* __restrict__ 
   __shared__ uint32_t s_gbase[RADIX];     // global output base per digit for this tile
   __shared__ uint32_t s_tile;
 
+  STAMP(0);
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = tid >> 6;
   const uint32_t lane = tid & 63;
+#ifdef RL_SORT_TICKET
   if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+#else
+  // Tile = blockIdx: blocks start in launch order on gfx950 (MI355X_MICROARCH.md, dispatch),
+  // so a tile waits only on earlier, already-running tiles; every spin is bounded (ERR_SPIN).
+  if (tid == 0) s_tile = blockIdx.x;
+#endif
   for (int i = tid; i < 4 * RADIX; i += 256) (&s_wcnt[0][0])[i] = 0;
   __syncthreads();
   const uint32_t tile = s_tile;
@@ -273,6 +391,8 @@ __global__ __launch_bounds__(256) void k_sort_pass(const uint64_t* __restrict__ 
       val[k] = 0;
     }
   }
+  __syncthreads();
+  STAMP(1);
   // Per-wave stable ranking, round by round in position order.
   const uint64_t lt = lanemask_lt();
 #pragma unroll
@@ -299,6 +419,7 @@ __global__ __launch_bounds__(256) void k_sort_pass(const uint64_t* __restrict__ 
     rank[k] = r;
   }
   __syncthreads();
+  STAMP(2);
   // Thread tid owns digit tid: tile count, per-wave exclusive offsets.
   uint32_t cnt = 0;
   {
@@ -316,25 +437,40 @@ __global__ __launch_bounds__(256) void k_sort_pass(const uint64_t* __restrict__ 
   } else {
     st_relaxed(&lb[tid], LB_AGG | cnt);
   }
+  STAMP(3);
+  // Windowed look-back: SORT_LB_WIN predecessor words of this digit in flight per round trip.
   uint32_t excl = 0;
   if (tile > 0) {
     int32_t j = (int32_t)tile - 1;
     uint32_t spins = 0;
-    while (j >= 0) {
-      const uint32_t v = ld_relaxed(&lookback[(size_t)j * RADIX + tid]);
-      const uint32_t f = v & ~LB_MASK;
-      if (f == 0) {
+    for (;;) {
+      uint32_t v[SORT_LB_WIN];
+#pragma unroll
+      for (int w = 0; w < SORT_LB_WIN; ++w)
+        v[w] = (j - w >= 0) ? ld_relaxed(&lookback[(size_t)(j - w) * RADIX + tid]) : LB_INC;
+      int w = 0;
+      bool done = false;
+#pragma unroll
+      for (int k = 0; k < SORT_LB_WIN; ++k) {
+        if (done || w != k) continue;
+        const uint32_t f = v[k] & ~LB_MASK;
+        if (f == 0) continue;  // not published yet: stop here, re-poll from this tile
+        excl += v[k] & LB_MASK;
+        if (f == LB_INC) done = true;
+        w = k + 1;
+      }
+      if (done) break;
+      j -= w;
+      if (w < SORT_LB_WIN) {
         if (++spins > SPIN_LIMIT) { atomicOr(&ctl->err, ERR_SPIN); break; }
         __builtin_amdgcn_s_sleep(1);
-        continue;
       }
-      excl += v & LB_MASK;
-      if (f == LB_INC) break;
-      --j;
     }
     st_relaxed(&lb[tid], LB_INC | (excl + cnt));
   }
-  s_gbase[tid] = bin_off[tid] + excl;
+  __syncthreads();
+  STAMP(4);
+  s_gbase[tid] = bin_offset_from_sub(sub_p, s_tstart) + excl;
   // Tile-local exclusive scan of digit counts (block scan over 256 threads).
   s_tstart[tid] = cnt;
   __syncthreads();
@@ -346,6 +482,7 @@ __global__ __launch_bounds__(256) void k_sort_pass(const uint64_t* __restrict__ 
   }
   s_tstart[tid] -= cnt;
   __syncthreads();
+  STAMP(5);
   // Stage the tile in digit order.
 #pragma unroll
   for (int k = 0; k < SORT_IPT; ++k) {
@@ -358,6 +495,7 @@ __global__ __launch_bounds__(256) void k_sort_pass(const uint64_t* __restrict__ 
     }
   }
   __syncthreads();
+  STAMP(6);
   const uint32_t tvalid = n - tbase < (uint32_t)SORT_TILE ? n - tbase : (uint32_t)SORT_TILE;
   for (uint32_t i = tid; i < tvalid; i += 256) {
     const uint64_t k = s_keys[i];
@@ -366,6 +504,8 @@ __global__ __launch_bounds__(256) void k_sort_pass(const uint64_t* __restrict__ 
     keys_out[o] = k;
     vals_out[o] = s_vals[i];
   }
+  __syncthreads();
+  STAMP(7);
 }
 
 // ---------------------------------------------------------------------------
@@ -375,8 +515,12 @@ __global__ __launch_bounds__(256) void k_sort_pass(const uint64_t* __restrict__ 
 // (A.f, A.s+B.s, A.hp, A.o|B.o) — associative. Tiles chain through decoupled look-back
 // on two self-flagged 64-bit granules per tile (sum|o and head position).
 // ---------------------------------------------------------------------------
-constexpr int SCAN_IPT = 8;
-constexpr int SCAN_TILE = 256 * SCAN_IPT;  // 2048
+#ifndef RL_SCAN_IPT
+#define RL_SCAN_IPT 8
+#endif
+constexpr int SCAN_IPT = RL_SCAN_IPT;
+constexpr int SCAN_TILE = 256 * SCAN_IPT;
+constexpr int LB_WIN = 8;
 constexpr uint64_t LB64_AGG = 1ull << 62;
 constexpr uint64_t LB64_INC = 2ull << 62;
 constexpr uint64_t LB64_FLAGS = 3ull << 62;
@@ -411,7 +555,8 @@ __global__ __launch_bounds__(256) void k_scan(const uint64_t* __restrict__ skeys
                                               const ItemRec* __restrict__ recs, uint32_t n_all, int lo_bit,
                                               int check_mixed, SortedRec* __restrict__ srec,
                                               uint64_t* __restrict__ lb_sum, uint64_t* __restrict__ lb_head,
-                                              uint32_t* tile_ctr, EngineCtl* ctl) {
+                                              uint32_t* tile_ctr, uint32_t* __restrict__ tile_heads,
+                                              EngineCtl* ctl) {
   __shared__ ScanEl s_wagg[4];
   __shared__ uint64_t s_lastkey[256];
   __shared__ uint64_t s_lastlo[256];
@@ -430,7 +575,7 @@ __global__ __launch_bounds__(256) void k_scan(const uint64_t* __restrict__ skeys
     s_mixed = 0;
   }
   __syncthreads();
-  const uint32_t n = n_all - ld_relaxed(&ctl->n_nil);
+  const uint32_t n = n_all - ctl->n_nil;  // written by k_fingerprint (earlier launch)
   const uint32_t tile = s_tile;
   const uint32_t base = tile * SCAN_TILE + tid * SCAN_IPT;
 
@@ -520,59 +665,69 @@ __global__ __launch_bounds__(256) void k_scan(const uint64_t* __restrict__ skeys
     if (w == wave) woff = tagg;
     tagg = scan_op(tagg, s_wagg[w]);
   }
-  // Decoupled look-back (thread 0).
-  if (tid == 0) {
-    ScanEl carry{0, 0, 0, 0};
-    if (tagg.f || tile == 0) {
-      // carry-out independent of predecessors for the part after the first head
-      if (tile == 0) {
+  // Decoupled look-back by wave 0: 64 predecessor tiles per round trip.
+  if (wave == 0) {
+    if (lane == 0) {
+      if (tagg.f || tile == 0) {
+        // carry-out independent of predecessors (the part after this tile's last head)
         st_relaxed64(&lb_head[tile], LB64_INC | tagg.hp);
         st_relaxed64(&lb_sum[tile], LB64_INC | (tagg.o ? LB64_O : 0) | (tagg.s & LB64_SUM));
       } else {
-        st_relaxed64(&lb_head[tile], LB64_INC | tagg.hp);
-        st_relaxed64(&lb_sum[tile], LB64_INC | (tagg.o ? LB64_O : 0) | (tagg.s & LB64_SUM));
+        st_relaxed64(&lb_sum[tile], LB64_AGG | (tagg.o ? LB64_O : 0) | (tagg.s & LB64_SUM));
       }
-    } else {
-      st_relaxed64(&lb_sum[tile], LB64_AGG | (tagg.o ? LB64_O : 0) | (tagg.s & LB64_SUM));
     }
+    ScanEl carry{0, 0, 0, 0};
     if (tile > 0) {
-      ScanEl acc{0, 0, 0, 0};
-      int32_t j = (int32_t)tile - 1;
+      int32_t top = (int32_t)tile - 1;
+      uint64_t acc_s = 0;
+      uint32_t acc_o = 0;
       uint32_t spins = 0;
-      while (j >= 0) {
-        const uint64_t v = ld_relaxed64(&lb_sum[j]);
-        const uint64_t f = v & LB64_FLAGS;
-        if (f == 0) {
-          if (++spins > SPIN_LIMIT) { atomicOr(&ctl->err, ERR_SPIN); break; }
+      for (;;) {
+        const int32_t t = top - (int32_t)lane;
+        const uint64_t v = t >= 0 ? ld_relaxed64(&lb_sum[t]) : LB64_INC;
+        const uint64_t hv = t >= 0 ? ld_relaxed64(&lb_head[t]) : LB64_INC;
+        const uint64_t fs = v & LB64_FLAGS;
+        const bool is_inc = fs == LB64_INC && (hv & LB64_FLAGS) != 0;
+        const bool not_ready = fs == 0 || (fs == LB64_INC && (hv & LB64_FLAGS) == 0);
+        const uint64_t incm = __ballot(is_inc);
+        const uint64_t zm = __ballot(not_ready);
+        const uint32_t fi = incm ? (uint32_t)__ffsll((unsigned long long)incm) - 1u : 64u;
+        const uint32_t fz = zm ? (uint32_t)__ffsll((unsigned long long)zm) - 1u : 64u;
+        const uint32_t take = fi < fz ? fi + 1u : fz;  // lanes [0, take) contribute
+        uint64_t cs = lane < take ? (v & LB64_SUM) : 0ull;
+        uint32_t co = (lane < take && (v & LB64_O)) ? 1u : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+          cs += __shfl_xor(cs, d, 64);
+          co |= __shfl_xor(co, d, 64);
+        }
+        acc_s += cs;
+        acc_o |= co;
+        if (fi < fz) {
+          const uint32_t hp = (uint32_t)__shfl((uint32_t)(hv & 0xFFFFFFFFull), (int)fi, 64);
+          carry = ScanEl{1, acc_o, hp, acc_s};
+          break;
+        }
+        top -= (int32_t)fz;
+        if (fz < 64u) {
+          if (++spins > SPIN_LIMIT) {
+            if (lane == 0) atomicOr(&ctl->err, ERR_SPIN);
+            break;
+          }
           __builtin_amdgcn_s_sleep(1);
-          continue;
         }
-        if (f == LB64_AGG) {
-          ScanEl a{0, (uint32_t)((v & LB64_O) != 0), 0, v & LB64_SUM};
-          acc = scan_op(a, acc);
-          --j;
-          continue;
-        }
-        // inclusive: fetch its head position too
-        uint64_t hv;
-        while (((hv = ld_relaxed64(&lb_head[j])) & LB64_FLAGS) == 0) {
-          if (++spins > SPIN_LIMIT) { atomicOr(&ctl->err, ERR_SPIN); break; }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        ScanEl a{1, (uint32_t)((v & LB64_O) != 0), (uint32_t)(hv & 0xFFFFFFFFull), v & LB64_SUM};
-        acc = scan_op(a, acc);
-        break;
       }
-      carry = acc;
-      if (!tagg.f) {
+      if (lane == 0 && !tagg.f) {
         const ScanEl out = scan_op(carry, tagg);
         st_relaxed64(&lb_head[tile], LB64_INC | out.hp);
         st_relaxed64(&lb_sum[tile], LB64_INC | (out.o ? LB64_O : 0) | (out.s & LB64_SUM));
       }
     }
-    s_carry = carry;
-    if (s_heads) atomicAdd(&ctl->n_segments, s_heads);
-    if (s_mixed) atomicOr(&ctl->err, ERR_NEED_RESORT);
+    if (lane == 0) {
+      s_carry = carry;
+      tile_heads[tile] = s_heads;
+      if (s_mixed) atomicOr(&ctl->err, ERR_NEED_RESORT);
+    }
   }
   __syncthreads();
   ScanEl run = scan_op(scan_op(s_carry, woff), wexcl);
@@ -602,10 +757,24 @@ constexpr uint32_t MAX_PROBE = 4096;
 __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ skeys, const SortedRec* __restrict__ srec,
                                                 const ItemRec* __restrict__ recs, const DevRule* __restrict__ rules,
                                                 uint32_t n_all, TableDesc tab, int local_cache,
-                                                SegInfo* __restrict__ seg, EngineCtl* ctl) {
-  const uint32_t errs = ld_relaxed(&ctl->err);
+                                                SegInfo* __restrict__ seg, const uint32_t* __restrict__ tile_heads,
+                                                uint32_t n_scan_tiles, EngineCtl* ctl) {
+  if (blockIdx.x == 0) {
+    // U = number of segment heads (k_scan per-tile counts); single writer of n_segments.
+    __shared__ uint32_t sh_u[256];
+    uint32_t u = 0;
+    for (uint32_t t = threadIdx.x; t < n_scan_tiles; t += 256) u += tile_heads[t];
+    sh_u[threadIdx.x] = u;
+    __syncthreads();
+    for (int d = 128; d > 0; d >>= 1) {
+      if (threadIdx.x < (uint32_t)d) sh_u[threadIdx.x] += sh_u[threadIdx.x + d];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) ctl->n_segments = sh_u[0];
+  }
+  const uint32_t errs = ctl->err;  // flags of earlier launches
   if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_BAD_INPUT | ERR_WINDOW_SPAN)) return;
-  const uint32_t n = n_all - ld_relaxed(&ctl->n_nil);
+  const uint32_t n = n_all - ctl->n_nil;  // written by k_fingerprint (earlier launch)
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
   if (j + 1 < n && (srec[j + 1].head & ~HEAD_MIXED_RULE) != j + 1) return;  // not a tail
@@ -617,7 +786,7 @@ __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ ske
   const uint32_t region = key_region(key);
   // Two window generations of one region in one batch must be adjacent (a batch may
   // straddle one window boundary); otherwise the older would read as empty.
-  if (ld_relaxed(&ctl->gen_max[region]) - ~ld_relaxed(&ctl->gen_min[region]) > 1u) {
+  if (ctl->gen_max[region] - ctl->gen_min[region] > 1u) {
     atomicOr(&ctl->err, ERR_WINDOW_SPAN);
     return;
   }
@@ -632,9 +801,14 @@ __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ ske
   bool existed = false;
   for (uint32_t probe = 0; probe < MAX_PROBE;) {
     Slot* s = rbase + (pos & mask);
+    // ctrl by an L1-bypassing atomic load (it may be CASed concurrently); the identity
+    // words in the same load burst (written by earlier batches, or by a concurrent
+    // claimer of a different key, which can never match).
     const uint64_t c = ld_relaxed64(&s->ctrl);
+    const uint64_t skey = s->key;
+    const uint32_t slohi = s->fp_lo_hi;
     const uint32_t g = (uint32_t)c;
-    if (g == G && (uint32_t)(c >> 32) == tag && s->key == key && s->fp_lo_hi == lohi) {
+    if (g == G && (uint32_t)(c >> 32) == tag && skey == key && slohi == lohi) {
       slot = s;
       existed = true;
       break;
@@ -664,8 +838,8 @@ __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ ske
   } else {
     slot->key = key;
     slot->fp_lo_hi = lohi;
-    atomicAdd(&ctl->n_inserted, 1u);
   }
+
   uint32_t freeze = SEG_NO_FREEZE;
   uint64_t final_count = base + tail.P;
   if (frozen_pre) {
@@ -721,9 +895,9 @@ __global__ __launch_bounds__(256) void k_decide(const SortedRec* __restrict__ sr
                                                 const DevRule* __restrict__ rules, uint32_t n_all,
                                                 rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
                                                 EngineCtl* ctl) {
-  const uint32_t errs = ld_relaxed(&ctl->err);
+  const uint32_t errs = ctl->err;  // flags of earlier launches
   if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_TABLE_FULL | ERR_BAD_INPUT | ERR_WINDOW_SPAN)) return;
-  const uint32_t n = n_all - ld_relaxed(&ctl->n_nil);
+  const uint32_t n = n_all - ctl->n_nil;  // written by k_fingerprint (earlier launch)
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
   const SortedRec r = srec[j];
@@ -773,8 +947,8 @@ __global__ __launch_bounds__(256) void k_decide(const SortedRec* __restrict__ sr
 // Host-side launchers (called from rl_engine.cpp).
 // ---------------------------------------------------------------------------
 void launch_fingerprint(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
-                        uint64_t* keys_orig, ItemRec* recs, rl_status* out,
-                        uint32_t* hist, int lo_bit, int npasses, EngineCtl* ctl) {
+                        uint64_t* keys_orig, ItemRec* recs, rl_status* out, uint32_t* req_thr, uint32_t* fpart,
+                        EngineCtl* ctl) {
   DevBatch d;
   d.n_desc = b.n_desc;
   d.n_req = b.n_req;
@@ -788,17 +962,21 @@ void launch_fingerprint(hipStream_t st, const rl_batch& b, const DevRule* rules,
   d.hits = b.hits_addend;
   const uint32_t grid = (b.n_desc + 255) / 256;
   hipLaunchKernelGGL(k_fingerprint, dim3(grid), dim3(256), 0, st, d, rules, n_rules, seed, keys_orig, recs, out,
-                     hist, lo_bit, npasses, ctl);
+                     req_thr, fpart, ctl);
 }
-void launch_histogram(hipStream_t st, const uint64_t* keys, uint32_t n, int lo_bit, int npasses, uint32_t* hist) {
-  uint32_t grid = (n + 255) / 256;
-  if (grid > 2048) grid = 2048;
-  if (grid == 0) grid = 1;
-  hipLaunchKernelGGL(k_histogram, dim3(grid), dim3(256), 0, st, keys, n, lo_bit, npasses, hist);
+uint32_t hist_blocks(uint32_t n) { return n ? (n + HIST_CHUNK - 1) / HIST_CHUNK : 1; }
+void launch_histogram(hipStream_t st, const uint64_t* keys, uint32_t n, int lo_bit, int npasses, uint32_t* part,
+                      const uint32_t* fpart, uint32_t* fpart2) {
+  hipLaunchKernelGGL(k_histogram, dim3(hist_blocks(n)), dim3(1024), 0, st, keys, n, lo_bit, npasses, part, fpart,
+                     fpart2);
 }
-void launch_hist_scan(hipStream_t st, const uint32_t* hist, uint32_t* offs, int npasses) {
-  hipLaunchKernelGGL(k_hist_scan, dim3(npasses), dim3(256), 0, st, hist, offs);
+void launch_hist_scan(hipStream_t st, const uint32_t* part, uint32_t n, uint32_t* sub, int npasses,
+                      const uint32_t* fpart2, EngineCtl* ctl) {
+  const uint32_t fpb = fpart2 ? hist_blocks(n) : 0;
+  hipLaunchKernelGGL(k_hist_scan, dim3(npasses * HIST_SUB + (fpb ? 1 : 0)), dim3(256), 0, st, part, hist_blocks(n),
+                     sub, npasses, fpart2, fpb, ctl);
 }
+uint32_t hist_sub_words() { return HIST_SUB * RADIX; }
 void launch_fallback_lo_keys(hipStream_t st, const ItemRec* recs, const uint64_t* keys_orig, uint32_t n,
                              uint64_t* k_out, uint32_t* v_out) {
   hipLaunchKernelGGL(k_fallback_lo_keys, dim3((n + 255) / 256), dim3(256), 0, st, recs, keys_orig, n, k_out, v_out);
@@ -816,15 +994,15 @@ void launch_sort_pass(hipStream_t st, const uint64_t* kin, const uint32_t* vin, 
 }
 void launch_scan(hipStream_t st, const uint64_t* skeys, const uint32_t* svals, const ItemRec* recs, uint32_t n,
                  int lo_bit, int check_mixed, SortedRec* srec, uint64_t* lb_sum, uint64_t* lb_head,
-                 uint32_t* tile_ctr, EngineCtl* ctl) {
+                 uint32_t* tile_ctr, uint32_t* tile_heads, EngineCtl* ctl) {
   hipLaunchKernelGGL(k_scan, dim3(scan_tiles(n)), dim3(256), 0, st, skeys, svals, recs, n, lo_bit, check_mixed, srec,
-                     lb_sum, lb_head, tile_ctr, ctl);
+                     lb_sum, lb_head, tile_ctr, tile_heads, ctl);
 }
 void launch_leader(hipStream_t st, const uint64_t* skeys, const SortedRec* srec, const ItemRec* recs,
                    const DevRule* rules, uint32_t n, const TableDesc& tab, int local_cache, SegInfo* seg,
-                   EngineCtl* ctl) {
+                   const uint32_t* tile_heads, EngineCtl* ctl) {
   hipLaunchKernelGGL(k_leader, dim3((n + 255) / 256), dim3(256), 0, st, skeys, srec, recs, rules, n, tab,
-                     local_cache, seg, ctl);
+                     local_cache, seg, tile_heads, scan_tiles(n), ctl);
 }
 void launch_decide(hipStream_t st, const SortedRec* srec, const SegInfo* seg, const DevRule* rules, uint32_t n,
                    rl_status* out, uint32_t* req_thr, EngineCtl* ctl) {
@@ -832,3 +1010,9 @@ void launch_decide(hipStream_t st, const SortedRec* srec, const SegInfo* seg, co
 }
 
 }  // namespace rlhip
+
+#ifdef RL_STAMPS
+extern "C" int rl_debug_stamps(uint64_t* out, uint32_t nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(rlhip::g_stamps), (size_t)nblocks * 8 * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -186,8 +186,8 @@ class Engine:
     def __init__(self, device: int = 0, log2_slots=(16, 16, 16, 14), near_limit_ratio: float = 0.8,
                  local_cache: bool = False, per_second_split: bool = False, max_batch_desc: int = 1 << 16,
                  max_batch_req: Optional[int] = None, max_blob_bytes: Optional[int] = None, sort_bits: int = 48,
-                 hash_seed: int = 0x5EE7AB1E5EED):
-        self.lib = load_library()
+                 hash_seed: int = 0x5EE7AB1E5EED, lib_path: Optional[os.PathLike] = None):
+        self.lib = load_library(lib_path)
         cfg = RlConfig()
         cfg.struct_size = C.sizeof(RlConfig)
         cfg.device = device

@@ -1,0 +1,228 @@
+#!/usr/bin/env python3
+"""bench.py — descriptor decisions/s of the HIP rate-limit decision path (BASELINE.json).
+
+Workload (N=1 line): BASELINE config 3 — 1e8 keys, Zipf s=1.1 over ranks mapped through a
+fixed permutation, rule by rank % 3 (SECOND 10 / MINUTE 600 / HOUR 36000), 1e6 descriptors
+per batch (one descriptor per request, hits_addend 1), `now` advancing 1 s per batch.
+A step = one batch through the whole device path (fingerprint, radix sort, segmented scan,
+table apply, decide). Inputs are resident in HBM before timing; outputs stay in HBM.
+
+Multi-GPU (torchrun, one rank per GPU): each rank owns an independent key shard (its own
+domain, its own counter table) and processes its own batch per step — weak scaling with
+no data-path collective. value = descriptors decided by all ranks / max-over-ranks time.
+
+Also reported (rank 0): per-kernel HIP-event times over an extra K steps, the roofline
+of the batch pipeline against §8(d)'s algorithmic bytes, and the CPU oracle timed on a
+bounded sample of the same stream (cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "api-ratelimit_amd"))
+
+import hiprl  # noqa: E402
+import workload  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3])
+    ap.add_argument("--desc", type=int, default=1_000_000, help="descriptors per batch")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--no-kernel-times", action="store_true")
+    ap.add_argument("--json-out", type=str, default="")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    d = args.desc
+    if args.config == 3:
+        gen, rules, log2 = workload.config3_batch, workload.CONFIG3_RULES, (22, 24, 25, 12)
+        wl = "config3: 1e8 keys Zipf s=1.1, SECOND/MINUTE/HOUR by rank%3, 1 descriptor/request"
+    elif args.config == 2:
+        gen, rules, log2 = workload.config2_batch, workload.CONFIG2_RULES, (22, 12, 12, 12)
+        wl = "config2: 1e6 uniform keys, SECOND L=5, 1 descriptor/request"
+    else:
+        gen, rules, log2 = workload.config1_batch, workload.CONFIG1_RULES, (16, 12, 12, 12)
+        wl = "config1: examples/ratelimit rules, 1e4 keys"
+    n_batches = args.warmup + args.steps * (1 if args.no_kernel_times else 2)
+    # Each rank is its own key shard: seed the stream by rank.
+    host_batches = []
+    t_gen = time.time()
+    for b in range(n_batches):
+        if args.config == 1:
+            hb = gen(b, d=d, seed=1 + 7919 * rank)
+        else:
+            hb = gen(b, d=d, seed=(3 if args.config == 3 else 2) + 7919 * rank)
+        host_batches.append(hb)
+    t_gen = time.time() - t_gen
+
+    eng = hiprl.Engine(device=local, log2_slots=log2, max_batch_desc=d, max_batch_req=d,
+                       max_blob_bytes=max(int(hb.blob.shape[0]) for hb in host_batches) + 64, sort_bits=48)
+    eng.load_rules(rules)
+
+    def upload(hb):
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        return dict(blob=t(hb.blob), off=t(hb.off.view(np.int32)), rule=t(hb.rule.view(np.int32)),
+                    req=t(hb.req_of.view(np.int32)), now=t(hb.now), hits=t(hb.hits.view(np.int32)),
+                    n_desc=hb.n_desc, n_req=hb.n_req, blob_bytes=int(hb.off[-1]))
+
+    dev_batches = [upload(hb) for hb in host_batches]
+    out = torch.empty(d * 20, dtype=torch.uint8, device=dev)
+    thr = torch.empty(d, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def step(db):
+        ptrs = [db["blob"].data_ptr(), db["off"].data_ptr(), db["rule"].data_ptr(), db["req"].data_ptr(),
+                db["now"].data_ptr(), db["hits"].data_ptr()]
+        eng.submit_device_async(db["n_desc"], db["n_req"], db["blob_bytes"], ptrs, out.data_ptr(), thr.data_ptr())
+        eng.wait()
+
+    for b in range(args.warmup):
+        step(dev_batches[b])
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in range(args.warmup, args.warmup + args.steps):
+        step(dev_batches[b])
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    total_desc = world * args.steps * d
+    value = total_desc / elapsed
+
+    # Per-kernel HIP-event timing over another K steps of the same stream.
+    kernel = None
+    uniq = []
+    if not args.no_kernel_times:
+        eng.set_timing(True)
+        for b in range(args.warmup + args.steps, args.warmup + 2 * args.steps):
+            step(dev_batches[b])
+            uniq.append(eng.last_batch_info()["unique_keys"])
+        kt = eng.kernel_times()
+        eng.set_timing(False)
+        kernel = {k: dict(total_ms=v[0], launches=v[1]) for k, v in kt.items() if v[1]}
+    info = eng.last_batch_info()
+    if not uniq:
+        uniq = [info["unique_keys"]]
+    stats = eng.stats()
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    # Roofline of the batch pipeline against §8(d) algorithmic bytes.
+    U = float(np.mean(uniq))
+    hb_last = host_batches[-1]
+    alg_bytes = workload.algorithmic_bytes(hb_last, int(U))
+    roofline = None
+    if kernel:
+        per_batch_ms = {k: v["total_ms"] / args.steps for k, v in kernel.items()}
+        pipe_ms = sum(v for k, v in per_batch_ms.items())
+        dom = max((k for k in per_batch_ms if k != "memset"), key=lambda k: per_batch_ms[k])
+        achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
+        prof_dir = ROOT / "profiles"
+        traffic = None
+        tf = prof_dir / "r01_pmc_traffic.json"
+        if tf.exists():
+            try:
+                traffic = json.loads(tf.read_text()).get("hbm_bytes_per_batch")
+            except Exception:
+                traffic = None
+        roofline = {
+            "bound": "hbm", "kernel": "batch pipeline (all kernels of one batch, HIP events on the engine stream)",
+            "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "algorithmic_bytes_per_batch": alg_bytes, "unique_keys_per_batch": int(U),
+            "pipeline_us_per_batch": round(pipe_ms * 1e3, 2),
+            "dominant_kernel": {"name": dom, "us_per_batch": round(per_batch_ms[dom] * 1e3, 2),
+                                "launches_per_batch": kernel[dom]["launches"] / args.steps,
+                                "avg_us_per_launch": round(kernel[dom]["total_ms"] * 1e3 / kernel[dom]["launches"], 2)},
+            "kernels_us_per_batch": {k: round(v * 1e3, 2) for k, v in per_batch_ms.items()},
+        }
+
+    cpu = None
+    if world == 1 and args.cpu_seconds > 0:
+        sys.path.insert(0, str(ROOT / "oracle"))
+        import oracle as orc
+
+        o = orc.Oracle()
+        o.load_rules(rules)
+        n_done, t_cpu, nb = 0, 0.0, 0
+        for hb in host_batches:
+            t1 = time.perf_counter()
+            o.submit(hb)
+            t_cpu += time.perf_counter() - t1
+            n_done += hb.n_desc
+            nb += 1
+            if t_cpu >= args.cpu_seconds:
+                break
+        cpu = {"value": round(n_done / t_cpu, 1), "unit": "descriptor decisions/s", "cores": 1, "kind": "port",
+               "sample": f"first {nb} batches ({n_done} descriptors) of the same stream through the C++ oracle "
+                         f"(serial DoLimit over an in-memory Redis stand-in), {t_cpu:.1f} s"}
+
+    line = {
+        "metric": "descriptor decisions/sec, 100M keys Zipf, 1-8 GPUs; % of HBM peak" if args.config == 3
+        else f"descriptor decisions/sec (config {args.config})",
+        "value": round(value, 1),
+        "unit": "descriptor decisions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded splitmix64 / bounded Zipf stream, generated on host, resident in HBM)",
+        "config": {"workload": wl, "descriptors_per_batch": d, "requests_per_batch": d,
+                   "parallelism": f"key-sharded x{world} (independent shards, no collective)",
+                   "sort_bits": 48, "unique_keys_per_batch": int(U)},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "engine": {"resorts": stats["resorts"], "batches": stats["batches"], "gen_s": round(t_gen, 1)},
+    }
+    s = json.dumps(line)
+    print(s, flush=True)
+    if args.json_out:
+        Path(args.json_out).write_text(s + "\n")
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
