@@ -118,6 +118,7 @@ enum : uint32_t {
   ERR_BAD_TIME = 8u,
   ERR_BAD_INPUT = 16u,    // rule id or request index out of range
   ERR_WINDOW_SPAN = 32u,  // a region saw window generations more than one apart in one batch
+  ERR_V2_FALLBACK = 64u,  // the bucketed pipeline cannot take this batch: rerun it on the LSD pipeline
 };
 
 // Small device control block, zeroed per batch. Same-line atomics serialise at the L2
@@ -127,13 +128,16 @@ struct EngineCtl {
   uint32_t err;          // atomicOr, only on an error
   uint32_t n_nil;        // nil-limit descriptors (sorted to the tail); written by k_hist_scan
   uint32_t n_segments;   // unique keys in the batch (U); written by k_leader block 0
-  uint32_t n_inserted;   // reserved
+  uint32_t n_inserted;   // unused (new keys are counted in tile_ctr[INS_CTR0..])
   uint32_t gen_min[8];   // per region: min window generation in the batch (k_hist_scan)
   uint32_t gen_max[8];   // per region: max window generation in the batch (k_hist_scan)
   uint32_t pad0[64 - 20];
   uint32_t tile_ctr[32][64];  // dynamic tile tickets, one 256-B line each
 };
 static_assert(sizeof(EngineCtl) == 256 + 32 * 256, "EngineCtl layout");
+// tile_ctr rows 16..23: per-batch new-key counters (k_leader, one row per wave id mod 8)
+constexpr int INS_CTR0 = 16;
+constexpr int INS_LINES = 8;
 constexpr int FP_PART_WORDS = 17;  // per fingerprint block: 8 x ~min gen, 8 x max gen, nil count
 
 // Counter table: 8 regions (unit x window parity), region r has 2^region_log2[r] slots.
@@ -141,6 +145,37 @@ struct TableDesc {
   Slot* slots;
   uint64_t region_base[8];  // slot offset of each region
   uint32_t region_log2[8];
+};
+
+// Hot-key set entry (v2 pipeline): a key prefix seen with many descriptors per batch.
+// (a, b) is the fingerprint lane state after the prefix bytes (length and unit folded in),
+// i.e. a 128-bit hash of (prefix bytes, unit); the window is not part of it.
+struct __attribute__((aligned(32))) HotEntry {
+  uint64_t a, b;
+  uint32_t unit;
+  uint32_t rule;   // the rule id every hot descriptor must carry (else the batch falls back)
+  uint32_t idx;    // hot index 0..HOT_MAX-1; 0xFFFFFFFF = empty slot
+  uint32_t pad;
+};
+constexpr int HOT_MAX = 256;              // hot prefixes per batch
+constexpr int HOT_SLOTS = 512;            // open-addressing table of HotEntry (device + LDS copy)
+constexpr int HOT_BUCKETS = 2 * HOT_MAX;  // hot prefix x window parity
+constexpr int MSD_BITS = 11;
+constexpr int MSD_BUCKETS = 1 << MSD_BITS;   // region(3) | 8 fingerprint bits
+constexpr int NBUCKETS = HOT_BUCKETS + MSD_BUCKETS + 1;
+constexpr uint32_t NIL_BUCKET = NBUCKETS - 1;
+constexpr int BUCKET_CAP = 1024;          // max descriptors in one MSD bucket on the fast path
+constexpr int BG_RANGE = 1024;            // k_bgroup: MSD buckets whose start lies in one 1024-window
+constexpr int BG_MAX = BG_RANGE + BUCKET_CAP;
+constexpr int V2_TILE = 4096;             // k_fp2 / k_bscatter arrival tile
+constexpr int HOT_CHUNK = 4096;           // k_bgroup hot-region chunk
+constexpr uint32_t HOT_MIN_SEG = 128;     // segments at least this long become hot candidates
+constexpr int CAND_MAX = 1024;
+constexpr int CAND_CTR = 30;  // EngineCtl::tile_ctr[CAND_CTR][0] counts hot candidates (own line)
+
+struct __attribute__((aligned(16))) HotCand {
+  uint64_t a, b;
+  uint32_t unit, rule, count, first_idx;
 };
 
 constexpr int RADIX_BITS = 8;

@@ -1,0 +1,94 @@
+// rl_device.h — device helpers shared by the v1 (LSD sort) and v2 (bucketed) pipelines.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rl_common.h"
+
+namespace rlhip {
+
+#define RL_DEV __device__ __forceinline__
+
+RL_DEV uint32_t ld_relaxed(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+RL_DEV uint64_t ld_relaxed64(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+RL_DEV void st_relaxed(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+RL_DEV void st_relaxed64(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+RL_DEV uint64_t lanemask_lt() {
+  const uint32_t lane = __lane_id();
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+constexpr uint32_t SPIN_LIMIT = 1u << 24;
+
+// ---------------------------------------------------------------------------
+// k_fingerprint
+// ---------------------------------------------------------------------------
+struct DevBatch {
+  uint32_t n_desc, n_req, blob_bytes, pad;
+  const uint8_t* blob;
+  const uint32_t* off;
+  const uint32_t* rule;
+  const uint32_t* req_of;
+  const int64_t* now;
+  const uint32_t* hits;
+};
+
+// Unaligned little-endian 8-byte words of a byte string, read as aligned dwords and
+// funnel-shifted (v_alignbyte_b32). The blob has >= 16 bytes of slack past its end.
+RL_DEV void hash_prefix(const uint8_t* blob, uint32_t off, uint32_t len, FpState& s) {
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(blob + (off & ~3u));
+  const uint32_t sh = (off & 3u) * 8u;
+  uint32_t d0 = p[0];
+  uint32_t rem = len;
+  for (uint32_t k = 0; rem > 0; ++k) {
+    const uint32_t d1 = p[2 * k + 1];
+    const uint32_t d2 = p[2 * k + 2];
+    uint32_t lo = sh ? __builtin_amdgcn_alignbyte(d1, d0, sh / 8) : d0;
+    uint32_t hi = sh ? __builtin_amdgcn_alignbyte(d2, d1, sh / 8) : d1;
+    uint64_t w = ((uint64_t)hi << 32) | lo;
+    if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
+    fp_word(s, w);
+    d0 = d2;
+    rem = rem > 8 ? rem - 8 : 0;
+  }
+}
+
+RL_DEV int64_t div_const(int64_t now, uint32_t unit) {
+  switch (unit) {
+    case RL_UNIT_SECOND: return now;
+    case RL_UNIT_MINUTE: return now / 60;
+    case RL_UNIT_HOUR: return now / 3600;
+    default: return now / 86400;
+  }
+}
+
+RL_DEV uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t o = __shfl_xor(v, d, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+RL_DEV uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t o = __shfl_xor(v, d, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+
+RL_DEV void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+}  // namespace rlhip

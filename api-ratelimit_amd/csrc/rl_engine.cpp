@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -33,7 +34,20 @@ void launch_sort_pass(hipStream_t, const uint64_t*, const uint32_t*, uint64_t*, 
 void launch_scan(hipStream_t, const uint64_t*, const uint32_t*, const ItemRec*, uint32_t, int, int, SortedRec*,
                  uint64_t*, uint64_t*, uint32_t*, uint32_t*, EngineCtl*);
 void launch_leader(hipStream_t, const uint64_t*, const SortedRec*, const ItemRec*, const DevRule*, uint32_t,
-                   const TableDesc&, int, SegInfo*, const uint32_t*, EngineCtl*);
+                   const TableDesc&, int, SegInfo*, const uint32_t*, uint32_t, HotCand*, EngineCtl*);
+uint32_t v2_tiles(uint32_t n);
+uint32_t v2_msd_wgs(uint32_t n);
+uint32_t v2_hot_wgs(uint32_t n);
+void launch_fp2(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, const HotEntry*, uint64_t*,
+                ItemRec*, uint16_t*, uint32_t*, rl_status*, uint32_t*, uint32_t*, uint32_t*, unsigned long long*,
+                EngineCtl*);
+void launch_bscan(hipStream_t, const uint32_t*, const unsigned long long*, uint32_t, uint32_t*, unsigned long long*,
+                  uint32_t*, const uint32_t*, EngineCtl*);
+void launch_bscatter(hipStream_t, const uint64_t*, const uint16_t*, const uint32_t*, uint32_t, const uint32_t*,
+                     const uint32_t*, const unsigned long long*, uint64_t*, uint32_t*, uint64_t*, EngineCtl*);
+void launch_bgroup(hipStream_t, const uint64_t*, const uint32_t*, const uint64_t*, const ItemRec*, const uint32_t*,
+                   uint32_t, uint64_t*, SortedRec*, uint32_t*, EngineCtl*);
+void launch_cand_state(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, const EngineCtl*);
 void launch_decide(hipStream_t, const SortedRec*, const SegInfo*, const DevRule*, uint32_t, rl_status*, uint32_t*,
                    EngineCtl*);
 }  // namespace rlhip
@@ -44,10 +58,19 @@ namespace {
 
 enum KernelId {
   KT_FINGERPRINT, KT_HISTOGRAM, KT_HIST_SCAN, KT_SORT_PASS, KT_SCAN, KT_LEADER, KT_DECIDE, KT_FALLBACK, KT_MEMSET,
-  KT_COUNT
+  KT_FP2, KT_BSCAN, KT_BSCATTER, KT_BGROUP, KT_CAND, KT_COUNT
 };
 const char* const kKernelNames[KT_COUNT] = {"k_fingerprint", "k_histogram", "k_hist_scan", "k_sort_pass", "k_scan",
-                                            "k_leader",      "k_decide",    "fallback",    "memset"};
+                                            "k_leader",      "k_decide",    "fallback",    "memset",      "k_fp2",
+                                            "k_bscan",       "k_bscatter",  "k_bgroup",    "k_cand_state"};
+
+enum Mode { MODE_V2 = 0, MODE_LSD = 1, MODE_LSD_FULL = 2 };
+
+// Hot-key set kept on the host between batches (v2 bucketing).
+struct HotKey {
+  uint64_t a, b;
+  uint32_t unit, rule, count;
+};
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -87,7 +110,21 @@ struct rl_engine {
   uint32_t* hist_part = nullptr;  // per-block partial digit histograms
   uint32_t* fp_part = nullptr;    // per-block fingerprint partials (generation range, nil count)
   uint32_t* fp_part2 = nullptr;   // the same folded per histogram block
-  uint32_t* tile_heads = nullptr; // per-scan-tile segment-head counts
+  uint32_t* tile_heads = nullptr; // per-scan-tile / per-workgroup segment-head counts
+  // v2 (bucketed) pipeline
+  uint16_t* bkt = nullptr;              // bucket id per descriptor
+  uint32_t* hbuf = nullptr;             // hits_addend per descriptor
+  uint32_t* tcount = nullptr;           // [tile][NBUCKETS]
+  uint32_t* toff = nullptr;             // [tile][NBUCKETS]
+  unsigned long long* thsum = nullptr;  // [tile][HOT_BUCKETS]
+  unsigned long long* hoff = nullptr;   // [tile][HOT_BUCKETS]
+  uint32_t* btotal = nullptr;           // [NBUCKETS]
+  uint64_t* bP = nullptr;               // hot descriptors: INCRBY prefix, bucket order
+  HotEntry* d_hot = nullptr;            // device hot-key table (HOT_SLOTS)
+  HotCand* d_cand = nullptr;            // hot-set candidates (CAND_MAX)
+  HotCand* h_cand = nullptr;            // pinned copy
+  std::vector<HotKey> hot;              // current hot-key set (index = hot idx)
+  bool hot_dirty = false;
   uint8_t* zero_block = nullptr;  // ctl | hist | lookbacks (zeroed per batch)
   size_t zero_cap = 0;
   EngineCtl* h_ctl = nullptr;     // pinned copy of the control block
@@ -157,13 +194,16 @@ struct rl_engine {
     return z;
   }
 
-  int run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bool full);
+  int run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, int mode);
   int finish();
+  int upload_hot();
+  void update_hot(uint32_t n_cand);
   int enqueue_d2h();
 };
 
-int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bool full) {
+int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, int mode) {
   const uint32_t n = b.n_desc;
+  const bool full = mode == MODE_LSD_FULL;
   const int passes = full ? 16 : npasses;
   const ZLayout z = zlayout(n, passes);
   EngineCtl* ctl = reinterpret_cast<EngineCtl*>(zero_block + z.ctl);
@@ -174,13 +214,46 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bo
   const size_t lb_pass_stride = (size_t)sort_tiles(n > 0 ? n : 1) * RADIX;  // per-digit look-back words
   hipError_t e;
   timed(KT_MEMSET, [&] {
-    hipMemsetAsync(zero_block, 0, z.total, stream);
+    // the bucketed pipeline keeps no look-back state: only the control block is cleared
+    hipMemsetAsync(zero_block, 0, mode == MODE_V2 ? z.ctl + sizeof(EngineCtl) : z.total, stream);
     // request throttles are zeroed by k_fingerprint; only an empty batch needs a memset
     if (b.n_req && n == 0) hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
   });
   if (n == 0) {
     e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpyAsync(ctl)");
+  }
+  if (mode == MODE_V2) {
+    // Bucketed pipeline: fingerprint + bucket histograms, per-bucket scan, stable bucket
+    // scatter, LDS grouping, then the shared leader / decide kernels.
+    if (hot_dirty) {
+      int rc = upload_hot();
+      if (rc) return rc;
+    }
+    timed(KT_FP2, [&] {
+      launch_fp2(stream, b, d_rules, n_rules, cfg.hash_seed, d_hot, keys_orig, recs, bkt, hbuf, out, thr, fp_part,
+                 tcount, thsum, ctl);
+    });
+    timed(KT_BSCAN, [&] { launch_bscan(stream, tcount, thsum, n, toff, hoff, btotal, fp_part, ctl); });
+    timed(KT_BSCATTER, [&] {
+      launch_bscatter(stream, keys_orig, bkt, hbuf, n, btotal, toff, hoff, keys_a, vals_a, bP, ctl);
+    });
+    timed(KT_BGROUP, [&] {
+      launch_bgroup(stream, keys_a, vals_a, bP, recs, btotal, n, keys_b, srec, tile_heads, ctl);
+    });
+    const uint32_t n_heads = v2_msd_wgs(n) + v2_hot_wgs(n);
+    timed(KT_LEADER, [&] {
+      launch_leader(stream, keys_b, srec, recs, d_rules, n, tab, cfg.local_cache ? 1 : 0, seg, tile_heads, n_heads,
+                    d_cand, ctl);
+    });
+    timed(KT_DECIDE, [&] { launch_decide(stream, srec, seg, d_rules, n, out, thr, ctl); });
+    timed(KT_CAND, [&] { launch_cand_state(stream, b, d_rules, cfg.hash_seed, d_cand, ctl); });
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "kernel launch");
+    e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_cand, d_cand, sizeof(HotCand) * CAND_MAX, hipMemcpyDeviceToHost, stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(ctl)");
+    return 0;
   }
   const uint64_t* skeys;
   const uint32_t* svals;
@@ -250,14 +323,84 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, bo
                 &ctl->tile_ctr[31][0], tile_heads, ctl);
   });
   timed(KT_LEADER, [&] {
-    launch_leader(stream, skeys, srec, recs, d_rules, n, tab, cfg.local_cache ? 1 : 0, seg, tile_heads, ctl);
+    launch_leader(stream, skeys, srec, recs, d_rules, n, tab, cfg.local_cache ? 1 : 0, seg, tile_heads,
+                  scan_tiles(n), d_cand, ctl);
   });
   timed(KT_DECIDE, [&] { launch_decide(stream, srec, seg, d_rules, n, out, thr, ctl); });
+  timed(KT_CAND, [&] { launch_cand_state(stream, b, d_rules, cfg.hash_seed, d_cand, ctl); });
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
   e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(h_cand, d_cand, sizeof(HotCand) * CAND_MAX, hipMemcpyDeviceToHost, stream);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(ctl)");
   return 0;
+}
+
+// Upload the hot-key set as an open-addressing table (slot = a>>40 mod HOT_SLOTS).
+int rl_engine::upload_hot() {
+  std::vector<HotEntry> t(HOT_SLOTS);
+  for (auto& x : t) {
+    x.a = x.b = 0;
+    x.unit = x.rule = 0;
+    x.idx = 0xFFFFFFFFu;
+    x.pad = 0;
+  }
+  for (size_t i = 0; i < hot.size(); ++i) {
+    uint32_t s = (uint32_t)(hot[i].a >> 40) & (HOT_SLOTS - 1);
+    while (t[s].idx != 0xFFFFFFFFu) s = (s + 1) & (HOT_SLOTS - 1);
+    t[s].a = hot[i].a;
+    t[s].b = hot[i].b;
+    t[s].unit = hot[i].unit;
+    t[s].rule = hot[i].rule;
+    t[s].idx = (uint32_t)i;
+  }
+  // pinned bounce buffer: h_cand is reused (large enough: CAND_MAX * 32 B >= HOT_SLOTS * 32 B)
+  static_assert(sizeof(HotCand) * CAND_MAX >= sizeof(HotEntry) * HOT_SLOTS, "bounce buffer");
+  hipError_t e = hipStreamSynchronize(stream);
+  if (e == hipSuccess) {
+    memcpy(h_cand, t.data(), sizeof(HotEntry) * HOT_SLOTS);
+    e = hipMemcpyAsync(d_hot, h_cand, sizeof(HotEntry) * HOT_SLOTS, hipMemcpyHostToDevice, stream);
+  }
+  if (e != hipSuccess) return hip_fail(e, "upload hot set");
+  hot_dirty = false;
+  st.hot_keys = hot.size();
+  return 0;
+}
+
+// Rebuild the hot-key set from this batch's long segments (k_leader candidates with their
+// prefix state from k_cand_state). Keys are (prefix state, unit); two windows of one
+// prefix merge. Keep the HOT_MAX longest with at least HOT_MIN_SEG descriptors.
+void rl_engine::update_hot(uint32_t n_cand) {
+  n_cand = n_cand < (uint32_t)CAND_MAX ? n_cand : (uint32_t)CAND_MAX;
+  std::vector<HotKey> next;
+  for (uint32_t i = 0; i < n_cand; ++i) {
+    const HotCand& c = h_cand[i];
+    bool merged = false;
+    for (auto& x : next)
+      if (x.a == c.a && x.b == c.b && x.unit == c.unit) {
+        x.count += c.count;
+        if (x.rule != c.rule) x.count = 0;  // two rules on one prefix: not bucketable
+        merged = true;
+        break;
+      }
+    if (!merged) next.push_back(HotKey{c.a, c.b, c.unit, c.rule, c.count});
+  }
+  next.erase(std::remove_if(next.begin(), next.end(), [](const HotKey& x) { return x.count < HOT_MIN_SEG; }),
+             next.end());
+  std::sort(next.begin(), next.end(), [](const HotKey& x, const HotKey& y) { return x.count > y.count; });
+  if (next.size() > (size_t)HOT_MAX) next.resize(HOT_MAX);
+  // canonical order, so an unchanged set (the steady state of a skewed stream) costs no upload
+  auto ident_less = [](const HotKey& x, const HotKey& y) {
+    return x.a != y.a ? x.a < y.a : x.b != y.b ? x.b < y.b : x.unit < y.unit;
+  };
+  std::sort(next.begin(), next.end(), ident_less);
+  bool same = next.size() == hot.size();
+  for (size_t i = 0; same && i < next.size(); ++i)
+    same = next[i].a == hot[i].a && next[i].b == hot[i].b && next[i].unit == hot[i].unit && next[i].rule == hot[i].rule;
+  if (!same) {
+    hot = std::move(next);
+    hot_dirty = true;
+  }
 }
 
 // Wait for the in-flight batch, run the full-fingerprint re-sort if needed, copy
@@ -266,11 +409,22 @@ int rl_engine::finish() {
   hipError_t e = hipStreamSynchronize(stream);
   if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
   uint32_t errs = h_ctl->err;
+  if ((errs & ERR_V2_FALLBACK) && !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME))) {
+    // The bucketed pipeline refused the batch before touching the table (oversized
+    // bucket or a hot prefix with a second rule): run it on the LSD pipeline.
+    ++st.lsd_fallbacks;
+    int rc = run_pipeline(dev_batch, pend_out_dev, pend_thr_dev, MODE_LSD);
+    if (rc) return rc;
+    if (host_path && (rc = enqueue_d2h()) != 0) return rc;
+    e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+    errs = h_ctl->err;
+  }
   if (errs & ERR_NEED_RESORT) {
     // A sort-prefix run held two fingerprints: nothing touched the table (k_leader and
     // k_decide return early), so re-run the batch on the full fingerprint order.
     ++st.resorts;
-    int rc = run_pipeline(dev_batch, pend_out_dev, pend_thr_dev, true);
+    int rc = run_pipeline(dev_batch, pend_out_dev, pend_thr_dev, MODE_LSD_FULL);
     if (rc) return rc;
     if (host_path && (rc = enqueue_d2h()) != 0) return rc;
     e = hipStreamSynchronize(stream);
@@ -294,13 +448,14 @@ int rl_engine::finish() {
   if (errs & ERR_TABLE_FULL) return fail(RL_ENOSPC, "counter table region full (raise log2_slots)");
   if (errs & ERR_SPIN) return fail(RL_EDEVICE, "device look-back spin limit exceeded");
   if (errs & ERR_NEED_RESORT) return fail(RL_EDEVICE, "full-fingerprint re-sort still found a mixed run");
+  if (!(cfg.flags & RL_CFG_LSD_ONLY)) update_hot(h_ctl->tile_ctr[CAND_CTR][0]);
   last_unique = h_ctl->n_segments;
   last_n = dev_batch.n_desc;
   last_req = dev_batch.n_req;
   last_blob = dev_batch.blob_bytes;
   st.batches += 1;
   st.descriptors += dev_batch.n_desc;
-  st.live_slots_hint += h_ctl->n_inserted;
+  for (int k = 0; k < INS_LINES; ++k) st.live_slots_hint += h_ctl->tile_ctr[INS_CTR0 + k][0];
   if (host_path) {
     if (dev_batch.n_desc) memcpy(user_out, h_out, (size_t)dev_batch.n_desc * sizeof(rl_status));
     if (dev_batch.n_req) memcpy(user_thr, h_thr, (size_t)dev_batch.n_req * 4);
@@ -387,7 +542,25 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   chk(hipMalloc(&e->hist_part, (size_t)hist_blocks((uint32_t)N) * MAX_PASSES * RADIX * 4));
   chk(hipMalloc(&e->fp_part2, (size_t)hist_blocks((uint32_t)N) * FP_PART_WORDS * 4 + 64));
   chk(hipMalloc(&e->fp_part, ((N + 255) / 256) * FP_PART_WORDS * 4 + 64));
-  chk(hipMalloc(&e->tile_heads, (size_t)scan_tiles((uint32_t)N) * 4 + 64));
+  {
+    const size_t nh = std::max<size_t>(scan_tiles((uint32_t)N), v2_msd_wgs((uint32_t)N) + v2_hot_wgs((uint32_t)N));
+    chk(hipMalloc(&e->tile_heads, nh * 4 + 64));
+  }
+  {
+    const size_t T = v2_tiles((uint32_t)N);
+    chk(hipMalloc(&e->bkt, N * 2 + 64));
+    chk(hipMalloc(&e->hbuf, N * 4 + 64));
+    chk(hipMalloc(&e->tcount, T * NBUCKETS * 4));
+    chk(hipMalloc(&e->toff, T * NBUCKETS * 4));
+    chk(hipMalloc(&e->thsum, T * HOT_BUCKETS * 8));
+    chk(hipMalloc(&e->hoff, T * HOT_BUCKETS * 8));
+    chk(hipMalloc(&e->btotal, (NBUCKETS + 1) * 4));
+    chk(hipMalloc(&e->bP, N * 8 + 64));
+    chk(hipMalloc(&e->d_hot, sizeof(HotEntry) * HOT_SLOTS));
+    chk(hipMalloc(&e->d_cand, sizeof(HotCand) * CAND_MAX));
+    chk(hipHostMalloc(&e->h_cand, sizeof(HotCand) * CAND_MAX, hipHostMallocDefault));
+    e->hot_dirty = true;  // upload the empty table before the first batch
+  }
 
   e->zero_cap = e->zlayout((uint32_t)N, MAX_PASSES).total;
   chk(hipMalloc(&e->zero_block, e->zero_cap));
@@ -427,6 +600,17 @@ void rl_destroy(rl_engine* e) {
   hipFree(e->fp_part);
   hipFree(e->fp_part2);
   hipFree(e->tile_heads);
+  hipFree(e->bkt);
+  hipFree(e->hbuf);
+  hipFree(e->tcount);
+  hipFree(e->toff);
+  hipFree(e->thsum);
+  hipFree(e->hoff);
+  hipFree(e->btotal);
+  hipFree(e->bP);
+  hipFree(e->d_hot);
+  hipFree(e->d_cand);
+  hipHostFree(e->h_cand);
 
   hipFree(e->zero_block);
   hipHostFree(e->h_ctl);
@@ -529,7 +713,7 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
   d.req_of = reinterpret_cast<const uint32_t*>(e->d_in + o_req);
   d.now = reinterpret_cast<const int64_t*>(e->d_in + o_now);
   d.hits_addend = reinterpret_cast<const uint32_t*>(e->d_in + o_hits);
-  int rc = e->run_pipeline(d, e->d_out, e->d_thr, false);
+  int rc = e->run_pipeline(d, e->d_out, e->d_thr, (e->cfg.flags & RL_CFG_LSD_ONLY) ? MODE_LSD : MODE_V2);
   if (rc) return rc;
   e->dev_batch = d;
   e->pend_out_dev = e->d_out;
@@ -557,7 +741,7 @@ int rl_submit_device(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t
     return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req)", c.max_batch_desc,
                    c.max_batch_req);
   if (!e->d_rules) rl_load_rules(e, nullptr, 0);
-  int rc = e->run_pipeline(*b, d_out, d_req_throttle_ms, false);
+  int rc = e->run_pipeline(*b, d_out, d_req_throttle_ms, (e->cfg.flags & RL_CFG_LSD_ONLY) ? MODE_LSD : MODE_V2);
   if (rc) return rc;
   e->dev_batch = *b;
   e->pend_out_dev = d_out;
@@ -572,6 +756,8 @@ void* rl_stream(rl_engine* e) { return e ? (void*)e->stream : nullptr; }
 int rl_reset(rl_engine* e) {
   if (!e) return RL_EINVAL;
   if (e->in_flight) return e->fail(RL_ESTATE, "rl_reset while a batch is in flight");
+  e->hot.clear();
+  e->hot_dirty = true;
   hipError_t he = hipMemsetAsync(e->table, 0, e->table_slots * sizeof(Slot), e->stream);
   if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
   return he == hipSuccess ? 0 : e->hip_fail(he, "rl_reset");

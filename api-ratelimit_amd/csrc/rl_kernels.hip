@@ -20,30 +20,9 @@
 #include <stdint.h>
 
 #include "rl_common.h"
+#include "rl_device.h"
 
 namespace rlhip {
-
-#define RL_DEV __device__ __forceinline__
-
-RL_DEV uint32_t ld_relaxed(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-RL_DEV uint64_t ld_relaxed64(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-RL_DEV void st_relaxed(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-RL_DEV void st_relaxed64(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-RL_DEV uint64_t lanemask_lt() {
-  const uint32_t lane = __lane_id();
-  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
-}
-
-constexpr uint32_t SPIN_LIMIT = 1u << 24;
 
 #ifdef RL_STAMPS
 // Diagnostic build only: per-block phase timestamps of the last sort pass (s_memtime).
@@ -52,65 +31,6 @@ __device__ uint64_t g_stamps[4096][8];
 #else
 #define STAMP(k) do { } while (0)
 #endif
-
-// ---------------------------------------------------------------------------
-// k_fingerprint
-// ---------------------------------------------------------------------------
-struct DevBatch {
-  uint32_t n_desc, n_req, blob_bytes, pad;
-  const uint8_t* blob;
-  const uint32_t* off;
-  const uint32_t* rule;
-  const uint32_t* req_of;
-  const int64_t* now;
-  const uint32_t* hits;
-};
-
-// Unaligned little-endian 8-byte words of a byte string, read as aligned dwords and
-// funnel-shifted (v_alignbyte_b32). The blob has >= 16 bytes of slack past its end.
-RL_DEV void hash_prefix(const uint8_t* blob, uint32_t off, uint32_t len, FpState& s) {
-  const uint32_t* p = reinterpret_cast<const uint32_t*>(blob + (off & ~3u));
-  const uint32_t sh = (off & 3u) * 8u;
-  uint32_t d0 = p[0];
-  uint32_t rem = len;
-  for (uint32_t k = 0; rem > 0; ++k) {
-    const uint32_t d1 = p[2 * k + 1];
-    const uint32_t d2 = p[2 * k + 2];
-    uint32_t lo = sh ? __builtin_amdgcn_alignbyte(d1, d0, sh / 8) : d0;
-    uint32_t hi = sh ? __builtin_amdgcn_alignbyte(d2, d1, sh / 8) : d1;
-    uint64_t w = ((uint64_t)hi << 32) | lo;
-    if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
-    fp_word(s, w);
-    d0 = d2;
-    rem = rem > 8 ? rem - 8 : 0;
-  }
-}
-
-RL_DEV int64_t div_const(int64_t now, uint32_t unit) {
-  switch (unit) {
-    case RL_UNIT_SECOND: return now;
-    case RL_UNIT_MINUTE: return now / 60;
-    case RL_UNIT_HOUR: return now / 3600;
-    default: return now / 86400;
-  }
-}
-
-RL_DEV uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t o = __shfl_xor(v, d, 64);
-    v = o < v ? o : v;
-  }
-  return v;
-}
-RL_DEV uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t o = __shfl_xor(v, d, 64);
-    v = o > v ? o : v;
-  }
-  return v;
-}
 
 __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
                                                      uint64_t seed, uint64_t* __restrict__ keys_orig,
@@ -758,7 +678,7 @@ __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ ske
                                                 const ItemRec* __restrict__ recs, const DevRule* __restrict__ rules,
                                                 uint32_t n_all, TableDesc tab, int local_cache,
                                                 SegInfo* __restrict__ seg, const uint32_t* __restrict__ tile_heads,
-                                                uint32_t n_scan_tiles, EngineCtl* ctl) {
+                                                uint32_t n_scan_tiles, HotCand* __restrict__ cand, EngineCtl* ctl) {
   if (blockIdx.x == 0) {
     // U = number of segment heads (k_scan per-tile counts); single writer of n_segments.
     __shared__ uint32_t sh_u[256];
@@ -773,14 +693,28 @@ __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ ske
     if (threadIdx.x == 0) ctl->n_segments = sh_u[0];
   }
   const uint32_t errs = ctl->err;  // flags of earlier launches
-  if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_BAD_INPUT | ERR_WINDOW_SPAN)) return;
-  const uint32_t n = n_all - ctl->n_nil;  // written by k_fingerprint (earlier launch)
+  if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_BAD_INPUT | ERR_WINDOW_SPAN | ERR_V2_FALLBACK)) return;
+  const uint32_t n = n_all - ctl->n_nil;  // written by an earlier launch
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
   if (j + 1 < n && (srec[j + 1].head & ~HEAD_MIXED_RULE) != j + 1) return;  // not a tail
   const SortedRec tail = srec[j];
   const uint32_t hp = tail.head & ~HEAD_MIXED_RULE;
   const bool mixed_rule = (tail.head & HEAD_MIXED_RULE) != 0;
+  if (j - hp + 1 >= HOT_MIN_SEG && !mixed_rule) {
+    // long segment: a hot-set candidate for the next batch (v2 bucketing)
+    const uint32_t c = atomicAdd(&ctl->tile_ctr[CAND_CTR][0], 1u);
+    if (c < (uint32_t)CAND_MAX) {
+      HotCand hc;
+      hc.a = 0;
+      hc.b = 0;
+      hc.unit = 0;
+      hc.rule = tail.rule;
+      hc.count = j - hp + 1;
+      hc.first_idx = srec[hp].idx;
+      cand[c] = hc;
+    }
+  }
   const uint64_t key = skeys[j];
   const ItemRec rec = recs[tail.idx];
   const uint32_t region = key_region(key);
@@ -839,6 +773,12 @@ __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ ske
     slot->key = key;
     slot->fp_lo_hi = lohi;
   }
+  {  // new-key count (engine stats): one atomic per wave, spread over INS_LINES lines
+    const uint64_t ins = __ballot(!existed);
+    if (ins && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1))
+      atomicAdd(&ctl->tile_ctr[INS_CTR0 + ((blockIdx.x * 4 + (threadIdx.x >> 6)) & (INS_LINES - 1))][0],
+                (uint32_t)__popcll(ins));
+  }
 
   uint32_t freeze = SEG_NO_FREEZE;
   uint64_t final_count = base + tail.P;
@@ -896,7 +836,9 @@ __global__ __launch_bounds__(256) void k_decide(const SortedRec* __restrict__ sr
                                                 rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
                                                 EngineCtl* ctl) {
   const uint32_t errs = ctl->err;  // flags of earlier launches
-  if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_TABLE_FULL | ERR_BAD_INPUT | ERR_WINDOW_SPAN)) return;
+  if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_TABLE_FULL | ERR_BAD_INPUT | ERR_WINDOW_SPAN |
+              ERR_V2_FALLBACK))
+    return;
   const uint32_t n = n_all - ctl->n_nil;  // written by k_fingerprint (earlier launch)
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
@@ -1000,9 +942,9 @@ void launch_scan(hipStream_t st, const uint64_t* skeys, const uint32_t* svals, c
 }
 void launch_leader(hipStream_t st, const uint64_t* skeys, const SortedRec* srec, const ItemRec* recs,
                    const DevRule* rules, uint32_t n, const TableDesc& tab, int local_cache, SegInfo* seg,
-                   const uint32_t* tile_heads, EngineCtl* ctl) {
+                   const uint32_t* heads, uint32_t n_heads, HotCand* cand, EngineCtl* ctl) {
   hipLaunchKernelGGL(k_leader, dim3((n + 255) / 256), dim3(256), 0, st, skeys, srec, recs, rules, n, tab,
-                     local_cache, seg, tile_heads, scan_tiles(n), ctl);
+                     local_cache, seg, heads, n_heads, cand, ctl);
 }
 void launch_decide(hipStream_t st, const SortedRec* srec, const SegInfo* seg, const DevRule* rules, uint32_t n,
                    rl_status* out, uint32_t* req_thr, EngineCtl* ctl) {

@@ -41,7 +41,7 @@ class RlConfig(C.Structure):
     _fields_ = [("struct_size", C.c_uint32), ("device", C.c_int32), ("log2_slots", C.c_uint32 * 4),
                 ("near_limit_ratio", C.c_float), ("local_cache", C.c_uint32), ("per_second_split", C.c_uint32),
                 ("max_batch_desc", C.c_uint32), ("max_batch_req", C.c_uint32), ("max_blob_bytes", C.c_uint32),
-                ("sort_bits", C.c_uint32), ("hash_seed", C.c_uint64)]
+                ("sort_bits", C.c_uint32), ("flags", C.c_uint32), ("hash_seed", C.c_uint64)]
 
 
 class RlRule(C.Structure):
@@ -56,7 +56,7 @@ class RlBatch(C.Structure):
 
 class RlEngineStats(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("descriptors", C.c_uint64), ("resorts", C.c_uint64),
-                ("live_slots_hint", C.c_uint64)]
+                ("live_slots_hint", C.c_uint64), ("lsd_fallbacks", C.c_uint64), ("hot_keys", C.c_uint64)]
 
 
 # (name, argtypes, restype) of every symbol include/rl_hip.h declares
@@ -186,7 +186,7 @@ class Engine:
     def __init__(self, device: int = 0, log2_slots=(16, 16, 16, 14), near_limit_ratio: float = 0.8,
                  local_cache: bool = False, per_second_split: bool = False, max_batch_desc: int = 1 << 16,
                  max_batch_req: Optional[int] = None, max_blob_bytes: Optional[int] = None, sort_bits: int = 48,
-                 hash_seed: int = 0x5EE7AB1E5EED, lib_path: Optional[os.PathLike] = None):
+                 hash_seed: int = 0x5EE7AB1E5EED, lib_path: Optional[os.PathLike] = None, lsd_only: bool = False):
         self.lib = load_library(lib_path)
         cfg = RlConfig()
         cfg.struct_size = C.sizeof(RlConfig)
@@ -200,6 +200,7 @@ class Engine:
         cfg.max_batch_req = max_batch_req or max_batch_desc
         cfg.max_blob_bytes = max_blob_bytes or max_batch_desc * 64
         cfg.sort_bits = sort_bits
+        cfg.flags = 1 if lsd_only else 0
         cfg.hash_seed = hash_seed
         self.cfg = cfg
         h = C.c_void_p()

@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--desc", type=int, default=1_000_000, help="descriptors per batch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-kernel-times", action="store_true")
+    ap.add_argument("--pipeline", choices=["bucketed", "lsd"], default="bucketed",
+                    help="decision pipeline (bucketed default; lsd = radix-sort pipeline only)")
     ap.add_argument("--json-out", type=str, default="")
     return ap.parse_args()
 
@@ -85,7 +87,8 @@ def main():
     t_gen = time.time() - t_gen
 
     eng = hiprl.Engine(device=local, log2_slots=log2, max_batch_desc=d, max_batch_req=d,
-                       max_blob_bytes=max(int(hb.blob.shape[0]) for hb in host_batches) + 64, sort_bits=48)
+                       max_blob_bytes=max(int(hb.blob.shape[0]) for hb in host_batches) + 64, sort_bits=48,
+                       lsd_only=args.pipeline == "lsd")
     eng.load_rules(rules)
 
     def upload(hb):
@@ -211,10 +214,11 @@ def main():
         "data": "synthetic (seeded splitmix64 / bounded Zipf stream, generated on host, resident in HBM)",
         "config": {"workload": wl, "descriptors_per_batch": d, "requests_per_batch": d,
                    "parallelism": f"key-sharded x{world} (independent shards, no collective)",
-                   "sort_bits": 48, "unique_keys_per_batch": int(U)},
+                   "pipeline": args.pipeline, "unique_keys_per_batch": int(U)},
         "roofline": roofline,
         "cpu_baseline": cpu,
-        "engine": {"resorts": stats["resorts"], "batches": stats["batches"], "gen_s": round(t_gen, 1)},
+        "engine": {"resorts": stats["resorts"], "lsd_fallbacks": stats["lsd_fallbacks"], "hot_keys": stats["hot_keys"],
+                   "batches": stats["batches"], "gen_s": round(t_gen, 1)},
     }
     s = json.dumps(line)
     print(s, flush=True)

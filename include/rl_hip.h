@@ -65,9 +65,15 @@ typedef struct rl_config {
   uint32_t max_batch_desc;     /* capacity: descriptors per batch (HIP_BATCH_LIMIT) */
   uint32_t max_batch_req;      /* capacity: requests per batch */
   uint32_t max_blob_bytes;     /* capacity: key-prefix bytes per batch */
-  uint32_t sort_bits;          /* fingerprint bits radix-sorted per batch (8..64, multiple of 8; 0 = 48) */
+  uint32_t sort_bits;          /* LSD pipeline: fingerprint bits radix-sorted per batch (8..64, multiple of 8; 0 = 48) */
+  uint32_t flags;              /* RL_CFG_* */
   uint64_t hash_seed;          /* fingerprint seed (randomise per process against hash flooding) */
 } rl_config;
+
+/* rl_config.flags */
+enum {
+  RL_CFG_LSD_ONLY = 1u  /* always use the LSD radix-sort pipeline (default: bucketed pipeline, LSD as fallback) */
+};
 
 /* One rate-limit rule: config.RateLimit.Limit (src/config/config.go:26-32). */
 typedef struct rl_rule {
@@ -110,6 +116,8 @@ typedef struct rl_engine_stats {
   uint64_t descriptors;       /* descriptors decided */
   uint64_t resorts;           /* batches re-sorted on the full fingerprint after a sort-prefix collision */
   uint64_t live_slots_hint;   /* keys inserted since creation (monotone; not a live count) */
+  uint64_t lsd_fallbacks;     /* batches the bucketed pipeline handed to the LSD pipeline */
+  uint64_t hot_keys;          /* size of the hot-key set used by the last batch */
 } rl_engine_stats;
 
 int rl_create(const rl_config* cfg, rl_engine** out);

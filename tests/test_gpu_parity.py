@@ -15,6 +15,7 @@ import pytest
 import hiprl
 import oracle
 import streams
+import workload
 
 pytestmark = pytest.mark.gpu
 
@@ -71,32 +72,35 @@ def batch_sizes(reqs, rng, max_bs):
     return sizes
 
 
-def run_both(reqs, sizes, local_cache, sort_bits=48, ratio=0.8):
+def run_both(reqs, sizes, local_cache, sort_bits=48, ratio=0.8, lsd_only=False):
     o = oracle.Oracle(near_limit_ratio=ratio, local_cache=local_cache)
     o.load_rules(RULES)
-    e = hiprl.Engine(near_limit_ratio=ratio, local_cache=local_cache, sort_bits=sort_bits, max_batch_desc=1 << 17)
+    e = hiprl.Engine(near_limit_ratio=ratio, local_cache=local_cache, sort_bits=sort_bits, max_batch_desc=1 << 17,
+                     lsd_only=lsd_only)
     e.load_rules(RULES)
     a = streams.replay(o, reqs, sizes)
     b = streams.replay(e, reqs, sizes)
+    e.ref_oracle = o
     return a, b, e
 
 
+@pytest.mark.parametrize("lsd_only", [False, True], ids=["bucketed", "lsd"])
 @pytest.mark.parametrize("local_cache", [False, True])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_random_streams(seed, local_cache):
+def test_random_streams(seed, local_cache, lsd_only):
     reqs = make_stream(seed, 6000, t0=1_700_000_000 - 7 + seed * 3600 * 24 - 130)
     sizes = batch_sizes(reqs, np.random.default_rng(seed + 100), 1500)
-    (ost, othr), (gst, gthr), _ = run_both(reqs, sizes, local_cache)
-    streams.assert_same(ost, othr, gst, gthr, f"seed={seed} local={local_cache}")
+    (ost, othr), (gst, gthr), _ = run_both(reqs, sizes, local_cache, lsd_only=lsd_only)
+    streams.assert_same(ost, othr, gst, gthr, f"seed={seed} local={local_cache} lsd={lsd_only}")
 
 
 @pytest.mark.parametrize("sort_bits", [8, 16, 64])
 def test_sort_prefix_widths_and_resort(sort_bits):
-    """Narrow sort prefixes make different keys share a sorted run; the engine must detect
-    it and re-sort on the full fingerprint (resorts > 0 at 8 bits) with identical output."""
+    """Narrow sort prefixes make different keys share a sorted run; the LSD pipeline must
+    detect it and re-sort on the full fingerprint (resorts > 0 at 8 bits) with identical output."""
     reqs = make_stream(11, 4000, t0=1_600_000_000, keyspace=400)
     sizes = batch_sizes(reqs, np.random.default_rng(5), 2000)
-    (ost, othr), (gst, gthr), eng = run_both(reqs, sizes, True, sort_bits=sort_bits)
+    (ost, othr), (gst, gthr), eng = run_both(reqs, sizes, True, sort_bits=sort_bits, lsd_only=True)
     streams.assert_same(ost, othr, gst, gthr, f"sort_bits={sort_bits}")
     if sort_bits == 8:
         assert eng.stats()["resorts"] > 0
@@ -115,8 +119,90 @@ def test_hot_key_long_segments():
         else:
             reqs.append(("hot", [[("k", f"c{i % 997}")]], [1 + 4], 1, t))
     for lc in (False, True):
-        (ost, othr), (gst, gthr), _ = run_both(reqs, [len(reqs)], lc)
-        streams.assert_same(ost, othr, gst, gthr, f"hot local={lc}")
+        for lsd in (False, True):
+            (ost, othr), (gst, gthr), _ = run_both(reqs, [len(reqs)], lc, lsd_only=lsd)
+            streams.assert_same(ost, othr, gst, gthr, f"hot local={lc} lsd={lsd}")
+
+
+def hot_stream(n_batches, per_batch, t0, rule_of=None, seed=0):
+    """Batches dominated by a few keys (each >= HOT_MIN_SEG per batch, one beyond a 4096
+    hot chunk), plus a cold tail; `now` advances 1 s per batch so SECOND keys roll over
+    and alternate window parity."""
+    rng = np.random.default_rng(seed)
+    reqs, sizes = [], []
+    for b in range(n_batches):
+        t = t0 + b
+        for i in range(per_batch):
+            x = rng.random()
+            if x < 0.45:
+                k, r = "h0", 2            # SECOND L=10
+            elif x < 0.55:
+                k, r = "h1", 3 + 4 * 1    # MINUTE L=40
+            elif x < 0.62:
+                k, r = f"h{2 + int(rng.integers(0, 6))}", 1 + 4 * 2  # HOUR L=3
+            else:
+                k, r = f"c{int(rng.integers(0, 5000))}", 3 + 4 * 3   # DAY L=40
+            if rule_of is not None:
+                r = rule_of(b, k, r)
+            reqs.append(("hs", [[("k", k)]], [r], int(rng.integers(0, 4)), t))
+        sizes.append(per_batch)
+    return reqs, sizes
+
+
+@pytest.mark.parametrize("local_cache", [False, True])
+def test_hot_set_across_batches(local_cache):
+    """The bucketed pipeline learns hot keys from one batch and gives them their own
+    buckets in the next; results stay bit-exact as they roll over windows."""
+    reqs, sizes = hot_stream(6, 12000, t0=1_700_000_000 - 3, seed=local_cache)
+    (ost, othr), (gst, gthr), eng = run_both(reqs, sizes, local_cache)
+    streams.assert_same(ost, othr, gst, gthr, f"hotset local={local_cache}")
+    s = eng.stats()
+    assert s["hot_keys"] >= 2, s  # h0, h1 always; h2..h7 hover around HOT_MIN_SEG
+    # only the first batch (no hot set yet, one key > 1024 descriptors in an MSD bucket)
+    assert s["lsd_fallbacks"] == 1, s
+    assert s["live_slots_hint"] == eng.ref_oracle.num_keys(), s  # one insert per (key, window)
+
+
+def test_hot_key_changes_rule():
+    """A hot key submitted under a second rule in a later batch sends that batch to the
+    LSD pipeline (before anything touches the table); results stay bit-exact."""
+    def rule_of(b, k, r):
+        return 1 if (b == 3 and k == "h0") else r   # same unit (SECOND), other limit
+    reqs, sizes = hot_stream(5, 8000, t0=1_700_000_100, rule_of=rule_of, seed=7)
+    (ost, othr), (gst, gthr), eng = run_both(reqs, sizes, True)
+    streams.assert_same(ost, othr, gst, gthr, "hot rule change")
+    assert eng.stats()["lsd_fallbacks"] >= 1
+
+
+def test_oversized_bucket_falls_back():
+    """More descriptors than the 2048 MSD buckets hold (1024 each) go to the LSD pipeline."""
+    b = workload.config2_batch(0, d=2_400_000, N=3_000_000)
+    o = oracle.Oracle(near_limit_ratio=0.8, local_cache=True)
+    o.load_rules(workload.CONFIG2_RULES)
+    e = hiprl.Engine(log2_slots=(23, 12, 12, 12), local_cache=True, max_batch_desc=b.n_desc, max_batch_req=b.n_desc,
+                     max_blob_bytes=int(b.blob.shape[0]) + 64)
+    e.load_rules(workload.CONFIG2_RULES)
+    ost, othr = o.submit(b, threads=8)
+    gst, gthr = e.submit(b)
+    streams.assert_same(ost, othr, gst, gthr, "oversized bucket")
+    assert e.stats()["lsd_fallbacks"] == 1
+
+
+def test_config3_zipf_batches():
+    """The benchmark workload (config 3: 1e8 keys Zipf(1.1), three units) at 1M descriptors
+    per batch, three consecutive batches, bit-exact against the oracle."""
+    d = 1_000_000
+    o = oracle.Oracle(near_limit_ratio=0.8, local_cache=True)
+    o.load_rules(workload.CONFIG3_RULES)
+    e = hiprl.Engine(log2_slots=(22, 24, 25, 12), local_cache=True, max_batch_desc=d, max_batch_req=d, max_blob_bytes=24 * d)
+    e.load_rules(workload.CONFIG3_RULES)
+    for k in range(3):
+        b = workload.config3_batch(k, d=d)
+        ost, othr = o.submit(b, threads=8)
+        gst, gthr = e.submit(b)
+        streams.assert_same(ost, othr, gst, gthr, f"config3 batch {k}")
+    s = e.stats()
+    assert s["hot_keys"] > 0 and s["lsd_fallbacks"] == 1, s  # batch 0 learns the hot set
 
 
 def test_window_rollover_across_batches():
