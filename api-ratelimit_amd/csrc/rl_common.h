@@ -161,7 +161,7 @@ constexpr int HOT_MAX = 256;              // hot prefixes per batch
 constexpr int HOT_SLOTS = 512;            // open-addressing table of HotEntry (device + LDS copy)
 constexpr int HOT_BUCKETS = 2 * HOT_MAX;  // hot prefix x window parity
 constexpr int MSD_BITS = 11;
-constexpr int MSD_BUCKETS = 1 << MSD_BITS;   // region(3) | 8 fingerprint bits
+constexpr int MSD_BUCKETS = 1 << MSD_BITS;   // 11 fingerprint bits below the region bits
 constexpr int NBUCKETS = HOT_BUCKETS + MSD_BUCKETS + 1;
 constexpr uint32_t NIL_BUCKET = NBUCKETS - 1;
 constexpr int BUCKET_CAP = 1024;          // max descriptors in one MSD bucket on the fast path
@@ -169,14 +169,29 @@ constexpr int BG_RANGE = 1024;            // k_bgroup: MSD buckets whose start l
 constexpr int BG_MAX = BG_RANGE + BUCKET_CAP;
 constexpr int V2_TILE = 4096;             // k_fp2 / k_bscatter arrival tile
 constexpr int HOT_CHUNK = 4096;           // k_bgroup hot-region chunk
-constexpr uint32_t HOT_MIN_SEG = 128;     // segments at least this long become hot candidates
+constexpr uint32_t HOT_MIN_SEG = 128;     // a new key joins the hot set with at least this many descriptors
+constexpr uint32_t HOT_CAND_MIN = 64;     // segments at least this long are reported (hot keys stay hot)
 constexpr int CAND_MAX = 1024;
 constexpr int CAND_CTR = 30;  // EngineCtl::tile_ctr[CAND_CTR][0] counts hot candidates (own line)
 
 struct __attribute__((aligned(16))) HotCand {
   uint64_t a, b;
-  uint32_t unit, rule, count, first_idx;
+  uint32_t unit, rule, count, first_idx;  // first_idx ~0: (a, b, unit) already filled in
 };
+
+// Per-batch state of one hot bucket (one key): identity from k_fp2, table slot and base
+// from k_bscan, first over-limit position from k_bscatter; k_bgroup decides from it.
+struct __attribute__((aligned(16))) HotBucket {
+  uint64_t key;    // sort key (identical writes from every tile that sees the bucket)
+  uint64_t fp_lo;
+  uint64_t base;   // counter before this batch
+  uint64_t slot;   // Slot* of the key; 0 = no table update (empty bucket or error)
+  uint32_t gen;    // window generation
+  uint32_t flags;  // HB_FROZEN_PRE: the local cache already holds the key
+  uint32_t jpos;   // first bucket position whose INCRBY reply exceeds the limit (~0: none)
+  uint32_t pad;
+};
+constexpr uint32_t HB_FROZEN_PRE = 1u;
 
 constexpr int RADIX_BITS = 8;
 constexpr int RADIX = 1 << RADIX_BITS;

@@ -40,14 +40,17 @@ uint32_t v2_msd_wgs(uint32_t n);
 uint32_t v2_hot_wgs(uint32_t n);
 void launch_fp2(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, const HotEntry*, uint64_t*,
                 ItemRec*, uint16_t*, uint32_t*, rl_status*, uint32_t*, uint32_t*, uint32_t*, unsigned long long*,
-                EngineCtl*);
+                HotBucket*, EngineCtl*);
 void launch_bscan(hipStream_t, const uint32_t*, const unsigned long long*, uint32_t, uint32_t*, unsigned long long*,
-                  uint32_t*, const uint32_t*, EngineCtl*);
-void launch_bscatter(hipStream_t, const uint64_t*, const uint16_t*, const uint32_t*, uint32_t, const uint32_t*,
-                     const uint32_t*, const unsigned long long*, uint64_t*, uint32_t*, uint64_t*, EngineCtl*);
-void launch_bgroup(hipStream_t, const uint64_t*, const uint32_t*, const uint64_t*, const ItemRec*, const uint32_t*,
-                   uint32_t, uint64_t*, SortedRec*, uint32_t*, EngineCtl*);
-void launch_cand_state(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, const EngineCtl*);
+                  uint32_t*, const uint32_t*, const HotEntry*, HotBucket*, const TableDesc&, HotCand*, EngineCtl*);
+void launch_bscatter(hipStream_t, const uint64_t*, const ItemRec*, const uint16_t*, const uint32_t*, uint32_t,
+                     const uint32_t*, const uint32_t*, const unsigned long long*, uint64_t*, ItemRec*, uint64_t*,
+                     uint32_t*, HotBucket*, const DevRule*, int, EngineCtl*);
+void launch_bgroup(hipStream_t, const uint64_t*, const ItemRec*, const uint64_t*, const uint32_t*, uint32_t,
+                   uint64_t*, SortedRec*, uint32_t*, const ItemRec*, const DevRule*, const TableDesc&, int, SegInfo*,
+                   const HotBucket*, rl_status*, uint32_t*, HotCand*, EngineCtl*);
+void launch_cand_state(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, const uint32_t*, uint32_t,
+                       EngineCtl*);
 void launch_decide(hipStream_t, const SortedRec*, const SegInfo*, const DevRule*, uint32_t, rl_status*, uint32_t*,
                    EngineCtl*);
 }  // namespace rlhip
@@ -120,7 +123,10 @@ struct rl_engine {
   unsigned long long* hoff = nullptr;   // [tile][HOT_BUCKETS]
   uint32_t* btotal = nullptr;           // [NBUCKETS]
   uint64_t* bP = nullptr;               // hot descriptors: INCRBY prefix, bucket order
-  HotEntry* d_hot = nullptr;            // device hot-key table (HOT_SLOTS)
+  ItemRec* brec = nullptr;              // arrival records in bucket order (pad = descriptor index)
+  uint32_t* bbase = nullptr;            // [NBUCKETS + 1] bucket start positions
+  HotEntry* d_hot = nullptr;            // device hot-key table (HOT_SLOTS) + list by hot index (HOT_MAX)
+  HotBucket* hbk = nullptr;             // per hot bucket batch state (HOT_BUCKETS)
   HotCand* d_cand = nullptr;            // hot-set candidates (CAND_MAX)
   HotCand* h_cand = nullptr;            // pinned copy
   std::vector<HotKey> hot;              // current hot-key set (index = hot idx)
@@ -230,24 +236,24 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
       int rc = upload_hot();
       if (rc) return rc;
     }
+    const int lc = cfg.local_cache ? 1 : 0;
     timed(KT_FP2, [&] {
       launch_fp2(stream, b, d_rules, n_rules, cfg.hash_seed, d_hot, keys_orig, recs, bkt, hbuf, out, thr, fp_part,
-                 tcount, thsum, ctl);
+                 tcount, thsum, hbk, ctl);
     });
-    timed(KT_BSCAN, [&] { launch_bscan(stream, tcount, thsum, n, toff, hoff, btotal, fp_part, ctl); });
+    timed(KT_BSCAN, [&] {
+      launch_bscan(stream, tcount, thsum, n, toff, hoff, btotal, fp_part, d_hot + HOT_SLOTS, hbk, tab, d_cand, ctl);
+    });
     timed(KT_BSCATTER, [&] {
-      launch_bscatter(stream, keys_orig, bkt, hbuf, n, btotal, toff, hoff, keys_a, vals_a, bP, ctl);
+      launch_bscatter(stream, keys_orig, recs, bkt, hbuf, n, btotal, toff, hoff, keys_a, brec, bP, bbase, hbk, d_rules,
+                      lc, ctl);
     });
     timed(KT_BGROUP, [&] {
-      launch_bgroup(stream, keys_a, vals_a, bP, recs, btotal, n, keys_b, srec, tile_heads, ctl);
+      launch_bgroup(stream, keys_a, brec, bP, bbase, n, keys_b, srec, tile_heads, recs, d_rules, tab, lc, seg, hbk,
+                    out, thr, d_cand, ctl);
     });
     const uint32_t n_heads = v2_msd_wgs(n) + v2_hot_wgs(n);
-    timed(KT_LEADER, [&] {
-      launch_leader(stream, keys_b, srec, recs, d_rules, n, tab, cfg.local_cache ? 1 : 0, seg, tile_heads, n_heads,
-                    d_cand, ctl);
-    });
-    timed(KT_DECIDE, [&] { launch_decide(stream, srec, seg, d_rules, n, out, thr, ctl); });
-    timed(KT_CAND, [&] { launch_cand_state(stream, b, d_rules, cfg.hash_seed, d_cand, ctl); });
+    timed(KT_CAND, [&] { launch_cand_state(stream, b, d_rules, cfg.hash_seed, d_cand, tile_heads, n_heads, ctl); });
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
@@ -327,7 +333,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
                   scan_tiles(n), d_cand, ctl);
   });
   timed(KT_DECIDE, [&] { launch_decide(stream, srec, seg, d_rules, n, out, thr, ctl); });
-  timed(KT_CAND, [&] { launch_cand_state(stream, b, d_rules, cfg.hash_seed, d_cand, ctl); });
+  timed(KT_CAND, [&] { launch_cand_state(stream, b, d_rules, cfg.hash_seed, d_cand, nullptr, 0, ctl); });
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
   e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
@@ -336,9 +342,10 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   return 0;
 }
 
-// Upload the hot-key set as an open-addressing table (slot = a>>40 mod HOT_SLOTS).
+// Upload the hot-key set: an open-addressing table (slot = a>>40 mod HOT_SLOTS) followed by
+// the entries in hot-index order.
 int rl_engine::upload_hot() {
-  std::vector<HotEntry> t(HOT_SLOTS);
+  std::vector<HotEntry> t(HOT_SLOTS + HOT_MAX);
   for (auto& x : t) {
     x.a = x.b = 0;
     x.unit = x.rule = 0;
@@ -346,20 +353,24 @@ int rl_engine::upload_hot() {
     x.pad = 0;
   }
   for (size_t i = 0; i < hot.size(); ++i) {
-    uint32_t s = (uint32_t)(hot[i].a >> 40) & (HOT_SLOTS - 1);
+    HotEntry he;
+    he.a = hot[i].a;
+    he.b = hot[i].b;
+    he.unit = hot[i].unit;
+    he.rule = hot[i].rule;
+    he.idx = (uint32_t)i;
+    he.pad = 0;
+    uint32_t s = (uint32_t)(he.a >> 40) & (HOT_SLOTS - 1);
     while (t[s].idx != 0xFFFFFFFFu) s = (s + 1) & (HOT_SLOTS - 1);
-    t[s].a = hot[i].a;
-    t[s].b = hot[i].b;
-    t[s].unit = hot[i].unit;
-    t[s].rule = hot[i].rule;
-    t[s].idx = (uint32_t)i;
+    t[s] = he;
+    t[HOT_SLOTS + i] = he;
   }
-  // pinned bounce buffer: h_cand is reused (large enough: CAND_MAX * 32 B >= HOT_SLOTS * 32 B)
-  static_assert(sizeof(HotCand) * CAND_MAX >= sizeof(HotEntry) * HOT_SLOTS, "bounce buffer");
+  // pinned bounce buffer: h_cand is reused (it is idle between batches)
+  static_assert(sizeof(HotCand) * CAND_MAX >= sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX), "bounce buffer");
   hipError_t e = hipStreamSynchronize(stream);
   if (e == hipSuccess) {
-    memcpy(h_cand, t.data(), sizeof(HotEntry) * HOT_SLOTS);
-    e = hipMemcpyAsync(d_hot, h_cand, sizeof(HotEntry) * HOT_SLOTS, hipMemcpyHostToDevice, stream);
+    memcpy(h_cand, t.data(), sizeof(HotEntry) * t.size());
+    e = hipMemcpyAsync(d_hot, h_cand, sizeof(HotEntry) * t.size(), hipMemcpyHostToDevice, stream);
   }
   if (e != hipSuccess) return hip_fail(e, "upload hot set");
   hot_dirty = false;
@@ -367,37 +378,62 @@ int rl_engine::upload_hot() {
   return 0;
 }
 
-// Rebuild the hot-key set from this batch's long segments (k_leader candidates with their
-// prefix state from k_cand_state). Keys are (prefix state, unit); two windows of one
-// prefix merge. Keep the HOT_MAX longest with at least HOT_MIN_SEG descriptors.
+// Maintain the hot-key set from this batch's long segments (candidates with their prefix
+// state). Keys are (prefix state, unit); the two windows of one prefix merge; a prefix seen
+// under two rules is not bucketable. Hysteresis keeps the set (and its upload) stable on a
+// steady skewed stream: a hot key stays while it has >= HOT_CAND_MIN descriptors per batch,
+// a new key joins with >= HOT_MIN_SEG while there is room.
 void rl_engine::update_hot(uint32_t n_cand) {
   n_cand = n_cand < (uint32_t)CAND_MAX ? n_cand : (uint32_t)CAND_MAX;
-  std::vector<HotKey> next;
-  for (uint32_t i = 0; i < n_cand; ++i) {
-    const HotCand& c = h_cand[i];
-    bool merged = false;
-    for (auto& x : next)
-      if (x.a == c.a && x.b == c.b && x.unit == c.unit) {
-        x.count += c.count;
-        if (x.rule != c.rule) x.count = 0;  // two rules on one prefix: not bucketable
-        merged = true;
-        break;
-      }
-    if (!merged) next.push_back(HotKey{c.a, c.b, c.unit, c.rule, c.count});
-  }
-  next.erase(std::remove_if(next.begin(), next.end(), [](const HotKey& x) { return x.count < HOT_MIN_SEG; }),
-             next.end());
-  std::sort(next.begin(), next.end(), [](const HotKey& x, const HotKey& y) { return x.count > y.count; });
-  if (next.size() > (size_t)HOT_MAX) next.resize(HOT_MAX);
-  // canonical order, so an unchanged set (the steady state of a skewed stream) costs no upload
   auto ident_less = [](const HotKey& x, const HotKey& y) {
     return x.a != y.a ? x.a < y.a : x.b != y.b ? x.b < y.b : x.unit < y.unit;
   };
-  std::sort(next.begin(), next.end(), ident_less);
-  bool same = next.size() == hot.size();
-  for (size_t i = 0; same && i < next.size(); ++i)
-    same = next[i].a == hot[i].a && next[i].b == hot[i].b && next[i].unit == hot[i].unit && next[i].rule == hot[i].rule;
-  if (!same) {
+  auto same_ident = [](const HotKey& x, const HotKey& y) { return x.a == y.a && x.b == y.b && x.unit == y.unit; };
+  std::vector<HotKey> agg;
+  agg.reserve(n_cand);
+  for (uint32_t i = 0; i < n_cand; ++i) {
+    const HotCand& c = h_cand[i];
+    agg.push_back(HotKey{c.a, c.b, c.unit, c.rule, c.count});
+  }
+  std::sort(agg.begin(), agg.end(), ident_less);
+  std::vector<HotKey> merged;  // count 0 marks a rule conflict
+  for (const HotKey& x : agg) {
+    if (!merged.empty() && same_ident(merged.back(), x)) {
+      HotKey& m = merged.back();
+      if (m.rule != x.rule) m.count = 0, m.rule = 0xFFFFFFFFu;
+      else if (m.rule != 0xFFFFFFFFu) m.count += x.count;
+    } else {
+      merged.push_back(x);
+    }
+  }
+  auto find = [&](const HotKey& k) -> const HotKey* {
+    auto it = std::lower_bound(merged.begin(), merged.end(), k, ident_less);
+    return (it != merged.end() && same_ident(*it, k)) ? &*it : nullptr;
+  };
+  std::vector<HotKey> next;
+  bool changed = false;
+  for (const HotKey& x : hot) {
+    const HotKey* m = find(x);
+    if (m && m->rule == x.rule && m->count >= HOT_CAND_MIN) next.push_back(*m);
+    else changed = true;
+  }
+  if (next.size() < (size_t)HOT_MAX) {
+    std::vector<HotKey> cur(hot);
+    std::sort(cur.begin(), cur.end(), ident_less);
+    std::vector<HotKey> fresh;
+    for (const HotKey& m : merged) {
+      if (m.count < HOT_MIN_SEG || m.rule == 0xFFFFFFFFu) continue;
+      auto it = std::lower_bound(cur.begin(), cur.end(), m, ident_less);
+      if (it == cur.end() || !same_ident(*it, m)) fresh.push_back(m);
+    }
+    std::sort(fresh.begin(), fresh.end(), [](const HotKey& x, const HotKey& y) { return x.count > y.count; });
+    for (const HotKey& m : fresh) {
+      if (next.size() >= (size_t)HOT_MAX) break;
+      next.push_back(m);
+      changed = true;
+    }
+  }
+  if (changed) {
     hot = std::move(next);
     hot_dirty = true;
   }
@@ -409,10 +445,12 @@ int rl_engine::finish() {
   hipError_t e = hipStreamSynchronize(stream);
   if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
   uint32_t errs = h_ctl->err;
+  bool fell_back = false;
   if ((errs & ERR_V2_FALLBACK) && !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME))) {
     // The bucketed pipeline refused the batch before touching the table (oversized
     // bucket or a hot prefix with a second rule): run it on the LSD pipeline.
     ++st.lsd_fallbacks;
+    fell_back = true;
     int rc = run_pipeline(dev_batch, pend_out_dev, pend_thr_dev, MODE_LSD);
     if (rc) return rc;
     if (host_path && (rc = enqueue_d2h()) != 0) return rc;
@@ -448,7 +486,10 @@ int rl_engine::finish() {
   if (errs & ERR_TABLE_FULL) return fail(RL_ENOSPC, "counter table region full (raise log2_slots)");
   if (errs & ERR_SPIN) return fail(RL_EDEVICE, "device look-back spin limit exceeded");
   if (errs & ERR_NEED_RESORT) return fail(RL_EDEVICE, "full-fingerprint re-sort still found a mixed run");
-  if (!(cfg.flags & RL_CFG_LSD_ONLY)) update_hot(h_ctl->tile_ctr[CAND_CTR][0]);
+  // Hot-set maintenance costs host time between batches: every batch while the set is
+  // empty or after a fallback, else every 8th batch (a skewed stream's head moves slowly).
+  if (!(cfg.flags & RL_CFG_LSD_ONLY) && (hot.empty() || fell_back || (st.batches & 7) == 0))
+    update_hot(h_ctl->tile_ctr[CAND_CTR][0]);
   last_unique = h_ctl->n_segments;
   last_n = dev_batch.n_desc;
   last_req = dev_batch.n_req;
@@ -556,7 +597,10 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     chk(hipMalloc(&e->hoff, T * HOT_BUCKETS * 8));
     chk(hipMalloc(&e->btotal, (NBUCKETS + 1) * 4));
     chk(hipMalloc(&e->bP, N * 8 + 64));
-    chk(hipMalloc(&e->d_hot, sizeof(HotEntry) * HOT_SLOTS));
+    chk(hipMalloc(&e->brec, N * sizeof(ItemRec)));
+    chk(hipMalloc(&e->bbase, (NBUCKETS + 1) * 4));
+    chk(hipMalloc(&e->d_hot, sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX)));
+    chk(hipMalloc(&e->hbk, sizeof(HotBucket) * HOT_BUCKETS));
     chk(hipMalloc(&e->d_cand, sizeof(HotCand) * CAND_MAX));
     chk(hipHostMalloc(&e->h_cand, sizeof(HotCand) * CAND_MAX, hipHostMallocDefault));
     e->hot_dirty = true;  // upload the empty table before the first batch
@@ -608,7 +652,10 @@ void rl_destroy(rl_engine* e) {
   hipFree(e->hoff);
   hipFree(e->btotal);
   hipFree(e->bP);
+  hipFree(e->brec);
+  hipFree(e->bbase);
   hipFree(e->d_hot);
+  hipFree(e->hbk);
   hipFree(e->d_cand);
   hipHostFree(e->h_cand);
 

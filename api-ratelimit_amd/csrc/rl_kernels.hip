@@ -21,6 +21,7 @@
 
 #include "rl_common.h"
 #include "rl_device.h"
+#include "rl_decide.h"
 
 namespace rlhip {
 
@@ -672,8 +673,6 @@ __global__ __launch_bounds__(256) void k_scan(const uint64_t* __restrict__ skeys
 // ---------------------------------------------------------------------------
 // k_leader — one thread per unique key (segment tail).
 // ---------------------------------------------------------------------------
-constexpr uint32_t MAX_PROBE = 4096;
-
 __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ skeys, const SortedRec* __restrict__ srec,
                                                 const ItemRec* __restrict__ recs, const DevRule* __restrict__ rules,
                                                 uint32_t n_all, TableDesc tab, int local_cache,
@@ -701,129 +700,9 @@ __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ ske
   const SortedRec tail = srec[j];
   const uint32_t hp = tail.head & ~HEAD_MIXED_RULE;
   const bool mixed_rule = (tail.head & HEAD_MIXED_RULE) != 0;
-  if (j - hp + 1 >= HOT_MIN_SEG && !mixed_rule) {
-    // long segment: a hot-set candidate for the next batch (v2 bucketing)
-    const uint32_t c = atomicAdd(&ctl->tile_ctr[CAND_CTR][0], 1u);
-    if (c < (uint32_t)CAND_MAX) {
-      HotCand hc;
-      hc.a = 0;
-      hc.b = 0;
-      hc.unit = 0;
-      hc.rule = tail.rule;
-      hc.count = j - hp + 1;
-      hc.first_idx = srec[hp].idx;
-      cand[c] = hc;
-    }
-  }
-  const uint64_t key = skeys[j];
-  const ItemRec rec = recs[tail.idx];
-  const uint32_t region = key_region(key);
-  // Two window generations of one region in one batch must be adjacent (a batch may
-  // straddle one window boundary); otherwise the older would read as empty.
-  if (ctl->gen_max[region] - ctl->gen_min[region] > 1u) {
-    atomicOr(&ctl->err, ERR_WINDOW_SPAN);
-    return;
-  }
-  const uint32_t lg = tab.region_log2[region];
-  const uint64_t mask = (1ull << lg) - 1ull;
-  Slot* rbase = tab.slots + tab.region_base[region];
-  uint64_t pos = (key << 3) >> (64 - lg);  // top lg bits below the region bits
-  const uint32_t G = rec.gen;
-  const uint32_t tag = (uint32_t)rec.fp_lo;
-  const uint32_t lohi = (uint32_t)(rec.fp_lo >> 32);
-  Slot* slot = nullptr;
-  bool existed = false;
-  for (uint32_t probe = 0; probe < MAX_PROBE;) {
-    Slot* s = rbase + (pos & mask);
-    // ctrl by an L1-bypassing atomic load (it may be CASed concurrently); the identity
-    // words in the same load burst (written by earlier batches, or by a concurrent
-    // claimer of a different key, which can never match).
-    const uint64_t c = ld_relaxed64(&s->ctrl);
-    const uint64_t skey = s->key;
-    const uint32_t slohi = s->fp_lo_hi;
-    const uint32_t g = (uint32_t)c;
-    if (g == G && (uint32_t)(c >> 32) == tag && skey == key && slohi == lohi) {
-      slot = s;
-      existed = true;
-      break;
-    }
-    if (g < G) {
-      // empty for this window generation: claim it
-      const unsigned long long want = ((unsigned long long)tag << 32) | G;
-      const unsigned long long old = atomicCAS((unsigned long long*)&s->ctrl, (unsigned long long)c, want);
-      if (old == c) {
-        slot = s;
-        break;
-      }
-      continue;  // lost the race: re-examine this slot
-    }
-    ++pos;
-    ++probe;
-  }
-  if (!slot) {
-    atomicOr(&ctl->err, ERR_TABLE_FULL);
-    return;
-  }
-  uint64_t base = 0;
-  bool frozen_pre = false;
-  if (existed) {
-    base = slot->count;
-    frozen_pre = (slot->flags & SLOT_FROZEN) != 0;
-  } else {
-    slot->key = key;
-    slot->fp_lo_hi = lohi;
-  }
-  {  // new-key count (engine stats): one atomic per wave, spread over INS_LINES lines
-    const uint64_t ins = __ballot(!existed);
-    if (ins && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1))
-      atomicAdd(&ctl->tile_ctr[INS_CTR0 + ((blockIdx.x * 4 + (threadIdx.x >> 6)) & (INS_LINES - 1))][0],
-                (uint32_t)__popcll(ins));
-  }
-
-  uint32_t freeze = SEG_NO_FREEZE;
-  uint64_t final_count = base + tail.P;
-  if (frozen_pre) {
-    // every descriptor is a local-cache hit: no INCRBY (fixed_cache_impl.go:61-65)
-    freeze = SEG_FROZEN_BEFORE;
-    final_count = base;
-  } else if (local_cache) {
-    // first descriptor whose INCRBY reply exceeds its limit (base_limiter.go:88,94-106);
-    // all later requests of this key are local-cache hits.
-    uint32_t jstar = 0xFFFFFFFFu;
-    const uint32_t L0 = rules[tail.rule].L;
-    if (!mixed_rule && base + tail.P < (1ull << 32)) {
-      // after = base + P is strictly increasing in the segment: binary search.
-      if ((uint64_t)(uint32_t)(base + tail.P) > L0) {
-        uint32_t lo_i = hp, hi_i = j;
-        while (lo_i < hi_i) {
-          const uint32_t mid = lo_i + (hi_i - lo_i) / 2;
-          if (base + srec[mid].P > (uint64_t)L0) hi_i = mid; else lo_i = mid + 1;
-        }
-        jstar = lo_i;
-      }
-    } else {
-      for (uint32_t k = hp; k <= j; ++k) {
-        const SortedRec r = srec[k];
-        if ((uint32_t)(base + r.P) > rules[r.rule].L) { jstar = k; break; }
-      }
-    }
-    if (jstar != 0xFFFFFFFFu) {
-      const uint32_t rstar = srec[jstar].req;
-      uint32_t last = jstar;
-      while (last < j && srec[last + 1].req == rstar) ++last;
-      freeze = rstar;
-      final_count = base + srec[last].P;
-    }
-  }
-  slot->count = final_count;
-  if (freeze != SEG_NO_FREEZE && freeze != SEG_FROZEN_BEFORE) slot->flags = slot->flags | SLOT_FROZEN;
-  if (!existed && freeze == SEG_NO_FREEZE) slot->flags = 0;
-  if (!existed && freeze != SEG_NO_FREEZE && freeze != SEG_FROZEN_BEFORE) slot->flags = SLOT_FROZEN;
-  SegInfo si;
-  si.base = base;
-  si.freeze = freeze;
-  si.pad = 0;
-  seg[hp] = si;
+  if (j - hp + 1 >= HOT_CAND_MIN && !mixed_rule)  // hot-set candidate for the bucketed pipeline
+    emit_candidate(ctl, cand, tail.rule, j - hp + 1, srec[hp].idx);
+  leader_segment(hp, j, tail, mixed_rule, skeys, srec, recs, rules, tab, local_cache, seg, ctl);
 }
 
 // ---------------------------------------------------------------------------
@@ -842,47 +721,7 @@ __global__ __launch_bounds__(256) void k_decide(const SortedRec* __restrict__ sr
   const uint32_t n = n_all - ctl->n_nil;  // written by k_fingerprint (earlier launch)
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
-  const SortedRec r = srec[j];
-  const SegInfo si = seg[r.head & ~HEAD_MIXED_RULE];
-  const DevRule R = rules[r.rule];
-  const uint32_t h = r.h;
-  const uint32_t reset = R.div - (uint32_t)r.now_mod;  // div - now % div
-  rl_status st;
-  st.reset_s = reset;
-  st.over_limit_delta = 0;
-  st.near_limit_delta = 0;
-  const bool local_hit = si.freeze == SEG_FROZEN_BEFORE || (si.freeze != SEG_NO_FREEZE && r.req > si.freeze);
-  uint32_t throttle = 0;
-  if (local_hit) {
-    st.code_flags = RL_CODE_OVER_LIMIT | ((RL_FLAG_HAS_LIMIT | RL_FLAG_LOCAL_CACHE_HIT) << 8);
-    st.limit_remaining = 0;
-    st.over_limit_delta = h;
-  } else {
-    const uint32_t after = (uint32_t)(si.base + r.P);
-    const uint32_t before = after - h;
-    const uint32_t L = R.L, near = R.near;
-    if (after > L) {
-      st.code_flags = RL_CODE_OVER_LIMIT | (RL_FLAG_HAS_LIMIT << 8);
-      st.limit_remaining = 0;
-      if (before >= L) {
-        st.over_limit_delta = h;
-      } else {
-        st.over_limit_delta = after - L;
-        st.near_limit_delta = L - (near > before ? near : before);
-      }
-    } else {
-      st.code_flags = RL_CODE_OK | (RL_FLAG_HAS_LIMIT << 8);
-      st.limit_remaining = L - after;
-      if (after > near) {
-        const uint32_t millis = reset * 1000u;  // uint32(end - now) * 1000
-        const uint32_t calls = (L - after) > 1u ? (L - after) : 1u;
-        throttle = millis / calls;
-        st.near_limit_delta = before >= near ? h : after - near;
-      }
-    }
-  }
-  out[r.idx] = st;
-  if (throttle) atomicMax(&req_thr[r.req], throttle);
+  decide_pos(j, srec, seg, rules, out, req_thr);
 }
 
 // ---------------------------------------------------------------------------

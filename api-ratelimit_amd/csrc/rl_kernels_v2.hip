@@ -21,8 +21,19 @@
 
 #include "rl_common.h"
 #include "rl_device.h"
+#include "rl_decide.h"
 
 namespace rlhip {
+
+#ifdef RL_STAMPS
+// Diagnostic build only: per-block phase timestamps of k_bgroup (s_memrealtime, 100 MHz).
+__device__ uint64_t g_bg_stamps[2048][10];
+#define BSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < 2048) g_bg_stamps[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define BSTAMPV(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 2048) g_bg_stamps[blockIdx.x][k] = (v); } while (0)
+#else
+#define BSTAMP(k) do { } while (0)
+#define BSTAMPV(k, v) do { } while (0)
+#endif
 
 // ---------------------------------------------------------------------------
 // k_fp2
@@ -49,13 +60,88 @@ RL_DEV uint32_t hot_lookup(const HotEntry* sh_hot, uint64_t a, uint64_t b, uint3
   return 0xFFFFFFFFu;
 }
 
-__global__ __launch_bounds__(256) void k_fp2(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
-                                             uint64_t seed, const HotEntry* __restrict__ hot,
-                                             uint64_t* __restrict__ keys_orig, ItemRec* __restrict__ recs,
-                                             uint16_t* __restrict__ bkt, uint32_t* __restrict__ hbuf,
-                                             rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
-                                             uint32_t* __restrict__ fpart, uint32_t* __restrict__ tcount,
-                                             unsigned long long* __restrict__ thsum, EngineCtl* ctl) {
+constexpr int V2_THREADS = 1024;                 // k_fp2 / k_bscatter: 16 waves per tile
+constexpr int V2_WAVES = V2_THREADS / 64;
+constexpr int V2_ROUNDS = V2_TILE / V2_THREADS;  // 4 rounds of 64 per wave
+constexpr uint32_t BKT_SENTINEL = 4095;          // past-the-end items (sorts last in 12 bits)
+
+// Lanes of this wave holding the same 12-bit value (among `valid` lanes).
+RL_DEV uint64_t match12(uint32_t d, bool valid) {
+  uint64_t m = __ballot(valid);
+#pragma unroll
+  for (int b = 0; b < 12; ++b) {
+    const bool bit = (d >> b) & 1u;
+    const uint64_t bal = __ballot(bit);
+    m &= bit ? bal : ~bal;
+  }
+  return m;
+}
+
+template <class T>
+RL_DEV T wave_incl_scan(T x) {
+  const uint32_t lane = __lane_id();
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const T y = __shfl_up(x, s, 64);
+    if (lane >= (uint32_t)s) x += y;
+  }
+  return x;
+}
+
+// Exclusive scan over a block of NT threads (one value each); sh_w holds NT/64 words.
+template <int NT>
+RL_DEV uint32_t block_excl_scan(uint32_t v, uint32_t* sh_w, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t incl = wave_incl_scan<uint32_t>(v);
+  if (lane == 63) sh_w[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    const uint32_t x = sh_w[w];
+    before += (uint32_t)w < wave ? x : 0u;
+    total += x;
+  }
+  __syncthreads();
+  return before + incl - v;
+}
+
+// Global bucket bases (exclusive scan of the NBUCKETS totals) into LDS, by NT threads.
+template <int NT>
+RL_DEV void bucket_bases(const uint32_t* __restrict__ btotal, uint32_t* s_base, uint32_t* sh_w) {
+  constexpr int PER = (NBUCKETS + NT - 1) / NT;
+  const uint32_t tid = threadIdx.x;
+  uint32_t v[PER], sum = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t b = tid * PER + k;
+    v[k] = b < (uint32_t)NBUCKETS ? btotal[b] : 0u;
+    sum += v[k];
+  }
+  uint32_t total;
+  uint32_t run = block_excl_scan<NT>(sum, sh_w, total);
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const uint32_t b = tid * PER + k;
+    if (b < (uint32_t)NBUCKETS) s_base[b] = run;
+    run += v[k];
+  }
+  if (tid == 0) s_base[NBUCKETS] = total;
+  __syncthreads();
+}
+
+// Tile histograms are stored bucket-major: [bucket][tile].
+__global__ __launch_bounds__(V2_THREADS) void k_fp2(DevBatch in, const DevRule* __restrict__ rules,
+                                                    uint32_t n_rules, uint64_t seed,
+                                                    const HotEntry* __restrict__ hot,
+                                                    uint64_t* __restrict__ keys_orig, ItemRec* __restrict__ recs,
+                                                    uint16_t* __restrict__ bkt, uint32_t* __restrict__ hbuf,
+                                                    rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
+                                                    uint32_t* __restrict__ fpart, uint32_t ntiles,
+                                                    uint32_t* __restrict__ tcount,
+                                                    unsigned long long* __restrict__ thsum,
+                                                    HotBucket* __restrict__ hb, EngineCtl* ctl) {
   __shared__ HotEntry sh_hot[HOT_SLOTS];
   __shared__ uint32_t sh_cnt[NBUCKETS];
   __shared__ unsigned long long sh_hs[HOT_BUCKETS];
@@ -63,9 +149,9 @@ __global__ __launch_bounds__(256) void k_fp2(DevBatch in, const DevRule* __restr
   __shared__ uint32_t sh_gmin[8], sh_gmax[8];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < HOT_SLOTS; i += 256) sh_hot[i] = hot[i];
-  for (int i = tid; i < NBUCKETS; i += 256) sh_cnt[i] = 0;
-  for (int i = tid; i < HOT_BUCKETS; i += 256) sh_hs[i] = 0;
+  for (int i = tid; i < HOT_SLOTS; i += V2_THREADS) sh_hot[i] = hot[i];
+  for (int i = tid; i < NBUCKETS; i += V2_THREADS) sh_cnt[i] = 0;
+  for (int i = tid; i < HOT_BUCKETS; i += V2_THREADS) sh_hs[i] = 0;
   if (tid < 8) { sh_gmin[tid] = 0; sh_gmax[tid] = 0; }
   if (tid == 0) { sh_nil = 0; sh_err = 0; }
   __syncthreads();
@@ -75,83 +161,105 @@ __global__ __launch_bounds__(256) void k_fp2(DevBatch in, const DevRule* __restr
   uint32_t gmin[8], gmax[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) { gmin[r] = 0xFFFFFFFFu; gmax[r] = 0; }
-  for (int k = 0; k < V2_TILE / 256; ++k) {
-    const uint32_t i = tile * V2_TILE + wave * (V2_TILE / 4) + k * 64 + lane;
-    if (i >= in.n_desc) break;
-    const uint32_t r = in.rule[i];
-    const uint32_t q = in.req_of[i];
-    const bool q_ok = q < in.n_req;
-    const int64_t now = q_ok ? in.now[q] : 0;
-    const uint32_t ha = q_ok ? in.hits[q] : 1u;
-    if (q_ok) {  // zero the ThrottleMillis of the requests this descriptor opens
-      const uint32_t pq = i == 0 ? 0u : in.req_of[i - 1];
-      const uint32_t first = i == 0 ? 0u : (pq < q ? pq + 1u : q + 1u);
-      for (uint32_t rr = first; rr <= q; ++rr) req_thr[rr] = 0;
-      if (i + 1 == in.n_desc)
-        for (uint32_t rr = q + 1; rr < in.n_req; ++rr) req_thr[rr] = 0;
-    }
-    ItemRec rec;
-    rec.rule = r;
-    rec.req = q;
-    rec.h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
-    rec.fp_lo = 0;
-    rec.now_mod = 0;
-    rec.gen = 0;
-    rec.pad = 0;
-    uint64_t key = NIL_KEY;
-    uint32_t bucket = NIL_BUCKET;
-    if (r != RL_NIL_RULE && (r >= n_rules || !q_ok)) err |= ERR_BAD_INPUT;
-    if (r != RL_NIL_RULE && r < n_rules && q_ok) {
-      if (now < 0 || now > 0xFFFFFFF0ll) {
-        err |= ERR_BAD_TIME;
-      } else {
-        const DevRule R = rules[r];
-        const int64_t widx = div_const(now, R.unit);
-        const int64_t ws = widx * (int64_t)R.div;  // (now/divider)*divider  cache_key.go:66-68
-        const uint32_t o0 = in.off[i], o1 = in.off[i + 1];
-        FpState s = fp_init(o1 - o0, R.unit, seed);
-        hash_prefix(in.blob, o0, o1 - o0, s);
-        uint32_t hot_rule = 0;
-        const uint32_t hidx = hot_lookup(sh_hot, s.a, s.b, R.unit, hot_rule);
-        uint64_t hi, lo;
-        fp_final(s, (uint64_t)ws, hi, lo);
-        const uint32_t region = (R.unit - 1u) * 2u + (uint32_t)(widx & 1);
-        key = make_sort_key(region, hi);
-        rec.fp_lo = lo;
-        rec.now_mod = (int32_t)(now - ws);
-        rec.gen = (uint32_t)widx + 1u;
-#pragma unroll
-        for (int rg = 0; rg < 8; ++rg)  // static register indexing
-          if ((uint32_t)rg == region) {
-            gmin[rg] = rec.gen < gmin[rg] ? rec.gen : gmin[rg];
-            gmax[rg] = rec.gen > gmax[rg] ? rec.gen : gmax[rg];
-          }
-        if (hidx != 0xFFFFFFFFu) {
-          // a hot prefix must keep one rule in the batch (its bucket is one key)
-          if (hot_rule != r) err |= ERR_V2_FALLBACK;
-          bucket = hidx * 2u + (uint32_t)(widx & 1);
+  for (int k = 0; k < V2_ROUNDS; ++k) {
+    const uint32_t i = tile * V2_TILE + wave * (V2_TILE / V2_WAVES) + k * 64 + lane;
+    const bool valid = i < in.n_desc;
+    uint32_t bucket = NIL_BUCKET, hh = 1;
+    uint64_t hkey = 0, hlo = 0;
+    uint32_t hgen = 0;
+    if (valid) {
+      const uint32_t r = in.rule[i];
+      const uint32_t q = in.req_of[i];
+      const bool q_ok = q < in.n_req;
+      const int64_t now = q_ok ? in.now[q] : 0;
+      const uint32_t ha = q_ok ? in.hits[q] : 1u;
+      if (q_ok) {  // zero the ThrottleMillis of the requests this descriptor opens
+        const uint32_t pq = i == 0 ? 0u : in.req_of[i - 1];
+        const uint32_t first = i == 0 ? 0u : (pq < q ? pq + 1u : q + 1u);
+        for (uint32_t rr = first; rr <= q; ++rr) req_thr[rr] = 0;
+        if (i + 1 == in.n_desc)
+          for (uint32_t rr = q + 1; rr < in.n_req; ++rr) req_thr[rr] = 0;
+      }
+      ItemRec rec;
+      rec.rule = r;
+      rec.req = q;
+      rec.h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
+      rec.fp_lo = 0;
+      rec.now_mod = 0;
+      rec.gen = 0;
+      rec.pad = 0;
+      uint64_t key = NIL_KEY;
+      if (r != RL_NIL_RULE && (r >= n_rules || !q_ok)) err |= ERR_BAD_INPUT;
+      if (r != RL_NIL_RULE && r < n_rules && q_ok) {
+        if (now < 0 || now > 0xFFFFFFF0ll) {
+          err |= ERR_BAD_TIME;
         } else {
-          bucket = HOT_BUCKETS + msd_bucket(key);
+          const DevRule R = rules[r];
+          const int64_t widx = div_const(now, R.unit);
+          const int64_t ws = widx * (int64_t)R.div;  // (now/divider)*divider  cache_key.go:66-68
+          const uint32_t o0 = in.off[i], o1 = in.off[i + 1];
+          FpState s = fp_init(o1 - o0, R.unit, seed);
+          hash_prefix(in.blob, o0, o1 - o0, s);
+          uint32_t hot_rule = 0;
+          const uint32_t hidx = hot_lookup(sh_hot, s.a, s.b, R.unit, hot_rule);
+          uint64_t hi, lo;
+          fp_final(s, (uint64_t)ws, hi, lo);
+          const uint32_t region = (R.unit - 1u) * 2u + (uint32_t)(widx & 1);
+          key = make_sort_key(region, hi);
+          rec.fp_lo = lo;
+          rec.now_mod = (int32_t)(now - ws);
+          rec.gen = (uint32_t)widx + 1u;
+#pragma unroll
+          for (int rg = 0; rg < 8; ++rg)  // static register indexing
+            if ((uint32_t)rg == region) {
+              gmin[rg] = rec.gen < gmin[rg] ? rec.gen : gmin[rg];
+              gmax[rg] = rec.gen > gmax[rg] ? rec.gen : gmax[rg];
+            }
+          if (hidx != 0xFFFFFFFFu) {
+            // a hot prefix must keep one rule in the batch (its bucket is one key)
+            if (hot_rule != r) err |= ERR_V2_FALLBACK;
+            bucket = hidx * 2u + (uint32_t)(widx & 1);
+          } else {
+            bucket = HOT_BUCKETS + msd_bucket(key);
+          }
         }
       }
+      recs[i] = rec;
+      keys_orig[i] = key;
+      hkey = key;
+      hlo = rec.fp_lo;
+      hgen = rec.gen;
+      bkt[i] = (uint16_t)bucket;
+      hbuf[i] = rec.h;
+      hh = rec.h;
+      if (bucket == NIL_BUCKET) {
+        // GetResponseDescriptorStatus("" key) -> {OK, nil limit, 0}  base_limiter.go:72-75
+        rl_status st;
+        st.code_flags = RL_CODE_OK;
+        st.limit_remaining = 0;
+        st.reset_s = 0;
+        st.over_limit_delta = 0;
+        st.near_limit_delta = 0;
+        out[i] = st;
+        ++nil_cnt;
+      }
     }
-    recs[i] = rec;
-    keys_orig[i] = key;
-    bkt[i] = (uint16_t)bucket;
-    hbuf[i] = rec.h;
-    if (bucket == NIL_BUCKET) {
-      // GetResponseDescriptorStatus("" key) -> {OK, nil limit, 0}  base_limiter.go:72-75
-      rl_status st;
-      st.code_flags = RL_CODE_OK;
-      st.limit_remaining = 0;
-      st.reset_s = 0;
-      st.over_limit_delta = 0;
-      st.near_limit_delta = 0;
-      out[i] = st;
-      ++nil_cnt;
+    // wave-aggregated tile histogram: one LDS atomic per distinct bucket of the round
+    const uint64_t m = match12(bucket, valid);
+    if (valid) {
+      const uint32_t c = (uint32_t)__popcll(m);
+      if (lane == (uint32_t)__ffsll((unsigned long long)m) - 1u) {
+        atomicAdd(&sh_cnt[bucket], c);
+        if (bucket < (uint32_t)HOT_BUCKETS) {
+          atomicAdd(&sh_hs[bucket], (unsigned long long)c);
+          // the bucket's key (one key per hot bucket; every tile writes the same values)
+          hb[bucket].key = hkey;
+          hb[bucket].fp_lo = hlo;
+          hb[bucket].gen = hgen;
+        }
+      }
+      if (bucket < (uint32_t)HOT_BUCKETS && hh > 1u) atomicAdd(&sh_hs[bucket], (unsigned long long)(hh - 1u));
     }
-    atomicAdd(&sh_cnt[bucket], 1u);
-    if (bucket < (uint32_t)HOT_BUCKETS) atomicAdd(&sh_hs[bucket], (unsigned long long)rec.h);
   }
   // block reductions (one LDS op per wave and region)
 #pragma unroll
@@ -167,8 +275,8 @@ __global__ __launch_bounds__(256) void k_fp2(DevBatch in, const DevRule* __restr
   if (lane == 0 && nil_cnt) atomicAdd(&sh_nil, nil_cnt);
   if (err) atomicOr(&sh_err, err);
   __syncthreads();
-  for (int b = tid; b < NBUCKETS; b += 256) tcount[(size_t)tile * NBUCKETS + b] = sh_cnt[b];
-  for (int b = tid; b < HOT_BUCKETS; b += 256) thsum[(size_t)tile * HOT_BUCKETS + b] = sh_hs[b];
+  for (int b = tid; b < NBUCKETS; b += V2_THREADS) tcount[(size_t)b * ntiles + tile] = sh_cnt[b];
+  for (int b = tid; b < HOT_BUCKETS; b += V2_THREADS) thsum[(size_t)b * ntiles + tile] = sh_hs[b];
   uint32_t* fp = fpart + (size_t)tile * FP_PART_WORDS;
   if (tid < 8) fp[tid] = sh_gmin[tid];
   else if (tid < 16) fp[tid] = sh_gmax[tid - 8];
@@ -177,37 +285,19 @@ __global__ __launch_bounds__(256) void k_fp2(DevBatch in, const DevRule* __restr
 }
 
 // ---------------------------------------------------------------------------
-// k_bscan — one block per bucket (+ one reducer block)
+// k_bscan — one wave per bucket: exclusive scan over tiles; last block folds fpart
 // ---------------------------------------------------------------------------
-template <class T>
-RL_DEV T block_excl_scan_256(T v, T* sh, T& total) {
-  const uint32_t tid = threadIdx.x;
-  sh[tid] = v;
-  __syncthreads();
-  for (int d = 1; d < 256; d <<= 1) {
-    const T t = tid >= (uint32_t)d ? sh[tid - d] : (T)0;
-    __syncthreads();
-    sh[tid] += t;
-    __syncthreads();
-  }
-  total = sh[255];
-  const T r = sh[tid] - v;
-  __syncthreads();
-  return r;
-}
-
+constexpr int BSCAN_WAVES = 4;
 __global__ __launch_bounds__(256) void k_bscan(const uint32_t* __restrict__ tcount,
                                                const unsigned long long* __restrict__ thsum, uint32_t ntiles,
                                                uint32_t* __restrict__ toff, unsigned long long* __restrict__ hoff,
                                                uint32_t* __restrict__ btotal, const uint32_t* __restrict__ fpart,
-                                               EngineCtl* ctl) {
-  __shared__ uint32_t sh32[256];
-  __shared__ unsigned long long sh64[256];
-  __shared__ uint32_t shm[FP_PART_WORDS][256];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t b = blockIdx.x;
-  if (b == NBUCKETS) {
+                                               const HotEntry* __restrict__ hot_list, HotBucket* __restrict__ hb,
+                                               TableDesc tab, HotCand* __restrict__ cand, EngineCtl* ctl) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (blockIdx.x == gridDim.x - 1) {
     // fold the per-tile fingerprint partials: generation range per region, nil count
+    __shared__ uint32_t shm[FP_PART_WORDS][256];
     for (int w = 0; w < FP_PART_WORDS; ++w) {
       uint32_t v = 0;
       for (uint32_t g = tid; g < ntiles; g += 256) {
@@ -230,158 +320,229 @@ __global__ __launch_bounds__(256) void k_bscan(const uint32_t* __restrict__ tcou
     else if (tid == 16) ctl->n_nil = shm[16][0];
     return;
   }
-  // each thread owns a contiguous run of tiles
-  const uint32_t per = (ntiles + 255) / 256;
-  const uint32_t t0 = tid * per, t1 = min(ntiles, t0 + per);
-  uint32_t c = 0;
-  for (uint32_t t = t0; t < t1; ++t) c += tcount[(size_t)t * NBUCKETS + b];
-  uint32_t total;
-  uint32_t run = block_excl_scan_256<uint32_t>(c, sh32, total);
-  for (uint32_t t = t0; t < t1; ++t) {
-    toff[(size_t)t * NBUCKETS + b] = run;
-    run += tcount[(size_t)t * NBUCKETS + b];
+  const uint32_t b = blockIdx.x * BSCAN_WAVES + wave;
+  if (b >= (uint32_t)NBUCKETS) return;
+  const uint32_t* tc = tcount + (size_t)b * ntiles;
+  uint32_t* to = toff + (size_t)b * ntiles;
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < ntiles; t0 += 64) {
+    const uint32_t t = t0 + lane;
+    const uint32_t v = t < ntiles ? tc[t] : 0u;
+    const uint32_t incl = wave_incl_scan<uint32_t>(v);
+    if (t < ntiles) to[t] = carry + incl - v;
+    carry += __shfl(incl, 63, 64);
   }
-  if (tid == 0) {
-    btotal[b] = total;
-    if (b >= (uint32_t)HOT_BUCKETS && b < NIL_BUCKET && total > (uint32_t)BUCKET_CAP)
+  if (lane == 0) {
+    btotal[b] = carry;
+    if (b >= (uint32_t)HOT_BUCKETS && b < NIL_BUCKET && carry > (uint32_t)BUCKET_CAP)
       atomicOr(&ctl->err, ERR_V2_FALLBACK);
   }
   if (b < (uint32_t)HOT_BUCKETS) {
-    unsigned long long s = 0;
-    for (uint32_t t = t0; t < t1; ++t) s += thsum[(size_t)t * HOT_BUCKETS + b];
-    unsigned long long tot;
-    unsigned long long r = block_excl_scan_256<unsigned long long>(s, sh64, tot);
-    for (uint32_t t = t0; t < t1; ++t) {
-      hoff[(size_t)t * HOT_BUCKETS + b] = r;
-      r += thsum[(size_t)t * HOT_BUCKETS + b];
+    // Hot key leader, part 1: find or claim the key's slot and read the counter before this
+    // batch. A claimed slot starts at count 0 (invisible if the batch is later rejected);
+    // k_bgroup writes the final count.
+    if (lane == 0) {
+      HotBucket x = hb[b];
+      x.jpos = 0xFFFFFFFFu;
+      x.slot = 0;
+      x.base = 0;
+      x.flags = 0;
+      const uint32_t errs = ctl->err;  // flags of k_fp2
+      if (carry && !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME | ERR_V2_FALLBACK))) {
+        Slot* slot = nullptr;
+        bool existed = false;
+        if (!table_claim(tab, x.key, x.fp_lo, x.gen, slot, existed)) {
+          atomicOr(&ctl->err, ERR_TABLE_FULL);
+        } else {
+          if (existed) {
+            x.base = slot->count;
+            x.flags = (slot->flags & SLOT_FROZEN) ? HB_FROZEN_PRE : 0u;
+          } else {
+            slot->key = x.key;
+            slot->fp_lo_hi = (uint32_t)(x.fp_lo >> 32);
+            slot->count = 0;
+            slot->flags = 0;
+          }
+          x.slot = (uint64_t)(uintptr_t)slot;
+          count_inserts(!existed, ctl);
+        }
+        if (carry >= HOT_CAND_MIN) {  // stays hot: report with its known prefix state
+          const HotEntry& he = hot_list[b >> 1];
+          emit_candidate(ctl, cand, he.rule, carry, 0xFFFFFFFFu, he.a, he.b, he.unit);
+        }
+      }
+      hb[b] = x;
+    }
+    const unsigned long long* hs = thsum + (size_t)b * ntiles;
+    unsigned long long* ho = hoff + (size_t)b * ntiles;
+    unsigned long long hc = 0;
+    for (uint32_t t0 = 0; t0 < ntiles; t0 += 64) {
+      const uint32_t t = t0 + lane;
+      const unsigned long long v = t < ntiles ? hs[t] : 0ull;
+      const unsigned long long incl = wave_incl_scan<unsigned long long>(v);
+      if (t < ntiles) ho[t] = hc + incl - v;
+      hc += __shfl(incl, 63, 64);
     }
   }
 }
 
-// Bucket bases (exclusive scan of NBUCKETS totals) into LDS; every thread of a 256-block calls.
-RL_DEV void bucket_bases(const uint32_t* __restrict__ btotal, uint32_t* s_base, uint32_t* sh_scan) {
-  const uint32_t tid = threadIdx.x;
-  constexpr int PER = (NBUCKETS + 255) / 256;
-  uint32_t v[PER];
-  uint32_t sum = 0;
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const uint32_t b = tid * PER + k;
-    v[k] = b < (uint32_t)NBUCKETS ? btotal[b] : 0u;
-    sum += v[k];
-  }
-  uint32_t total;
-  uint32_t run = block_excl_scan_256<uint32_t>(sum, sh_scan, total);
-#pragma unroll
-  for (int k = 0; k < PER; ++k) {
-    const uint32_t b = tid * PER + k;
-    if (b < (uint32_t)NBUCKETS) s_base[b] = run;
-    run += v[k];
-  }
-  if (tid == 0) s_base[NBUCKETS] = total;
-  __syncthreads();
+// ---------------------------------------------------------------------------
+// k_bscatter — stable counting scatter into bucket order (same tiles as k_fp2).
+// The tile is first sorted by bucket in LDS (two stable 6-bit passes), so the global
+// writes of one bucket are contiguous; a segmented scan over the sorted tile gives each
+// descriptor its rank in (tile, bucket) and, for hot buckets, its in-tile h prefix.
+// ---------------------------------------------------------------------------
+struct SegEl {
+  uint32_t f, hp;
+  unsigned long long s;
+};
+RL_DEV SegEl seg_op(const SegEl& a, const SegEl& b) {
+  if (b.f) return b;
+  return SegEl{a.f, a.hp, a.s + b.s};
 }
 
-// ---------------------------------------------------------------------------
-// k_bscatter — stable counting scatter into bucket order (same tile / item mapping as k_fp2)
-// ---------------------------------------------------------------------------
-constexpr int BS_IPT = V2_TILE / 256;
-
-__global__ __launch_bounds__(256) void k_bscatter(const uint64_t* __restrict__ keys_orig,
-                                                  const uint16_t* __restrict__ bkt, const uint32_t* __restrict__ hbuf,
-                                                  uint32_t n, const uint32_t* __restrict__ btotal,
-                                                  const uint32_t* __restrict__ toff,
-                                                  const unsigned long long* __restrict__ hoff,
-                                                  uint64_t* __restrict__ bkey, uint32_t* __restrict__ bidx,
-                                                  uint64_t* __restrict__ bP, EngineCtl* ctl) {
-  __shared__ uint32_t s_base[NBUCKETS + 1];
-  __shared__ uint32_t s_wcnt[4][NBUCKETS];
-  __shared__ unsigned long long s_whs[4][HOT_BUCKETS];
-  __shared__ uint32_t sh_scan[256];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t lane = tid & 63, wave = tid >> 6;
-  if (ctl->err & (ERR_V2_FALLBACK | ERR_BAD_INPUT | ERR_BAD_TIME)) return;
-  const uint32_t tile = blockIdx.x;
-  for (int i = tid; i < 4 * NBUCKETS; i += 256) (&s_wcnt[0][0])[i] = 0;
-  for (int i = tid; i < 4 * HOT_BUCKETS; i += 256) (&s_whs[0][0])[i] = 0;
-  bucket_bases(btotal, s_base, sh_scan);  // includes a barrier
-
-  uint32_t bk[BS_IPT], rank[BS_IPT];
-  unsigned long long hp[BS_IPT];  // wave-local inclusive h prefix (hot descriptors)
+// One stable LDS counting pass over 64 digits of the tile (V2_THREADS threads).
+RL_DEV void tile_digit_pass(const uint16_t* s_d, const uint16_t* src, uint16_t* dst, int shift,
+                            uint32_t (*s_cnt)[64], uint32_t* sh_w) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < V2_WAVES * 64; i += V2_THREADS) (&s_cnt[0][0])[i] = 0;
+  __syncthreads();
   const uint64_t lt = lanemask_lt();
+  uint32_t dg[V2_ROUNDS], rk[V2_ROUNDS], sv[V2_ROUNDS];
 #pragma unroll
-  for (int k = 0; k < BS_IPT; ++k) {
-    const uint32_t i = tile * V2_TILE + wave * (V2_TILE / 4) + k * 64 + lane;
-    const bool valid = i < n;
-    const uint32_t d = valid ? bkt[i] : 0u;
-    const uint32_t h = valid ? hbuf[i] : 0u;
-    uint64_t m = __ballot(valid);
+  for (int r = 0; r < V2_ROUNDS; ++r) {
+    const uint32_t p = wave * (V2_TILE / V2_WAVES) + r * 64 + lane;
+    const uint32_t o = src[p];
+    const uint32_t d = ((uint32_t)s_d[o] >> shift) & 63u;
+    uint64_t m = ~0ull;
 #pragma unroll
-    for (int b = 0; b < 12; ++b) {
+    for (int b = 0; b < 6; ++b) {
       const bool bit = (d >> b) & 1u;
       const uint64_t bal = __ballot(bit);
       m &= bit ? bal : ~bal;
     }
-    // hot descriptors: inclusive prefix of h among same-bucket lanes of this round
-    unsigned long long hin = 0;
-    uint64_t hotm = __ballot(valid && d < (uint32_t)HOT_BUCKETS);
-    while (hotm) {
-      const uint32_t ld = (uint32_t)__ffsll((unsigned long long)hotm) - 1u;
-      const uint32_t db = (uint32_t)__shfl((int)d, (int)ld, 64);
-      const bool mine = valid && d == db;
-      unsigned long long x = mine ? (unsigned long long)h : 0ull;
-#pragma unroll
-      for (int s = 1; s < 64; s <<= 1) {
-        const unsigned long long y = __shfl_up(x, s, 64);
-        if (lane >= (uint32_t)s) x += y;
-      }
-      if (mine) hin = x;
-      hotm &= ~__ballot(mine);
-    }
-    uint32_t r = 0;
-    unsigned long long hsum_before = 0;
-    if (valid) {
-      const uint32_t before = s_wcnt[wave][d];
-      if (d < (uint32_t)HOT_BUCKETS) hsum_before = s_whs[wave][d];
-      r = before + (uint32_t)__popcll(m & lt);
-      const uint32_t leader = 63u - (uint32_t)__clzll((unsigned long long)m);  // highest lane of the group
-      __builtin_amdgcn_wave_barrier();
-      if (lane == leader) {
-        s_wcnt[wave][d] = before + (uint32_t)__popcll(m);
-        if (d < (uint32_t)HOT_BUCKETS) s_whs[wave][d] = hsum_before + hin;  // leader holds the group total
-      }
-    }
+    const uint32_t before = s_cnt[wave][d];
     __builtin_amdgcn_wave_barrier();
-    bk[k] = d;
-    rank[k] = r;
-    hp[k] = hsum_before + hin;
+    if (lane == (uint32_t)__ffsll((unsigned long long)m) - 1u) s_cnt[wave][d] = before + (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+    dg[r] = d;
+    rk[r] = before + (uint32_t)__popcll(m & lt);
+    sv[r] = o;
   }
   __syncthreads();
-  // per bucket: per-wave exclusive offsets (counts, and h-sums for hot buckets)
-  for (int b = tid; b < NBUCKETS; b += 256) {
-    const uint32_t c0 = s_wcnt[0][b], c1 = s_wcnt[1][b], c2 = s_wcnt[2][b];
-    s_wcnt[0][b] = 0;
-    s_wcnt[1][b] = c0;
-    s_wcnt[2][b] = c0 + c1;
-    s_wcnt[3][b] = c0 + c1 + c2;
-    if (b < HOT_BUCKETS) {
-      const unsigned long long h0 = s_whs[0][b], h1 = s_whs[1][b], h2 = s_whs[2][b];
-      s_whs[0][b] = 0;
-      s_whs[1][b] = h0;
-      s_whs[2][b] = h0 + h1;
-      s_whs[3][b] = h0 + h1 + h2;
-    }
+  {  // digit-major exclusive offsets: entry (digit, wave) = tid
+    const uint32_t d = tid >> 4, w = tid & 15;
+    const uint32_t v = s_cnt[w][d];
+    uint32_t total;
+    const uint32_t off = block_excl_scan<V2_THREADS>(v, sh_w, total);
+    s_cnt[w][d] = off;
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < BS_IPT; ++k) {
-    const uint32_t i = tile * V2_TILE + wave * (V2_TILE / 4) + k * 64 + lane;
-    if (i >= n) continue;
-    const uint32_t d = bk[k];
-    const uint32_t pos = s_base[d] + toff[(size_t)tile * NBUCKETS + d] + s_wcnt[wave][d] + rank[k];
+  for (int r = 0; r < V2_ROUNDS; ++r) dst[s_cnt[wave][dg[r]] + rk[r]] = (uint16_t)sv[r];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(V2_THREADS) void k_bscatter(const uint64_t* __restrict__ keys_orig,
+                                                         const ItemRec* __restrict__ recs,
+                                                         const uint16_t* __restrict__ bkt,
+                                                         const uint32_t* __restrict__ hbuf, uint32_t n,
+                                                         uint32_t ntiles, const uint32_t* __restrict__ btotal,
+                                                         const uint32_t* __restrict__ toff,
+                                                         const unsigned long long* __restrict__ hoff,
+                                                         uint64_t* __restrict__ bkey, ItemRec* __restrict__ brec,
+                                                         uint64_t* __restrict__ bP, uint32_t* __restrict__ bbase,
+                                                         HotBucket* __restrict__ hb,
+                                                         const DevRule* __restrict__ rules, int local_cache,
+                                                         EngineCtl* ctl) {
+  static_assert(V2_WAVES * 64 == V2_THREADS && V2_WAVES == 16, "digit-major scan assumes 16 waves x 64 digits");
+  __shared__ uint32_t s_base[NBUCKETS + 1];
+  __shared__ uint16_t s_d[V2_TILE];
+  __shared__ uint16_t s_pa[V2_TILE], s_pb[V2_TILE];
+  __shared__ uint32_t s_h[V2_TILE];
+  __shared__ uint32_t s_cnt[V2_WAVES][64];
+  __shared__ uint32_t sh_w[V2_WAVES];
+  __shared__ SegEl s_agg[V2_WAVES];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (ctl->err & (ERR_V2_FALLBACK | ERR_BAD_INPUT | ERR_BAD_TIME)) return;
+  const uint32_t tile = blockIdx.x;
+  const uint32_t t0 = tile * V2_TILE;
+  for (int o = tid; o < V2_TILE; o += V2_THREADS) {
+    const uint32_t i = t0 + o;
+    const bool valid = i < n;
+    s_d[o] = valid ? bkt[i] : (uint16_t)BKT_SENTINEL;
+    s_h[o] = valid ? hbuf[i] : 0u;
+    s_pa[o] = (uint16_t)o;
+  }
+  bucket_bases<V2_THREADS>(btotal, s_base, sh_w);  // includes barriers
+  if (tile == 0)  // publish the bases for k_bgroup
+    for (int b = tid; b <= NBUCKETS; b += V2_THREADS) bbase[b] = s_base[b];
+  tile_digit_pass(s_d, s_pa, s_pb, 0, s_cnt, sh_w);
+  tile_digit_pass(s_d, s_pb, s_pa, 6, s_cnt, sh_w);
+  // segmented scan over the sorted tile (blocked: V2_ROUNDS consecutive positions per thread)
+  const uint32_t s0 = tid * V2_ROUNDS;
+  uint32_t od[V2_ROUNDS], dd[V2_ROUNDS], fl[V2_ROUNDS];
+  unsigned long long hv[V2_ROUNDS];
+  uint32_t prev_d = s0 == 0 ? 0xFFFFFFFFu : s_d[s_pa[s0 - 1]];
+  SegEl t{0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < V2_ROUNDS; ++q) {
+    const uint32_t o = s_pa[s0 + q];
+    const uint32_t d = s_d[o];
+    od[q] = o;
+    dd[q] = d;
+    fl[q] = d != prev_d;
+    hv[q] = s_h[o];
+    prev_d = d;
+    t = seg_op(t, SegEl{fl[q], s0 + q, hv[q]});
+  }
+  SegEl incl = t;
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    SegEl y;
+    y.f = __shfl_up(incl.f, s, 64);
+    y.hp = __shfl_up(incl.hp, s, 64);
+    y.s = __shfl_up(incl.s, s, 64);
+    if (lane >= (uint32_t)s) incl = seg_op(y, incl);
+  }
+  if (lane == 63) s_agg[wave] = incl;
+  SegEl wex;
+  wex.f = __shfl_up(incl.f, 1, 64);
+  wex.hp = __shfl_up(incl.hp, 1, 64);
+  wex.s = __shfl_up(incl.s, 1, 64);
+  if (lane == 0) wex = SegEl{0, 0, 0};
+  __syncthreads();
+  SegEl run{0, 0, 0};
+  for (uint32_t w = 0; w < wave; ++w) run = seg_op(run, s_agg[w]);
+  run = seg_op(run, wex);
+#pragma unroll
+  for (int q = 0; q < V2_ROUNDS; ++q) {
+    run = seg_op(run, SegEl{fl[q], s0 + q, hv[q]});
+    const uint32_t d = dd[q];
+    if (d >= (uint32_t)NBUCKETS) continue;  // past the end of the batch
+    const uint32_t i = t0 + od[q];
+    const uint32_t pos = s_base[d] + toff[(size_t)d * ntiles + tile] + (s0 + q - run.hp);
+    // bucketed copy of the arrival record; pad carries the descriptor index
+    ItemRec r = recs[i];
+    r.pad = i;
     bkey[pos] = keys_orig[i];
-    bidx[pos] = i;
-    if (d < (uint32_t)HOT_BUCKETS) bP[pos] = hoff[(size_t)tile * HOT_BUCKETS + d] + s_whs[wave][d] + hp[k];
+    brec[pos] = r;
+    if (d < (uint32_t)HOT_BUCKETS) {
+      const uint64_t P = hoff[(size_t)d * ntiles + tile] + run.s;
+      bP[pos] = P;
+      if (local_cache) {
+        // Local cache: the key freezes at the first descriptor whose INCRBY reply exceeds
+        // the limit. Candidates are the upward crossings (after > L >= before, or the
+        // bucket's first descriptor); the earliest one is that descriptor.
+        const HotBucket& x = hb[d];
+        if (x.slot && !(x.flags & HB_FROZEN_PRE)) {
+          const uint32_t after = (uint32_t)(x.base + P);
+          const uint32_t before = after - r.h;
+          const uint32_t L = rules[r.rule].L;
+          if (after > L && (before <= L || pos == s_base[d])) atomicMin(&hb[d].jpos, pos);
+        }
+      }
+    }
   }
 }
 
@@ -405,7 +566,8 @@ RL_DEV BgScanEl bg_op(const BgScanEl& a, const BgScanEl& b) {
 
 // Stable LDS radix pass: order src -> dst by 8-bit digit (key >> shift) of m items.
 RL_DEV void lds_radix_pass(const uint64_t* s_key, const uint16_t* src, uint16_t* dst, uint32_t m, int shift,
-                           uint32_t (*s_cnt)[RADIX], uint32_t* s_dstart, uint32_t* sh_scan) {
+                           uint32_t (*s_cnt)[RADIX], uint32_t* sh_w) {
+  constexpr int ENT = BG_WAVES * RADIX / BG_THREADS;  // (digit, wave) counters per thread
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < BG_WAVES * RADIX; i += BG_THREADS) (&s_cnt[0][0])[i] = 0;
   __syncthreads();
@@ -436,85 +598,72 @@ RL_DEV void lds_radix_pass(const uint64_t* s_key, const uint16_t* src, uint16_t*
     rk[r] = rr;
   }
   __syncthreads();
-  // digit totals + per-wave exclusive offsets (threads 0..255 own one digit each), then an
-  // exclusive scan over the 256 digit totals (every thread takes part in the barriers)
-  uint32_t tot = 0;
-  if (tid < RADIX) {
-    for (int w = 0; w < BG_WAVES; ++w) {
-      const uint32_t c = s_cnt[w][tid];
-      s_cnt[w][tid] = tot;
-      tot += c;
+  {  // digit-major exclusive offsets over (digit, wave): entries ENT*tid .. ENT*tid+ENT-1
+    uint32_t v[ENT], sum = 0;
+#pragma unroll
+    for (int j = 0; j < ENT; ++j) {
+      const uint32_t e = tid * ENT + j;
+      v[j] = s_cnt[e % BG_WAVES][e / BG_WAVES];
+      sum += v[j];
     }
-    sh_scan[tid] = tot;
+    uint32_t total;
+    uint32_t run = block_excl_scan<BG_THREADS>(sum, sh_w, total);
+#pragma unroll
+    for (int j = 0; j < ENT; ++j) {
+      const uint32_t e = tid * ENT + j;
+      s_cnt[e % BG_WAVES][e / BG_WAVES] = run;
+      run += v[j];
+    }
   }
-  __syncthreads();
-  for (int d = 1; d < RADIX; d <<= 1) {
-    const uint32_t t = (tid < RADIX && tid >= (uint32_t)d) ? sh_scan[tid - d] : 0u;
-    __syncthreads();
-    if (tid < RADIX) sh_scan[tid] += t;
-    __syncthreads();
-  }
-  if (tid < RADIX) s_dstart[tid] = sh_scan[tid] - tot;
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < BG_ROUNDS; ++r) {
     const uint32_t k = wave * BG_PER_WAVE + r * 64 + lane;
-    if (k < m) dst[s_dstart[dg[r]] + s_cnt[wave][dg[r]] + rk[r]] = src[k];
+    if (k < m) dst[s_cnt[wave][dg[r]] + rk[r]] = src[k];
   }
   __syncthreads();
 }
 
 __global__ __launch_bounds__(BG_THREADS) void k_bgroup(const uint64_t* __restrict__ bkey,
-                                                       const uint32_t* __restrict__ bidx,
+                                                       const ItemRec* __restrict__ brec,
                                                        const uint64_t* __restrict__ bP,
-                                                       const ItemRec* __restrict__ recs,
-                                                       const uint32_t* __restrict__ btotal, uint32_t n_msd_wg,
+                                                       const uint32_t* __restrict__ bbase, uint32_t n_msd_wg,
                                                        uint64_t* __restrict__ skeys, SortedRec* __restrict__ srec,
-                                                       uint32_t* __restrict__ wg_heads, EngineCtl* ctl) {
+                                                       uint32_t* __restrict__ wg_heads,
+                                                       const ItemRec* __restrict__ recs,
+                                                       const DevRule* __restrict__ rules, TableDesc tab,
+                                                       int local_cache, SegInfo* __restrict__ seg,
+                                                       const HotBucket* __restrict__ hb,
+                                                       rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
+                                                       HotCand* __restrict__ cand, EngineCtl* ctl) {
   __shared__ uint32_t s_base[NBUCKETS + 1];
-  __shared__ uint32_t sh_scan[256];
   __shared__ uint64_t s_key[BG_MAX];
   __shared__ uint64_t s_lo[BG_MAX];
   __shared__ uint32_t s_h[BG_MAX];
   __shared__ uint32_t s_rule[BG_MAX];
   __shared__ uint16_t s_pa[BG_MAX], s_pb[BG_MAX];
   __shared__ uint32_t s_cnt[BG_WAVES][RADIX];
-  __shared__ uint32_t s_dstart[RADIX];
   __shared__ BgScanEl s_wagg[BG_WAVES];
   __shared__ uint32_t s_mixed, s_heads;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (ctl->err & (ERR_V2_FALLBACK | ERR_BAD_INPUT | ERR_BAD_TIME)) return;
-  // bucket bases with the first 256 threads' scan helper: all threads take part
+  // Nothing touches the table unless the whole batch is valid: errors of earlier kernels,
+  // or two window generations more than one apart in a region.
+  if (ctl->err) return;
   {
-    constexpr int PER = (NBUCKETS + BG_THREADS - 1) / BG_THREADS;
-    uint32_t v[PER], sum = 0;
+    bool span = false;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const uint32_t b = tid * PER + k;
-      v[k] = b < (uint32_t)NBUCKETS ? btotal[b] : 0u;
-      sum += v[k];
+    for (int rg = 0; rg < 8; ++rg) span |= ctl->gen_max[rg] - ctl->gen_min[rg] > 1u;
+    if (span) {
+      if (tid == 0) atomicOr(&ctl->err, ERR_WINDOW_SPAN);
+      return;
     }
-    // 512-thread exclusive scan via two 256 halves
-    __shared__ uint32_t sh512[BG_THREADS];
-    sh512[tid] = sum;
-    __syncthreads();
-    for (int d = 1; d < BG_THREADS; d <<= 1) {
-      const uint32_t t = tid >= (uint32_t)d ? sh512[tid - d] : 0u;
-      __syncthreads();
-      sh512[tid] += t;
-      __syncthreads();
-    }
-    uint32_t run = sh512[tid] - sum;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const uint32_t b = tid * PER + k;
-      if (b < (uint32_t)NBUCKETS) s_base[b] = run;
-      run += v[k];
-    }
-    if (tid == BG_THREADS - 1) s_base[NBUCKETS] = sh512[tid];
-    if (tid == 0) { s_mixed = 0; s_heads = 0; }
-    __syncthreads();
   }
+  __shared__ uint32_t sh_w[BG_WAVES];
+  BSTAMP(0);
+  if (tid == 0) { s_mixed = 0; s_heads = 0; }
+  for (int b = tid; b <= NBUCKETS; b += BG_THREADS) s_base[b] = bbase[b];
+  __syncthreads();
+  BSTAMP(1);
   const uint32_t hot_end = s_base[HOT_BUCKETS];
   if (blockIdx.x >= n_msd_wg) {
     // Hot chunk: each hot bucket is one key in arrival order; P comes from k_bscatter.
@@ -524,6 +673,10 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgroup(const uint64_t* __restric
       if (tid == 0) wg_heads[blockIdx.x] = 0;
       return;
     }
+#ifdef RL_BG_SKIP_HOT
+    if (tid == 0) wg_heads[blockIdx.x] = 0;
+    return;
+#endif
     const uint32_t p1 = min(hot_end, p0 + HOT_CHUNK);
     uint32_t heads = 0;
     for (uint32_t p = p0 + tid; p < p1; p += BG_THREADS) {
@@ -533,20 +686,43 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgroup(const uint64_t* __restric
         const uint32_t mid = (lo_b + hi_b + 1) / 2;
         if (s_base[mid] <= p) lo_b = mid; else hi_b = mid - 1;
       }
-      const uint32_t head = s_base[lo_b];
+      const uint32_t head = s_base[lo_b], end = s_base[lo_b + 1];
       heads += head == p;
-      const uint32_t idx = bidx[p];
-      const ItemRec r = recs[idx];
+      const HotBucket x = hb[lo_b];
+      if (!x.slot) continue;  // unreachable for a valid batch (k_bscan claimed every non-empty bucket)
+      const ItemRec r = brec[p];
       SortedRec o;
       o.P = bP[p];
       o.head = head;
-      o.idx = idx;
+      o.idx = r.pad;
       o.rule = r.rule;
       o.req = r.req;
       o.h = r.h;
       o.now_mod = r.now_mod;
-      srec[p] = o;
-      skeys[p] = bkey[p];
+      SegInfo si;
+      si.base = x.base;
+      si.pad = 0;
+      uint32_t rstar = SEG_NO_FREEZE;
+      if (x.flags & HB_FROZEN_PRE) {
+        si.freeze = SEG_FROZEN_BEFORE;
+      } else {
+        if (x.jpos != 0xFFFFFFFFu) rstar = brec[x.jpos].req;
+        si.freeze = rstar;
+      }
+      decide_one(o, si, rules[r.rule], out, req_thr);
+      // Hot key leader, part 2: the one descriptor that ends the key's INCRBYs writes the
+      // counter (the last of the freezing request, else the bucket's last descriptor).
+      if (!(x.flags & HB_FROZEN_PRE)) {
+        Slot* slot = reinterpret_cast<Slot*>(x.slot);
+        if (rstar != SEG_NO_FREEZE) {
+          if (r.req == rstar && (p + 1 == end || brec[p + 1].req != rstar)) {
+            slot->count = x.base + o.P;
+            slot->flags = SLOT_FROZEN;
+          }
+        } else if (p + 1 == end) {
+          slot->count = x.base + o.P;
+        }
+      }
     }
     for (int d = 32; d >= 1; d >>= 1) heads += __shfl_xor(heads, d, 64);
     if (lane == 0 && heads) atomicAdd(&s_heads, heads);
@@ -569,14 +745,18 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgroup(const uint64_t* __restric
   const uint32_t b1 = w1 >= msd_end ? NIL_BUCKET : first_bucket_at_or_after(w1);
   const uint32_t r0 = s_base[b0], r1 = s_base[b1];
   const uint32_t m = r1 - r0;
+#ifdef RL_BG_SKIP_MSD
+  if (tid == 0) wg_heads[blockIdx.x] = 0;
+  return;
+#endif
   if (m == 0) {
     if (tid == 0) wg_heads[blockIdx.x] = 0;
     return;
   }
+  BSTAMPV(9, m);
   // load (key, fp_lo, h, rule) of the range; identity order = perm
   for (uint32_t k = tid; k < m; k += BG_THREADS) {
-    const uint32_t idx = bidx[r0 + k];
-    const ItemRec r = recs[idx];
+    const ItemRec r = brec[r0 + k];
     s_key[k] = bkey[r0 + k];
     s_lo[k] = r.fp_lo;
     s_h[k] = r.h;
@@ -586,40 +766,69 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgroup(const uint64_t* __restric
   __syncthreads();
   // Stable grouping: 3 LDS radix passes on the 24 key bits below the bucket bits. Equal keys
   // end adjacent; different buckets never interleave (they arrive bucket by bucket).
-  lds_radix_pass(s_key, s_pa, s_pb, m, GK_SHIFT, s_cnt, s_dstart, sh_scan);
-  lds_radix_pass(s_key, s_pb, s_pa, m, GK_SHIFT + 8, s_cnt, s_dstart, sh_scan);
-  lds_radix_pass(s_key, s_pa, s_pb, m, GK_SHIFT + 16, s_cnt, s_dstart, sh_scan);
+#ifndef RL_BG_SKIP_RADIX
+  BSTAMP(2);
+  lds_radix_pass(s_key, s_pa, s_pb, m, GK_SHIFT, s_cnt, sh_w);
+  BSTAMP(3);
+  lds_radix_pass(s_key, s_pb, s_pa, m, GK_SHIFT + 8, s_cnt, sh_w);
+  BSTAMP(4);
+  lds_radix_pass(s_key, s_pa, s_pb, m, GK_SHIFT + 16, s_cnt, sh_w);
+  BSTAMP(5);
+#else
+  for (uint32_t k = tid; k < m; k += BG_THREADS) s_pb[k] = s_pa[k];
+  __syncthreads();
+#endif
   uint16_t* perm = s_pb;
-  // Runs of equal grouped bits holding two different identities (other region bits or a
-  // fingerprint collision on 35 bits): regroup them stably (one thread; rare and short).
+  // A run of equal grouped bits holding two identities (35-bit collision, ~1 per batch):
+  // regroup this range on 32 bits below the bucket bits; a collision on those 43 bits too
+  // (~1 in 300 batches) is regrouped by one thread (stable partition by full identity).
   for (uint32_t k = tid + 1; k < m; k += BG_THREADS) {
     const uint32_t a = perm[k - 1], b = perm[k];
     if (gkey(s_key[a]) == gkey(s_key[b]) && (s_key[a] != s_key[b] || s_lo[a] != s_lo[b])) s_mixed = 1;
   }
   __syncthreads();
-  if (s_mixed && tid == 0) {
-    uint32_t k = 0;
-    while (k < m) {
-      uint32_t e = k + 1;
-      while (e < m && gkey(s_key[perm[e]]) == gkey(s_key[perm[k]])) ++e;
-      // stable partition of perm[k..e) by identity, first-seen identity first
-      for (uint32_t s = k; s < e;) {
-        const uint32_t ref = perm[s];
-        uint32_t w = s + 1;
-        for (uint32_t t = s + 1; t < e; ++t) {
-          const uint32_t x = perm[t];
-          if (s_key[x] == s_key[ref] && s_lo[x] == s_lo[ref]) {
-            // move x to position w, shifting [w, t) right by one
-            for (uint32_t u = t; u > w; --u) perm[u] = perm[u - 1];
-            perm[w++] = (uint16_t)x;
-          }
-        }
-        s = w;
-      }
-      k = e;
+  if (s_mixed) {  // block-uniform
+    for (uint32_t k = tid; k < m; k += BG_THREADS) s_pa[k] = (uint16_t)k;
+    __syncthreads();
+    lds_radix_pass(s_key, s_pa, s_pb, m, GK_SHIFT - 8, s_cnt, sh_w);
+    lds_radix_pass(s_key, s_pb, s_pa, m, GK_SHIFT, s_cnt, sh_w);
+    lds_radix_pass(s_key, s_pa, s_pb, m, GK_SHIFT + 8, s_cnt, sh_w);
+    lds_radix_pass(s_key, s_pb, s_pa, m, GK_SHIFT + 16, s_cnt, sh_w);
+    for (uint32_t k = tid; k < m; k += BG_THREADS) s_pb[k] = s_pa[k];
+    __syncthreads();
+    if (tid == 0) s_mixed = 0;
+    __syncthreads();
+    for (uint32_t k = tid + 1; k < m; k += BG_THREADS) {
+      const uint32_t a = perm[k - 1], b = perm[k];
+      if ((s_key[a] << 3) >> (GK_SHIFT - 5) == (s_key[b] << 3) >> (GK_SHIFT - 5) &&
+          (s_key[a] != s_key[b] || s_lo[a] != s_lo[b]))
+        s_mixed = 1;
     }
+    __syncthreads();
+    if (s_mixed && tid == 0) {
+      uint32_t k = 0;
+      while (k < m) {
+        uint32_t e = k + 1;
+        while (e < m && gkey(s_key[perm[e]]) == gkey(s_key[perm[k]])) ++e;
+        for (uint32_t s = k; s < e;) {  // stable partition of perm[k..e), first-seen identity first
+          const uint32_t ref = perm[s];
+          uint32_t w = s + 1;
+          for (uint32_t t = s + 1; t < e; ++t) {
+            const uint32_t x = perm[t];
+            if (s_key[x] == s_key[ref] && s_lo[x] == s_lo[ref]) {
+              for (uint32_t u = t; u > w; --u) perm[u] = perm[u - 1];
+              perm[w++] = (uint16_t)x;
+            }
+          }
+          s = w;
+        }
+        k = e;
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
+  BSTAMP(6);
+  BSTAMPV(8, s_mixed);
   // Segmented inclusive prefix of h over the grouped order (blocked: BG_IPT per thread).
   const uint32_t k0 = tid * BG_IPT;
   BgScanEl t{0, 0, 0, 0};
@@ -659,6 +868,7 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgroup(const uint64_t* __restric
   for (uint32_t w = 0; w < wave; ++w) run = bg_op(run, s_wagg[w]);
   run = bg_op(run, wex);
   uint32_t heads = 0;
+  SortedRec mine[BG_IPT];
 #pragma unroll
   for (int q = 0; q < BG_IPT; ++q) {
     const uint32_t k = k0 + q;
@@ -666,33 +876,60 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgroup(const uint64_t* __restric
     const uint32_t x = perm[k];
     run = bg_op(run, BgScanEl{hd[q], rc[q], k, (unsigned long long)s_h[x]});
     heads += hd[q];
-    const uint32_t idx = bidx[r0 + x];
-    const ItemRec r = recs[idx];
+    const ItemRec r = brec[r0 + x];
     SortedRec o;
     o.P = run.s;
     o.head = (r0 + run.hp) | (run.o ? HEAD_MIXED_RULE : 0u);
-    o.idx = idx;
+    o.idx = r.pad;
     o.rule = r.rule;
     o.req = r.req;
     o.h = r.h;
     o.now_mod = r.now_mod;
+    mine[q] = o;
     srec[r0 + k] = o;
     skeys[r0 + k] = s_key[x];
   }
   for (int d = 32; d >= 1; d >>= 1) heads += __shfl_xor(heads, d, 64);
   if (lane == 0 && heads) atomicAdd(&s_heads, heads);
-  __syncthreads();
+  __syncthreads();  // the range's sorted records are visible to the whole workgroup
+  BSTAMP(7);
+  // Leader: one thread per segment tail — table probe/claim, INCRBY of the segment in
+  // serial order, local-cache freeze (every key of the range is complete in this range).
+  for (uint32_t k = tid; k < m; k += BG_THREADS) {
+    const uint32_t j = r0 + k;
+    if (k + 1 < m && (srec[j + 1].head & ~HEAD_MIXED_RULE) != j + 1) continue;  // not a tail
+    const SortedRec tail = srec[j];
+    const uint32_t hp = tail.head & ~HEAD_MIXED_RULE;
+    const bool mixed_rule = (tail.head & HEAD_MIXED_RULE) != 0;
+    if (j - hp + 1 >= HOT_CAND_MIN && !mixed_rule) emit_candidate(ctl, cand, tail.rule, j - hp + 1, srec[hp].idx);
+    leader_segment(hp, j, tail, mixed_rule, skeys, srec, recs, rules, tab, local_cache, seg, ctl);
+  }
+  __syncthreads();  // SegInfo of every segment of the range is visible
+#pragma unroll
+  for (int q = 0; q < BG_IPT; ++q) {
+    if (k0 + q >= m) break;
+    const SortedRec& o = mine[q];
+    decide_one(o, seg[o.head & ~HEAD_MIXED_RULE], rules[o.rule], out, req_thr);
+  }
   if (tid == 0) wg_heads[blockIdx.x] = s_heads;
 }
 
 // Hot-set candidates: recompute the prefix lane state (a, b) of each candidate's first
 // descriptor (the batch input is still resident).
 __global__ void k_cand_state(DevBatch in, const DevRule* __restrict__ rules, uint64_t seed, HotCand* cand,
-                             const EngineCtl* ctl) {
+                             const uint32_t* __restrict__ wg_heads, uint32_t n_heads, EngineCtl* ctl) {
+  if (blockIdx.x == 0 && n_heads) {
+    // U = segment heads of the batch (bucketed pipeline; single writer of n_segments)
+    uint32_t u = 0;
+    for (uint32_t t = threadIdx.x; t < n_heads; t += 64) u += wg_heads[t];
+    for (int d = 32; d >= 1; d >>= 1) u += __shfl_xor(u, d, 64);
+    if (threadIdx.x == 0) ctl->n_segments = u;
+  }
   const uint32_t i = blockIdx.x * 64 + threadIdx.x;
   const uint32_t nc = min((uint32_t)CAND_MAX, ctl->tile_ctr[CAND_CTR][0]);
   if (i >= nc) return;
   HotCand c = cand[i];
+  if (c.first_idx == 0xFFFFFFFFu) return;  // a hot key: state already known
   const uint32_t d = c.first_idx;
   const uint32_t o0 = in.off[d], o1 = in.off[d + 1];
   const uint32_t unit = rules[c.rule].unit;
@@ -714,7 +951,7 @@ uint32_t v2_hot_wgs(uint32_t n) { return n ? (n + HOT_CHUNK - 1) / HOT_CHUNK : 1
 void launch_fp2(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
                 const HotEntry* hot, uint64_t* keys_orig, ItemRec* recs, uint16_t* bkt, uint32_t* hbuf,
                 rl_status* out, uint32_t* req_thr, uint32_t* fpart, uint32_t* tcount, unsigned long long* thsum,
-                EngineCtl* ctl) {
+                HotBucket* hb, EngineCtl* ctl) {
   DevBatch d;
   d.n_desc = b.n_desc;
   d.n_req = b.n_req;
@@ -726,28 +963,32 @@ void launch_fp2(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_
   d.req_of = b.req_of;
   d.now = b.now;
   d.hits = b.hits_addend;
-  hipLaunchKernelGGL(k_fp2, dim3(v2_tiles(b.n_desc)), dim3(256), 0, st, d, rules, n_rules, seed, hot, keys_orig, recs,
-                     bkt, hbuf, out, req_thr, fpart, tcount, thsum, ctl);
+  hipLaunchKernelGGL(k_fp2, dim3(v2_tiles(b.n_desc)), dim3(V2_THREADS), 0, st, d, rules, n_rules, seed, hot,
+                     keys_orig, recs, bkt, hbuf, out, req_thr, fpart, v2_tiles(b.n_desc), tcount, thsum, hb, ctl);
 }
 void launch_bscan(hipStream_t st, const uint32_t* tcount, const unsigned long long* thsum, uint32_t n,
-                  uint32_t* toff, unsigned long long* hoff, uint32_t* btotal, const uint32_t* fpart, EngineCtl* ctl) {
-  hipLaunchKernelGGL(k_bscan, dim3(NBUCKETS + 1), dim3(256), 0, st, tcount, thsum, v2_tiles(n), toff, hoff, btotal,
-                     fpart, ctl);
+                  uint32_t* toff, unsigned long long* hoff, uint32_t* btotal, const uint32_t* fpart,
+                  const HotEntry* hot_list, HotBucket* hb, const TableDesc& tab, HotCand* cand, EngineCtl* ctl) {
+  hipLaunchKernelGGL(k_bscan, dim3((NBUCKETS + BSCAN_WAVES - 1) / BSCAN_WAVES + 1), dim3(256), 0, st, tcount, thsum,
+                     v2_tiles(n), toff, hoff, btotal, fpart, hot_list, hb, tab, cand, ctl);
 }
-void launch_bscatter(hipStream_t st, const uint64_t* keys_orig, const uint16_t* bkt, const uint32_t* hbuf, uint32_t n,
-                     const uint32_t* btotal, const uint32_t* toff, const unsigned long long* hoff, uint64_t* bkey,
-                     uint32_t* bidx, uint64_t* bP, EngineCtl* ctl) {
-  hipLaunchKernelGGL(k_bscatter, dim3(v2_tiles(n)), dim3(256), 0, st, keys_orig, bkt, hbuf, n, btotal, toff, hoff,
-                     bkey, bidx, bP, ctl);
+void launch_bscatter(hipStream_t st, const uint64_t* keys_orig, const ItemRec* recs, const uint16_t* bkt,
+                     const uint32_t* hbuf, uint32_t n, const uint32_t* btotal, const uint32_t* toff,
+                     const unsigned long long* hoff, uint64_t* bkey, ItemRec* brec, uint64_t* bP, uint32_t* bbase,
+                     HotBucket* hb, const DevRule* rules, int local_cache, EngineCtl* ctl) {
+  hipLaunchKernelGGL(k_bscatter, dim3(v2_tiles(n)), dim3(V2_THREADS), 0, st, keys_orig, recs, bkt, hbuf, n,
+                     v2_tiles(n), btotal, toff, hoff, bkey, brec, bP, bbase, hb, rules, local_cache, ctl);
 }
-void launch_bgroup(hipStream_t st, const uint64_t* bkey, const uint32_t* bidx, const uint64_t* bP,
-                   const ItemRec* recs, const uint32_t* btotal, uint32_t n, uint64_t* skeys, SortedRec* srec,
-                   uint32_t* wg_heads, EngineCtl* ctl) {
-  hipLaunchKernelGGL(k_bgroup, dim3(v2_msd_wgs(n) + v2_hot_wgs(n)), dim3(BG_THREADS), 0, st, bkey, bidx, bP, recs,
-                     btotal, v2_msd_wgs(n), skeys, srec, wg_heads, ctl);
+void launch_bgroup(hipStream_t st, const uint64_t* bkey, const ItemRec* brec, const uint64_t* bP,
+                   const uint32_t* bbase, uint32_t n, uint64_t* skeys, SortedRec* srec, uint32_t* wg_heads,
+                   const ItemRec* recs, const DevRule* rules, const TableDesc& tab, int local_cache, SegInfo* seg,
+                   const HotBucket* hb, rl_status* out, uint32_t* req_thr, HotCand* cand, EngineCtl* ctl) {
+  hipLaunchKernelGGL(k_bgroup, dim3(v2_msd_wgs(n) + v2_hot_wgs(n)), dim3(BG_THREADS), 0, st, bkey, brec, bP, bbase,
+                     v2_msd_wgs(n), skeys, srec, wg_heads, recs, rules, tab, local_cache, seg, hb, out, req_thr, cand,
+                     ctl);
 }
 void launch_cand_state(hipStream_t st, const rl_batch& b, const DevRule* rules, uint64_t seed, HotCand* cand,
-                       const EngineCtl* ctl) {
+                       const uint32_t* wg_heads, uint32_t n_heads, EngineCtl* ctl) {
   DevBatch d;
   d.n_desc = b.n_desc;
   d.n_req = b.n_req;
@@ -759,7 +1000,15 @@ void launch_cand_state(hipStream_t st, const rl_batch& b, const DevRule* rules, 
   d.req_of = b.req_of;
   d.now = b.now;
   d.hits = b.hits_addend;
-  hipLaunchKernelGGL(k_cand_state, dim3(CAND_MAX / 64), dim3(64), 0, st, d, rules, seed, cand, ctl);
+  hipLaunchKernelGGL(k_cand_state, dim3(CAND_MAX / 64), dim3(64), 0, st, d, rules, seed, cand, wg_heads, n_heads,
+                     ctl);
 }
 
 }  // namespace rlhip
+
+#ifdef RL_STAMPS
+extern "C" int rl_debug_bg_stamps(uint64_t* out, uint32_t nblocks) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(rlhip::g_bg_stamps), (size_t)nblocks * 10 * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

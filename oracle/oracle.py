@@ -124,6 +124,21 @@ def cache_key(prefix: bytes, unit: int, now: int) -> bytes:
     return buf.raw[:n]
 
 
+def fingerprints(blob: np.ndarray, off: np.ndarray, window_start: int, unit: int, seed: int):
+    """Fingerprints (hi, lo uint64 arrays) of every prefix blob[off[i]:off[i+1]]."""
+    n = len(off) - 1
+    hi = np.zeros(n, np.uint64)
+    lo = np.zeros(n, np.uint64)
+    L = lib()
+    L.rlo_fingerprint_many.restype = None
+    L.rlo_fingerprint_many.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64,
+                                       C.c_void_p, C.c_void_p]
+    blob = np.ascontiguousarray(blob, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    L.rlo_fingerprint_many(_p(blob), _p(off), n, window_start, unit, seed, _p(hi), _p(lo))
+    return hi, lo
+
+
 def fingerprint(prefix: bytes, window_start: int, unit: int, seed: int):
     hi, lo = C.c_uint64(), C.c_uint64()
     lib().rlo_fingerprint(prefix, len(prefix), window_start, unit, seed, C.byref(hi), C.byref(lo))

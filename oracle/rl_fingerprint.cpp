@@ -34,3 +34,10 @@ extern "C" void rlo_fingerprint(const uint8_t* prefix, uint32_t len, uint64_t wi
   *hi = fmix(a + rotl(b, 23));
   *lo = fmix(b ^ (a * 0xC4CEB9FE1A85EC53ull));
 }
+
+// Batch form over a prefix blob (test-fixture generation: searching fingerprint collisions).
+extern "C" void rlo_fingerprint_many(const uint8_t* blob, const uint32_t* off, uint32_t n, uint64_t window_start,
+                                     uint32_t unit, uint64_t seed, uint64_t* hi, uint64_t* lo) {
+  for (uint32_t i = 0; i < n; ++i)
+    rlo_fingerprint(blob + off[i], off[i + 1] - off[i], window_start, unit, seed, hi + i, lo + i);
+}

@@ -96,6 +96,8 @@ void rlo_local_cache_stats(rlo_engine* e, uint64_t* hit, uint64_t* miss, uint64_
  * fingerprint kernel (tests/test_fingerprint*.py); decisions above never use it. */
 void rlo_fingerprint(const uint8_t* prefix, uint32_t len, uint64_t window_start, uint32_t region, uint64_t seed,
                      uint64_t* hi, uint64_t* lo);
+void rlo_fingerprint_many(const uint8_t* blob, const uint32_t* off, uint32_t n, uint64_t window_start, uint32_t unit,
+                          uint64_t seed, uint64_t* hi, uint64_t* lo);
 
 #ifdef __cplusplus
 }

@@ -245,3 +245,31 @@ def test_error_paths():
     small.load_rules([(5, hiprl.SECOND)])
     with pytest.raises(hiprl.RedisError, match="full"):
         small.submit(hiprl.build_batch([("d", [[("a", str(i))]], [0], 1, 10) for i in range(100)]))
+
+
+@pytest.mark.parametrize("which", ["g35", "g43"])
+def test_grouping_collisions(which):
+    """Two keys whose fingerprints agree on the bucketed pipeline's grouping bits
+    (tests/golden/collisions.json), interleaved in one batch: a 35-bit collision is
+    regrouped in LDS on wider bits, a 43-bit one by the single-thread stable partition.
+    Either way the decisions are bit-exact and the batch stays on the bucketed pipeline."""
+    import json
+    from pathlib import Path
+    c = json.loads((Path(__file__).parent / "golden" / "collisions.json").read_text())
+    a, b = c["g35"] if which == "g35" else c["g43"]
+    rng = np.random.default_rng(3)
+    reqs = []
+    for i in range(20000):
+        if i % 97 == 0:
+            k = a if rng.random() < 0.5 else b
+            reqs.append(("coll", [[("k", k)]], [0], int(rng.integers(0, 3)), c["now"]))  # rule 0: L=1 SECOND
+        else:
+            reqs.append(("cold", [[("k", str(int(rng.integers(0, 50000))))]], [2], 1, c["now"]))
+    o = oracle.Oracle(near_limit_ratio=0.8, local_cache=True)
+    o.load_rules(RULES)
+    e = hiprl.Engine(local_cache=True, max_batch_desc=1 << 15, hash_seed=c["seed"])
+    e.load_rules(RULES)
+    (ost, othr) = streams.replay(o, reqs)
+    (gst, gthr) = streams.replay(e, reqs)
+    streams.assert_same(ost, othr, gst, gthr, which)
+    assert e.stats()["lsd_fallbacks"] == 0, e.stats()

@@ -1,12 +1,14 @@
 #!/bin/bash
 # Build timing variants of the HIP library (tools only; not used by the product).
+# Usage: tools/build_variants.sh "NAME:-DFLAG ..." ...
 set -e
 cd "$(dirname "$0")/../api-ratelimit_amd/csrc"
 mkdir -p ../../tools/variants
-for v in "A:-DRL_SORT_IPT=16 -DRL_SORT_LB_WIN=16" "B:-DRL_SORT_IPT=16 -DRL_SORT_LB_WIN=32" "C:-DRL_SORT_IPT=8 -DRL_SORT_LB_WIN=16" "D:-DRL_SORT_IPT=8 -DRL_SORT_LB_WIN=32" "E:-DRL_SORT_IPT=16 -DRL_SORT_LB_WIN=16 -DRL_SORT_TICKET" "F:-DRL_SORT_IPT=16 -DRL_SORT_LB_WIN=8"; do
+rm -f ../../tools/variants/lib_*.so
+for v in "$@"; do
   name=${v%%:*}; flags=${v#*:}
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -Wno-unused-result $flags -shared \
-     -o ../../tools/variants/lib_$name.so rl_kernels.hip rl_engine.cpp rl_cache.cpp -lpthread &
+     -o ../../tools/variants/lib_$name.so rl_kernels.hip rl_kernels_v2.hip rl_engine.cpp rl_cache.cpp -lpthread &
 done
 wait
-ls -la ../../tools/variants
+ls ../../tools/variants
