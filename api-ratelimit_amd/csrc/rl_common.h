@@ -193,6 +193,79 @@ struct __attribute__((aligned(16))) HotBucket {
 };
 constexpr uint32_t HB_FROZEN_PRE = 1u;
 
+// ---------------------------------------------------------------------------
+// v3 pipeline (rl_kernels_v3.hip)
+// ---------------------------------------------------------------------------
+constexpr int V3_TILE = 2048;             // k3_hist / k3_place arrival tile
+constexpr int V3_THREADS = 512;
+constexpr int V3_ROW16 = (NBUCKETS + 7) / 8 * 8;  // tile histogram row (u16 counts)
+constexpr int V3_SCAN_BUCKETS = HOT_BUCKETS + MSD_BUCKETS;  // buckets k3_scan scans (not NIL)
+constexpr int V3_GRANGE = 256;            // k3_group: MSD buckets whose start lies in one 256-window
+constexpr int V3_GCAP = 768;              // k3_group: records staged in LDS (larger ranges run in place)
+constexpr int V3_GHASH = 1024;            // k3_group: LDS hash slots (power of two, > V3_GCAP)
+constexpr int V3_RULE_BITS = 15;          // MRec.rn = rule | now_mod << 15 (now_mod < 86400 < 2^17)
+constexpr uint32_t V3_MAX_RULES = 1u << V3_RULE_BITS;
+constexpr int DFR_CTR = 29;               // EngineCtl::tile_ctr[DFR_CTR][0] counts deferred hot descriptors
+constexpr int SCAN_CTR = 28;              // EngineCtl::tile_ctr[SCAN_CTR][0]: k3_scan blocks done
+
+// Per-descriptor record in arrival order (32 B), written by k3_hist, read by k3_place.
+struct __attribute__((aligned(16))) ARec {
+  uint64_t kp;       // MSD: sort key; hot: INCRBY prefix of the key inside the tile (inclusive)
+  uint64_t lo;       // fp_lo
+  uint32_t req;      // request index
+  uint32_t h;        // max(1, hits_addend)
+  uint32_t rn;       // rule | now_mod << V3_RULE_BITS
+  uint16_t bucket;   // hot / MSD / NIL_BUCKET
+  uint16_t rank;     // MSD: position inside (tile, bucket)
+};
+
+// MSD descriptor in bucket order (32 B), written by k3_place, grouped by k3_group.
+struct __attribute__((aligned(16))) MRec {
+  uint64_t key;      // sort key (region | fp.hi >> 3)
+  uint64_t fp_lo;
+  uint32_t idx;      // arrival index
+  uint32_t req;      // request index
+  uint32_t h;        // max(1, hits_addend)
+  uint32_t rn;       // rule | now_mod << V3_RULE_BITS
+};
+
+// Per-batch state of one hot bucket (one key) in the v3 pipeline. k3_scan fills it (table
+// claim, counter before the batch, h total); k3_place records the freezing request.
+struct __attribute__((aligned(16))) HotBucket3 {
+  uint64_t key;
+  uint64_t fp_lo;
+  uint64_t base;    // counter before this batch
+  uint64_t slot;    // Slot* of the key; 0 = bucket empty (or batch rejected)
+  uint64_t total;   // sum of h over the bucket's descriptors
+  uint32_t rule;
+  uint32_t flags;   // HB_FROZEN_PRE
+  uint32_t rstar;   // request that froze the key in this batch (local cache), ~0 = none yet
+  uint32_t pad[3];
+};
+
+// Global scratch of k3_group for ranges too large for LDS (indexed by bucket-order position;
+// slot/cnt/base hold 4 words per position; base holds each key's list end).
+struct V3GroupScratch {
+  uint64_t* key;
+  uint64_t* lo;
+  uint4* pay;
+  uint64_t* P;
+  uint32_t* slot;
+  uint32_t* cnt;
+  uint32_t* base;
+  uint32_t* list;
+  uint32_t* grp;
+  uint32_t* rank;
+  uint32_t* tail;
+  uint32_t* cursor;  // one word per k3_group workgroup
+};
+
+// A hot descriptor whose decision needs the freezing request of an earlier tile (k3_group).
+struct __attribute__((aligned(16))) Deferred {
+  uint64_t P;        // INCRBY prefix of the key up to and including this descriptor
+  uint32_t idx, bucket, req, h, rule, now_mod;
+};
+
 constexpr int RADIX_BITS = 8;
 constexpr int RADIX = 1 << RADIX_BITS;
 constexpr int MAX_PASSES = 16;

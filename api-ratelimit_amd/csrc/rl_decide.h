@@ -53,6 +53,89 @@ RL_DEV bool table_claim(const TableDesc& tab, uint64_t key, uint64_t fp_lo, uint
   return slot != nullptr;
 }
 
+// First probe slot of a key in its region.
+RL_DEV Slot* slot_first(const TableDesc& tab, uint64_t key) {
+  const uint32_t region = key_region(key);
+  const uint32_t lg = tab.region_log2[region];
+  return tab.slots + tab.region_base[region] + (((key << 3) >> (64 - lg)) & ((1ull << lg) - 1ull));
+}
+
+// A whole 32-B slot, read ahead of its use with two 16-B loads (table_claim_pre).
+struct SlotView {
+  uint64_t ctrl, key;
+  uint32_t lohi, flags;
+  uint64_t count;
+};
+RL_DEV SlotView load_slot(const Slot* s) {
+  const uint4 a = reinterpret_cast<const uint4*>(s)[0];
+  const uint4 b = reinterpret_cast<const uint4*>(s)[1];
+  SlotView v;
+  v.ctrl = (uint64_t)a.x | ((uint64_t)a.y << 32);
+  v.key = (uint64_t)a.z | ((uint64_t)a.w << 32);
+  v.lohi = b.x;
+  v.flags = b.y;
+  v.count = (uint64_t)b.z | ((uint64_t)b.w << 32);
+  return v;
+}
+
+// table_claim with the first probe slot already read (pre). The read-ahead may predate a
+// concurrent claim of that slot by another key: a claim is permanent for the window
+// generation, so a stale "taken by another key" stays true, a stale "free" makes the CAS
+// fail and the slot is re-read. A key's own slot is only claimed by its own leader, and
+// count/flags are only written by that leader, so the read-ahead values of the key's slot
+// are current. Also returns the counter and flags of an existing slot.
+RL_DEV bool table_claim_pre(const TableDesc& tab, uint64_t key, uint64_t fp_lo, uint32_t G, const SlotView pre,
+                            Slot*& slot_out, bool& existed_out, uint64_t& count_out, uint32_t& flags_out) {
+  const uint32_t region = key_region(key);
+  const uint32_t lg = tab.region_log2[region];
+  const uint64_t mask = (1ull << lg) - 1ull;
+  Slot* rbase = tab.slots + tab.region_base[region];
+  uint64_t pos = (key << 3) >> (64 - lg);
+  const uint32_t tag = (uint32_t)fp_lo;
+  const uint32_t lohi = (uint32_t)(fp_lo >> 32);
+  bool use_pre = true;
+  slot_out = nullptr;
+  existed_out = false;
+  count_out = 0;
+  flags_out = 0;
+  for (uint32_t probe = 0; probe < MAX_PROBE;) {
+    Slot* s = rbase + (pos & mask);
+    uint64_t c, skey;
+    uint32_t slohi;
+    if (use_pre) {
+      c = pre.ctrl;
+      skey = pre.key;
+      slohi = pre.lohi;
+    } else {
+      c = ld_relaxed64(&s->ctrl);
+      skey = s->key;
+      slohi = s->fp_lo_hi;
+    }
+    const uint32_t g = (uint32_t)c;
+    if (g == G && (uint32_t)(c >> 32) == tag && skey == key && slohi == lohi) {
+      slot_out = s;
+      existed_out = true;
+      count_out = use_pre ? pre.count : s->count;
+      flags_out = use_pre ? pre.flags : s->flags;
+      return true;
+    }
+    if (g < G) {  // empty for this window generation: claim it
+      const unsigned long long want = ((unsigned long long)tag << 32) | G;
+      const unsigned long long old = atomicCAS((unsigned long long*)&s->ctrl, (unsigned long long)c, want);
+      if (old == c) {
+        slot_out = s;
+        return true;
+      }
+      use_pre = false;
+      continue;  // lost the race (or a stale read-ahead): re-examine this slot
+    }
+    use_pre = false;
+    ++pos;
+    ++probe;
+  }
+  return false;
+}
+
 // Report a long segment as a hot-set candidate for the next batch (bucketed pipeline).
 RL_DEV void emit_candidate(EngineCtl* ctl, HotCand* __restrict__ cand, uint32_t rule, uint32_t count,
                            uint32_t first_idx, uint64_t a = 0, uint64_t b = 0, uint32_t unit = 0) {

@@ -53,6 +53,22 @@ void launch_cand_state(hipStream_t, const rl_batch&, const DevRule*, uint64_t, H
                        EngineCtl*);
 void launch_decide(hipStream_t, const SortedRec*, const SegInfo*, const DevRule*, uint32_t, rl_status*, uint32_t*,
                    EngineCtl*);
+uint32_t v3_tiles(uint32_t n);
+uint32_t v3_group_wgs(uint32_t n);
+uint32_t v3_scan_blocks();
+void launch_v3_hist(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, const HotEntry*, uint32_t*,
+                    uint32_t*, uint16_t*, unsigned long long*, ARec*, EngineCtl*);
+void launch_v3_scan(hipStream_t, uint32_t, const uint16_t*, const unsigned long long*, uint32_t*, unsigned long long*,
+                    uint32_t*, const uint32_t*, const HotEntry*, HotBucket3*, const TableDesc&, int, HotCand*,
+                    uint32_t*, EngineCtl*);
+void launch_v3_bases(hipStream_t, uint32_t, const uint32_t*, uint32_t*, uint32_t*);
+void launch_v3_place(hipStream_t, uint32_t, const ARec*, const DevRule*, const uint32_t*, const unsigned long long*,
+                     const uint32_t*, HotBucket3*, int, MRec*, rl_status*, uint32_t*, Deferred*, EngineCtl*);
+void launch_v3_group(hipStream_t, uint32_t, const MRec*, const uint32_t*, const DevRule*, const TableDesc&, int,
+                     rl_status*, uint32_t*, const Deferred*, const HotBucket3*, HotCand*, const V3GroupScratch&,
+                     uint32_t*, EngineCtl*);
+void launch_v3_tail(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, const uint32_t*, uint32_t,
+                    EngineCtl*, EngineCtl*);
 }  // namespace rlhip
 
 using namespace rlhip;
@@ -61,13 +77,16 @@ namespace {
 
 enum KernelId {
   KT_FINGERPRINT, KT_HISTOGRAM, KT_HIST_SCAN, KT_SORT_PASS, KT_SCAN, KT_LEADER, KT_DECIDE, KT_FALLBACK, KT_MEMSET,
-  KT_FP2, KT_BSCAN, KT_BSCATTER, KT_BGROUP, KT_CAND, KT_COUNT
+  KT_FP2, KT_BSCAN, KT_BSCATTER, KT_BGROUP, KT_CAND, KT_V3_HIST, KT_V3_SCAN, KT_V3_PLACE, KT_V3_GROUP, KT_V3_TAIL,
+  KT_V3_BASES, KT_COUNT
 };
 const char* const kKernelNames[KT_COUNT] = {"k_fingerprint", "k_histogram", "k_hist_scan", "k_sort_pass", "k_scan",
                                             "k_leader",      "k_decide",    "fallback",    "memset",      "k_fp2",
-                                            "k_bscan",       "k_bscatter",  "k_bgroup",    "k_cand_state"};
+                                            "k_bscan",       "k_bscatter",  "k_bgroup",    "k_cand_state",
+                                            "k3_hist",       "k3_scan",     "k3_place",    "k3_group",
+                                            "k3_tail",       "k3_bases"};
 
-enum Mode { MODE_V2 = 0, MODE_LSD = 1, MODE_LSD_FULL = 2 };
+enum Mode { MODE_V2 = 0, MODE_LSD = 1, MODE_LSD_FULL = 2, MODE_V3 = 3 };
 
 // Hot-key set kept on the host between batches (v2 bucketing).
 struct HotKey {
@@ -131,6 +150,22 @@ struct rl_engine {
   HotCand* h_cand = nullptr;            // pinned copy
   std::vector<HotKey> hot;              // current hot-key set (index = hot idx)
   bool hot_dirty = false;
+  // v3 pipeline
+  uint16_t* v3_tcount = nullptr;            // [tile][V3_ROW16]
+  uint32_t* v3_toff = nullptr;              // [tile][MSD_BUCKETS]
+  unsigned long long* v3_thsum = nullptr;   // [tile][HOT_BUCKETS]
+  unsigned long long* v3_hoff = nullptr;    // [tile][HOT_BUCKETS]
+  MRec* v3_mrec = nullptr;                  // MSD records in bucket order
+  Deferred* v3_dfr = nullptr;               // deferred hot descriptors
+  HotBucket3* v3_hb = nullptr;              // per hot bucket batch state
+  uint32_t* v3_rng = nullptr;               // k3_group range starts
+  uint32_t* v3_bbase = nullptr;             // MSD bucket start positions
+  ARec* v3_arec = nullptr;                  // per-descriptor records (arrival order)
+  V3GroupScratch v3_gs{};                   // k3_group scratch for ranges too large for LDS
+  uint32_t* v3_heads = nullptr;             // per-workgroup unique-key counts (k3_group, then k3_scan)
+  EngineCtl* v3_ctl[2] = {nullptr, nullptr};  // control blocks: batch k uses [k&1], k3_tail clears the other
+  uint32_t v3_cur = 0;
+  bool want_cand = true;                    // copy the hot-set candidates back after this batch
   uint8_t* zero_block = nullptr;  // ctl | hist | lookbacks (zeroed per batch)
   size_t zero_cap = 0;
   EngineCtl* h_ctl = nullptr;     // pinned copy of the control block
@@ -201,6 +236,11 @@ struct rl_engine {
   }
 
   int run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, int mode);
+  int default_mode() const {
+    if (cfg.flags & RL_CFG_LSD_ONLY) return MODE_LSD;
+    if (cfg.flags & RL_CFG_V2) return MODE_V2;
+    return n_rules <= V3_MAX_RULES ? MODE_V3 : MODE_LSD;  // MRec packs the rule id in 15 bits
+  }
   int finish();
   int upload_hot();
   void update_hot(uint32_t n_cand);
@@ -219,6 +259,50 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   uint64_t* lb_head = reinterpret_cast<uint64_t*>(zero_block + z.lb_head);
   const size_t lb_pass_stride = (size_t)sort_tiles(n > 0 ? n : 1) * RADIX;  // per-digit look-back words
   hipError_t e;
+  if (mode == MODE_V3) {
+    if (n == 0) {
+      hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
+      hipMemsetAsync(v3_ctl[v3_cur], 0, sizeof(EngineCtl), stream);
+      e = hipMemcpyAsync(h_ctl, v3_ctl[v3_cur], sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
+      return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpyAsync(ctl)");
+    }
+    if (hot_dirty) {
+      int rc = upload_hot();
+      if (rc) return rc;
+    }
+    EngineCtl* c3 = v3_ctl[v3_cur];
+    EngineCtl* c3n = v3_ctl[v3_cur ^ 1u];
+    const int lc = cfg.local_cache ? 1 : 0;
+    const uint32_t nw = v3_group_wgs(n);
+    timed(KT_V3_HIST, [&] {
+      launch_v3_hist(stream, b, d_rules, n_rules, cfg.hash_seed, d_hot, thr, fp_part, v3_tcount, v3_thsum, v3_arec,
+                     c3);
+    });
+    timed(KT_V3_SCAN, [&] {
+      launch_v3_scan(stream, n, v3_tcount, v3_thsum, v3_toff, v3_hoff, btotal, fp_part, d_hot + HOT_SLOTS, v3_hb, tab,
+                     lc, d_cand, v3_heads + nw + 1, c3);
+    });
+    timed(KT_V3_BASES, [&] { launch_v3_bases(stream, n, btotal, v3_bbase, v3_rng); });
+    timed(KT_V3_PLACE, [&] {
+      launch_v3_place(stream, n, v3_arec, d_rules, v3_toff, v3_hoff, v3_bbase, v3_hb, lc, v3_mrec, out, thr, v3_dfr,
+                      c3);
+    });
+    timed(KT_V3_GROUP, [&] {
+      launch_v3_group(stream, n, v3_mrec, v3_rng, d_rules, tab, lc, out, thr, v3_dfr, v3_hb, d_cand, v3_gs, v3_heads,
+                      c3);
+    });
+    timed(KT_V3_TAIL, [&] {
+      launch_v3_tail(stream, b, d_rules, cfg.hash_seed, d_cand, v3_heads, nw + 1 + v3_scan_blocks(), c3, c3n);
+    });
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "kernel launch");
+    e = hipMemcpyAsync(h_ctl, c3, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess && want_cand)
+      e = hipMemcpyAsync(h_cand, d_cand, sizeof(HotCand) * CAND_MAX, hipMemcpyDeviceToHost, stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(ctl)");
+    v3_cur ^= 1u;
+    return 0;
+  }
   timed(KT_MEMSET, [&] {
     // the bucketed pipeline keeps no look-back state: only the control block is cleared
     hipMemsetAsync(zero_block, 0, mode == MODE_V2 ? z.ctl + sizeof(EngineCtl) : z.total, stream);
@@ -488,14 +572,16 @@ int rl_engine::finish() {
   if (errs & ERR_NEED_RESORT) return fail(RL_EDEVICE, "full-fingerprint re-sort still found a mixed run");
   // Hot-set maintenance costs host time between batches: every batch while the set is
   // empty or after a fallback, else every 8th batch (a skewed stream's head moves slowly).
-  if (!(cfg.flags & RL_CFG_LSD_ONLY) && (hot.empty() || fell_back || (st.batches & 7) == 0))
-    update_hot(h_ctl->tile_ctr[CAND_CTR][0]);
+  if (!(cfg.flags & RL_CFG_LSD_ONLY) && (want_cand || fell_back)) update_hot(h_ctl->tile_ctr[CAND_CTR][0]);
   last_unique = h_ctl->n_segments;
   last_n = dev_batch.n_desc;
   last_req = dev_batch.n_req;
   last_blob = dev_batch.blob_bytes;
   st.batches += 1;
   st.descriptors += dev_batch.n_desc;
+  // Hot-set maintenance costs a candidate copy and host time between batches: every batch
+  // while the set is empty, else every 8th batch (a skewed stream's head moves slowly).
+  want_cand = hot.empty() || (st.batches & 7) == 0;
   for (int k = 0; k < INS_LINES; ++k) st.live_slots_hint += h_ctl->tile_ctr[INS_CTR0 + k][0];
   if (host_path) {
     if (dev_batch.n_desc) memcpy(user_out, h_out, (size_t)dev_batch.n_desc * sizeof(rl_status));
@@ -605,6 +691,37 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     chk(hipHostMalloc(&e->h_cand, sizeof(HotCand) * CAND_MAX, hipHostMallocDefault));
     e->hot_dirty = true;  // upload the empty table before the first batch
   }
+  {
+    const size_t T3 = v3_tiles((uint32_t)N);
+    chk(hipMalloc(&e->v3_tcount, T3 * V3_ROW16 * 2));
+    chk(hipMalloc(&e->v3_toff, T3 * MSD_BUCKETS * 4));
+    chk(hipMalloc(&e->v3_thsum, T3 * HOT_BUCKETS * 8));
+    chk(hipMalloc(&e->v3_hoff, T3 * HOT_BUCKETS * 8));
+    chk(hipMalloc(&e->v3_mrec, N * sizeof(MRec) + 64));
+    chk(hipMalloc(&e->v3_dfr, N * sizeof(Deferred) + 64));
+    chk(hipMalloc(&e->v3_hb, HOT_BUCKETS * sizeof(HotBucket3)));
+    chk(hipMalloc(&e->v3_rng, (v3_group_wgs((uint32_t)N) + 2) * 4));
+    chk(hipMalloc(&e->v3_bbase, (MSD_BUCKETS + 1) * 4));
+    chk(hipMalloc(&e->v3_arec, N * sizeof(ARec) + 64));
+    V3GroupScratch& g = e->v3_gs;
+    chk(hipMalloc(&g.key, N * 8 + 64));
+    chk(hipMalloc(&g.lo, N * 8 + 64));
+    chk(hipMalloc(&g.pay, N * 16 + 64));
+    chk(hipMalloc(&g.P, N * 8 + 64));
+    chk(hipMalloc(&g.slot, N * 16 + 64));
+    chk(hipMalloc(&g.cnt, N * 16 + 64));
+    chk(hipMalloc(&g.base, N * 16 + 64));
+    chk(hipMalloc(&g.list, N * 4 + 64));
+    chk(hipMalloc(&g.grp, N * 4 + 64));
+    chk(hipMalloc(&g.rank, N * 4 + 64));
+    chk(hipMalloc(&g.tail, N * 4 + 64));
+    chk(hipMalloc(&g.cursor, (v3_group_wgs((uint32_t)N) + 2) * 4));
+    chk(hipMalloc(&e->v3_heads, (v3_group_wgs((uint32_t)N) + 1 + v3_scan_blocks()) * 4 + 64));
+    for (int k = 0; k < 2; ++k) {
+      chk(hipMalloc(&e->v3_ctl[k], sizeof(EngineCtl)));
+      if (he == hipSuccess) chk(hipMemset(e->v3_ctl[k], 0, sizeof(EngineCtl)));
+    }
+  }
 
   e->zero_cap = e->zlayout((uint32_t)N, MAX_PASSES).total;
   chk(hipMalloc(&e->zero_block, e->zero_cap));
@@ -658,6 +775,23 @@ void rl_destroy(rl_engine* e) {
   hipFree(e->hbk);
   hipFree(e->d_cand);
   hipHostFree(e->h_cand);
+  hipFree(e->v3_tcount);
+  hipFree(e->v3_toff);
+  hipFree(e->v3_thsum);
+  hipFree(e->v3_hoff);
+  hipFree(e->v3_mrec);
+  hipFree(e->v3_dfr);
+  hipFree(e->v3_hb);
+  hipFree(e->v3_rng);
+  hipFree(e->v3_bbase);
+  hipFree(e->v3_arec);
+  for (void* p : {(void*)e->v3_gs.key, (void*)e->v3_gs.lo, (void*)e->v3_gs.pay, (void*)e->v3_gs.P,
+                  (void*)e->v3_gs.slot, (void*)e->v3_gs.cnt, (void*)e->v3_gs.base, (void*)e->v3_gs.list,
+                  (void*)e->v3_gs.grp, (void*)e->v3_gs.rank, (void*)e->v3_gs.tail, (void*)e->v3_gs.cursor})
+    hipFree(p);
+  hipFree(e->v3_heads);
+  hipFree(e->v3_ctl[0]);
+  hipFree(e->v3_ctl[1]);
 
   hipFree(e->zero_block);
   hipHostFree(e->h_ctl);
@@ -760,7 +894,7 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
   d.req_of = reinterpret_cast<const uint32_t*>(e->d_in + o_req);
   d.now = reinterpret_cast<const int64_t*>(e->d_in + o_now);
   d.hits_addend = reinterpret_cast<const uint32_t*>(e->d_in + o_hits);
-  int rc = e->run_pipeline(d, e->d_out, e->d_thr, (e->cfg.flags & RL_CFG_LSD_ONLY) ? MODE_LSD : MODE_V2);
+  int rc = e->run_pipeline(d, e->d_out, e->d_thr, e->default_mode());
   if (rc) return rc;
   e->dev_batch = d;
   e->pend_out_dev = e->d_out;
@@ -788,7 +922,7 @@ int rl_submit_device(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t
     return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req)", c.max_batch_desc,
                    c.max_batch_req);
   if (!e->d_rules) rl_load_rules(e, nullptr, 0);
-  int rc = e->run_pipeline(*b, d_out, d_req_throttle_ms, (e->cfg.flags & RL_CFG_LSD_ONLY) ? MODE_LSD : MODE_V2);
+  int rc = e->run_pipeline(*b, d_out, d_req_throttle_ms, e->default_mode());
   if (rc) return rc;
   e->dev_batch = *b;
   e->pend_out_dev = d_out;

@@ -37,6 +37,9 @@ STATUS_DTYPE = np.dtype([("code_flags", "<u4"), ("limit_remaining", "<u4"), ("re
                          ("over_limit_delta", "<u4"), ("near_limit_delta", "<u4")])
 
 
+PIPELINE_FLAGS = {"v3": 0, "lsd": 1, "v2": 2}  # rl_config.flags (RL_CFG_LSD_ONLY, RL_CFG_V2)
+
+
 class RlConfig(C.Structure):
     _fields_ = [("struct_size", C.c_uint32), ("device", C.c_int32), ("log2_slots", C.c_uint32 * 4),
                 ("near_limit_ratio", C.c_float), ("local_cache", C.c_uint32), ("per_second_split", C.c_uint32),
@@ -186,7 +189,15 @@ class Engine:
     def __init__(self, device: int = 0, log2_slots=(16, 16, 16, 14), near_limit_ratio: float = 0.8,
                  local_cache: bool = False, per_second_split: bool = False, max_batch_desc: int = 1 << 16,
                  max_batch_req: Optional[int] = None, max_blob_bytes: Optional[int] = None, sort_bits: int = 48,
-                 hash_seed: int = 0x5EE7AB1E5EED, lib_path: Optional[os.PathLike] = None, lsd_only: bool = False):
+                 hash_seed: int = 0x5EE7AB1E5EED, lib_path: Optional[os.PathLike] = None, lsd_only: bool = False,
+                 pipeline: str = "v3"):
+        """pipeline: "v3" (default: hot keys decided in place, MSD buckets grouped in LDS),
+        "v2" (bucketed pipeline kept for comparison) or "lsd" (radix-sort pipeline, also the
+        fallback of the other two). lsd_only=True is pipeline="lsd"."""
+        if lsd_only:
+            pipeline = "lsd"
+        if pipeline not in PIPELINE_FLAGS:
+            raise ValueError(f"pipeline must be one of {sorted(PIPELINE_FLAGS)}")
         self.lib = load_library(lib_path)
         cfg = RlConfig()
         cfg.struct_size = C.sizeof(RlConfig)
@@ -200,7 +211,7 @@ class Engine:
         cfg.max_batch_req = max_batch_req or max_batch_desc
         cfg.max_blob_bytes = max_blob_bytes or max_batch_desc * 64
         cfg.sort_bits = sort_bits
-        cfg.flags = 1 if lsd_only else 0
+        cfg.flags = PIPELINE_FLAGS[pipeline]
         cfg.hash_seed = hash_seed
         self.cfg = cfg
         h = C.c_void_p()
@@ -263,7 +274,7 @@ class Engine:
         self._check(self.lib.rl_set_timing(self.h, int(on)), "rl_set_timing")
 
     def kernel_times(self) -> dict:
-        cap = 16
+        cap = 32
         names = (C.c_char_p * cap)()
         ms = (C.c_double * cap)()
         cnt = (C.c_uint64 * cap)()

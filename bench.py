@@ -44,8 +44,8 @@ def parse():
     ap.add_argument("--desc", type=int, default=1_000_000, help="descriptors per batch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-kernel-times", action="store_true")
-    ap.add_argument("--pipeline", choices=["bucketed", "lsd"], default="bucketed",
-                    help="decision pipeline (bucketed default; lsd = radix-sort pipeline only)")
+    ap.add_argument("--pipeline", choices=["v3", "v2", "lsd"], default="v3",
+                    help="decision pipeline (v3 default; v2 = bucketed pipeline; lsd = radix-sort pipeline only)")
     ap.add_argument("--json-out", type=str, default="")
     return ap.parse_args()
 
@@ -88,7 +88,7 @@ def main():
 
     eng = hiprl.Engine(device=local, log2_slots=log2, max_batch_desc=d, max_batch_req=d,
                        max_blob_bytes=max(int(hb.blob.shape[0]) for hb in host_batches) + 64, sort_bits=48,
-                       lsd_only=args.pipeline == "lsd")
+                       pipeline=args.pipeline)
     eng.load_rules(rules)
 
     def upload(hb):

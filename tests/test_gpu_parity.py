@@ -72,11 +72,14 @@ def batch_sizes(reqs, rng, max_bs):
     return sizes
 
 
-def run_both(reqs, sizes, local_cache, sort_bits=48, ratio=0.8, lsd_only=False):
+PIPELINES = ["v3", "v2", "lsd"]
+
+
+def run_both(reqs, sizes, local_cache, sort_bits=48, ratio=0.8, lsd_only=False, pipeline="v3"):
     o = oracle.Oracle(near_limit_ratio=ratio, local_cache=local_cache)
     o.load_rules(RULES)
     e = hiprl.Engine(near_limit_ratio=ratio, local_cache=local_cache, sort_bits=sort_bits, max_batch_desc=1 << 17,
-                     lsd_only=lsd_only)
+                     lsd_only=lsd_only, pipeline=pipeline)
     e.load_rules(RULES)
     a = streams.replay(o, reqs, sizes)
     b = streams.replay(e, reqs, sizes)
@@ -84,14 +87,14 @@ def run_both(reqs, sizes, local_cache, sort_bits=48, ratio=0.8, lsd_only=False):
     return a, b, e
 
 
-@pytest.mark.parametrize("lsd_only", [False, True], ids=["bucketed", "lsd"])
+@pytest.mark.parametrize("pipeline", PIPELINES)
 @pytest.mark.parametrize("local_cache", [False, True])
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_random_streams(seed, local_cache, lsd_only):
+def test_random_streams(seed, local_cache, pipeline):
     reqs = make_stream(seed, 6000, t0=1_700_000_000 - 7 + seed * 3600 * 24 - 130)
     sizes = batch_sizes(reqs, np.random.default_rng(seed + 100), 1500)
-    (ost, othr), (gst, gthr), _ = run_both(reqs, sizes, local_cache, lsd_only=lsd_only)
-    streams.assert_same(ost, othr, gst, gthr, f"seed={seed} local={local_cache} lsd={lsd_only}")
+    (ost, othr), (gst, gthr), _ = run_both(reqs, sizes, local_cache, pipeline=pipeline)
+    streams.assert_same(ost, othr, gst, gthr, f"seed={seed} local={local_cache} pipeline={pipeline}")
 
 
 @pytest.mark.parametrize("sort_bits", [8, 16, 64])
@@ -119,9 +122,9 @@ def test_hot_key_long_segments():
         else:
             reqs.append(("hot", [[("k", f"c{i % 997}")]], [1 + 4], 1, t))
     for lc in (False, True):
-        for lsd in (False, True):
-            (ost, othr), (gst, gthr), _ = run_both(reqs, [len(reqs)], lc, lsd_only=lsd)
-            streams.assert_same(ost, othr, gst, gthr, f"hot local={lc} lsd={lsd}")
+        for pl in PIPELINES:
+            (ost, othr), (gst, gthr), _ = run_both(reqs, [len(reqs)], lc, pipeline=pl)
+            streams.assert_same(ost, othr, gst, gthr, f"hot local={lc} pipeline={pl}")
 
 
 def hot_stream(n_batches, per_batch, t0, rule_of=None, seed=0):
@@ -149,12 +152,13 @@ def hot_stream(n_batches, per_batch, t0, rule_of=None, seed=0):
     return reqs, sizes
 
 
+@pytest.mark.parametrize("pipeline", ["v3", "v2"])
 @pytest.mark.parametrize("local_cache", [False, True])
-def test_hot_set_across_batches(local_cache):
-    """The bucketed pipeline learns hot keys from one batch and gives them their own
+def test_hot_set_across_batches(local_cache, pipeline):
+    """The bucketed pipelines learn hot keys from one batch and give them their own
     buckets in the next; results stay bit-exact as they roll over windows."""
     reqs, sizes = hot_stream(6, 12000, t0=1_700_000_000 - 3, seed=local_cache)
-    (ost, othr), (gst, gthr), eng = run_both(reqs, sizes, local_cache)
+    (ost, othr), (gst, gthr), eng = run_both(reqs, sizes, local_cache, pipeline=pipeline)
     streams.assert_same(ost, othr, gst, gthr, f"hotset local={local_cache}")
     s = eng.stats()
     assert s["hot_keys"] >= 2, s  # h0, h1 always; h2..h7 hover around HOT_MIN_SEG
@@ -163,13 +167,14 @@ def test_hot_set_across_batches(local_cache):
     assert s["live_slots_hint"] == eng.ref_oracle.num_keys(), s  # one insert per (key, window)
 
 
-def test_hot_key_changes_rule():
+@pytest.mark.parametrize("pipeline", ["v3", "v2"])
+def test_hot_key_changes_rule(pipeline):
     """A hot key submitted under a second rule in a later batch sends that batch to the
     LSD pipeline (before anything touches the table); results stay bit-exact."""
     def rule_of(b, k, r):
         return 1 if (b == 3 and k == "h0") else r   # same unit (SECOND), other limit
     reqs, sizes = hot_stream(5, 8000, t0=1_700_000_100, rule_of=rule_of, seed=7)
-    (ost, othr), (gst, gthr), eng = run_both(reqs, sizes, True)
+    (ost, othr), (gst, gthr), eng = run_both(reqs, sizes, True, pipeline=pipeline)
     streams.assert_same(ost, othr, gst, gthr, "hot rule change")
     assert eng.stats()["lsd_fallbacks"] >= 1
 
@@ -273,3 +278,42 @@ def test_grouping_collisions(which):
     (gst, gthr) = streams.replay(e, reqs)
     streams.assert_same(ost, othr, gst, gthr, which)
     assert e.stats()["lsd_fallbacks"] == 0, e.stats()
+
+
+@pytest.mark.parametrize("L", [500, 3000, 20])
+def test_hot_freeze_in_straddling_request(L):
+    """v3 decides hot keys in arrival-order tiles of 2048 descriptors. When the local cache
+    freezes a hot key inside a request that continues into later tiles, those later
+    descriptors still INCRBY (all lookups of a request precede its Sets,
+    fixed_cache_impl.go:55-86); requests after it are local-cache hits. Long requests of
+    one hot key start mid-tile and straddle 1-3 tile boundaries."""
+    t = 1_700_000_500
+    def batch(b, n):
+        reqs = []
+        rng = np.random.default_rng(b)
+        while len(reqs) < n:
+            x = rng.random()
+            if x < 0.002:
+                # one request holding many descriptors of the hot key
+                k = int(rng.integers(300, 5000))
+                reqs.append(("st", [[("k", "hot")]] * k, [3] * k, 1, t + b))
+            elif x < 0.5:
+                reqs.append(("st", [[("k", "hot")]], [3], int(rng.integers(0, 3)), t + b))
+            else:
+                reqs.append(("st", [[("k", f"c{int(rng.integers(0, 3000))}")]], [1], 1, t + b))
+        return reqs
+    rules = [(L, u) for u in UNITS for L in (1, 3, 10, 40)]
+    rules[3] = (L, hiprl.SECOND)  # a new window every batch: the key freezes again in each
+    reqs, sizes = [], []
+    for b in range(4):
+        r = batch(b, 3000)
+        reqs += r
+        sizes.append(len(r))
+    o = oracle.Oracle(near_limit_ratio=0.8, local_cache=True)
+    o.load_rules(rules)
+    e = hiprl.Engine(near_limit_ratio=0.8, local_cache=True, max_batch_desc=1 << 17)
+    e.load_rules(rules)
+    a = streams.replay(o, reqs, sizes)
+    g = streams.replay(e, reqs, sizes)
+    streams.assert_same(*a, *g, f"straddle L={L}")
+    assert e.stats()["hot_keys"] >= 1
