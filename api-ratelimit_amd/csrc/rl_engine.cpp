@@ -61,12 +61,12 @@ void launch_v3_hist(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint
 void launch_v3_scan(hipStream_t, uint32_t, const uint16_t*, const unsigned long long*, uint32_t*, unsigned long long*,
                     uint32_t*, const uint32_t*, const HotEntry*, HotBucket3*, const TableDesc&, int, HotCand*,
                     uint32_t*, EngineCtl*);
-void launch_v3_bases(hipStream_t, uint32_t, const uint32_t*, uint32_t*, uint32_t*);
+void launch_v3_bases(hipStream_t, uint32_t, const uint32_t*, uint32_t*, uint32_t*, uint32_t*);
 void launch_v3_place(hipStream_t, uint32_t, const ARec*, const DevRule*, const uint32_t*, const unsigned long long*,
                      const uint32_t*, HotBucket3*, int, MRec*, rl_status*, uint32_t*, Deferred*, EngineCtl*);
 void launch_v3_group(hipStream_t, uint32_t, const MRec*, const uint32_t*, const DevRule*, const TableDesc&, int,
-                     rl_status*, uint32_t*, const Deferred*, const HotBucket3*, HotCand*, const V3GroupScratch&,
-                     uint32_t*, EngineCtl*);
+                     rl_status*, uint32_t*, const Deferred*, const HotBucket3*, HotCand*, int, const uint32_t*,
+                     const uint32_t*, const V3GroupScratch&, uint32_t*, EngineCtl*);
 void launch_v3_tail(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, const uint32_t*, uint32_t,
                     EngineCtl*, EngineCtl*);
 }  // namespace rlhip
@@ -160,6 +160,7 @@ struct rl_engine {
   HotBucket3* v3_hb = nullptr;              // per hot bucket batch state
   uint32_t* v3_rng = nullptr;               // k3_group range starts
   uint32_t* v3_bbase = nullptr;             // MSD bucket start positions
+  uint32_t* v3_rngb = nullptr;              // k3_group range: index of its first bucket
   ARec* v3_arec = nullptr;                  // per-descriptor records (arrival order)
   V3GroupScratch v3_gs{};                   // k3_group scratch for ranges too large for LDS
   uint32_t* v3_heads = nullptr;             // per-workgroup unique-key counts (k3_group, then k3_scan)
@@ -282,14 +283,14 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
       launch_v3_scan(stream, n, v3_tcount, v3_thsum, v3_toff, v3_hoff, btotal, fp_part, d_hot + HOT_SLOTS, v3_hb, tab,
                      lc, d_cand, v3_heads + nw + 1, c3);
     });
-    timed(KT_V3_BASES, [&] { launch_v3_bases(stream, n, btotal, v3_bbase, v3_rng); });
+    timed(KT_V3_BASES, [&] { launch_v3_bases(stream, n, btotal, v3_bbase, v3_rng, v3_rngb); });
     timed(KT_V3_PLACE, [&] {
       launch_v3_place(stream, n, v3_arec, d_rules, v3_toff, v3_hoff, v3_bbase, v3_hb, lc, v3_mrec, out, thr, v3_dfr,
                       c3);
     });
     timed(KT_V3_GROUP, [&] {
-      launch_v3_group(stream, n, v3_mrec, v3_rng, d_rules, tab, lc, out, thr, v3_dfr, v3_hb, d_cand, v3_gs, v3_heads,
-                      c3);
+      launch_v3_group(stream, n, v3_mrec, v3_rng, d_rules, tab, lc, out, thr, v3_dfr, v3_hb, d_cand, want_cand ? 1 : 0,
+                      v3_rngb, v3_bbase, v3_gs, v3_heads, c3);
     });
     timed(KT_V3_TAIL, [&] {
       launch_v3_tail(stream, b, d_rules, cfg.hash_seed, d_cand, v3_heads, nw + 1 + v3_scan_blocks(), c3, c3n);
@@ -702,6 +703,7 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     chk(hipMalloc(&e->v3_hb, HOT_BUCKETS * sizeof(HotBucket3)));
     chk(hipMalloc(&e->v3_rng, (v3_group_wgs((uint32_t)N) + 2) * 4));
     chk(hipMalloc(&e->v3_bbase, (MSD_BUCKETS + 1) * 4));
+    chk(hipMalloc(&e->v3_rngb, (v3_group_wgs((uint32_t)N) + 2) * 4));
     chk(hipMalloc(&e->v3_arec, N * sizeof(ARec) + 64));
     V3GroupScratch& g = e->v3_gs;
     chk(hipMalloc(&g.key, N * 8 + 64));
@@ -784,6 +786,7 @@ void rl_destroy(rl_engine* e) {
   hipFree(e->v3_hb);
   hipFree(e->v3_rng);
   hipFree(e->v3_bbase);
+  hipFree(e->v3_rngb);
   hipFree(e->v3_arec);
   for (void* p : {(void*)e->v3_gs.key, (void*)e->v3_gs.lo, (void*)e->v3_gs.pay, (void*)e->v3_gs.P,
                   (void*)e->v3_gs.slot, (void*)e->v3_gs.cnt, (void*)e->v3_gs.base, (void*)e->v3_gs.list,

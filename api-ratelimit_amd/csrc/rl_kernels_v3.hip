@@ -649,7 +649,7 @@ __global__ __launch_bounds__(SCAN_NT) void k3_scan(const uint16_t* __restrict__ 
           atomicOr(&ctl->err, ERR_V2_FALLBACK);
         heads = 1;
       }
-      count_inserts(slot != nullptr && !existed, ctl);
+      if (slot != nullptr && !existed) heads |= 1u << 16;  // a new table slot
       if (ctot >= HOT_CAND_MIN) emit_candidate(ctl, cand, he.rule, ctot, 0xFFFFFFFFu, he.a, he.b, he.unit);
     }
     hb[b] = x;
@@ -667,7 +667,8 @@ __global__ __launch_bounds__(SCAN_NT) void k3_scan(const uint16_t* __restrict__ 
 // start of its first bucket).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(SCAN_NT) void k3_bases(const uint32_t* __restrict__ btotal, uint32_t* __restrict__ bbase,
-                                                    uint32_t* __restrict__ rng, uint32_t n_ranges) {
+                                                    uint32_t* __restrict__ rng, uint32_t* __restrict__ rngb,
+                                                    uint32_t n_ranges) {
   __shared__ uint32_t s_base[MSD_BUCKETS + 1];
   __shared__ uint32_t sh_w[SCAN_W];
   const uint32_t tid = threadIdx.x;
@@ -696,11 +697,17 @@ __global__ __launch_bounds__(SCAN_NT) void k3_bases(const uint32_t* __restrict__
     const uint32_t hi = s_base[bb];
     const uint32_t lo = bb == 0 ? 0u : s_base[bb - 1] + 1u;
     const uint32_t wend = min(n_ranges, hi / (uint32_t)V3_GRANGE);
-    for (uint32_t w = (lo + V3_GRANGE - 1) / V3_GRANGE; w <= wend; ++w) rng[w] = hi;
+    for (uint32_t w = (lo + V3_GRANGE - 1) / V3_GRANGE; w <= wend; ++w) {
+      rng[w] = hi;
+      rngb[w] = bb;
+    }
   }
   // ranges starting after the last bucket's start: empty (all threads share the fill)
   const uint32_t last = s_base[MSD_BUCKETS - 1] + 1u;
-  for (uint32_t w = (last + V3_GRANGE - 1) / V3_GRANGE + tid; w <= n_ranges; w += SCAN_NT) rng[w] = total;
+  for (uint32_t w = (last + V3_GRANGE - 1) / V3_GRANGE + tid; w <= n_ranges; w += SCAN_NT) {
+    rng[w] = total;
+    rngb[w] = MSD_BUCKETS;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1017,17 +1024,18 @@ RL_DEV void group_scan(const GStore& g, uint32_t m, LSeg* s_agg, LSeg* s_carry) 
 // serial order, local-cache freeze (fixed_cache_impl.go:55-123, base_limiter.go:88-106).
 RL_DEV void group_lead(const GStore& g, uint32_t k, uint64_t key, uint64_t lo, uint32_t rule,
                        const DevRule* __restrict__ rules, const TableDesc& tab, int local_cache, HotCand* cand,
-                       EngineCtl* ctl, bool has_pre, const SlotView pre, uint64_t& base_out,
-                       uint32_t& freeze_out) {
+                       EngineCtl* ctl, bool has_pre, const SlotView pre, int cand_on, uint64_t& base_out,
+                       uint32_t& freeze_out, bool& inserted) {
   base_out = 0;
   freeze_out = SEG_NO_FREEZE;
   const uint32_t s = g.grp[k];
   const uint32_t n = g.cnt[s], e1 = g.end[s], e0 = e1 - n;
   const uint64_t Pk = g.P[k];
   bool mixed = false;
-  if (n >= HOT_CAND_MIN || local_cache) {
+  inserted = false;
+  if ((cand_on && n >= HOT_MIN_SEG) || local_cache) {
     for (uint32_t e = e0; e < e1; ++e) mixed |= rule_of(g.recs[g.list[e]].rn) != rule;
-    if (n >= HOT_CAND_MIN && !mixed) emit_candidate(ctl, cand, rule, n, g.pay[g.list[e0]].x);
+    if (cand_on && n >= HOT_MIN_SEG && !mixed) emit_candidate(ctl, cand, rule, n, g.pay[g.list[e0]].x);
   }
   const uint32_t gen = ctl->gen_max[key_region(key)];  // the region's one generation (k3_scan)
   Slot* slot = nullptr;
@@ -1049,7 +1057,7 @@ RL_DEV void group_lead(const GStore& g, uint32_t k, uint64_t key, uint64_t lo, u
     slot->key = key;
     slot->fp_lo_hi = (uint32_t)(lo >> 32);
   }
-  count_inserts(!existed, ctl);
+  inserted = !existed;
   uint32_t freeze = SEG_NO_FREEZE;
   uint64_t final_count = base + Pk;
   if (frozen_pre) {
@@ -1082,14 +1090,15 @@ RL_DEV void group_lead(const GStore& g, uint32_t k, uint64_t key, uint64_t lo, u
 
 RL_DEV uint32_t group_tail(const GStore& g, uint32_t k) { return g.list[g.end[g.grp[k]] - 1u]; }
 
-// All phases of one range; returns the keys this thread led. The LDS path (m <= G_CAP, at
+// All phases of one range; returns the keys this thread led (low 16 bits) and the new table
+// slots they claimed (high 16 bits). The LDS path (m <= G_CAP, at
 // most G_IPT records per thread) reads each record's first table slot ahead, right after
 // staging, so the leaders' table probes overlap the grouping.
 template <bool LDS>
 RL_DEV uint32_t group_range(const GStore& g, uint32_t hs, const MRec* __restrict__ recs, uint32_t m,
                             const DevRule* __restrict__ rules, const TableDesc& tab, int local_cache,
-                            rl_status* __restrict__ out, uint32_t* __restrict__ req_thr, HotCand* cand, LSeg* s_agg,
-                            LSeg* s_carry, EngineCtl* ctl) {
+                            rl_status* __restrict__ out, uint32_t* __restrict__ req_thr, HotCand* cand, int cand_on,
+                            LSeg* s_agg, LSeg* s_carry, EngineCtl* ctl) {
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
   uint32_t heads = 0;
   for (uint32_t s = tid; s < hs; s += G_NT) {
@@ -1151,8 +1160,10 @@ RL_DEV uint32_t group_range(const GStore& g, uint32_t hs, const MRec* __restrict
       const uint64_t key = g.key[k], lo = g.lo[k];                                                   \
       uint64_t base;                                                                                 \
       uint32_t frz;                                                                                  \
-      group_lead(g, k, key, lo, rule_of(own##J.w), rules, tab, local_cache, cand, ctl, true, pre##J, base, \
-                 frz);                                                                               \
+      bool ins;                                                                                      \
+      group_lead(g, k, key, lo, rule_of(own##J.w), rules, tab, local_cache, cand, ctl, true, pre##J, cand_on, \
+                 base, frz, ins);                                                                    \
+      heads += ins ? 1u << 16 : 0u;                                                                  \
       g.key[k] = base;                                                                               \
       g.lo[k] = frz;                                                                                 \
     }                                                                                                \
@@ -1168,7 +1179,10 @@ RL_DEV uint32_t group_range(const GStore& g, uint32_t hs, const MRec* __restrict
       const uint64_t key = g.key[k], lo = g.lo[k];
       uint64_t base;
       uint32_t frz;
-      group_lead(g, k, key, lo, rule_of(recs[k].rn), rules, tab, local_cache, cand, ctl, false, pre0, base, frz);
+      bool ins;
+      group_lead(g, k, key, lo, rule_of(recs[k].rn), rules, tab, local_cache, cand, ctl, false, pre0, cand_on, base,
+                 frz, ins);
+      heads += ins ? 1u << 16 : 0u;
       g.key[k] = base;
       g.lo[k] = frz;
     }
@@ -1201,7 +1215,9 @@ __global__ __launch_bounds__(G_NT) void k3_group(const MRec* __restrict__ mrec, 
                                                  int local_cache, rl_status* __restrict__ out,
                                                  uint32_t* __restrict__ req_thr, const Deferred* __restrict__ dfr,
                                                  const HotBucket3* __restrict__ hb, HotCand* __restrict__ cand,
-                                                 V3GroupScratch gs, uint32_t* __restrict__ wg_heads, EngineCtl* ctl) {
+                                                 int cand_on, const uint32_t* __restrict__ rngb,
+                                                 const uint32_t* __restrict__ bbase, V3GroupScratch gs,
+                                                 uint32_t* __restrict__ wg_heads, EngineCtl* ctl) {
   __shared__ uint64_t s_key[G_CAP];
   __shared__ uint64_t s_lo[G_CAP];
   __shared__ uint2 s_pay[G_CAP];
@@ -1215,6 +1231,7 @@ __global__ __launch_bounds__(G_NT) void k3_group(const MRec* __restrict__ mrec, 
   __shared__ LSeg s_carry;
   __shared__ uint32_t s_cursor, s_heads;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
+  ST3(2, 6);
   if (ctl->err) {
     if (tid == 0) wg_heads[blockIdx.x] = 0;
     return;
@@ -1239,35 +1256,51 @@ __global__ __launch_bounds__(G_NT) void k3_group(const MRec* __restrict__ mrec, 
   const uint32_t m = r1 - r0;
   if (m == 0) {
     if (tid == 0) wg_heads[blockIdx.x] = 0;
+    ST3(2, 5);
     return;
   }
   ST3(2, 0);
   ST3V(2, 7, m);
-  if (tid == 0) { s_cursor = 0; s_heads = 0; }
-  uint32_t heads;
-  if (m <= (uint32_t)G_CAP) {
-    const GStore g{s_key, s_lo, s_pay, s_P, s_slot, s_cnt, s_end, s_list, s_grp, &s_cursor, G_HASH - 1, mrec + r0};
-    heads =
-        group_range<true>(g, G_HASH, mrec + r0, m, rules, tab, local_cache, out, req_thr, cand, s_agg, &s_carry, ctl);
-  } else {
-    // A range larger than the LDS stage (a bucket holding a very frequent key that is not in
-    // the hot set yet): the same phases on global scratch.
-    uint32_t hs = 2;
-    while (hs < 2 * m) hs <<= 1;  // <= 4m: 4 words per position
-    const GStore g{gs.key + r0,
-                   gs.lo + r0,
-                   reinterpret_cast<uint2*>(gs.pay) + r0,
-                   gs.P + r0,
-                   gs.slot + 4 * (size_t)r0,
-                   gs.cnt + 4 * (size_t)r0,
-                   reinterpret_cast<uint16_t*>(gs.base) + 4 * (size_t)r0,
-                   reinterpret_cast<uint16_t*>(gs.list) + r0,
-                   reinterpret_cast<uint16_t*>(gs.grp) + r0,
-                   gs.cursor + blockIdx.x,
-                   hs - 1,
-                   mrec + r0};
-    if (tid == 0) *g.cursor = 0;
-    heads = group_range<false>(g, hs, mrec + r0, m, rules, tab, local_cache, out, req_thr, cand, s_agg, &s_carry, ctl);
+  if (tid == 0) s_heads = 0;
+  uint32_t heads = 0;
+  // Sub-ranges of whole buckets that fit the LDS stage; a single bucket larger than the stage
+  // (a very frequent key not in the hot set yet) runs on global scratch. Block-uniform.
+  uint32_t bk = rngb[blockIdx.x], pos = r0;
+  while (pos < r1) {
+    uint32_t e = pos;
+    while (bk < (uint32_t)MSD_BUCKETS && bbase[bk + 1] <= r1 && bbase[bk + 1] - pos <= (uint32_t)G_CAP) {
+      e = bbase[bk + 1];
+      ++bk;
+    }
+    __syncthreads();  // the previous sub-range is done with LDS
+    if (tid == 0) s_cursor = 0;
+    if (e > pos) {
+      const GStore g{s_key, s_lo, s_pay, s_P, s_slot, s_cnt, s_end, s_list, s_grp, &s_cursor, G_HASH - 1, mrec + pos};
+      heads += group_range<true>(g, G_HASH, mrec + pos, e - pos, rules, tab, local_cache, out, req_thr, cand, cand_on,
+                                 s_agg, &s_carry, ctl);
+    } else {
+      e = bbase[bk + 1];
+      ++bk;
+      const uint32_t mm = e - pos;
+      uint32_t hs = 2;
+      while (hs < 2 * mm) hs <<= 1;  // <= 4 mm: 4 words per position
+      const GStore g{gs.key + pos,
+                     gs.lo + pos,
+                     reinterpret_cast<uint2*>(gs.pay) + pos,
+                     gs.P + pos,
+                     gs.slot + 4 * (size_t)pos,
+                     gs.cnt + 4 * (size_t)pos,
+                     reinterpret_cast<uint16_t*>(gs.base) + 4 * (size_t)pos,
+                     reinterpret_cast<uint16_t*>(gs.list) + pos,
+                     reinterpret_cast<uint16_t*>(gs.grp) + pos,
+                     gs.cursor + blockIdx.x,
+                     hs - 1,
+                     mrec + pos};
+      if (tid == 0) *g.cursor = 0;
+      heads += group_range<false>(g, hs, mrec + pos, mm, rules, tab, local_cache, out, req_thr, cand, cand_on, s_agg,
+                                  &s_carry, ctl);
+    }
+    pos = e;
   }
   heads = wave_sum(heads);
   if (lane == 0 && heads) atomicAdd(&s_heads, heads);
@@ -1283,12 +1316,15 @@ constexpr int TAIL_NT = 256;
 __global__ __launch_bounds__(TAIL_NT) void k3_tail(DevBatch in, const DevRule* __restrict__ rules, uint64_t seed,
                                                    HotCand* cand, const uint32_t* __restrict__ wg_heads,
                                                    uint32_t n_heads, EngineCtl* ctl, EngineCtl* next_ctl) {
-  __shared__ uint32_t s_u;
+  __shared__ uint32_t s_u, s_ins;
   if (blockIdx.x == 0) {
     // U = Σ per-workgroup unique-key counts; 8 independent loads per lane per step
-    if (threadIdx.x == 0) s_u = 0;
+    if (threadIdx.x == 0) {
+      s_u = 0;
+      s_ins = 0;
+    }
     __syncthreads();
-    uint32_t u = 0;
+    uint32_t u = 0, ins = 0;
     for (uint32_t t0 = 0; t0 < n_heads; t0 += TAIL_NT * 8) {
       uint32_t v[8];
 #pragma unroll
@@ -1297,12 +1333,22 @@ __global__ __launch_bounds__(TAIL_NT) void k3_tail(DevBatch in, const DevRule* _
         v[k] = t < n_heads ? wg_heads[t] : 0u;
       }
 #pragma unroll
-      for (int k = 0; k < 8; ++k) u += v[k];
+      for (int k = 0; k < 8; ++k) {
+        u += v[k] & 0xFFFFu;
+        ins += v[k] >> 16;
+      }
     }
     u = wave_sum(u);
-    if ((threadIdx.x & 63) == 0 && u) atomicAdd(&s_u, u);
+    ins = wave_sum(ins);
+    if ((threadIdx.x & 63) == 0) {
+      if (u) atomicAdd(&s_u, u);
+      if (ins) atomicAdd(&s_ins, ins);
+    }
     __syncthreads();
-    if (threadIdx.x == 0) ctl->n_segments = s_u;
+    if (threadIdx.x == 0) {
+      ctl->n_segments = s_u;
+      ctl->tile_ctr[INS_CTR0][0] += s_ins;  // new table slots (engine stats)
+    }
   }
   {
     uint32_t* z = reinterpret_cast<uint32_t*>(next_ctl);
@@ -1360,8 +1406,9 @@ void launch_v3_scan(hipStream_t st, uint32_t n, const uint16_t* tcount, const un
   hipLaunchKernelGGL(v3::k3_scan, dim3(v3_scan_blocks()), dim3(v3::SCAN_NT), 0, st, tcount, thsum, v3_tiles(n), toff,
                      hoff, btotal, fpart, hot_list, hb, tab, local_cache, cand, heads_out, ctl);
 }
-void launch_v3_bases(hipStream_t st, uint32_t n, const uint32_t* btotal, uint32_t* bbase, uint32_t* rng) {
-  hipLaunchKernelGGL(v3::k3_bases, dim3(1), dim3(v3::SCAN_NT), 0, st, btotal, bbase, rng, v3_group_wgs(n));
+void launch_v3_bases(hipStream_t st, uint32_t n, const uint32_t* btotal, uint32_t* bbase, uint32_t* rng,
+                     uint32_t* rngb) {
+  hipLaunchKernelGGL(v3::k3_bases, dim3(1), dim3(v3::SCAN_NT), 0, st, btotal, bbase, rng, rngb, v3_group_wgs(n));
 }
 void launch_v3_place(hipStream_t st, uint32_t n, const ARec* arec, const DevRule* rules, const uint32_t* toff,
                      const unsigned long long* hoff, const uint32_t* bbase, HotBucket3* hb, int local_cache,
@@ -1371,11 +1418,11 @@ void launch_v3_place(hipStream_t st, uint32_t n, const ARec* arec, const DevRule
 }
 void launch_v3_group(hipStream_t st, uint32_t n, const MRec* mrec, const uint32_t* rng, const DevRule* rules,
                      const TableDesc& tab, int local_cache, rl_status* out, uint32_t* req_thr, const Deferred* dfr,
-                     const HotBucket3* hb, HotCand* cand, const V3GroupScratch& gs, uint32_t* wg_heads,
-                     EngineCtl* ctl) {
+                     const HotBucket3* hb, HotCand* cand, int cand_on, const uint32_t* rngb, const uint32_t* bbase,
+                     const V3GroupScratch& gs, uint32_t* wg_heads, EngineCtl* ctl) {
   const uint32_t nw = v3_group_wgs(n);
   hipLaunchKernelGGL(v3::k3_group, dim3(nw + 1), dim3(v3::G_NT), 0, st, mrec, rng, nw, rules, tab, local_cache, out,
-                     req_thr, dfr, hb, cand, gs, wg_heads, ctl);
+                     req_thr, dfr, hb, cand, cand_on, rngb, bbase, gs, wg_heads, ctl);
 }
 void launch_v3_tail(hipStream_t st, const rl_batch& b, const DevRule* rules, uint64_t seed, HotCand* cand,
                     const uint32_t* wg_heads, uint32_t n_heads, EngineCtl* ctl, EngineCtl* next_ctl) {

@@ -20,7 +20,7 @@ eng.load_rules(workload.CONFIG3_RULES)
 dev = torch.device("cuda", 0)
 out = torch.empty(d * 20, dtype=torch.uint8, device=dev)
 thr = torch.empty(d, dtype=torch.int32, device=dev)
-for b in range(5):
+for b in range(int(sys.argv[1]) if len(sys.argv) > 1 else 5):
     hb = workload.config3_batch(b, d=d)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     db = [t(hb.blob), t(hb.off.view(np.int32)), t(hb.rule.view(np.int32)), t(hb.req_of.view(np.int32)), t(hb.now),
@@ -38,6 +38,21 @@ names = {0: ("k3_hist", ntiles, ["start", "hot+zero", "loaded", "sorted", "scann
          3: ("k3_scan", 8, ["start", "folded", "pass1", "pass2", "claimed"]),
          1: ("k3_place", ntiles, ["start", "loaded", "crossing", "end"]),
          2: ("k3_group", (d + 255) // 256, ["start", "staged", "laid", "scanned", "led", "end"])}
+# absolute span of each kernel's stamped blocks (s_memrealtime is chip-global): first stamp to
+# last stamp, and the gap from the previous kernel's last stamp
+spans = {}
+for k, (nm, nb, ph) in names.items():
+    cols = [0, 5] if k != 2 else [6, 5]
+    a0 = st[k, :nb + (1 if k == 2 else 0), cols[0]].astype(np.int64)
+    a1 = st[k, :nb + (1 if k == 2 else 0), :].max(axis=1).astype(np.int64)
+    ok = a0 > a0.max() - 1_000_000
+    spans[nm] = (a0[ok].min(), a1[ok].max())
+prev = None
+for nm in ["k3_hist", "k3_scan", "k3_place", "k3_group"]:
+    b, e = spans[nm]
+    gap = "" if prev is None else f"  gap after previous {(b - prev) / 100:.1f} us"
+    print(f"{nm:9s} first..last stamp {(e - b) / 100:6.1f} us{gap}")
+    prev = e
 for k, (nm, nb, ph) in names.items():
     a = st[k, :nb, :len(ph)].astype(np.int64)
     newest = a[:, 0].max()
@@ -57,3 +72,15 @@ for k, (nm, nb, ph) in names.items():
     if k == 2:
         m = st[2, :nb, 7][live]
         print(f"   records per block: median {np.median(m):.0f} max {m.max()}")
+        # every block (empty ranges included): entry stamp 6, exit stamp 5
+        ent = st[2, :nb + 1, 6].astype(np.int64)
+        ex = st[2, :nb + 1, 5].astype(np.int64)
+        ok = ent > ent.max() - 1_000_000
+        e0 = ent[ok].min()
+        print(f"   all {ok.sum()} blocks: entry span {(ent[ok].max() - e0) / 100:.1f} us, "
+              f"last exit {(ex[ok].max() - e0) / 100:.1f} us; entry of block 0 {(ent[0] - e0) / 100:.1f} us")
+        live_all = ok & (st[2, :nb + 1, 7] > 0)
+        order = np.argsort(ent[ok])
+        print("   entry times (us) of blocks by index decile:",
+              [round(float((np.median(ent[i:i + nb // 10][ok[i:i + nb // 10]]) - e0) / 100), 1)
+               for i in range(0, nb, nb // 10)])
