@@ -208,6 +208,36 @@ constexpr uint32_t V3_MAX_RULES = 1u << V3_RULE_BITS;
 constexpr int DFR_CTR = 29;               // EngineCtl::tile_ctr[DFR_CTR][0] counts deferred hot descriptors
 constexpr int SCAN_CTR = 28;              // EngineCtl::tile_ctr[SCAN_CTR][0]: k3_scan blocks done
 
+// Multi-GPU: a descriptor routed to the GPU that owns its key (32 B). The owner needs the
+// key identity before the window (prefix lanes), the request time, the rule, hits_addend and
+// a request id that orders requests across origins: origin << ROUTE_REQ_BITS | request.
+struct __attribute__((aligned(16))) RRec {
+  uint64_t a, b;     // fingerprint lane state after the key-prefix bytes (unit folded in)
+  uint32_t now;      // request time, unix seconds (< 2^32, checked at the origin)
+  uint32_t rule;     // rule id (every shard loads the same rule table)
+  uint32_t h;        // max(1, hits_addend)
+  uint32_t greq;     // global request id
+};
+// Owner shard of a key: a mix of the prefix lanes, so every window of a key (and every
+// origin) maps to the same GPU. Multiply-shift keeps it uniform for any shard count.
+__host__ __device__ __forceinline__ uint32_t route_owner(uint64_t a, uint64_t b, uint32_t n_shards) {
+  const uint64_t x = fmix64(a ^ rotl64(b, 29));
+  return (uint32_t)(((x >> 32) * (uint64_t)n_shards) >> 32);
+}
+// Reply of an owner to an origin, one per routed record (24 B): the DescriptorStatus and the
+// record's ThrottleMillis contribution.
+struct RReply {
+  rl_status st;
+  uint32_t thr;
+};
+static_assert(sizeof(RReply) == 24, "RReply is 6 words");
+constexpr int ROUTE_REQ_BITS = 27;
+constexpr uint32_t ROUTE_MAX_SHARDS = 16;
+constexpr uint8_t ROUTE_LOCAL = 0xFF;  // descriptor decided at the origin (nil limit)
+// rl_batch.reserved bit: prefix_blob holds RRec records (rl_submit_routed), n_req = n_desc and
+// every record has its own ThrottleMillis slot.
+constexpr uint32_t RL_BATCH_ROUTED = 1u;
+
 // Per-descriptor record in arrival order (32 B), written by k3_hist, read by k3_place.
 struct __attribute__((aligned(16))) ARec {
   uint64_t kp;       // MSD: sort key; hot: INCRBY prefix of the key inside the tile (inclusive)

@@ -241,8 +241,9 @@ RL_DEV void leader_segment(uint32_t hp, uint32_t j, const SortedRec& tail, bool 
 
 // GetResponseDescriptorStatus + checkOverLimitThreshold + checkNearLimitThreshold +
 // CalculateReset (base_limiter.go:70-195, utilities.go:34-38) for one descriptor.
+// thr_idx: the ThrottleMillis slot (the request index; a routed record's own position).
 RL_DEV void decide_one(const SortedRec& r, const SegInfo& si, const DevRule& R, rl_status* __restrict__ out,
-                       uint32_t* __restrict__ req_thr) {
+                       uint32_t* __restrict__ req_thr, uint32_t thr_idx) {
   const uint32_t h = r.h;
   const uint32_t reset = R.div - (uint32_t)r.now_mod;  // div - now % div
   rl_status st;
@@ -280,13 +281,14 @@ RL_DEV void decide_one(const SortedRec& r, const SegInfo& si, const DevRule& R, 
     }
   }
   out[r.idx] = st;
-  if (throttle) atomicMax(&req_thr[r.req], throttle);
+  if (throttle) atomicMax(&req_thr[thr_idx], throttle);
 }
 
 RL_DEV void decide_pos(uint32_t j, const SortedRec* __restrict__ srec, const SegInfo* __restrict__ seg,
-                       const DevRule* __restrict__ rules, rl_status* __restrict__ out, uint32_t* __restrict__ req_thr) {
+                       const DevRule* __restrict__ rules, rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
+                       int routed) {
   const SortedRec r = srec[j];
-  decide_one(r, seg[r.head & ~HEAD_MIXED_RULE], rules[r.rule], out, req_thr);
+  decide_one(r, seg[r.head & ~HEAD_MIXED_RULE], rules[r.rule], out, req_thr, routed ? r.idx : r.req);
 }
 
 }  // namespace rlhip

@@ -40,7 +40,23 @@ struct DevBatch {
   const uint32_t* req_of;
   const int64_t* now;
   const uint32_t* hits;
+  const RRec* recs;  // routed batch (multi-GPU owner side): records instead of prefix bytes
 };
+inline DevBatch make_dev_batch(const rl_batch& b) {
+  DevBatch d;
+  d.n_desc = b.n_desc;
+  d.n_req = b.n_req;
+  d.blob_bytes = b.blob_bytes;
+  d.pad = 0;
+  d.blob = b.prefix_blob;
+  d.off = b.prefix_off;
+  d.rule = b.rule_id;
+  d.req_of = b.req_of;
+  d.now = b.now;
+  d.hits = b.hits_addend;
+  d.recs = (b.reserved & RL_BATCH_ROUTED) ? reinterpret_cast<const RRec*>(b.prefix_blob) : nullptr;
+  return d;
+}
 
 // Unaligned little-endian 8-byte words of a byte string, read as aligned dwords and
 // funnel-shifted (v_alignbyte_b32). The blob has >= 16 bytes of slack past its end.

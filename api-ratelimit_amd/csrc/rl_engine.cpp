@@ -51,8 +51,14 @@ void launch_bgroup(hipStream_t, const uint64_t*, const ItemRec*, const uint64_t*
                    const HotBucket*, rl_status*, uint32_t*, HotCand*, EngineCtl*);
 void launch_cand_state(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, const uint32_t*, uint32_t,
                        EngineCtl*);
-void launch_decide(hipStream_t, const SortedRec*, const SegInfo*, const DevRule*, uint32_t, rl_status*, uint32_t*,
+void launch_decide(hipStream_t, const SortedRec*, const SegInfo*, const DevRule*, uint32_t, rl_status*, uint32_t*, int,
                    EngineCtl*);
+uint32_t route_bcnt_words(uint32_t n);
+void launch_route_pack(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint32_t, uint32_t, RRec*,
+                       uint8_t*, uint32_t*, RRec*, uint32_t*, uint32_t*, EngineCtl*);
+void launch_route_reply(hipStream_t, uint32_t, const rl_status*, const uint32_t*, RReply*);
+void launch_route_unpack(hipStream_t, uint32_t, const uint32_t*, const uint32_t*, const RReply*, rl_status*,
+                         uint32_t*);
 uint32_t v3_tiles(uint32_t n);
 uint32_t v3_group_wgs(uint32_t n);
 uint32_t v3_scan_blocks();
@@ -63,10 +69,10 @@ void launch_v3_scan(hipStream_t, uint32_t, const uint16_t*, const unsigned long 
                     uint32_t*, EngineCtl*);
 void launch_v3_bases(hipStream_t, uint32_t, const uint32_t*, uint32_t*, uint32_t*, uint32_t*);
 void launch_v3_place(hipStream_t, uint32_t, const ARec*, const DevRule*, const uint32_t*, const unsigned long long*,
-                     const uint32_t*, HotBucket3*, int, MRec*, rl_status*, uint32_t*, Deferred*, EngineCtl*);
+                     const uint32_t*, HotBucket3*, int, MRec*, rl_status*, uint32_t*, Deferred*, int, EngineCtl*);
 void launch_v3_group(hipStream_t, uint32_t, const MRec*, const uint32_t*, const DevRule*, const TableDesc&, int,
                      rl_status*, uint32_t*, const Deferred*, const HotBucket3*, HotCand*, int, const uint32_t*,
-                     const uint32_t*, const V3GroupScratch&, uint32_t*, EngineCtl*);
+                     const uint32_t*, const V3GroupScratch&, uint32_t*, int, EngineCtl*);
 void launch_v3_tail(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, const uint32_t*, uint32_t,
                     EngineCtl*, EngineCtl*);
 }  // namespace rlhip
@@ -101,7 +107,8 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 struct rl_engine {
   rl_config cfg{};
   int lo_bit = 16, npasses = 6;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;      // the stream all work is ordered on (own_stream or rl_set_stream's)
+  hipStream_t own_stream = nullptr;
   std::string err;
 
   // counter table
@@ -170,6 +177,15 @@ struct rl_engine {
   uint8_t* zero_block = nullptr;  // ctl | hist | lookbacks (zeroed per batch)
   size_t zero_cap = 0;
   EngineCtl* h_ctl = nullptr;     // pinned copy of the control block
+
+  // multi-GPU router scratch (allocated on first use)
+  RRec* r_tmp = nullptr;           // origin: routed records in descriptor order
+  uint8_t* r_own = nullptr;        // origin: owner per descriptor
+  uint32_t* r_bcnt = nullptr;      // origin: per (block, owner) counts -> send offsets
+  EngineCtl* r_ctl = nullptr;      // origin: error word of rl_route_pack
+  uint32_t* h_route = nullptr;     // pinned: [0] err, [1..16] send counts
+  uint32_t* r_thr = nullptr;       // owner: ThrottleMillis per routed record
+  RReply* pend_reply = nullptr;    // owner: reply destination of the in-flight routed batch
 
   // in-flight batch
   bool in_flight = false;
@@ -259,6 +275,8 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   uint64_t* lb_sum = reinterpret_cast<uint64_t*>(zero_block + z.lb_sum);
   uint64_t* lb_head = reinterpret_cast<uint64_t*>(zero_block + z.lb_head);
   const size_t lb_pass_stride = (size_t)sort_tiles(n > 0 ? n : 1) * RADIX;  // per-digit look-back words
+  const int routed = (b.reserved & RL_BATCH_ROUTED) ? 1 : 0;
+  if (routed && mode == MODE_V2) mode = MODE_LSD;  // the v2 loader reads prefix bytes only
   hipError_t e;
   if (mode == MODE_V3) {
     if (n == 0) {
@@ -286,11 +304,11 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     timed(KT_V3_BASES, [&] { launch_v3_bases(stream, n, btotal, v3_bbase, v3_rng, v3_rngb); });
     timed(KT_V3_PLACE, [&] {
       launch_v3_place(stream, n, v3_arec, d_rules, v3_toff, v3_hoff, v3_bbase, v3_hb, lc, v3_mrec, out, thr, v3_dfr,
-                      c3);
+                      routed, c3);
     });
     timed(KT_V3_GROUP, [&] {
       launch_v3_group(stream, n, v3_mrec, v3_rng, d_rules, tab, lc, out, thr, v3_dfr, v3_hb, d_cand, want_cand ? 1 : 0,
-                      v3_rngb, v3_bbase, v3_gs, v3_heads, c3);
+                      v3_rngb, v3_bbase, v3_gs, v3_heads, routed, c3);
     });
     timed(KT_V3_TAIL, [&] {
       launch_v3_tail(stream, b, d_rules, cfg.hash_seed, d_cand, v3_heads, nw + 1 + v3_scan_blocks(), c3, c3n);
@@ -417,7 +435,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     launch_leader(stream, skeys, srec, recs, d_rules, n, tab, cfg.local_cache ? 1 : 0, seg, tile_heads,
                   scan_tiles(n), d_cand, ctl);
   });
-  timed(KT_DECIDE, [&] { launch_decide(stream, srec, seg, d_rules, n, out, thr, ctl); });
+  timed(KT_DECIDE, [&] { launch_decide(stream, srec, seg, d_rules, n, out, thr, routed, ctl); });
   timed(KT_CAND, [&] { launch_cand_state(stream, b, d_rules, cfg.hash_seed, d_cand, nullptr, 0, ctl); });
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
@@ -538,6 +556,7 @@ int rl_engine::finish() {
     fell_back = true;
     int rc = run_pipeline(dev_batch, pend_out_dev, pend_thr_dev, MODE_LSD);
     if (rc) return rc;
+    if (pend_reply) launch_route_reply(stream, dev_batch.n_desc, pend_out_dev, pend_thr_dev, pend_reply);
     if (host_path && (rc = enqueue_d2h()) != 0) return rc;
     e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
@@ -549,6 +568,7 @@ int rl_engine::finish() {
     ++st.resorts;
     int rc = run_pipeline(dev_batch, pend_out_dev, pend_thr_dev, MODE_LSD_FULL);
     if (rc) return rc;
+    if (pend_reply) launch_route_reply(stream, dev_batch.n_desc, pend_out_dev, pend_thr_dev, pend_reply);
     if (host_path && (rc = enqueue_d2h()) != 0) return rc;
     e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
@@ -635,7 +655,8 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   hipError_t he = hipSetDevice(c.device);
   if (he != hipSuccess) { delete e; return RL_EHIP; }
   auto chk = [&](hipError_t x) { if (x != hipSuccess && he == hipSuccess) he = x; };
-  chk(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+  chk(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
+  e->stream = e->own_stream;
   // counter table: 8 regions (unit x window parity)
   size_t off = 0;
   for (int r = 0; r < 8; ++r) {
@@ -796,9 +817,15 @@ void rl_destroy(rl_engine* e) {
   hipFree(e->v3_ctl[0]);
   hipFree(e->v3_ctl[1]);
 
+  hipFree(e->r_tmp);
+  hipFree(e->r_own);
+  hipFree(e->r_bcnt);
+  hipFree(e->r_ctl);
+  hipHostFree(e->h_route);
+  hipFree(e->r_thr);
   hipFree(e->zero_block);
   hipHostFree(e->h_ctl);
-  if (e->stream) hipStreamDestroy(e->stream);
+  if (e->own_stream) hipStreamDestroy(e->own_stream);
   delete e;
 }
 
@@ -845,6 +872,7 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
   if (b->n_desc > c.max_batch_desc || b->n_req > c.max_batch_req || b->blob_bytes > c.max_blob_bytes)
     return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req, %u blob bytes)", c.max_batch_desc,
                    c.max_batch_req, c.max_blob_bytes);
+  if (b->reserved) return e->fail(RL_EINVAL, "rl_batch.reserved must be 0");
   if (!e->d_rules) rl_load_rules(e, nullptr, 0);
   // Host-side validation of the batch layout.
   if (b->n_desc && (!b->prefix_off || !b->rule_id || !b->req_of || !out))
@@ -904,6 +932,7 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
   e->pend_thr_dev = e->d_thr;
   e->user_out = out;
   e->user_thr = req_throttle_ms;
+  e->pend_reply = nullptr;
   e->host_path = true;
   if ((rc = e->enqueue_d2h()) != 0) return rc;
   e->in_flight = true;
@@ -924,18 +953,112 @@ int rl_submit_device(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t
   if (b->n_desc > c.max_batch_desc || b->n_req > c.max_batch_req)
     return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req)", c.max_batch_desc,
                    c.max_batch_req);
+  if (b->reserved) return e->fail(RL_EINVAL, "rl_batch.reserved must be 0");
   if (!e->d_rules) rl_load_rules(e, nullptr, 0);
   int rc = e->run_pipeline(*b, d_out, d_req_throttle_ms, e->default_mode());
   if (rc) return rc;
   e->dev_batch = *b;
   e->pend_out_dev = d_out;
   e->pend_thr_dev = d_req_throttle_ms;
+  e->pend_reply = nullptr;
   e->host_path = false;
   e->in_flight = true;
   return 0;
 }
 
 void* rl_stream(rl_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int rl_set_stream(rl_engine* e, void* hip_stream) {
+  if (!e) return RL_EINVAL;
+  if (e->in_flight) return e->fail(RL_ESTATE, "rl_set_stream while a batch is in flight");
+  hipError_t he = hipStreamSynchronize(e->stream);  // work already queued finishes first
+  if (he != hipSuccess) return e->hip_fail(he, "hipStreamSynchronize");
+  e->stream = hip_stream ? (hipStream_t)hip_stream : e->own_stream;
+  return 0;
+}
+
+int rl_route_pack(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_shards, void* d_send,
+                  uint32_t* d_send_counts, uint32_t* d_perm, uint32_t* h_send_counts) {
+  if (!e || !b) return RL_EINVAL;
+  if (e->in_flight) return e->fail(RL_ESTATE, "rl_route_pack while a batch is in flight (call rl_wait)");
+  if (n_shards == 0 || n_shards > ROUTE_MAX_SHARDS || origin >= ROUTE_MAX_SHARDS)
+    return e->fail(RL_EINVAL, "n_shards must be 1..%u and origin < %u", ROUTE_MAX_SHARDS, ROUTE_MAX_SHARDS);
+  if (b->n_desc > e->cfg.max_batch_desc) return e->fail(RL_ECAPACITY, "batch exceeds engine capacity");
+  if (b->n_req > RL_ROUTE_MAX_REQ) return e->fail(RL_EINVAL, "routed batch holds more than 2^27 requests");
+  if (b->reserved) return e->fail(RL_EINVAL, "rl_batch.reserved must be 0");
+  if (!d_send_counts || !h_send_counts || (b->n_desc && (!d_send || !d_perm)))
+    return e->fail(RL_EINVAL, "null routing buffer");
+  if (!e->d_rules) rl_load_rules(e, nullptr, 0);
+  hipError_t he = hipSuccess;
+  auto chk = [&](hipError_t x) { if (x != hipSuccess && he == hipSuccess) he = x; };
+  const size_t N = e->cfg.max_batch_desc ? e->cfg.max_batch_desc : 1;
+  if (!e->r_tmp) {
+    chk(hipMalloc(&e->r_tmp, N * sizeof(RRec)));
+    chk(hipMalloc(&e->r_own, N));
+    chk(hipMalloc(&e->r_bcnt, (size_t)route_bcnt_words((uint32_t)N) * 4));
+    chk(hipMalloc(&e->r_ctl, sizeof(EngineCtl)));
+    chk(hipHostMalloc(&e->h_route, 64 * 4, hipHostMallocDefault));
+    if (he != hipSuccess) return e->hip_fail(he, "router scratch allocation");
+  }
+  chk(hipMemsetAsync(e->r_ctl, 0, sizeof(EngineCtl), e->stream));
+  launch_route_pack(e->stream, *b, e->d_rules, e->n_rules, e->cfg.hash_seed, origin, n_shards, e->r_tmp, e->r_own,
+                    e->r_bcnt, reinterpret_cast<RRec*>(d_send), d_send_counts, d_perm, e->r_ctl);
+  chk(hipGetLastError());
+  chk(hipMemcpyAsync(e->h_route, e->r_ctl, 4, hipMemcpyDeviceToHost, e->stream));
+  chk(hipMemcpyAsync(e->h_route + 1, d_send_counts, n_shards * 4, hipMemcpyDeviceToHost, e->stream));
+  chk(hipStreamSynchronize(e->stream));
+  if (he != hipSuccess) return e->hip_fail(he, "rl_route_pack");
+  const uint32_t errs = e->h_route[0];
+  if (errs & ERR_BAD_INPUT) return e->fail(RL_EINVAL, "batch references an unknown rule id or request index");
+  if (errs & ERR_BAD_TIME) return e->fail(RL_EINVAL, "request time outside [0, 2^32) unix seconds");
+  memcpy(h_send_counts, e->h_route + 1, n_shards * 4);
+  return 0;
+}
+
+int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_reply) {
+  if (!e) return RL_EINVAL;
+  if (e->in_flight) return e->fail(RL_ESTATE, "rl_submit_routed while a batch is in flight (call rl_wait)");
+  if (n > e->cfg.max_batch_desc)
+    return e->fail(RL_ECAPACITY, "routed batch of %u records exceeds engine capacity (%u desc)", n,
+                   e->cfg.max_batch_desc);
+  if (n && (!d_records || !d_reply)) return e->fail(RL_EINVAL, "null routed buffer");
+  if (!e->d_rules) rl_load_rules(e, nullptr, 0);
+  if (!e->r_thr) {
+    hipError_t he = hipMalloc(&e->r_thr, (size_t)(e->cfg.max_batch_desc ? e->cfg.max_batch_desc : 1) * 4);
+    if (he != hipSuccess) return e->hip_fail(he, "router scratch allocation");
+  }
+  rl_batch b{};
+  b.n_desc = n;
+  b.n_req = n;  // every record has its own ThrottleMillis slot
+  b.reserved = RL_BATCH_ROUTED;
+  b.prefix_blob = reinterpret_cast<const uint8_t*>(d_records);
+  int rc = e->run_pipeline(b, e->d_out, e->r_thr, e->default_mode());
+  if (rc) return rc;
+  launch_route_reply(e->stream, n, e->d_out, e->r_thr, reinterpret_cast<RReply*>(d_reply));
+  e->dev_batch = b;
+  e->pend_out_dev = e->d_out;
+  e->pend_thr_dev = e->r_thr;
+  e->pend_reply = reinterpret_cast<RReply*>(d_reply);
+  e->host_path = false;
+  e->in_flight = true;
+  return 0;
+}
+
+int rl_route_unpack(rl_engine* e, const rl_batch* b, const uint32_t* d_perm, const void* d_reply, rl_status* d_out,
+                    uint32_t* d_req_throttle_ms) {
+  if (!e || !b) return RL_EINVAL;
+  if (e->in_flight) return e->fail(RL_ESTATE, "rl_route_unpack while a batch is in flight (call rl_wait)");
+  if (b->n_desc && (!d_perm || !d_out || !b->req_of)) return e->fail(RL_EINVAL, "null routing buffer");
+  if (b->n_req && !d_req_throttle_ms) return e->fail(RL_EINVAL, "null throttle buffer");
+  hipError_t he = hipSuccess;
+  if (b->n_req) he = hipMemsetAsync(d_req_throttle_ms, 0, (size_t)b->n_req * 4, e->stream);
+  if (he == hipSuccess) {
+    launch_route_unpack(e->stream, b->n_desc, b->req_of, d_perm, reinterpret_cast<const RReply*>(d_reply), d_out,
+                        d_req_throttle_ms);
+    he = hipGetLastError();
+  }
+  return he == hipSuccess ? 0 : e->hip_fail(he, "rl_route_unpack");
+}
 
 int rl_reset(rl_engine* e) {
   if (!e) return RL_EINVAL;

@@ -51,7 +51,37 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
   bool nil = true;
   uint64_t key = NIL_KEY;
   uint32_t region = 8, gen = 0;
-  if (i < in.n_desc) {
+  if (i < in.n_desc && in.recs) {
+    // Routed record (multi-GPU owner): the key prefix arrives as its fingerprint lane state.
+    const RRec x = in.recs[i];
+    req_thr[i] = 0;  // one ThrottleMillis slot per record
+    ItemRec rec;
+    rec.rule = x.rule;
+    rec.req = x.greq;
+    rec.h = x.h;
+    rec.fp_lo = 0;
+    rec.now_mod = 0;
+    rec.gen = 0;
+    rec.pad = 0;
+    if (x.rule >= n_rules) {
+      err |= ERR_BAD_INPUT;
+    } else {
+      const DevRule R = rules[x.rule];
+      const int64_t widx = div_const((int64_t)x.now, R.unit);
+      const int64_t ws = widx * (int64_t)R.div;
+      uint64_t hi, lo;
+      fp_final(FpState{x.a, x.b}, (uint64_t)ws, hi, lo);
+      region = (R.unit - 1u) * 2u + (uint32_t)(widx & 1);
+      key = make_sort_key(region, hi);
+      rec.fp_lo = lo;
+      rec.now_mod = (int32_t)((int64_t)x.now - ws);
+      rec.gen = (uint32_t)widx + 1u;
+      gen = rec.gen;
+      nil = false;
+    }
+    recs[i] = rec;
+    keys_orig[i] = key;
+  } else if (i < in.n_desc) {
     const uint32_t r = in.rule[i];
     const uint32_t q = in.req_of[i];
     const bool q_ok = q < in.n_req;
@@ -713,7 +743,7 @@ __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ ske
 __global__ __launch_bounds__(256) void k_decide(const SortedRec* __restrict__ srec, const SegInfo* __restrict__ seg,
                                                 const DevRule* __restrict__ rules, uint32_t n_all,
                                                 rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
-                                                EngineCtl* ctl) {
+                                                int routed, EngineCtl* ctl) {
   const uint32_t errs = ctl->err;  // flags of earlier launches
   if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_TABLE_FULL | ERR_BAD_INPUT | ERR_WINDOW_SPAN |
               ERR_V2_FALLBACK))
@@ -721,7 +751,7 @@ __global__ __launch_bounds__(256) void k_decide(const SortedRec* __restrict__ sr
   const uint32_t n = n_all - ctl->n_nil;  // written by k_fingerprint (earlier launch)
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
-  decide_pos(j, srec, seg, rules, out, req_thr);
+  decide_pos(j, srec, seg, rules, out, req_thr, routed);
 }
 
 // ---------------------------------------------------------------------------
@@ -730,17 +760,7 @@ __global__ __launch_bounds__(256) void k_decide(const SortedRec* __restrict__ sr
 void launch_fingerprint(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
                         uint64_t* keys_orig, ItemRec* recs, rl_status* out, uint32_t* req_thr, uint32_t* fpart,
                         EngineCtl* ctl) {
-  DevBatch d;
-  d.n_desc = b.n_desc;
-  d.n_req = b.n_req;
-  d.blob_bytes = b.blob_bytes;
-  d.pad = 0;
-  d.blob = b.prefix_blob;
-  d.off = b.prefix_off;
-  d.rule = b.rule_id;
-  d.req_of = b.req_of;
-  d.now = b.now;
-  d.hits = b.hits_addend;
+  const DevBatch d = make_dev_batch(b);
   const uint32_t grid = (b.n_desc + 255) / 256;
   hipLaunchKernelGGL(k_fingerprint, dim3(grid), dim3(256), 0, st, d, rules, n_rules, seed, keys_orig, recs, out,
                      req_thr, fpart, ctl);
@@ -786,8 +806,9 @@ void launch_leader(hipStream_t st, const uint64_t* skeys, const SortedRec* srec,
                      local_cache, seg, heads, n_heads, cand, ctl);
 }
 void launch_decide(hipStream_t st, const SortedRec* srec, const SegInfo* seg, const DevRule* rules, uint32_t n,
-                   rl_status* out, uint32_t* req_thr, EngineCtl* ctl) {
-  hipLaunchKernelGGL(k_decide, dim3((n + 255) / 256), dim3(256), 0, st, srec, seg, rules, n, out, req_thr, ctl);
+                   rl_status* out, uint32_t* req_thr, int routed, EngineCtl* ctl) {
+  hipLaunchKernelGGL(k_decide, dim3((n + 255) / 256), dim3(256), 0, st, srec, seg, rules, n, out, req_thr, routed,
+                     ctl);
 }
 
 }  // namespace rlhip

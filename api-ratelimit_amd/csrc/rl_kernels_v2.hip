@@ -709,7 +709,7 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgroup(const uint64_t* __restric
         if (x.jpos != 0xFFFFFFFFu) rstar = brec[x.jpos].req;
         si.freeze = rstar;
       }
-      decide_one(o, si, rules[r.rule], out, req_thr);
+      decide_one(o, si, rules[r.rule], out, req_thr, o.req);
       // Hot key leader, part 2: the one descriptor that ends the key's INCRBYs writes the
       // counter (the last of the freezing request, else the bucket's last descriptor).
       if (!(x.flags & HB_FROZEN_PRE)) {
@@ -909,7 +909,7 @@ __global__ __launch_bounds__(BG_THREADS) void k_bgroup(const uint64_t* __restric
   for (int q = 0; q < BG_IPT; ++q) {
     if (k0 + q >= m) break;
     const SortedRec& o = mine[q];
-    decide_one(o, seg[o.head & ~HEAD_MIXED_RULE], rules[o.rule], out, req_thr);
+    decide_one(o, seg[o.head & ~HEAD_MIXED_RULE], rules[o.rule], out, req_thr, o.req);
   }
   if (tid == 0) wg_heads[blockIdx.x] = s_heads;
 }
@@ -931,12 +931,17 @@ __global__ void k_cand_state(DevBatch in, const DevRule* __restrict__ rules, uin
   HotCand c = cand[i];
   if (c.first_idx == 0xFFFFFFFFu) return;  // a hot key: state already known
   const uint32_t d = c.first_idx;
-  const uint32_t o0 = in.off[d], o1 = in.off[d + 1];
   const uint32_t unit = rules[c.rule].unit;
-  FpState s = fp_init(o1 - o0, unit, seed);
-  hash_prefix(in.blob, o0, o1 - o0, s);
-  c.a = s.a;
-  c.b = s.b;
+  if (in.recs) {  // routed batch: the record carries the prefix state
+    c.a = in.recs[d].a;
+    c.b = in.recs[d].b;
+  } else {
+    const uint32_t o0 = in.off[d], o1 = in.off[d + 1];
+    FpState s = fp_init(o1 - o0, unit, seed);
+    hash_prefix(in.blob, o0, o1 - o0, s);
+    c.a = s.a;
+    c.b = s.b;
+  }
   c.unit = unit;
   cand[i] = c;
 }
@@ -952,17 +957,7 @@ void launch_fp2(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_
                 const HotEntry* hot, uint64_t* keys_orig, ItemRec* recs, uint16_t* bkt, uint32_t* hbuf,
                 rl_status* out, uint32_t* req_thr, uint32_t* fpart, uint32_t* tcount, unsigned long long* thsum,
                 HotBucket* hb, EngineCtl* ctl) {
-  DevBatch d;
-  d.n_desc = b.n_desc;
-  d.n_req = b.n_req;
-  d.blob_bytes = b.blob_bytes;
-  d.pad = 0;
-  d.blob = b.prefix_blob;
-  d.off = b.prefix_off;
-  d.rule = b.rule_id;
-  d.req_of = b.req_of;
-  d.now = b.now;
-  d.hits = b.hits_addend;
+  const DevBatch d = make_dev_batch(b);
   hipLaunchKernelGGL(k_fp2, dim3(v2_tiles(b.n_desc)), dim3(V2_THREADS), 0, st, d, rules, n_rules, seed, hot,
                      keys_orig, recs, bkt, hbuf, out, req_thr, fpart, v2_tiles(b.n_desc), tcount, thsum, hb, ctl);
 }
@@ -989,17 +984,7 @@ void launch_bgroup(hipStream_t st, const uint64_t* bkey, const ItemRec* brec, co
 }
 void launch_cand_state(hipStream_t st, const rl_batch& b, const DevRule* rules, uint64_t seed, HotCand* cand,
                        const uint32_t* wg_heads, uint32_t n_heads, EngineCtl* ctl) {
-  DevBatch d;
-  d.n_desc = b.n_desc;
-  d.n_req = b.n_req;
-  d.blob_bytes = b.blob_bytes;
-  d.pad = 0;
-  d.blob = b.prefix_blob;
-  d.off = b.prefix_off;
-  d.rule = b.rule_id;
-  d.req_of = b.req_of;
-  d.now = b.now;
-  d.hits = b.hits_addend;
+  const DevBatch d = make_dev_batch(b);
   hipLaunchKernelGGL(k_cand_state, dim3(CAND_MAX / 64), dim3(64), 0, st, d, rules, seed, cand, wg_heads, n_heads,
                      ctl);
 }

@@ -145,6 +145,28 @@ RL_DEV FpState prefix_state(const uint8_t* blob, uint32_t off, uint32_t len, uin
   return s;
 }
 
+// Window, sort key, gen and bucket of one valid descriptor from its prefix state.
+RL_DEV void key_of(D3& x, const FpState& s, int64_t now, const DevRule& rr, const HotEntry* sh_hot, uint32_t& err) {
+  const uint32_t unit = rr.unit;
+  const int64_t widx = div_const(now, unit);
+  const int64_t ws = widx * (int64_t)rr.div;  // (now/divider)*divider  cache_key.go:66-68
+  uint32_t hot_rule = 0;
+  const uint32_t hidx = hot_lookup(sh_hot, s.a, s.b, unit, hot_rule);
+  uint64_t hi, lo;
+  fp_final(s, (uint64_t)ws, hi, lo);
+  const uint32_t region = (unit - 1u) * 2u + (uint32_t)(widx & 1);
+  x.key = make_sort_key(region, hi);
+  x.lo = lo;
+  x.gen = (uint32_t)widx + 1u;
+  x.now_mod = (uint32_t)(now - ws);
+  if (hidx != 0xFFFFFFFFu) {
+    if (hot_rule != x.rule) err |= ERR_V2_FALLBACK;  // a hot bucket must hold one key under one rule
+    x.bucket = hidx * 2u + (uint32_t)(widx & 1);
+  } else {
+    x.bucket = HOT_BUCKETS + msd_bucket(x.key);
+  }
+}
+
 RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, uint32_t n_rules, uint64_t seed,
                        const HotEntry* sh_hot, uint32_t t0, D3 (&d)[R], uint32_t& err) {
   const uint32_t tid = threadIdx.x;
@@ -228,8 +250,6 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
       continue;
     }
     const uint32_t unit = rr[r].unit;
-    const int64_t widx = div_const(now[r], unit);
-    const int64_t ws = widx * (int64_t)rr[r].div;  // (now/divider)*divider  cache_key.go:66-68
     const uint32_t sh = o0[r] & 3u;
     FpState s = fp_init(len[r], unit, seed);
     uint32_t rem = len[r];
@@ -247,21 +267,55 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
     constexpr int DONE_DW = 2 * ((PRE_DW - 1) / 2);  // dword holding the next word's first byte
     if (rem)
       hash_tail(reinterpret_cast<const uint32_t*>(in.blob + (o0[r] & ~3u)) + DONE_DW, dw[r][DONE_DW], sh, rem, s);
-    uint32_t hot_rule = 0;
-    const uint32_t hidx = hot_lookup(sh_hot, s.a, s.b, unit, hot_rule);
-    uint64_t hi, lo;
-    fp_final(s, (uint64_t)ws, hi, lo);
-    const uint32_t region = (unit - 1u) * 2u + (uint32_t)(widx & 1);
-    x.key = make_sort_key(region, hi);
-    x.lo = lo;
-    x.gen = (uint32_t)widx + 1u;
-    x.now_mod = (uint32_t)(now[r] - ws);
-    if (hidx != 0xFFFFFFFFu) {
-      if (hot_rule != x.rule) err |= ERR_V2_FALLBACK;  // a hot bucket must hold one key under one rule
-      x.bucket = hidx * 2u + (uint32_t)(widx & 1);
+    key_of(x, s, now[r], rr[r], sh_hot, err);
+  }
+}
+
+// Routed batch (owner side of the multi-GPU router): each record already carries the
+// prefix state of its key, its rule, now and hits (one 32-B load per descriptor).
+RL_DEV void load_routed(const DevBatch& in, const DevRule* __restrict__ rules, uint32_t n_rules,
+                        const HotEntry* sh_hot, uint32_t t0, D3 (&d)[R], uint32_t& err) {
+  const uint32_t tid = threadIdx.x;
+  RRec rc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t i = t0 + r * NT + tid;
+    if (i < in.n_desc) {
+      rc[r] = in.recs[i];
     } else {
-      x.bucket = HOT_BUCKETS + msd_bucket(x.key);
+      rc[r].a = rc[r].b = 0;
+      rc[r].now = rc[r].h = rc[r].greq = 0;
+      rc[r].rule = RL_NIL_RULE;
     }
+  }
+  DevRule rr[R];
+  bool ok[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    ok[r] = rc[r].rule < n_rules;
+    if (ok[r]) rr[r] = rules[rc[r].rule];
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t i = t0 + r * NT + tid;
+    D3& x = d[r];
+    x.req = rc[r].greq;
+    x.rule = rc[r].rule;
+    x.h = rc[r].h > 1u ? rc[r].h : 1u;
+    x.now_mod = 0;
+    x.gen = 0;
+    x.key = NIL_KEY;
+    x.lo = 0;
+    x.bucket = i < in.n_desc ? NIL_BUCKET : BKT_NONE;
+    if (!ok[r]) {
+      if (i < in.n_desc && rc[r].rule != RL_NIL_RULE) err |= ERR_BAD_INPUT;
+      continue;
+    }
+    if (rc[r].now > 0xFFFFFFF0u) {
+      err |= ERR_BAD_TIME;
+      continue;
+    }
+    key_of(x, FpState{rc[r].a, rc[r].b}, (int64_t)rc[r].now, rr[r], sh_hot, err);
   }
 }
 
@@ -324,6 +378,7 @@ RL_DEV SegEl seg_op(const SegEl& a, const SegEl& b) {
 // ---------------------------------------------------------------------------
 // k3_hist
 // ---------------------------------------------------------------------------
+template <bool ROUTED>
 __global__ __launch_bounds__(NT) void k3_hist(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
                                               uint64_t seed, const HotEntry* __restrict__ hot,
                                               uint32_t* __restrict__ req_thr, uint32_t* __restrict__ fpart,
@@ -360,7 +415,10 @@ __global__ __launch_bounds__(NT) void k3_hist(DevBatch in, const DevRule* __rest
   ST3(0, 1);
   D3 d[R];
   uint32_t err = 0;
-  load_descs(in, rules, n_rules, seed, sh_hot, t0, d, err);
+  if (ROUTED)
+    load_routed(in, rules, n_rules, sh_hot, t0, d, err);
+  else
+    load_descs(in, rules, n_rules, seed, sh_hot, t0, d, err);
   ST3(0, 2);
   uint32_t gmin[8], gmax[8], nil = 0;
 #pragma unroll
@@ -725,9 +783,10 @@ RL_DEV rl_status local_hit_status(uint32_t h, uint32_t reset) {
 }
 
 // Decision of a descriptor whose INCRBY post-value is base + P (decide_one in rl_decide.h).
+// routed: a routed record's ThrottleMillis slot is its own position (idx), not its request.
 RL_DEV void decide_at(uint32_t idx, uint32_t req, uint32_t rule, uint32_t h, uint32_t now_mod, uint64_t base,
                       uint64_t P, uint32_t freeze, const DevRule* __restrict__ rules, rl_status* __restrict__ out,
-                      uint32_t* __restrict__ req_thr) {
+                      uint32_t* __restrict__ req_thr, int routed) {
   SortedRec o;
   o.P = P;
   o.head = 0;
@@ -740,7 +799,7 @@ RL_DEV void decide_at(uint32_t idx, uint32_t req, uint32_t rule, uint32_t h, uin
   si.base = base;
   si.freeze = freeze;
   si.pad = 0;
-  decide_one(o, si, rules[rule], out, req_thr);
+  decide_one(o, si, rules[rule], out, req_thr, routed ? idx : req);
 }
 
 __global__ __launch_bounds__(NT) void k3_place(uint32_t n, const ARec* __restrict__ arec,
@@ -748,7 +807,7 @@ __global__ __launch_bounds__(NT) void k3_place(uint32_t n, const ARec* __restric
                                                const unsigned long long* __restrict__ hoff,
                                                const uint32_t* __restrict__ bbase, HotBucket3* __restrict__ hb,
                                                int local_cache, MRec* __restrict__ mrec, rl_status* __restrict__ out,
-                                               uint32_t* __restrict__ req_thr, Deferred* __restrict__ dfr,
+                                               uint32_t* __restrict__ req_thr, Deferred* __restrict__ dfr, int routed,
                                                EngineCtl* ctl) {
   __shared__ uint32_t s_rstar[HOT_BUCKETS];
   const uint32_t tid = threadIdx.x;
@@ -828,7 +887,7 @@ __global__ __launch_bounds__(NT) void k3_place(uint32_t n, const ARec* __restric
       }
       const uint64_t after = hx.base + P[r];
       if (!local_cache || after <= rl.L) {
-        decide_at(i, x.req, rule, x.h, now_mod, hx.base, P[r], SEG_NO_FREEZE, rules, out, req_thr);
+        decide_at(i, x.req, rule, x.h, now_mod, hx.base, P[r], SEG_NO_FREEZE, rules, out, req_thr, routed);
         continue;
       }
       const uint32_t rs = s_rstar[b];
@@ -837,7 +896,7 @@ __global__ __launch_bounds__(NT) void k3_place(uint32_t n, const ARec* __restric
         if (x.req > rs) {
           out[i] = local_hit_status(x.h, rl.div - now_mod);
         } else {  // same request as the freezing descriptor: its INCRBY still happens
-          decide_at(i, x.req, rule, x.h, now_mod, hx.base, P[r], SEG_NO_FREEZE, rules, out, req_thr);
+          decide_at(i, x.req, rule, x.h, now_mod, hx.base, P[r], SEG_NO_FREEZE, rules, out, req_thr, routed);
           atomicMax((unsigned long long*)&slot->count, (unsigned long long)after);
         }
       } else if (x.req > q0) {  // froze in an earlier tile, in a request <= q0
@@ -1098,7 +1157,7 @@ template <bool LDS>
 RL_DEV uint32_t group_range(const GStore& g, uint32_t hs, const MRec* __restrict__ recs, uint32_t m,
                             const DevRule* __restrict__ rules, const TableDesc& tab, int local_cache,
                             rl_status* __restrict__ out, uint32_t* __restrict__ req_thr, HotCand* cand, int cand_on,
-                            LSeg* s_agg, LSeg* s_carry, EngineCtl* ctl) {
+                            int routed, LSeg* s_agg, LSeg* s_carry, EngineCtl* ctl) {
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
   uint32_t heads = 0;
   for (uint32_t s = tid; s < hs; s += G_NT) {
@@ -1193,7 +1252,7 @@ RL_DEV uint32_t group_range(const GStore& g, uint32_t hs, const MRec* __restrict
   auto decide_k = [&](uint32_t k, const uint4& pk) {
     const uint32_t t = group_tail(g, k);
     decide_at(pk.x, pk.y, rule_of(pk.w), pk.z, pk.w >> V3_RULE_BITS, g.key[t], g.P[k], (uint32_t)g.lo[t], rules, out,
-              req_thr);
+              req_thr, routed);
   };
 #undef RL_G_STAGE
 #undef RL_G_LEAD
@@ -1217,7 +1276,7 @@ __global__ __launch_bounds__(G_NT) void k3_group(const MRec* __restrict__ mrec, 
                                                  const HotBucket3* __restrict__ hb, HotCand* __restrict__ cand,
                                                  int cand_on, const uint32_t* __restrict__ rngb,
                                                  const uint32_t* __restrict__ bbase, V3GroupScratch gs,
-                                                 uint32_t* __restrict__ wg_heads, EngineCtl* ctl) {
+                                                 uint32_t* __restrict__ wg_heads, int routed, EngineCtl* ctl) {
   __shared__ uint64_t s_key[G_CAP];
   __shared__ uint64_t s_lo[G_CAP];
   __shared__ uint2 s_pay[G_CAP];
@@ -1245,7 +1304,7 @@ __global__ __launch_bounds__(G_NT) void k3_group(const MRec* __restrict__ mrec, 
       if (df.req > x.rstar) {
         out[df.idx] = local_hit_status(df.h, rules[df.rule].div - df.now_mod);
       } else {
-        decide_at(df.idx, df.req, df.rule, df.h, df.now_mod, x.base, df.P, SEG_NO_FREEZE, rules, out, req_thr);
+        decide_at(df.idx, df.req, df.rule, df.h, df.now_mod, x.base, df.P, SEG_NO_FREEZE, rules, out, req_thr, routed);
         atomicMax((unsigned long long*)&reinterpret_cast<Slot*>(x.slot)->count, (unsigned long long)(x.base + df.P));
       }
     }
@@ -1277,7 +1336,7 @@ __global__ __launch_bounds__(G_NT) void k3_group(const MRec* __restrict__ mrec, 
     if (e > pos) {
       const GStore g{s_key, s_lo, s_pay, s_P, s_slot, s_cnt, s_end, s_list, s_grp, &s_cursor, G_HASH - 1, mrec + pos};
       heads += group_range<true>(g, G_HASH, mrec + pos, e - pos, rules, tab, local_cache, out, req_thr, cand, cand_on,
-                                 s_agg, &s_carry, ctl);
+                                 routed, s_agg, &s_carry, ctl);
     } else {
       e = bbase[bk + 1];
       ++bk;
@@ -1297,8 +1356,8 @@ __global__ __launch_bounds__(G_NT) void k3_group(const MRec* __restrict__ mrec, 
                      hs - 1,
                      mrec + pos};
       if (tid == 0) *g.cursor = 0;
-      heads += group_range<false>(g, hs, mrec + pos, mm, rules, tab, local_cache, out, req_thr, cand, cand_on, s_agg,
-                                  &s_carry, ctl);
+      heads += group_range<false>(g, hs, mrec + pos, mm, rules, tab, local_cache, out, req_thr, cand, cand_on, routed,
+                                  s_agg, &s_carry, ctl);
     }
     pos = e;
   }
@@ -1361,11 +1420,16 @@ __global__ __launch_bounds__(TAIL_NT) void k3_tail(DevBatch in, const DevRule* _
   HotCand c = cand[i];
   if (c.first_idx == 0xFFFFFFFFu) return;  // a hot key: state already known
   const uint32_t d = c.first_idx;
-  const uint32_t o0 = in.off[d], o1 = in.off[d + 1];
   const uint32_t unit = rules[c.rule].unit;
-  const FpState s = prefix_state(in.blob, o0, o1 - o0, unit, seed);
-  c.a = s.a;
-  c.b = s.b;
+  if (in.recs) {  // routed batch: the record already carries the prefix state
+    c.a = in.recs[d].a;
+    c.b = in.recs[d].b;
+  } else {
+    const uint32_t o0 = in.off[d], o1 = in.off[d + 1];
+    const FpState s = prefix_state(in.blob, o0, o1 - o0, unit, seed);
+    c.a = s.a;
+    c.b = s.b;
+  }
   c.unit = unit;
   cand[i] = c;
 }
@@ -1375,20 +1439,7 @@ __global__ __launch_bounds__(TAIL_NT) void k3_tail(DevBatch in, const DevRule* _
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-static DevBatch dev_batch(const rl_batch& b) {
-  DevBatch d;
-  d.n_desc = b.n_desc;
-  d.n_req = b.n_req;
-  d.blob_bytes = b.blob_bytes;
-  d.pad = 0;
-  d.blob = b.prefix_blob;
-  d.off = b.prefix_off;
-  d.rule = b.rule_id;
-  d.req_of = b.req_of;
-  d.now = b.now;
-  d.hits = b.hits_addend;
-  return d;
-}
+static DevBatch dev_batch(const rl_batch& b) { return make_dev_batch(b); }
 
 uint32_t v3_tiles(uint32_t n) { return n ? (n + V3_TILE - 1) / V3_TILE : 1; }
 uint32_t v3_group_wgs(uint32_t n) { return n ? (n + V3_GRANGE - 1) / V3_GRANGE : 1; }
@@ -1397,8 +1448,13 @@ uint32_t v3_scan_blocks() { return V3_SCAN_BUCKETS / 64; }
 void launch_v3_hist(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
                     const HotEntry* hot, uint32_t* req_thr, uint32_t* fpart, uint16_t* tcount,
                     unsigned long long* thsum, ARec* arec, EngineCtl* ctl) {
-  hipLaunchKernelGGL(v3::k3_hist, dim3(v3_tiles(b.n_desc)), dim3(V3_THREADS), 0, st, dev_batch(b), rules, n_rules,
-                     seed, hot, req_thr, fpart, tcount, thsum, arec, ctl);
+  const DevBatch in = dev_batch(b);
+  if (in.recs)
+    hipLaunchKernelGGL(v3::k3_hist<true>, dim3(v3_tiles(b.n_desc)), dim3(V3_THREADS), 0, st, in, rules, n_rules,
+                       seed, hot, req_thr, fpart, tcount, thsum, arec, ctl);
+  else
+    hipLaunchKernelGGL(v3::k3_hist<false>, dim3(v3_tiles(b.n_desc)), dim3(V3_THREADS), 0, st, in, rules, n_rules,
+                       seed, hot, req_thr, fpart, tcount, thsum, arec, ctl);
 }
 void launch_v3_scan(hipStream_t st, uint32_t n, const uint16_t* tcount, const unsigned long long* thsum,
                     uint32_t* toff, unsigned long long* hoff, uint32_t* btotal, const uint32_t* fpart, const HotEntry* hot_list, HotBucket3* hb, const TableDesc& tab,
@@ -1412,17 +1468,17 @@ void launch_v3_bases(hipStream_t st, uint32_t n, const uint32_t* btotal, uint32_
 }
 void launch_v3_place(hipStream_t st, uint32_t n, const ARec* arec, const DevRule* rules, const uint32_t* toff,
                      const unsigned long long* hoff, const uint32_t* bbase, HotBucket3* hb, int local_cache,
-                     MRec* mrec, rl_status* out, uint32_t* req_thr, Deferred* dfr, EngineCtl* ctl) {
+                     MRec* mrec, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed, EngineCtl* ctl) {
   hipLaunchKernelGGL(v3::k3_place, dim3(v3_tiles(n)), dim3(V3_THREADS), 0, st, n, arec, rules, toff, hoff, bbase, hb,
-                     local_cache, mrec, out, req_thr, dfr, ctl);
+                     local_cache, mrec, out, req_thr, dfr, routed, ctl);
 }
 void launch_v3_group(hipStream_t st, uint32_t n, const MRec* mrec, const uint32_t* rng, const DevRule* rules,
                      const TableDesc& tab, int local_cache, rl_status* out, uint32_t* req_thr, const Deferred* dfr,
                      const HotBucket3* hb, HotCand* cand, int cand_on, const uint32_t* rngb, const uint32_t* bbase,
-                     const V3GroupScratch& gs, uint32_t* wg_heads, EngineCtl* ctl) {
+                     const V3GroupScratch& gs, uint32_t* wg_heads, int routed, EngineCtl* ctl) {
   const uint32_t nw = v3_group_wgs(n);
   hipLaunchKernelGGL(v3::k3_group, dim3(nw + 1), dim3(v3::G_NT), 0, st, mrec, rng, nw, rules, tab, local_cache, out,
-                     req_thr, dfr, hb, cand, cand_on, rngb, bbase, gs, wg_heads, ctl);
+                     req_thr, dfr, hb, cand, cand_on, rngb, bbase, gs, wg_heads, routed, ctl);
 }
 void launch_v3_tail(hipStream_t st, const rl_batch& b, const DevRule* rules, uint64_t seed, HotCand* cand,
                     const uint32_t* wg_heads, uint32_t n_heads, EngineCtl* ctl, EngineCtl* next_ctl) {

@@ -80,7 +80,18 @@ ABI = [
                          C.c_uint32, C.POINTER(C.c_uint32)], C.c_int),
     ("rl_last_batch_info", [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                             C.POINTER(C.c_uint64)], C.c_int),
+    ("rl_set_stream", [C.c_void_p, C.c_void_p], C.c_int),
+    ("rl_route_pack", [C.c_void_p, C.POINTER(RlBatch), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                       C.POINTER(C.c_uint32)], C.c_int),
+    ("rl_submit_routed", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p], C.c_int),
+    ("rl_route_unpack", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
 ]
+
+# multi-GPU router record sizes (include/rl_hip.h RL_ROUTE_*)
+ROUTE_RECORD_BYTES = 32
+ROUTE_REPLY_BYTES = 24
+ROUTE_MAX_SHARDS = 16
+ROUTE_LOCAL = 0xFFFFFFFF
 
 _lib = None
 
@@ -289,6 +300,33 @@ class Engine:
 
     def stream(self) -> int:
         return self.lib.rl_stream(self.h) or 0
+
+    def set_stream(self, hip_stream: int):
+        """Order the engine's work on an external HIP stream (0 = the engine's own)."""
+        self._check(self.lib.rl_set_stream(self.h, hip_stream or None), "rl_set_stream")
+
+    # -- multi-GPU router (include/rl_hip.h, "Multi-GPU router") -----------------------
+    def route_pack(self, n_desc: int, n_req: int, blob_bytes: int, ptrs, origin: int, n_shards: int, send_ptr: int,
+                   send_counts_ptr: int, perm_ptr: int) -> list:
+        """Device batch -> routed records grouped by owner; returns the per-owner counts."""
+        s = RlBatch()
+        s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
+        s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        counts = (C.c_uint32 * n_shards)()
+        self._check(self.lib.rl_route_pack(self.h, C.byref(s), origin, n_shards, send_ptr, send_counts_ptr, perm_ptr,
+                                           counts), "rl_route_pack")
+        return list(counts)
+
+    def submit_routed_async(self, rec_ptr: int, n: int, reply_ptr: int):
+        self._check(self.lib.rl_submit_routed(self.h, rec_ptr, n, reply_ptr), "rl_submit_routed")
+
+    def route_unpack(self, n_desc: int, n_req: int, req_of_ptr: int, perm_ptr: int, reply_ptr: int, out_ptr: int,
+                     thr_ptr: int):
+        s = RlBatch()
+        s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, 0, 0
+        s.req_of = req_of_ptr
+        self._check(self.lib.rl_route_unpack(self.h, C.byref(s), perm_ptr, reply_ptr, out_ptr, thr_ptr),
+                    "rl_route_unpack")
 
 
 # ---------------------------------------------------------------------------

@@ -1,0 +1,135 @@
+"""Multi-GPU routed DoLimit step (include/rl_hip.h "Multi-GPU router").
+
+One process per GPU. The key space is hash-sharded one shard per GPU: the owner of a key is
+a mix of its prefix fingerprint lanes (rl_common.h route_owner), so every window of a key
+and every origin agree on it — the analogue of the reference sending each key's INCRBY to
+the Redis server that holds it (src/redis/fixed_cache_impl.go:66-80,
+src/redis/driver_impl.go:56-90). One step of a rank:
+
+  1. pack      its own batch -> 32-B records grouped by owner (+ counts, perm)
+  2. all-to-all of the per-owner counts
+  3. all-to-all of the records (variable splits)
+  4. decide    the records received from every origin, origin-major (the owner's engine)
+  5. all-to-all of the 24-B replies (reverse splits)
+  6. unpack    replies -> rl_status[n_desc] and ThrottleMillis[n_req] in its own order
+
+The exchange is plain torch.distributed (RCCL over xGMI for "nccl", gloo on CPU for the
+tests); the shard object does steps 1, 4 and 6. EngineShard is the product shard (HIP
+engine, device tensors); a test shard with the same byte layouts can stand in on CPU.
+
+An owner decides what it receives as if the origins' batches had been submitted to one
+engine in rank order, so the multi-GPU result equals one serial DoLimit stream.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+import hiprl
+
+REC = hiprl.ROUTE_RECORD_BYTES
+REP = hiprl.ROUTE_REPLY_BYTES
+STATUS_BYTES = 20
+
+
+@dataclass
+class DeviceBatch:
+    """A flat batch (rl_batch layout) resident on the shard's device."""
+    blob: torch.Tensor   # uint8
+    off: torch.Tensor    # int32 [n_desc + 1]
+    rule: torch.Tensor   # int32 [n_desc]
+    req_of: torch.Tensor  # int32 [n_desc]
+    now: torch.Tensor    # int64 [n_req]
+    hits: torch.Tensor   # int32 [n_req]
+    nbytes: int = -1     # prefix bytes used (off[-1]); -1 = read it from the device
+
+    @property
+    def n_desc(self) -> int:
+        return int(self.rule.shape[0])
+
+    @property
+    def n_req(self) -> int:
+        return int(self.now.shape[0])
+
+    @classmethod
+    def from_host(cls, b: "hiprl.Batch", device) -> "DeviceBatch":
+        import numpy as np
+
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+        # the device path reads prefix bytes as 16-B loads: keep 16 B of slack past the end
+        blob = np.zeros(int(b.blob.shape[0]) + 16, np.uint8)
+        blob[:b.blob.shape[0]] = b.blob
+        return cls(t(blob), t(b.off.view(np.int32)), t(b.rule.view(np.int32)), t(b.req_of.view(np.int32)),
+                   t(b.now), t(b.hits.view(np.int32)), int(b.off[-1]))
+
+    def ptrs(self):
+        return [self.blob.data_ptr(), self.off.data_ptr(), self.rule.data_ptr(), self.req_of.data_ptr(),
+                self.now.data_ptr(), self.hits.data_ptr()]
+
+    def blob_bytes(self) -> int:
+        if self.nbytes < 0:
+            self.nbytes = int(self.off[-1].item()) if self.n_desc else 0
+        return self.nbytes
+
+
+class EngineShard:
+    """The product shard: one hiprl.Engine on this rank's GPU, ordered on torch's current
+    stream (RCCL collectives synchronise with it, so no host waits are needed between steps
+    beyond the count exchange and the owner's batch)."""
+
+    def __init__(self, engine: "hiprl.Engine", rank: int, world: int, device, max_desc: int):
+        if world > hiprl.ROUTE_MAX_SHARDS:
+            raise ValueError(f"at most {hiprl.ROUTE_MAX_SHARDS} shards")
+        self.eng, self.rank, self.world, self.device = engine, rank, world, device
+        self.eng.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        self.send = torch.empty(max_desc * REC, dtype=torch.uint8, device=device)
+        self.perm = torch.empty(max(1, max_desc), dtype=torch.int32, device=device)
+        self.counts = torch.empty(world, dtype=torch.int32, device=device)
+
+    def empty(self, nbytes: int) -> torch.Tensor:
+        return torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+
+    def pack(self, b: DeviceBatch):
+        counts = self.eng.route_pack(b.n_desc, b.n_req, b.blob_bytes(), b.ptrs(), self.rank, self.world,
+                                     self.send.data_ptr(), self.counts.data_ptr(), self.perm.data_ptr())
+        return self.send[:sum(counts) * REC], self.counts, counts, self.perm[:b.n_desc]
+
+    def decide(self, recv: torch.Tensor, n: int) -> torch.Tensor:
+        reply = self.empty(n * REP)
+        self.eng.submit_routed_async(recv.data_ptr() if n else 0, n, reply.data_ptr() if n else 0)
+        self.eng.wait()
+        return reply
+
+    def unpack(self, b: DeviceBatch, perm: torch.Tensor, back: torch.Tensor):
+        out = self.empty(b.n_desc * STATUS_BYTES)
+        thr = torch.empty(b.n_req, dtype=torch.int32, device=self.device)
+        self.eng.route_unpack(b.n_desc, b.n_req, b.req_of.data_ptr(), perm.data_ptr(),
+                              back.data_ptr() if back.numel() else 0, out.data_ptr(), thr.data_ptr())
+        return out, thr
+
+
+class ShardRouter:
+    """Steps 2, 3 and 5 of the routed step over a torch.distributed group."""
+
+    def __init__(self, shard, group=None):
+        self.shard = shard
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.last_recv = 0  # records this rank decided as owner in the last step
+
+    def step(self, b):
+        sh = self.shard
+        send, counts_t, counts, perm = sh.pack(b)
+        rcounts_t = torch.empty_like(counts_t)
+        dist.all_to_all_single(rcounts_t, counts_t, group=self.group)
+        rcounts = [int(x) for x in rcounts_t.tolist()]
+        n_in = sum(rcounts)
+        recv = sh.empty(n_in * REC)
+        dist.all_to_all_single(recv, send, [c * REC for c in rcounts], [c * REC for c in counts], group=self.group)
+        reply = sh.decide(recv, n_in)
+        back = sh.empty(sum(counts) * REP)
+        dist.all_to_all_single(back, reply, [c * REP for c in counts], [c * REP for c in rcounts], group=self.group)
+        self.last_recv = n_in
+        return sh.unpack(b, perm, back)

@@ -7,9 +7,12 @@ per batch (one descriptor per request, hits_addend 1), `now` advancing 1 s per b
 A step = one batch through the whole device path (fingerprint, radix sort, segmented scan,
 table apply, decide). Inputs are resident in HBM before timing; outputs stay in HBM.
 
-Multi-GPU (torchrun, one rank per GPU): each rank owns an independent key shard (its own
-domain, its own counter table) and processes its own batch per step — weak scaling with
-no data-path collective. value = descriptors decided by all ranks / max-over-ranks time.
+Multi-GPU (torchrun, one rank per GPU): the key space is hash-sharded one
+shard per GPU. Every rank ingests its own 1e6-descriptor batch per step, routes each
+descriptor to the GPU owning its key with an RCCL all-to-all (32-B records), the owners
+decide, and the 24-B replies return with the reverse all-to-all (api-ratelimit_amd/router.py)
+— weak scaling. value = descriptors decided for all ranks / max-over-ranks time.
+--independent runs N unrouted replicas instead (each rank its own key space).
 
 Also reported (rank 0): per-kernel HIP-event times over an extra K steps, the roofline
 of the batch pipeline against §8(d)'s algorithmic bytes, and the CPU oracle timed on a
@@ -30,6 +33,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "api-ratelimit_amd"))
 
 import hiprl  # noqa: E402
+import router  # noqa: E402
 import workload  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -46,6 +50,8 @@ def parse():
     ap.add_argument("--no-kernel-times", action="store_true")
     ap.add_argument("--pipeline", choices=["v3", "v2", "lsd"], default="v3",
                     help="decision pipeline (v3 default; v2 = bucketed pipeline; lsd = radix-sort pipeline only)")
+    ap.add_argument("--independent", action="store_true",
+                    help="N>1: unrouted replicas (each rank its own key space) instead of RCCL routing")
     ap.add_argument("--json-out", type=str, default="")
     return ap.parse_args()
 
@@ -86,26 +92,27 @@ def main():
         host_batches.append(hb)
     t_gen = time.time() - t_gen
 
-    eng = hiprl.Engine(device=local, log2_slots=log2, max_batch_desc=d, max_batch_req=d,
+    routed = world > 1 and not args.independent
+    # an owner may receive up to every origin's batch (hot keys concentrate on their owner)
+    cap = d * world if routed else d
+    eng = hiprl.Engine(device=local, log2_slots=log2, max_batch_desc=cap, max_batch_req=cap,
                        max_blob_bytes=max(int(hb.blob.shape[0]) for hb in host_batches) + 64, sort_bits=48,
                        pipeline=args.pipeline)
     eng.load_rules(rules)
 
-    def upload(hb):
-        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-        return dict(blob=t(hb.blob), off=t(hb.off.view(np.int32)), rule=t(hb.rule.view(np.int32)),
-                    req=t(hb.req_of.view(np.int32)), now=t(hb.now), hits=t(hb.hits.view(np.int32)),
-                    n_desc=hb.n_desc, n_req=hb.n_req, blob_bytes=int(hb.off[-1]))
-
-    dev_batches = [upload(hb) for hb in host_batches]
+    dev_batches = [router.DeviceBatch.from_host(hb, dev) for hb in host_batches]
     out = torch.empty(d * 20, dtype=torch.uint8, device=dev)
     thr = torch.empty(d, dtype=torch.int32, device=dev)
+    rtr = None
+    if routed:
+        rtr = router.ShardRouter(router.EngineShard(eng, rank, world, dev, d))
     torch.cuda.synchronize()
 
     def step(db):
-        ptrs = [db["blob"].data_ptr(), db["off"].data_ptr(), db["rule"].data_ptr(), db["req"].data_ptr(),
-                db["now"].data_ptr(), db["hits"].data_ptr()]
-        eng.submit_device_async(db["n_desc"], db["n_req"], db["blob_bytes"], ptrs, out.data_ptr(), thr.data_ptr())
+        if rtr is not None:
+            rtr.step(db)
+            return
+        eng.submit_device_async(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), out.data_ptr(), thr.data_ptr())
         eng.wait()
 
     for b in range(args.warmup):
@@ -213,7 +220,9 @@ def main():
         "dtype": "u64",
         "data": "synthetic (seeded splitmix64 / bounded Zipf stream, generated on host, resident in HBM)",
         "config": {"workload": wl, "descriptors_per_batch": d, "requests_per_batch": d,
-                   "parallelism": f"key-sharded x{world} (independent shards, no collective)",
+                   "parallelism": (f"key-sharded x{world}, RCCL all-to-all routing (32-B records out, 24-B replies back)"
+                                   if routed else "single shard" if world == 1
+                                   else f"x{world} independent replicas (no collective)"),
                    "pipeline": args.pipeline, "unique_keys_per_batch": int(U)},
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -143,6 +143,46 @@ int rl_submit_device(rl_engine* e, const rl_batch* device_batch, rl_status* d_ou
 /* The engine's HIP stream (hipStream_t), for ordering external work against it. */
 void* rl_stream(rl_engine* e);
 
+/* Run the engine's work on an external stream (e.g. the stream RCCL collectives run on), so
+ * that device-side ordering needs no host synchronisation; NULL restores the engine's own
+ * stream. The stream must outlive its use. Not while a batch is in flight. */
+int rl_set_stream(rl_engine* e, void* hip_stream);
+
+/* ---- Multi-GPU router -------------------------------------------------
+ * One engine per GPU; GPU s owns the keys whose prefix fingerprint maps to s (every window
+ * of a key lands on the same GPU, like a Redis cluster slot for the reference's INCRBY
+ * pipeline, src/redis/fixed_cache_impl.go:66-80, driver_impl.go:56-90). All shards must use
+ * the same hash_seed and rule table. One routed step:
+ *   origin: rl_route_pack       batch -> records grouped by owner, per-owner counts
+ *   RCCL:   all-to-all of counts, then of records (send_counts / received counts)
+ *   owner:  rl_submit_routed    records received from every origin (origin-major) -> replies
+ *   RCCL:   all-to-all of replies (reverse splits)
+ *   origin: rl_route_unpack     replies -> rl_status[n_desc], ThrottleMillis[n_req]
+ * An owner decides records in origin-major order, i.e. as if the origins' batches had been
+ * submitted to one engine one after another. */
+#define RL_ROUTE_RECORD_BYTES 32u
+#define RL_ROUTE_REPLY_BYTES 24u
+#define RL_ROUTE_MAX_SHARDS 16u
+#define RL_ROUTE_MAX_REQ (1u << 27) /* requests per origin batch */
+#define RL_ROUTE_LOCAL 0xFFFFFFFFu  /* perm[] value of a nil-limit descriptor (decided at the origin) */
+
+/* Device batch -> d_send[n_desc routed records, grouped by owner 0..n_shards-1, serial order
+ * inside each group], d_perm[n_desc] (record position, or RL_ROUTE_LOCAL), per-owner record
+ * counts in d_send_counts[n_shards] and h_send_counts[n_shards]. Validates the batch
+ * (unknown rule / request index, time outside [0, 2^32)) and synchronises the stream. */
+int rl_route_pack(rl_engine* e, const rl_batch* device_batch, uint32_t origin, uint32_t n_shards, void* d_send,
+                  uint32_t* d_send_counts, uint32_t* d_perm, uint32_t* h_send_counts);
+
+/* Owner side: decide n routed records (device memory, RL_ROUTE_RECORD_BYTES each) and write
+ * one reply per record (RL_ROUTE_REPLY_BYTES each: rl_status + ThrottleMillis) into d_reply.
+ * Asynchronous like rl_submit_device; rl_wait() completes it. */
+int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_reply);
+
+/* Origin side: replies (in d_send order) -> d_out[n_desc] and d_req_throttle_ms[n_req].
+ * Ordered on the engine stream; no host synchronisation. */
+int rl_route_unpack(rl_engine* e, const rl_batch* device_batch, const uint32_t* d_perm, const void* d_reply,
+                    rl_status* d_out, uint32_t* d_req_throttle_ms);
+
 /* Clear the counter table and local-cache state (FLUSHALL analogue; tests and restarts). */
 int rl_reset(rl_engine* e);
 

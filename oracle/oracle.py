@@ -139,6 +139,24 @@ def fingerprints(blob: np.ndarray, off: np.ndarray, window_start: int, unit: int
     return hi, lo
 
 
+def prefix_lanes(prefix: bytes, unit: int, seed: int):
+    """Fingerprint lanes (a, b) of a key prefix before the window: the routed key identity."""
+    a, b = C.c_uint64(), C.c_uint64()
+    L = lib()
+    L.rlo_prefix_lanes.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_uint64)]
+    L.rlo_prefix_lanes.restype = None
+    L.rlo_prefix_lanes(prefix, len(prefix), unit, seed, C.byref(a), C.byref(b))
+    return a.value, b.value
+
+
+def route_owner(a: int, b: int, n_shards: int) -> int:
+    L = lib()
+    L.rlo_route_owner.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
+    L.rlo_route_owner.restype = C.c_uint32
+    return int(L.rlo_route_owner(a, b, n_shards))
+
+
 def fingerprint(prefix: bytes, window_start: int, unit: int, seed: int):
     hi, lo = C.c_uint64(), C.c_uint64()
     lib().rlo_fingerprint(prefix, len(prefix), window_start, unit, seed, C.byref(hi), C.byref(lo))

@@ -17,6 +17,28 @@ inline uint64_t fmix(uint64_t x) {
 }
 }  // namespace
 
+// Prefix lanes (a, b) before the window is folded in: also the routed record's key identity.
+extern "C" void rlo_prefix_lanes(const uint8_t* prefix, uint32_t len, uint32_t unit, uint64_t seed, uint64_t* a_out,
+                                 uint64_t* b_out) {
+  uint64_t a = seed ^ 0x9E3779B97F4A7C15ull;
+  uint64_t b = (seed + 0xC2B2AE3D27D4EB4Full) ^ ((uint64_t)len << 32) ^ (uint64_t)unit;
+  for (uint32_t o = 0; o < len; o += 8) {
+    uint64_t w = 0;
+    for (uint32_t k = 0; k < 8 && o + k < len; ++k) w |= (uint64_t)prefix[o + k] << (8 * k);
+    a = rotl((a ^ w) * 0x165667B19E3779F9ull, 31);
+    b = (b + w) * 0xD6E8FEB86659FD93ull;
+    b ^= b >> 29;
+  }
+  *a_out = a;
+  *b_out = b;
+}
+
+// Multi-GPU owner of a key (the product's route_owner): multiply-shift of a lane mix.
+extern "C" uint32_t rlo_route_owner(uint64_t a, uint64_t b, uint32_t n_shards) {
+  const uint64_t x = fmix(a ^ rotl(b, 29));
+  return (uint32_t)(((x >> 32) * (uint64_t)n_shards) >> 32);
+}
+
 extern "C" void rlo_fingerprint(const uint8_t* prefix, uint32_t len, uint64_t window_start, uint32_t region,
                                 uint64_t seed, uint64_t* hi, uint64_t* lo) {
   // lanes: a = seed ^ K0, b = (seed + K1) ^ (len << 32) ^ unit

@@ -96,6 +96,9 @@ void rlo_local_cache_stats(rlo_engine* e, uint64_t* hit, uint64_t* miss, uint64_
  * fingerprint kernel (tests/test_fingerprint*.py); decisions above never use it. */
 void rlo_fingerprint(const uint8_t* prefix, uint32_t len, uint64_t window_start, uint32_t region, uint64_t seed,
                      uint64_t* hi, uint64_t* lo);
+/* Multi-GPU routing restated (tests of the router): prefix lanes and owner shard. */
+void rlo_prefix_lanes(const uint8_t* prefix, uint32_t len, uint32_t unit, uint64_t seed, uint64_t* a, uint64_t* b);
+uint32_t rlo_route_owner(uint64_t a, uint64_t b, uint32_t n_shards);
 void rlo_fingerprint_many(const uint8_t* blob, const uint32_t* off, uint32_t n, uint64_t window_start, uint32_t unit,
                           uint64_t seed, uint64_t* hi, uint64_t* lo);
 

@@ -5,6 +5,8 @@ i.e. oracle.Oracle (CPU restatement) or hiprl.Engine (HIP path via the C ABI).
 """
 from __future__ import annotations
 
+import zlib
+
 import numpy as np
 
 import hiprl
@@ -118,3 +120,59 @@ def assert_same(a_st, a_thr, b_st, b_thr, ctx=""):
         bad = np.nonzero(a_thr != b_thr)[0]
         i = int(bad[0])
         raise AssertionError(f"{ctx}: {len(bad)} request throttles differ; first at {i}: {a_thr[i]} vs {b_thr[i]}")
+
+
+# ---------------------------------------------------------------------------
+# Seeded random request streams (parity tests, router tests)
+# ---------------------------------------------------------------------------
+UNITS = [hiprl.SECOND, hiprl.MINUTE, hiprl.HOUR, hiprl.DAY]
+LS = [1, 3, 10, 40]  # limits per unit -> rule id = u * len(LS) + l
+RULES = [(L, u) for u in UNITS for L in LS]
+
+
+def make_stream(seed, n_req, t0, keyspace=40, max_desc=4, nil_p=0.08, override_p=0.05, dt_max=2):
+    rng = np.random.default_rng(seed)
+    reqs = []
+    t = t0
+    for _ in range(n_req):
+        if rng.random() < 0.02:
+            t += int(rng.integers(1, dt_max + 1))
+        dom = ["dom", "a", "a_b"][int(rng.integers(0, 3))]
+        nd = int(rng.integers(1, max_desc + 1))
+        descs, rules = [], []
+        for _ in range(nd):
+            kind = rng.random()
+            if kind < 0.1:  # colliding entry splits: same key string
+                descs.append([("a_b", "c")] if rng.random() < 0.5 else [("a", "b_c")])
+            else:
+                ne = int(rng.integers(1, 4))
+                descs.append([(f"k{j}", f"v{int(rng.integers(0, keyspace))}") for j in range(ne)])
+            if rng.random() < nil_p:
+                rules.append(NIL)
+                continue
+            prefix = hiprl.cache_key_prefix(dom, descs[-1])
+            hsh = zlib.crc32(prefix)
+            u = hsh % 4  # the unit is a function of the key string
+            li = (hsh >> 8) % len(LS)
+            if rng.random() < override_p:
+                li = int(rng.integers(0, len(LS)))
+            rules.append(u * len(LS) + li)
+        if rng.random() < 0.05 and nd > 0:  # duplicate a descriptor inside the request
+            descs.append(descs[0])
+            rules.append(rules[0])
+        reqs.append((dom, descs, rules, int(rng.integers(0, 9)), t))
+    return reqs
+
+
+def batch_sizes(reqs, rng, max_bs):
+    """Random batch cuts that keep each batch within two adjacent seconds."""
+    sizes, i = [], 0
+    while i < len(reqs):
+        bs = int(rng.integers(1, max_bs + 1))
+        j = i + 1
+        t_lo = reqs[i][4]
+        while j < len(reqs) and j - i < bs and reqs[j][4] - t_lo <= 1:
+            j += 1
+        sizes.append(j - i)
+        i = j
+    return sizes
