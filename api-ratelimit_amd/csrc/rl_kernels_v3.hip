@@ -370,7 +370,7 @@ struct SegEl {
   uint32_t f, hp;
   unsigned long long s;
 };
-RL_DEV SegEl seg_op(const SegEl& a, const SegEl& b) {
+RL_DEV SegEl seg_op(const SegEl a, const SegEl b) {
   if (b.f) return b;
   return SegEl{a.f, a.hp, a.s + b.s};
 }
@@ -497,7 +497,11 @@ __global__ __launch_bounds__(NT) void k3_hist(DevBatch in, const DevRule* __rest
     if (lane == 0) wex = SegEl{0, 0, 0};
     __syncthreads();
     SegEl run{0, 0, 0};
-    for (uint32_t w = 0; w < wave; ++w) run = seg_op(run, s_agg[w]);
+#pragma unroll
+    for (int w = 0; w < W - 1; ++w) {
+      const SegEl a = s_agg[w];  // wave-uniform LDS read; no private copy of the array
+      if ((uint32_t)w < wave) run = seg_op(run, a);
+    }
     run = seg_op(run, wex);
 #pragma unroll
     for (int q = 0; q < R; ++q) {

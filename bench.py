@@ -48,12 +48,40 @@ def parse():
     ap.add_argument("--desc", type=int, default=1_000_000, help="descriptors per batch")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-kernel-times", action="store_true")
+    ap.add_argument("--no-roofline-probe", action="store_true")
     ap.add_argument("--pipeline", choices=["v3", "v2", "lsd"], default="v3",
                     help="decision pipeline (v3 default; v2 = bucketed pipeline; lsd = radix-sort pipeline only)")
     ap.add_argument("--independent", action="store_true",
                     help="N>1: unrouted replicas (each rank its own key space) instead of RCCL routing")
     ap.add_argument("--json-out", type=str, default="")
     return ap.parse_args()
+
+
+def random_access_roofline(eng, alg_bytes, U, pipe_ms, step_ms):
+    import ctypes as C
+
+    lp = ROOT / "tools" / "microbench" / "libroofline_probe.so"
+    if not lp.exists() or U <= 0:
+        return None
+    lib = C.CDLL(str(lp))
+    lib.rl_probe_roofline.argtypes = [C.c_uint64, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                      C.POINTER(C.c_double)]
+    lib.rl_probe_roofline.restype = C.c_int
+    slots = sum(2 << int(x) for x in eng.cfg.log2_slots)  # 8 regions: unit x window parity
+    gbs, rate, rus = C.c_double(), C.c_double(), C.c_double()
+    if lib.rl_probe_roofline(slots, U, C.byref(gbs), C.byref(rate), C.byref(rus)):
+        return None
+    stream_bytes = alg_bytes - 64 * U
+    t_roof_us = stream_bytes / (gbs.value * 1e9) * 1e6 + U / rate.value * 1e6
+    return {"t_roof_us": round(t_roof_us, 2), "frac_of_step": round(t_roof_us / (step_ms * 1e3), 4),
+            "frac_of_kernel_time": round(t_roof_us / (pipe_ms * 1e3), 4),
+            "streaming_bytes": int(stream_bytes), "copy_GBps": round(gbs.value, 1),
+            "table_slots": int(1 << (slots.bit_length() - 1)), "U": U,
+            "slot_rmw_per_s": round(rate.value, 1), "slot_rmw_us": round(rus.value, 2),
+            "atomics_per_s": round(U / (step_ms * 1e-3), 1),
+            "definition": "SURVEY.md 8(d): t_roof = streaming_B / copy_BW + U / RMW_rate (U random 32-B slot "
+                          "load + 64-bit atomicAdd on a table of the engine's size, power-of-two rounded); "
+                          "frac = t_roof / t"}
 
 
 def main():
@@ -167,7 +195,9 @@ def main():
         achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
         prof_dir = ROOT / "profiles"
         traffic = None
-        tf = prof_dir / "r01_pmc_traffic.json"
+        # PMC traffic of this pipeline from the committed rocprofv3 --pmc passes (tools/profile_round.sh)
+        tf = prof_dir / {"v3": "r01_v3_pmc_traffic.json", "v2": "r01_v2_pmc_traffic.json",
+                         "lsd": "r01_pmc_traffic.json"}[args.pipeline]
         if tf.exists():
             try:
                 traffic = json.loads(tf.read_text()).get("hbm_bytes_per_batch")
@@ -184,6 +214,13 @@ def main():
                                 "avg_us_per_launch": round(kernel[dom]["total_ms"] * 1e3 / kernel[dom]["launches"], 2)},
             "kernels_us_per_batch": {k: round(v * 1e3, 2) for k, v in per_batch_ms.items()},
         }
+
+    # SURVEY.md §8d random-access roofline: t_roof = streaming bytes / copy bandwidth + U /
+    # random slot-RMW rate, both measured here on a table of the engine's size.
+    if roofline is not None and not args.no_roofline_probe:
+        ra = random_access_roofline(eng, alg_bytes, int(U), pipe_ms, elapsed / args.steps * 1e3)
+        if ra:
+            roofline["random_access"] = ra
 
     cpu = None
     if world == 1 and args.cpu_seconds > 0:

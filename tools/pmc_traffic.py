@@ -15,12 +15,12 @@ steps = int(sys.argv[3]) if len(sys.argv) > 3 else 7  # warmup + steps of the pm
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].replace("rlhip::", "")
+        k = r["Kernel_Name"].split("(")[0].split("::")[-1].replace("void ", "")
         vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 per_kernel = {}
 fetch_raw = write = 0.0
 for k, c in vals.items():
-    if not k.startswith("k_"):
+    if not (k.startswith("k_") or k.startswith("k3_")):
         continue
     n_fetch = len(c.get("FETCH_SIZE", []))
     per_batch = n_fetch / steps if n_fetch else 0
@@ -32,7 +32,12 @@ for k, c in vals.items():
                                      max(1.0, sum(c.get("TCC_HIT_sum", [0])) + sum(c.get("TCC_MISS_sum", [0]))))}
     fetch_raw += f * per_batch
     write += w * per_batch
-res = {"hbm_bytes_per_batch": fetch_raw * 2 + write, "fetch_bytes_raw_per_batch": fetch_raw,
+# steady state: kernels that run every batch (the LSD fallback of the first batch, before a
+# hot set exists, runs once per process and is reported per kernel only)
+ss_f = sum(v["fetch_bytes_raw"] * v["launches_per_batch"] for v in per_kernel.values() if v["launches_per_batch"] >= 0.9)
+ss_w = sum(v["write_bytes"] * v["launches_per_batch"] for v in per_kernel.values() if v["launches_per_batch"] >= 0.9)
+res = {"hbm_bytes_per_batch": ss_f * 2 + ss_w, "steady_state_fetch_bytes_raw": ss_f, "steady_state_write_bytes": ss_w,
+       "all_kernels_hbm_bytes_per_batch": fetch_raw * 2 + write, "fetch_bytes_raw_per_batch": fetch_raw,
        "fetch_bytes_x2_per_batch": fetch_raw * 2, "write_bytes_per_batch": write,
        "note": "FETCH_SIZE x2 per MI355X_MICROARCH.md gfx950 correction; WRITE_SIZE uncorrected",
        "per_kernel_per_launch": per_kernel}
