@@ -1,4 +1,4 @@
-// rl_kernels_v3.hip — the default decision pipeline: five launches per batch.
+// rl_kernels_v3.hip — the default decision pipeline: six launches per batch.
 //
 // Same contract and outputs as the LSD pipeline (rl_kernels.hip, kept as the fallback).
 // The batch input is read once; hot keys are decided where they stand in arrival order,
@@ -10,8 +10,8 @@
 //              the in-tile INCRBY prefix of every hot descriptor, the in-tile rank of every
 //              other one; one 32-B record per descriptor (ARec); zero ThrottleMillis
 //   k3_scan    per bucket: exclusive scan over tiles (counts; h sums of hot buckets); per hot
-//              bucket: table claim and the counter before the batch (one key per bucket);
-//              the last workgroup: bucket start positions and k3_group ranges
+//              bucket: table claim and the counter before the batch (one key per bucket)
+//   k3_bases   bucket start positions and k3_group ranges
 //   k3_place   per descriptor: hot -> INCRBY post-value = base + tile prefix + in-tile prefix,
 //              decision written in place; nil limit -> decided in place; the rest -> 32-B MRec
 //              scattered into bucket order
