@@ -200,7 +200,10 @@ constexpr int V3_TILE = 2048;             // k3_hist / k3_place arrival tile
 constexpr int V3_THREADS = 512;
 constexpr int V3_ROW16 = (NBUCKETS + 7) / 8 * 8;  // tile histogram row (u16 counts)
 constexpr int V3_SCAN_BUCKETS = HOT_BUCKETS + MSD_BUCKETS;  // buckets k3_scan scans (not NIL)
-constexpr int V3_GRANGE = 256;            // k3_group: MSD buckets whose start lies in one 256-window
+#ifndef RL_V3_GRANGE
+#define RL_V3_GRANGE 256
+#endif
+constexpr int V3_GRANGE = RL_V3_GRANGE;            // k3_group: MSD buckets whose start lies in one 256-window
 constexpr int V3_GCAP = 768;              // k3_group: records staged in LDS (larger ranges run in place)
 constexpr int V3_GHASH = 1024;            // k3_group: LDS hash slots (power of two, > V3_GCAP)
 constexpr int V3_RULE_BITS = 15;          // MRec.rn = rule | now_mod << 15 (now_mod < 86400 < 2^17)

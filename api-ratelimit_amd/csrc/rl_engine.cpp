@@ -75,6 +75,21 @@ void launch_v3_group(hipStream_t, uint32_t, const MRec*, const uint32_t*, const 
                      const uint32_t*, const V3GroupScratch&, uint32_t*, int, EngineCtl*);
 void launch_v3_tail(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, const uint32_t*, uint32_t,
                     EngineCtl*, EngineCtl*);
+uint32_t v4_tiles(uint32_t n);
+uint32_t v4_group_blocks(uint32_t n);
+uint32_t v4_scan_blocks();
+size_t v4_scratch_bytes();
+void launch_v4_hist(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, const HotEntry*, uint32_t*,
+                    uint32_t*, uint16_t*, unsigned long long*, MRec*, rl_status*, EngineCtl*);
+void launch_v4_scan(hipStream_t, uint32_t, const uint16_t*, const unsigned long long*, unsigned long long*,
+                    const uint32_t*, const HotEntry*, HotBucket3*, const TableDesc&, int, HotCand*, uint32_t*,
+                    uint16_t*, void*, EngineCtl*);
+void launch_v4_place(hipStream_t, const rl_batch&, const MRec*, const uint16_t*, const uint16_t*, void*,
+                     const DevRule*, const unsigned long long*, HotBucket3*, int, MRec*, rl_status*, uint32_t*,
+                     Deferred*, int, EngineCtl*);
+void launch_v4_group(hipStream_t, const rl_batch&, MRec*, const DevRule*, const TableDesc&, int, rl_status*,
+                     uint32_t*, const HotBucket3*, const Deferred*, HotCand*, int, uint64_t, void*, uint32_t*,
+                     const uint32_t*, int, EngineCtl*, EngineCtl*);
 }  // namespace rlhip
 
 using namespace rlhip;
@@ -84,15 +99,16 @@ namespace {
 enum KernelId {
   KT_FINGERPRINT, KT_HISTOGRAM, KT_HIST_SCAN, KT_SORT_PASS, KT_SCAN, KT_LEADER, KT_DECIDE, KT_FALLBACK, KT_MEMSET,
   KT_FP2, KT_BSCAN, KT_BSCATTER, KT_BGROUP, KT_CAND, KT_V3_HIST, KT_V3_SCAN, KT_V3_PLACE, KT_V3_GROUP, KT_V3_TAIL,
-  KT_V3_BASES, KT_COUNT
+  KT_V3_BASES, KT_V4_HIST, KT_V4_SCAN, KT_V4_PLACE, KT_V4_GROUP, KT_COUNT
 };
 const char* const kKernelNames[KT_COUNT] = {"k_fingerprint", "k_histogram", "k_hist_scan", "k_sort_pass", "k_scan",
                                             "k_leader",      "k_decide",    "fallback",    "memset",      "k_fp2",
                                             "k_bscan",       "k_bscatter",  "k_bgroup",    "k_cand_state",
                                             "k3_hist",       "k3_scan",     "k3_place",    "k3_group",
-                                            "k3_tail",       "k3_bases"};
+                                            "k3_tail",       "k3_bases",    "k4_hist",     "k4_scan",
+                                            "k4_place",      "k4_group"};
 
-enum Mode { MODE_V2 = 0, MODE_LSD = 1, MODE_LSD_FULL = 2, MODE_V3 = 3 };
+enum Mode { MODE_V2 = 0, MODE_LSD = 1, MODE_LSD_FULL = 2, MODE_V3 = 3, MODE_V4 = 4 };
 
 // Hot-key set kept on the host between batches (v2 bucketing).
 struct HotKey {
@@ -172,6 +188,10 @@ struct rl_engine {
   V3GroupScratch v3_gs{};                   // k3_group scratch for ranges too large for LDS
   uint32_t* v3_heads = nullptr;             // per-workgroup unique-key counts (k3_group, then k3_scan)
   EngineCtl* v3_ctl[2] = {nullptr, nullptr};  // control blocks: batch k uses [k&1], k3_tail clears the other
+  // v4 pipeline (shares v3_tcount = bucket starts, v3_thsum, v3_hoff, v3_mrec = tile-sorted
+  // records, v3_dfr, v3_hb and v3_ctl)
+  void* v4_scratch = nullptr;               // k4_group global scratch for a bucket too large for LDS
+  uint32_t* v4_heads = nullptr;             // per-block unique-key counts (k4_group, then k4_scan)
   uint32_t v3_cur = 0;
   bool want_cand = true;                    // copy the hot-set candidates back after this batch
   uint8_t* zero_block = nullptr;  // ctl | hist | lookbacks (zeroed per batch)
@@ -256,7 +276,8 @@ struct rl_engine {
   int default_mode() const {
     if (cfg.flags & RL_CFG_LSD_ONLY) return MODE_LSD;
     if (cfg.flags & RL_CFG_V2) return MODE_V2;
-    return n_rules <= V3_MAX_RULES ? MODE_V3 : MODE_LSD;  // MRec packs the rule id in 15 bits
+    if (n_rules > V3_MAX_RULES) return MODE_LSD;  // MRec packs the rule id in 15 bits
+    return (cfg.flags & RL_CFG_V3) ? MODE_V3 : MODE_V4;
   }
   int finish();
   int upload_hot();
@@ -278,6 +299,51 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   const int routed = (b.reserved & RL_BATCH_ROUTED) ? 1 : 0;
   if (routed && mode == MODE_V2) mode = MODE_LSD;  // the v2 loader reads prefix bytes only
   hipError_t e;
+  if (mode == MODE_V4) {
+    if (n == 0) {
+      hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
+      hipMemsetAsync(v3_ctl[v3_cur], 0, sizeof(EngineCtl), stream);
+      e = hipMemcpyAsync(h_ctl, v3_ctl[v3_cur], sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
+      return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpyAsync(ctl)");
+    }
+    if (hot_dirty) {
+      int rc = upload_hot();
+      if (rc) return rc;
+    }
+    EngineCtl* c4 = v3_ctl[v3_cur];
+    EngineCtl* c4n = v3_ctl[v3_cur ^ 1u];
+    const int lc = cfg.local_cache ? 1 : 0;
+    const uint32_t ng = v4_group_blocks(n);
+    // v4 buffers: v3_arec = tile-sorted records, v3_tcount = bucket starts per tile,
+    // v3_toff (as u16) = per (tile, MSD bucket) records in earlier tiles, v3_mrec = MSD records
+    // in bucket order
+    MRec* srt = reinterpret_cast<MRec*>(v3_arec);
+    uint16_t* toff16 = reinterpret_cast<uint16_t*>(v3_toff);
+    timed(KT_V4_HIST, [&] {
+      launch_v4_hist(stream, b, d_rules, n_rules, cfg.hash_seed, d_hot, thr, fp_part, v3_tcount, v3_thsum, srt, out,
+                     c4);
+    });
+    timed(KT_V4_SCAN, [&] {
+      launch_v4_scan(stream, n, v3_tcount, v3_thsum, v3_hoff, fp_part, d_hot + HOT_SLOTS, v3_hb, tab, lc, d_cand,
+                     v4_heads + ng, toff16, v4_scratch, c4);
+    });
+    timed(KT_V4_PLACE, [&] {
+      launch_v4_place(stream, b, srt, v3_tcount, toff16, v4_scratch, d_rules, v3_hoff, v3_hb, lc, v3_mrec, out, thr,
+                      v3_dfr, routed, c4);
+    });
+    timed(KT_V4_GROUP, [&] {
+      launch_v4_group(stream, b, v3_mrec, d_rules, tab, lc, out, thr, v3_hb, v3_dfr, d_cand, want_cand ? 1 : 0,
+                      cfg.hash_seed, v4_scratch, v4_heads, v4_heads + ng, routed, c4, c4n);
+    });
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(e, "kernel launch");
+    e = hipMemcpyAsync(h_ctl, c4, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess && want_cand)
+      e = hipMemcpyAsync(h_cand, d_cand, sizeof(HotCand) * CAND_MAX, hipMemcpyDeviceToHost, stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(ctl)");
+    v3_cur ^= 1u;
+    return 0;
+  }
   if (mode == MODE_V3) {
     if (n == 0) {
       hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
@@ -740,6 +806,8 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     chk(hipMalloc(&g.tail, N * 4 + 64));
     chk(hipMalloc(&g.cursor, (v3_group_wgs((uint32_t)N) + 2) * 4));
     chk(hipMalloc(&e->v3_heads, (v3_group_wgs((uint32_t)N) + 1 + v3_scan_blocks()) * 4 + 64));
+    chk(hipMalloc(&e->v4_heads, (v4_group_blocks((uint32_t)N) + v4_scan_blocks()) * 4 + 64));
+    chk(hipMalloc(&e->v4_scratch, v4_scratch_bytes()));
     for (int k = 0; k < 2; ++k) {
       chk(hipMalloc(&e->v3_ctl[k], sizeof(EngineCtl)));
       if (he == hipSuccess) chk(hipMemset(e->v3_ctl[k], 0, sizeof(EngineCtl)));
@@ -814,6 +882,8 @@ void rl_destroy(rl_engine* e) {
                   (void*)e->v3_gs.grp, (void*)e->v3_gs.rank, (void*)e->v3_gs.tail, (void*)e->v3_gs.cursor})
     hipFree(p);
   hipFree(e->v3_heads);
+  hipFree(e->v4_heads);
+  hipFree(e->v4_scratch);
   hipFree(e->v3_ctl[0]);
   hipFree(e->v3_ctl[1]);
 

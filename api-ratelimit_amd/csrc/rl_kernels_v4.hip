@@ -1,0 +1,1219 @@
+// rl_kernels_v4.hip — the default decision pipeline: three launches per batch.
+//
+// Same contract and outputs as the LSD pipeline (rl_kernels.hip) and v3. Compared with v3
+// the records are written ONCE, already grouped: each tile writes its descriptors sorted by
+// bucket, and the group kernel gathers a bucket's runs straight from every tile (the row of
+// bucket starts of each tile says where), so there is no bucket-order scatter pass, no
+// bucket-base pass and no tail launch.
+//
+//   k4_hist    per 2048-descriptor tile: fingerprint (fixed_cache_impl.go:43-53 via
+//              cache_key.go:57-68), hot-set lookup, bucket; stable LDS sort of the tile by
+//              bucket and a segmented scan; the tile's records in bucket order (32-B MRec; a
+//              hot record carries its in-tile INCRBY prefix), the row of bucket starts, the
+//              hot buckets' h sums; nil-limit descriptors decided (base_limiter.go:72-75)
+//   k4_scan    per hot bucket: exclusive scan of the h sums over tiles, table claim and the
+//              counter before the batch; per MSD bucket: the batch total (size check), and
+//              per group of 64 MSD buckets the k4_group ranges (whole buckets packed up to the
+//              LDS stage) — all before any table write, so a refused batch leaves the table
+//              untouched
+//   k4_group   block j: (H) hot descriptors of half j&1 of tile j>>1, decided in place:
+//              post-value = base + tile prefix + in-tile prefix (local-cache freeze by request);
+//              (M) MSD range j: runs gathered from every tile into LDS (tile-major =
+//              arrival order inside a key), grouped by full fingerprint, segmented INCRBY
+//              prefix, one leader per key (table probe/claim, serial-order INCRBY, local-cache
+//              freeze), decisions. The last block to finish decides the deferred hot
+//              descriptors, counts U, fills hot-set candidates and clears the next control block.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rl_common.h"
+#include "rl_decide.h"
+#include "rl_device.h"
+#include "rl_v3_dev.h"
+
+namespace rlhip {
+namespace v4 {
+
+using v3::D3;
+using v3::NT;
+using v3::R;
+using v3::SegEl;
+using v3::T;
+using v3::W;
+using v3::BKT_NONE;
+
+constexpr int ROW = V3_ROW16;  // u16 bucket starts per tile (entries [0, NBUCKETS] used)
+static_assert(ROW >= NBUCKETS + 1, "row holds every bucket start and the end");
+constexpr int GBLOCKS = 1024;              // k4_group blocks (at least; 4 per CU, one round)
+constexpr int MSD_GROUPS = MSD_BUCKETS / 64;  // k4_scan blocks of MSD buckets (one range list each)
+constexpr int RANGE_MAX = 64;              // ranges per MSD group (one per bucket at most)
+// k4_scan -> k4_place / k4_group, one array of words: [0, MSD_GROUPS) ranges per group;
+// R_START: per group RANGE_MAX + 1 range starts (bucket inside the group, last = 64);
+// R_BPRE: per MSD bucket the exclusive prefix of bucket totals inside its group;
+// R_GTOT: per group its record total.
+constexpr int R_START = MSD_GROUPS;
+constexpr int R_BPRE = R_START + MSD_GROUPS * (RANGE_MAX + 1);
+constexpr int R_GTOT = R_BPRE + MSD_BUCKETS;
+constexpr int RANGE_WORDS = R_GTOT + MSD_GROUPS;
+constexpr int HOT_HALF = HOT_BUCKETS / 2;  // hot buckets per k4_group hot part
+constexpr int DONE_CTR = 27;               // EngineCtl::tile_ctr[DONE_CTR][0]: k4_group blocks done
+constexpr int G_NT = 256;
+constexpr int G_W = G_NT / 64;
+constexpr int G_CAP = 640;      // records grouped in LDS (a larger pair runs bucket by bucket)
+constexpr int G_HASH = 1024;    // LDS hash slots (power of two > G_CAP)
+constexpr int G_IPT = 3;        // positions per thread kept in registers (table read-ahead)
+constexpr int GS_HASH = 2048;   // global-scratch hash slots (> BUCKET_CAP)
+constexpr uint32_t G_EMPTY = 0xFFFFFFFFu;
+static_assert(G_CAP <= G_NT * G_IPT && G_HASH > G_CAP && GS_HASH > BUCKET_CAP, "k4_group geometry");
+static_assert(DONE_CTR != DFR_CTR && DONE_CTR != SCAN_CTR && DONE_CTR != CAND_CTR &&
+                  (DONE_CTR < INS_CTR0 || DONE_CTR >= INS_CTR0 + INS_LINES),
+              "control-block rows");
+
+RL_DEV uint32_t rule_of(uint32_t rn) { return rn & (V3_MAX_RULES - 1u); }
+
+#ifdef RL_STAMPS
+// Diagnostic build only (tools/stamps4.py): per-block phase timestamps (s_memrealtime, 100 MHz)
+// of wave 0 of k4_group blocks.
+__device__ uint64_t g_st4[4096][8];
+#define ST4(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_st4[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define ST4V(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_st4[blockIdx.x][k] = (v); } while (0)
+#else
+#define ST4(k) do { } while (0)
+#define ST4V(k, v) do { } while (0)
+#endif
+
+// Stores handed to the last k4_group block bypass the L2 of the storing XCD (sc1, written
+// through), and the last block reads them with sc1 loads: no agent-scope fences
+// (MI355X_MICROARCH.md, hand-off table row 1).
+RL_DEV void st_sc1_32B(void* p, const void* v) {
+  const uint64_t* s = reinterpret_cast<const uint64_t*>(v);
+  uint64_t* d = reinterpret_cast<uint64_t*>(p);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) st_relaxed64(d + k, s[k]);
+}
+RL_DEV void ld_sc1_32B(void* v, const void* p) {
+  const uint64_t* s = reinterpret_cast<const uint64_t*>(p);
+  uint64_t* d = reinterpret_cast<uint64_t*>(v);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) d[k] = ld_relaxed64(s + k);
+}
+RL_DEV void emit_cand_sc1(EngineCtl* ctl, HotCand* __restrict__ cand, uint32_t rule, uint32_t count,
+                          uint32_t first_idx, uint64_t a = 0, uint64_t b = 0, uint32_t unit = 0) {
+  const uint32_t c = atomicAdd(&ctl->tile_ctr[CAND_CTR][0], 1u);
+  if (c < (uint32_t)CAND_MAX) {
+    HotCand hc;
+    hc.a = a;
+    hc.b = b;
+    hc.unit = unit;
+    hc.rule = rule;
+    hc.count = count;
+    hc.first_idx = first_idx;
+    st_sc1_32B(&cand[c], &hc);
+  }
+}
+static_assert(sizeof(HotCand) == 32 && sizeof(Deferred) == 32, "32-B hand-off records");
+constexpr int SHARD_CTR0 = 0;  // EngineCtl::tile_ctr[0..7][0]: k4_group blocks done, by blockIdx & 7
+
+// ---------------------------------------------------------------------------
+// k4_hist
+// ---------------------------------------------------------------------------
+template <bool ROUTED>
+__global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
+                                              uint64_t seed, const HotEntry* __restrict__ hot,
+                                              uint32_t* __restrict__ req_thr, uint32_t* __restrict__ fpart,
+                                              uint16_t* __restrict__ tstart, unsigned long long* __restrict__ thsum,
+                                              MRec* __restrict__ srec, rl_status* __restrict__ out, EngineCtl* ctl) {
+  __shared__ HotEntry sh_hot[HOT_SLOTS];
+  __shared__ uint16_t sh_cnt[ROW];
+  __shared__ unsigned long long sh_hs[HOT_BUCKETS];
+  __shared__ uint16_t s_d[T];
+  __shared__ uint16_t s_pa[T], s_pb[T];
+  __shared__ uint32_t s_h[T];
+  __shared__ unsigned long long s_res[T];
+  __shared__ uint32_t s_cnt[W][64];
+  __shared__ uint32_t sh_w[W];
+  __shared__ SegEl s_agg[W];
+  __shared__ uint32_t sh_f[FP_PART_WORDS];
+  __shared__ uint32_t sh_err;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t tile = blockIdx.x, ntiles = gridDim.x;
+  const uint32_t t0 = tile * T;
+  v3::load_hot_table(hot, sh_hot);
+  for (int b = tid; b < ROW / 2; b += NT) reinterpret_cast<uint32_t*>(sh_cnt)[b] = 0;
+  for (int b = tid; b < HOT_BUCKETS; b += NT) sh_hs[b] = 0;
+  if (tid < FP_PART_WORDS) sh_f[tid] = 0;
+  if (tid == 0) sh_err = 0;
+  // DoLimitResponse.ThrottleMillis starts at 0 for every request (base_limiter.go:163-165)
+  {
+    const uint32_t per = (in.n_req + ntiles - 1) / ntiles;
+    const uint32_t r0 = tile * per, r1 = min(in.n_req, r0 + per);
+    for (uint32_t q = r0 + tid; q < r1; q += NT) req_thr[q] = 0;
+  }
+  __syncthreads();
+  D3 d[R];
+  uint32_t err = 0;
+  if (ROUTED)
+    v3::load_routed(in, rules, n_rules, sh_hot, t0, d, err);
+  else
+    v3::load_descs(in, rules, n_rules, seed, sh_hot, t0, d, err);
+  uint32_t gmin[8], gmax[8], nil = 0;
+#pragma unroll
+  for (int rg = 0; rg < 8; ++rg) { gmin[rg] = 0xFFFFFFFFu; gmax[rg] = 0; }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t o = r * NT + tid;
+    const uint32_t b = d[r].bucket;
+    s_d[o] = (uint16_t)b;
+    s_h[o] = d[r].h;
+    s_pa[o] = (uint16_t)o;
+    if (b < NIL_BUCKET) {
+      const uint32_t region = key_region(d[r].key);
+#pragma unroll
+      for (int rg = 0; rg < 8; ++rg)  // static register indexing
+        if ((uint32_t)rg == region) {
+          gmin[rg] = d[r].gen < gmin[rg] ? d[r].gen : gmin[rg];
+          gmax[rg] = d[r].gen > gmax[rg] ? d[r].gen : gmax[rg];
+        }
+    } else if (b == NIL_BUCKET) {
+      ++nil;
+    }
+  }
+#pragma unroll
+  for (int rg = 0; rg < 8; ++rg) {
+    const uint32_t mx = wave_max_u32(gmax[rg]);
+    if (mx) {  // wave-uniform
+      const uint32_t mn = wave_min_u32(gmin[rg]);
+      if (lane == 0) {
+        atomicMax(&sh_f[rg], ~mn);
+        atomicMax(&sh_f[8 + rg], mx);
+      }
+    }
+  }
+  nil = v3::wave_sum(nil);
+  if (lane == 0 && nil) atomicAdd(&sh_f[16], nil);
+  if (err) atomicOr(&sh_err, err);
+  // Stable sort of the tile by bucket, then a segmented scan in sorted order:
+  // hot -> inclusive prefix of h inside (tile, bucket); each bucket's last descriptor ->
+  // the bucket's count (and h sum) in this tile.
+  v3::tile_digit_pass(s_d, s_pa, s_pb, 0, s_cnt, sh_w);  // includes barriers
+  v3::tile_digit_pass(s_d, s_pb, s_pa, 6, s_cnt, sh_w);
+  {
+    const uint32_t s0 = tid * R;
+    uint32_t od[R], dd[R], fl[R];
+    unsigned long long hv[R];
+    uint32_t prev_d = s0 == 0 ? 0xFFFFFFFFu : s_d[s_pa[s0 - 1]];
+    const uint32_t next_d = s0 + R < (uint32_t)T ? s_d[s_pa[s0 + R]] : 0xFFFFFFFFu;
+    SegEl t{0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const uint32_t o = s_pa[s0 + q];
+      const uint32_t dv = s_d[o];
+      od[q] = o;
+      dd[q] = dv;
+      fl[q] = dv != prev_d;
+      hv[q] = s_h[o];
+      prev_d = dv;
+      t = v3::seg_op(t, SegEl{fl[q], s0 + q, hv[q]});
+    }
+    SegEl incl = t;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      SegEl y;
+      y.f = __shfl_up(incl.f, s, 64);
+      y.hp = __shfl_up(incl.hp, s, 64);
+      y.s = __shfl_up(incl.s, s, 64);
+      if (lane >= (uint32_t)s) incl = v3::seg_op(y, incl);
+    }
+    if (lane == 63) s_agg[wave] = incl;
+    SegEl wex;
+    wex.f = __shfl_up(incl.f, 1, 64);
+    wex.hp = __shfl_up(incl.hp, 1, 64);
+    wex.s = __shfl_up(incl.s, 1, 64);
+    if (lane == 0) wex = SegEl{0, 0, 0};
+    __syncthreads();
+    SegEl run{0, 0, 0};
+#pragma unroll
+    for (int w = 0; w < W - 1; ++w) {
+      const SegEl a = s_agg[w];  // wave-uniform LDS read
+      if ((uint32_t)w < wave) run = v3::seg_op(run, a);
+    }
+    run = v3::seg_op(run, wex);
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      run = v3::seg_op(run, SegEl{fl[q], s0 + q, hv[q]});
+      const uint32_t b = dd[q];
+      if (b < (uint32_t)HOT_BUCKETS) s_res[od[q]] = run.s;
+      s_pb[od[q]] = (uint16_t)(s0 + q);  // sorted position of descriptor od[q]
+      const uint32_t nd = q + 1 < R ? dd[q + 1] : next_d;
+      if (b < NIL_BUCKET && nd != b) {  // the bucket's last descriptor of the tile
+        sh_cnt[b] = (uint16_t)(s0 + q + 1u - run.hp);
+        if (b < (uint32_t)HOT_BUCKETS) sh_hs[b] = run.s;
+      }
+    }
+  }
+  __syncthreads();
+  // Bucket starts of the tile: exclusive scan of the counts (entries [0, ROW), 6 per thread).
+  {
+    constexpr int PER = (ROW + NT - 1) / NT;
+    uint32_t v[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t e = tid * PER + k;
+      v[k] = e < (uint32_t)ROW ? sh_cnt[e] : 0u;
+      sum += v[k];
+    }
+    uint32_t total;
+    uint32_t run = v3::block_excl_scan<NT>(sum, sh_w, total);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t e = tid * PER + k;
+      if (e < (uint32_t)ROW) sh_cnt[e] = (uint16_t)run;
+      run += v[k];
+    }
+  }
+  // Records in bucket order. A hot record carries its in-tile INCRBY prefix and its bucket;
+  // an MSD record its sort key and fp_lo; a nil-limit descriptor is decided here.
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t o = r * NT + tid;
+    const uint32_t i = t0 + o;
+    const D3& x = d[r];
+    if (x.bucket == BKT_NONE) continue;
+    if (x.bucket == NIL_BUCKET) {
+      // GetResponseDescriptorStatus("" key) -> {OK, nil limit, 0}  base_limiter.go:72-75
+      rl_status st;
+      st.code_flags = RL_CODE_OK;
+      st.limit_remaining = 0;
+      st.reset_s = 0;
+      st.over_limit_delta = 0;
+      st.near_limit_delta = 0;
+      out[i] = st;
+      continue;
+    }
+    const bool hotb = x.bucket < (uint32_t)HOT_BUCKETS;
+    MRec m;
+    m.key = hotb ? (uint64_t)s_res[o] : x.key;
+    m.fp_lo = hotb ? (uint64_t)x.bucket : x.lo;
+    m.idx = i;
+    m.req = x.req;
+    m.h = x.h;
+    m.rn = rule_of(x.rule) | (x.now_mod << V3_RULE_BITS);
+    srec[t0 + s_pb[o]] = m;
+  }
+  __syncthreads();
+  uint32_t* trow = reinterpret_cast<uint32_t*>(tstart + (size_t)tile * ROW);
+  for (int b = tid; b < ROW / 2; b += NT) trow[b] = reinterpret_cast<const uint32_t*>(sh_cnt)[b];
+  unsigned long long* hrow = thsum + (size_t)tile * HOT_BUCKETS;
+  for (int b = tid; b < HOT_BUCKETS; b += NT) hrow[b] = sh_hs[b];
+  if (tid < FP_PART_WORDS) fpart[(size_t)tile * FP_PART_WORDS + tid] = sh_f[tid];
+  if (tid == 0 && sh_err) atomicOr(&ctl->err, sh_err);
+}
+
+// ---------------------------------------------------------------------------
+// k4_scan — 64 buckets per block (one per lane); the 16 waves split the tiles.
+// ---------------------------------------------------------------------------
+constexpr int SCAN_NT = 1024;
+constexpr int SCAN_W = SCAN_NT / 64;
+constexpr int SCAN_U = 16;  // column loads in flight per lane
+static_assert(HOT_BUCKETS % 64 == 0 && V3_SCAN_BUCKETS % 64 == 0, "bucket blocks");
+
+__global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ tstart,
+                                                   const unsigned long long* __restrict__ thsum, uint32_t ntiles,
+                                                   unsigned long long* __restrict__ hoff,
+                                                   const uint32_t* __restrict__ fpart,
+                                                   const HotEntry* __restrict__ hot_list, HotBucket3* __restrict__ hb,
+                                                   TableDesc tab, int local_cache, HotCand* __restrict__ cand,
+                                                   uint32_t* __restrict__ heads_out, uint16_t* __restrict__ toff,
+                                                   uint32_t* __restrict__ ranges, EngineCtl* ctl) {
+  __shared__ uint32_t s_f[FP_PART_WORDS];
+  __shared__ uint32_t s_tot[64];
+  __shared__ uint32_t s_pc[SCAN_W][64];
+  __shared__ unsigned long long s_ph[SCAN_W][64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < FP_PART_WORDS) s_f[tid] = 0;
+  __syncthreads();
+  // Fold the per-tile partials (every block): generation range per region, nil count.
+  {
+    uint32_t v[FP_PART_WORDS];
+#pragma unroll
+    for (int w = 0; w < FP_PART_WORDS; ++w) v[w] = 0;
+    for (uint32_t g = tid; g < ntiles; g += SCAN_NT) {
+#pragma unroll
+      for (int w = 0; w < FP_PART_WORDS; ++w) {
+        const uint32_t x = fpart[(size_t)g * FP_PART_WORDS + w];
+        v[w] = w < 16 ? (x > v[w] ? x : v[w]) : v[w] + x;
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < FP_PART_WORDS; ++w) {
+      const uint32_t x = w < 16 ? wave_max_u32(v[w]) : v3::wave_sum(v[w]);
+      if (lane == 0 && x) {
+        if (w < 16) atomicMax(&s_f[w], x);
+        else atomicAdd(&s_f[w], x);
+      }
+    }
+  }
+  __syncthreads();
+  // Two window generations of one region in one batch must be adjacent;
+  // a region's generations share its parity, so a valid batch has ONE generation per region.
+  bool span = false;
+#pragma unroll
+  for (int rg = 0; rg < 8; ++rg) {
+    const uint32_t mx = s_f[8 + rg], mn = ~s_f[rg];
+    span |= mx != 0 && mx - mn > 1u;
+  }
+  if (blockIdx.x == 0) {
+    if (tid < 8) ctl->gen_min[tid] = ~s_f[tid];
+    else if (tid < 16) ctl->gen_max[tid - 8] = s_f[tid];
+    else if (tid == 16) ctl->n_nil = s_f[16];
+    if (tid == 0 && span) atomicOr(&ctl->err, ERR_WINDOW_SPAN);
+  }
+  // Column pass: bucket b = lane of this block, tiles [wave*Q, wave*Q + Q).
+  const uint32_t b = blockIdx.x * 64 + lane;
+  const bool hotb = blockIdx.x * 64 < (uint32_t)HOT_BUCKETS;  // block-uniform
+  const uint32_t Q = (ntiles + SCAN_W - 1) / SCAN_W;
+  const uint32_t tb = min(ntiles, wave * Q), te = min(ntiles, tb + Q);
+  uint32_t c = 0;
+  unsigned long long hs = 0;
+  for (uint32_t t = tb; t < te; t += SCAN_U) {
+    uint32_t cv[SCAN_U];
+    unsigned long long hv[SCAN_U];
+#pragma unroll
+    for (int u = 0; u < SCAN_U; ++u) {
+      const uint16_t* row = tstart + (size_t)(t + u) * ROW + b;
+      cv[u] = t + u < te ? (uint32_t)row[1] - (uint32_t)row[0] : 0u;
+      hv[u] = (hotb && t + u < te) ? thsum[(size_t)(t + u) * HOT_BUCKETS + b] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < SCAN_U; ++u) {
+      c += cv[u];
+      hs += hv[u];
+    }
+  }
+  s_pc[wave][lane] = c;
+  if (hotb) s_ph[wave][lane] = hs;
+  __syncthreads();
+  uint32_t ctot = 0, crun = 0;
+  unsigned long long hrun = 0, htot = 0;
+#pragma unroll
+  for (int w = 0; w < SCAN_W; ++w) {
+    const uint32_t x = s_pc[w][lane];
+    ctot += x;
+    crun += (uint32_t)w < wave ? x : 0u;
+    if (hotb) {
+      const unsigned long long y = s_ph[w][lane];
+      hrun += (uint32_t)w < wave ? y : 0ull;
+      htot += y;
+    }
+  }
+  if (!hotb) {
+    // per (tile, MSD bucket): the records of the bucket in earlier tiles (u16: a bucket holds
+    // at most BUCKET_CAP records on this path; a larger one sends the batch to the LSD pipeline
+    // before anything touches the table)
+    const uint32_t mb = b - HOT_BUCKETS;
+    for (uint32_t t = tb; t < te; t += SCAN_U) {
+      uint32_t cv[SCAN_U];
+#pragma unroll
+      for (int u = 0; u < SCAN_U; ++u) {
+        const uint16_t* row = tstart + (size_t)(t + u) * ROW + b;
+        cv[u] = t + u < te ? (uint32_t)row[1] - (uint32_t)row[0] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < SCAN_U; ++u) {
+        if (t + u < te) toff[(size_t)(t + u) * MSD_BUCKETS + mb] = (uint16_t)crun;
+        crun += cv[u];
+      }
+    }
+    if (wave != 0) return;
+    if (ctot > (uint32_t)BUCKET_CAP) atomicOr(&ctl->err, ERR_V2_FALLBACK);
+    const uint32_t g = blockIdx.x - HOT_BUCKETS / 64;
+    const uint32_t incl = v3::wave_incl_scan<uint32_t>(ctot);
+    ranges[R_BPRE + mb] = incl - ctot;
+    if (lane == 63) ranges[R_GTOT + g] = incl;
+    // Pack the group's 64 buckets greedily into k4_group ranges of whole buckets holding at
+    // most G_CAP records (a single larger bucket is a range of its own).
+    s_tot[lane] = ctot;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (lane == 0) {
+      heads_out[blockIdx.x] = 0;
+      uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
+      uint32_t nr = 0, cur = 0;
+      rb[0] = 0;
+      for (int k = 0; k < 64; ++k) {
+        const uint32_t c = s_tot[k];
+        if (cur && cur + c > (uint32_t)G_CAP) {
+          rb[++nr] = k;
+          cur = 0;
+        }
+        cur += c;
+      }
+      rb[++nr] = 64;
+      ranges[g] = nr;
+    }
+    return;
+  }
+  for (uint32_t t = tb; t < te; t += SCAN_U) {
+    unsigned long long hv[SCAN_U];
+#pragma unroll
+    for (int u = 0; u < SCAN_U; ++u) hv[u] = t + u < te ? thsum[(size_t)(t + u) * HOT_BUCKETS + b] : 0ull;
+#pragma unroll
+    for (int u = 0; u < SCAN_U; ++u) {
+      if (t + u < te) hoff[(size_t)(t + u) * HOT_BUCKETS + b] = hrun;
+      hrun += hv[u];
+    }
+  }
+  if (wave == 0) {
+    // Hot key leader: find or claim the key's slot and read the counter before this batch. A
+    // claimed slot starts at count 0, which is invisible if the batch is later rejected.
+    HotBucket3 x;
+    x.key = x.fp_lo = x.base = x.slot = x.total = 0;
+    x.rule = 0;
+    x.flags = 0;
+    x.rstar = 0xFFFFFFFFu;
+    x.pad[0] = x.pad[1] = x.pad[2] = 0;
+    const uint32_t errs = ctl->err;  // flags of k4_hist
+    uint32_t heads = 0;
+    if (ctot && !span && !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME | ERR_V2_FALLBACK))) {
+      const HotEntry he = hot_list[b >> 1];
+      const uint32_t region = (he.unit - 1u) * 2u + (b & 1u);
+      const uint32_t gen = s_f[8 + region];  // the region's one generation in this batch
+      const uint64_t ws = (uint64_t)(gen - 1u) * unit_div(he.unit);
+      uint64_t hi, lo;
+      fp_final(FpState{he.a, he.b}, ws, hi, lo);
+      x.key = make_sort_key(region, hi);
+      x.fp_lo = lo;
+      x.rule = he.rule;
+      x.total = htot;
+      Slot* slot = nullptr;
+      bool existed = false;
+      if (!table_claim(tab, x.key, lo, gen, slot, existed)) {
+        atomicOr(&ctl->err, ERR_TABLE_FULL);
+      } else {
+        if (existed) {
+          x.base = slot->count;
+          x.flags = (slot->flags & SLOT_FROZEN) ? HB_FROZEN_PRE : 0u;
+        } else {
+          slot->key = x.key;
+          slot->fp_lo_hi = (uint32_t)(lo >> 32);
+          slot->count = 0;
+          slot->flags = 0;
+        }
+        x.slot = (uint64_t)(uintptr_t)slot;
+        // The local-cache freeze point is found from a monotone INCRBY sequence; a batch whose
+        // counter would pass 2^32 goes to the LSD pipeline (uint32 wraparound, R10).
+        if (local_cache && !(x.flags & HB_FROZEN_PRE) && x.base + htot >= (1ull << 32))
+          atomicOr(&ctl->err, ERR_V2_FALLBACK);
+        heads = 1;
+      }
+      if (slot != nullptr && !existed) heads |= 1u << 16;  // a new table slot
+      if (ctot >= HOT_CAND_MIN) emit_candidate(ctl, cand, he.rule, ctot, 0xFFFFFFFFu, he.a, he.b, he.unit);
+    }
+    hb[b] = x;
+    heads = v3::wave_sum(heads);
+    if (lane == 0) heads_out[blockIdx.x] = heads;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k4_group
+// ---------------------------------------------------------------------------
+// Storage of one grouped range: LDS arrays (G_CAP records) or a block's global scratch.
+struct GS {
+  MRec* rec;       // staged records by position; a leader overwrites its own key with the
+                   // counter before the batch and its fp_lo with the freeze
+  uint64_t* P;     // INCRBY prefix by position
+  uint16_t* list;  // positions grouped by key, each key's in position (= arrival) order
+  uint16_t* grp;   // position -> hash slot
+  uint32_t* slot;  // hash slot -> first position inserted with the key (G_EMPTY = free)
+  uint32_t* cnt;   // hash slot -> records of the key
+  uint16_t* end;   // hash slot -> end of the key's list (start = end - cnt)
+  uint32_t* cursor;
+  uint32_t hs;     // hash slots (power of two)
+};
+
+// Barrier between phases. The LDS path exchanges data through LDS only, so it waits for
+// LDS traffic alone and leaves the table read-ahead loads in flight across the barrier.
+template <bool LDS>
+RL_DEV void gbar() {
+  if constexpr (LDS) {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  } else {
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
+RL_DEV void g_insert(const GS& g, uint32_t k) {
+  const uint64_t key = g.rec[k].key, lo = g.rec[k].fp_lo;
+  const uint32_t hmask = g.hs - 1u;
+  uint32_t s = (uint32_t)key & hmask;
+  for (;;) {
+    const uint32_t v = atomicCAS(&g.slot[s], G_EMPTY, k);
+    if (v == G_EMPTY || (g.rec[v].key == key && g.rec[v].fp_lo == lo)) break;
+    s = (s + 1) & hmask;
+  }
+  g.grp[k] = (uint16_t)s;
+  atomicAdd(&g.cnt[s], 1u);
+}
+
+// One wave: each key's list in position order (positions [0, m), 64 at a time).
+RL_DEV void g_layout(const GS& g, uint32_t m) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t lt = lanemask_lt();
+  for (uint32_t c = 0; c < m; c += 64) {
+    const uint32_t k = c + lane;
+    const bool valid = k < m;
+    const uint32_t s = valid ? g.grp[k] : 0u;
+    uint64_t mm = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      if ((g.hs >> b) <= 1u) break;  // wave-uniform
+      const bool bit = (s >> b) & 1u;
+      const uint64_t bal = __ballot(bit);
+      mm &= bit ? bal : ~bal;
+    }
+    uint32_t before = 0;
+    if (valid) before = g.end[s];
+    __builtin_amdgcn_wave_barrier();
+    if (valid) {
+      if (lane == (uint32_t)__ffsll((unsigned long long)mm) - 1u) g.end[s] = (uint16_t)(before + (uint32_t)__popcll(mm));
+      g.list[before + (uint32_t)__popcll(mm & lt)] = (uint16_t)k;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+struct LSeg {
+  uint32_t f;
+  unsigned long long s;
+};
+RL_DEV LSeg lseg_op(const LSeg& a, const LSeg& b) { return b.f ? b : LSeg{a.f, a.s + b.s}; }
+
+// Segmented inclusive scan of h over the lists (list positions [0, m) in chunks of
+// G_NT * G_IPT, blocked G_IPT per thread): g.P[position] = INCRBY prefix of its key.
+template <bool LDS>
+RL_DEV void g_scan(const GS& g, uint32_t m, LSeg* s_agg, LSeg* s_carry) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) *s_carry = LSeg{0, 0};
+  gbar<LDS>();
+  for (uint32_t c0 = 0; c0 < m; c0 += G_NT * G_IPT) {
+    uint32_t pos[G_IPT], hd[G_IPT];
+    unsigned long long hv[G_IPT];
+    LSeg t{0, 0};
+#pragma unroll
+    for (int q = 0; q < G_IPT; ++q) {
+      const uint32_t e = c0 + tid * G_IPT + q;
+      pos[q] = 0xFFFFFFFFu;
+      hd[q] = 0;
+      hv[q] = 0;
+      if (e < m) {
+        const uint32_t k = g.list[e];
+        const uint32_t s = g.grp[k];
+        pos[q] = k;
+        hd[q] = e == (uint32_t)g.end[s] - g.cnt[s];
+        hv[q] = g.rec[k].h;
+        t = lseg_op(t, LSeg{hd[q], hv[q]});
+      }
+    }
+    LSeg incl = t;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      LSeg y;
+      y.f = __shfl_up(incl.f, d, 64);
+      y.s = __shfl_up(incl.s, d, 64);
+      if (lane >= (uint32_t)d) incl = lseg_op(y, incl);
+    }
+    if (lane == 63) s_agg[wave] = incl;
+    LSeg wex;
+    wex.f = __shfl_up(incl.f, 1, 64);
+    wex.s = __shfl_up(incl.s, 1, 64);
+    if (lane == 0) wex = LSeg{0, 0};
+    gbar<LDS>();
+    LSeg run = *s_carry;
+    for (uint32_t w = 0; w < wave; ++w) run = lseg_op(run, s_agg[w]);
+    run = lseg_op(run, wex);
+#pragma unroll
+    for (int q = 0; q < G_IPT; ++q) {
+      if (pos[q] == 0xFFFFFFFFu) continue;
+      run = lseg_op(run, LSeg{hd[q], hv[q]});
+      g.P[pos[q]] = run.s;
+    }
+    gbar<LDS>();
+    if (tid == G_NT - 1) {  // carry = the whole chunk, folded onto the previous carry
+      LSeg all = *s_carry;
+      for (int w = 0; w < G_W; ++w) all = lseg_op(all, s_agg[w]);
+      *s_carry = all;
+    }
+    gbar<LDS>();
+  }
+}
+
+RL_DEV uint32_t g_tail(const GS& g, uint32_t k) { return g.list[g.end[g.grp[k]] - 1u]; }
+
+// Run by the key's last record: table probe/claim, INCRBY of the key's whole sequence in
+// serial order, local-cache freeze (fixed_cache_impl.go:55-123, base_limiter.go:88-106).
+// Leaves the counter before the batch in rec[k].key and the freeze in rec[k].fp_lo.
+RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, const TableDesc& tab, int local_cache,
+                   HotCand* cand, EngineCtl* ctl, bool has_pre, const SlotView& pre, int cand_on, uint32_t& heads) {
+  const uint64_t key = g.rec[k].key, lo = g.rec[k].fp_lo;
+  const uint32_t rule = rule_of(g.rec[k].rn);
+  const uint32_t s = g.grp[k];
+  const uint32_t n = g.cnt[s], e1 = g.end[s], e0 = e1 - n;
+  const uint64_t Pk = g.P[k];
+  bool mixed = false;
+  heads += 1;
+  if ((cand_on && n >= HOT_MIN_SEG) || local_cache) {
+    for (uint32_t e = e0; e < e1; ++e) mixed |= rule_of(g.rec[g.list[e]].rn) != rule;
+    if (cand_on && n >= HOT_MIN_SEG && !mixed) emit_cand_sc1(ctl, cand, rule, n, g.rec[g.list[e0]].idx);
+  }
+  const uint32_t gen = ctl->gen_max[key_region(key)];  // the region's one generation (k4_scan)
+  Slot* slot = nullptr;
+  bool existed = false;
+  uint64_t base = 0;
+  uint32_t sflags = 0;
+  const bool claimed = has_pre ? table_claim_pre(tab, key, lo, gen, pre, slot, existed, base, sflags)
+                               : table_claim(tab, key, lo, gen, slot, existed);
+  if (!claimed) {
+    atomicOr(&ctl->err, ERR_TABLE_FULL);
+    g.rec[k].key = 0;
+    g.rec[k].fp_lo = SEG_NO_FREEZE;
+    return;
+  }
+  if (existed && !has_pre) {
+    base = slot->count;
+    sflags = slot->flags;
+  }
+  const bool frozen_pre = existed && (sflags & SLOT_FROZEN) != 0;
+  if (!existed) {
+    slot->key = key;
+    slot->fp_lo_hi = (uint32_t)(lo >> 32);
+    heads += 1u << 16;
+  }
+  uint32_t freeze = SEG_NO_FREEZE;
+  uint64_t final_count = base + Pk;
+  if (frozen_pre) {
+    freeze = SEG_FROZEN_BEFORE;  // every descriptor is a local-cache hit: no INCRBY
+    final_count = base;
+  } else if (local_cache) {
+    // the first record (arrival order) whose INCRBY reply exceeds its limit freezes the key;
+    // the INCRBYs of its own request still happen (all lookups precede the Sets)
+    const bool exact = !mixed && base + Pk < (1ull << 32);
+    for (uint32_t e = e0; e < e1; ++e) {
+      const uint32_t j = g.list[e];
+      const uint64_t after = base + g.P[j];
+      const uint32_t L = rules[rule_of(g.rec[j].rn)].L;
+      if (exact ? after > (uint64_t)L : (uint32_t)after > L) {
+        const uint32_t rstar = g.rec[j].req;
+        uint64_t last = g.P[j];
+        for (uint32_t f = e + 1; f < e1 && g.rec[g.list[f]].req == rstar; ++f) last = g.P[g.list[f]];
+        freeze = rstar;
+        final_count = base + last;
+        break;
+      }
+    }
+  }
+  slot->count = final_count;
+  if (freeze != SEG_NO_FREEZE && freeze != SEG_FROZEN_BEFORE) slot->flags = SLOT_FROZEN;
+  else if (!existed) slot->flags = 0;
+  g.rec[k].key = base;
+  g.rec[k].fp_lo = freeze;
+}
+
+// All phases of one staged range of m records (whole keys). Returns the keys led (low 16
+// bits) and the new table slots claimed (high 16 bits) by this thread.
+template <bool LDS>
+RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__ rules, const TableDesc& tab,
+                            int local_cache, rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
+                            HotCand* cand, int cand_on, int routed, LSeg* s_agg, LSeg* s_carry, uint32_t* sh_w,
+                            EngineCtl* ctl) {
+  const uint32_t tid = threadIdx.x, wave = tid >> 6;
+  uint32_t heads = 0;
+  // The staging (and the hash-table reset before it) is complete: read each position's first
+  // table slot ahead, so the leaders' probes overlap the grouping.
+  SlotView pre[G_IPT];
+  if constexpr (LDS) {
+#pragma unroll
+    for (int j = 0; j < G_IPT; ++j) {
+      const uint32_t k = tid + j * G_NT;
+      if (k < m) pre[j] = load_slot(slot_first(tab, g.rec[k].key));
+    }
+  }
+  for (uint32_t k = tid; k < m; k += G_NT) g_insert(g, k);
+  gbar<LDS>();
+  ST4(1);
+  // each key's list start: exclusive prefix of the per-slot counts (hash-slot order)
+  {
+    const uint32_t spt = g.hs / G_NT, s0 = tid * spt;
+    uint32_t sum = 0;
+    for (uint32_t q = 0; q < spt; ++q) sum += g.cnt[s0 + q];
+    uint32_t tot;
+    uint32_t run = v3::block_excl_scan<G_NT>(sum, sh_w, tot);
+    for (uint32_t q = 0; q < spt; ++q) {
+      g.end[s0 + q] = (uint16_t)run;
+      run += g.cnt[s0 + q];
+    }
+  }
+  gbar<LDS>();
+  ST4(6);
+  if (wave == 0) g_layout(g, m);
+  gbar<LDS>();
+  ST4(7);
+  g_scan<LDS>(g, m, s_agg, s_carry);
+  gbar<LDS>();
+  ST4(3);
+  if constexpr (LDS) {
+#pragma unroll
+    for (int j = 0; j < G_IPT; ++j) {
+      const uint32_t k = tid + j * G_NT;
+      if (k < m && g_tail(g, k) == k)
+        g_lead(g, k, rules, tab, local_cache, cand, ctl, true, pre[j], cand_on, heads);
+    }
+  } else {
+    for (uint32_t k = tid; k < m; k += G_NT)
+      if (g_tail(g, k) == k) g_lead(g, k, rules, tab, local_cache, cand, ctl, false, SlotView{}, cand_on, heads);
+  }
+  __threadfence_block();
+  __syncthreads();
+  ST4(4);
+  for (uint32_t k = tid; k < m; k += G_NT) {
+    const MRec x = g.rec[k];
+    const uint32_t t = g_tail(g, k);
+    const MRec& lt = g.rec[t];
+    v3::decide_at(x.idx, x.req, rule_of(x.rn), x.h, x.rn >> V3_RULE_BITS, lt.key, g.P[k], (uint32_t)lt.fp_lo, rules,
+                  out, req_thr, routed);
+  }
+  return heads;
+}
+
+// ---------------------------------------------------------------------------
+// k4_place — per tile (tile-sorted records): hot descriptors decided in place (v3's k3_place
+// hot branch), MSD records scattered to their bucket position (bucket base + records of the
+// bucket in earlier tiles + rank inside the tile's run).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restrict__ srec,
+                                               const uint16_t* __restrict__ tstart,
+                                               const uint16_t* __restrict__ toff,
+                                               const uint32_t* __restrict__ ranges,
+                                               const DevRule* __restrict__ rules,
+                                               const unsigned long long* __restrict__ hoff,
+                                               HotBucket3* __restrict__ hb, int local_cache,
+                                               MRec* __restrict__ mrec, rl_status* __restrict__ out,
+                                               uint32_t* __restrict__ req_thr, Deferred* __restrict__ dfr, int routed,
+                                               EngineCtl* ctl) {
+  __shared__ uint16_t s_row[ROW];
+  __shared__ uint16_t s_toff[MSD_BUCKETS];
+  __shared__ uint32_t s_gpre[MSD_GROUPS];
+  __shared__ uint32_t s_rstar[HOT_BUCKETS];
+  __shared__ uint32_t s_err;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t t = blockIdx.x, t0 = t * T;
+  if (tid == 0) s_err = ctl->err;
+  {
+    const uint32_t* rsrc = reinterpret_cast<const uint32_t*>(tstart + (size_t)t * ROW);
+    for (int k = tid; k < ROW / 2; k += NT) reinterpret_cast<uint32_t*>(s_row)[k] = rsrc[k];
+    const uint32_t* osrc = reinterpret_cast<const uint32_t*>(toff + (size_t)t * MSD_BUCKETS);
+    for (int k = tid; k < MSD_BUCKETS / 2; k += NT) reinterpret_cast<uint32_t*>(s_toff)[k] = osrc[k];
+  }
+  if (tid < 64) {  // group bases: exclusive prefix of the group totals (one wave)
+    const uint32_t v = tid < (uint32_t)MSD_GROUPS ? ranges[R_GTOT + tid] : 0u;
+    const uint32_t incl = v3::wave_incl_scan<uint32_t>(v);
+    if (tid < (uint32_t)MSD_GROUPS) s_gpre[tid] = incl - v;
+  }
+  if (local_cache)
+    for (int b = tid; b < HOT_BUCKETS; b += NT) s_rstar[b] = 0xFFFFFFFFu;
+  __syncthreads();
+  // Nothing is decided and nothing touches the table unless the whole batch is valid.
+  if (s_err) return;
+  // Hot keys without a freeze in this batch: the final counter is base + total (block 0).
+  if (t == 0) {
+    for (int b = tid; b < HOT_BUCKETS; b += NT) {
+      const HotBucket3 x = hb[b];
+      if (!x.slot || (x.flags & HB_FROZEN_PRE)) continue;
+      if (!local_cache || x.base + x.total <= (uint64_t)rules[x.rule].L)
+        reinterpret_cast<Slot*>(x.slot)->count = x.base + x.total;
+    }
+  }
+  const uint32_t nhot = s_row[HOT_BUCKETS], nrec = s_row[NIL_BUCKET];
+  const MRec* src = srec + t0;
+  const unsigned long long* hrow = hoff + (size_t)t * HOT_BUCKETS;
+  // MSD records: scattered to bucket order (arrival order inside a bucket: tiles in order,
+  // the tile's run in order)
+  for (uint32_t p = nhot + tid; p < nrec; p += NT) {
+    const MRec m = src[p];
+    const uint32_t mb = v3::msd_bucket(m.key);
+    const uint32_t pos = s_gpre[mb >> 6] + ranges[R_BPRE + mb] + s_toff[mb] + (p - s_row[HOT_BUCKETS + mb]);
+    mrec[pos] = m;
+  }
+  if (nhot == 0) return;  // block-uniform
+  if (local_cache) {
+    // The descriptor whose INCRBY reply first exceeds the limit freezes the key
+    // (base_limiter.go:94-106). The post-value is monotone (k4_scan), so it is the unique
+    // descriptor with after > L >= before, or the key's first descriptor of the batch.
+    for (uint32_t p = tid; p < nhot; p += NT) {
+      const MRec a = src[p];
+      const uint32_t b = (uint32_t)a.fp_lo;
+      const HotBucket3& x = hb[b];
+      if (x.flags & HB_FROZEN_PRE) continue;
+      const uint64_t P = hrow[b] + a.key;
+      const uint64_t after = x.base + P;
+      const uint32_t L = rules[rule_of(a.rn)].L;
+      if (after > L && (after - a.h <= L || P == a.h)) {
+        s_rstar[b] = a.req;
+        hb[b].rstar = a.req;
+        reinterpret_cast<Slot*>(x.slot)->flags = SLOT_FROZEN;
+      }
+    }
+    __syncthreads();
+  }
+  const uint32_t q0 = routed ? in.recs[t0].greq : in.req_of[t0];  // request of the tile's first descriptor
+  for (uint32_t p = tid; p < nhot; p += NT) {
+    const MRec a = src[p];
+    const uint32_t b = (uint32_t)a.fp_lo;
+    const uint32_t rule = rule_of(a.rn), now_mod = a.rn >> V3_RULE_BITS;
+    const uint32_t i = a.idx;
+    const unsigned long long P = hrow[b] + a.key;
+    const HotBucket3& hx = hb[b];
+    const DevRule& rl = rules[rule];
+    if (hx.flags & HB_FROZEN_PRE) {
+      out[i] = v3::local_hit_status(a.h, rl.div - now_mod);  // every descriptor is a local-cache hit
+      continue;
+    }
+    const uint64_t after = hx.base + P;
+    if (!local_cache || after <= rl.L) {
+      v3::decide_at(i, a.req, rule, a.h, now_mod, hx.base, P, SEG_NO_FREEZE, rules, out, req_thr, routed);
+      continue;
+    }
+    const uint32_t rs = s_rstar[b];
+    Slot* slot = reinterpret_cast<Slot*>(hx.slot);
+    if (rs != 0xFFFFFFFFu) {  // the freezing descriptor is in this tile, at or before this one
+      if (a.req > rs) {
+        out[i] = v3::local_hit_status(a.h, rl.div - now_mod);
+      } else {  // same request as the freezing descriptor: its INCRBY still happens
+        v3::decide_at(i, a.req, rule, a.h, now_mod, hx.base, P, SEG_NO_FREEZE, rules, out, req_thr, routed);
+        atomicMax((unsigned long long*)&slot->count, (unsigned long long)after);
+      }
+    } else if (a.req > q0) {  // froze in an earlier tile, in a request <= q0
+      out[i] = v3::local_hit_status(a.h, rl.div - now_mod);
+    } else {  // a request that began in an earlier tile: decided by k4_group
+      const uint32_t e = atomicAdd(&ctl->tile_ctr[DFR_CTR][0], 1u);
+      Deferred df;
+      df.P = P;
+      df.idx = i;
+      df.bucket = b;
+      df.req = a.req;
+      df.h = a.h;
+      df.rule = rule;
+      df.now_mod = now_mod;
+      dfr[e] = df;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k4_group — one block per range of whole MSD buckets (k4_scan packs them to fit LDS; a range
+// of one bucket larger than the stage runs on the block's global scratch). Every block also
+// decides a share of the deferred hot descriptors; the last block to finish counts U, fills
+// the hot-set candidates and clears the next batch's control block.
+// ---------------------------------------------------------------------------
+struct GScratch4 {
+  uint64_t* P;     // [GBLOCKS][BUCKET_CAP]
+  uint16_t* list;  // [GBLOCKS][BUCKET_CAP]
+  uint16_t* grp;   // [GBLOCKS][BUCKET_CAP]
+  uint32_t* slot;  // [GBLOCKS][GS_HASH]
+  uint32_t* cnt;   // [GBLOCKS][GS_HASH]
+  uint16_t* end;   // [GBLOCKS][GS_HASH]
+  uint32_t* cursor;  // [GBLOCKS]
+};
+
+__global__ __launch_bounds__(G_NT) void k4_group(DevBatch in, MRec* __restrict__ mrec,
+                                                 const DevRule* __restrict__ rules, TableDesc tab, int local_cache,
+                                                 rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
+                                                 const HotBucket3* __restrict__ hb, const Deferred* __restrict__ dfr,
+                                                 HotCand* __restrict__ cand, int cand_on, uint64_t seed,
+                                                 GScratch4 gs, uint32_t* __restrict__ wg_heads,
+                                                 const uint32_t* __restrict__ scan_heads, uint32_t n_scan_heads,
+                                                 const uint32_t* __restrict__ ranges, int routed, EngineCtl* ctl,
+                                                 EngineCtl* next_ctl) {
+  __shared__ MRec s_rec[G_CAP];
+  __shared__ uint64_t s_P[G_CAP];
+  __shared__ uint16_t s_list[G_CAP];
+  __shared__ uint16_t s_grp[G_CAP];
+  __shared__ uint32_t s_slot[G_HASH];
+  __shared__ uint32_t s_cnt[G_HASH];
+  __shared__ uint16_t s_end[G_HASH];
+  __shared__ LSeg s_agg[G_W];
+  __shared__ LSeg s_carry;
+  __shared__ uint32_t s_cursor, s_heads, s_last, s_err;
+  __shared__ uint32_t s_rn[MSD_GROUPS + 1], s_gpre[MSD_GROUPS + 1];
+  __shared__ uint32_t sh_w[G_W];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t j = blockIdx.x;
+  uint32_t heads = 0;
+  if (tid < 64) {  // ranges per group and record bases of the groups: prefixes (one wave)
+    const uint32_t v = tid < (uint32_t)MSD_GROUPS ? ranges[tid] : 0u;
+    const uint32_t w = tid < (uint32_t)MSD_GROUPS ? ranges[R_GTOT + tid] : 0u;
+    const uint32_t iv = v3::wave_incl_scan<uint32_t>(v), iw = v3::wave_incl_scan<uint32_t>(w);
+    if (tid <= (uint32_t)MSD_GROUPS) {
+      s_rn[tid] = iv - v;
+      s_gpre[tid] = iw - w;
+    }
+  }
+  if (tid == 0) {
+    s_heads = 0;
+    s_err = ld_relaxed(&ctl->err);
+  }
+  __syncthreads();
+  ST4(0);
+  if (s_err == 0) {
+    // Hot descriptors of a request that began before the tile where their key froze
+    // (k4_place, a previous launch, recorded them and the freezing requests).
+    const uint32_t nd = ctl->tile_ctr[DFR_CTR][0];
+    for (uint32_t e = j * G_NT + tid; e < nd; e += gridDim.x * G_NT) {
+      const Deferred df = dfr[e];
+      const HotBucket3& x = hb[df.bucket];
+      if (df.req > x.rstar) {
+        out[df.idx] = v3::local_hit_status(df.h, rules[df.rule].div - df.now_mod);
+      } else {
+        v3::decide_at(df.idx, df.req, df.rule, df.h, df.now_mod, x.base, df.P, SEG_NO_FREEZE, rules, out, req_thr,
+                      routed);
+        atomicMax((unsigned long long*)&reinterpret_cast<Slot*>(x.slot)->count, (unsigned long long)(x.base + df.P));
+      }
+    }
+    const uint32_t nr = s_rn[MSD_GROUPS];
+    for (uint32_t r = j; j < (uint32_t)GBLOCKS && r < nr; r += GBLOCKS) {
+      uint32_t g = 0;
+      while (g + 1 < (uint32_t)MSD_GROUPS && s_rn[g + 1] <= r) ++g;
+      const uint32_t q = r - s_rn[g];
+      const uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
+      const uint32_t k0 = rb[q], k1 = rb[q + 1];
+      const uint32_t r0 = s_gpre[g] + ranges[R_BPRE + g * 64 + k0];
+      const uint32_t r1 = k1 == 64u ? s_gpre[g + 1] : s_gpre[g] + ranges[R_BPRE + g * 64 + k1];
+      const uint32_t m = r1 - r0;
+      if (m == 0) continue;
+      __syncthreads();  // the previous range is done with LDS
+      if (m <= (uint32_t)G_CAP) {
+        for (uint32_t s = tid; s < (uint32_t)G_HASH; s += G_NT) {
+          s_slot[s] = G_EMPTY;
+          s_cnt[s] = 0;
+        }
+        if (tid == 0) s_cursor = 0;
+        const MRec* src = mrec + r0;
+#pragma unroll
+        for (int u = 0; u < G_IPT; ++u) {
+          const uint32_t k = tid + u * G_NT;
+          if (k < m) s_rec[k] = src[k];
+        }
+        __syncthreads();
+        ST4(2);
+        const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
+        heads += group_range<true>(gl, m, rules, tab, local_cache, out, req_thr, cand, cand_on, routed, s_agg,
+                                   &s_carry, sh_w, ctl);
+        continue;
+      }
+      // One bucket larger than the LDS stage. Its keys split by the fingerprint bit below the
+      // bucket bits into two halves of whole keys; each half that fits is grouped in LDS.
+      constexpr int SPLIT_BIT = 64 - 3 - MSD_BITS - 1;
+      constexpr int SU = BUCKET_CAP / G_NT;
+      const MRec* src = mrec + r0;
+      uint32_t fl[SU], n0 = 0;
+#pragma unroll
+      for (int u = 0; u < SU; ++u) {
+        const uint32_t k = tid + u * G_NT;
+        fl[u] = k < m ? (uint32_t)(src[k].key >> SPLIT_BIT) & 1u : 2u;
+        n0 += fl[u] == 0u;
+      }
+      uint32_t tot0;
+      v3::block_excl_scan<G_NT>(n0, sh_w, tot0);
+      if (tot0 <= (uint32_t)G_CAP && m - tot0 <= (uint32_t)G_CAP) {
+        for (uint32_t part = 0; part < 2u; ++part) {
+          __syncthreads();  // the previous half is done with LDS
+          for (uint32_t s = tid; s < (uint32_t)G_HASH; s += G_NT) {
+            s_slot[s] = G_EMPTY;
+            s_cnt[s] = 0;
+          }
+          // compact the half's records in position (= arrival) order: one block scan per
+          // 256-position chunk
+          uint32_t mp = 0;
+#pragma unroll
+          for (int u = 0; u < SU; ++u) {
+            const uint32_t k = tid + u * G_NT;
+            uint32_t ct;
+            const uint32_t pos = mp + v3::block_excl_scan<G_NT>(fl[u] == part ? 1u : 0u, sh_w, ct);
+            if (fl[u] == part) s_rec[pos] = src[k];
+            mp += ct;
+          }
+          if (tid == 0) s_cursor = 0;
+          __syncthreads();
+          if (mp == 0) continue;
+          const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
+          heads += group_range<true>(gl, mp, rules, tab, local_cache, out, req_thr, cand, cand_on, routed, s_agg,
+                                     &s_carry, sh_w, ctl);
+        }
+      } else {
+        // grouped in place in bucket order (global scratch)
+        const GS gg{mrec + r0,                        gs.P + (size_t)j * BUCKET_CAP,
+                    gs.list + (size_t)j * BUCKET_CAP,  gs.grp + (size_t)j * BUCKET_CAP,
+                    gs.slot + (size_t)j * GS_HASH,     gs.cnt + (size_t)j * GS_HASH,
+                    gs.end + (size_t)j * GS_HASH,      gs.cursor + j,
+                    GS_HASH};
+        for (uint32_t s = tid; s < (uint32_t)GS_HASH; s += G_NT) {
+          gg.slot[s] = G_EMPTY;
+          gg.cnt[s] = 0;
+        }
+        if (tid == 0) *gg.cursor = 0;
+        __threadfence_block();
+        __syncthreads();
+        heads += group_range<false>(gg, m, rules, tab, local_cache, out, req_thr, cand, cand_on, routed, s_agg,
+                                    &s_carry, sh_w, ctl);
+      }
+    }
+  }
+  heads = v3::wave_sum(heads);
+  __syncthreads();
+  if (lane == 0 && heads) atomicAdd(&s_heads, heads);
+  __syncthreads();
+  ST4(5);
+  // The last block to finish: U, hot-set candidates, next control block. Hand-off without
+  // fences: every wave waits for its own stores (the sc1 ones the last block reads among
+  // them), then one lane adds to the block's shard counter (blockIdx & 7); the last block of a
+  // shard adds to the global counter; the last of those is the last block.
+  if (tid == 0) st_relaxed(&wg_heads[j], s_heads);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const uint32_t shard = j & 7u;
+    const uint32_t per = (gridDim.x - shard + 7u) / 8u;  // blocks of this shard
+    bool last = atomicAdd(&ctl->tile_ctr[SHARD_CTR0 + shard][0], 1u) == per - 1u;
+    if (last) {
+      const uint32_t shards = gridDim.x < 8u ? gridDim.x : 8u;
+      last = atomicAdd(&ctl->tile_ctr[DONE_CTR][0], 1u) == shards - 1u;
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // U = Σ per-block unique-key counts (this kernel and k4_scan's hot leaders)
+  if (tid == 0) s_heads = 0;
+  if (tid == 1) s_cursor = 0;
+  __syncthreads();
+  {
+    uint32_t u = 0, ins = 0;
+    for (uint32_t k = tid; k < gridDim.x + n_scan_heads; k += G_NT) {
+      const uint32_t v = k < gridDim.x ? ld_relaxed(&wg_heads[k]) : scan_heads[k - gridDim.x];
+      u += v & 0xFFFFu;
+      ins += v >> 16;
+    }
+    u = v3::wave_sum(u);
+    ins = v3::wave_sum(ins);
+    if (lane == 0) {
+      if (u) atomicAdd(&s_heads, u);
+      if (ins) atomicAdd(&s_cursor, ins);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    ctl->n_segments = s_heads;
+    ctl->tile_ctr[INS_CTR0][0] += s_cursor;  // new table slots (engine stats)
+  }
+  // hot-set candidates found by leaders: their key-prefix state
+  const uint32_t nc = min((uint32_t)CAND_MAX, ld_relaxed(&ctl->tile_ctr[CAND_CTR][0]));
+  for (uint32_t i = tid; i < nc; i += G_NT) {
+    HotCand c;
+    ld_sc1_32B(&c, &cand[i]);
+    if (c.first_idx == 0xFFFFFFFFu) continue;  // a hot key: state already known
+    const uint32_t d = c.first_idx;
+    const uint32_t unit = rules[c.rule].unit;
+    if (in.recs) {  // routed batch: the record already carries the prefix state
+      c.a = in.recs[d].a;
+      c.b = in.recs[d].b;
+    } else {
+      const uint32_t o0 = in.off[d], o1 = in.off[d + 1];
+      const FpState st = v3::prefix_state(in.blob, o0, o1 - o0, unit, seed);
+      c.a = st.a;
+      c.b = st.b;
+    }
+    c.unit = unit;
+    cand[i] = c;
+  }
+  uint32_t* z = reinterpret_cast<uint32_t*>(next_ctl);
+  constexpr uint32_t words = sizeof(EngineCtl) / 4;
+  for (uint32_t w = tid; w < words; w += G_NT) z[w] = 0;
+}
+
+}  // namespace v4
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+uint32_t v4_tiles(uint32_t n) { return n ? (n + V3_TILE - 1) / V3_TILE : 1; }
+uint32_t v4_group_blocks(uint32_t) { return v4::GBLOCKS; }
+uint32_t v4_scan_blocks() { return V3_SCAN_BUCKETS / 64; }
+size_t v4_scratch_bytes() {
+  using namespace v4;
+  return (size_t)GBLOCKS * BUCKET_CAP * (8 + 2 + 2) + (size_t)GBLOCKS * GS_HASH * (4 + 4 + 2) + (size_t)GBLOCKS * 4 +
+         RANGE_WORDS * 4 + 1024;
+}
+static uint32_t* v4_ranges(void* scratch) {  // the last RANGE_WORDS words (+ slack) of the scratch
+  return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(scratch) + v4_scratch_bytes() - 1024 -
+                                     v4::RANGE_WORDS * 4);
+}
+
+void launch_v4_hist(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
+                    const HotEntry* hot, uint32_t* req_thr, uint32_t* fpart, uint16_t* tstart,
+                    unsigned long long* thsum, MRec* srec, rl_status* out, EngineCtl* ctl) {
+  const DevBatch in = make_dev_batch(b);
+  if (in.recs)
+    hipLaunchKernelGGL(v4::k4_hist<true>, dim3(v4_tiles(b.n_desc)), dim3(V3_THREADS), 0, st, in, rules, n_rules, seed,
+                       hot, req_thr, fpart, tstart, thsum, srec, out, ctl);
+  else
+    hipLaunchKernelGGL(v4::k4_hist<false>, dim3(v4_tiles(b.n_desc)), dim3(V3_THREADS), 0, st, in, rules, n_rules,
+                       seed, hot, req_thr, fpart, tstart, thsum, srec, out, ctl);
+}
+void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const unsigned long long* thsum,
+                    unsigned long long* hoff, const uint32_t* fpart, const HotEntry* hot_list, HotBucket3* hb,
+                    const TableDesc& tab, int local_cache, HotCand* cand, uint32_t* heads_out, uint16_t* toff,
+                    void* scratch, EngineCtl* ctl) {
+  hipLaunchKernelGGL(v4::k4_scan, dim3(v4_scan_blocks()), dim3(v4::SCAN_NT), 0, st, tstart, thsum, v4_tiles(n), hoff,
+                     fpart, hot_list, hb, tab, local_cache, cand, heads_out, toff, v4_ranges(scratch), ctl);
+}
+void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart, const uint16_t* toff,
+                     void* scratch, const DevRule* rules, const unsigned long long* hoff, HotBucket3* hb,
+                     int local_cache, MRec* mrec, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
+                     EngineCtl* ctl) {
+  hipLaunchKernelGGL(v4::k4_place, dim3(v4_tiles(b.n_desc)), dim3(V3_THREADS), 0, st, make_dev_batch(b), srec, tstart,
+                     toff, v4_ranges(scratch), rules, hoff, hb, local_cache, mrec, out, req_thr, dfr, routed, ctl);
+}
+void launch_v4_group(hipStream_t st, const rl_batch& b, MRec* mrec, const DevRule* rules, const TableDesc& tab,
+                     int local_cache, rl_status* out, uint32_t* req_thr, const HotBucket3* hb, const Deferred* dfr,
+                     HotCand* cand, int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads,
+                     const uint32_t* scan_heads, int routed, EngineCtl* ctl, EngineCtl* next_ctl) {
+  using namespace v4;
+  uint8_t* p = reinterpret_cast<uint8_t*>(scratch);
+  GScratch4 gs;
+  gs.P = reinterpret_cast<uint64_t*>(p);
+  p += (size_t)GBLOCKS * BUCKET_CAP * 8;
+  gs.slot = reinterpret_cast<uint32_t*>(p);
+  p += (size_t)GBLOCKS * GS_HASH * 4;
+  gs.cnt = reinterpret_cast<uint32_t*>(p);
+  p += (size_t)GBLOCKS * GS_HASH * 4;
+  gs.cursor = reinterpret_cast<uint32_t*>(p);
+  p += (size_t)GBLOCKS * 4;
+  gs.list = reinterpret_cast<uint16_t*>(p);
+  p += (size_t)GBLOCKS * BUCKET_CAP * 2;
+  gs.grp = reinterpret_cast<uint16_t*>(p);
+  p += (size_t)GBLOCKS * BUCKET_CAP * 2;
+  gs.end = reinterpret_cast<uint16_t*>(p);
+  hipLaunchKernelGGL(k4_group, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), mrec, rules, tab, local_cache, out,
+                     req_thr, hb, dfr, cand, cand_on, seed, gs, wg_heads, scan_heads, v4_scan_blocks(),
+                     v4_ranges(scratch), routed, ctl, next_ctl);
+}
+
+}  // namespace rlhip
+
+#ifdef RL_STAMPS
+extern "C" int rl_debug_st4(uint64_t* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(rlhip::v4::g_st4), sizeof(uint64_t) * 4096 * 8, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

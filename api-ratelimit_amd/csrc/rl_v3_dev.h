@@ -1,0 +1,380 @@
+// rl_v3_dev.h — device helpers of the bucketed decision pipelines (v3 and v4):
+// descriptor loading + fingerprint, hot-set lookup, LDS tile sort, segmented scan element,
+// decisions of hot / local-cache-hit descriptors. Included by rl_kernels_v3.hip and
+// rl_kernels_v4.hip only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rl_common.h"
+#include "rl_decide.h"
+#include "rl_device.h"
+
+namespace rlhip {
+namespace v3 {
+
+constexpr int T = V3_TILE;
+constexpr int NT = V3_THREADS;
+constexpr int R = T / NT;      // descriptors per thread
+constexpr int W = NT / 64;     // waves per tile block
+constexpr int PRE_DW = 12;     // blob dwords preloaded per descriptor (prefixes up to 40 B hash inline)
+constexpr uint32_t BKT_NONE = 4095;  // past the end of the batch (sorts last in 12 bits)
+static_assert(NBUCKETS <= 4095, "bucket ids are 12-bit");
+static_assert(T <= 65536, "u16 tile offsets");
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+
+RL_DEV uint32_t msd_bucket(uint64_t key) { return (uint32_t)((key << 3) >> (64 - MSD_BITS)); }
+RL_DEV uint32_t rule_of(uint32_t rn) { return rn & (V3_MAX_RULES - 1u); }
+
+RL_DEV uint32_t hot_lookup(const HotEntry* sh_hot, uint64_t a, uint64_t b, uint32_t unit, uint32_t& rule) {
+  uint32_t s = (uint32_t)(a >> 40) & (HOT_SLOTS - 1);
+  for (int probe = 0; probe < HOT_SLOTS; ++probe) {
+    const HotEntry& e = sh_hot[s];
+    if (e.idx == 0xFFFFFFFFu) return 0xFFFFFFFFu;
+    if (e.a == a && e.b == b && e.unit == unit) {
+      rule = e.rule;
+      return e.idx;
+    }
+    s = (s + 1) & (HOT_SLOTS - 1);
+  }
+  return 0xFFFFFFFFu;
+}
+
+template <class V>
+RL_DEV V wave_sum(V x) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+template <class V>
+RL_DEV V wave_incl_scan(V x) {
+  const uint32_t lane = __lane_id();
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const V y = __shfl_up(x, s, 64);
+    if (lane >= (uint32_t)s) x += y;
+  }
+  return x;
+}
+
+// Exclusive scan over a block of NTH threads (one value each); sh_w holds NTH/64 words.
+template <int NTH>
+RL_DEV uint32_t block_excl_scan(uint32_t v, uint32_t* sh_w, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t incl = wave_incl_scan<uint32_t>(v);
+  if (lane == 63) sh_w[wave] = incl;
+  __syncthreads();
+  uint32_t before = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < NTH / 64; ++w) {
+    const uint32_t x = sh_w[w];
+    before += (uint32_t)w < wave ? x : 0u;
+    total += x;
+  }
+  __syncthreads();
+  return before + incl - v;
+}
+
+// ---------------------------------------------------------------------------
+// Per-descriptor input: load + fingerprint. The loads of a thread's R descriptors are
+// issued together in two dependent levels: (rule, request, prefix offsets), then (now,
+// hits_addend, rule entry, prefix bytes as 16-B loads).
+// ---------------------------------------------------------------------------
+struct D3 {
+  uint64_t key, lo;
+  uint32_t req, rule, h, now_mod, bucket, gen;
+};
+
+// Words of a prefix beyond the preloaded dwords. p[0] = d0 is the dword holding the first
+// remaining byte at byte offset sh; only dwords that overlap the prefix are read.
+RL_DEV void hash_tail(const uint32_t* p, uint32_t d0, uint32_t sh, uint32_t rem, FpState& s) {
+  for (uint32_t k = 0; rem > 0; ++k) {
+    const uint32_t d1 = sh + rem > 4 ? p[2 * k + 1] : 0u;
+    const uint32_t d2 = sh + rem > 8 ? p[2 * k + 2] : 0u;
+    const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    uint64_t w = ((uint64_t)hi << 32) | lo;
+    if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
+    fp_word(s, w);
+    d0 = d2;
+    rem = rem > 8 ? rem - 8 : 0;
+  }
+}
+
+// Prefix state (lanes a, b) of a byte string, reading only dwords that overlap it.
+RL_DEV FpState prefix_state(const uint8_t* blob, uint32_t off, uint32_t len, uint32_t unit, uint64_t seed) {
+  FpState s = fp_init(len, unit, seed);
+  if (len) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(blob + (off & ~3u));
+    hash_tail(p, p[0], off & 3u, len, s);
+  }
+  return s;
+}
+
+// Window, sort key, gen and bucket of one valid descriptor from its prefix state.
+RL_DEV void key_of(D3& x, const FpState& s, int64_t now, const DevRule& rr, const HotEntry* sh_hot, uint32_t& err) {
+  const uint32_t unit = rr.unit;
+  const int64_t widx = div_const(now, unit);
+  const int64_t ws = widx * (int64_t)rr.div;  // (now/divider)*divider  cache_key.go:66-68
+  uint32_t hot_rule = 0;
+  const uint32_t hidx = hot_lookup(sh_hot, s.a, s.b, unit, hot_rule);
+  uint64_t hi, lo;
+  fp_final(s, (uint64_t)ws, hi, lo);
+  const uint32_t region = (unit - 1u) * 2u + (uint32_t)(widx & 1);
+  x.key = make_sort_key(region, hi);
+  x.lo = lo;
+  x.gen = (uint32_t)widx + 1u;
+  x.now_mod = (uint32_t)(now - ws);
+  if (hidx != 0xFFFFFFFFu) {
+    if (hot_rule != x.rule) err |= ERR_V2_FALLBACK;  // a hot bucket must hold one key under one rule
+    x.bucket = hidx * 2u + (uint32_t)(widx & 1);
+  } else {
+    x.bucket = HOT_BUCKETS + msd_bucket(x.key);
+  }
+}
+
+RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, uint32_t n_rules, uint64_t seed,
+                       const HotEntry* sh_hot, uint32_t t0, D3 (&d)[R], uint32_t& err) {
+  const uint32_t tid = threadIdx.x;
+  uint32_t rl[R], q[R], o0[R], len[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t i = t0 + r * NT + tid;
+    const bool v = i < in.n_desc;
+    rl[r] = v ? in.rule[i] : RL_NIL_RULE;
+    q[r] = v ? in.req_of[i] : 0u;
+    const uint32_t a = v ? in.off[i] : 0u;
+    const uint32_t b = v ? in.off[i + 1] : 0u;
+    o0[r] = a;
+    len[r] = b - a;
+  }
+  const uint32_t lim = (in.blob_bytes + 3u) & ~3u;
+  int64_t now[R];
+  uint32_t ha[R];
+  DevRule rr[R];
+  bool ok[R];
+  uint32_t dw[R][PRE_DW];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t i = t0 + r * NT + tid;
+    const bool v = i < in.n_desc;
+    const bool q_ok = q[r] < in.n_req;
+    ok[r] = v && rl[r] != RL_NIL_RULE && rl[r] < n_rules && q_ok;
+    if (v && rl[r] != RL_NIL_RULE && !ok[r]) err |= ERR_BAD_INPUT;
+#ifdef RL_V_NOL2  // timing experiment only: no per-request loads
+    now[r] = in.now[0];
+    ha[r] = 1u;
+#else
+    now[r] = (v && q_ok) ? in.now[q[r]] : 0;
+    ha[r] = (v && q_ok) ? in.hits[q[r]] : 1u;
+#endif
+    if (ok[r]) {
+      rr[r] = rules[rl[r]];
+    } else {
+      rr[r].L = rr[r].near = 0;
+      rr[r].div = 1;
+      rr[r].unit = RL_UNIT_SECOND;
+    }
+    const uint32_t a = o0[r] & ~3u;
+#ifdef RL_V_NOBLOB  // timing experiment only: no prefix bytes
+    const uint32_t need = 0;
+#else
+    const uint32_t need = ok[r] ? (((o0[r] & 3u) + len[r] + 3u) & ~3u) : 0u;  // bytes from a
+#endif
+#pragma unroll
+    for (int c = 0; c < PRE_DW / 4; ++c) {
+      const uint32_t cb = a + 16u * c;
+      if (16u * c < need && cb + 16u <= lim) {
+        const u32x4 x = *reinterpret_cast<const u32x4*>(in.blob + cb);
+        dw[r][4 * c] = x.x;
+        dw[r][4 * c + 1] = x.y;
+        dw[r][4 * c + 2] = x.z;
+        dw[r][4 * c + 3] = x.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          dw[r][4 * c + k] =
+              16u * c + 4u * k < need ? *reinterpret_cast<const uint32_t*>(in.blob + cb + 4u * k) : 0u;
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t i = t0 + r * NT + tid;
+    D3& x = d[r];
+    x.req = q[r];
+    x.rule = rl[r];
+    x.h = ha[r] > 1u ? ha[r] : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
+    x.now_mod = 0;
+    x.gen = 0;
+    x.key = NIL_KEY;
+    x.lo = 0;
+    x.bucket = i < in.n_desc ? NIL_BUCKET : BKT_NONE;
+    if (!ok[r]) continue;
+    if (now[r] < 0 || now[r] > 0xFFFFFFF0ll) {
+      err |= ERR_BAD_TIME;
+      continue;
+    }
+    const uint32_t unit = rr[r].unit;
+    const uint32_t sh = o0[r] & 3u;
+    FpState s = fp_init(len[r], unit, seed);
+    uint32_t rem = len[r];
+#pragma unroll
+    for (int k = 0; k < (PRE_DW - 1) / 2; ++k) {
+      if (rem > 0) {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(dw[r][2 * k + 1], dw[r][2 * k], sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(dw[r][2 * k + 2], dw[r][2 * k + 1], sh);
+        uint64_t w = ((uint64_t)hi << 32) | lo;
+        if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
+        fp_word(s, w);
+        rem = rem > 8 ? rem - 8 : 0;
+      }
+    }
+    constexpr int DONE_DW = 2 * ((PRE_DW - 1) / 2);  // dword holding the next word's first byte
+    if (rem)
+      hash_tail(reinterpret_cast<const uint32_t*>(in.blob + (o0[r] & ~3u)) + DONE_DW, dw[r][DONE_DW], sh, rem, s);
+    key_of(x, s, now[r], rr[r], sh_hot, err);
+  }
+}
+
+// Routed batch (owner side of the multi-GPU router): each record already carries the
+// prefix state of its key, its rule, now and hits (one 32-B load per descriptor).
+RL_DEV void load_routed(const DevBatch& in, const DevRule* __restrict__ rules, uint32_t n_rules,
+                        const HotEntry* sh_hot, uint32_t t0, D3 (&d)[R], uint32_t& err) {
+  const uint32_t tid = threadIdx.x;
+  RRec rc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t i = t0 + r * NT + tid;
+    if (i < in.n_desc) {
+      rc[r] = in.recs[i];
+    } else {
+      rc[r].a = rc[r].b = 0;
+      rc[r].now = rc[r].h = rc[r].greq = 0;
+      rc[r].rule = RL_NIL_RULE;
+    }
+  }
+  DevRule rr[R];
+  bool ok[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    ok[r] = rc[r].rule < n_rules;
+    if (ok[r]) rr[r] = rules[rc[r].rule];
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t i = t0 + r * NT + tid;
+    D3& x = d[r];
+    x.req = rc[r].greq;
+    x.rule = rc[r].rule;
+    x.h = rc[r].h > 1u ? rc[r].h : 1u;
+    x.now_mod = 0;
+    x.gen = 0;
+    x.key = NIL_KEY;
+    x.lo = 0;
+    x.bucket = i < in.n_desc ? NIL_BUCKET : BKT_NONE;
+    if (!ok[r]) {
+      if (i < in.n_desc && rc[r].rule != RL_NIL_RULE) err |= ERR_BAD_INPUT;
+      continue;
+    }
+    if (rc[r].now > 0xFFFFFFF0u) {
+      err |= ERR_BAD_TIME;
+      continue;
+    }
+    key_of(x, FpState{rc[r].a, rc[r].b}, (int64_t)rc[r].now, rr[r], sh_hot, err);
+  }
+}
+
+RL_DEV void load_hot_table(const HotEntry* __restrict__ hot, HotEntry* sh_hot) {
+  for (int k = threadIdx.x; k < HOT_SLOTS; k += blockDim.x) sh_hot[k] = hot[k];
+}
+
+// One stable LDS counting pass over 64 digits of the tile: src -> dst by (s_d[x] >> shift) & 63.
+RL_DEV void tile_digit_pass(const uint16_t* s_d, const uint16_t* src, uint16_t* dst, int shift, uint32_t (*s_cnt)[64],
+                            uint32_t* sh_w) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < W * 64; i += NT) (&s_cnt[0][0])[i] = 0;
+  __syncthreads();
+  const uint64_t lt = lanemask_lt();
+  uint32_t dg[R], rk[R], sv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t p = wave * (T / W) + r * 64 + lane;
+    const uint32_t o = src[p];
+    const uint32_t dd = ((uint32_t)s_d[o] >> shift) & 63u;
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (int bt = 0; bt < 6; ++bt) {
+      const bool bit = (dd >> bt) & 1u;
+      const uint64_t bal = __ballot(bit);
+      m &= bit ? bal : ~bal;
+    }
+    const uint32_t before = s_cnt[wave][dd];
+    __builtin_amdgcn_wave_barrier();
+    if (lane == (uint32_t)__ffsll((unsigned long long)m) - 1u) s_cnt[wave][dd] = before + (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+    dg[r] = dd;
+    rk[r] = before + (uint32_t)__popcll(m & lt);
+    sv[r] = o;
+  }
+  __syncthreads();
+  {  // digit-major exclusive offsets: entry (digit, wave) = tid
+    static_assert(W * 64 == NT, "one (digit, wave) entry per thread");
+    const uint32_t dd = tid / W, w = tid % W;
+    const uint32_t v = s_cnt[w][dd];
+    uint32_t total;
+    const uint32_t off = block_excl_scan<NT>(v, sh_w, total);
+    s_cnt[w][dd] = off;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < R; ++r) dst[s_cnt[wave][dg[r]] + rk[r]] = (uint16_t)sv[r];
+  __syncthreads();
+}
+
+struct SegEl {
+  uint32_t f, hp;
+  unsigned long long s;
+};
+RL_DEV SegEl seg_op(const SegEl a, const SegEl b) {
+  if (b.f) return b;
+  return SegEl{a.f, a.hp, a.s + b.s};
+}
+
+
+RL_DEV rl_status local_hit_status(uint32_t h, uint32_t reset) {
+  // base_limiter.go:76-81: OVER_LIMIT from the local cache, no INCRBY
+  rl_status st;
+  st.code_flags = RL_CODE_OVER_LIMIT | ((RL_FLAG_HAS_LIMIT | RL_FLAG_LOCAL_CACHE_HIT) << 8);
+  st.limit_remaining = 0;
+  st.reset_s = reset;
+  st.over_limit_delta = h;
+  st.near_limit_delta = 0;
+  return st;
+}
+
+// Decision of a descriptor whose INCRBY post-value is base + P (decide_one in rl_decide.h).
+// routed: a routed record's ThrottleMillis slot is its own position (idx), not its request.
+RL_DEV void decide_at(uint32_t idx, uint32_t req, uint32_t rule, uint32_t h, uint32_t now_mod, uint64_t base,
+                      uint64_t P, uint32_t freeze, const DevRule* __restrict__ rules, rl_status* __restrict__ out,
+                      uint32_t* __restrict__ req_thr, int routed) {
+  SortedRec o;
+  o.P = P;
+  o.head = 0;
+  o.idx = idx;
+  o.rule = rule;
+  o.req = req;
+  o.h = h;
+  o.now_mod = (int32_t)now_mod;
+  SegInfo si;
+  si.base = base;
+  si.freeze = freeze;
+  si.pad = 0;
+  decide_one(o, si, rules[rule], out, req_thr, routed ? idx : req);
+}
+
+}  // namespace v3
+}  // namespace rlhip

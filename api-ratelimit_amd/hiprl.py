@@ -37,7 +37,7 @@ STATUS_DTYPE = np.dtype([("code_flags", "<u4"), ("limit_remaining", "<u4"), ("re
                          ("over_limit_delta", "<u4"), ("near_limit_delta", "<u4")])
 
 
-PIPELINE_FLAGS = {"v3": 0, "lsd": 1, "v2": 2}  # rl_config.flags (RL_CFG_LSD_ONLY, RL_CFG_V2)
+PIPELINE_FLAGS = {"v4": 0, "lsd": 1, "v2": 2, "v3": 4}  # rl_config.flags (RL_CFG_LSD_ONLY, RL_CFG_V2, RL_CFG_V3)
 
 
 class RlConfig(C.Structure):
@@ -201,10 +201,11 @@ class Engine:
                  local_cache: bool = False, per_second_split: bool = False, max_batch_desc: int = 1 << 16,
                  max_batch_req: Optional[int] = None, max_blob_bytes: Optional[int] = None, sort_bits: int = 48,
                  hash_seed: int = 0x5EE7AB1E5EED, lib_path: Optional[os.PathLike] = None, lsd_only: bool = False,
-                 pipeline: str = "v3"):
-        """pipeline: "v3" (default: hot keys decided in place, MSD buckets grouped in LDS),
-        "v2" (bucketed pipeline kept for comparison) or "lsd" (radix-sort pipeline, also the
-        fallback of the other two). lsd_only=True is pipeline="lsd"."""
+                 pipeline: str = "v4"):
+        """pipeline: "v4" (default: tile-sorted records, hot keys decided in place, MSD buckets
+        gathered and grouped in LDS), "v3" / "v2" (earlier bucketed pipelines kept for
+        comparison) or "lsd" (radix-sort pipeline, also the fallback of the others).
+        lsd_only=True is pipeline="lsd"."""
         if lsd_only:
             pipeline = "lsd"
         if pipeline not in PIPELINE_FLAGS:

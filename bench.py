@@ -49,8 +49,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-kernel-times", action="store_true")
     ap.add_argument("--no-roofline-probe", action="store_true")
-    ap.add_argument("--pipeline", choices=["v3", "v2", "lsd"], default="v3",
-                    help="decision pipeline (v3 default; v2 = bucketed pipeline; lsd = radix-sort pipeline only)")
+    ap.add_argument("--pipeline", choices=["v4", "v3", "v2", "lsd"], default="v4",
+                    help="decision pipeline (v4 default; v3 / v2 = earlier bucketed pipelines; lsd = radix-sort only)")
     ap.add_argument("--independent", action="store_true",
                     help="N>1: unrouted replicas (each rank its own key space) instead of RCCL routing")
     ap.add_argument("--json-out", type=str, default="")
@@ -196,7 +196,7 @@ def main():
         prof_dir = ROOT / "profiles"
         traffic = None
         # PMC traffic of this pipeline from the committed rocprofv3 --pmc passes (tools/profile_round.sh)
-        tf = prof_dir / {"v3": "r01_v3_pmc_traffic.json", "v2": "r01_v2_pmc_traffic.json",
+        tf = prof_dir / {"v4": "r01_v4_pmc_traffic.json", "v3": "r01_v3_pmc_traffic.json", "v2": "r01_v2_pmc_traffic.json",
                          "lsd": "r01_pmc_traffic.json"}[args.pipeline]
         if tf.exists():
             try:

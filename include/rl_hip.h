@@ -72,8 +72,9 @@ typedef struct rl_config {
 
 /* rl_config.flags */
 enum {
-  RL_CFG_LSD_ONLY = 1u,  /* always use the LSD radix-sort pipeline (default: v3 pipeline, LSD as fallback) */
-  RL_CFG_V2 = 2u         /* use the v2 bucketed pipeline (kept for comparison) */
+  RL_CFG_LSD_ONLY = 1u,  /* always use the LSD radix-sort pipeline (default: v4 pipeline, LSD as fallback) */
+  RL_CFG_V2 = 2u,        /* use the v2 bucketed pipeline (kept for comparison) */
+  RL_CFG_V3 = 4u         /* use the v3 pipeline (kept for comparison) */
 };
 
 /* One rate-limit rule: config.RateLimit.Limit (src/config/config.go:26-32). */

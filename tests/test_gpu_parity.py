@@ -20,10 +20,10 @@ pytestmark = pytest.mark.gpu
 
 from streams import LS, RULES, UNITS, batch_sizes, make_stream  # noqa: E402,F401
 
-PIPELINES = ["v3", "v2", "lsd"]
+PIPELINES = ["v4", "v3", "v2", "lsd"]
 
 
-def run_both(reqs, sizes, local_cache, sort_bits=48, ratio=0.8, lsd_only=False, pipeline="v3"):
+def run_both(reqs, sizes, local_cache, sort_bits=48, ratio=0.8, lsd_only=False, pipeline="v4"):
     o = oracle.Oracle(near_limit_ratio=ratio, local_cache=local_cache)
     o.load_rules(RULES)
     e = hiprl.Engine(near_limit_ratio=ratio, local_cache=local_cache, sort_bits=sort_bits, max_batch_desc=1 << 17,
@@ -100,7 +100,7 @@ def hot_stream(n_batches, per_batch, t0, rule_of=None, seed=0):
     return reqs, sizes
 
 
-@pytest.mark.parametrize("pipeline", ["v3", "v2"])
+@pytest.mark.parametrize("pipeline", ["v4", "v3", "v2"])
 @pytest.mark.parametrize("local_cache", [False, True])
 def test_hot_set_across_batches(local_cache, pipeline):
     """The bucketed pipelines learn hot keys from one batch and give them their own
@@ -115,7 +115,7 @@ def test_hot_set_across_batches(local_cache, pipeline):
     assert s["live_slots_hint"] == eng.ref_oracle.num_keys(), s  # one insert per (key, window)
 
 
-@pytest.mark.parametrize("pipeline", ["v3", "v2"])
+@pytest.mark.parametrize("pipeline", ["v4", "v3", "v2"])
 def test_hot_key_changes_rule(pipeline):
     """A hot key submitted under a second rule in a later batch sends that batch to the
     LSD pipeline (before anything touches the table); results stay bit-exact."""
@@ -230,7 +230,7 @@ def test_grouping_collisions(which):
 
 @pytest.mark.parametrize("L", [500, 3000, 20])
 def test_hot_freeze_in_straddling_request(L):
-    """v3 decides hot keys in arrival-order tiles of 2048 descriptors. When the local cache
+    """v3 and v4 decide hot keys in arrival-order tiles of 2048 descriptors. When the local cache
     freezes a hot key inside a request that continues into later tiles, those later
     descriptors still INCRBY (all lookups of a request precede its Sets,
     fixed_cache_impl.go:55-86); requests after it are local-cache hits. Long requests of

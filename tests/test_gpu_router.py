@@ -68,14 +68,15 @@ def stream_batches(G, steps, per, seed, keyspace=30):
     return out
 
 
-@pytest.mark.parametrize("pipeline", ["v3", "lsd"])
+@pytest.mark.parametrize("pipeline", ["v4", "v3", "lsd"])
 @pytest.mark.parametrize("local_cache", [False, True])
 @pytest.mark.parametrize("G", [2, 4])
 def test_routed_random_streams(G, local_cache, pipeline):
     run_routed(G, stream_batches(G, 4, 1500, seed=G), local_cache, pipeline)
 
 
-def test_routed_hot_keys_v3():
+@pytest.mark.parametrize("pipeline", ["v4", "v3"])
+def test_routed_hot_keys(pipeline):
     """A few keys take most descriptors on every origin: the owners' hot sets form from
     routed candidates and later steps decide those keys in v3's hot buckets."""
     G, steps = 3, 12
@@ -93,7 +94,7 @@ def test_routed_hot_keys_v3():
             row.append(hiprl.build_batch(reqs))
         out.append(row)
     for lc in (False, True):
-        shards = run_routed(G, out, lc, "v3")
+        shards = run_routed(G, out, lc, pipeline)
         assert max(sh.eng.stats()["hot_keys"] for sh in shards) > 0
 
 
@@ -104,4 +105,4 @@ def test_routed_empty_and_nil_only():
     b_empty = hiprl.build_batch([])
     b_nil = hiprl.build_batch([("d", [[("k", "v")], [("k", "w")]], [nil, nil], 1, 1_700_000_000)])
     b_one = hiprl.build_batch([("d", [[("k", "v")]], [1], 2, 1_700_000_000)])
-    run_routed(G, [[b_empty, b_nil, b_one], [b_one, b_empty, b_empty], [b_nil, b_nil, b_nil]], True, "v3")
+    run_routed(G, [[b_empty, b_nil, b_one], [b_one, b_empty, b_empty], [b_nil, b_nil, b_nil]], True, "v4")
