@@ -926,7 +926,7 @@ struct GScratch4 {
   uint32_t* cursor;  // [GBLOCKS]
 };
 
-__global__ __launch_bounds__(G_NT) void k4_group(DevBatch in, MRec* __restrict__ mrec,
+__global__ __launch_bounds__(G_NT, 4) void k4_group(DevBatch in, MRec* __restrict__ mrec,
                                                  const DevRule* __restrict__ rules, TableDesc tab, int local_cache,
                                                  rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
                                                  const HotBucket3* __restrict__ hb, const Deferred* __restrict__ dfr,
@@ -1016,13 +1016,11 @@ __global__ __launch_bounds__(G_NT) void k4_group(DevBatch in, MRec* __restrict__
       constexpr int SPLIT_BIT = 64 - 3 - MSD_BITS - 1;
       constexpr int SU = BUCKET_CAP / G_NT;
       const MRec* src = mrec + r0;
-      uint32_t fl[SU], n0 = 0;
-#pragma unroll
-      for (int u = 0; u < SU; ++u) {
-        const uint32_t k = tid + u * G_NT;
-        fl[u] = k < m ? (uint32_t)(src[k].key >> SPLIT_BIT) & 1u : 2u;
-        n0 += fl[u] == 0u;
-      }
+      auto half_of = [&](uint32_t k) -> uint32_t {
+        return k < m ? (uint32_t)(__builtin_nontemporal_load(&src[k].key) >> SPLIT_BIT) & 1u : 2u;
+      };
+      uint32_t n0 = 0;
+      for (int u = 0; u < SU; ++u) n0 += half_of(tid + u * G_NT) == 0u;
       uint32_t tot0;
       v3::block_excl_scan<G_NT>(n0, sh_w, tot0);
       if (tot0 <= (uint32_t)G_CAP && m - tot0 <= (uint32_t)G_CAP) {
@@ -1035,12 +1033,12 @@ __global__ __launch_bounds__(G_NT) void k4_group(DevBatch in, MRec* __restrict__
           // compact the half's records in position (= arrival) order: one block scan per
           // 256-position chunk
           uint32_t mp = 0;
-#pragma unroll
           for (int u = 0; u < SU; ++u) {
             const uint32_t k = tid + u * G_NT;
+            const bool mine = half_of(k) == part;
             uint32_t ct;
-            const uint32_t pos = mp + v3::block_excl_scan<G_NT>(fl[u] == part ? 1u : 0u, sh_w, ct);
-            if (fl[u] == part) s_rec[pos] = src[k];
+            const uint32_t pos = mp + v3::block_excl_scan<G_NT>(mine ? 1u : 0u, sh_w, ct);
+            if (mine) s_rec[pos] = src[k];
             mp += ct;
           }
           if (tid == 0) s_cursor = 0;

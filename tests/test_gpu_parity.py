@@ -265,3 +265,51 @@ def test_hot_freeze_in_straddling_request(L):
     g = streams.replay(e, reqs, sizes)
     streams.assert_same(*a, *g, f"straddle L={L}")
     assert e.stats()["hot_keys"] >= 1
+
+
+def _bucket_keys(prefix: str, now: int, n: int = 20000):
+    """Key ids whose fingerprints (engine default seed, SECOND unit) share one MSD bucket
+    (hi bits 63..53) with different split bits (hi bit 52); also every id's bucket."""
+    ids = np.arange(n, dtype=np.uint64)
+    blob, off = workload.prefix_blob([prefix.encode() + b"_k_", ids, b"_"])
+    hi, _ = oracle.fingerprints(blob, off, now, hiprl.SECOND, 0x5EE7AB1E5EED)
+    bkt = hi >> np.uint64(53)
+    half = (hi >> np.uint64(52)) & np.uint64(1)
+    for i in range(n):
+        same = np.nonzero((bkt == bkt[i]) & (half != half[i]))[0]
+        if len(same):
+            return int(i), int(same[0]), bkt
+    raise AssertionError("no split pair")
+
+
+@pytest.mark.parametrize("local_cache", [False, True])
+def test_v4_oversized_bucket_paths(local_cache):
+    """v4 groups each MSD range in LDS (at most 640 records). A larger bucket of a first
+    batch (no hot set yet) is split by the fingerprint bit below the bucket bits into two
+    halves of whole keys (keys a, b: ~480 descriptors each, same bucket, different halves);
+    a half still too large (key c: ~800 descriptors) is grouped in the block's global
+    scratch. Bit-exact either way, and the batch stays on the v4 pipeline."""
+    now = 1_700_000_100
+    a, b, bkt = _bucket_keys("sp", now)
+    c = next(i for i in range(len(bkt)) if bkt[i] != bkt[a])
+    rng = np.random.default_rng(11)
+    reqs = []
+    for i in range(8000):
+        x = rng.random()
+        if x < 0.06:
+            k = a
+        elif x < 0.12:
+            k = b
+        elif x < 0.22:
+            k = c
+        else:
+            k = 20000 + int(rng.integers(0, 3000))
+        reqs.append(("sp", [[("k", str(k))]], [2], int(rng.integers(0, 3)), now))  # SECOND L=10
+    o = oracle.Oracle(near_limit_ratio=0.8, local_cache=local_cache)
+    o.load_rules(RULES)
+    e = hiprl.Engine(near_limit_ratio=0.8, local_cache=local_cache, max_batch_desc=1 << 14, pipeline="v4")
+    e.load_rules(RULES)
+    g = streams.replay(e, reqs, [len(reqs)])
+    ref = streams.replay(o, reqs, [len(reqs)])
+    streams.assert_same(*ref, *g, f"v4 oversized local={local_cache}")
+    assert e.stats()["lsd_fallbacks"] == 0, e.stats()
