@@ -20,7 +20,7 @@ for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
 per_kernel = {}
 fetch_raw = write = 0.0
 for k, c in vals.items():
-    if not (k.startswith("k_") or k.startswith("k3_")):
+    if not k.startswith(("k_", "k3_", "k4_")):
         continue
     n_fetch = len(c.get("FETCH_SIZE", []))
     per_batch = n_fetch / steps if n_fetch else 0
