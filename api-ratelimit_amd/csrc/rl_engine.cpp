@@ -17,6 +17,7 @@
 
 #include "rl_common.h"
 #include "rl_hip.h"
+#include "rl_resolve.h"
 
 namespace rlhip {
 void launch_fingerprint(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint64_t*, ItemRec*,
@@ -83,10 +84,10 @@ void launch_v4_hist(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint
                     uint32_t*, uint16_t*, unsigned long long*, MRec*, rl_status*, EngineCtl*);
 void launch_v4_scan(hipStream_t, uint32_t, const uint16_t*, const unsigned long long*, unsigned long long*,
                     const uint32_t*, const HotEntry*, HotBucket3*, const TableDesc&, int, HotCand*, uint32_t*,
-                    uint16_t*, void*, EngineCtl*);
+                    uint16_t*, void*, const uint32_t*, EngineCtl*);
 void launch_v4_place(hipStream_t, const rl_batch&, const MRec*, const uint16_t*, const uint16_t*, void*,
                      const DevRule*, const unsigned long long*, HotBucket3*, int, MRec*, rl_status*, uint32_t*,
-                     Deferred*, int, EngineCtl*);
+                     Deferred*, int, uint32_t*, EngineCtl*);
 void launch_v4_group(hipStream_t, const rl_batch&, MRec*, const DevRule*, const TableDesc&, int, rl_status*,
                      uint32_t*, const HotBucket3*, const Deferred*, HotCand*, int, uint64_t, void*, uint32_t*,
                      const uint32_t*, int, EngineCtl*, EngineCtl*);
@@ -193,10 +194,42 @@ struct rl_engine {
   void* v4_scratch = nullptr;               // k4_group global scratch for a bucket too large for LDS
   uint32_t* v4_heads = nullptr;             // per-block unique-key counts (k4_group, then k4_scan)
   uint32_t v3_cur = 0;
-  bool want_cand = true;                    // copy the hot-set candidates back after this batch
+  // v4 with two batches in flight (rl_submit_pipelined): k4_hist of batch k runs on `front`
+  // while batch k-1's k4_scan/k4_place/k4_group run on `stream`. Per slot (k & 1): the
+  // tile-sorted records, bucket-start rows, hot h sums, fingerprint partials, pinned control
+  // block and candidate copies; control blocks rotate over three (k4_group of batch k clears
+  // batch k+2's); hot tables are versioned (an upload never rewrites the one in use).
+  hipStream_t front = nullptr;
+  hipEvent_t ev_front[2] = {nullptr, nullptr};  // k4_hist of the slot's batch done (on front)
+  hipEvent_t ev_done[2] = {nullptr, nullptr};   // the slot's batch done (on stream)
+  hipEvent_t ev_ready = nullptr;                // inputs of a non-pipelined submit ready (on stream)
+  hipEvent_t ev_hot = nullptr;                  // hot-set upload copy done (staging reusable)
+  MRec* v4_srt[2] = {nullptr, nullptr};
+  uint16_t* v4_tcount[2] = {nullptr, nullptr};
+  unsigned long long* v4_thsum[2] = {nullptr, nullptr};
+  uint32_t* v4_fpart[2] = {nullptr, nullptr};
+  EngineCtl* v4_ctl[3] = {nullptr, nullptr, nullptr};
+  uint32_t* d_poison = nullptr;                 // set by k4_place of a refused batch, read by k4_scan
+  HotEntry* d_hot_buf[2] = {nullptr, nullptr};  // d_hot = d_hot_buf[hot_ver]
+  int hot_ver = 0;
+  HotEntry* h_hot_stage = nullptr;              // pinned upload staging
+  EngineCtl* h_ctl_s[2] = {nullptr, nullptr};
+  HotCand* h_cand_s[2] = {nullptr, nullptr};
+  uint64_t sub_seq = 0;                         // batches submitted (slot = seq & 1, control block = seq % 3)
+  bool inputs_ready = false;                    // this submit's inputs are complete (pipelined submit)
+  bool want_cand = true;                        // copy the hot-set candidates back after the next batch
   uint8_t* zero_block = nullptr;  // ctl | hist | lookbacks (zeroed per batch)
   size_t zero_cap = 0;
   EngineCtl* h_ctl = nullptr;     // pinned copy of the control block
+
+  // descriptor tree (rl_load_tree / rl_resolve)
+  TreeNodeDev* d_tree_nodes = nullptr;
+  uint32_t* d_tree_slots = nullptr;
+  uint8_t* d_tree_names = nullptr;
+  TreeDesc2 tree{};
+  bool has_tree = false;
+  uint8_t* d_res = nullptr;  // rl_resolve staging (grown on demand)
+  size_t res_cap = 0;
 
   // multi-GPU router scratch (allocated on first use)
   RRec* r_tmp = nullptr;           // origin: routed records in descriptor order
@@ -207,7 +240,23 @@ struct rl_engine {
   uint32_t* r_thr = nullptr;       // owner: ThrottleMillis per routed record
   RReply* pend_reply = nullptr;    // owner: reply destination of the in-flight routed batch
 
-  // in-flight batch
+  // in-flight batches: the oldest in the fields below, a second (pipelined) one in `nxt`
+  struct Flight {
+    rl_batch b{};
+    rl_status* out = nullptr;
+    uint32_t* thr = nullptr;
+    RReply* reply = nullptr;
+    uint32_t slot = 0;
+    bool want_cand = false;
+    bool settled = false;    // reruns done (by the previous batch's finish)
+    bool fell_back = false;
+    uint32_t errs = 0;
+  };
+  Flight nxt;
+  Flight cur_view;  // the oldest batch as a Flight (finish)
+  bool has_next = false;
+  uint32_t cur_slot = 0;
+  bool cur_want_cand = false;
   bool in_flight = false;
   bool host_path = false;
   rl_batch dev_batch{};            // device pointers of the in-flight batch
@@ -280,7 +329,25 @@ struct rl_engine {
     return (cfg.flags & RL_CFG_V3) ? MODE_V3 : MODE_V4;
   }
   int finish();
-  int upload_hot();
+  int settle(Flight& f);
+  void begin_submit() {
+    const uint32_t s = (uint32_t)(sub_seq & 1u);
+    h_ctl = h_ctl_s[s];
+    h_cand = h_cand_s[s];
+  }
+  // Record the submitted batch's completion point and advance the slot.
+  void end_submit(bool pipelined_second) {
+    const uint32_t s = (uint32_t)(sub_seq & 1u);
+    hipEventRecord(ev_done[s], stream);
+    if (!pipelined_second) {
+      cur_view = Flight{};
+      cur_slot = s;
+      cur_want_cand = want_cand;
+    }
+    ++sub_seq;
+    inputs_ready = false;
+  }
+  int upload_hot(hipStream_t us);
   void update_hot(uint32_t n_cand);
   int enqueue_d2h();
 };
@@ -300,36 +367,55 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   if (routed && mode == MODE_V2) mode = MODE_LSD;  // the v2 loader reads prefix bytes only
   hipError_t e;
   if (mode == MODE_V4) {
+    const uint32_t sl = (uint32_t)(sub_seq & 1u);
+    EngineCtl* c4 = v4_ctl[sub_seq % 3];
+    EngineCtl* c4n = v4_ctl[(sub_seq + 2) % 3];  // batch seq+2's control block (k4_group clears it)
     if (n == 0) {
       hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
-      hipMemsetAsync(v3_ctl[v3_cur], 0, sizeof(EngineCtl), stream);
-      e = hipMemcpyAsync(h_ctl, v3_ctl[v3_cur], sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
+      hipMemsetAsync(c4, 0, sizeof(EngineCtl), stream);
+      hipMemsetAsync(c4n, 0, sizeof(EngineCtl), stream);
+      e = hipMemcpyAsync(h_ctl, c4, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
       return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpyAsync(ctl)");
     }
+    // k4_hist runs on the front stream while the previous batch is still being decided (a
+    // pipelined submit behind an in-flight batch); otherwise, or when kernels are timed, on
+    // the engine stream
+    const bool split = !timing && in_flight;
+    hipStream_t fs = split ? front : stream;
+    if (split) {
+      hipStreamWaitEvent(front, ev_done[sl], 0);  // slot buffers and control block free (batch seq-2 done)
+      if (!inputs_ready) {                        // inputs come from work queued on the stream
+        hipEventRecord(ev_ready, stream);
+        hipStreamWaitEvent(front, ev_ready, 0);
+      }
+    }
     if (hot_dirty) {
-      int rc = upload_hot();
+      int rc = upload_hot(fs);
       if (rc) return rc;
     }
-    EngineCtl* c4 = v3_ctl[v3_cur];
-    EngineCtl* c4n = v3_ctl[v3_cur ^ 1u];
+    const HotEntry* hot_t = d_hot;
     const int lc = cfg.local_cache ? 1 : 0;
     const uint32_t ng = v4_group_blocks(n);
-    // v4 buffers: v3_arec = tile-sorted records, v3_tcount = bucket starts per tile,
+    // v4 buffers: v4_srt = tile-sorted records, v4_tcount = bucket starts per tile,
     // v3_toff (as u16) = per (tile, MSD bucket) records in earlier tiles, v3_mrec = MSD records
     // in bucket order
-    MRec* srt = reinterpret_cast<MRec*>(v3_arec);
+    MRec* srt = v4_srt[sl];
     uint16_t* toff16 = reinterpret_cast<uint16_t*>(v3_toff);
     timed(KT_V4_HIST, [&] {
-      launch_v4_hist(stream, b, d_rules, n_rules, cfg.hash_seed, d_hot, thr, fp_part, v3_tcount, v3_thsum, srt, out,
-                     c4);
+      launch_v4_hist(fs, b, d_rules, n_rules, cfg.hash_seed, hot_t, thr, v4_fpart[sl], v4_tcount[sl], v4_thsum[sl],
+                     srt, out, c4);
     });
+    if (split) {
+      hipEventRecord(ev_front[sl], front);
+      hipStreamWaitEvent(stream, ev_front[sl], 0);
+    }
     timed(KT_V4_SCAN, [&] {
-      launch_v4_scan(stream, n, v3_tcount, v3_thsum, v3_hoff, fp_part, d_hot + HOT_SLOTS, v3_hb, tab, lc, d_cand,
-                     v4_heads + ng, toff16, v4_scratch, c4);
+      launch_v4_scan(stream, n, v4_tcount[sl], v4_thsum[sl], v3_hoff, v4_fpart[sl], hot_t + HOT_SLOTS, v3_hb, tab, lc,
+                     d_cand, v4_heads + ng, toff16, v4_scratch, d_poison, c4);
     });
     timed(KT_V4_PLACE, [&] {
-      launch_v4_place(stream, b, srt, v3_tcount, toff16, v4_scratch, d_rules, v3_hoff, v3_hb, lc, v3_mrec, out, thr,
-                      v3_dfr, routed, c4);
+      launch_v4_place(stream, b, srt, v4_tcount[sl], toff16, v4_scratch, d_rules, v3_hoff, v3_hb, lc, v3_mrec, out,
+                      thr, v3_dfr, routed, d_poison, c4);
     });
     timed(KT_V4_GROUP, [&] {
       launch_v4_group(stream, b, v3_mrec, d_rules, tab, lc, out, thr, v3_hb, v3_dfr, d_cand, want_cand ? 1 : 0,
@@ -341,7 +427,6 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     if (e == hipSuccess && want_cand)
       e = hipMemcpyAsync(h_cand, d_cand, sizeof(HotCand) * CAND_MAX, hipMemcpyDeviceToHost, stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(ctl)");
-    v3_cur ^= 1u;
     return 0;
   }
   if (mode == MODE_V3) {
@@ -352,7 +437,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
       return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpyAsync(ctl)");
     }
     if (hot_dirty) {
-      int rc = upload_hot();
+      int rc = upload_hot(stream);
       if (rc) return rc;
     }
     EngineCtl* c3 = v3_ctl[v3_cur];
@@ -402,7 +487,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     // Bucketed pipeline: fingerprint + bucket histograms, per-bucket scan, stable bucket
     // scatter, LDS grouping, then the shared leader / decide kernels.
     if (hot_dirty) {
-      int rc = upload_hot();
+      int rc = upload_hot(stream);
       if (rc) return rc;
     }
     const int lc = cfg.local_cache ? 1 : 0;
@@ -513,7 +598,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
 
 // Upload the hot-key set: an open-addressing table (slot = a>>40 mod HOT_SLOTS) followed by
 // the entries in hot-index order.
-int rl_engine::upload_hot() {
+int rl_engine::upload_hot(hipStream_t us) {
   std::vector<HotEntry> t(HOT_SLOTS + HOT_MAX);
   for (auto& x : t) {
     x.a = x.b = 0;
@@ -534,14 +619,17 @@ int rl_engine::upload_hot() {
     t[s] = he;
     t[HOT_SLOTS + i] = he;
   }
-  // pinned bounce buffer: h_cand is reused (it is idle between batches)
-  static_assert(sizeof(HotCand) * CAND_MAX >= sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX), "bounce buffer");
-  hipError_t e = hipStreamSynchronize(stream);
+  // Into the version no in-flight batch reads (at most one batch is in flight here, and it
+  // uses the current version), through a pinned staging buffer whose last copy is done.
+  hipError_t e = hipEventSynchronize(ev_hot);
   if (e == hipSuccess) {
-    memcpy(h_cand, t.data(), sizeof(HotEntry) * t.size());
-    e = hipMemcpyAsync(d_hot, h_cand, sizeof(HotEntry) * t.size(), hipMemcpyHostToDevice, stream);
+    memcpy(h_hot_stage, t.data(), sizeof(HotEntry) * t.size());
+    e = hipMemcpyAsync(d_hot_buf[hot_ver ^ 1], h_hot_stage, sizeof(HotEntry) * t.size(), hipMemcpyHostToDevice, us);
   }
+  if (e == hipSuccess) e = hipEventRecord(ev_hot, us);
   if (e != hipSuccess) return hip_fail(e, "upload hot set");
+  hot_ver ^= 1;
+  d_hot = d_hot_buf[hot_ver];
   hot_dirty = false;
   st.hot_keys = hot.size();
   return 0;
@@ -608,22 +696,27 @@ void rl_engine::update_hot(uint32_t n_cand) {
   }
 }
 
-// Wait for the in-flight batch, run the full-fingerprint re-sort if needed, copy
-// host-path outputs back.
-int rl_engine::finish() {
-  hipError_t e = hipStreamSynchronize(stream);
-  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+// Wait for an in-flight batch and rerun it if the device refused it: on the LSD pipeline
+// when the bucketed pipeline could not take it, on the full fingerprint order when a sort-
+// prefix run held two fingerprints. Reruns are synchronous, so they are on the table before
+// anything submitted later.
+int rl_engine::settle(Flight& f) {
+  h_ctl = h_ctl_s[f.slot];
+  h_cand = h_cand_s[f.slot];
+  hipError_t e = timing ? hipStreamSynchronize(stream) : hipEventSynchronize(ev_done[f.slot]);
+  if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+  const bool host = &f == &cur_view && host_path;
   uint32_t errs = h_ctl->err;
-  bool fell_back = false;
   if ((errs & ERR_V2_FALLBACK) && !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME))) {
     // The bucketed pipeline refused the batch before touching the table (oversized
-    // bucket or a hot prefix with a second rule): run it on the LSD pipeline.
+    // bucket, a hot prefix with a second rule, or the batch before it was refused):
+    // run it on the LSD pipeline.
     ++st.lsd_fallbacks;
-    fell_back = true;
-    int rc = run_pipeline(dev_batch, pend_out_dev, pend_thr_dev, MODE_LSD);
+    f.fell_back = true;
+    int rc = run_pipeline(f.b, f.out, f.thr, MODE_LSD);
     if (rc) return rc;
-    if (pend_reply) launch_route_reply(stream, dev_batch.n_desc, pend_out_dev, pend_thr_dev, pend_reply);
-    if (host_path && (rc = enqueue_d2h()) != 0) return rc;
+    if (f.reply) launch_route_reply(stream, f.b.n_desc, f.out, f.thr, f.reply);
+    if (host && (rc = enqueue_d2h()) != 0) return rc;
     e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     errs = h_ctl->err;
@@ -632,15 +725,53 @@ int rl_engine::finish() {
     // A sort-prefix run held two fingerprints: nothing touched the table (k_leader and
     // k_decide return early), so re-run the batch on the full fingerprint order.
     ++st.resorts;
-    int rc = run_pipeline(dev_batch, pend_out_dev, pend_thr_dev, MODE_LSD_FULL);
+    int rc = run_pipeline(f.b, f.out, f.thr, MODE_LSD_FULL);
     if (rc) return rc;
-    if (pend_reply) launch_route_reply(stream, dev_batch.n_desc, pend_out_dev, pend_thr_dev, pend_reply);
-    if (host_path && (rc = enqueue_d2h()) != 0) return rc;
+    if (f.reply) launch_route_reply(stream, f.b.n_desc, f.out, f.thr, f.reply);
+    if (host && (rc = enqueue_d2h()) != 0) return rc;
     e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     errs = h_ctl->err;
   }
+  f.errs = errs;
+  f.settled = true;
+  return 0;
+}
+
+// Complete the oldest in-flight batch: reruns (settle), then errors, hot-set maintenance,
+// stats and the host-path copy. A refused batch poisons the batch behind it (k4_place ->
+// k4_scan), so that one is settled here too, before anything else can be submitted.
+int rl_engine::finish() {
+  cur_view.b = dev_batch;
+  cur_view.out = pend_out_dev;
+  cur_view.thr = pend_thr_dev;
+  cur_view.reply = pend_reply;
+  cur_view.slot = cur_slot;
+  cur_view.want_cand = cur_want_cand;
+  Flight& f = cur_view;
+  const bool settled_here = !f.settled;  // else the previous batch's finish reran this one
+  if (settled_here) {
+    int rc = settle(f);
+    if (rc) return rc;
+  }
+  if (settled_here && f.fell_back) {
+    hipError_t e = hipMemsetAsync(d_poison, 0, 4, stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(poison)");
+    if (has_next && !nxt.settled) {
+      int rc = settle(nxt);
+      if (rc) return rc;
+      if (nxt.fell_back) {
+        e = hipMemsetAsync(d_poison, 0, 4, stream);
+        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(poison)");
+      }
+    }
+  }
+  h_ctl = h_ctl_s[f.slot];
+  h_cand = h_cand_s[f.slot];
+  const uint32_t errs = f.errs;
   if (timing) {
+    hipError_t e = hipStreamSynchronize(stream);  // the next batch's marks too
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     for (auto& m : marks) {
       float ms = 0;
       hipEventElapsedTime(&ms, m.a, m.b);
@@ -659,7 +790,7 @@ int rl_engine::finish() {
   if (errs & ERR_NEED_RESORT) return fail(RL_EDEVICE, "full-fingerprint re-sort still found a mixed run");
   // Hot-set maintenance costs host time between batches: every batch while the set is
   // empty or after a fallback, else every 8th batch (a skewed stream's head moves slowly).
-  if (!(cfg.flags & RL_CFG_LSD_ONLY) && (want_cand || fell_back)) update_hot(h_ctl->tile_ctr[CAND_CTR][0]);
+  if (!(cfg.flags & RL_CFG_LSD_ONLY) && (f.want_cand || f.fell_back)) update_hot(h_ctl->tile_ctr[CAND_CTR][0]);
   last_unique = h_ctl->n_segments;
   last_n = dev_batch.n_desc;
   last_req = dev_batch.n_req;
@@ -773,10 +904,13 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     chk(hipMalloc(&e->bP, N * 8 + 64));
     chk(hipMalloc(&e->brec, N * sizeof(ItemRec)));
     chk(hipMalloc(&e->bbase, (NBUCKETS + 1) * 4));
-    chk(hipMalloc(&e->d_hot, sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX)));
+    for (int k = 0; k < 2; ++k) chk(hipMalloc(&e->d_hot_buf[k], sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX)));
+    e->d_hot = e->d_hot_buf[0];
+    chk(hipHostMalloc(&e->h_hot_stage, sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX), hipHostMallocDefault));
     chk(hipMalloc(&e->hbk, sizeof(HotBucket) * HOT_BUCKETS));
     chk(hipMalloc(&e->d_cand, sizeof(HotCand) * CAND_MAX));
-    chk(hipHostMalloc(&e->h_cand, sizeof(HotCand) * CAND_MAX, hipHostMallocDefault));
+    for (int k = 0; k < 2; ++k) chk(hipHostMalloc(&e->h_cand_s[k], sizeof(HotCand) * CAND_MAX, hipHostMallocDefault));
+    e->h_cand = e->h_cand_s[0];
     e->hot_dirty = true;  // upload the empty table before the first batch
   }
   {
@@ -812,11 +946,32 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
       chk(hipMalloc(&e->v3_ctl[k], sizeof(EngineCtl)));
       if (he == hipSuccess) chk(hipMemset(e->v3_ctl[k], 0, sizeof(EngineCtl)));
     }
+    // v4 slot 0 shares the v3 per-tile buffers (an engine runs one of the two pipelines)
+    e->v4_srt[0] = reinterpret_cast<MRec*>(e->v3_arec);
+    e->v4_tcount[0] = e->v3_tcount;
+    e->v4_thsum[0] = e->v3_thsum;
+    static_assert(sizeof(MRec) == sizeof(ARec), "v4 tile records reuse the ARec buffer");
+    chk(hipMalloc(&e->v4_srt[1], N * sizeof(MRec) + 64));
+    chk(hipMalloc(&e->v4_tcount[1], T3 * V3_ROW16 * 2));
+    chk(hipMalloc(&e->v4_thsum[1], T3 * HOT_BUCKETS * 8));
+    for (int k = 0; k < 2; ++k) chk(hipMalloc(&e->v4_fpart[k], T3 * FP_PART_WORDS * 4 + 64));
+    for (int k = 0; k < 3; ++k) {
+      chk(hipMalloc(&e->v4_ctl[k], sizeof(EngineCtl)));
+      if (he == hipSuccess) chk(hipMemset(e->v4_ctl[k], 0, sizeof(EngineCtl)));
+    }
+    chk(hipMalloc(&e->d_poison, 64));
+    if (he == hipSuccess) chk(hipMemset(e->d_poison, 0, 64));
   }
 
   e->zero_cap = e->zlayout((uint32_t)N, MAX_PASSES).total;
   chk(hipMalloc(&e->zero_block, e->zero_cap));
-  chk(hipHostMalloc(&e->h_ctl, sizeof(EngineCtl), hipHostMallocDefault));
+  for (int k = 0; k < 2; ++k) chk(hipHostMalloc(&e->h_ctl_s[k], sizeof(EngineCtl), hipHostMallocDefault));
+  e->h_ctl = e->h_ctl_s[0];
+  chk(hipStreamCreateWithFlags(&e->front, hipStreamNonBlocking));
+  for (hipEvent_t* ev : {&e->ev_front[0], &e->ev_front[1], &e->ev_done[0], &e->ev_done[1], &e->ev_ready, &e->ev_hot}) {
+    chk(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    if (he == hipSuccess) chk(hipEventRecord(*ev, e->stream));
+  }
   if (he == hipSuccess) chk(hipMemset(e->zero_block, 0, e->zero_cap));
   if (he == hipSuccess) chk(hipDeviceSynchronize());
   if (he != hipSuccess) {
@@ -830,7 +985,26 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
 void rl_destroy(rl_engine* e) {
   if (!e) return;
   if (e->stream) hipStreamSynchronize(e->stream);
+  if (e->front) hipStreamSynchronize(e->front);
   for (auto ev : e->ev_pool) hipEventDestroy(ev);
+  for (hipEvent_t ev : {e->ev_front[0], e->ev_front[1], e->ev_done[0], e->ev_done[1], e->ev_ready, e->ev_hot})
+    if (ev) hipEventDestroy(ev);
+  for (int k = 0; k < 2; ++k) {
+    hipFree(e->d_hot_buf[k]);
+    hipHostFree(e->h_cand_s[k]);
+    hipHostFree(e->h_ctl_s[k]);
+    hipFree(e->v4_fpart[k]);
+  }
+  hipFree(e->v4_srt[1]);
+  hipFree(e->v4_tcount[1]);
+  hipFree(e->v4_thsum[1]);
+  for (int k = 0; k < 3; ++k) hipFree(e->v4_ctl[k]);
+  hipFree(e->d_poison);
+  hipFree(e->d_tree_nodes);
+  hipFree(e->d_tree_slots);
+  hipFree(e->d_tree_names);
+  hipFree(e->d_res);
+  hipHostFree(e->h_hot_stage);
   hipFree(e->table);
   hipFree(e->d_rules);
   hipFree(e->d_in);
@@ -862,10 +1036,8 @@ void rl_destroy(rl_engine* e) {
   hipFree(e->bP);
   hipFree(e->brec);
   hipFree(e->bbase);
-  hipFree(e->d_hot);
   hipFree(e->hbk);
   hipFree(e->d_cand);
-  hipHostFree(e->h_cand);
   hipFree(e->v3_tcount);
   hipFree(e->v3_toff);
   hipFree(e->v3_thsum);
@@ -894,7 +1066,7 @@ void rl_destroy(rl_engine* e) {
   hipHostFree(e->h_route);
   hipFree(e->r_thr);
   hipFree(e->zero_block);
-  hipHostFree(e->h_ctl);
+  if (e->front) hipStreamDestroy(e->front);
   if (e->own_stream) hipStreamDestroy(e->own_stream);
   delete e;
 }
@@ -995,6 +1167,7 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
   d.req_of = reinterpret_cast<const uint32_t*>(e->d_in + o_req);
   d.now = reinterpret_cast<const int64_t*>(e->d_in + o_now);
   d.hits_addend = reinterpret_cast<const uint32_t*>(e->d_in + o_hits);
+  e->begin_submit();
   int rc = e->run_pipeline(d, e->d_out, e->d_thr, e->default_mode());
   if (rc) return rc;
   e->dev_batch = d;
@@ -1005,6 +1178,7 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
   e->pend_reply = nullptr;
   e->host_path = true;
   if ((rc = e->enqueue_d2h()) != 0) return rc;
+  e->end_submit(false);
   e->in_flight = true;
   return 0;
 }
@@ -1012,8 +1186,22 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
 int rl_wait(rl_engine* e) {
   if (!e) return RL_EINVAL;
   if (!e->in_flight) return e->fail(RL_ESTATE, "rl_wait without a batch in flight");
+  const int rc = e->finish();
   e->in_flight = false;
-  return e->finish();
+  if (e->has_next) {  // the pipelined batch becomes the oldest
+    const rl_engine::Flight& n = e->nxt;
+    e->dev_batch = n.b;
+    e->pend_out_dev = n.out;
+    e->pend_thr_dev = n.thr;
+    e->pend_reply = nullptr;
+    e->host_path = false;
+    e->cur_slot = n.slot;
+    e->cur_want_cand = n.want_cand;
+    e->cur_view = n;
+    e->has_next = false;
+    e->in_flight = true;
+  }
+  return rc;
 }
 
 int rl_submit_device(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t* d_req_throttle_ms) {
@@ -1025,6 +1213,7 @@ int rl_submit_device(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t
                    c.max_batch_req);
   if (b->reserved) return e->fail(RL_EINVAL, "rl_batch.reserved must be 0");
   if (!e->d_rules) rl_load_rules(e, nullptr, 0);
+  e->begin_submit();
   int rc = e->run_pipeline(*b, d_out, d_req_throttle_ms, e->default_mode());
   if (rc) return rc;
   e->dev_batch = *b;
@@ -1032,7 +1221,49 @@ int rl_submit_device(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t
   e->pend_thr_dev = d_req_throttle_ms;
   e->pend_reply = nullptr;
   e->host_path = false;
+  e->end_submit(false);
   e->in_flight = true;
+  return 0;
+}
+
+int rl_submit_pipelined(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t* d_req_throttle_ms) {
+  if (!e || !b) return RL_EINVAL;
+  if (e->has_next) return e->fail(RL_ESTATE, "rl_submit_pipelined with two batches in flight (call rl_wait)");
+  const rl_config& c = e->cfg;
+  if (b->n_desc > c.max_batch_desc || b->n_req > c.max_batch_req)
+    return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req)", c.max_batch_desc,
+                   c.max_batch_req);
+  if (b->reserved) return e->fail(RL_EINVAL, "rl_batch.reserved must be 0");
+  const bool second = e->in_flight;
+  if (second && e->default_mode() != MODE_V4)
+    return e->fail(RL_ESTATE, "a second batch in flight needs the v4 pipeline (call rl_wait)");
+  if (second && (e->pend_out_dev == d_out || e->pend_thr_dev == d_req_throttle_ms))
+    return e->fail(RL_EINVAL, "the two in-flight batches need distinct output buffers");
+  if (!e->d_rules) rl_load_rules(e, nullptr, 0);
+  e->begin_submit();
+  e->inputs_ready = true;
+  const uint32_t slot = (uint32_t)(e->sub_seq & 1u);
+  const bool want = e->want_cand;
+  int rc = e->run_pipeline(*b, d_out, d_req_throttle_ms, e->default_mode());
+  if (rc) return rc;
+  if (second) {
+    rl_engine::Flight& n = e->nxt;
+    n = rl_engine::Flight{};
+    n.b = *b;
+    n.out = d_out;
+    n.thr = d_req_throttle_ms;
+    n.slot = slot;
+    n.want_cand = want;
+    e->has_next = true;
+  } else {
+    e->dev_batch = *b;
+    e->pend_out_dev = d_out;
+    e->pend_thr_dev = d_req_throttle_ms;
+    e->pend_reply = nullptr;
+    e->host_path = false;
+    e->in_flight = true;
+  }
+  e->end_submit(second);
   return 0;
 }
 
@@ -1102,6 +1333,7 @@ int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_re
   b.n_req = n;  // every record has its own ThrottleMillis slot
   b.reserved = RL_BATCH_ROUTED;
   b.prefix_blob = reinterpret_cast<const uint8_t*>(d_records);
+  e->begin_submit();
   int rc = e->run_pipeline(b, e->d_out, e->r_thr, e->default_mode());
   if (rc) return rc;
   launch_route_reply(e->stream, n, e->d_out, e->r_thr, reinterpret_cast<RReply*>(d_reply));
@@ -1110,6 +1342,7 @@ int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_re
   e->pend_thr_dev = e->r_thr;
   e->pend_reply = reinterpret_cast<RReply*>(d_reply);
   e->host_path = false;
+  e->end_submit(false);
   e->in_flight = true;
   return 0;
 }
@@ -1148,6 +1381,7 @@ int rl_get_stats(rl_engine* e, rl_engine_stats* s) {
 
 int rl_set_timing(rl_engine* e, int on) {
   if (!e) return RL_EINVAL;
+  if (e->in_flight) return e->fail(RL_ESTATE, "rl_set_timing while a batch is in flight");
   e->timing = on != 0;
   for (int k = 0; k < KT_COUNT; ++k) { e->kt_ms[k] = 0; e->kt_n[k] = 0; }
   return 0;
@@ -1173,6 +1407,117 @@ int rl_last_batch_info(rl_engine* e, uint64_t* unique_keys, uint64_t* n_desc, ui
   if (n_req) *n_req = e->last_req;
   if (blob_bytes) *blob_bytes = e->last_blob;
   return 0;
+}
+
+}  // extern "C"
+
+extern "C" {
+
+int rl_load_tree(rl_engine* e, const rl_tree_node* nodes, uint32_t n_nodes, const uint8_t* names, uint32_t names_len) {
+  if (!e) return RL_EINVAL;
+  if (e->in_flight) return e->fail(RL_ESTATE, "rl_load_tree while a batch is in flight");
+  if ((n_nodes && !nodes) || (names_len && !names)) return e->fail(RL_EINVAL, "null tree array");
+  std::vector<TreeNodeDev> hn;
+  std::vector<uint32_t> hs;
+  std::string err;
+  int rc = build_tree(nodes, n_nodes, names, names_len, hn, hs, err);
+  if (rc) return e->fail(rc, "%s", err.c_str());
+  hipError_t he = hipStreamSynchronize(e->stream);  // resolutions queued on the old tree finish first
+  hipFree(e->d_tree_nodes);
+  hipFree(e->d_tree_slots);
+  hipFree(e->d_tree_names);
+  e->d_tree_nodes = nullptr;
+  e->d_tree_slots = nullptr;
+  e->d_tree_names = nullptr;
+  e->has_tree = false;
+  if (he == hipSuccess) he = hipMalloc(&e->d_tree_nodes, std::max<size_t>(1, hn.size()) * sizeof(TreeNodeDev));
+  if (he == hipSuccess) he = hipMalloc(&e->d_tree_slots, hs.size() * 4);
+  if (he == hipSuccess) he = hipMalloc(&e->d_tree_names, std::max<size_t>(16, names_len));
+  if (he == hipSuccess && !hn.empty())
+    he = hipMemcpy(e->d_tree_nodes, hn.data(), hn.size() * sizeof(TreeNodeDev), hipMemcpyHostToDevice);
+  if (he == hipSuccess) he = hipMemcpy(e->d_tree_slots, hs.data(), hs.size() * 4, hipMemcpyHostToDevice);
+  if (he == hipSuccess && names_len) he = hipMemcpy(e->d_tree_names, names, names_len, hipMemcpyHostToDevice);
+  if (he != hipSuccess) return e->hip_fail(he, "rl_load_tree");
+  e->tree.nodes = e->d_tree_nodes;
+  e->tree.slots = e->d_tree_slots;
+  e->tree.names = e->d_tree_names;
+  e->tree.mask = (uint32_t)hs.size() - 1u;
+  e->has_tree = true;
+  return 0;
+}
+
+static ResolveIn resolve_in(const rl_resolve_batch* b) {
+  ResolveIn in;
+  in.n_desc = b->n_desc;
+  in.bytes = b->bytes;
+  in.domain = b->domain;
+  in.entry_first = b->entry_first;
+  in.entry = b->entry;
+  in.override_rule = b->override_rule;
+  return in;
+}
+
+int rl_resolve_device(rl_engine* e, const rl_resolve_batch* b, uint32_t* d_rule_out) {
+  if (!e || !b) return RL_EINVAL;
+  if (!e->has_tree) return e->fail(RL_ESTATE, "rl_resolve without a tree (rl_load_tree)");
+  if (b->reserved) return e->fail(RL_EINVAL, "rl_resolve_batch.reserved must be 0");
+  if (!b->n_desc) return 0;
+  if (!b->domain || !b->entry_first || !d_rule_out || (b->n_entries && (!b->entry || !b->bytes)))
+    return e->fail(RL_EINVAL, "null resolve array");
+  launch_resolve(e->stream, resolve_in(b), e->tree, d_rule_out);
+  hipError_t he = hipGetLastError();
+  return he == hipSuccess ? 0 : e->hip_fail(he, "k_resolve launch");
+}
+
+int rl_resolve(rl_engine* e, const rl_resolve_batch* b, uint32_t* rule_out) {
+  if (!e || !b) return RL_EINVAL;
+  if (e->in_flight) return e->fail(RL_ESTATE, "rl_resolve while a batch is in flight");
+  if (!e->has_tree) return e->fail(RL_ESTATE, "rl_resolve without a tree (rl_load_tree)");
+  if (b->reserved) return e->fail(RL_EINVAL, "rl_resolve_batch.reserved must be 0");
+  const uint32_t n = b->n_desc, ne = b->n_entries;
+  if (!n) return 0;
+  if (!b->domain || !b->entry_first || !rule_out || (ne && (!b->entry || !b->bytes)))
+    return e->fail(RL_EINVAL, "null resolve array");
+  // Host-side bounds checks: every string inside bytes, entry ranges monotone and inside n_entries.
+  if (b->entry_first[0] != 0 || b->entry_first[n] != ne) return e->fail(RL_EINVAL, "entry_first must span [0, n_entries]");
+  for (uint32_t i = 0; i < n; ++i) {
+    if (b->entry_first[i + 1] < b->entry_first[i]) return e->fail(RL_EINVAL, "entry_first not monotone at %u", i);
+    if ((uint64_t)b->domain[2 * i] + b->domain[2 * i + 1] > b->bytes_len)
+      return e->fail(RL_EINVAL, "domain string outside bytes at %u", i);
+  }
+  for (uint32_t k = 0; k < ne; ++k)
+    if ((uint64_t)b->entry[4 * k] + b->entry[4 * k + 1] > b->bytes_len ||
+        (uint64_t)b->entry[4 * k + 2] + b->entry[4 * k + 3] > b->bytes_len)
+      return e->fail(RL_EINVAL, "entry string outside bytes at %u", k);
+  const size_t o_dom = align_up(b->bytes_len + 16, 256), o_ef = o_dom + align_up((size_t)n * 8, 256),
+               o_ent = o_ef + align_up(((size_t)n + 1) * 4, 256), o_ov = o_ent + align_up((size_t)ne * 16, 256),
+               o_out = o_ov + align_up((size_t)n * 4, 256), total = o_out + align_up((size_t)n * 4, 256);
+  hipError_t he = hipSuccess;
+  if (total > e->res_cap) {
+    hipFree(e->d_res);
+    e->d_res = nullptr;
+    he = hipMalloc(&e->d_res, total);
+    if (he != hipSuccess) { e->res_cap = 0; return e->hip_fail(he, "rl_resolve staging"); }
+    e->res_cap = total;
+  }
+  uint8_t* d = e->d_res;
+  struct Cp { size_t o; const void* src; size_t n; } cps[] = {
+      {0, b->bytes, b->bytes_len}, {o_dom, b->domain, (size_t)n * 8}, {o_ef, b->entry_first, ((size_t)n + 1) * 4},
+      {o_ent, b->entry, (size_t)ne * 16}, {o_ov, b->override_rule, b->override_rule ? (size_t)n * 4 : 0}};
+  for (auto& c : cps)
+    if (c.n && he == hipSuccess) he = hipMemcpyAsync(d + c.o, c.src, c.n, hipMemcpyHostToDevice, e->stream);
+  if (he != hipSuccess) return e->hip_fail(he, "rl_resolve H2D");
+  rl_resolve_batch db = *b;
+  db.bytes = d;
+  db.domain = reinterpret_cast<const uint32_t*>(d + o_dom);
+  db.entry_first = reinterpret_cast<const uint32_t*>(d + o_ef);
+  db.entry = reinterpret_cast<const uint32_t*>(d + o_ent);
+  db.override_rule = b->override_rule ? reinterpret_cast<const uint32_t*>(d + o_ov) : nullptr;
+  int rc = rl_resolve_device(e, &db, reinterpret_cast<uint32_t*>(d + o_out));
+  if (rc) return rc;
+  he = hipMemcpyAsync(rule_out, d + o_out, (size_t)n * 4, hipMemcpyDeviceToHost, e->stream);
+  if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
+  return he == hipSuccess ? 0 : e->hip_fail(he, "rl_resolve D2H");
 }
 
 }  // extern "C"

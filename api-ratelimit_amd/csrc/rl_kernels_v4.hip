@@ -324,12 +324,19 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
                                                    const HotEntry* __restrict__ hot_list, HotBucket3* __restrict__ hb,
                                                    TableDesc tab, int local_cache, HotCand* __restrict__ cand,
                                                    uint32_t* __restrict__ heads_out, uint16_t* __restrict__ toff,
-                                                   uint32_t* __restrict__ ranges, EngineCtl* ctl) {
+                                                   uint32_t* __restrict__ ranges, const uint32_t* __restrict__ poison,
+                                                   EngineCtl* ctl) {
   __shared__ uint32_t s_f[FP_PART_WORDS];
   __shared__ uint32_t s_tot[64];
   __shared__ uint32_t s_pc[SCAN_W][64];
   __shared__ unsigned long long s_ph[SCAN_W][64];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // A batch submitted behind a refused one (two batches in flight) is refused too, before
+  // anything touches the table: the engine reruns both, in order (rl_engine::settle).
+  if (*poison) {
+    if (blockIdx.x == 0 && tid == 0) atomicOr(&ctl->err, ERR_V2_FALLBACK);
+    return;
+  }
   if (tid < FP_PART_WORDS) s_f[tid] = 0;
   __syncthreads();
   // Fold the per-tile partials (every block): generation range per region, nil count.
@@ -800,7 +807,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
                                                HotBucket3* __restrict__ hb, int local_cache,
                                                MRec* __restrict__ mrec, rl_status* __restrict__ out,
                                                uint32_t* __restrict__ req_thr, Deferred* __restrict__ dfr, int routed,
-                                               EngineCtl* ctl) {
+                                               uint32_t* __restrict__ poison, EngineCtl* ctl) {
   __shared__ uint16_t s_row[ROW];
   __shared__ uint16_t s_toff[MSD_BUCKETS];
   __shared__ uint32_t s_gpre[MSD_GROUPS];
@@ -823,6 +830,8 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
   if (local_cache)
     for (int b = tid; b < HOT_BUCKETS; b += NT) s_rstar[b] = 0xFFFFFFFFu;
   __syncthreads();
+  // A batch the engine will rerun on the LSD pipeline poisons the next batch's k4_scan.
+  if (t == 0 && tid == 0 && (s_err & ERR_V2_FALLBACK) && !(s_err & (ERR_BAD_INPUT | ERR_BAD_TIME))) *poison = 1u;
   // Nothing is decided and nothing touches the table unless the whole batch is valid.
   if (s_err) return;
   // Hot keys without a freeze in this batch: the final counter is base + total (block 0).
@@ -1171,16 +1180,17 @@ void launch_v4_hist(hipStream_t st, const rl_batch& b, const DevRule* rules, uin
 void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const unsigned long long* thsum,
                     unsigned long long* hoff, const uint32_t* fpart, const HotEntry* hot_list, HotBucket3* hb,
                     const TableDesc& tab, int local_cache, HotCand* cand, uint32_t* heads_out, uint16_t* toff,
-                    void* scratch, EngineCtl* ctl) {
+                    void* scratch, const uint32_t* poison, EngineCtl* ctl) {
   hipLaunchKernelGGL(v4::k4_scan, dim3(v4_scan_blocks()), dim3(v4::SCAN_NT), 0, st, tstart, thsum, v4_tiles(n), hoff,
-                     fpart, hot_list, hb, tab, local_cache, cand, heads_out, toff, v4_ranges(scratch), ctl);
+                     fpart, hot_list, hb, tab, local_cache, cand, heads_out, toff, v4_ranges(scratch), poison, ctl);
 }
 void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart, const uint16_t* toff,
                      void* scratch, const DevRule* rules, const unsigned long long* hoff, HotBucket3* hb,
                      int local_cache, MRec* mrec, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
-                     EngineCtl* ctl) {
+                     uint32_t* poison, EngineCtl* ctl) {
   hipLaunchKernelGGL(v4::k4_place, dim3(v4_tiles(b.n_desc)), dim3(V3_THREADS), 0, st, make_dev_batch(b), srec, tstart,
-                     toff, v4_ranges(scratch), rules, hoff, hb, local_cache, mrec, out, req_thr, dfr, routed, ctl);
+                     toff, v4_ranges(scratch), rules, hoff, hb, local_cache, mrec, out, req_thr, dfr, routed, poison,
+                     ctl);
 }
 void launch_v4_group(hipStream_t st, const rl_batch& b, MRec* mrec, const DevRule* rules, const TableDesc& tab,
                      int local_cache, rl_status* out, uint32_t* req_thr, const HotBucket3* hb, const Deferred* dfr,

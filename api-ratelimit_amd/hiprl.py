@@ -57,6 +57,19 @@ class RlBatch(C.Structure):
                 ("req_of", C.c_void_p), ("now", C.c_void_p), ("hits_addend", C.c_void_p)]
 
 
+class RlTreeNode(C.Structure):
+    _fields_ = [("parent", C.c_uint32), ("name_off", C.c_uint32), ("name_len", C.c_uint32), ("rule", C.c_uint32)]
+
+
+class RlResolveBatch(C.Structure):
+    _fields_ = [("n_desc", C.c_uint32), ("n_entries", C.c_uint32), ("bytes_len", C.c_uint32), ("reserved", C.c_uint32),
+                ("bytes", C.c_void_p), ("domain", C.c_void_p), ("entry_first", C.c_void_p), ("entry", C.c_void_p),
+                ("override_rule", C.c_void_p)]
+
+
+TREE_ROOT = 0xFFFFFFFF
+
+
 class RlEngineStats(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("descriptors", C.c_uint64), ("resorts", C.c_uint64),
                 ("live_slots_hint", C.c_uint64), ("lsd_fallbacks", C.c_uint64), ("hot_keys", C.c_uint64)]
@@ -72,6 +85,7 @@ ABI = [
     ("rl_submit", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
     ("rl_wait", [C.c_void_p], C.c_int),
     ("rl_submit_device", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
+    ("rl_submit_pipelined", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
     ("rl_stream", [C.c_void_p], C.c_void_p),
     ("rl_reset", [C.c_void_p], C.c_int),
     ("rl_get_stats", [C.c_void_p, C.POINTER(RlEngineStats)], C.c_int),
@@ -85,6 +99,9 @@ ABI = [
                        C.POINTER(C.c_uint32)], C.c_int),
     ("rl_submit_routed", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p], C.c_int),
     ("rl_route_unpack", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
+    ("rl_load_tree", [C.c_void_p, C.POINTER(RlTreeNode), C.c_uint32, C.c_void_p, C.c_uint32], C.c_int),
+    ("rl_resolve", [C.c_void_p, C.POINTER(RlResolveBatch), C.c_void_p], C.c_int),
+    ("rl_resolve_device", [C.c_void_p, C.POINTER(RlResolveBatch), C.c_void_p], C.c_int),
 ]
 
 # multi-GPU router record sizes (include/rl_hip.h RL_ROUTE_*)
@@ -271,8 +288,30 @@ class Engine:
         s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
         self._check(self.lib.rl_submit_device(self.h, C.byref(s), out_ptr, thr_ptr), "rl_submit_device")
 
+    def submit_pipelined(self, n_desc: int, n_req: int, blob_bytes: int, ptrs, out_ptr: int, thr_ptr: int):
+        """Device batch with complete inputs, behind at most one batch in flight (rl_submit_pipelined):
+        wait() completes the oldest. The two in-flight batches need distinct output buffers."""
+        s = RlBatch()
+        s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
+        s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        self._check(self.lib.rl_submit_pipelined(self.h, C.byref(s), out_ptr, thr_ptr), "rl_submit_pipelined")
+
     def wait(self):
         self._check(self.lib.rl_wait(self.h), "rl_wait")
+
+    def load_tree(self, nodes: np.ndarray, names: bytes):
+        """nodes: uint32 [n, 4] (parent, name_off, name_len, rule); names: the tree's map keys."""
+        nodes = np.ascontiguousarray(nodes, dtype=np.uint32).reshape(-1, 4)
+        nb = np.frombuffer(bytes(names) or b"\0", np.uint8)
+        self._check(self.lib.rl_load_tree(self.h, nodes.ctypes.data_as(C.POINTER(RlTreeNode)), nodes.shape[0],
+                                          nb.ctypes.data, len(names)), "rl_load_tree")
+
+    def resolve(self, rb) -> np.ndarray:
+        """GetLimit for every descriptor of an rl_config.ResolveBatch -> rule id per descriptor."""
+        out = np.zeros(max(1, rb.n_desc), np.uint32)
+        s = rb.struct()
+        self._check(self.lib.rl_resolve(self.h, C.byref(s), _ptr(out)), "rl_resolve")
+        return out[:rb.n_desc]
 
     def reset(self):
         self._check(self.lib.rl_reset(self.h), "rl_reset")

@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--independent", action="store_true",
                     help="N>1: unrouted replicas (each rank its own key space) instead of RCCL routing")
     ap.add_argument("--json-out", type=str, default="")
+    ap.add_argument("--serial", action="store_true",
+                    help="one batch in flight (rl_submit_device + rl_wait per step) instead of two (rl_submit_pipelined)")
     return ap.parse_args()
 
 
@@ -129,28 +131,41 @@ def main():
     eng.load_rules(rules)
 
     dev_batches = [router.DeviceBatch.from_host(hb, dev) for hb in host_batches]
-    out = torch.empty(d * 20, dtype=torch.uint8, device=dev)
-    thr = torch.empty(d, dtype=torch.int32, device=dev)
+    # two output buffers: with two batches in flight each needs its own
+    outs = [torch.empty(d * 20, dtype=torch.uint8, device=dev) for _ in range(2)]
+    thrs = [torch.empty(d, dtype=torch.int32, device=dev) for _ in range(2)]
     rtr = None
     if routed:
         rtr = router.ShardRouter(router.EngineShard(eng, rank, world, dev, d))
     torch.cuda.synchronize()
 
-    def step(db):
-        if rtr is not None:
-            rtr.step(db)
-            return
-        eng.submit_device_async(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), out.data_ptr(), thr.data_ptr())
-        eng.wait()
+    pipelined = rtr is None and not args.serial
 
-    for b in range(args.warmup):
-        step(dev_batches[b])
+    def run(b0, b1):
+        """Batches [b0, b1): one step per batch. Pipelined: batch k+1 is submitted before batch k
+        is waited for (the micro-batcher's double buffering); every batch is complete on return."""
+        for j, b in enumerate(range(b0, b1)):
+            db = dev_batches[b]
+            if rtr is not None:
+                rtr.step(db)
+                continue
+            args_ = (db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), outs[j & 1].data_ptr(), thrs[j & 1].data_ptr())
+            if pipelined:
+                eng.submit_pipelined(*args_)
+                if j:
+                    eng.wait()
+            else:
+                eng.submit_device_async(*args_)
+                eng.wait()
+        if pipelined and b1 > b0:
+            eng.wait()
+
+    run(0, args.warmup)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for b in range(args.warmup, args.warmup + args.steps):
-        step(dev_batches[b])
+    run(args.warmup, args.warmup + args.steps)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -168,7 +183,7 @@ def main():
     if not args.no_kernel_times:
         eng.set_timing(True)
         for b in range(args.warmup + args.steps, args.warmup + 2 * args.steps):
-            step(dev_batches[b])
+            run(b, b + 1)
             uniq.append(eng.last_batch_info()["unique_keys"])
         kt = eng.kernel_times()
         eng.set_timing(False)
@@ -260,7 +275,8 @@ def main():
                    "parallelism": (f"key-sharded x{world}, RCCL all-to-all routing (32-B records out, 24-B replies back)"
                                    if routed else "single shard" if world == 1
                                    else f"x{world} independent replicas (no collective)"),
-                   "pipeline": args.pipeline, "unique_keys_per_batch": int(U)},
+                   "pipeline": args.pipeline, "batches_in_flight": 2 if pipelined else 1,
+                   "unique_keys_per_batch": int(U)},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "engine": {"resorts": stats["resorts"], "lsd_fallbacks": stats["lsd_fallbacks"], "hot_keys": stats["hot_keys"],

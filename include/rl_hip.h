@@ -141,6 +141,17 @@ int rl_wait(rl_engine* e);
  * and by the benchmark. */
 int rl_submit_device(rl_engine* e, const rl_batch* device_batch, rl_status* d_out, uint32_t* d_req_throttle_ms);
 
+/* Device-memory batch whose inputs are complete when the call is made, submitted behind at
+ * most one batch still in flight (the micro-batcher's double buffering: batch k+1 is handed
+ * over before rl_wait returns batch k). The engine fingerprints and tile-sorts batch k+1 on
+ * a second stream while batch k is decided, and decides k+1 strictly after k, so the
+ * results equal two serial rl_submit_device/rl_wait rounds. rl_wait completes the oldest
+ * batch. The two in-flight batches need distinct d_out / d_req_throttle_ms buffers. A second
+ * batch in flight needs the default (v4) pipeline; otherwise RL_ESTATE. Replaces nothing in
+ * the reference: it is how the batcher overlaps the radix-style implicit pipelining of
+ * src/redis/driver_impl.go:84-89 across batches. */
+int rl_submit_pipelined(rl_engine* e, const rl_batch* device_batch, rl_status* d_out, uint32_t* d_req_throttle_ms);
+
 /* The engine's HIP stream (hipStream_t), for ordering external work against it. */
 void* rl_stream(rl_engine* e);
 
@@ -200,6 +211,48 @@ int rl_kernel_times(rl_engine* e, const char** names, double* total_ms, uint64_t
  * (segments), descriptors, requests and prefix bytes, read back from the device. */
 int rl_last_batch_info(rl_engine* e, uint64_t* unique_keys, uint64_t* n_desc, uint64_t* n_req,
                        uint64_t* blob_bytes);
+
+/* ---- Descriptor-tree resolution (GetLimit) ------------------------
+ * Replaces rateLimitConfigImpl.GetLimit (src/config/config_impl.go:274-323) per descriptor,
+ * batched on the device: it yields the rule id each descriptor of an rl_batch carries.
+ * The tree is the loaded YAML config (loadDescriptors, config_impl.go:115-165) flattened:
+ * node i has a parent (a node before it, or RL_TREE_ROOT for a domain), its map key in
+ * `names` (the domain name, or finalKey = key["_" value], config_impl.go:126-129) and the
+ * rule id of its limit (RL_NIL_RULE = no rate_limit). Stats keys (FullKey) stay on the host. */
+#define RL_TREE_ROOT 0xFFFFFFFFu
+typedef struct rl_tree_node {
+  uint32_t parent;
+  uint32_t name_off;
+  uint32_t name_len;
+  uint32_t rule;
+} rl_tree_node;
+
+/* Replace the tree. RL_EINVAL on a forward parent, an empty key, or a duplicate (parent,
+ * name) — the reference's "duplicate descriptor composite key" / "duplicate domain" panics.
+ * Not while a batch is in flight. */
+int rl_load_tree(rl_engine* e, const rl_tree_node* nodes, uint32_t n_nodes, const uint8_t* names,
+                 uint32_t names_len);
+
+/* One resolution batch. Strings are (offset, length) ranges of `bytes`. override_rule (may
+ * be NULL) holds, per descriptor, the rule id the host registered for descriptor.Limit
+ * (config_impl.go:286-296; RL_NIL_RULE = no override): it applies when the domain exists. */
+typedef struct rl_resolve_batch {
+  uint32_t n_desc;
+  uint32_t n_entries;
+  uint32_t bytes_len;
+  uint32_t reserved;            /* 0 */
+  const uint8_t* bytes;
+  const uint32_t* domain;       /* [2 n_desc]: domain (off, len) per descriptor */
+  const uint32_t* entry_first;  /* [n_desc + 1]: entries of descriptor i are [entry_first[i], entry_first[i+1]) */
+  const uint32_t* entry;        /* [4 n_entries]: key off, key len, value off, value len */
+  const uint32_t* override_rule;
+} rl_resolve_batch;
+
+/* Host memory in and out; synchronous. rule_out[n_desc]. */
+int rl_resolve(rl_engine* e, const rl_resolve_batch* batch, uint32_t* rule_out);
+/* Device memory in and out; ordered on the engine's stream (before an rl_submit_device of
+ * the same batch), asynchronous. */
+int rl_resolve_device(rl_engine* e, const rl_resolve_batch* device_batch, uint32_t* d_rule_out);
 
 #ifdef __cplusplus
 }
