@@ -193,3 +193,81 @@ def algorithmic_bytes(batch: Batch, unique_keys: int) -> int:
     d, r = batch.n_desc, batch.n_req
     prefix = int(batch.off[-1]) - int(batch.off[0])
     return prefix + 12 * d + 12 * r + 20 * d + 4 * r + 64 * unique_keys
+
+
+# ---------------------------------------------------------------------------------------
+# Config 4: nested 4-entry descriptors matched by a synthetic 4-level YAML tree
+# (GetLimit semantics, config_impl.go:274-323), resolved on the device (rl_resolve).
+# ---------------------------------------------------------------------------------------
+CONFIG4_KEYS = ("a", "b", "c", "d")
+CONFIG4_UNITS = ("second", "minute", "hour", "day")
+
+
+def config4_yaml(seed: int = 4, fan: int = 6, domain: str = "bench4") -> str:
+    """A seeded 4-level descriptor tree in the reference's YAML schema: at each level a
+    key-only default node (most of the time) and `fan` key/value nodes; limits at random
+    depths (always on level-4 defaults), some nodes whitelisted (no limit)."""
+    rng = np.random.default_rng(seed)
+    lines = [f"domain: {domain}", "descriptors:"]
+
+    def node(level: int, value, ind: str):
+        lines.append(f"{ind}- key: {CONFIG4_KEYS[level]}")
+        if value is not None:
+            lines.append(f'{ind}  value: "{value}"')
+        if (level == 3 and value is None) or rng.random() < 0.45:
+            lines.append(f"{ind}  rate_limit:")
+            lines.append(f"{ind}    unit: {CONFIG4_UNITS[int(rng.integers(0, 3))]}")
+            lines.append(f"{ind}    requests_per_unit: {int(rng.integers(1, 50))}")
+        if level < 3:
+            lines.append(f"{ind}  descriptors:")
+            children(level + 1, ind + "    ")
+
+    def children(level: int, ind: str):
+        if rng.random() < 0.85:
+            node(level, None, ind)
+        for v in range(fan):
+            if rng.random() < 0.8:
+                node(level, v, ind)
+
+    children(0, "  ")
+    return "\n".join(lines) + "\n"
+
+
+def config4_descriptors(seed: int, n: int, fan: int = 6, values: int = 1000, domain: str = "bench4"):
+    """n descriptors [(domain, [(key, value)...])]: mostly 4 entries a,b,c,d with values that
+    hit the tree's key/value nodes (< fan) or fall back to its defaults; some shorter, some
+    with a foreign key or an unknown domain."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        ne = 4 if rng.random() < 0.8 else int(rng.integers(1, 4))
+        ents = []
+        for lv in range(ne):
+            key = CONFIG4_KEYS[lv] if rng.random() < 0.97 else "x"
+            v = int(rng.integers(0, fan)) if rng.random() < 0.5 else int(rng.integers(0, values))
+            ents.append((key, str(v)))
+        dom = domain if rng.random() < 0.97 else "other"
+        out.append((dom, ents))
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# Config 5: a sustained stream over simulated seconds (window rollover / expiry, variable
+# hits_addend h ~ U{1..8}, near-limit ratio 0.8), mixed SECOND / MINUTE / HOUR rules.
+# ---------------------------------------------------------------------------------------
+CONFIG5_RULES = [(20, SECOND), (400, MINUTE), (9000, HOUR)]
+
+
+def config5_batch(b: int, d: int, N: int, batches_per_s: int = 1, s: float = 1.1, seed: int = 5,
+                  t0: int = 1_700_000_000 - 37) -> Batch:
+    """Batch b of config 5: Zipf(1.1) keys over N, rule by rank % 3, 1 descriptor per
+    request, h ~ U{1..8} per request, now = t0 + b // batches_per_s (t0 is chosen so the
+    stream crosses minute and hour boundaries early)."""
+    rank = Zipf(N, s).sample(seed, b, d) - 1
+    key = permute(rank, N)
+    blob, off = prefix_blob([b"c5_k_", key, b"_"])
+    u = splitmix64(np.uint64(seed) * np.uint64(1 << 40) + np.uint64(1 << 32) + np.uint64(b) * np.uint64(1 << 24)
+                   + np.arange(d, dtype=np.uint64))
+    h = (u % np.uint64(8) + np.uint64(1)).astype(np.uint32)
+    return Batch(blob, off, (rank % 3).astype(np.uint32), np.arange(d, dtype=np.uint32),
+                 np.full(d, t0 + b // batches_per_s, np.int64), h)
