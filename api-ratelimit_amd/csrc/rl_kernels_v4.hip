@@ -314,8 +314,34 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
 // ---------------------------------------------------------------------------
 constexpr int SCAN_NT = 1024;
 constexpr int SCAN_W = SCAN_NT / 64;
-constexpr int SCAN_U = 16;  // column loads in flight per lane
+constexpr int SCAN_U = 16;  // column loads in flight per lane (columns longer than SCAN_Q)
+constexpr int SCAN_Q = 32;  // column entries per lane kept in registers
 static_assert(HOT_BUCKETS % 64 == 0 && V3_SCAN_BUCKETS % 64 == 0, "bucket blocks");
+static_assert(T < 65536 && SCAN_Q % 2 == 0, "per-tile counts pack in u16 pairs");
+
+// Counts of bucket b (= this lane's) in tiles [tb, tb + SCAN_Q) ∩ [tb, te): each lane loads
+// its bucket's start and takes the next bucket's start from the next lane; lane 63's next
+// start is the wave-uniform entry 64 of the block's row segment.
+RL_DEV void column_counts(const uint16_t* __restrict__ tstart, uint32_t b, uint32_t tb, uint32_t te,
+                          uint32_t (&cq)[SCAN_Q]) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t b0 = blockIdx.x * 64;
+  tb = __builtin_amdgcn_readfirstlane(tb);  // wave-uniform: the row-end loads are scalar
+  te = __builtin_amdgcn_readfirstlane(te);
+  uint32_t e[SCAN_Q];
+#pragma unroll
+  for (int u = 0; u < SCAN_Q; ++u) {
+    const uint16_t* row = tstart + (size_t)(tb + u) * ROW;
+    const bool v = tb + u < te;
+    cq[u] = v ? (uint32_t)row[b] : 0u;
+    e[u] = v ? (uint32_t)row[b0 + 64] : 0u;
+  }
+#pragma unroll
+  for (int u = 0; u < SCAN_Q; ++u) {
+    const uint32_t nx = __shfl_down(cq[u], 1, 64);
+    cq[u] = (lane < 63 ? nx : e[u]) - cq[u];
+  }
+}
 
 __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ tstart,
                                                    const unsigned long long* __restrict__ thsum, uint32_t ntiles,
@@ -382,19 +408,33 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
   const uint32_t tb = min(ntiles, wave * Q), te = min(ntiles, tb + Q);
   uint32_t c = 0;
   unsigned long long hs = 0;
-  for (uint32_t t = tb; t < te; t += SCAN_U) {
-    uint32_t cv[SCAN_U];
-    unsigned long long hv[SCAN_U];
+  // MSD blocks with up to SCAN_Q tiles per wave (batches up to SCAN_W * SCAN_Q tiles, 1M
+  // descriptors at 2048 per tile) load the column once, all loads in flight together, and
+  // keep the counts in registers for the prefix pass below.
+  const bool in_regs = !hotb && Q <= (uint32_t)SCAN_Q;  // block-uniform
+  uint32_t cpk[SCAN_Q / 2];  // counts (<= T each) packed in u16 pairs
+  if (in_regs) {
+    uint32_t cq[SCAN_Q];
+    column_counts(tstart, b, tb, te, cq);
 #pragma unroll
-    for (int u = 0; u < SCAN_U; ++u) {
-      const uint16_t* row = tstart + (size_t)(t + u) * ROW + b;
-      cv[u] = t + u < te ? (uint32_t)row[1] - (uint32_t)row[0] : 0u;
-      hv[u] = (hotb && t + u < te) ? thsum[(size_t)(t + u) * HOT_BUCKETS + b] : 0ull;
-    }
+    for (int u = 0; u < SCAN_Q; ++u) c += cq[u];
 #pragma unroll
-    for (int u = 0; u < SCAN_U; ++u) {
-      c += cv[u];
-      hs += hv[u];
+    for (int u = 0; u < SCAN_Q / 2; ++u) cpk[u] = cq[2 * u] | (cq[2 * u + 1] << 16);
+  } else {
+    for (uint32_t t = tb; t < te; t += SCAN_U) {
+      uint32_t cv[SCAN_U];
+      unsigned long long hv[SCAN_U];
+#pragma unroll
+      for (int u = 0; u < SCAN_U; ++u) {
+        const uint16_t* row = tstart + (size_t)(t + u) * ROW + b;
+        cv[u] = t + u < te ? (uint32_t)row[1] - (uint32_t)row[0] : 0u;
+        hv[u] = (hotb && t + u < te) ? thsum[(size_t)(t + u) * HOT_BUCKETS + b] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < SCAN_U; ++u) {
+        c += cv[u];
+        hs += hv[u];
+      }
     }
   }
   s_pc[wave][lane] = c;
@@ -418,7 +458,14 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     // at most BUCKET_CAP records on this path; a larger one sends the batch to the LSD pipeline
     // before anything touches the table)
     const uint32_t mb = b - HOT_BUCKETS;
-    for (uint32_t t = tb; t < te; t += SCAN_U) {
+    if (in_regs) {
+#pragma unroll
+      for (int u = 0; u < SCAN_Q; ++u) {
+        if (tb + u < te) toff[(size_t)(tb + u) * MSD_BUCKETS + mb] = (uint16_t)crun;
+        crun += (cpk[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
+      }
+    }
+    for (uint32_t t = in_regs ? te : tb; t < te; t += SCAN_U) {
       uint32_t cv[SCAN_U];
 #pragma unroll
       for (int u = 0; u < SCAN_U; ++u) {

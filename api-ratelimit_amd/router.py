@@ -75,15 +75,19 @@ class DeviceBatch:
 
 
 class EngineShard:
-    """The product shard: one hiprl.Engine on this rank's GPU, ordered on torch's current
-    stream (RCCL collectives synchronise with it, so no host waits are needed between steps
-    beyond the count exchange and the owner's batch)."""
+    """The product shard: one hiprl.Engine on this rank's GPU, on a stream of its own that is
+    ordered against the caller's current stream by device-side waits in both directions around
+    every call (RCCL collectives run on the caller's stream, so no host waits are needed between
+    steps beyond the count exchange and the owner's batch). A dedicated stream, not the
+    caller's: torch's default stream is the HIP null stream, which has no handle to pass over
+    the C ABI (NULL there means the engine's own, non-blocking stream)."""
 
     def __init__(self, engine: "hiprl.Engine", rank: int, world: int, device, max_desc: int):
         if world > hiprl.ROUTE_MAX_SHARDS:
             raise ValueError(f"at most {hiprl.ROUTE_MAX_SHARDS} shards")
         self.eng, self.rank, self.world, self.device = engine, rank, world, device
-        self.eng.set_stream(torch.cuda.current_stream(device).cuda_stream)
+        self.stream = torch.cuda.Stream(device)
+        self.eng.set_stream(self.stream.cuda_stream)
         self.send = torch.empty(max_desc * REC, dtype=torch.uint8, device=device)
         self.perm = torch.empty(max(1, max_desc), dtype=torch.int32, device=device)
         self.counts = torch.empty(world, dtype=torch.int32, device=device)
@@ -91,22 +95,34 @@ class EngineShard:
     def empty(self, nbytes: int) -> torch.Tensor:
         return torch.empty(nbytes, dtype=torch.uint8, device=self.device)
 
+    def _enter(self):
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))  # inputs written by the caller
+
+    def _leave(self):
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)  # outputs used by the caller
+
     def pack(self, b: DeviceBatch):
+        self._enter()
         counts = self.eng.route_pack(b.n_desc, b.n_req, b.blob_bytes(), b.ptrs(), self.rank, self.world,
                                      self.send.data_ptr(), self.counts.data_ptr(), self.perm.data_ptr())
+        self._leave()
         return self.send[:sum(counts) * REC], self.counts, counts, self.perm[:b.n_desc]
 
     def decide(self, recv: torch.Tensor, n: int) -> torch.Tensor:
         reply = self.empty(n * REP)
+        self._enter()
         self.eng.submit_routed_async(recv.data_ptr() if n else 0, n, reply.data_ptr() if n else 0)
         self.eng.wait()
+        self._leave()
         return reply
 
     def unpack(self, b: DeviceBatch, perm: torch.Tensor, back: torch.Tensor):
         out = self.empty(b.n_desc * STATUS_BYTES)
         thr = torch.empty(b.n_req, dtype=torch.int32, device=self.device)
+        self._enter()
         self.eng.route_unpack(b.n_desc, b.n_req, b.req_of.data_ptr(), perm.data_ptr(),
                               back.data_ptr() if back.numel() else 0, out.data_ptr(), thr.data_ptr())
+        self._leave()
         return out, thr
 
 
