@@ -1,10 +1,11 @@
-// rl_kernels_v4.hip — the default decision pipeline: three launches per batch.
+// rl_kernels_v4.hip — the default decision pipeline: four launches per batch.
 //
 // Same contract and outputs as the LSD pipeline (rl_kernels.hip) and v3. Compared with v3
-// the records are written ONCE, already grouped: each tile writes its descriptors sorted by
-// bucket, and the group kernel gathers a bucket's runs straight from every tile (the row of
-// bucket starts of each tile says where), so there is no bucket-order scatter pass, no
-// bucket-base pass and no tail launch.
+// each tile writes its descriptors ONCE, already sorted by bucket, and a row of bucket starts
+// per tile; the MSD records then move once more, from the tile-sorted runs to bucket order
+// (k4_place), and there is no bucket-base pass and no tail launch. k4_hist needs nothing
+// from the table, so with two batches in flight it runs for batch k+1 on a second stream
+// while batch k is decided (rl_engine.cpp, rl_submit_pipelined).
 //
 //   k4_hist    per 2048-descriptor tile: fingerprint (fixed_cache_impl.go:43-53 via
 //              cache_key.go:57-68), hot-set lookup, bucket; stable LDS sort of the tile by
@@ -12,17 +13,18 @@
 //              hot record carries its in-tile INCRBY prefix), the row of bucket starts, the
 //              hot buckets' h sums; nil-limit descriptors decided (base_limiter.go:72-75)
 //   k4_scan    per hot bucket: exclusive scan of the h sums over tiles, table claim and the
-//              counter before the batch; per MSD bucket: the batch total (size check), and
-//              per group of 64 MSD buckets the k4_group ranges (whole buckets packed up to the
-//              LDS stage) — all before any table write, so a refused batch leaves the table
-//              untouched
-//   k4_group   block j: (H) hot descriptors of half j&1 of tile j>>1, decided in place:
-//              post-value = base + tile prefix + in-tile prefix (local-cache freeze by request);
-//              (M) MSD range j: runs gathered from every tile into LDS (tile-major =
-//              arrival order inside a key), grouped by full fingerprint, segmented INCRBY
-//              prefix, one leader per key (table probe/claim, serial-order INCRBY, local-cache
-//              freeze), decisions. The last block to finish decides the deferred hot
-//              descriptors, counts U, fills hot-set candidates and clears the next control block.
+//              counter before the batch; per MSD bucket: the records in earlier tiles, the
+//              batch total (size check), and per group of 64 MSD buckets the k4_group ranges
+//              (whole buckets packed up to the LDS stage) — all before any table write, so a
+//              refused batch leaves the table untouched
+//   k4_place   per tile: hot descriptors decided in place (post-value = base + tile prefix +
+//              in-tile prefix; local-cache freezes of requests that straddle tiles deferred);
+//              MSD records scattered from the tile's runs to their bucket position
+//   k4_group   per MSD range: records into LDS (bucket order = arrival order inside a key),
+//              grouped by full fingerprint, segmented INCRBY prefix, one leader per key
+//              (table probe/claim, serial-order INCRBY, local-cache freeze), decisions. The
+//              last block to finish decides the deferred hot descriptors, counts U, fills
+//              hot-set candidates and clears the control block of batch k+2.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
