@@ -121,6 +121,12 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 }  // namespace
 
+// Batches in flight at once (rl_submit_pipelined): the host-side per-batch state (pinned
+// control-block and candidate copies, completion events, hot-table versions) has one slot
+// per batch in flight; device buffers of k4_hist have two slots, because k4_hist of batch k
+// waits for batch k-2 to finish on the GPU whatever the host has submitted.
+constexpr int HSLOTS = RL_MAX_IN_FLIGHT;
+
 struct rl_engine {
   rl_config cfg{};
   int lo_bit = 16, npasses = 6;
@@ -201,7 +207,7 @@ struct rl_engine {
   // batch k+2's); hot tables are versioned (an upload never rewrites the one in use).
   hipStream_t front = nullptr;
   hipEvent_t ev_front[2] = {nullptr, nullptr};  // k4_hist of the slot's batch done (on front)
-  hipEvent_t ev_done[2] = {nullptr, nullptr};   // the slot's batch done (on stream)
+  hipEvent_t ev_done[HSLOTS] = {};              // the host slot's batch done (on stream)
   hipEvent_t ev_ready = nullptr;                // inputs of a non-pipelined submit ready (on stream)
   hipEvent_t ev_hot = nullptr;                  // hot-set upload copy done (staging reusable)
   MRec* v4_srt[2] = {nullptr, nullptr};
@@ -210,11 +216,11 @@ struct rl_engine {
   uint32_t* v4_fpart[2] = {nullptr, nullptr};
   EngineCtl* v4_ctl[3] = {nullptr, nullptr, nullptr};
   uint32_t* d_poison = nullptr;                 // set by k4_place of a refused batch, read by k4_scan
-  HotEntry* d_hot_buf[2] = {nullptr, nullptr};  // d_hot = d_hot_buf[hot_ver]
+  HotEntry* d_hot_buf[HSLOTS] = {};             // d_hot = d_hot_buf[hot_ver]; one per batch in flight
   int hot_ver = 0;
   HotEntry* h_hot_stage = nullptr;              // pinned upload staging
-  EngineCtl* h_ctl_s[2] = {nullptr, nullptr};
-  HotCand* h_cand_s[2] = {nullptr, nullptr};
+  EngineCtl* h_ctl_s[HSLOTS] = {};
+  HotCand* h_cand_s[HSLOTS] = {};
   uint64_t sub_seq = 0;                         // batches submitted (slot = seq & 1, control block = seq % 3)
   bool inputs_ready = false;                    // this submit's inputs are complete (pipelined submit)
   bool want_cand = true;                        // copy the hot-set candidates back after the next batch
@@ -252,9 +258,9 @@ struct rl_engine {
     bool fell_back = false;
     uint32_t errs = 0;
   };
-  Flight nxt;
+  Flight nxt[HSLOTS - 1];  // pipelined batches behind the oldest, in submission order
   Flight cur_view;  // the oldest batch as a Flight (finish)
-  bool has_next = false;
+  int n_next = 0;
   uint32_t cur_slot = 0;
   bool cur_want_cand = false;
   bool in_flight = false;
@@ -331,13 +337,13 @@ struct rl_engine {
   int finish();
   int settle(Flight& f);
   void begin_submit() {
-    const uint32_t s = (uint32_t)(sub_seq & 1u);
+    const uint32_t s = (uint32_t)(sub_seq % HSLOTS);
     h_ctl = h_ctl_s[s];
     h_cand = h_cand_s[s];
   }
   // Record the submitted batch's completion point and advance the slot.
   void end_submit(bool pipelined_second) {
-    const uint32_t s = (uint32_t)(sub_seq & 1u);
+    const uint32_t s = (uint32_t)(sub_seq % HSLOTS);
     hipEventRecord(ev_done[s], stream);
     if (!pipelined_second) {
       cur_view = Flight{};
@@ -383,7 +389,8 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     const bool split = !timing && in_flight;
     hipStream_t fs = split ? front : stream;
     if (split) {
-      hipStreamWaitEvent(front, ev_done[sl], 0);  // slot buffers and control block free (batch seq-2 done)
+      // slot buffers and control block free: batch seq-2 done (its host slot)
+      hipStreamWaitEvent(front, ev_done[(sub_seq + HSLOTS - 2) % HSLOTS], 0);
       if (!inputs_ready) {                        // inputs come from work queued on the stream
         hipEventRecord(ev_ready, stream);
         hipStreamWaitEvent(front, ev_ready, 0);
@@ -624,11 +631,12 @@ int rl_engine::upload_hot(hipStream_t us) {
   hipError_t e = hipEventSynchronize(ev_hot);
   if (e == hipSuccess) {
     memcpy(h_hot_stage, t.data(), sizeof(HotEntry) * t.size());
-    e = hipMemcpyAsync(d_hot_buf[hot_ver ^ 1], h_hot_stage, sizeof(HotEntry) * t.size(), hipMemcpyHostToDevice, us);
+    e = hipMemcpyAsync(d_hot_buf[(hot_ver + 1) % HSLOTS], h_hot_stage, sizeof(HotEntry) * t.size(),
+                       hipMemcpyHostToDevice, us);
   }
   if (e == hipSuccess) e = hipEventRecord(ev_hot, us);
   if (e != hipSuccess) return hip_fail(e, "upload hot set");
-  hot_ver ^= 1;
+  hot_ver = (hot_ver + 1) % HSLOTS;
   d_hot = d_hot_buf[hot_ver];
   hot_dirty = false;
   st.hot_keys = hot.size();
@@ -700,10 +708,23 @@ void rl_engine::update_hot(uint32_t n_cand) {
 // when the bucketed pipeline could not take it, on the full fingerprint order when a sort-
 // prefix run held two fingerprints. Reruns are synchronous, so they are on the table before
 // anything submitted later.
+// Wait for a batch's completion event by polling. A blocking wait wakes the submitter thread
+// ≈20 µs after the GPU signals, and with two batches in flight that delay lands directly on
+// the next batch's k4_hist (it is submitted after this wait returns). The submitter thread is
+// dedicated to its device (rl_hip.h threading rule), so spinning costs no other work; after a
+// bounded spin (a batch far longer than any steady-state one) it falls back to blocking.
+static hipError_t wait_event_polling(hipEvent_t ev) {
+  for (int k = 0; k < (1 << 18); ++k) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e;
+  }
+  return hipEventSynchronize(ev);
+}
+
 int rl_engine::settle(Flight& f) {
   h_ctl = h_ctl_s[f.slot];
   h_cand = h_cand_s[f.slot];
-  hipError_t e = timing ? hipStreamSynchronize(stream) : hipEventSynchronize(ev_done[f.slot]);
+  hipError_t e = timing ? hipStreamSynchronize(stream) : wait_event_polling(ev_done[f.slot]);
   if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
   const bool host = &f == &cur_view && host_path;
   uint32_t errs = h_ctl->err;
@@ -757,15 +778,15 @@ int rl_engine::finish() {
   if (settled_here && f.fell_back) {
     hipError_t e = hipMemsetAsync(d_poison, 0, 4, stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(poison)");
-    if (has_next && !nxt.settled) {
-      int rc = settle(nxt);
+    for (int q = 0; q < n_next && !nxt[q].settled; ++q) {  // refused in turn (poison chain)
+      int rc = settle(nxt[q]);
       if (rc) return rc;
-      if (nxt.fell_back) {
-        e = hipMemsetAsync(d_poison, 0, 4, stream);
-        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(poison)");
-      }
+      if (!nxt[q].fell_back) break;
+      hipError_t e2 = hipMemsetAsync(d_poison, 0, 4, stream);
+      if (e2 != hipSuccess) return hip_fail(e2, "hipMemsetAsync(poison)");
     }
   }
+
   h_ctl = h_ctl_s[f.slot];
   h_cand = h_cand_s[f.slot];
   const uint32_t errs = f.errs;
@@ -904,12 +925,13 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     chk(hipMalloc(&e->bP, N * 8 + 64));
     chk(hipMalloc(&e->brec, N * sizeof(ItemRec)));
     chk(hipMalloc(&e->bbase, (NBUCKETS + 1) * 4));
-    for (int k = 0; k < 2; ++k) chk(hipMalloc(&e->d_hot_buf[k], sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX)));
+    for (int k = 0; k < HSLOTS; ++k) chk(hipMalloc(&e->d_hot_buf[k], sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX)));
     e->d_hot = e->d_hot_buf[0];
     chk(hipHostMalloc(&e->h_hot_stage, sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX), hipHostMallocDefault));
     chk(hipMalloc(&e->hbk, sizeof(HotBucket) * HOT_BUCKETS));
     chk(hipMalloc(&e->d_cand, sizeof(HotCand) * CAND_MAX));
-    for (int k = 0; k < 2; ++k) chk(hipHostMalloc(&e->h_cand_s[k], sizeof(HotCand) * CAND_MAX, hipHostMallocDefault));
+    for (int k = 0; k < HSLOTS; ++k)
+      chk(hipHostMalloc(&e->h_cand_s[k], sizeof(HotCand) * CAND_MAX, hipHostMallocDefault));
     e->h_cand = e->h_cand_s[0];
     e->hot_dirty = true;  // upload the empty table before the first batch
   }
@@ -965,10 +987,12 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
 
   e->zero_cap = e->zlayout((uint32_t)N, MAX_PASSES).total;
   chk(hipMalloc(&e->zero_block, e->zero_cap));
-  for (int k = 0; k < 2; ++k) chk(hipHostMalloc(&e->h_ctl_s[k], sizeof(EngineCtl), hipHostMallocDefault));
+  for (int k = 0; k < HSLOTS; ++k) chk(hipHostMalloc(&e->h_ctl_s[k], sizeof(EngineCtl), hipHostMallocDefault));
   e->h_ctl = e->h_ctl_s[0];
   chk(hipStreamCreateWithFlags(&e->front, hipStreamNonBlocking));
-  for (hipEvent_t* ev : {&e->ev_front[0], &e->ev_front[1], &e->ev_done[0], &e->ev_done[1], &e->ev_ready, &e->ev_hot}) {
+  std::vector<hipEvent_t*> evs = {&e->ev_front[0], &e->ev_front[1], &e->ev_ready, &e->ev_hot};
+  for (int k = 0; k < HSLOTS; ++k) evs.push_back(&e->ev_done[k]);
+  for (hipEvent_t* ev : evs) {
     chk(hipEventCreateWithFlags(ev, hipEventDisableTiming));
     if (he == hipSuccess) chk(hipEventRecord(*ev, e->stream));
   }
@@ -987,14 +1011,15 @@ void rl_destroy(rl_engine* e) {
   if (e->stream) hipStreamSynchronize(e->stream);
   if (e->front) hipStreamSynchronize(e->front);
   for (auto ev : e->ev_pool) hipEventDestroy(ev);
-  for (hipEvent_t ev : {e->ev_front[0], e->ev_front[1], e->ev_done[0], e->ev_done[1], e->ev_ready, e->ev_hot})
+  for (hipEvent_t ev : {e->ev_front[0], e->ev_front[1], e->ev_ready, e->ev_hot})
     if (ev) hipEventDestroy(ev);
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < HSLOTS; ++k) {
+    if (e->ev_done[k]) hipEventDestroy(e->ev_done[k]);
     hipFree(e->d_hot_buf[k]);
     hipHostFree(e->h_cand_s[k]);
     hipHostFree(e->h_ctl_s[k]);
-    hipFree(e->v4_fpart[k]);
   }
+  for (int k = 0; k < 2; ++k) hipFree(e->v4_fpart[k]);
   hipFree(e->v4_srt[1]);
   hipFree(e->v4_tcount[1]);
   hipFree(e->v4_thsum[1]);
@@ -1188,8 +1213,9 @@ int rl_wait(rl_engine* e) {
   if (!e->in_flight) return e->fail(RL_ESTATE, "rl_wait without a batch in flight");
   const int rc = e->finish();
   e->in_flight = false;
-  if (e->has_next) {  // the pipelined batch becomes the oldest
-    const rl_engine::Flight& n = e->nxt;
+  if (e->n_next) {  // the next pipelined batch becomes the oldest
+    const rl_engine::Flight n = e->nxt[0];
+    for (int q = 1; q < e->n_next; ++q) e->nxt[q - 1] = e->nxt[q];
     e->dev_batch = n.b;
     e->pend_out_dev = n.out;
     e->pend_thr_dev = n.thr;
@@ -1198,7 +1224,7 @@ int rl_wait(rl_engine* e) {
     e->cur_slot = n.slot;
     e->cur_want_cand = n.want_cand;
     e->cur_view = n;
-    e->has_next = false;
+    e->n_next -= 1;
     e->in_flight = true;
   }
   return rc;
@@ -1228,7 +1254,8 @@ int rl_submit_device(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t
 
 int rl_submit_pipelined(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t* d_req_throttle_ms) {
   if (!e || !b) return RL_EINVAL;
-  if (e->has_next) return e->fail(RL_ESTATE, "rl_submit_pipelined with two batches in flight (call rl_wait)");
+  if (e->in_flight && e->n_next + 1 >= HSLOTS)
+    return e->fail(RL_ESTATE, "rl_submit_pipelined with %d batches in flight (call rl_wait)", HSLOTS);
   const rl_config& c = e->cfg;
   if (b->n_desc > c.max_batch_desc || b->n_req > c.max_batch_req)
     return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req)", c.max_batch_desc,
@@ -1237,24 +1264,26 @@ int rl_submit_pipelined(rl_engine* e, const rl_batch* b, rl_status* d_out, uint3
   const bool second = e->in_flight;
   if (second && e->default_mode() != MODE_V4)
     return e->fail(RL_ESTATE, "a second batch in flight needs the v4 pipeline (call rl_wait)");
-  if (second && (e->pend_out_dev == d_out || e->pend_thr_dev == d_req_throttle_ms))
-    return e->fail(RL_EINVAL, "the two in-flight batches need distinct output buffers");
+  bool shared = second && (e->pend_out_dev == d_out || e->pend_thr_dev == d_req_throttle_ms);
+  for (int q = 0; second && q < e->n_next; ++q)
+    shared |= e->nxt[q].out == d_out || e->nxt[q].thr == d_req_throttle_ms;
+  if (shared) return e->fail(RL_EINVAL, "batches in flight together need distinct output buffers");
   if (!e->d_rules) rl_load_rules(e, nullptr, 0);
   e->begin_submit();
   e->inputs_ready = true;
-  const uint32_t slot = (uint32_t)(e->sub_seq & 1u);
+  const uint32_t slot = (uint32_t)(e->sub_seq % HSLOTS);
   const bool want = e->want_cand;
   int rc = e->run_pipeline(*b, d_out, d_req_throttle_ms, e->default_mode());
   if (rc) return rc;
   if (second) {
-    rl_engine::Flight& n = e->nxt;
+    rl_engine::Flight& n = e->nxt[e->n_next];
     n = rl_engine::Flight{};
     n.b = *b;
     n.out = d_out;
     n.thr = d_req_throttle_ms;
     n.slot = slot;
     n.want_cand = want;
-    e->has_next = true;
+    e->n_next += 1;
   } else {
     e->dev_batch = *b;
     e->pend_out_dev = d_out;

@@ -17,7 +17,8 @@ constexpr int T = V3_TILE;
 constexpr int NT = V3_THREADS;
 constexpr int R = T / NT;      // descriptors per thread
 constexpr int W = NT / 64;     // waves per tile block
-constexpr int PRE_DW = 12;     // blob dwords preloaded per descriptor (prefixes up to 40 B hash inline)
+constexpr int PRE_DW = 8;      // blob dwords preloaded per descriptor (prefixes up to 24 B hash inline)
+static_assert(PRE_DW % 4 == 0, "the preload is whole 16-B loads");
 constexpr uint32_t BKT_NONE = 4095;  // past the end of the batch (sorts last in 12 bits)
 static_assert(NBUCKETS <= 4095, "bucket ids are 12-bit");
 static_assert(T <= 65536, "u16 tile offsets");

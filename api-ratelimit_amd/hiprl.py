@@ -68,6 +68,7 @@ class RlResolveBatch(C.Structure):
 
 
 TREE_ROOT = 0xFFFFFFFF
+MAX_IN_FLIGHT = 3  # RL_MAX_IN_FLIGHT: batches in flight at once through rl_submit_pipelined
 
 
 class RlEngineStats(C.Structure):
@@ -288,12 +289,21 @@ class Engine:
         s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
         self._check(self.lib.rl_submit_device(self.h, C.byref(s), out_ptr, thr_ptr), "rl_submit_device")
 
-    def submit_pipelined(self, n_desc: int, n_req: int, blob_bytes: int, ptrs, out_ptr: int, thr_ptr: int):
-        """Device batch with complete inputs, behind at most one batch in flight (rl_submit_pipelined):
-        wait() completes the oldest. The two in-flight batches need distinct output buffers."""
+    @staticmethod
+    def device_batch(n_desc: int, n_req: int, blob_bytes: int, ptrs) -> RlBatch:
+        """An rl_batch of device pointers (ptrs = blob, off, rule, req_of, now, hits)."""
         s = RlBatch()
         s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
         s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        return s
+
+    def submit_pipelined(self, n_desc: int, n_req: int, blob_bytes: int, ptrs, out_ptr: int, thr_ptr: int):
+        """Device batch with complete inputs, behind at most one batch in flight (rl_submit_pipelined):
+        wait() completes the oldest. The two in-flight batches need distinct output buffers."""
+        self.submit_pipelined_batch(self.device_batch(n_desc, n_req, blob_bytes, ptrs), out_ptr, thr_ptr)
+
+    def submit_pipelined_batch(self, s: RlBatch, out_ptr: int, thr_ptr: int):
+        """submit_pipelined with a prebuilt device_batch() (no per-call marshalling)."""
         self._check(self.lib.rl_submit_pipelined(self.h, C.byref(s), out_ptr, thr_ptr), "rl_submit_pipelined")
 
     def wait(self):

