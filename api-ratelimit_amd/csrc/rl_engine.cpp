@@ -352,9 +352,19 @@ struct rl_engine {
     }
     ++sub_seq;
     inputs_ready = false;
+    if (cand_pending) {
+      cand_pending = false;
+      update_hot(cand_stash.data(), (uint32_t)cand_stash.size());
+    }
   }
   int upload_hot(hipStream_t us);
-  void update_hot(uint32_t n_cand);
+  void update_hot(const HotCand* cand, uint32_t n_cand);
+  // Hot-set maintenance from a completed batch's candidates runs after the next submit has
+  // enqueued its kernels (end_submit), not between rl_wait and that submit, where it would
+  // delay the next batch's k4_hist; the set it yields applies one batch later. Decisions do
+  // not depend on the hot set, only speed does.
+  std::vector<HotCand> cand_stash;
+  bool cand_pending = false;
   int enqueue_d2h();
 };
 
@@ -648,7 +658,7 @@ int rl_engine::upload_hot(hipStream_t us) {
 // under two rules is not bucketable. Hysteresis keeps the set (and its upload) stable on a
 // steady skewed stream: a hot key stays while it has >= HOT_CAND_MIN descriptors per batch,
 // a new key joins with >= HOT_MIN_SEG while there is room.
-void rl_engine::update_hot(uint32_t n_cand) {
+void rl_engine::update_hot(const HotCand* cand, uint32_t n_cand) {
   n_cand = n_cand < (uint32_t)CAND_MAX ? n_cand : (uint32_t)CAND_MAX;
   auto ident_less = [](const HotKey& x, const HotKey& y) {
     return x.a != y.a ? x.a < y.a : x.b != y.b ? x.b < y.b : x.unit < y.unit;
@@ -657,7 +667,7 @@ void rl_engine::update_hot(uint32_t n_cand) {
   std::vector<HotKey> agg;
   agg.reserve(n_cand);
   for (uint32_t i = 0; i < n_cand; ++i) {
-    const HotCand& c = h_cand[i];
+    const HotCand& c = cand[i];
     agg.push_back(HotKey{c.a, c.b, c.unit, c.rule, c.count});
   }
   std::sort(agg.begin(), agg.end(), ident_less);
@@ -811,7 +821,15 @@ int rl_engine::finish() {
   if (errs & ERR_NEED_RESORT) return fail(RL_EDEVICE, "full-fingerprint re-sort still found a mixed run");
   // Hot-set maintenance costs host time between batches: every batch while the set is
   // empty or after a fallback, else every 8th batch (a skewed stream's head moves slowly).
-  if (!(cfg.flags & RL_CFG_LSD_ONLY) && (f.want_cand || f.fell_back)) update_hot(h_ctl->tile_ctr[CAND_CTR][0]);
+  if (!(cfg.flags & RL_CFG_LSD_ONLY) && (f.want_cand || f.fell_back)) {
+    const uint32_t nc = std::min(h_ctl->tile_ctr[CAND_CTR][0], (uint32_t)CAND_MAX);
+    if (f.fell_back) {  // rare: take the set now
+      update_hot(h_cand, nc);
+    } else {
+      cand_stash.assign(h_cand, h_cand + nc);
+      cand_pending = true;
+    }
+  }
   last_unique = h_ctl->n_segments;
   last_n = dev_batch.n_desc;
   last_req = dev_batch.n_req;
@@ -1397,6 +1415,8 @@ int rl_reset(rl_engine* e) {
   if (e->in_flight) return e->fail(RL_ESTATE, "rl_reset while a batch is in flight");
   e->hot.clear();
   e->hot_dirty = true;
+  e->cand_pending = false;
+  e->cand_stash.clear();
   hipError_t he = hipMemsetAsync(e->table, 0, e->table_slots * sizeof(Slot), e->stream);
   if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
   return he == hipSuccess ? 0 : e->hip_fail(he, "rl_reset");
