@@ -79,7 +79,10 @@ RL_DEV uint32_t rule_of(uint32_t rn) { return rn & (V3_MAX_RULES - 1u); }
 __device__ uint64_t g_st4[4096][8];
 #define ST4(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_st4[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define ST4V(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_st4[blockIdx.x][k] = (v); } while (0)
+// k4_scan blocks stamp rows 2048 + block (thread 0).
+#define ST5(k) do { if (threadIdx.x == 0) g_st4[2048 + blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
+#define ST5(k) do { } while (0)
 #define ST4(k) do { } while (0)
 #define ST4V(k, v) do { } while (0)
 #endif
@@ -317,17 +320,23 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
 constexpr int SCAN_NT = 1024;
 constexpr int SCAN_W = SCAN_NT / 64;
 constexpr int SCAN_U = 16;  // column loads in flight per lane (columns longer than SCAN_Q)
-constexpr int SCAN_Q = 32;  // column entries per lane kept in registers
+constexpr int SCAN_Q = 32;  // MSD column entries per lane kept in registers
+// Hot blocks take 16 buckets each over 64 tile slices (lane = slice % 4 * 16 + bucket, wave =
+// slice / 4): 32 blocks instead of 8, so the hot columns (u16 starts + u64 h sums of every
+// tile) are pulled by 32 CUs, 8 tiles per lane at config 3.
+constexpr int HOT_PER_BLOCK = 16;
+constexpr int HOT_SCAN_BLOCKS = HOT_BUCKETS / HOT_PER_BLOCK;
+constexpr int HOT_SLICES = SCAN_NT / HOT_PER_BLOCK;
+constexpr int HOT_Q = 16;   // hot column entries per lane kept in registers
 static_assert(HOT_BUCKETS % 64 == 0 && V3_SCAN_BUCKETS % 64 == 0, "bucket blocks");
 static_assert(T < 65536 && SCAN_Q % 2 == 0, "per-tile counts pack in u16 pairs");
 
 // Counts of bucket b (= this lane's) in tiles [tb, tb + SCAN_Q) ∩ [tb, te): each lane loads
 // its bucket's start and takes the next bucket's start from the next lane; lane 63's next
 // start is the wave-uniform entry 64 of the block's row segment.
-RL_DEV void column_counts(const uint16_t* __restrict__ tstart, uint32_t b, uint32_t tb, uint32_t te,
+RL_DEV void column_counts(const uint16_t* __restrict__ tstart, uint32_t b, uint32_t b0, uint32_t tb, uint32_t te,
                           uint32_t (&cq)[SCAN_Q]) {
   const uint32_t lane = threadIdx.x & 63;
-  const uint32_t b0 = blockIdx.x * 64;
   tb = __builtin_amdgcn_readfirstlane(tb);  // wave-uniform: the row-end loads are scalar
   te = __builtin_amdgcn_readfirstlane(te);
   uint32_t e[SCAN_Q];
@@ -355,7 +364,6 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
                                                    uint32_t* __restrict__ ranges, const uint32_t* __restrict__ poison,
                                                    EngineCtl* ctl) {
   __shared__ uint32_t s_f[FP_PART_WORDS];
-  __shared__ uint32_t s_tot[64];
   __shared__ uint32_t s_pc[SCAN_W][64];
   __shared__ unsigned long long s_ph[SCAN_W][64];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -365,59 +373,47 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     if (blockIdx.x == 0 && tid == 0) atomicOr(&ctl->err, ERR_V2_FALLBACK);
     return;
   }
+  ST5(0);
+  const bool hotb = blockIdx.x < (uint32_t)HOT_SCAN_BLOCKS;  // block-uniform
+  // Hot blocks fold the per-tile partials (generation range per region, nil count; the hot
+  // claims need the generations, block 0 publishes them). The partials' loads are issued
+  // here and reduced after the column pass, so the two latencies overlap; MSD blocks need
+  // none of it.
   if (tid < FP_PART_WORDS) s_f[tid] = 0;
-  __syncthreads();
-  // Fold the per-tile partials (every block): generation range per region, nil count.
-  {
-    uint32_t v[FP_PART_WORDS];
+  uint32_t fv[FP_PART_WORDS];
 #pragma unroll
-    for (int w = 0; w < FP_PART_WORDS; ++w) v[w] = 0;
-    for (uint32_t g = tid; g < ntiles; g += SCAN_NT) {
-#pragma unroll
-      for (int w = 0; w < FP_PART_WORDS; ++w) {
-        const uint32_t x = fpart[(size_t)g * FP_PART_WORDS + w];
-        v[w] = w < 16 ? (x > v[w] ? x : v[w]) : v[w] + x;
-      }
-    }
-#pragma unroll
-    for (int w = 0; w < FP_PART_WORDS; ++w) {
-      const uint32_t x = w < 16 ? wave_max_u32(v[w]) : v3::wave_sum(v[w]);
-      if (lane == 0 && x) {
-        if (w < 16) atomicMax(&s_f[w], x);
-        else atomicAdd(&s_f[w], x);
-      }
-    }
-  }
-  __syncthreads();
-  // Two window generations of one region in one batch must be adjacent;
-  // a region's generations share its parity, so a valid batch has ONE generation per region.
-  bool span = false;
-#pragma unroll
-  for (int rg = 0; rg < 8; ++rg) {
-    const uint32_t mx = s_f[8 + rg], mn = ~s_f[rg];
-    span |= mx != 0 && mx - mn > 1u;
-  }
-  if (blockIdx.x == 0) {
-    if (tid < 8) ctl->gen_min[tid] = ~s_f[tid];
-    else if (tid < 16) ctl->gen_max[tid - 8] = s_f[tid];
-    else if (tid == 16) ctl->n_nil = s_f[16];
-    if (tid == 0 && span) atomicOr(&ctl->err, ERR_WINDOW_SPAN);
-  }
-  // Column pass: bucket b = lane of this block, tiles [wave*Q, wave*Q + Q).
-  const uint32_t b = blockIdx.x * 64 + lane;
-  const bool hotb = blockIdx.x * 64 < (uint32_t)HOT_BUCKETS;  // block-uniform
-  const uint32_t Q = (ntiles + SCAN_W - 1) / SCAN_W;
-  const uint32_t tb = min(ntiles, wave * Q), te = min(ntiles, tb + Q);
+  for (int w = 0; w < FP_PART_WORDS; ++w)
+    fv[w] = hotb && tid < ntiles ? fpart[(size_t)tid * FP_PART_WORDS + w] : 0u;
+  // Column pass. MSD blocks: bucket b = lane, tiles [wave*Q, wave*Q + Q). Hot blocks: bucket
+  // b = lane % 16 of the block's 16, tile slice wave * 4 + lane / 16.
+  const uint32_t m = blockIdx.x - HOT_SCAN_BLOCKS;  // MSD block (group of 64 buckets)
+  const uint32_t bb = lane & (HOT_PER_BLOCK - 1u);
+  const uint32_t nsl = hotb ? HOT_SLICES : SCAN_W;
+  const uint32_t slice = hotb ? wave * (64 / HOT_PER_BLOCK) + lane / HOT_PER_BLOCK : wave;
+  const uint32_t b = hotb ? blockIdx.x * HOT_PER_BLOCK + bb : HOT_BUCKETS + m * 64 + lane;
+  const uint32_t Q = (ntiles + nsl - 1) / nsl;
+  const uint32_t tb = min(ntiles, slice * Q), te = min(ntiles, tb + Q);
   uint32_t c = 0;
   unsigned long long hs = 0;
-  // MSD blocks with up to SCAN_Q tiles per wave (batches up to SCAN_W * SCAN_Q tiles, 1M
-  // descriptors at 2048 per tile) load the column once, all loads in flight together, and
-  // keep the counts in registers for the prefix pass below.
-  const bool in_regs = !hotb && Q <= (uint32_t)SCAN_Q;  // block-uniform
-  uint32_t cpk[SCAN_Q / 2];  // counts (<= T each) packed in u16 pairs
-  if (in_regs) {
+  // Columns up to SCAN_Q (MSD) / HOT_Q (hot) tiles per lane are loaded once, all loads in
+  // flight together, and kept in registers for the prefix pass below.
+  const bool in_regs = Q <= (uint32_t)(hotb ? HOT_Q : SCAN_Q);  // block-uniform
+  uint32_t cpk[SCAN_Q / 2];  // MSD: counts (<= T each) packed in u16 pairs
+  unsigned long long hq[HOT_Q];  // hot: h sums
+  if (in_regs && hotb) {
+#pragma unroll
+    for (int u = 0; u < HOT_Q; ++u) {
+      const uint32_t t = tb + u;
+      const uint16_t* row = tstart + (size_t)t * ROW + b;
+      const bool v = t < te;
+      c += v ? (uint32_t)row[1] - (uint32_t)row[0] : 0u;
+      hq[u] = v ? thsum[(size_t)t * HOT_BUCKETS + b] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < HOT_Q; ++u) hs += hq[u];
+  } else if (in_regs) {
     uint32_t cq[SCAN_Q];
-    column_counts(tstart, b, tb, te, cq);
+    column_counts(tstart, b, HOT_BUCKETS + m * 64, tb, te, cq);
 #pragma unroll
     for (int u = 0; u < SCAN_Q; ++u) c += cq[u];
 #pragma unroll
@@ -440,19 +436,63 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     }
   }
   s_pc[wave][lane] = c;
-  if (hotb) s_ph[wave][lane] = hs;
+  bool span = false;
+  if (hotb) {
+    s_ph[wave][lane] = hs;
+    for (uint32_t g = tid + SCAN_NT; g < ntiles; g += SCAN_NT) {  // batches over SCAN_NT tiles
+#pragma unroll
+      for (int w = 0; w < FP_PART_WORDS; ++w) {
+        const uint32_t x = fpart[(size_t)g * FP_PART_WORDS + w];
+        fv[w] = w < 16 ? (x > fv[w] ? x : fv[w]) : fv[w] + x;
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < FP_PART_WORDS; ++w) {
+      const uint32_t x = w < 16 ? wave_max_u32(fv[w]) : v3::wave_sum(fv[w]);
+      if (lane == 0 && x) {
+        if (w < 16) atomicMax(&s_f[w], x);
+        else atomicAdd(&s_f[w], x);
+      }
+    }
+  }
   __syncthreads();
+  ST5(2);
+  if (hotb) {
+    // Two window generations of one region in one batch must be adjacent;
+    // a region's generations share its parity, so a valid batch has ONE generation per region.
+#pragma unroll
+    for (int rg = 0; rg < 8; ++rg) {
+      const uint32_t mx = s_f[8 + rg], mn = ~s_f[rg];
+      span |= mx != 0 && mx - mn > 1u;
+    }
+    if (blockIdx.x == 0) {
+      if (tid < 8) ctl->gen_min[tid] = ~s_f[tid];
+      else if (tid < 16) ctl->gen_max[tid - 8] = s_f[tid];
+      else if (tid == 16) ctl->n_nil = s_f[16];
+      if (tid == 0 && span) atomicOr(&ctl->err, ERR_WINDOW_SPAN);
+    }
+  }
   uint32_t ctot = 0, crun = 0;
   unsigned long long hrun = 0, htot = 0;
+  if (hotb) {  // bucket totals over the 64 slices; h sums of the slices before this lane's
 #pragma unroll
-  for (int w = 0; w < SCAN_W; ++w) {
-    const uint32_t x = s_pc[w][lane];
-    ctot += x;
-    crun += (uint32_t)w < wave ? x : 0u;
-    if (hotb) {
-      const unsigned long long y = s_ph[w][lane];
-      hrun += (uint32_t)w < wave ? y : 0ull;
-      htot += y;
+    for (int w = 0; w < SCAN_W; ++w) {
+#pragma unroll
+      for (int q = 0; q < 64 / HOT_PER_BLOCK; ++q) {
+        const uint32_t sl = (uint32_t)(w * (64 / HOT_PER_BLOCK) + q);
+        const uint32_t x = s_pc[w][q * HOT_PER_BLOCK + bb];
+        const unsigned long long y = s_ph[w][q * HOT_PER_BLOCK + bb];
+        ctot += x;
+        htot += y;
+        hrun += sl < slice ? y : 0ull;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int w = 0; w < SCAN_W; ++w) {
+      const uint32_t x = s_pc[w][lane];
+      ctot += x;
+      crun += (uint32_t)w < wave ? x : 0u;
     }
   }
   if (!hotb) {
@@ -481,35 +521,48 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
       }
     }
     if (wave != 0) return;
+    ST5(3);
     if (ctot > (uint32_t)BUCKET_CAP) atomicOr(&ctl->err, ERR_V2_FALLBACK);
-    const uint32_t g = blockIdx.x - HOT_BUCKETS / 64;
+    const uint32_t g = m;
     const uint32_t incl = v3::wave_incl_scan<uint32_t>(ctot);
     ranges[R_BPRE + mb] = incl - ctot;
     if (lane == 63) ranges[R_GTOT + g] = incl;
     // Pack the group's 64 buckets greedily into k4_group ranges of whole buckets holding at
-    // most G_CAP records (a single larger bucket is a range of its own).
-    s_tot[lane] = ctot;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // most G_CAP records (a single larger bucket is a range of its own). The walk is
+    // wave-uniform over the lanes' totals (readlane: no LDS round trip per bucket); lane 0
+    // stores.
+    uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
+    uint32_t nr = 0, cur = 0;
     if (lane == 0) {
       heads_out[blockIdx.x] = 0;
-      uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
-      uint32_t nr = 0, cur = 0;
       rb[0] = 0;
-      for (int k = 0; k < 64; ++k) {
-        const uint32_t c = s_tot[k];
-        if (cur && cur + c > (uint32_t)G_CAP) {
-          rb[++nr] = k;
-          cur = 0;
-        }
-        cur += c;
+    }
+#pragma unroll
+    for (int k = 0; k < 64; ++k) {
+      const uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)ctot, k);
+      if (cur && cur + cb > (uint32_t)G_CAP) {
+        ++nr;
+        if (lane == 0) rb[nr] = k;
+        cur = 0;
       }
-      rb[++nr] = 64;
+      cur += cb;
+    }
+    ++nr;
+    if (lane == 0) {
+      rb[nr] = 64;
       ranges[g] = nr;
     }
+    ST5(4);
     return;
   }
-  for (uint32_t t = tb; t < te; t += SCAN_U) {
+  if (in_regs) {
+#pragma unroll
+    for (int u = 0; u < HOT_Q; ++u) {
+      if (tb + u < te) hoff[(size_t)(tb + u) * HOT_BUCKETS + b] = hrun;
+      hrun += hq[u];
+    }
+  }
+  for (uint32_t t = in_regs ? te : tb; t < te; t += SCAN_U) {
     unsigned long long hv[SCAN_U];
 #pragma unroll
     for (int u = 0; u < SCAN_U; ++u) hv[u] = t + u < te ? thsum[(size_t)(t + u) * HOT_BUCKETS + b] : 0ull;
@@ -520,6 +573,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     }
   }
   if (wave == 0) {
+    ST5(3);
     // Hot key leader: find or claim the key's slot and read the counter before this batch. A
     // claimed slot starts at count 0, which is invisible if the batch is later rejected.
     HotBucket3 x;
@@ -530,7 +584,9 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     x.pad[0] = x.pad[1] = x.pad[2] = 0;
     const uint32_t errs = ctl->err;  // flags of k4_hist
     uint32_t heads = 0;
-    if (ctot && !span && !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME | ERR_V2_FALLBACK))) {
+    // lanes 0..15 of wave 0 (slice 0) lead the block's 16 hot buckets
+    if (lane < (uint32_t)HOT_PER_BLOCK && ctot && !span &&
+        !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME | ERR_V2_FALLBACK))) {
       const HotEntry he = hot_list[b >> 1];
       const uint32_t region = (he.unit - 1u) * 2u + (b & 1u);
       const uint32_t gen = s_f[8 + region];  // the region's one generation in this batch
@@ -565,9 +621,10 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
       if (slot != nullptr && !existed) heads |= 1u << 16;  // a new table slot
       if (ctot >= HOT_CAND_MIN) emit_candidate(ctl, cand, he.rule, ctot, 0xFFFFFFFFu, he.a, he.b, he.unit);
     }
-    hb[b] = x;
+    if (lane < (uint32_t)HOT_PER_BLOCK) hb[b] = x;
     heads = v3::wave_sum(heads);
     if (lane == 0) heads_out[blockIdx.x] = heads;
+    ST5(4);
   }
 }
 
@@ -1204,7 +1261,7 @@ __global__ __launch_bounds__(G_NT, 4) void k4_group(DevBatch in, MRec* __restric
 // ---------------------------------------------------------------------------
 uint32_t v4_tiles(uint32_t n) { return n ? (n + V3_TILE - 1) / V3_TILE : 1; }
 uint32_t v4_group_blocks(uint32_t) { return v4::GBLOCKS; }
-uint32_t v4_scan_blocks() { return V3_SCAN_BUCKETS / 64; }
+uint32_t v4_scan_blocks() { return v4::HOT_SCAN_BLOCKS + v4::MSD_GROUPS; }
 size_t v4_scratch_bytes() {
   using namespace v4;
   return (size_t)GBLOCKS * BUCKET_CAP * (8 + 2 + 2) + (size_t)GBLOCKS * GS_HASH * (4 + 4 + 2) + (size_t)GBLOCKS * 4 +
