@@ -48,9 +48,9 @@ constexpr int ROW = V3_ROW16;  // u16 bucket starts per tile (entries [0, NBUCKE
 static_assert(ROW >= NBUCKETS + 1, "row holds every bucket start and the end");
 constexpr int GBLOCKS = 1024;              // k4_group blocks (at least; 4 per CU, one round)
 constexpr int MSD_GROUPS = MSD_BUCKETS / 64;  // k4_scan blocks of MSD buckets (one range list each)
-constexpr int RANGE_MAX = 64;              // ranges per MSD group (one per bucket at most)
+constexpr int RANGE_MAX = 128;             // ranges per MSD group (two per bucket at most)
 // k4_scan -> k4_place / k4_group, one array of words: [0, MSD_GROUPS) ranges per group;
-// R_START: per group RANGE_MAX + 1 range starts (bucket inside the group, last = 64);
+// R_START: per group RANGE_MAX + 1 range entries (bucket << 1 | half inside the group, last = 128);
 // R_BPRE: per MSD bucket the exclusive prefix of bucket totals inside its group;
 // R_GTOT: per group its record total.
 constexpr int R_START = MSD_GROUPS;
@@ -79,12 +79,15 @@ RL_DEV uint32_t rule_of(uint32_t rn) { return rn & (V3_MAX_RULES - 1u); }
 __device__ uint64_t g_st4[4096][8];
 #define ST4(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_st4[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define ST4V(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_st4[blockIdx.x][k] = (v); } while (0)
+// k4_group per-block facts in rows 3072 + block: [0] records grouped, [1] keys led, [2] ranges, [3] split ranges
+#define ST4X(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_st4[3072 + blockIdx.x][k] += (v); } while (0)
 // k4_scan blocks stamp rows 2048 + block (thread 0).
 #define ST5(k) do { if (threadIdx.x == 0) g_st4[2048 + blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define ST5(k) do { } while (0)
 #define ST4(k) do { } while (0)
 #define ST4V(k, v) do { } while (0)
+#define ST4X(k, v) do { } while (0)
 #endif
 
 // Stores handed to the last k4_group block bypass the L2 of the storing XCD (sc1, written
@@ -532,7 +535,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     // wave-uniform over the lanes' totals (readlane: no LDS round trip per bucket); lane 0
     // stores.
     uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
-    uint32_t nr = 0, cur = 0;
+    uint32_t nr = 0, cur = 0, last = 0;  // last = rb[nr]
     if (lane == 0) {
       heads_out[blockIdx.x] = 0;
       rb[0] = 0;
@@ -540,16 +543,31 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
 #pragma unroll
     for (int k = 0; k < 64; ++k) {
       const uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)ctot, k);
+      const uint32_t ek = (uint32_t)k << 1;
+      if (cb > (uint32_t)G_CAP) {
+        // Oversized bucket (<= BUCKET_CAP): two ranges of its own, one per fingerprint half
+        // (entries ek and ek | 1), grouped by two blocks; the next bucket starts a range.
+        if (last != ek) {
+          ++nr;
+          if (lane == 0) rb[nr] = ek;
+        }
+        ++nr;
+        if (lane == 0) rb[nr] = ek | 1u;
+        last = ek | 1u;
+        cur = cb;
+        continue;
+      }
       if (cur && cur + cb > (uint32_t)G_CAP) {
         ++nr;
-        if (lane == 0) rb[nr] = k;
+        if (lane == 0) rb[nr] = ek;
+        last = ek;
         cur = 0;
       }
       cur += cb;
     }
     ++nr;
     if (lane == 0) {
-      rb[nr] = 64;
+      rb[nr] = 64u << 1;
       ranges[g] = nr;
     }
     ST5(4);
@@ -1101,13 +1119,17 @@ __global__ __launch_bounds__(G_NT, 4) void k4_group(DevBatch in, MRec* __restric
       while (g + 1 < (uint32_t)MSD_GROUPS && s_rn[g + 1] <= r) ++g;
       const uint32_t q = r - s_rn[g];
       const uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
-      const uint32_t k0 = rb[q], k1 = rb[q + 1];
+      // Range entries are bucket << 1 | half (see k4_scan): [e0, e1) is whole buckets, or one
+      // fingerprint half of an oversized bucket (e0 odd: half 1; e1 == e0 | 1: half 0).
+      const uint32_t e0 = rb[q], e1 = rb[q + 1];
+      const int split_half = (e0 & 1u) ? 1 : (e1 == (e0 | 1u) ? 0 : -1);
+      const uint32_t k0 = e0 >> 1, k1 = split_half >= 0 ? k0 + 1u : e1 >> 1;
       const uint32_t r0 = s_gpre[g] + ranges[R_BPRE + g * 64 + k0];
       const uint32_t r1 = k1 == 64u ? s_gpre[g + 1] : s_gpre[g] + ranges[R_BPRE + g * 64 + k1];
       const uint32_t m = r1 - r0;
       if (m == 0) continue;
       __syncthreads();  // the previous range is done with LDS
-      if (m <= (uint32_t)G_CAP) {
+      if (m <= (uint32_t)G_CAP && split_half < 0) {
         for (uint32_t s = tid; s < (uint32_t)G_HASH; s += G_NT) {
           s_slot[s] = G_EMPTY;
           s_cnt[s] = 0;
@@ -1122,12 +1144,20 @@ __global__ __launch_bounds__(G_NT, 4) void k4_group(DevBatch in, MRec* __restric
         __syncthreads();
         ST4(2);
         const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
-        heads += group_range<true>(gl, m, rules, tab, local_cache, out, req_thr, cand, cand_on, routed, s_agg,
-                                   &s_carry, sh_w, ctl);
+        {
+          const uint32_t hh = group_range<true>(gl, m, rules, tab, local_cache, out, req_thr, cand, cand_on, routed,
+                                                s_agg, &s_carry, sh_w, ctl);
+          heads += hh;
+          ST4X(0, m);
+          ST4X(1, hh & 0xFFFFu);
+          ST4X(2, 1);
+        }
         continue;
       }
       // One bucket larger than the LDS stage. Its keys split by the fingerprint bit below the
       // bucket bits into two halves of whole keys; each half that fits is grouped in LDS.
+      ST4X(3, 1);
+      ST4X(0, m);
       constexpr int SPLIT_BIT = 64 - 3 - MSD_BITS - 1;
       constexpr int SU = BUCKET_CAP / G_NT;
       const MRec* src = mrec + r0;
@@ -1139,7 +1169,8 @@ __global__ __launch_bounds__(G_NT, 4) void k4_group(DevBatch in, MRec* __restric
       uint32_t tot0;
       v3::block_excl_scan<G_NT>(n0, sh_w, tot0);
       if (tot0 <= (uint32_t)G_CAP && m - tot0 <= (uint32_t)G_CAP) {
-        for (uint32_t part = 0; part < 2u; ++part) {
+        // a split range takes its own half (the other half is another block's range)
+        for (uint32_t part = split_half == 1 ? 1u : 0u; part < (split_half == 0 ? 1u : 2u); ++part) {
           __syncthreads();  // the previous half is done with LDS
           for (uint32_t s = tid; s < (uint32_t)G_HASH; s += G_NT) {
             s_slot[s] = G_EMPTY;
@@ -1163,8 +1194,9 @@ __global__ __launch_bounds__(G_NT, 4) void k4_group(DevBatch in, MRec* __restric
           heads += group_range<true>(gl, mp, rules, tab, local_cache, out, req_thr, cand, cand_on, routed, s_agg,
                                      &s_carry, sh_w, ctl);
         }
-      } else {
-        // grouped in place in bucket order (global scratch)
+      } else if (split_half != 1) {
+        // grouped in place in bucket order (global scratch); for a split bucket by its half-0
+        // range's block (the half-1 block has nothing to do)
         const GS gg{mrec + r0,                        gs.P + (size_t)j * BUCKET_CAP,
                     gs.list + (size_t)j * BUCKET_CAP,  gs.grp + (size_t)j * BUCKET_CAP,
                     gs.slot + (size_t)j * GS_HASH,     gs.cnt + (size_t)j * GS_HASH,

@@ -47,3 +47,18 @@ for j in range(dd.shape[1]):
           f"  max {dd[:, j].max():7.2f}")
 print(f"   busy blocks {len(a)}; done time p50/p90/max {np.median(rel[:, 7]):.1f}/{np.percentile(rel[:, 7], 90):.1f}/{rel[:, 7].max():.1f}")
 print(f"   staged time p10/p50/p90 {np.percentile(rel[:, 1], 10):.1f}/{np.median(rel[:, 1]):.1f}/{np.percentile(rel[:, 1], 90):.1f}")
+# per-block facts (rows 3072 + block, last batch accumulates over the run: divide by batches)
+fx = st[3072:3072 + 1024, :4].astype(np.int64)
+nbat = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+done = np.full(1024, np.nan)
+allrel = (st[:1024, 5].astype(np.int64) - t0) / 100.0
+ok = st[:1024, 2] > 0
+done[ok] = allrel[ok]
+order = np.argsort(-np.nan_to_num(done, nan=-1))
+print("slowest blocks: block done_us recs/batch keys/batch ranges/batch splits/batch")
+for k in order[:12]:
+    print(f"   {k:5d} {done[k]:7.1f} {fx[k,0]/nbat:8.1f} {fx[k,1]/nbat:8.1f} {fx[k,2]/nbat:5.2f} {fx[k,3]/nbat:5.2f}")
+sel = ok
+print("corr(done, recs) = %.2f, corr(done, keys) = %.2f" % (np.corrcoef(done[sel], fx[sel, 0])[0, 1],
+                                                           np.corrcoef(done[sel], fx[sel, 1])[0, 1]))
+print("median recs/batch %.1f keys/batch %.1f" % (np.median(fx[sel, 0]) / nbat, np.median(fx[sel, 1]) / nbat))
