@@ -221,7 +221,7 @@ struct rl_engine {
   HotEntry* h_hot_stage = nullptr;              // pinned upload staging
   EngineCtl* h_ctl_s[HSLOTS] = {};
   HotCand* h_cand_s[HSLOTS] = {};
-  uint64_t sub_seq = 0;                         // batches submitted (slot = seq & 1, control block = seq % 3)
+  uint64_t sub_seq = 0;                         // batches submitted (host slot = seq % HSLOTS, device slot = seq & 1, control block = seq % 3)
   bool inputs_ready = false;                    // this submit's inputs are complete (pipelined submit)
   bool want_cand = true;                        // copy the hot-set candidates back after the next batch
   uint8_t* zero_block = nullptr;  // ctl | hist | lookbacks (zeroed per batch)
