@@ -222,7 +222,7 @@ def main():
         prof_dir = ROOT / "profiles"
         traffic = None
         # PMC traffic of this pipeline from the committed rocprofv3 --pmc passes (tools/profile_round.sh)
-        tf = prof_dir / {"v4": "r01_v6_pmc_traffic.json", "v3": "r01_v3_pmc_traffic.json", "v2": "r01_v2_pmc_traffic.json",
+        tf = prof_dir / {"v4": "r01_v7_pmc_traffic.json", "v3": "r01_v3_pmc_traffic.json", "v2": "r01_v2_pmc_traffic.json",
                          "lsd": "r01_pmc_traffic.json"}[args.pipeline]
         if tf.exists():
             try:
