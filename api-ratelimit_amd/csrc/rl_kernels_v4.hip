@@ -56,7 +56,8 @@ constexpr int RANGE_MAX = 128;             // ranges per MSD group (two per buck
 constexpr int R_START = MSD_GROUPS;
 constexpr int R_BPRE = R_START + MSD_GROUPS * (RANGE_MAX + 1);
 constexpr int R_GTOT = R_BPRE + MSD_BUCKETS;
-constexpr int RANGE_WORDS = R_GTOT + MSD_GROUPS;
+constexpr int R_BTOT = R_GTOT + MSD_GROUPS;  // per MSD bucket its batch total (k4_scan block pair hand-off)
+constexpr int RANGE_WORDS = R_BTOT + MSD_BUCKETS;
 constexpr int HOT_HALF = HOT_BUCKETS / 2;  // hot buckets per k4_group hot part
 constexpr int DONE_CTR = 27;               // EngineCtl::tile_ctr[DONE_CTR][0]: k4_group blocks done
 constexpr int G_NT = 256;
@@ -323,7 +324,13 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
 constexpr int SCAN_NT = 1024;
 constexpr int SCAN_W = SCAN_NT / 64;
 constexpr int SCAN_U = 16;  // column loads in flight per lane (columns longer than SCAN_Q)
-constexpr int SCAN_Q = 32;  // MSD column entries per lane kept in registers
+// MSD blocks come in pairs per group of 64 buckets: 32 buckets each over 32 tile slices
+// (lane = slice % 2 * 32 + bucket, wave = slice / 2), so 64 CUs pull the MSD columns; the
+// second block of a pair to finish packs the group's ranges from both blocks' totals.
+constexpr int MSD_HALF = 32;
+constexpr int MSD_SCAN_BLOCKS = 2 * MSD_GROUPS;
+constexpr int PAIR_CTR = 8;  // EngineCtl::tile_ctr[PAIR_CTR][g]: blocks of MSD group g done
+constexpr int SCAN_Q = 16;  // MSD column entries per lane kept in registers
 // Hot blocks take 16 buckets each over 64 tile slices (lane = slice % 4 * 16 + bucket, wave =
 // slice / 4): 32 blocks instead of 8, so the hot columns (u16 starts + u64 h sums of every
 // tile) are pulled by 32 CUs, 8 tiles per lane at config 3.
@@ -333,27 +340,29 @@ constexpr int HOT_SLICES = SCAN_NT / HOT_PER_BLOCK;
 constexpr int HOT_Q = 16;   // hot column entries per lane kept in registers
 static_assert(HOT_BUCKETS % 64 == 0 && V3_SCAN_BUCKETS % 64 == 0, "bucket blocks");
 static_assert(T < 65536 && SCAN_Q % 2 == 0, "per-tile counts pack in u16 pairs");
+static_assert(MSD_GROUPS <= 64 && PAIR_CTR != DONE_CTR && PAIR_CTR != DFR_CTR && PAIR_CTR != CAND_CTR &&
+                  (PAIR_CTR < INS_CTR0 || PAIR_CTR >= INS_CTR0 + INS_LINES) && PAIR_CTR >= SHARD_CTR0 + 8,
+              "pair counters: one control-block row of their own");
 
-// Counts of bucket b (= this lane's) in tiles [tb, tb + SCAN_Q) ∩ [tb, te): each lane loads
-// its bucket's start and takes the next bucket's start from the next lane; lane 63's next
-// start is the wave-uniform entry 64 of the block's row segment.
+// Counts of bucket b (= this lane's) in tiles [tb, tb + SCAN_Q) ∩ [tb, te), for 32-lane
+// segments of 32 consecutive buckets starting at b0: each lane loads its bucket's start and
+// takes the next bucket's start from the next lane; the segment's last lane takes entry 32
+// of the row segment.
 RL_DEV void column_counts(const uint16_t* __restrict__ tstart, uint32_t b, uint32_t b0, uint32_t tb, uint32_t te,
                           uint32_t (&cq)[SCAN_Q]) {
   const uint32_t lane = threadIdx.x & 63;
-  tb = __builtin_amdgcn_readfirstlane(tb);  // wave-uniform: the row-end loads are scalar
-  te = __builtin_amdgcn_readfirstlane(te);
   uint32_t e[SCAN_Q];
 #pragma unroll
   for (int u = 0; u < SCAN_Q; ++u) {
     const uint16_t* row = tstart + (size_t)(tb + u) * ROW;
     const bool v = tb + u < te;
     cq[u] = v ? (uint32_t)row[b] : 0u;
-    e[u] = v ? (uint32_t)row[b0 + 64] : 0u;
+    e[u] = v ? (uint32_t)row[b0 + MSD_HALF] : 0u;
   }
 #pragma unroll
   for (int u = 0; u < SCAN_Q; ++u) {
-    const uint32_t nx = __shfl_down(cq[u], 1, 64);
-    cq[u] = (lane < 63 ? nx : e[u]) - cq[u];
+    const uint32_t nx = __shfl_down(cq[u], 1, MSD_HALF);
+    cq[u] = ((lane & (MSD_HALF - 1u)) < MSD_HALF - 1u ? nx : e[u]) - cq[u];
   }
 }
 
@@ -389,11 +398,14 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     fv[w] = hotb && tid < ntiles ? fpart[(size_t)tid * FP_PART_WORDS + w] : 0u;
   // Column pass. MSD blocks: bucket b = lane, tiles [wave*Q, wave*Q + Q). Hot blocks: bucket
   // b = lane % 16 of the block's 16, tile slice wave * 4 + lane / 16.
-  const uint32_t m = blockIdx.x - HOT_SCAN_BLOCKS;  // MSD block (group of 64 buckets)
-  const uint32_t bb = lane & (HOT_PER_BLOCK - 1u);
-  const uint32_t nsl = hotb ? HOT_SLICES : SCAN_W;
-  const uint32_t slice = hotb ? wave * (64 / HOT_PER_BLOCK) + lane / HOT_PER_BLOCK : wave;
-  const uint32_t b = hotb ? blockIdx.x * HOT_PER_BLOCK + bb : HOT_BUCKETS + m * 64 + lane;
+  const uint32_t m2 = blockIdx.x - HOT_SCAN_BLOCKS;  // MSD block: half m2 & 1 of group m2 / 2
+  const uint32_t m = m2 >> 1, mh = m2 & 1u;
+  const uint32_t bpb = hotb ? HOT_PER_BLOCK : MSD_HALF;  // buckets per block
+  const uint32_t bb = lane & (bpb - 1u);
+  const uint32_t nsl = SCAN_NT / bpb;  // tile slices
+  const uint32_t slice = wave * (64 / bpb) + lane / bpb;
+  const uint32_t mb0 = HOT_BUCKETS + m * 64 + mh * MSD_HALF;  // MSD: first bucket of the block
+  const uint32_t b = hotb ? blockIdx.x * HOT_PER_BLOCK + bb : mb0 + bb;
   const uint32_t Q = (ntiles + nsl - 1) / nsl;
   const uint32_t tb = min(ntiles, slice * Q), te = min(ntiles, tb + Q);
   uint32_t c = 0;
@@ -416,7 +428,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     for (int u = 0; u < HOT_Q; ++u) hs += hq[u];
   } else if (in_regs) {
     uint32_t cq[SCAN_Q];
-    column_counts(tstart, b, HOT_BUCKETS + m * 64, tb, te, cq);
+    column_counts(tstart, b, mb0, tb, te, cq);
 #pragma unroll
     for (int u = 0; u < SCAN_Q; ++u) c += cq[u];
 #pragma unroll
@@ -490,12 +502,16 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
         hrun += sl < slice ? y : 0ull;
       }
     }
-  } else {
+  } else {  // bucket totals over the 32 slices; counts of the slices before this lane's
 #pragma unroll
     for (int w = 0; w < SCAN_W; ++w) {
-      const uint32_t x = s_pc[w][lane];
-      ctot += x;
-      crun += (uint32_t)w < wave ? x : 0u;
+#pragma unroll
+      for (int q = 0; q < 64 / MSD_HALF; ++q) {
+        const uint32_t sl = (uint32_t)(w * (64 / MSD_HALF) + q);
+        const uint32_t x = s_pc[w][q * MSD_HALF + bb];
+        ctot += x;
+        crun += sl < slice ? x : 0u;
+      }
     }
   }
   if (!hotb) {
@@ -525,10 +541,21 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     }
     if (wave != 0) return;
     ST5(3);
-    if (ctot > (uint32_t)BUCKET_CAP) atomicOr(&ctl->err, ERR_V2_FALLBACK);
+    if (lane == 0) heads_out[blockIdx.x] = 0;
+    // Hand-off inside the pair: this block's 32 bucket totals (lanes 0..31 = slice 0), then
+    // the pair counter; the second block to arrive reads both halves and packs the group.
+    if (lane < (uint32_t)MSD_HALF) {
+      if (ctot > (uint32_t)BUCKET_CAP) atomicOr(&ctl->err, ERR_V2_FALLBACK);
+      st_relaxed(&ranges[R_BTOT + mb], ctot);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t arrived = 0;
+    if (lane == 0) arrived = atomicAdd(&ctl->tile_ctr[PAIR_CTR][m], 1u);
+    if (__builtin_amdgcn_readfirstlane(arrived) == 0u) return;  // the other block packs
+    ctot = ld_relaxed(&ranges[R_BTOT + m * 64 + lane]);  // bucket lane of the group
     const uint32_t g = m;
     const uint32_t incl = v3::wave_incl_scan<uint32_t>(ctot);
-    ranges[R_BPRE + mb] = incl - ctot;
+    ranges[R_BPRE + m * 64 + lane] = incl - ctot;
     if (lane == 63) ranges[R_GTOT + g] = incl;
     // Pack the group's 64 buckets greedily into k4_group ranges of whole buckets holding at
     // most G_CAP records (a single larger bucket is a range of its own). The walk is
@@ -536,10 +563,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     // stores.
     uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
     uint32_t nr = 0, cur = 0, last = 0;  // last = rb[nr]
-    if (lane == 0) {
-      heads_out[blockIdx.x] = 0;
-      rb[0] = 0;
-    }
+    if (lane == 0) rb[0] = 0;
 #pragma unroll
     for (int k = 0; k < 64; ++k) {
       const uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)ctot, k);
@@ -1293,7 +1317,7 @@ __global__ __launch_bounds__(G_NT, 4) void k4_group(DevBatch in, MRec* __restric
 // ---------------------------------------------------------------------------
 uint32_t v4_tiles(uint32_t n) { return n ? (n + V3_TILE - 1) / V3_TILE : 1; }
 uint32_t v4_group_blocks(uint32_t) { return v4::GBLOCKS; }
-uint32_t v4_scan_blocks() { return v4::HOT_SCAN_BLOCKS + v4::MSD_GROUPS; }
+uint32_t v4_scan_blocks() { return v4::HOT_SCAN_BLOCKS + v4::MSD_SCAN_BLOCKS; }
 size_t v4_scratch_bytes() {
   using namespace v4;
   return (size_t)GBLOCKS * BUCKET_CAP * (8 + 2 + 2) + (size_t)GBLOCKS * GS_HASH * (4 + 4 + 2) + (size_t)GBLOCKS * 4 +

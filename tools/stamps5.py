@@ -34,7 +34,7 @@ print(eng.stats())
 st = np.zeros((4096, 8), np.uint64)
 eng.lib.rl_debug_st4.argtypes = [C.c_void_p]
 assert eng.lib.rl_debug_st4(st.ctypes.data) == 0
-a = st[2048:2048 + 64, :5].astype(np.int64)
+a = st[2048:2048 + 96, :5].astype(np.int64)
 t0 = a[:, 0].min()
 rel = (a - t0) / 100.0
 names = ["entry", "fold", "columns", "prefix", "tail"]
