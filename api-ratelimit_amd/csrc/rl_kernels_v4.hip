@@ -62,8 +62,13 @@ constexpr int HOT_HALF = HOT_BUCKETS / 2;  // hot buckets per k4_group hot part
 constexpr int DONE_CTR = 27;               // EngineCtl::tile_ctr[DONE_CTR][0]: k4_group blocks done
 constexpr int G_NT = 256;
 constexpr int G_W = G_NT / 64;
-constexpr int G_CAP = 640;      // records grouped in LDS (a larger pair runs bucket by bucket)
-constexpr int G_HASH = 1024;    // LDS hash slots (power of two > G_CAP)
+#ifndef RL_G_CAP
+#define RL_G_CAP 640
+#define RL_G_HASH 1024
+#define RL_G_OCC 4
+#endif
+constexpr int G_CAP = RL_G_CAP;    // records grouped in LDS (a larger pair runs bucket by bucket)
+constexpr int G_HASH = RL_G_HASH;  // LDS hash slots (power of two > G_CAP)
 constexpr int G_IPT = 3;        // positions per thread kept in registers (table read-ahead)
 constexpr int GS_HASH = 2048;   // global-scratch hash slots (> BUCKET_CAP)
 constexpr uint32_t G_EMPTY = 0xFFFFFFFFu;
@@ -1083,7 +1088,7 @@ struct GScratch4 {
   uint32_t* cursor;  // [GBLOCKS]
 };
 
-__global__ __launch_bounds__(G_NT, 4) void k4_group(DevBatch in, MRec* __restrict__ mrec,
+__global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __restrict__ mrec,
                                                  const DevRule* __restrict__ rules, TableDesc tab, int local_cache,
                                                  rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
                                                  const HotBucket3* __restrict__ hb, const Deferred* __restrict__ dfr,
