@@ -8,14 +8,17 @@
 namespace rlhip {
 
 // ---------------------------------------------------------------------------
-// Key fingerprint. A key is the exact byte string of
+// Key identity. A Redis key is the exact byte string of
 // GenerateCacheKey (src/limiter/cache_key.go:57-68) = prefix || decimal(window_start).
 // The prefix always ends in '_' and the decimal has none, so (prefix bytes,
-// window_start) <-> key string is a bijection; the fingerprint hashes exactly those
-// two parts, plus the unit (each unit has its own key space).
-// Two 64-bit lanes over 8-byte little-endian words (tail zero-padded, length folded
-// in). Each lane step is a bijection of the lane state for a fixed word, so two
-// equal-length prefixes that differ anywhere give different lane-a states.
+// window_start) <-> key string is a bijection; the fingerprint hashes exactly those two
+// parts and nothing else: a MINUTE key "p_3600" and an HOUR key "p_3600" are one string,
+// hence one table slot, exactly as they are one freecache entry (base_limiter.go:57-66)
+// and — without REDIS_PERSECOND, or for MINUTE/HOUR/DAY always — one Redis counter
+// (fixed_cache_impl.go:74-85). The slot holds both stores' counters.
+// Two 64-bit lanes over 8-byte little-endian words (tail zero-padded, length folded in).
+// Each lane step is a bijection of the lane state for a fixed word, so two equal-length
+// prefixes that differ anywhere give different lane-a states.
 // ---------------------------------------------------------------------------
 constexpr uint64_t K0 = 0x9E3779B97F4A7C15ull;
 constexpr uint64_t K1 = 0xC2B2AE3D27D4EB4Full;
@@ -30,19 +33,20 @@ __host__ __device__ __forceinline__ uint64_t fmix64(uint64_t x) {
   return x;
 }
 struct FpState { uint64_t a, b; };
-__host__ __device__ __forceinline__ FpState fp_init(uint32_t len, uint32_t unit, uint64_t seed) {
-  return FpState{seed ^ K0, (seed + K1) ^ ((uint64_t)len << 32) ^ (uint64_t)unit};
+__host__ __device__ __forceinline__ FpState fp_init(uint32_t len, uint64_t seed) {
+  return FpState{seed ^ K0, (seed + K1) ^ ((uint64_t)len << 32)};
 }
 __host__ __device__ __forceinline__ void fp_word(FpState& s, uint64_t w) {
   s.a = rotl64((s.a ^ w) * K2, 31);
   s.b = (s.b + w) * K3;
   s.b ^= s.b >> 29;
 }
+// Identity = (sort key: region | hi >> 3, lo & 0xFFFFFFFF): 93 bits.
 __host__ __device__ __forceinline__ void fp_final(FpState s, uint64_t window_start, uint64_t& hi, uint64_t& lo) {
   s.a ^= window_start * K1;
   s.b = (s.b ^ window_start) * K2;
   hi = fmix64(s.a + rotl64(s.b, 23));
-  lo = fmix64(s.b ^ (s.a * K5));
+  lo = fmix64(s.b ^ (s.a * K5)) & 0xFFFFFFFFull;
 }
 
 // Units (rl_hip.h RL_UNIT_*): divider = utils.UnitToDivider (src/utils/utilities.go:19-32)
@@ -50,9 +54,32 @@ __host__ __device__ __forceinline__ uint32_t unit_div(uint32_t unit) {
   return unit == RL_UNIT_SECOND ? 1u : unit == RL_UNIT_MINUTE ? 60u : unit == RL_UNIT_HOUR ? 3600u : 86400u;
 }
 
-// Sort key: [region:3 | fingerprint.hi >> 3]. region = (unit-1)*2 + (window_index & 1):
-// every (unit, window parity) owns one region of the counter table. ~0 marks nil-limit
-// descriptors, which sort last and are decided without the table.
+// Home unit of a key string: the largest unit whose divider divides its window start.
+// Every unit that can produce the string divides it, so all of them are <= home, and every
+// touch of the string happens inside the home unit's window [ws, ws + div(home)).
+__host__ __device__ __forceinline__ uint32_t home_unit(uint32_t ws) {
+  return ws % 86400u == 0 ? (uint32_t)RL_UNIT_DAY
+         : ws % 3600u == 0 ? (uint32_t)RL_UNIT_HOUR
+         : ws % 60u == 0   ? (uint32_t)RL_UNIT_MINUTE
+                           : (uint32_t)RL_UNIT_SECOND;
+}
+// Table region (home unit x window parity) and window generation (home window index + 1)
+// of a key string.
+struct Place { uint32_t region, gen; };
+__host__ __device__ __forceinline__ Place place_of(uint32_t ws) {
+  const uint32_t H = home_unit(ws);
+  const uint32_t w = ws / unit_div(H);
+  return Place{(H - 1u) * 2u + (w & 1u), w + 1u};
+}
+// Window start of every key of (region, gen).
+__host__ __device__ __forceinline__ uint32_t region_ws(uint32_t region, uint32_t gen) {
+  return (gen - 1u) * unit_div(region / 2u + 1u);
+}
+// Latest admissible request time: ws + div and t + div stay below 2^32.
+constexpr int64_t MAX_NOW = 0xFFFD0000ll;
+
+// Sort key: [region:3 | fingerprint.hi >> 3]. ~0 marks nil-limit descriptors, which sort
+// last and are decided without the table.
 constexpr uint64_t NIL_KEY = ~0ull;
 __host__ __device__ __forceinline__ uint64_t make_sort_key(uint32_t region, uint64_t hi) {
   uint64_t k = ((uint64_t)region << 61) | (hi >> 3);
@@ -60,20 +87,21 @@ __host__ __device__ __forceinline__ uint64_t make_sort_key(uint32_t region, uint
 }
 __host__ __device__ __forceinline__ uint32_t key_region(uint64_t k) { return (uint32_t)(k >> 61); }
 
-// Per-descriptor record written by the fingerprint kernel in arrival order (32 B).
+// Per-descriptor record written by the LSD fingerprint kernel in arrival order (32 B).
 struct __attribute__((aligned(16))) ItemRec {
   uint64_t fp_lo;    // low fingerprint lane (identity = (sort key, fp_lo))
   uint32_t rule;     // rule id or RL_NIL_RULE
   uint32_t req;      // request index
   uint32_t h;        // max(1, hits_addend)
   int32_t now_mod;   // now - window_start (CalculateReset: div - now % div)
-  uint32_t gen;      // window_index + 1 (0 = never-used slot)
+  uint32_t gen;      // home window index + 1 (0 = never-used slot)
   uint32_t pad;
 };
 
-// Per-descriptor record in sorted order written by the scan kernel (32 B).
+// Per-descriptor record in sorted order written by the LSD scan kernel (32 B).
 struct __attribute__((aligned(16))) SortedRec {
-  uint64_t P;        // inclusive prefix sum of h within the key's segment
+  uint64_t P;        // inclusive prefix sum of h within the key's segment (exotic keys: the
+                     // leader overwrites it with the INCRBY reply | local-hit << 32)
   uint32_t head;     // sorted position of the segment head; bit31: rule changes within segment so far
   uint32_t idx;      // arrival index
   uint32_t rule;
@@ -83,24 +111,33 @@ struct __attribute__((aligned(16))) SortedRec {
 };
 constexpr uint32_t HEAD_MIXED_RULE = 0x80000000u;
 
-// Per-segment decision state written by the leader kernel at the segment head (16 B).
+// Per-segment decision state written by the leader at the segment head (16 B).
 struct __attribute__((aligned(16))) SegInfo {
   uint64_t base;     // counter before this batch (INCRBY post-value = base + P)
-  uint32_t freeze;   // SEG_NO_FREEZE, SEG_FROZEN_BEFORE, or the request index R* that froze the key
+  uint32_t freeze;   // SEG_NO_FREEZE, SEG_FROZEN_BEFORE, SEG_EXOTIC, or the request R* that froze the key
   uint32_t pad;
 };
 constexpr uint32_t SEG_NO_FREEZE = 0xFFFFFFFFu;
 constexpr uint32_t SEG_FROZEN_BEFORE = 0xFFFFFFFEu;
+constexpr uint32_t SEG_EXOTIC = 0xFFFFFFFDu;  // per-descriptor replies (P = reply | local-hit << 32)
+constexpr uint64_t P_LOCAL_HIT = 1ull << 32;
 
-// Counter-table slot (32 B). word0 = gen | (fp_lo low 32 bits) << 32 is the claim word.
+// Counter-table slot (32 B): one Redis key string. word0 = gen | tag << 32 is the claim word.
+//   count/exp: the main store's counter (int64 in Redis, observed as uint32: fixed_cache_impl.go:51)
+//              and its expiry second (alive while now < exp; 0 = absent);
+//   pcount:    the per-second store's counter (REDIS_PERSECOND; only SECOND keys use it, all at
+//              now == window start, so its TTL never decides an outcome);
+//   frz:       the local over-limit cache entry of the string (freecache TTL = div of the rule
+//              that went over, base_limiter.go:102): frozen while now < frz; 0 = none.
 struct __attribute__((aligned(32))) Slot {
   uint64_t ctrl;     // gen (low 32) | tag = (uint32)fp_lo (high 32)
   uint64_t key;      // sort key (region | fp.hi >> 3)
-  uint32_t fp_lo_hi; // fp_lo >> 32
-  uint32_t flags;    // SLOT_FROZEN: local over-limit cache holds this key
-  uint64_t count;    // Redis counter value (INCRBY semantics, int64 in Redis)
+  uint32_t count;
+  uint32_t exp;
+  uint32_t pcount;
+  uint32_t frz;
 };
-constexpr uint32_t SLOT_FROZEN = 1u;
+static_assert(sizeof(Slot) == 32, "Slot is 32 B");
 
 // Rule table entry on the device.
 struct __attribute__((aligned(16))) DevRule {
@@ -112,13 +149,13 @@ struct __attribute__((aligned(16))) DevRule {
 
 // Device error flags (bitmask in EngineCtl.err).
 enum : uint32_t {
-  ERR_TABLE_FULL = 1u,
+  ERR_TABLE_FULL = 1u,    // a region would pass its load limit: refused before any table write
   ERR_SPIN = 2u,
-  ERR_NEED_RESORT = 4u,  // a sort-prefix run holds two different fingerprints
+  ERR_NEED_RESORT = 4u,   // a sort-prefix run holds two different fingerprints
   ERR_BAD_TIME = 8u,
   ERR_BAD_INPUT = 16u,    // rule id or request index out of range
   ERR_WINDOW_SPAN = 32u,  // a region saw window generations more than one apart in one batch
-  ERR_V2_FALLBACK = 64u,  // the bucketed pipeline cannot take this batch: rerun it on the LSD pipeline
+  ERR_FALLBACK = 64u,     // the bucketed pipeline cannot take this batch: rerun it on the LSD pipeline
 };
 
 // Small device control block, zeroed per batch. Same-line atomics serialise at the L2
@@ -126,34 +163,53 @@ enum : uint32_t {
 // either written once by a single reducer block or lives on a 256-B line of its own.
 struct EngineCtl {
   uint32_t err;          // atomicOr, only on an error
-  uint32_t n_nil;        // nil-limit descriptors (sorted to the tail); written by k_hist_scan
-  uint32_t n_segments;   // unique keys in the batch (U); written by k_leader block 0
-  uint32_t n_inserted;   // unused (new keys are counted in tile_ctr[INS_CTR0..])
-  uint32_t gen_min[8];   // per region: min window generation in the batch (k_hist_scan)
-  uint32_t gen_max[8];   // per region: max window generation in the batch (k_hist_scan)
-  uint32_t pad0[64 - 20];
-  uint32_t tile_ctr[32][64];  // dynamic tile tickets, one 256-B line each
+  uint32_t n_nil;        // nil-limit descriptors (sorted to the tail)
+  uint32_t n_segments;   // unique keys in the batch (U)
+  uint32_t n_inserted;   // new table slots of the batch (all regions)
+  uint32_t gen_min[8];   // per region: min window generation in the batch
+  uint32_t gen_max[8];   // per region: max window generation in the batch
+  uint32_t ins[8];       // per region: new table slots of the batch
+  uint32_t pad0[64 - 28];
+  uint32_t tile_ctr[32][64];  // dynamic tile tickets / hand-off counters, one 256-B line each
 };
 static_assert(sizeof(EngineCtl) == 256 + 32 * 256, "EngineCtl layout");
-// tile_ctr rows 16..23: per-batch new-key counters (k_leader, one row per wave id mod 8)
+// tile_ctr rows 16..23: per-region new-slot counters of the LSD leader (row INS_CTR0 + region)
 constexpr int INS_CTR0 = 16;
 constexpr int INS_LINES = 8;
-constexpr int FP_PART_WORDS = 17;  // per fingerprint block: 8 x ~min gen, 8 x max gen, nil count
 
-// Counter table: 8 regions (unit x window parity), region r has 2^region_log2[r] slots.
+// Per-block fingerprint partials: ~min / max home generation per region, nil count,
+// max unit window + 1 per (unit, window parity) (hot keys), descriptors per region.
+constexpr int FP_GMIN = 0, FP_GMAX = 8, FP_NIL = 16, FP_UW = 17, FP_CNT = 25;
+constexpr int FP_PART_WORDS = 33;
+__host__ __device__ __forceinline__ bool fp_is_max(int w) { return w < FP_NIL || (w >= FP_UW && w < FP_CNT); }
+
+// Counter table: 8 regions (home unit x window parity), region r has 2^region_log2[r] slots.
 struct TableDesc {
   Slot* slots;
   uint64_t region_base[8];  // slot offset of each region
   uint32_t region_log2[8];
+  uint32_t split;           // REDIS_PERSECOND: SECOND rules count in the per-second store
+  uint32_t local_cache;     // local over-limit cache on
+};
+__host__ __device__ __forceinline__ bool per_second_store(const TableDesc& t, uint32_t unit) {
+  return t.split && unit == RL_UNIT_SECOND;
+}
+
+// Per-region occupancy kept across batches (capacity check before any table write).
+struct RegionOcc {
+  uint32_t gen;    // window generation the count belongs to
+  uint32_t live;   // slots claimed for that generation
+  uint32_t limit;  // load limit (slots)
+  uint32_t pad;
 };
 
-// Hot-key set entry (v2 pipeline): a key prefix seen with many descriptors per batch.
-// (a, b) is the fingerprint lane state after the prefix bytes (length and unit folded in),
-// i.e. a 128-bit hash of (prefix bytes, unit); the window is not part of it.
+// Hot-key set entry: a key prefix seen with many descriptors per batch. (a, b) is the
+// fingerprint lane state after the prefix bytes (length folded in), i.e. a 128-bit hash of
+// the prefix bytes; the window is not part of it.
 struct __attribute__((aligned(32))) HotEntry {
   uint64_t a, b;
   uint32_t unit;
-  uint32_t rule;   // the rule id every hot descriptor must carry (else the batch falls back)
+  uint32_t rule;   // the rule id every descriptor of the prefix must carry (else the batch falls back)
   uint32_t idx;    // hot index 0..HOT_MAX-1; 0xFFFFFFFF = empty slot
   uint32_t pad;
 };
@@ -165,10 +221,6 @@ constexpr int MSD_BUCKETS = 1 << MSD_BITS;   // 11 fingerprint bits below the re
 constexpr int NBUCKETS = HOT_BUCKETS + MSD_BUCKETS + 1;
 constexpr uint32_t NIL_BUCKET = NBUCKETS - 1;
 constexpr int BUCKET_CAP = 1024;          // max descriptors in one MSD bucket on the fast path
-constexpr int BG_RANGE = 1024;            // k_bgroup: MSD buckets whose start lies in one 1024-window
-constexpr int BG_MAX = BG_RANGE + BUCKET_CAP;
-constexpr int V2_TILE = 4096;             // k_fp2 / k_bscatter arrival tile
-constexpr int HOT_CHUNK = 4096;           // k_bgroup hot-region chunk
 constexpr uint32_t HOT_MIN_SEG = 128;     // a new key joins the hot set with at least this many descriptors
 constexpr uint32_t HOT_CAND_MIN = 64;     // segments at least this long are reported (hot keys stay hot)
 constexpr int CAND_MAX = 1024;
@@ -179,44 +231,22 @@ struct __attribute__((aligned(16))) HotCand {
   uint32_t unit, rule, count, first_idx;  // first_idx ~0: (a, b, unit) already filled in
 };
 
-// Per-batch state of one hot bucket (one key): identity from k_fp2, table slot and base
-// from k_bscan, first over-limit position from k_bscatter; k_bgroup decides from it.
-struct __attribute__((aligned(16))) HotBucket {
-  uint64_t key;    // sort key (identical writes from every tile that sees the bucket)
-  uint64_t fp_lo;
-  uint64_t base;   // counter before this batch
-  uint64_t slot;   // Slot* of the key; 0 = no table update (empty bucket or error)
-  uint32_t gen;    // window generation
-  uint32_t flags;  // HB_FROZEN_PRE: the local cache already holds the key
-  uint32_t jpos;   // first bucket position whose INCRBY reply exceeds the limit (~0: none)
-  uint32_t pad;
-};
-constexpr uint32_t HB_FROZEN_PRE = 1u;
-
 // ---------------------------------------------------------------------------
-// v3 pipeline (rl_kernels_v3.hip)
+// v4 pipeline (rl_kernels_v4.hip)
 // ---------------------------------------------------------------------------
-constexpr int V3_TILE = 2048;             // k3_hist / k3_place arrival tile
-constexpr int V3_THREADS = 512;
-constexpr int V3_ROW16 = (NBUCKETS + 7) / 8 * 8;  // tile histogram row (u16 counts)
-constexpr int V3_SCAN_BUCKETS = HOT_BUCKETS + MSD_BUCKETS;  // buckets k3_scan scans (not NIL)
-#ifndef RL_V3_GRANGE
-#define RL_V3_GRANGE 256
-#endif
-constexpr int V3_GRANGE = RL_V3_GRANGE;            // k3_group: MSD buckets whose start lies in one 256-window
-constexpr int V3_GCAP = 768;              // k3_group: records staged in LDS (larger ranges run in place)
-constexpr int V3_GHASH = 1024;            // k3_group: LDS hash slots (power of two, > V3_GCAP)
-constexpr int V3_RULE_BITS = 15;          // MRec.rn = rule | now_mod << 15 (now_mod < 86400 < 2^17)
-constexpr uint32_t V3_MAX_RULES = 1u << V3_RULE_BITS;
+constexpr int V4_TILE = 2048;             // k4_hist / k4_place arrival tile
+constexpr int V4_THREADS = 512;
+constexpr int V4_ROW16 = (NBUCKETS + 7) / 8 * 8;  // tile row of u16 bucket starts
+constexpr int V4_RULE_BITS = 15;          // MRec.rn = rule | now_mod << 15 (now_mod < 86400 < 2^17)
+constexpr uint32_t V4_MAX_RULES = 1u << V4_RULE_BITS;
 constexpr int DFR_CTR = 29;               // EngineCtl::tile_ctr[DFR_CTR][0] counts deferred hot descriptors
-constexpr int SCAN_CTR = 28;              // EngineCtl::tile_ctr[SCAN_CTR][0]: k3_scan blocks done
 
 // Multi-GPU: a descriptor routed to the GPU that owns its key (32 B). The owner needs the
 // key identity before the window (prefix lanes), the request time, the rule, hits_addend and
 // a request id that orders requests across origins: origin << ROUTE_REQ_BITS | request.
 struct __attribute__((aligned(16))) RRec {
-  uint64_t a, b;     // fingerprint lane state after the key-prefix bytes (unit folded in)
-  uint32_t now;      // request time, unix seconds (< 2^32, checked at the origin)
+  uint64_t a, b;     // fingerprint lane state after the key-prefix bytes
+  uint32_t now;      // request time, unix seconds (<= MAX_NOW, checked at the origin)
   uint32_t rule;     // rule id (every shard loads the same rule table)
   uint32_t h;        // max(1, hits_addend)
   uint32_t greq;     // global request id
@@ -241,59 +271,38 @@ constexpr uint8_t ROUTE_LOCAL = 0xFF;  // descriptor decided at the origin (nil 
 // every record has its own ThrottleMillis slot.
 constexpr uint32_t RL_BATCH_ROUTED = 1u;
 
-// Per-descriptor record in arrival order (32 B), written by k3_hist, read by k3_place.
-struct __attribute__((aligned(16))) ARec {
-  uint64_t kp;       // MSD: sort key; hot: INCRBY prefix of the key inside the tile (inclusive)
-  uint64_t lo;       // fp_lo
-  uint32_t req;      // request index
-  uint32_t h;        // max(1, hits_addend)
-  uint32_t rn;       // rule | now_mod << V3_RULE_BITS
-  uint16_t bucket;   // hot / MSD / NIL_BUCKET
-  uint16_t rank;     // MSD: position inside (tile, bucket)
-};
-
-// MSD descriptor in bucket order (32 B), written by k3_place, grouped by k3_group.
+// MSD descriptor record (32 B): tile-sorted (k4_hist) and in bucket order (k4_place,
+// grouped by k4_group). A hot record carries its in-tile INCRBY prefix in `key` and its hot
+// bucket in `fp_lo`.
 struct __attribute__((aligned(16))) MRec {
   uint64_t key;      // sort key (region | fp.hi >> 3)
   uint64_t fp_lo;
   uint32_t idx;      // arrival index
   uint32_t req;      // request index
   uint32_t h;        // max(1, hits_addend)
-  uint32_t rn;       // rule | now_mod << V3_RULE_BITS
+  uint32_t rn;       // rule | now_mod << V4_RULE_BITS
 };
 
-// Per-batch state of one hot bucket (one key) in the v3 pipeline. k3_scan fills it (table
-// claim, counter before the batch, h total); k3_place records the freezing request.
-struct __attribute__((aligned(16))) HotBucket3 {
+// Per-batch state of one hot bucket (one key). k4_scan fills it (table claim, counter before
+// the batch, h total); k4_place records the freezing request and the times the last INCRBY
+// happened at (exact EXPIRE / freecache TTLs, finalised by k4_group's last block).
+struct __attribute__((aligned(16))) HotBucket {
   uint64_t key;
   uint64_t fp_lo;
   uint64_t base;    // counter before this batch
   uint64_t slot;    // Slot* of the key; 0 = bucket empty (or batch rejected)
   uint64_t total;   // sum of h over the bucket's descriptors
   uint32_t rule;
-  uint32_t flags;   // HB_FROZEN_PRE
+  uint32_t flags;   // HB_FROZEN_PRE | HB_PS
   uint32_t rstar;   // request that froze the key in this batch (local cache), ~0 = none yet
-  uint32_t pad[3];
+  uint32_t ws;      // window start of the key string
+  uint32_t t_all;   // time of the key's last descriptor of the batch (P == total)
+  uint32_t t_rstar; // time of the freezing request
 };
+constexpr uint32_t HB_FROZEN_PRE = 1u;  // the local cache holds the key for the whole batch
+constexpr uint32_t HB_PS = 2u;          // counts in the per-second store
 
-// Global scratch of k3_group for ranges too large for LDS (indexed by bucket-order position;
-// slot/cnt/base hold 4 words per position; base holds each key's list end).
-struct V3GroupScratch {
-  uint64_t* key;
-  uint64_t* lo;
-  uint4* pay;
-  uint64_t* P;
-  uint32_t* slot;
-  uint32_t* cnt;
-  uint32_t* base;
-  uint32_t* list;
-  uint32_t* grp;
-  uint32_t* rank;
-  uint32_t* tail;
-  uint32_t* cursor;  // one word per k3_group workgroup
-};
-
-// A hot descriptor whose decision needs the freezing request of an earlier tile (k3_group).
+// A hot descriptor whose decision needs the freezing request of an earlier tile (k4_group).
 struct __attribute__((aligned(16))) Deferred {
   uint64_t P;        // INCRBY prefix of the key up to and including this descriptor
   uint32_t idx, bucket, req, h, rule, now_mod;

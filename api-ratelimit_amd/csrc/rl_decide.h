@@ -1,15 +1,16 @@
 // rl_decide.h — per-key table update and per-descriptor decision, shared by the LSD
-// pipeline (k_leader / k_decide) and the bucketed pipeline (k_bscan / k_bgroup).
+// pipeline (k_leader / k_decide) and the v4 pipeline (k4_scan / k4_place / k4_group).
 #pragma once
 #include "rl_device.h"
 
 namespace rlhip {
 
-constexpr uint32_t MAX_PROBE = 4096;
-
 // Find the slot of (key, fp_lo) for window generation G in its region, or claim an empty one
-// (a slot whose generation is older than G is empty for this window: window expiry).
-// Returns false when MAX_PROBE slots are all taken.
+// (a slot whose generation is older than G is empty for this window: window expiry). The
+// capacity check (RegionOcc, before any table write) keeps every region below its load
+// limit, so a free slot always exists within the region: the probe is bounded by its size.
+// A claimed slot is reset by the caller (slot_reset) before anything reads it: a key's slot
+// is only ever looked up by the key's one leader of the batch.
 RL_DEV bool table_claim(const TableDesc& tab, uint64_t key, uint64_t fp_lo, uint32_t G, Slot*& slot_out,
                         bool& existed_out) {
   const uint32_t region = key_region(key);
@@ -18,19 +19,17 @@ RL_DEV bool table_claim(const TableDesc& tab, uint64_t key, uint64_t fp_lo, uint
   Slot* rbase = tab.slots + tab.region_base[region];
   uint64_t pos = (key << 3) >> (64 - lg);  // top lg bits below the region bits
   const uint32_t tag = (uint32_t)fp_lo;
-  const uint32_t lohi = (uint32_t)(fp_lo >> 32);
   Slot* slot = nullptr;
   bool existed = false;
-  for (uint32_t probe = 0; probe < MAX_PROBE;) {
+  for (uint64_t probe = 0; probe <= mask;) {
     Slot* s = rbase + (pos & mask);
-    // ctrl by an L1-bypassing atomic load (it may be CASed concurrently); the identity
-    // words in the same load burst (written by earlier batches, or by a concurrent
-    // claimer of a different key, which can never match).
+    // ctrl by an L1-bypassing atomic load (it may be CASed concurrently); the key word is
+    // written by earlier batches, or by a concurrent claimer of a different key, which can
+    // never match.
     const uint64_t c = ld_relaxed64(&s->ctrl);
     const uint64_t skey = s->key;
-    const uint32_t slohi = s->fp_lo_hi;
     const uint32_t g = (uint32_t)c;
-    if (g == G && (uint32_t)(c >> 32) == tag && skey == key && slohi == lohi) {
+    if (g == G && (uint32_t)(c >> 32) == tag && skey == key) {
       slot = s;
       existed = true;
       break;
@@ -60,11 +59,16 @@ RL_DEV Slot* slot_first(const TableDesc& tab, uint64_t key) {
   return tab.slots + tab.region_base[region] + (((key << 3) >> (64 - lg)) & ((1ull << lg) - 1ull));
 }
 
+// The per-key state of a slot: both stores' counters, the main counter's expiry and the
+// local-cache entry's expiry (rl_common.h Slot).
+struct KeyState {
+  uint32_t count, exp, pcount, frz;
+};
+
 // A whole 32-B slot, read ahead of its use with two 16-B loads (table_claim_pre).
 struct SlotView {
   uint64_t ctrl, key;
-  uint32_t lohi, flags;
-  uint64_t count;
+  KeyState st;
 };
 RL_DEV SlotView load_slot(const Slot* s) {
   const uint4 a = reinterpret_cast<const uint4*>(s)[0];
@@ -72,51 +76,60 @@ RL_DEV SlotView load_slot(const Slot* s) {
   SlotView v;
   v.ctrl = (uint64_t)a.x | ((uint64_t)a.y << 32);
   v.key = (uint64_t)a.z | ((uint64_t)a.w << 32);
-  v.lohi = b.x;
-  v.flags = b.y;
-  v.count = (uint64_t)b.z | ((uint64_t)b.w << 32);
+  v.st = KeyState{b.x, b.y, b.z, b.w};
   return v;
+}
+RL_DEV KeyState read_state(const Slot* s) {
+  const uint4 b = reinterpret_cast<const uint4*>(s)[1];
+  return KeyState{b.x, b.y, b.z, b.w};
+}
+RL_DEV void write_state(Slot* s, const KeyState& k) {
+  uint4 v;
+  v.x = k.count;
+  v.y = k.exp;
+  v.z = k.pcount;
+  v.w = k.frz;
+  reinterpret_cast<uint4*>(s)[1] = v;
+}
+// A freshly claimed slot: the string is absent from both stores and from the local cache.
+RL_DEV void slot_reset(Slot* s, uint64_t key) {
+  s->key = key;
+  write_state(s, KeyState{0, 0, 0, 0});
 }
 
 // table_claim with the first probe slot already read (pre). The read-ahead may predate a
 // concurrent claim of that slot by another key: a claim is permanent for the window
 // generation, so a stale "taken by another key" stays true, a stale "free" makes the CAS
 // fail and the slot is re-read. A key's own slot is only claimed by its own leader, and
-// count/flags are only written by that leader, so the read-ahead values of the key's slot
-// are current. Also returns the counter and flags of an existing slot.
+// its state is only written by that leader, so the read-ahead state of the key's slot is
+// current. Returns the state of an existing slot (zeros for a claimed one).
 RL_DEV bool table_claim_pre(const TableDesc& tab, uint64_t key, uint64_t fp_lo, uint32_t G, const SlotView pre,
-                            Slot*& slot_out, bool& existed_out, uint64_t& count_out, uint32_t& flags_out) {
+                            Slot*& slot_out, bool& existed_out, KeyState& st_out) {
   const uint32_t region = key_region(key);
   const uint32_t lg = tab.region_log2[region];
   const uint64_t mask = (1ull << lg) - 1ull;
   Slot* rbase = tab.slots + tab.region_base[region];
   uint64_t pos = (key << 3) >> (64 - lg);
   const uint32_t tag = (uint32_t)fp_lo;
-  const uint32_t lohi = (uint32_t)(fp_lo >> 32);
   bool use_pre = true;
   slot_out = nullptr;
   existed_out = false;
-  count_out = 0;
-  flags_out = 0;
-  for (uint32_t probe = 0; probe < MAX_PROBE;) {
+  st_out = KeyState{0, 0, 0, 0};
+  for (uint64_t probe = 0; probe <= mask;) {
     Slot* s = rbase + (pos & mask);
     uint64_t c, skey;
-    uint32_t slohi;
     if (use_pre) {
       c = pre.ctrl;
       skey = pre.key;
-      slohi = pre.lohi;
     } else {
       c = ld_relaxed64(&s->ctrl);
       skey = s->key;
-      slohi = s->fp_lo_hi;
     }
     const uint32_t g = (uint32_t)c;
-    if (g == G && (uint32_t)(c >> 32) == tag && skey == key && slohi == lohi) {
+    if (g == G && (uint32_t)(c >> 32) == tag && skey == key) {
       slot_out = s;
       existed_out = true;
-      count_out = use_pre ? pre.count : s->count;
-      flags_out = use_pre ? pre.flags : s->flags;
+      st_out = use_pre ? pre.st : read_state(s);
       return true;
     }
     if (g < G) {  // empty for this window generation: claim it
@@ -136,7 +149,106 @@ RL_DEV bool table_claim_pre(const TableDesc& tab, uint64_t key, uint64_t fp_lo, 
   return false;
 }
 
-// Report a long segment as a hot-set candidate for the next batch (bucketed pipeline).
+// Fast-path state of a key all of whose descriptors in the batch have one unit (one store),
+// touched inside its window [ws, ws + div): the counter before the batch and whether the
+// local cache holds the key for the whole batch. False when an expiry can fall among the
+// batch's touches (a string shared by units of different sizes): the key then
+// takes the exact sequential path (exotic_sequence).
+//   EXPIRE key div (fixed_cache_impl.go:69-72, jitter 0): alive while now < exp;
+//   freecache Set(key, TTL = div) (base_limiter.go:102): hit while now < frz.
+RL_DEV bool fast_state(const KeyState& s, bool ps, bool local_cache, uint32_t ws, uint32_t div, uint64_t& base,
+                       bool& frozen_pre) {
+  if (ps) base = s.pcount;
+  else if (s.exp <= ws) base = 0;
+  else if (s.exp >= ws + div) base = s.count;
+  else return false;
+  if (!local_cache || s.frz <= ws) frozen_pre = false;
+  else if (s.frz >= ws + div) frozen_pre = true;
+  else return false;
+  return true;
+}
+
+// One descriptor of a key's batch sequence, for the sequential path.
+struct SeqItem {
+  uint32_t req, t, h, rule;
+};
+
+// Exact serial DoLimit of one key's descriptors (positions 0..n-1 in arrival order), for keys
+// the fast path cannot take. Per request: every descriptor of the key sees the local-cache
+// lookup made before the request's INCRBYs (fixed_cache_impl.go:55-86); each INCRBY goes to
+// its store (main or per-second, :74-85), a main counter past its EXPIRE restarts at 0; then
+// every descriptor whose reply exceeds its limit Sets the local cache with TTL = its unit's
+// divider (base_limiter.go:94-106), the last Set winning. put(q, reply | P_LOCAL_HIT).
+template <class Get, class Put>
+RL_DEV void exotic_sequence(KeyState& s, const TableDesc& tab, const DevRule* __restrict__ rules, uint32_t n, Get get,
+                            Put put) {
+  uint32_t e = 0;
+  while (e < n) {
+    const SeqItem d0 = get(e);
+    const bool hit = tab.local_cache && d0.t < s.frz;
+    uint32_t f = e;
+    bool set = false;
+    uint32_t nf = 0;
+    for (; f < n; ++f) {
+      const SeqItem d = f == e ? d0 : get(f);
+      if (d.req != d0.req) break;
+      if (hit) {
+        put(f, P_LOCAL_HIT);
+        continue;
+      }
+      const DevRule R = rules[d.rule];
+      uint32_t after;
+      if (per_second_store(tab, R.unit)) {
+        s.pcount += d.h;
+        after = s.pcount;
+      } else {
+        if (d.t >= s.exp) s.count = 0;  // expired (or absent): INCRBY starts from 0
+        s.count += d.h;
+        s.exp = d.t + R.div;
+        after = s.count;
+      }
+      put(f, (uint64_t)after);
+      if (tab.local_cache && after > R.L) {
+        set = true;
+        nf = d.t + R.div;
+      }
+    }
+    if (set) s.frz = nf;
+    e = f;
+  }
+}
+
+// Capacity check, before any table write: every region the batch touches must
+// stay within its load limit even if each of its descriptors claimed a new slot. Counts are
+// per window generation: a newer generation finds the region empty (its older slots are
+// free for it). gmax / cnt: the batch's generation and descriptor count per region.
+RL_DEV uint32_t region_live(const RegionOcc& o, uint32_t gen) { return (o.gen < gen) ? 0u : o.live; }
+RL_DEV bool capacity_ok(const RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* cnt) {
+  bool ok = true;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    if (!cnt[r]) continue;
+    const RegionOcc o = occ[r];
+    ok &= (uint64_t)region_live(o, gmax[r]) + cnt[r] <= (uint64_t)o.limit;
+  }
+  return ok;
+}
+// After the batch: add its new slots (one thread).
+RL_DEV void occ_update(RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* ins) {
+  for (int r = 0; r < 8; ++r) {
+    if (!gmax[r]) continue;  // region untouched
+    RegionOcc o = occ[r];
+    if (o.gen < gmax[r]) {
+      o.gen = gmax[r];
+      o.live = ins[r];
+    } else {
+      o.live += ins[r];
+    }
+    occ[r] = o;
+  }
+}
+
+// Report a long segment as a hot-set candidate for the next batch.
 RL_DEV void emit_candidate(EngineCtl* ctl, HotCand* __restrict__ cand, uint32_t rule, uint32_t count,
                            uint32_t first_idx, uint64_t a = 0, uint64_t b = 0, uint32_t unit = 0) {
   const uint32_t c = atomicAdd(&ctl->tile_ctr[CAND_CTR][0], 1u);
@@ -152,21 +264,24 @@ RL_DEV void emit_candidate(EngineCtl* ctl, HotCand* __restrict__ cand, uint32_t 
   }
 }
 
-// New-key count for the engine stats: one atomic per wave, spread over INS_LINES lines.
-RL_DEV void count_inserts(bool inserted, EngineCtl* ctl) {
-  const uint64_t ins = __ballot(inserted);
-  if (ins && (threadIdx.x & 63) == (uint32_t)(__ffsll((unsigned long long)__ballot(1)) - 1))
-    atomicAdd(&ctl->tile_ctr[INS_CTR0 + ((blockIdx.x * 4 + (threadIdx.x >> 6)) & (INS_LINES - 1))][0],
-              (uint32_t)__popcll(ins));
+// New-slot count per region (LSD leader): one atomic per wave and region on the region's line.
+RL_DEV void count_inserts(bool inserted, uint32_t region, EngineCtl* ctl) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (uint32_t r = 0; r < 8; ++r) {
+    const uint64_t m = __ballot(inserted && region == r);
+    if (m && lane == (uint32_t)(__ffsll((unsigned long long)m) - 1))
+      atomicAdd(&ctl->tile_ctr[INS_CTR0 + r][0], (uint32_t)__popcll(m));
+  }
 }
 
 // Table update for the segment [hp, j] of the sorted order (one unique key): INCRBY of the
-// whole segment in serial order, local-cache freeze (fixed_cache_impl.go:55-123,
-// base_limiter.go:88-106). Writes the key's SegInfo at seg[hp].
+// whole segment in serial order, EXPIRE, local-cache freeze (fixed_cache_impl.go:55-123,
+// base_limiter.go:88-106). Writes the key's SegInfo at seg[hp]; an exotic key (fast_state
+// false, or units mixed in the segment) gets per-descriptor replies in srec[k].P.
 RL_DEV void leader_segment(uint32_t hp, uint32_t j, const SortedRec& tail, bool mixed_rule,
-                           const uint64_t* __restrict__ skeys, const SortedRec* __restrict__ srec,
+                           const uint64_t* __restrict__ skeys, SortedRec* __restrict__ srec,
                            const ItemRec* __restrict__ recs, const DevRule* __restrict__ rules, const TableDesc& tab,
-                           int local_cache, SegInfo* __restrict__ seg, EngineCtl* ctl) {
+                           SegInfo* __restrict__ seg, EngineCtl* ctl) {
   const uint64_t key = skeys[j];
   const ItemRec rec = recs[tail.idx];
   const uint32_t region = key_region(key);
@@ -179,38 +294,54 @@ RL_DEV void leader_segment(uint32_t hp, uint32_t j, const SortedRec& tail, bool 
   Slot* slot = nullptr;
   bool existed = false;
   if (!table_claim(tab, key, rec.fp_lo, rec.gen, slot, existed)) {
-    atomicOr(&ctl->err, ERR_TABLE_FULL);
+    atomicOr(&ctl->err, ERR_TABLE_FULL);  // unreachable below the load limit
     return;
   }
+  if (!existed) slot_reset(slot, key);
+  count_inserts(!existed, region, ctl);
+  KeyState ks = existed ? read_state(slot) : KeyState{0, 0, 0, 0};
+  const uint32_t ws = region_ws(region, rec.gen);
+  const DevRule R0 = rules[tail.rule];
+  bool exotic = false;
+  if (mixed_rule)
+    for (uint32_t k = hp; k <= j; ++k) exotic |= rules[srec[k].rule].unit != R0.unit;
+  const bool ps = per_second_store(tab, R0.unit);
   uint64_t base = 0;
   bool frozen_pre = false;
-  if (existed) {
-    base = slot->count;
-    frozen_pre = (slot->flags & SLOT_FROZEN) != 0;
-  } else {
-    slot->key = key;
-    slot->fp_lo_hi = (uint32_t)(rec.fp_lo >> 32);
+  if (!exotic) exotic = !fast_state(ks, ps, tab.local_cache != 0, ws, R0.div, base, frozen_pre);
+  SegInfo si;
+  si.pad = 0;
+  if (exotic) {
+    exotic_sequence(
+        ks, tab, rules, j - hp + 1,
+        [&](uint32_t q) {
+          const SortedRec r = srec[hp + q];
+          return SeqItem{r.req, ws + (uint32_t)r.now_mod, r.h, r.rule};
+        },
+        [&](uint32_t q, uint64_t v) { srec[hp + q].P = v; });
+    write_state(slot, ks);
+    si.base = 0;
+    si.freeze = SEG_EXOTIC;
+    seg[hp] = si;
+    return;
   }
-  count_inserts(!existed, ctl);
-
   uint32_t freeze = SEG_NO_FREEZE;
+  uint32_t last = j;  // the last descriptor whose INCRBY happens
   uint64_t final_count = base + tail.P;
   if (frozen_pre) {
     // every descriptor is a local-cache hit: no INCRBY (fixed_cache_impl.go:61-65)
     freeze = SEG_FROZEN_BEFORE;
-    final_count = base;
-  } else if (local_cache) {
+  } else if (tab.local_cache) {
     // first descriptor whose INCRBY reply exceeds its limit (base_limiter.go:88,94-106);
     // all later requests of this key are local-cache hits.
     uint32_t jstar = 0xFFFFFFFFu;
-    const uint32_t L0 = rules[tail.rule].L;
     if (!mixed_rule && base + tail.P < (1ull << 32)) {
       // after = base + P is strictly increasing in the segment: binary search.
-      if ((uint64_t)(uint32_t)(base + tail.P) > L0) {
+      if ((uint64_t)(uint32_t)(base + tail.P) > R0.L) {
         uint32_t lo_i = hp, hi_i = j;
         while (lo_i < hi_i) {
           const uint32_t mid = lo_i + (hi_i - lo_i) / 2;
-          if (base + srec[mid].P > (uint64_t)L0) hi_i = mid; else lo_i = mid + 1;
+          if (base + srec[mid].P > (uint64_t)R0.L) hi_i = mid; else lo_i = mid + 1;
         }
         jstar = lo_i;
       }
@@ -222,20 +353,25 @@ RL_DEV void leader_segment(uint32_t hp, uint32_t j, const SortedRec& tail, bool 
     }
     if (jstar != 0xFFFFFFFFu) {
       const uint32_t rstar = srec[jstar].req;
-      uint32_t last = jstar;
+      last = jstar;
       while (last < j && srec[last + 1].req == rstar) ++last;
       freeze = rstar;
       final_count = base + srec[last].P;
     }
   }
-  slot->count = final_count;
-  if (freeze != SEG_NO_FREEZE && freeze != SEG_FROZEN_BEFORE) slot->flags = slot->flags | SLOT_FROZEN;
-  if (!existed && freeze == SEG_NO_FREEZE) slot->flags = 0;
-  if (!existed && freeze != SEG_NO_FREEZE && freeze != SEG_FROZEN_BEFORE) slot->flags = SLOT_FROZEN;
-  SegInfo si;
+  if (freeze != SEG_FROZEN_BEFORE) {
+    const uint32_t t_last = ws + (uint32_t)srec[last].now_mod;
+    if (ps) {
+      ks.pcount = (uint32_t)final_count;
+    } else {
+      ks.count = (uint32_t)final_count;
+      ks.exp = t_last + R0.div;
+    }
+    if (freeze != SEG_NO_FREEZE) ks.frz = t_last + R0.div;
+    write_state(slot, ks);
+  }
   si.base = base;
   si.freeze = freeze;
-  si.pad = 0;
   seg[hp] = si;
 }
 
@@ -250,14 +386,21 @@ RL_DEV void decide_one(const SortedRec& r, const SegInfo& si, const DevRule& R, 
   st.reset_s = reset;
   st.over_limit_delta = 0;
   st.near_limit_delta = 0;
-  const bool local_hit = si.freeze == SEG_FROZEN_BEFORE || (si.freeze != SEG_NO_FREEZE && r.req > si.freeze);
+  bool local_hit;
+  uint32_t after;
+  if (si.freeze == SEG_EXOTIC) {
+    local_hit = (r.P & P_LOCAL_HIT) != 0;
+    after = (uint32_t)r.P;
+  } else {
+    local_hit = si.freeze == SEG_FROZEN_BEFORE || (si.freeze != SEG_NO_FREEZE && r.req > si.freeze);
+    after = (uint32_t)(si.base + r.P);
+  }
   uint32_t throttle = 0;
   if (local_hit) {
     st.code_flags = RL_CODE_OVER_LIMIT | ((RL_FLAG_HAS_LIMIT | RL_FLAG_LOCAL_CACHE_HIT) << 8);
     st.limit_remaining = 0;
     st.over_limit_delta = h;
   } else {
-    const uint32_t after = (uint32_t)(si.base + r.P);
     const uint32_t before = after - h;
     const uint32_t L = R.L, near = R.near;
     if (after > L) {

@@ -1,4 +1,4 @@
-// rl_device.h — device helpers shared by the v1 (LSD sort) and v2 (bucketed) pipelines.
+// rl_device.h — device helpers shared by the LSD and v4 pipelines.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -1,16 +1,18 @@
 // rl_engine.cpp — host runtime behind the C ABI in include/rl_hip.h.
 //
-// Owns the HBM counter table, the per-batch scratch, one HIP stream, and the launch
-// sequence of the decision pipeline (rl_kernels.hip). The host path mirrors what
-// fixedRateLimitCacheImpl.DoLimit does around redis PipeDo (src/redis/fixed_cache_impl.go:
-// 91-102): ship the batch, run it, bring the per-descriptor INCRBY outcomes back — except
-// that the decisions themselves are also computed on the device.
+// Owns the HBM counter table, the per-batch scratch, the HIP streams, the pinned host
+// staging and the launch sequence of the decision pipelines (rl_kernels_v4.hip, default;
+// rl_kernels.hip, LSD fallback). The host path mirrors what fixedRateLimitCacheImpl.DoLimit
+// does around redis PipeDo (src/redis/fixed_cache_impl.go:91-102): ship the batch, run it,
+// bring the per-descriptor outcomes back — except that the decisions themselves are also
+// computed on the device, and up to RL_MAX_IN_FLIGHT batches overlap (copies in, kernels,
+// copies out), as radix's implicit pipelining overlaps round trips (driver_impl.go:84-89).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
-#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -23,7 +25,8 @@ namespace rlhip {
 void launch_fingerprint(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint64_t*, ItemRec*,
                         rl_status*, uint32_t*, uint32_t*, EngineCtl*);
 void launch_histogram(hipStream_t, const uint64_t*, uint32_t, int, int, uint32_t*, const uint32_t*, uint32_t*);
-void launch_hist_scan(hipStream_t, const uint32_t*, uint32_t, uint32_t*, int, const uint32_t*, EngineCtl*);
+void launch_hist_scan(hipStream_t, const uint32_t*, uint32_t, uint32_t*, int, const uint32_t*, const RegionOcc*,
+                      EngineCtl*);
 uint32_t hist_blocks(uint32_t n);
 uint32_t hist_sub_words();
 void launch_fallback_lo_keys(hipStream_t, const ItemRec*, const uint64_t*, uint32_t, uint64_t*, uint32_t*);
@@ -34,48 +37,18 @@ void launch_sort_pass(hipStream_t, const uint64_t*, const uint32_t*, uint64_t*, 
                       const uint32_t*, uint32_t*, uint32_t*, EngineCtl*);
 void launch_scan(hipStream_t, const uint64_t*, const uint32_t*, const ItemRec*, uint32_t, int, int, SortedRec*,
                  uint64_t*, uint64_t*, uint32_t*, uint32_t*, EngineCtl*);
-void launch_leader(hipStream_t, const uint64_t*, const SortedRec*, const ItemRec*, const DevRule*, uint32_t,
-                   const TableDesc&, int, SegInfo*, const uint32_t*, uint32_t, HotCand*, EngineCtl*);
-uint32_t v2_tiles(uint32_t n);
-uint32_t v2_msd_wgs(uint32_t n);
-uint32_t v2_hot_wgs(uint32_t n);
-void launch_fp2(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, const HotEntry*, uint64_t*,
-                ItemRec*, uint16_t*, uint32_t*, rl_status*, uint32_t*, uint32_t*, uint32_t*, unsigned long long*,
-                HotBucket*, EngineCtl*);
-void launch_bscan(hipStream_t, const uint32_t*, const unsigned long long*, uint32_t, uint32_t*, unsigned long long*,
-                  uint32_t*, const uint32_t*, const HotEntry*, HotBucket*, const TableDesc&, HotCand*, EngineCtl*);
-void launch_bscatter(hipStream_t, const uint64_t*, const ItemRec*, const uint16_t*, const uint32_t*, uint32_t,
-                     const uint32_t*, const uint32_t*, const unsigned long long*, uint64_t*, ItemRec*, uint64_t*,
-                     uint32_t*, HotBucket*, const DevRule*, int, EngineCtl*);
-void launch_bgroup(hipStream_t, const uint64_t*, const ItemRec*, const uint64_t*, const uint32_t*, uint32_t,
-                   uint64_t*, SortedRec*, uint32_t*, const ItemRec*, const DevRule*, const TableDesc&, int, SegInfo*,
-                   const HotBucket*, rl_status*, uint32_t*, HotCand*, EngineCtl*);
-void launch_cand_state(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, const uint32_t*, uint32_t,
-                       EngineCtl*);
+void launch_leader(hipStream_t, const uint64_t*, SortedRec*, const ItemRec*, const DevRule*, uint32_t,
+                   const TableDesc&, SegInfo*, const uint32_t*, uint32_t, HotCand*, EngineCtl*);
 void launch_decide(hipStream_t, const SortedRec*, const SegInfo*, const DevRule*, uint32_t, rl_status*, uint32_t*, int,
                    EngineCtl*);
+void launch_occ_update(hipStream_t, RegionOcc*, EngineCtl*);
+void launch_cand_state(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, EngineCtl*);
 uint32_t route_bcnt_words(uint32_t n);
 void launch_route_pack(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint32_t, uint32_t, RRec*,
                        uint8_t*, uint32_t*, RRec*, uint32_t*, uint32_t*, EngineCtl*);
 void launch_route_reply(hipStream_t, uint32_t, const rl_status*, const uint32_t*, RReply*);
 void launch_route_unpack(hipStream_t, uint32_t, const uint32_t*, const uint32_t*, const RReply*, rl_status*,
                          uint32_t*);
-uint32_t v3_tiles(uint32_t n);
-uint32_t v3_group_wgs(uint32_t n);
-uint32_t v3_scan_blocks();
-void launch_v3_hist(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, const HotEntry*, uint32_t*,
-                    uint32_t*, uint16_t*, unsigned long long*, ARec*, EngineCtl*);
-void launch_v3_scan(hipStream_t, uint32_t, const uint16_t*, const unsigned long long*, uint32_t*, unsigned long long*,
-                    uint32_t*, const uint32_t*, const HotEntry*, HotBucket3*, const TableDesc&, int, HotCand*,
-                    uint32_t*, EngineCtl*);
-void launch_v3_bases(hipStream_t, uint32_t, const uint32_t*, uint32_t*, uint32_t*, uint32_t*);
-void launch_v3_place(hipStream_t, uint32_t, const ARec*, const DevRule*, const uint32_t*, const unsigned long long*,
-                     const uint32_t*, HotBucket3*, int, MRec*, rl_status*, uint32_t*, Deferred*, int, EngineCtl*);
-void launch_v3_group(hipStream_t, uint32_t, const MRec*, const uint32_t*, const DevRule*, const TableDesc&, int,
-                     rl_status*, uint32_t*, const Deferred*, const HotBucket3*, HotCand*, int, const uint32_t*,
-                     const uint32_t*, const V3GroupScratch&, uint32_t*, int, EngineCtl*);
-void launch_v3_tail(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, const uint32_t*, uint32_t,
-                    EngineCtl*, EngineCtl*);
 uint32_t v4_tiles(uint32_t n);
 uint32_t v4_group_blocks(uint32_t n);
 uint32_t v4_scan_blocks();
@@ -83,14 +56,14 @@ size_t v4_scratch_bytes();
 void launch_v4_hist(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, const HotEntry*, uint32_t*,
                     uint32_t*, uint16_t*, unsigned long long*, MRec*, rl_status*, EngineCtl*);
 void launch_v4_scan(hipStream_t, uint32_t, const uint16_t*, const unsigned long long*, unsigned long long*,
-                    const uint32_t*, const HotEntry*, HotBucket3*, const TableDesc&, int, HotCand*, uint32_t*,
-                    uint16_t*, void*, const uint32_t*, EngineCtl*);
+                    const uint32_t*, const HotEntry*, HotBucket*, const TableDesc&, HotCand*, uint32_t*, uint32_t*,
+                    uint16_t*, void*, const uint32_t*, const RegionOcc*, EngineCtl*);
 void launch_v4_place(hipStream_t, const rl_batch&, const MRec*, const uint16_t*, const uint16_t*, void*,
-                     const DevRule*, const unsigned long long*, HotBucket3*, int, MRec*, rl_status*, uint32_t*,
+                     const DevRule*, const unsigned long long*, HotBucket*, int, MRec*, rl_status*, uint32_t*,
                      Deferred*, int, uint32_t*, EngineCtl*);
-void launch_v4_group(hipStream_t, const rl_batch&, MRec*, const DevRule*, const TableDesc&, int, rl_status*,
-                     uint32_t*, const HotBucket3*, const Deferred*, HotCand*, int, uint64_t, void*, uint32_t*,
-                     const uint32_t*, int, EngineCtl*, EngineCtl*);
+void launch_v4_group(hipStream_t, const rl_batch&, MRec*, const DevRule*, const TableDesc&, rl_status*, uint32_t*,
+                     const HotBucket*, const Deferred*, HotCand*, int, uint64_t, void*, uint32_t*, uint32_t*,
+                     const uint32_t*, const uint32_t*, int, RegionOcc*, EngineCtl*, EngineCtl*);
 }  // namespace rlhip
 
 using namespace rlhip;
@@ -99,19 +72,15 @@ namespace {
 
 enum KernelId {
   KT_FINGERPRINT, KT_HISTOGRAM, KT_HIST_SCAN, KT_SORT_PASS, KT_SCAN, KT_LEADER, KT_DECIDE, KT_FALLBACK, KT_MEMSET,
-  KT_FP2, KT_BSCAN, KT_BSCATTER, KT_BGROUP, KT_CAND, KT_V3_HIST, KT_V3_SCAN, KT_V3_PLACE, KT_V3_GROUP, KT_V3_TAIL,
-  KT_V3_BASES, KT_V4_HIST, KT_V4_SCAN, KT_V4_PLACE, KT_V4_GROUP, KT_COUNT
+  KT_CAND, KT_V4_HIST, KT_V4_SCAN, KT_V4_PLACE, KT_V4_GROUP, KT_COUNT
 };
 const char* const kKernelNames[KT_COUNT] = {"k_fingerprint", "k_histogram", "k_hist_scan", "k_sort_pass", "k_scan",
-                                            "k_leader",      "k_decide",    "fallback",    "memset",      "k_fp2",
-                                            "k_bscan",       "k_bscatter",  "k_bgroup",    "k_cand_state",
-                                            "k3_hist",       "k3_scan",     "k3_place",    "k3_group",
-                                            "k3_tail",       "k3_bases",    "k4_hist",     "k4_scan",
-                                            "k4_place",      "k4_group"};
+                                            "k_leader",      "k_decide",    "fallback",    "memset",      "k_cand_state",
+                                            "k4_hist",       "k4_scan",     "k4_place",    "k4_group"};
 
-enum Mode { MODE_V2 = 0, MODE_LSD = 1, MODE_LSD_FULL = 2, MODE_V3 = 3, MODE_V4 = 4 };
+enum Mode { MODE_LSD = 1, MODE_LSD_FULL = 2, MODE_V4 = 4 };
 
-// Hot-key set kept on the host between batches (v2 bucketing).
+// Hot-key set kept on the host between batches.
 struct HotKey {
   uint64_t a, b;
   uint32_t unit, rule, count;
@@ -119,40 +88,61 @@ struct HotKey {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Wait for an event by polling. A blocking wait wakes the submitter thread ≈20 µs after the
+// GPU signals, and with two batches in flight that delay lands directly on the next batch's
+// k4_hist (it is submitted after this wait returns). The submitter thread is dedicated to its
+// device (rl_hip.h threading rule), so spinning costs no other work; after a bounded spin (a
+// batch far longer than any steady-state one) it falls back to blocking.
+hipError_t wait_event_polling(hipEvent_t ev) {
+  for (int k = 0; k < (1 << 18); ++k) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e;
+  }
+  return hipEventSynchronize(ev);
+}
+
 }  // namespace
 
-// Batches in flight at once (rl_submit_pipelined): the host-side per-batch state (pinned
-// control-block and candidate copies, completion events, hot-table versions) has one slot
-// per batch in flight; device buffers of k4_hist have two slots, because k4_hist of batch k
-// waits for batch k-2 to finish on the GPU whatever the host has submitted.
+// Host slots: one per batch in flight (pinned staging, control-block and candidate copies,
+// completion events, hot-table versions). v4 device buffers of k4_hist have two slots,
+// because k4_hist of batch k waits for batch k-2 to finish on the GPU.
 constexpr int HSLOTS = RL_MAX_IN_FLIGHT;
 
 struct rl_engine {
   rl_config cfg{};
   int lo_bit = 16, npasses = 6;
-  hipStream_t stream = nullptr;      // the stream all work is ordered on (own_stream or rl_set_stream's)
+  hipStream_t stream = nullptr;      // the stream all kernels are ordered on (own_stream or rl_set_stream's)
   hipStream_t own_stream = nullptr;
+  hipStream_t front = nullptr;       // k4_hist of a batch submitted behind one in flight
+  hipStream_t xin = nullptr;         // host path: H2D copies
+  hipStream_t xout = nullptr;        // host path: D2H copies
   std::string err;
 
   // counter table
   Slot* table = nullptr;
   size_t table_slots = 0;
   TableDesc tab{};
+  RegionOcc* d_occ = nullptr;        // per-region occupancy (device, updated by the last kernel of a batch)
+  RegionOcc occ[8] = {};             // host mirror (same update from the control-block copy)
 
   // rules
   DevRule* d_rules = nullptr;
   uint32_t n_rules = 0, rules_cap = 0;
 
-  // host-path input staging (one contiguous region, same layout on host and device)
-  size_t in_bytes = 0;
-  uint8_t* d_in = nullptr;
-  uint8_t* h_in = nullptr;
-  rl_status* d_out = nullptr;
-  uint32_t* d_thr = nullptr;
-  rl_status* h_out = nullptr;
-  uint32_t* h_thr = nullptr;
+  // host staging (rl_submit): per host slot one pinned input region with the device layout,
+  // its device twin, device outputs and pinned outputs
+  struct Stage {
+    uint8_t* h_in = nullptr;
+    uint8_t* d_in = nullptr;
+    rl_status* d_out = nullptr;
+    uint32_t* d_thr = nullptr;
+    rl_status* h_out = nullptr;
+    uint32_t* h_thr = nullptr;
+  };
+  Stage stage[HSLOTS];
+  size_t in_bytes = 0, o_off = 0, o_rule = 0, o_req = 0, o_now = 0, o_hits = 0;
 
-  // scratch
+  // LSD pipeline scratch
   uint64_t *keys_orig = nullptr, *keys_a = nullptr, *keys_b = nullptr;
   uint32_t *vals_a = nullptr, *vals_b = nullptr;
   ItemRec* recs = nullptr;
@@ -160,73 +150,53 @@ struct rl_engine {
   SegInfo* seg = nullptr;
   uint32_t* offs = nullptr;
   uint32_t* hist_part = nullptr;  // per-block partial digit histograms
-  uint32_t* fp_part = nullptr;    // per-block fingerprint partials (generation range, nil count)
+  uint32_t* fp_part = nullptr;    // per-block fingerprint partials
   uint32_t* fp_part2 = nullptr;   // the same folded per histogram block
-  uint32_t* tile_heads = nullptr; // per-scan-tile / per-workgroup segment-head counts
-  // v2 (bucketed) pipeline
-  uint16_t* bkt = nullptr;              // bucket id per descriptor
-  uint32_t* hbuf = nullptr;             // hits_addend per descriptor
-  uint32_t* tcount = nullptr;           // [tile][NBUCKETS]
-  uint32_t* toff = nullptr;             // [tile][NBUCKETS]
-  unsigned long long* thsum = nullptr;  // [tile][HOT_BUCKETS]
-  unsigned long long* hoff = nullptr;   // [tile][HOT_BUCKETS]
-  uint32_t* btotal = nullptr;           // [NBUCKETS]
-  uint64_t* bP = nullptr;               // hot descriptors: INCRBY prefix, bucket order
-  ItemRec* brec = nullptr;              // arrival records in bucket order (pad = descriptor index)
-  uint32_t* bbase = nullptr;            // [NBUCKETS + 1] bucket start positions
-  HotEntry* d_hot = nullptr;            // device hot-key table (HOT_SLOTS) + list by hot index (HOT_MAX)
-  HotBucket* hbk = nullptr;             // per hot bucket batch state (HOT_BUCKETS)
-  HotCand* d_cand = nullptr;            // hot-set candidates (CAND_MAX)
-  HotCand* h_cand = nullptr;            // pinned copy
-  std::vector<HotKey> hot;              // current hot-key set (index = hot idx)
-  bool hot_dirty = false;
-  // v3 pipeline
-  uint16_t* v3_tcount = nullptr;            // [tile][V3_ROW16]
-  uint32_t* v3_toff = nullptr;              // [tile][MSD_BUCKETS]
-  unsigned long long* v3_thsum = nullptr;   // [tile][HOT_BUCKETS]
-  unsigned long long* v3_hoff = nullptr;    // [tile][HOT_BUCKETS]
-  MRec* v3_mrec = nullptr;                  // MSD records in bucket order
-  Deferred* v3_dfr = nullptr;               // deferred hot descriptors
-  HotBucket3* v3_hb = nullptr;              // per hot bucket batch state
-  uint32_t* v3_rng = nullptr;               // k3_group range starts
-  uint32_t* v3_bbase = nullptr;             // MSD bucket start positions
-  uint32_t* v3_rngb = nullptr;              // k3_group range: index of its first bucket
-  ARec* v3_arec = nullptr;                  // per-descriptor records (arrival order)
-  V3GroupScratch v3_gs{};                   // k3_group scratch for ranges too large for LDS
-  uint32_t* v3_heads = nullptr;             // per-workgroup unique-key counts (k3_group, then k3_scan)
-  EngineCtl* v3_ctl[2] = {nullptr, nullptr};  // control blocks: batch k uses [k&1], k3_tail clears the other
-  // v4 pipeline (shares v3_tcount = bucket starts, v3_thsum, v3_hoff, v3_mrec = tile-sorted
-  // records, v3_dfr, v3_hb and v3_ctl)
-  void* v4_scratch = nullptr;               // k4_group global scratch for a bucket too large for LDS
-  uint32_t* v4_heads = nullptr;             // per-block unique-key counts (k4_group, then k4_scan)
-  uint32_t v3_cur = 0;
-  // v4 with two batches in flight (rl_submit_pipelined): k4_hist of batch k runs on `front`
-  // while batch k-1's k4_scan/k4_place/k4_group run on `stream`. Per slot (k & 1): the
-  // tile-sorted records, bucket-start rows, hot h sums, fingerprint partials, pinned control
-  // block and candidate copies; control blocks rotate over three (k4_group of batch k clears
-  // batch k+2's); hot tables are versioned (an upload never rewrites the one in use).
-  hipStream_t front = nullptr;
-  hipEvent_t ev_front[2] = {nullptr, nullptr};  // k4_hist of the slot's batch done (on front)
-  hipEvent_t ev_done[HSLOTS] = {};              // the host slot's batch done (on stream)
-  hipEvent_t ev_ready = nullptr;                // inputs of a non-pipelined submit ready (on stream)
-  hipEvent_t ev_hot = nullptr;                  // hot-set upload copy done (staging reusable)
-  MRec* v4_srt[2] = {nullptr, nullptr};
-  uint16_t* v4_tcount[2] = {nullptr, nullptr};
-  unsigned long long* v4_thsum[2] = {nullptr, nullptr};
-  uint32_t* v4_fpart[2] = {nullptr, nullptr};
-  EngineCtl* v4_ctl[3] = {nullptr, nullptr, nullptr};
-  uint32_t* d_poison = nullptr;                 // set by k4_place of a refused batch, read by k4_scan
-  HotEntry* d_hot_buf[HSLOTS] = {};             // d_hot = d_hot_buf[hot_ver]; one per batch in flight
-  int hot_ver = 0;
-  HotEntry* h_hot_stage = nullptr;              // pinned upload staging
-  EngineCtl* h_ctl_s[HSLOTS] = {};
-  HotCand* h_cand_s[HSLOTS] = {};
-  uint64_t sub_seq = 0;                         // batches submitted (host slot = seq % HSLOTS, device slot = seq & 1, control block = seq % 3)
-  bool inputs_ready = false;                    // this submit's inputs are complete (pipelined submit)
-  bool want_cand = true;                        // copy the hot-set candidates back after the next batch
-  uint8_t* zero_block = nullptr;  // ctl | hist | lookbacks (zeroed per batch)
+  uint32_t* tile_heads = nullptr; // per-scan-tile segment-head counts
+  uint8_t* zero_block = nullptr;  // ctl | look-backs (zeroed per LSD batch)
   size_t zero_cap = 0;
-  EngineCtl* h_ctl = nullptr;     // pinned copy of the control block
+
+  // hot set (both pipelines)
+  HotEntry* d_hot = nullptr;                  // device hot-key table (HOT_SLOTS) + list by hot index (HOT_MAX)
+  HotEntry* d_hot_buf[HSLOTS] = {};           // d_hot = d_hot_buf[hot_ver]; one per batch in flight
+  int hot_ver = 0;
+  HotEntry* h_hot_stage = nullptr;            // pinned upload staging
+  HotCand* d_cand = nullptr;                  // hot-set candidates (CAND_MAX)
+  HotCand* h_cand = nullptr;                  // pinned copy (current host slot)
+  HotCand* h_cand_s[HSLOTS] = {};
+  std::vector<HotKey> hot;                    // current hot-key set (index = hot idx)
+  bool hot_dirty = true;
+  std::vector<HotCand> cand_stash;
+  bool cand_pending = false;
+  bool want_cand = true;                      // copy the candidates back after the next batch
+
+  // v4 pipeline
+  uint16_t* v4_tcount[2] = {};                // [tile][V4_ROW16] bucket starts
+  unsigned long long* v4_thsum[2] = {};       // [tile][HOT_BUCKETS] hot h sums
+  MRec* v4_srt[2] = {};                       // tile-sorted records
+  uint32_t* v4_fpart[2] = {};                 // per-tile fingerprint partials
+  uint16_t* v4_toff = nullptr;                // [tile][MSD_BUCKETS] records of the bucket in earlier tiles
+  unsigned long long* v4_hoff = nullptr;      // [tile][HOT_BUCKETS] exclusive h prefix over tiles
+  MRec* v4_mrec = nullptr;                    // MSD records in bucket order
+  Deferred* v4_dfr = nullptr;                 // deferred hot descriptors
+  HotBucket* v4_hb = nullptr;                 // per hot bucket batch state
+  void* v4_scratch = nullptr;                 // k4_group global scratch + k4_scan ranges
+  uint32_t* v4_heads = nullptr;               // per-block unique-key counts (k4_group, then k4_scan)
+  uint32_t* v4_ins = nullptr;                 // per-block new slots per region (k4_group, then k4_scan)
+  EngineCtl* v4_ctl[3] = {};                  // control blocks rotate over three (k4_group clears batch k+2's)
+  uint32_t* d_poison = nullptr;               // set by k4_place of a refused batch, read by k4_scan
+
+  // per host slot: pinned control block, completion events
+  EngineCtl* h_ctl = nullptr;
+  EngineCtl* h_ctl_s[HSLOTS] = {};
+  hipEvent_t ev_done[HSLOTS] = {};            // the slot's batch complete (outputs copied, for host batches)
+  hipEvent_t ev_in[HSLOTS] = {};              // host path: the slot's inputs copied in
+  hipEvent_t ev_kern[HSLOTS] = {};            // host path: the slot's kernels done (D2H may start)
+  hipEvent_t ev_front[2] = {};                // k4_hist of the device slot done (on front)
+  hipEvent_t ev_ready = nullptr;              // inputs of a non-pipelined submit ready (on stream)
+  hipEvent_t ev_hot = nullptr;                // hot-set upload copy done (staging reusable)
+  uint64_t sub_seq = 0;                       // batches submitted (host slot = seq % HSLOTS, device slot = seq & 1)
+  int acquired = -1;                          // host slot handed out by rl_host_acquire
 
   // descriptor tree (rl_load_tree / rl_resolve)
   TreeNodeDev* d_tree_nodes = nullptr;
@@ -244,32 +214,25 @@ struct rl_engine {
   EngineCtl* r_ctl = nullptr;      // origin: error word of rl_route_pack
   uint32_t* h_route = nullptr;     // pinned: [0] err, [1..16] send counts
   uint32_t* r_thr = nullptr;       // owner: ThrottleMillis per routed record
-  RReply* pend_reply = nullptr;    // owner: reply destination of the in-flight routed batch
+  rl_status* r_out = nullptr;      // owner: statuses per routed record
 
-  // in-flight batches: the oldest in the fields below, a second (pipelined) one in `nxt`
+  // batches in flight, oldest first
   struct Flight {
-    rl_batch b{};
-    rl_status* out = nullptr;
+    rl_batch b{};                  // device pointers
+    rl_status* out = nullptr;      // device outputs
     uint32_t* thr = nullptr;
-    RReply* reply = nullptr;
-    uint32_t slot = 0;
+    RReply* reply = nullptr;       // routed batch: reply destination
+    uint32_t slot = 0;             // host slot
     bool want_cand = false;
-    bool settled = false;    // reruns done (by the previous batch's finish)
+    bool settled = false;          // reruns done
     bool fell_back = false;
+    bool host = false;             // host batch: results D2H into the slot's pinned outputs
     uint32_t errs = 0;
+    rl_status* user_out = nullptr; // host batch: rl_wait copies here (may be null)
+    uint32_t* user_thr = nullptr;
   };
-  Flight nxt[HSLOTS - 1];  // pipelined batches behind the oldest, in submission order
-  Flight cur_view;  // the oldest batch as a Flight (finish)
-  int n_next = 0;
-  uint32_t cur_slot = 0;
-  bool cur_want_cand = false;
-  bool in_flight = false;
-  bool host_path = false;
-  rl_batch dev_batch{};            // device pointers of the in-flight batch
-  rl_status* pend_out_dev = nullptr;
-  uint32_t* pend_thr_dev = nullptr;
-  rl_status* user_out = nullptr;   // host path destinations
-  uint32_t* user_thr = nullptr;
+  Flight fl[HSLOTS];
+  int n_fl = 0;
 
   // timing
   bool timing = false;
@@ -293,9 +256,7 @@ struct rl_engine {
     err = buf;
     return code;
   }
-  int hip_fail(hipError_t e, const char* what) {
-    return fail(RL_EHIP, "%s: %s", what, hipGetErrorString(e));
-  }
+  int hip_fail(hipError_t e, const char* what) { return fail(RL_EHIP, "%s: %s", what, hipGetErrorString(e)); }
 
   hipEvent_t next_event() {
     if (ev_used == ev_pool.size()) {
@@ -315,7 +276,7 @@ struct rl_engine {
     marks.push_back({kid, a, b});
   }
 
-  // Layout of the per-batch zero block for n descriptors; returns the bytes used.
+  // Layout of the LSD per-batch zero block for n descriptors.
   struct ZLayout { size_t ctl, lb_sort, lb_sum, lb_head, total; };
   ZLayout zlayout(uint32_t n, int passes) const {
     ZLayout z;
@@ -327,48 +288,48 @@ struct rl_engine {
     return z;
   }
 
-  int run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, int mode);
   int default_mode() const {
     if (cfg.flags & RL_CFG_LSD_ONLY) return MODE_LSD;
-    if (cfg.flags & RL_CFG_V2) return MODE_V2;
-    if (n_rules > V3_MAX_RULES) return MODE_LSD;  // MRec packs the rule id in 15 bits
-    return (cfg.flags & RL_CFG_V3) ? MODE_V3 : MODE_V4;
+    if (n_rules > V4_MAX_RULES) return MODE_LSD;  // MRec packs the rule id in 15 bits
+    return MODE_V4;
   }
-  int finish();
-  int settle(Flight& f);
-  void begin_submit() {
-    const uint32_t s = (uint32_t)(sub_seq % HSLOTS);
-    h_ctl = h_ctl_s[s];
-    h_cand = h_cand_s[s];
-  }
-  // Record the submitted batch's completion point and advance the slot.
-  void end_submit(bool pipelined_second) {
-    const uint32_t s = (uint32_t)(sub_seq % HSLOTS);
-    hipEventRecord(ev_done[s], stream);
-    if (!pipelined_second) {
-      cur_view = Flight{};
-      cur_slot = s;
-      cur_want_cand = want_cand;
-    }
-    ++sub_seq;
-    inputs_ready = false;
-    if (cand_pending) {
-      cand_pending = false;
-      update_hot(cand_stash.data(), (uint32_t)cand_stash.size());
-    }
-  }
+  int run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, int mode, hipEvent_t in_ev, bool inputs_ready);
   int upload_hot(hipStream_t us);
   void update_hot(const HotCand* cand, uint32_t n_cand);
-  // Hot-set maintenance from a completed batch's candidates runs after the next submit has
-  // enqueued its kernels (end_submit), not between rl_wait and that submit, where it would
-  // delay the next batch's k4_hist; the set it yields applies one batch later. Decisions do
-  // not depend on the hot set, only speed does.
-  std::vector<HotCand> cand_stash;
-  bool cand_pending = false;
-  int enqueue_d2h();
+  int settle(Flight& f);
+  int finish(rl_status* out, uint32_t* thr, bool into);
+  int enqueue_d2h(const Flight& f, hipStream_t s);
+  int check_batch(const rl_batch* b, bool host);
+  int submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, RReply* reply, hipEvent_t in_ev,
+                    bool inputs_ready, bool host, rl_status* user_out, uint32_t* user_thr);
+  void occ_host_update(const EngineCtl* c) {
+    for (int r = 0; r < 8; ++r) {
+      if (!c->gen_max[r]) continue;
+      if (occ[r].gen < c->gen_max[r]) {
+        occ[r].gen = c->gen_max[r];
+        occ[r].live = c->ins[r];
+      } else {
+        occ[r].live += c->ins[r];
+      }
+    }
+  }
+  uint64_t live_total() const {
+    uint64_t s = 0;
+    for (int r = 0; r < 8; ++r) s += occ[r].live;
+    return s;
+  }
+  int reset_occ() {
+    for (int r = 0; r < 8; ++r) {
+      occ[r].gen = 0;
+      occ[r].live = 0;
+    }
+    hipError_t e = hipMemcpy(d_occ, occ, sizeof occ, hipMemcpyHostToDevice);
+    return e == hipSuccess ? 0 : hip_fail(e, "reset occupancy");
+  }
 };
 
-int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, int mode) {
+int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, int mode, hipEvent_t in_ev,
+                            bool inputs_ready) {
   const uint32_t n = b.n_desc;
   const bool full = mode == MODE_LSD_FULL;
   const int passes = full ? 16 : npasses;
@@ -380,31 +341,33 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   uint64_t* lb_head = reinterpret_cast<uint64_t*>(zero_block + z.lb_head);
   const size_t lb_pass_stride = (size_t)sort_tiles(n > 0 ? n : 1) * RADIX;  // per-digit look-back words
   const int routed = (b.reserved & RL_BATCH_ROUTED) ? 1 : 0;
-  if (routed && mode == MODE_V2) mode = MODE_LSD;  // the v2 loader reads prefix bytes only
   hipError_t e;
   if (mode == MODE_V4) {
     const uint32_t sl = (uint32_t)(sub_seq & 1u);
     EngineCtl* c4 = v4_ctl[sub_seq % 3];
     EngineCtl* c4n = v4_ctl[(sub_seq + 2) % 3];  // batch seq+2's control block (k4_group clears it)
+    // k4_hist runs on the front stream while the previous batch is still being decided (a
+    // submit behind a batch in flight); otherwise, or when kernels are timed, on the engine stream
+    const bool split = !timing && n_fl > 0;
+    hipStream_t fs = split ? front : stream;
+    if (split) {
+      // slot buffers and control block free: batch seq-2 done
+      hipStreamWaitEvent(front, ev_done[(sub_seq + HSLOTS - 2) % HSLOTS], 0);
+      if (in_ev) {
+        hipStreamWaitEvent(front, in_ev, 0);
+      } else if (!inputs_ready) {  // inputs come from work queued on the stream
+        hipEventRecord(ev_ready, stream);
+        hipStreamWaitEvent(front, ev_ready, 0);
+      }
+    } else if (in_ev) {
+      hipStreamWaitEvent(stream, in_ev, 0);
+    }
     if (n == 0) {
       hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
       hipMemsetAsync(c4, 0, sizeof(EngineCtl), stream);
       hipMemsetAsync(c4n, 0, sizeof(EngineCtl), stream);
       e = hipMemcpyAsync(h_ctl, c4, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
       return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpyAsync(ctl)");
-    }
-    // k4_hist runs on the front stream while the previous batch is still being decided (a
-    // pipelined submit behind an in-flight batch); otherwise, or when kernels are timed, on
-    // the engine stream
-    const bool split = !timing && in_flight;
-    hipStream_t fs = split ? front : stream;
-    if (split) {
-      // slot buffers and control block free: batch seq-2 done (its host slot)
-      hipStreamWaitEvent(front, ev_done[(sub_seq + HSLOTS - 2) % HSLOTS], 0);
-      if (!inputs_ready) {                        // inputs come from work queued on the stream
-        hipEventRecord(ev_ready, stream);
-        hipStreamWaitEvent(front, ev_ready, 0);
-      }
     }
     if (hot_dirty) {
       int rc = upload_hot(fs);
@@ -413,11 +376,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     const HotEntry* hot_t = d_hot;
     const int lc = cfg.local_cache ? 1 : 0;
     const uint32_t ng = v4_group_blocks(n);
-    // v4 buffers: v4_srt = tile-sorted records, v4_tcount = bucket starts per tile,
-    // v3_toff (as u16) = per (tile, MSD bucket) records in earlier tiles, v3_mrec = MSD records
-    // in bucket order
     MRec* srt = v4_srt[sl];
-    uint16_t* toff16 = reinterpret_cast<uint16_t*>(v3_toff);
     timed(KT_V4_HIST, [&] {
       launch_v4_hist(fs, b, d_rules, n_rules, cfg.hash_seed, hot_t, thr, v4_fpart[sl], v4_tcount[sl], v4_thsum[sl],
                      srt, out, c4);
@@ -427,16 +386,17 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
       hipStreamWaitEvent(stream, ev_front[sl], 0);
     }
     timed(KT_V4_SCAN, [&] {
-      launch_v4_scan(stream, n, v4_tcount[sl], v4_thsum[sl], v3_hoff, v4_fpart[sl], hot_t + HOT_SLOTS, v3_hb, tab, lc,
-                     d_cand, v4_heads + ng, toff16, v4_scratch, d_poison, c4);
+      launch_v4_scan(stream, n, v4_tcount[sl], v4_thsum[sl], v4_hoff, v4_fpart[sl], hot_t + HOT_SLOTS, v4_hb, tab,
+                     d_cand, v4_heads + ng, v4_ins + (size_t)ng * 8, v4_toff, v4_scratch, d_poison, d_occ, c4);
     });
     timed(KT_V4_PLACE, [&] {
-      launch_v4_place(stream, b, srt, v4_tcount[sl], toff16, v4_scratch, d_rules, v3_hoff, v3_hb, lc, v3_mrec, out,
-                      thr, v3_dfr, routed, d_poison, c4);
+      launch_v4_place(stream, b, srt, v4_tcount[sl], v4_toff, v4_scratch, d_rules, v4_hoff, v4_hb, lc, v4_mrec, out,
+                      thr, v4_dfr, routed, d_poison, c4);
     });
     timed(KT_V4_GROUP, [&] {
-      launch_v4_group(stream, b, v3_mrec, d_rules, tab, lc, out, thr, v3_hb, v3_dfr, d_cand, want_cand ? 1 : 0,
-                      cfg.hash_seed, v4_scratch, v4_heads, v4_heads + ng, routed, c4, c4n);
+      launch_v4_group(stream, b, v4_mrec, d_rules, tab, out, thr, v4_hb, v4_dfr, d_cand, want_cand ? 1 : 0,
+                      cfg.hash_seed, v4_scratch, v4_heads, v4_ins, v4_heads + ng, v4_ins + (size_t)ng * 8, routed,
+                      d_occ, c4, c4n);
     });
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
@@ -446,91 +406,15 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(ctl)");
     return 0;
   }
-  if (mode == MODE_V3) {
-    if (n == 0) {
-      hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
-      hipMemsetAsync(v3_ctl[v3_cur], 0, sizeof(EngineCtl), stream);
-      e = hipMemcpyAsync(h_ctl, v3_ctl[v3_cur], sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
-      return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpyAsync(ctl)");
-    }
-    if (hot_dirty) {
-      int rc = upload_hot(stream);
-      if (rc) return rc;
-    }
-    EngineCtl* c3 = v3_ctl[v3_cur];
-    EngineCtl* c3n = v3_ctl[v3_cur ^ 1u];
-    const int lc = cfg.local_cache ? 1 : 0;
-    const uint32_t nw = v3_group_wgs(n);
-    timed(KT_V3_HIST, [&] {
-      launch_v3_hist(stream, b, d_rules, n_rules, cfg.hash_seed, d_hot, thr, fp_part, v3_tcount, v3_thsum, v3_arec,
-                     c3);
-    });
-    timed(KT_V3_SCAN, [&] {
-      launch_v3_scan(stream, n, v3_tcount, v3_thsum, v3_toff, v3_hoff, btotal, fp_part, d_hot + HOT_SLOTS, v3_hb, tab,
-                     lc, d_cand, v3_heads + nw + 1, c3);
-    });
-    timed(KT_V3_BASES, [&] { launch_v3_bases(stream, n, btotal, v3_bbase, v3_rng, v3_rngb); });
-    timed(KT_V3_PLACE, [&] {
-      launch_v3_place(stream, n, v3_arec, d_rules, v3_toff, v3_hoff, v3_bbase, v3_hb, lc, v3_mrec, out, thr, v3_dfr,
-                      routed, c3);
-    });
-    timed(KT_V3_GROUP, [&] {
-      launch_v3_group(stream, n, v3_mrec, v3_rng, d_rules, tab, lc, out, thr, v3_dfr, v3_hb, d_cand, want_cand ? 1 : 0,
-                      v3_rngb, v3_bbase, v3_gs, v3_heads, routed, c3);
-    });
-    timed(KT_V3_TAIL, [&] {
-      launch_v3_tail(stream, b, d_rules, cfg.hash_seed, d_cand, v3_heads, nw + 1 + v3_scan_blocks(), c3, c3n);
-    });
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "kernel launch");
-    e = hipMemcpyAsync(h_ctl, c3, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess && want_cand)
-      e = hipMemcpyAsync(h_cand, d_cand, sizeof(HotCand) * CAND_MAX, hipMemcpyDeviceToHost, stream);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(ctl)");
-    v3_cur ^= 1u;
-    return 0;
-  }
+  if (in_ev) hipStreamWaitEvent(stream, in_ev, 0);
   timed(KT_MEMSET, [&] {
-    // the bucketed pipeline keeps no look-back state: only the control block is cleared
-    hipMemsetAsync(zero_block, 0, mode == MODE_V2 ? z.ctl + sizeof(EngineCtl) : z.total, stream);
+    hipMemsetAsync(zero_block, 0, z.total, stream);
     // request throttles are zeroed by k_fingerprint; only an empty batch needs a memset
     if (b.n_req && n == 0) hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
   });
   if (n == 0) {
     e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpyAsync(ctl)");
-  }
-  if (mode == MODE_V2) {
-    // Bucketed pipeline: fingerprint + bucket histograms, per-bucket scan, stable bucket
-    // scatter, LDS grouping, then the shared leader / decide kernels.
-    if (hot_dirty) {
-      int rc = upload_hot(stream);
-      if (rc) return rc;
-    }
-    const int lc = cfg.local_cache ? 1 : 0;
-    timed(KT_FP2, [&] {
-      launch_fp2(stream, b, d_rules, n_rules, cfg.hash_seed, d_hot, keys_orig, recs, bkt, hbuf, out, thr, fp_part,
-                 tcount, thsum, hbk, ctl);
-    });
-    timed(KT_BSCAN, [&] {
-      launch_bscan(stream, tcount, thsum, n, toff, hoff, btotal, fp_part, d_hot + HOT_SLOTS, hbk, tab, d_cand, ctl);
-    });
-    timed(KT_BSCATTER, [&] {
-      launch_bscatter(stream, keys_orig, recs, bkt, hbuf, n, btotal, toff, hoff, keys_a, brec, bP, bbase, hbk, d_rules,
-                      lc, ctl);
-    });
-    timed(KT_BGROUP, [&] {
-      launch_bgroup(stream, keys_a, brec, bP, bbase, n, keys_b, srec, tile_heads, recs, d_rules, tab, lc, seg, hbk,
-                    out, thr, d_cand, ctl);
-    });
-    const uint32_t n_heads = v2_msd_wgs(n) + v2_hot_wgs(n);
-    timed(KT_CAND, [&] { launch_cand_state(stream, b, d_rules, cfg.hash_seed, d_cand, tile_heads, n_heads, ctl); });
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(e, "kernel launch");
-    e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(h_cand, d_cand, sizeof(HotCand) * CAND_MAX, hipMemcpyDeviceToHost, stream);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(ctl)");
-    return 0;
   }
   const uint64_t* skeys;
   const uint32_t* svals;
@@ -539,7 +423,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
       launch_fingerprint(stream, b, d_rules, n_rules, cfg.hash_seed, keys_orig, recs, out, thr, fp_part, ctl);
     });
     timed(KT_HISTOGRAM, [&] { launch_histogram(stream, keys_orig, n, lo_bit, npasses, hist, fp_part, fp_part2); });
-    timed(KT_HIST_SCAN, [&] { launch_hist_scan(stream, hist, n, offs, npasses, fp_part2, ctl); });
+    timed(KT_HIST_SCAN, [&] { launch_hist_scan(stream, hist, n, offs, npasses, fp_part2, d_occ, ctl); });
     const uint64_t* kin = keys_orig;
     const uint32_t* vin = nullptr;
     for (int p = 0; p < npasses; ++p) {
@@ -560,7 +444,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
       launch_fingerprint(stream, b, d_rules, n_rules, cfg.hash_seed, keys_orig, recs, out, thr, fp_part, ctl);
       launch_fallback_lo_keys(stream, recs, keys_orig, n, keys_a, vals_a);
       launch_histogram(stream, keys_a, n, 0, 8, hist, fp_part, fp_part2);
-      launch_hist_scan(stream, hist, n, offs, 8, fp_part2, ctl);
+      launch_hist_scan(stream, hist, n, offs, 8, fp_part2, d_occ, ctl);
     });
     const uint64_t* kin = keys_a;
     const uint32_t* vin = vals_a;
@@ -578,7 +462,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     timed(KT_FALLBACK, [&] {
       launch_gather_keys(stream, keys_orig, vals_a, n, keys_b);
       launch_histogram(stream, keys_b, n, 0, 8, hist, nullptr, nullptr);
-      launch_hist_scan(stream, hist, n, offs + 8 * hist_sub_words(), 8, nullptr, ctl);
+      launch_hist_scan(stream, hist, n, offs + 8 * hist_sub_words(), 8, nullptr, nullptr, ctl);
     });
     kin = keys_b;
     vin = vals_a;
@@ -600,11 +484,13 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
                 &ctl->tile_ctr[31][0], tile_heads, ctl);
   });
   timed(KT_LEADER, [&] {
-    launch_leader(stream, skeys, srec, recs, d_rules, n, tab, cfg.local_cache ? 1 : 0, seg, tile_heads,
-                  scan_tiles(n), d_cand, ctl);
+    launch_leader(stream, skeys, srec, recs, d_rules, n, tab, seg, tile_heads, scan_tiles(n), d_cand, ctl);
   });
-  timed(KT_DECIDE, [&] { launch_decide(stream, srec, seg, d_rules, n, out, thr, routed, ctl); });
-  timed(KT_CAND, [&] { launch_cand_state(stream, b, d_rules, cfg.hash_seed, d_cand, nullptr, 0, ctl); });
+  timed(KT_DECIDE, [&] {
+    launch_decide(stream, srec, seg, d_rules, n, out, thr, routed, ctl);
+    launch_occ_update(stream, d_occ, ctl);
+  });
+  timed(KT_CAND, [&] { launch_cand_state(stream, b, d_rules, cfg.hash_seed, d_cand, ctl); });
   e = hipGetLastError();
   if (e != hipSuccess) return hip_fail(e, "kernel launch");
   e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
@@ -636,8 +522,8 @@ int rl_engine::upload_hot(hipStream_t us) {
     t[s] = he;
     t[HOT_SLOTS + i] = he;
   }
-  // Into the version no in-flight batch reads (at most one batch is in flight here, and it
-  // uses the current version), through a pinned staging buffer whose last copy is done.
+  // Into the version no in-flight batch reads, through a pinned staging buffer whose last
+  // copy is done.
   hipError_t e = hipEventSynchronize(ev_hot);
   if (e == hipSuccess) {
     memcpy(h_hot_stage, t.data(), sizeof(HotEntry) * t.size());
@@ -654,16 +540,14 @@ int rl_engine::upload_hot(hipStream_t us) {
 }
 
 // Maintain the hot-key set from this batch's long segments (candidates with their prefix
-// state). Keys are (prefix state, unit); the two windows of one prefix merge; a prefix seen
-// under two rules is not bucketable. Hysteresis keeps the set (and its upload) stable on a
-// steady skewed stream: a hot key stays while it has >= HOT_CAND_MIN descriptors per batch,
-// a new key joins with >= HOT_MIN_SEG while there is room.
+// state). Keys are prefix states; the two windows of one prefix merge; a prefix seen under
+// two rules (two units included) is not bucketable. Hysteresis keeps the set (and its upload)
+// stable on a steady skewed stream: a hot key stays while it has >= HOT_CAND_MIN descriptors
+// per batch, a new key joins with >= HOT_MIN_SEG while there is room.
 void rl_engine::update_hot(const HotCand* cand, uint32_t n_cand) {
   n_cand = n_cand < (uint32_t)CAND_MAX ? n_cand : (uint32_t)CAND_MAX;
-  auto ident_less = [](const HotKey& x, const HotKey& y) {
-    return x.a != y.a ? x.a < y.a : x.b != y.b ? x.b < y.b : x.unit < y.unit;
-  };
-  auto same_ident = [](const HotKey& x, const HotKey& y) { return x.a == y.a && x.b == y.b && x.unit == y.unit; };
+  auto ident_less = [](const HotKey& x, const HotKey& y) { return x.a != y.a ? x.a < y.a : x.b < y.b; };
+  auto same_ident = [](const HotKey& x, const HotKey& y) { return x.a == y.a && x.b == y.b; };
   std::vector<HotKey> agg;
   agg.reserve(n_cand);
   for (uint32_t i = 0; i < n_cand; ++i) {
@@ -714,40 +598,45 @@ void rl_engine::update_hot(const HotCand* cand, uint32_t n_cand) {
   }
 }
 
+int rl_engine::enqueue_d2h(const Flight& f, hipStream_t s) {
+  hipError_t e;
+  const Stage& g = stage[f.slot];
+  if (f.b.n_desc) {
+    e = hipMemcpyAsync(g.h_out, f.out, (size_t)f.b.n_desc * sizeof(rl_status), hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(D2H out)");
+  }
+  if (f.b.n_req) {
+    e = hipMemcpyAsync(g.h_thr, f.thr, (size_t)f.b.n_req * 4, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(D2H thr)");
+  }
+  return 0;
+}
+
 // Wait for an in-flight batch and rerun it if the device refused it: on the LSD pipeline
 // when the bucketed pipeline could not take it, on the full fingerprint order when a sort-
 // prefix run held two fingerprints. Reruns are synchronous, so they are on the table before
 // anything submitted later.
-// Wait for a batch's completion event by polling. A blocking wait wakes the submitter thread
-// ≈20 µs after the GPU signals, and with two batches in flight that delay lands directly on
-// the next batch's k4_hist (it is submitted after this wait returns). The submitter thread is
-// dedicated to its device (rl_hip.h threading rule), so spinning costs no other work; after a
-// bounded spin (a batch far longer than any steady-state one) it falls back to blocking.
-static hipError_t wait_event_polling(hipEvent_t ev) {
-  for (int k = 0; k < (1 << 18); ++k) {
-    const hipError_t e = hipEventQuery(ev);
-    if (e != hipErrorNotReady) return e;
-  }
-  return hipEventSynchronize(ev);
-}
-
 int rl_engine::settle(Flight& f) {
   h_ctl = h_ctl_s[f.slot];
   h_cand = h_cand_s[f.slot];
   hipError_t e = timing ? hipStreamSynchronize(stream) : wait_event_polling(ev_done[f.slot]);
+  if (e == hipSuccess && timing && f.host) e = hipStreamSynchronize(xout);
   if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
-  const bool host = &f == &cur_view && host_path;
   uint32_t errs = h_ctl->err;
-  if ((errs & ERR_V2_FALLBACK) && !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME))) {
-    // The bucketed pipeline refused the batch before touching the table (oversized
-    // bucket, a hot prefix with a second rule, or the batch before it was refused):
-    // run it on the LSD pipeline.
+  if ((errs & ERR_FALLBACK) && !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME))) {
+    // The bucketed pipeline refused the batch before touching the table (oversized bucket, a
+    // hot prefix with a second rule, an expiry inside a hot key's batch, or the batch before
+    // it was refused): run it on the LSD pipeline.
     ++st.lsd_fallbacks;
     f.fell_back = true;
-    int rc = run_pipeline(f.b, f.out, f.thr, MODE_LSD);
+    // slots the refused attempt's hot keys claimed (k4_group counted them into the device's
+    // occupancy): the same into the host mirror
+    occ_host_update(h_ctl);
+    st.inserted_keys += h_ctl->n_inserted;
+    int rc = run_pipeline(f.b, f.out, f.thr, MODE_LSD, nullptr, true);
     if (rc) return rc;
     if (f.reply) launch_route_reply(stream, f.b.n_desc, f.out, f.thr, f.reply);
-    if (host && (rc = enqueue_d2h()) != 0) return rc;
+    if (f.host && (rc = enqueue_d2h(f, stream)) != 0) return rc;
     e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     errs = h_ctl->err;
@@ -756,10 +645,10 @@ int rl_engine::settle(Flight& f) {
     // A sort-prefix run held two fingerprints: nothing touched the table (k_leader and
     // k_decide return early), so re-run the batch on the full fingerprint order.
     ++st.resorts;
-    int rc = run_pipeline(f.b, f.out, f.thr, MODE_LSD_FULL);
+    int rc = run_pipeline(f.b, f.out, f.thr, MODE_LSD_FULL, nullptr, true);
     if (rc) return rc;
     if (f.reply) launch_route_reply(stream, f.b.n_desc, f.out, f.thr, f.reply);
-    if (host && (rc = enqueue_d2h()) != 0) return rc;
+    if (f.host && (rc = enqueue_d2h(f, stream)) != 0) return rc;
     e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     errs = h_ctl->err;
@@ -772,14 +661,10 @@ int rl_engine::settle(Flight& f) {
 // Complete the oldest in-flight batch: reruns (settle), then errors, hot-set maintenance,
 // stats and the host-path copy. A refused batch poisons the batch behind it (k4_place ->
 // k4_scan), so that one is settled here too, before anything else can be submitted.
-int rl_engine::finish() {
-  cur_view.b = dev_batch;
-  cur_view.out = pend_out_dev;
-  cur_view.thr = pend_thr_dev;
-  cur_view.reply = pend_reply;
-  cur_view.slot = cur_slot;
-  cur_view.want_cand = cur_want_cand;
-  Flight& f = cur_view;
+int rl_engine::finish(rl_status* out_into, uint32_t* thr_into, bool into) {
+  Flight f = fl[0];
+  for (int q = 1; q < n_fl; ++q) fl[q - 1] = fl[q];
+  --n_fl;
   const bool settled_here = !f.settled;  // else the previous batch's finish reran this one
   if (settled_here) {
     int rc = settle(f);
@@ -788,15 +673,14 @@ int rl_engine::finish() {
   if (settled_here && f.fell_back) {
     hipError_t e = hipMemsetAsync(d_poison, 0, 4, stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync(poison)");
-    for (int q = 0; q < n_next && !nxt[q].settled; ++q) {  // refused in turn (poison chain)
-      int rc = settle(nxt[q]);
+    for (int q = 0; q < n_fl && !fl[q].settled; ++q) {  // refused in turn (poison chain)
+      int rc = settle(fl[q]);
       if (rc) return rc;
-      if (!nxt[q].fell_back) break;
+      if (!fl[q].fell_back) break;
       hipError_t e2 = hipMemsetAsync(d_poison, 0, 4, stream);
       if (e2 != hipSuccess) return hip_fail(e2, "hipMemsetAsync(poison)");
     }
   }
-
   h_ctl = h_ctl_s[f.slot];
   h_cand = h_cand_s[f.slot];
   const uint32_t errs = f.errs;
@@ -812,11 +696,15 @@ int rl_engine::finish() {
     marks.clear();
     ev_used = 0;
   }
-  if (errs & ERR_BAD_INPUT) return fail(RL_EINVAL, "batch references an unknown rule id or request index");
-  if (errs & ERR_BAD_TIME) return fail(RL_EINVAL, "request time outside [0, 2^32) unix seconds");
+  if (errs & ERR_BAD_INPUT)
+    return fail(RL_EINVAL, "batch references an unknown rule id or request index, or malformed prefix offsets / "
+                           "request order");
+  if (errs & ERR_BAD_TIME) return fail(RL_EINVAL, "request time outside [0, 0xFFFD0000] unix seconds");
   if (errs & ERR_WINDOW_SPAN)
     return fail(RL_EINVAL, "batch spans more than two windows of one unit; split it at window boundaries");
-  if (errs & ERR_TABLE_FULL) return fail(RL_ENOSPC, "counter table region full (raise log2_slots)");
+  if (errs & ERR_TABLE_FULL)
+    return fail(RL_ENOSPC, "counter table region would pass its load limit; batch refused before any update "
+                           "(raise log2_slots or max_load_permille)");
   if (errs & ERR_SPIN) return fail(RL_EDEVICE, "device look-back spin limit exceeded");
   if (errs & ERR_NEED_RESORT) return fail(RL_EDEVICE, "full-fingerprint re-sort still found a mixed run");
   // Hot-set maintenance costs host time between batches: every batch while the set is
@@ -830,32 +718,82 @@ int rl_engine::finish() {
       cand_pending = true;
     }
   }
+  occ_host_update(h_ctl);
   last_unique = h_ctl->n_segments;
-  last_n = dev_batch.n_desc;
-  last_req = dev_batch.n_req;
-  last_blob = dev_batch.blob_bytes;
+  last_n = f.b.n_desc;
+  last_req = f.b.n_req;
+  last_blob = f.b.blob_bytes;
   st.batches += 1;
-  st.descriptors += dev_batch.n_desc;
-  // Hot-set maintenance costs a candidate copy and host time between batches: every batch
-  // while the set is empty, else every 8th batch (a skewed stream's head moves slowly).
+  st.descriptors += f.b.n_desc;
+  st.inserted_keys += h_ctl->n_inserted;
+  st.live_keys = live_total();
   want_cand = hot.empty() || (st.batches & 7) == 0;
-  for (int k = 0; k < INS_LINES; ++k) st.live_slots_hint += h_ctl->tile_ctr[INS_CTR0 + k][0];
-  if (host_path) {
-    if (dev_batch.n_desc) memcpy(user_out, h_out, (size_t)dev_batch.n_desc * sizeof(rl_status));
-    if (dev_batch.n_req) memcpy(user_thr, h_thr, (size_t)dev_batch.n_req * 4);
+  if (f.host) {
+    rl_status* o = into ? out_into : f.user_out;
+    uint32_t* t = into ? thr_into : f.user_thr;
+    const Stage& g = stage[f.slot];
+    if (o && f.b.n_desc) memcpy(o, g.h_out, (size_t)f.b.n_desc * sizeof(rl_status));
+    if (t && f.b.n_req) memcpy(t, g.h_thr, (size_t)f.b.n_req * 4);
   }
   return 0;
 }
 
-int rl_engine::enqueue_d2h() {
-  hipError_t e;
-  if (dev_batch.n_desc) {
-    e = hipMemcpyAsync(h_out, d_out, (size_t)dev_batch.n_desc * sizeof(rl_status), hipMemcpyDeviceToHost, stream);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(D2H out)");
+int rl_engine::check_batch(const rl_batch* b, bool host) {
+  if (b->n_desc > cfg.max_batch_desc || b->n_req > cfg.max_batch_req || (host && b->blob_bytes > cfg.max_blob_bytes))
+    return fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req, %u blob bytes)", cfg.max_batch_desc,
+                cfg.max_batch_req, cfg.max_blob_bytes);
+  if (b->reserved) return fail(RL_EINVAL, "rl_batch.reserved must be 0");
+  if (b->n_desc && (!b->prefix_off || !b->rule_id || !b->req_of)) return fail(RL_EINVAL, "null descriptor array");
+  if (b->n_req && (!b->now || !b->hits_addend)) return fail(RL_EINVAL, "null request array");
+  if (!d_rules) {
+    int rc = rl_load_rules(this, nullptr, 0);
+    if (rc) return rc;
   }
-  if (dev_batch.n_req) {
-    e = hipMemcpyAsync(h_thr, d_thr, (size_t)dev_batch.n_req * 4, hipMemcpyDeviceToHost, stream);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(D2H thr)");
+  return 0;
+}
+
+// Common tail of every submit form: run the pipeline behind what is in flight, record the
+// completion point, queue the flight.
+int rl_engine::submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, RReply* reply, hipEvent_t in_ev,
+                             bool inputs_ready, bool host, rl_status* user_out, uint32_t* user_thr) {
+  const uint32_t s = (uint32_t)(sub_seq % HSLOTS);
+  h_ctl = h_ctl_s[s];
+  h_cand = h_cand_s[s];
+  const bool want = want_cand;
+  int rc = run_pipeline(d, out, thr, default_mode(), in_ev, inputs_ready);
+  if (rc) return rc;
+  if (reply) launch_route_reply(stream, d.n_desc, out, thr, reply);
+  Flight f;
+  f.b = d;
+  f.out = out;
+  f.thr = thr;
+  f.reply = reply;
+  f.slot = s;
+  f.want_cand = want;
+  f.host = host;
+  f.user_out = user_out;
+  f.user_thr = user_thr;
+  hipError_t e;
+  if (host) {
+    // outputs leave on the copy-out stream while the next batch's kernels run
+    e = hipEventRecord(ev_kern[s], stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(xout, ev_kern[s], 0);
+    if (e != hipSuccess) return hip_fail(e, "host path events");
+    if ((rc = enqueue_d2h(f, xout)) != 0) return rc;
+    e = hipEventRecord(ev_done[s], xout);
+  } else {
+    e = hipEventRecord(ev_done[s], stream);
+  }
+  if (e != hipSuccess) return hip_fail(e, "hipEventRecord(done)");
+  fl[n_fl++] = f;
+  ++sub_seq;
+  if (cand_pending) {
+    // Hot-set maintenance from a completed batch's candidates runs after the next submit has
+    // enqueued its kernels, not between rl_wait and that submit, where it would delay the
+    // next batch's k4_hist; the set it yields applies one batch later. Decisions do not
+    // depend on the hot set, only speed does.
+    cand_pending = false;
+    update_hot(cand_stash.data(), (uint32_t)cand_stash.size());
   }
   return 0;
 }
@@ -875,15 +813,17 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   rl_config& c = e->cfg;
   for (int u = 0; u < 4; ++u) {
     if (c.log2_slots[u] == 0) c.log2_slots[u] = 20;
-    if (c.log2_slots[u] < 4 || c.log2_slots[u] > 34) {
+    if (c.log2_slots[u] < 4 || c.log2_slots[u] > 31) {
       delete e;
       return RL_EINVAL;
     }
   }
+  if (c.max_load_permille == 0) c.max_load_permille = 750;
+  if (c.max_load_permille < 100 || c.max_load_permille > 950 || c.reserved) { delete e; return RL_EINVAL; }
   if (c.max_batch_desc == 0) c.max_batch_desc = 1u << 20;
   if (c.max_batch_req == 0) c.max_batch_req = c.max_batch_desc;
   if (c.max_blob_bytes == 0) c.max_blob_bytes = c.max_batch_desc * 64u;
-  if (c.max_batch_desc > (1u << 28)) { delete e; return RL_EINVAL; }
+  if (c.max_batch_desc > (1u << 28) || c.max_blob_bytes > (1u << 31)) { delete e; return RL_EINVAL; }
   if (c.sort_bits == 0) c.sort_bits = 48;
   if (c.sort_bits % 8 || c.sort_bits < 8 || c.sort_bits > 64) { delete e; return RL_EINVAL; }
   e->npasses = (int)c.sort_bits / 8;
@@ -892,29 +832,47 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   if (he != hipSuccess) { delete e; return RL_EHIP; }
   auto chk = [&](hipError_t x) { if (x != hipSuccess && he == hipSuccess) he = x; };
   chk(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
+  chk(hipStreamCreateWithFlags(&e->front, hipStreamNonBlocking));
+  chk(hipStreamCreateWithFlags(&e->xin, hipStreamNonBlocking));
+  chk(hipStreamCreateWithFlags(&e->xout, hipStreamNonBlocking));
   e->stream = e->own_stream;
-  // counter table: 8 regions (unit x window parity)
+  // counter table: 8 regions (home unit x window parity)
   size_t off = 0;
   for (int r = 0; r < 8; ++r) {
     const uint32_t lg = c.log2_slots[r / 2];
     e->tab.region_base[r] = off;
     e->tab.region_log2[r] = lg;
+    e->occ[r].gen = 0;
+    e->occ[r].live = 0;
+    e->occ[r].limit = (uint32_t)(((uint64_t)1 << lg) * c.max_load_permille / 1000);
+    e->occ[r].pad = 0;
     off += (size_t)1 << lg;
   }
+  e->tab.split = c.per_second_split ? 1u : 0u;
+  e->tab.local_cache = c.local_cache ? 1u : 0u;
   e->table_slots = off;
   chk(hipMalloc(&e->table, off * sizeof(Slot)));
   if (he == hipSuccess) chk(hipMemset(e->table, 0, off * sizeof(Slot)));
   e->tab.slots = e->table;
+  chk(hipMalloc(&e->d_occ, sizeof e->occ));
+  if (he == hipSuccess) chk(hipMemcpy(e->d_occ, e->occ, sizeof e->occ, hipMemcpyHostToDevice));
   const size_t N = c.max_batch_desc, R = c.max_batch_req, B = c.max_blob_bytes;
-  // input staging: blob | off | rule | req | now | hits
-  e->in_bytes = align_up(B + 16, 256) + align_up((N + 1) * 4, 256) + 2 * align_up(N * 4, 256) + align_up(R * 8, 256) +
-                align_up(R * 4, 256);
-  chk(hipMalloc(&e->d_in, e->in_bytes));
-  chk(hipHostMalloc(&e->h_in, e->in_bytes, hipHostMallocDefault));
-  chk(hipMalloc(&e->d_out, N * sizeof(rl_status)));
-  chk(hipMalloc(&e->d_thr, R * 4));
-  chk(hipHostMalloc(&e->h_out, N * sizeof(rl_status), hipHostMallocDefault));
-  chk(hipHostMalloc(&e->h_thr, R * 4, hipHostMallocDefault));
+  // host staging: blob | off | rule | req | now | hits (same layout on host and device)
+  e->o_off = align_up(B + 16, 256);
+  e->o_rule = e->o_off + align_up((N + 1) * 4, 256);
+  e->o_req = e->o_rule + align_up(N * 4, 256);
+  e->o_now = e->o_req + align_up(N * 4, 256);
+  e->o_hits = e->o_now + align_up(R * 8, 256);
+  e->in_bytes = e->o_hits + align_up(R * 4, 256);
+  for (auto& g : e->stage) {
+    chk(hipMalloc(&g.d_in, e->in_bytes));
+    chk(hipHostMalloc(&g.h_in, e->in_bytes, hipHostMallocDefault));
+    chk(hipMalloc(&g.d_out, N * sizeof(rl_status) + 64));
+    chk(hipMalloc(&g.d_thr, R * 4 + 64));
+    chk(hipHostMalloc(&g.h_out, N * sizeof(rl_status) + 64, hipHostMallocDefault));
+    chk(hipHostMalloc(&g.h_thr, R * 4 + 64, hipHostMallocDefault));
+  }
+  // LSD pipeline
   chk(hipMalloc(&e->keys_orig, N * 8));
   chk(hipMalloc(&e->keys_a, N * 8));
   chk(hipMalloc(&e->keys_b, N * 8));
@@ -927,74 +885,38 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   chk(hipMalloc(&e->hist_part, (size_t)hist_blocks((uint32_t)N) * MAX_PASSES * RADIX * 4));
   chk(hipMalloc(&e->fp_part2, (size_t)hist_blocks((uint32_t)N) * FP_PART_WORDS * 4 + 64));
   chk(hipMalloc(&e->fp_part, ((N + 255) / 256) * FP_PART_WORDS * 4 + 64));
-  {
-    const size_t nh = std::max<size_t>(scan_tiles((uint32_t)N), v2_msd_wgs((uint32_t)N) + v2_hot_wgs((uint32_t)N));
-    chk(hipMalloc(&e->tile_heads, nh * 4 + 64));
+  chk(hipMalloc(&e->tile_heads, (size_t)scan_tiles((uint32_t)N) * 4 + 64));
+  e->zero_cap = e->zlayout((uint32_t)N, MAX_PASSES).total;
+  chk(hipMalloc(&e->zero_block, e->zero_cap));
+  // hot set
+  for (int k = 0; k < HSLOTS; ++k) chk(hipMalloc(&e->d_hot_buf[k], sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX)));
+  e->d_hot = e->d_hot_buf[0];
+  chk(hipHostMalloc(&e->h_hot_stage, sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX), hipHostMallocDefault));
+  chk(hipMalloc(&e->d_cand, sizeof(HotCand) * CAND_MAX));
+  for (int k = 0; k < HSLOTS; ++k) {
+    chk(hipHostMalloc(&e->h_cand_s[k], sizeof(HotCand) * CAND_MAX, hipHostMallocDefault));
+    chk(hipHostMalloc(&e->h_ctl_s[k], sizeof(EngineCtl), hipHostMallocDefault));
   }
+  e->h_cand = e->h_cand_s[0];
+  e->h_ctl = e->h_ctl_s[0];
+  // v4 pipeline
   {
-    const size_t T = v2_tiles((uint32_t)N);
-    chk(hipMalloc(&e->bkt, N * 2 + 64));
-    chk(hipMalloc(&e->hbuf, N * 4 + 64));
-    chk(hipMalloc(&e->tcount, T * NBUCKETS * 4));
-    chk(hipMalloc(&e->toff, T * NBUCKETS * 4));
-    chk(hipMalloc(&e->thsum, T * HOT_BUCKETS * 8));
-    chk(hipMalloc(&e->hoff, T * HOT_BUCKETS * 8));
-    chk(hipMalloc(&e->btotal, (NBUCKETS + 1) * 4));
-    chk(hipMalloc(&e->bP, N * 8 + 64));
-    chk(hipMalloc(&e->brec, N * sizeof(ItemRec)));
-    chk(hipMalloc(&e->bbase, (NBUCKETS + 1) * 4));
-    for (int k = 0; k < HSLOTS; ++k) chk(hipMalloc(&e->d_hot_buf[k], sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX)));
-    e->d_hot = e->d_hot_buf[0];
-    chk(hipHostMalloc(&e->h_hot_stage, sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX), hipHostMallocDefault));
-    chk(hipMalloc(&e->hbk, sizeof(HotBucket) * HOT_BUCKETS));
-    chk(hipMalloc(&e->d_cand, sizeof(HotCand) * CAND_MAX));
-    for (int k = 0; k < HSLOTS; ++k)
-      chk(hipHostMalloc(&e->h_cand_s[k], sizeof(HotCand) * CAND_MAX, hipHostMallocDefault));
-    e->h_cand = e->h_cand_s[0];
-    e->hot_dirty = true;  // upload the empty table before the first batch
-  }
-  {
-    const size_t T3 = v3_tiles((uint32_t)N);
-    chk(hipMalloc(&e->v3_tcount, T3 * V3_ROW16 * 2));
-    chk(hipMalloc(&e->v3_toff, T3 * MSD_BUCKETS * 4));
-    chk(hipMalloc(&e->v3_thsum, T3 * HOT_BUCKETS * 8));
-    chk(hipMalloc(&e->v3_hoff, T3 * HOT_BUCKETS * 8));
-    chk(hipMalloc(&e->v3_mrec, N * sizeof(MRec) + 64));
-    chk(hipMalloc(&e->v3_dfr, N * sizeof(Deferred) + 64));
-    chk(hipMalloc(&e->v3_hb, HOT_BUCKETS * sizeof(HotBucket3)));
-    chk(hipMalloc(&e->v3_rng, (v3_group_wgs((uint32_t)N) + 2) * 4));
-    chk(hipMalloc(&e->v3_bbase, (MSD_BUCKETS + 1) * 4));
-    chk(hipMalloc(&e->v3_rngb, (v3_group_wgs((uint32_t)N) + 2) * 4));
-    chk(hipMalloc(&e->v3_arec, N * sizeof(ARec) + 64));
-    V3GroupScratch& g = e->v3_gs;
-    chk(hipMalloc(&g.key, N * 8 + 64));
-    chk(hipMalloc(&g.lo, N * 8 + 64));
-    chk(hipMalloc(&g.pay, N * 16 + 64));
-    chk(hipMalloc(&g.P, N * 8 + 64));
-    chk(hipMalloc(&g.slot, N * 16 + 64));
-    chk(hipMalloc(&g.cnt, N * 16 + 64));
-    chk(hipMalloc(&g.base, N * 16 + 64));
-    chk(hipMalloc(&g.list, N * 4 + 64));
-    chk(hipMalloc(&g.grp, N * 4 + 64));
-    chk(hipMalloc(&g.rank, N * 4 + 64));
-    chk(hipMalloc(&g.tail, N * 4 + 64));
-    chk(hipMalloc(&g.cursor, (v3_group_wgs((uint32_t)N) + 2) * 4));
-    chk(hipMalloc(&e->v3_heads, (v3_group_wgs((uint32_t)N) + 1 + v3_scan_blocks()) * 4 + 64));
-    chk(hipMalloc(&e->v4_heads, (v4_group_blocks((uint32_t)N) + v4_scan_blocks()) * 4 + 64));
-    chk(hipMalloc(&e->v4_scratch, v4_scratch_bytes()));
+    const size_t T4 = v4_tiles((uint32_t)N);
     for (int k = 0; k < 2; ++k) {
-      chk(hipMalloc(&e->v3_ctl[k], sizeof(EngineCtl)));
-      if (he == hipSuccess) chk(hipMemset(e->v3_ctl[k], 0, sizeof(EngineCtl)));
+      chk(hipMalloc(&e->v4_tcount[k], T4 * V4_ROW16 * 2));
+      chk(hipMalloc(&e->v4_thsum[k], T4 * HOT_BUCKETS * 8));
+      chk(hipMalloc(&e->v4_srt[k], N * sizeof(MRec) + 64));
+      chk(hipMalloc(&e->v4_fpart[k], T4 * FP_PART_WORDS * 4 + 64));
     }
-    // v4 slot 0 shares the v3 per-tile buffers (an engine runs one of the two pipelines)
-    e->v4_srt[0] = reinterpret_cast<MRec*>(e->v3_arec);
-    e->v4_tcount[0] = e->v3_tcount;
-    e->v4_thsum[0] = e->v3_thsum;
-    static_assert(sizeof(MRec) == sizeof(ARec), "v4 tile records reuse the ARec buffer");
-    chk(hipMalloc(&e->v4_srt[1], N * sizeof(MRec) + 64));
-    chk(hipMalloc(&e->v4_tcount[1], T3 * V3_ROW16 * 2));
-    chk(hipMalloc(&e->v4_thsum[1], T3 * HOT_BUCKETS * 8));
-    for (int k = 0; k < 2; ++k) chk(hipMalloc(&e->v4_fpart[k], T3 * FP_PART_WORDS * 4 + 64));
+    chk(hipMalloc(&e->v4_toff, T4 * MSD_BUCKETS * 2));
+    chk(hipMalloc(&e->v4_hoff, T4 * HOT_BUCKETS * 8));
+    chk(hipMalloc(&e->v4_mrec, N * sizeof(MRec) + 64));
+    chk(hipMalloc(&e->v4_dfr, N * sizeof(Deferred) + 64));
+    chk(hipMalloc(&e->v4_hb, HOT_BUCKETS * sizeof(HotBucket)));
+    const size_t nb = (size_t)v4_group_blocks((uint32_t)N) + v4_scan_blocks();
+    chk(hipMalloc(&e->v4_heads, nb * 4 + 64));
+    chk(hipMalloc(&e->v4_ins, nb * 8 * 4 + 64));
+    chk(hipMalloc(&e->v4_scratch, v4_scratch_bytes()));
     for (int k = 0; k < 3; ++k) {
       chk(hipMalloc(&e->v4_ctl[k], sizeof(EngineCtl)));
       if (he == hipSuccess) chk(hipMemset(e->v4_ctl[k], 0, sizeof(EngineCtl)));
@@ -1002,14 +924,12 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     chk(hipMalloc(&e->d_poison, 64));
     if (he == hipSuccess) chk(hipMemset(e->d_poison, 0, 64));
   }
-
-  e->zero_cap = e->zlayout((uint32_t)N, MAX_PASSES).total;
-  chk(hipMalloc(&e->zero_block, e->zero_cap));
-  for (int k = 0; k < HSLOTS; ++k) chk(hipHostMalloc(&e->h_ctl_s[k], sizeof(EngineCtl), hipHostMallocDefault));
-  e->h_ctl = e->h_ctl_s[0];
-  chk(hipStreamCreateWithFlags(&e->front, hipStreamNonBlocking));
   std::vector<hipEvent_t*> evs = {&e->ev_front[0], &e->ev_front[1], &e->ev_ready, &e->ev_hot};
-  for (int k = 0; k < HSLOTS; ++k) evs.push_back(&e->ev_done[k]);
+  for (int k = 0; k < HSLOTS; ++k) {
+    evs.push_back(&e->ev_done[k]);
+    evs.push_back(&e->ev_in[k]);
+    evs.push_back(&e->ev_kern[k]);
+  }
   for (hipEvent_t* ev : evs) {
     chk(hipEventCreateWithFlags(ev, hipEventDisableTiming));
     if (he == hipSuccess) chk(hipEventRecord(*ev, e->stream));
@@ -1026,97 +946,52 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
 
 void rl_destroy(rl_engine* e) {
   if (!e) return;
-  if (e->stream) hipStreamSynchronize(e->stream);
-  if (e->front) hipStreamSynchronize(e->front);
+  for (hipStream_t s : {e->stream, e->front, e->xin, e->xout})
+    if (s) hipStreamSynchronize(s);
   for (auto ev : e->ev_pool) hipEventDestroy(ev);
   for (hipEvent_t ev : {e->ev_front[0], e->ev_front[1], e->ev_ready, e->ev_hot})
     if (ev) hipEventDestroy(ev);
   for (int k = 0; k < HSLOTS; ++k) {
-    if (e->ev_done[k]) hipEventDestroy(e->ev_done[k]);
+    for (hipEvent_t ev : {e->ev_done[k], e->ev_in[k], e->ev_kern[k]})
+      if (ev) hipEventDestroy(ev);
     hipFree(e->d_hot_buf[k]);
     hipHostFree(e->h_cand_s[k]);
     hipHostFree(e->h_ctl_s[k]);
   }
-  for (int k = 0; k < 2; ++k) hipFree(e->v4_fpart[k]);
-  hipFree(e->v4_srt[1]);
-  hipFree(e->v4_tcount[1]);
-  hipFree(e->v4_thsum[1]);
+  for (auto& g : e->stage) {
+    hipFree(g.d_in);
+    hipHostFree(g.h_in);
+    hipFree(g.d_out);
+    hipFree(g.d_thr);
+    hipHostFree(g.h_out);
+    hipHostFree(g.h_thr);
+  }
+  for (int k = 0; k < 2; ++k) {
+    hipFree(e->v4_tcount[k]);
+    hipFree(e->v4_thsum[k]);
+    hipFree(e->v4_srt[k]);
+    hipFree(e->v4_fpart[k]);
+  }
   for (int k = 0; k < 3; ++k) hipFree(e->v4_ctl[k]);
-  hipFree(e->d_poison);
-  hipFree(e->d_tree_nodes);
-  hipFree(e->d_tree_slots);
-  hipFree(e->d_tree_names);
-  hipFree(e->d_res);
-  hipHostFree(e->h_hot_stage);
-  hipFree(e->table);
-  hipFree(e->d_rules);
-  hipFree(e->d_in);
-  hipHostFree(e->h_in);
-  hipFree(e->d_out);
-  hipFree(e->d_thr);
-  hipHostFree(e->h_out);
-  hipHostFree(e->h_thr);
-  hipFree(e->keys_orig);
-  hipFree(e->keys_a);
-  hipFree(e->keys_b);
-  hipFree(e->vals_a);
-  hipFree(e->vals_b);
-  hipFree(e->recs);
-  hipFree(e->srec);
-  hipFree(e->seg);
-  hipFree(e->offs);
-  hipFree(e->hist_part);
-  hipFree(e->fp_part);
-  hipFree(e->fp_part2);
-  hipFree(e->tile_heads);
-  hipFree(e->bkt);
-  hipFree(e->hbuf);
-  hipFree(e->tcount);
-  hipFree(e->toff);
-  hipFree(e->thsum);
-  hipFree(e->hoff);
-  hipFree(e->btotal);
-  hipFree(e->bP);
-  hipFree(e->brec);
-  hipFree(e->bbase);
-  hipFree(e->hbk);
-  hipFree(e->d_cand);
-  hipFree(e->v3_tcount);
-  hipFree(e->v3_toff);
-  hipFree(e->v3_thsum);
-  hipFree(e->v3_hoff);
-  hipFree(e->v3_mrec);
-  hipFree(e->v3_dfr);
-  hipFree(e->v3_hb);
-  hipFree(e->v3_rng);
-  hipFree(e->v3_bbase);
-  hipFree(e->v3_rngb);
-  hipFree(e->v3_arec);
-  for (void* p : {(void*)e->v3_gs.key, (void*)e->v3_gs.lo, (void*)e->v3_gs.pay, (void*)e->v3_gs.P,
-                  (void*)e->v3_gs.slot, (void*)e->v3_gs.cnt, (void*)e->v3_gs.base, (void*)e->v3_gs.list,
-                  (void*)e->v3_gs.grp, (void*)e->v3_gs.rank, (void*)e->v3_gs.tail, (void*)e->v3_gs.cursor})
+  for (void* p : {(void*)e->v4_toff, (void*)e->v4_hoff, (void*)e->v4_mrec, (void*)e->v4_dfr, (void*)e->v4_hb,
+                  (void*)e->v4_heads, (void*)e->v4_ins, e->v4_scratch, (void*)e->d_poison, (void*)e->d_tree_nodes,
+                  (void*)e->d_tree_slots, (void*)e->d_tree_names, (void*)e->d_res, (void*)e->table, (void*)e->d_occ,
+                  (void*)e->d_rules, (void*)e->keys_orig, (void*)e->keys_a, (void*)e->keys_b, (void*)e->vals_a,
+                  (void*)e->vals_b, (void*)e->recs, (void*)e->srec, (void*)e->seg, (void*)e->offs,
+                  (void*)e->hist_part, (void*)e->fp_part, (void*)e->fp_part2, (void*)e->tile_heads,
+                  (void*)e->zero_block, (void*)e->d_cand, (void*)e->r_tmp, (void*)e->r_own, (void*)e->r_bcnt,
+                  (void*)e->r_ctl, (void*)e->r_thr, (void*)e->r_out})
     hipFree(p);
-  hipFree(e->v3_heads);
-  hipFree(e->v4_heads);
-  hipFree(e->v4_scratch);
-  hipFree(e->v3_ctl[0]);
-  hipFree(e->v3_ctl[1]);
-
-  hipFree(e->r_tmp);
-  hipFree(e->r_own);
-  hipFree(e->r_bcnt);
-  hipFree(e->r_ctl);
+  hipHostFree(e->h_hot_stage);
   hipHostFree(e->h_route);
-  hipFree(e->r_thr);
-  hipFree(e->zero_block);
-  if (e->front) hipStreamDestroy(e->front);
-  if (e->own_stream) hipStreamDestroy(e->own_stream);
+  for (hipStream_t s : {e->front, e->xin, e->xout, e->own_stream})
+    if (s) hipStreamDestroy(s);
   delete e;
 }
 
 int rl_load_rules(rl_engine* e, const rl_rule* rules, uint32_t n) {
   if (!e) return RL_EINVAL;
-  if (e->in_flight) return e->fail(RL_ESTATE, "rl_load_rules while a batch is in flight");
+  if (e->n_fl) return e->fail(RL_ESTATE, "rl_load_rules while a batch is in flight");
   std::vector<DevRule> h(n);
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t u = rules[i].unit;
@@ -1129,18 +1004,13 @@ int rl_load_rules(rl_engine* e, const rl_rule* rules, uint32_t n) {
     h[i].div = unit_div(u);
     h[i].unit = u;
   }
-  if (n > e->rules_cap) {
+  if (n > e->rules_cap || !e->d_rules) {
     hipFree(e->d_rules);
     e->d_rules = nullptr;
     const uint32_t cap = n < 16 ? 16 : n;
     hipError_t he = hipMalloc(&e->d_rules, (size_t)cap * sizeof(DevRule));
     if (he != hipSuccess) return e->hip_fail(he, "hipMalloc(rules)");
     e->rules_cap = cap;
-  }
-  if (!e->d_rules) {
-    hipError_t he = hipMalloc(&e->d_rules, 16 * sizeof(DevRule));
-    if (he != hipSuccess) return e->hip_fail(he, "hipMalloc(rules)");
-    e->rules_cap = 16;
   }
   if (n) {
     hipError_t he = hipMemcpy(e->d_rules, h.data(), (size_t)n * sizeof(DevRule), hipMemcpyHostToDevice);
@@ -1150,175 +1020,104 @@ int rl_load_rules(rl_engine* e, const rl_rule* rules, uint32_t n) {
   return 0;
 }
 
+int rl_host_acquire(rl_engine* e, rl_host_batch* out) {
+  if (!e || !out) return RL_EINVAL;
+  if (e->n_fl >= HSLOTS) return e->fail(RL_ESTATE, "rl_host_acquire with %d batches in flight (call rl_wait)", HSLOTS);
+  const int s = (int)(e->sub_seq % HSLOTS);
+  uint8_t* h = e->stage[s].h_in;
+  out->prefix_blob = h;
+  out->prefix_off = reinterpret_cast<uint32_t*>(h + e->o_off);
+  out->rule_id = reinterpret_cast<uint32_t*>(h + e->o_rule);
+  out->req_of = reinterpret_cast<uint32_t*>(h + e->o_req);
+  out->now = reinterpret_cast<int64_t*>(h + e->o_now);
+  out->hits_addend = reinterpret_cast<uint32_t*>(h + e->o_hits);
+  out->max_desc = e->cfg.max_batch_desc;
+  out->max_req = e->cfg.max_batch_req;
+  out->max_blob = e->cfg.max_blob_bytes;
+  out->reserved = 0;
+  e->acquired = s;
+  return 0;
+}
+
 int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_throttle_ms) {
   if (!e || !b) return RL_EINVAL;
-  if (e->in_flight) return e->fail(RL_ESTATE, "rl_submit while a batch is in flight (call rl_wait)");
-  const rl_config& c = e->cfg;
-  if (b->n_desc > c.max_batch_desc || b->n_req > c.max_batch_req || b->blob_bytes > c.max_blob_bytes)
-    return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req, %u blob bytes)", c.max_batch_desc,
-                   c.max_batch_req, c.max_blob_bytes);
-  if (b->reserved) return e->fail(RL_EINVAL, "rl_batch.reserved must be 0");
-  if (!e->d_rules) rl_load_rules(e, nullptr, 0);
-  // Host-side validation of the batch layout.
-  if (b->n_desc && (!b->prefix_off || !b->rule_id || !b->req_of || !out))
-    return e->fail(RL_EINVAL, "null descriptor array");
-  if (b->n_req && (!b->now || !b->hits_addend || !req_throttle_ms)) return e->fail(RL_EINVAL, "null request array");
-  if (b->n_desc) {
-    if (b->prefix_off[b->n_desc] > b->blob_bytes) return e->fail(RL_EINVAL, "prefix offsets exceed blob");
-    for (uint32_t i = 0; i < b->n_desc; ++i) {
-      if (b->prefix_off[i + 1] < b->prefix_off[i]) return e->fail(RL_EINVAL, "prefix offsets not monotone at %u", i);
-      if (b->req_of[i] >= b->n_req || (i && b->req_of[i] < b->req_of[i - 1]))
-        return e->fail(RL_EINVAL, "req_of not non-decreasing / in range at %u", i);
-      if (b->rule_id[i] != RL_NIL_RULE && b->rule_id[i] >= e->n_rules)
-        return e->fail(RL_EINVAL, "unknown rule id %u at %u", b->rule_id[i], i);
-    }
-  }
-  // Stage into pinned memory with the device layout, one H2D copy.
-  const size_t N = c.max_batch_desc, B = c.max_blob_bytes;
-  uint8_t* h = e->h_in;
-  size_t o_blob = 0, o_off = align_up(B + 16, 256), o_rule = o_off + align_up((N + 1) * 4, 256),
-         o_req = o_rule + align_up(N * 4, 256), o_now = o_req + align_up(N * 4, 256),
-         o_hits = o_now + align_up((size_t)c.max_batch_req * 8, 256);
-  if (b->blob_bytes) memcpy(h + o_blob, b->prefix_blob, b->blob_bytes);
-  memset(h + o_blob + b->blob_bytes, 0, 16);
-  if (b->n_desc) {
-    memcpy(h + o_off, b->prefix_off, ((size_t)b->n_desc + 1) * 4);
-    memcpy(h + o_rule, b->rule_id, (size_t)b->n_desc * 4);
-    memcpy(h + o_req, b->req_of, (size_t)b->n_desc * 4);
-  }
-  if (b->n_req) {
-    memcpy(h + o_now, b->now, (size_t)b->n_req * 8);
-    memcpy(h + o_hits, b->hits_addend, (size_t)b->n_req * 4);
-  }
-  hipError_t he;
-  // Copy only the used extents of each array.
-  struct Seg { size_t o, n; } segs[] = {{o_blob, (size_t)b->blob_bytes + 16},
-                                        {o_off, ((size_t)b->n_desc + 1) * 4},
-                                        {o_rule, (size_t)b->n_desc * 4},
-                                        {o_req, (size_t)b->n_desc * 4},
-                                        {o_now, (size_t)b->n_req * 8},
-                                        {o_hits, (size_t)b->n_req * 4}};
-  for (auto& s : segs) {
-    if (!s.n) continue;
-    he = hipMemcpyAsync(e->d_in + s.o, h + s.o, s.n, hipMemcpyHostToDevice, e->stream);
-    if (he != hipSuccess) return e->hip_fail(he, "hipMemcpyAsync(H2D)");
-  }
-  rl_batch d = *b;
-  d.prefix_blob = e->d_in + o_blob;
-  d.prefix_off = reinterpret_cast<const uint32_t*>(e->d_in + o_off);
-  d.rule_id = reinterpret_cast<const uint32_t*>(e->d_in + o_rule);
-  d.req_of = reinterpret_cast<const uint32_t*>(e->d_in + o_req);
-  d.now = reinterpret_cast<const int64_t*>(e->d_in + o_now);
-  d.hits_addend = reinterpret_cast<const uint32_t*>(e->d_in + o_hits);
-  e->begin_submit();
-  int rc = e->run_pipeline(d, e->d_out, e->d_thr, e->default_mode());
+  if (e->n_fl >= HSLOTS) return e->fail(RL_ESTATE, "rl_submit with %d batches in flight (call rl_wait)", HSLOTS);
+  int rc = e->check_batch(b, true);
   if (rc) return rc;
-  e->dev_batch = d;
-  e->pend_out_dev = e->d_out;
-  e->pend_thr_dev = e->d_thr;
-  e->user_out = out;
-  e->user_thr = req_throttle_ms;
-  e->pend_reply = nullptr;
-  e->host_path = true;
-  if ((rc = e->enqueue_d2h()) != 0) return rc;
-  e->end_submit(false);
-  e->in_flight = true;
-  return 0;
+  if (e->n_fl && e->default_mode() != MODE_V4)
+    return e->fail(RL_ESTATE, "a second batch in flight needs the v4 pipeline (call rl_wait)");
+  const uint32_t s = (uint32_t)(e->sub_seq % HSLOTS);
+  rl_engine::Stage& g = e->stage[s];
+  uint8_t* h = g.h_in;
+  // Stage into the slot's pinned memory unless the caller built the batch there
+  // (rl_host_acquire); the slot's previous batch is complete (batches complete in order and
+  // fewer than HSLOTS are in flight).
+  struct Arr { const void* src; size_t o, n; } arrs[] = {
+      {b->prefix_blob, 0, b->blob_bytes}, {b->prefix_off, e->o_off, b->n_desc ? ((size_t)b->n_desc + 1) * 4 : 0},
+      {b->rule_id, e->o_rule, (size_t)b->n_desc * 4}, {b->req_of, e->o_req, (size_t)b->n_desc * 4},
+      {b->now, e->o_now, (size_t)b->n_req * 8}, {b->hits_addend, e->o_hits, (size_t)b->n_req * 4}};
+  for (auto& a : arrs)
+    if (a.n && a.src != h + a.o) memcpy(h + a.o, a.src, a.n);
+  memset(h + b->blob_bytes, 0, 16);  // slack for the device's 16-B word reads
+  e->acquired = -1;
+  hipError_t he = hipSuccess;
+  // Copy only the used extents of each array, on the copy-in stream: the previous batch's
+  // kernels keep running meanwhile.
+  const size_t ext[] = {(size_t)b->blob_bytes + 16, arrs[1].n, arrs[2].n, arrs[3].n, arrs[4].n, arrs[5].n};
+  for (int k = 0; k < 6 && he == hipSuccess; ++k)
+    if (ext[k]) he = hipMemcpyAsync(g.d_in + arrs[k].o, h + arrs[k].o, ext[k], hipMemcpyHostToDevice, e->xin);
+  if (he == hipSuccess) he = hipEventRecord(e->ev_in[s], e->xin);
+  if (he != hipSuccess) return e->hip_fail(he, "hipMemcpyAsync(H2D)");
+  rl_batch d = *b;
+  d.prefix_blob = g.d_in;
+  d.prefix_off = reinterpret_cast<const uint32_t*>(g.d_in + e->o_off);
+  d.rule_id = reinterpret_cast<const uint32_t*>(g.d_in + e->o_rule);
+  d.req_of = reinterpret_cast<const uint32_t*>(g.d_in + e->o_req);
+  d.now = reinterpret_cast<const int64_t*>(g.d_in + e->o_now);
+  d.hits_addend = reinterpret_cast<const uint32_t*>(g.d_in + e->o_hits);
+  e->st.host_batches += 1;
+  return e->submit_common(d, g.d_out, g.d_thr, nullptr, e->ev_in[s], false, true, out, req_throttle_ms);
 }
 
 int rl_wait(rl_engine* e) {
   if (!e) return RL_EINVAL;
-  if (!e->in_flight) return e->fail(RL_ESTATE, "rl_wait without a batch in flight");
-  const int rc = e->finish();
-  e->in_flight = false;
-  if (e->n_next) {  // the next pipelined batch becomes the oldest
-    const rl_engine::Flight n = e->nxt[0];
-    for (int q = 1; q < e->n_next; ++q) e->nxt[q - 1] = e->nxt[q];
-    e->dev_batch = n.b;
-    e->pend_out_dev = n.out;
-    e->pend_thr_dev = n.thr;
-    e->pend_reply = nullptr;
-    e->host_path = false;
-    e->cur_slot = n.slot;
-    e->cur_want_cand = n.want_cand;
-    e->cur_view = n;
-    e->n_next -= 1;
-    e->in_flight = true;
-  }
-  return rc;
+  if (!e->n_fl) return e->fail(RL_ESTATE, "rl_wait without a batch in flight");
+  return e->finish(nullptr, nullptr, false);
+}
+
+int rl_wait_into(rl_engine* e, rl_status* out, uint32_t* req_throttle_ms) {
+  if (!e) return RL_EINVAL;
+  if (!e->n_fl) return e->fail(RL_ESTATE, "rl_wait_into without a batch in flight");
+  return e->finish(out, req_throttle_ms, true);
 }
 
 int rl_submit_device(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t* d_req_throttle_ms) {
   if (!e || !b) return RL_EINVAL;
-  if (e->in_flight) return e->fail(RL_ESTATE, "rl_submit_device while a batch is in flight (call rl_wait)");
-  const rl_config& c = e->cfg;
-  if (b->n_desc > c.max_batch_desc || b->n_req > c.max_batch_req)
-    return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req)", c.max_batch_desc,
-                   c.max_batch_req);
-  if (b->reserved) return e->fail(RL_EINVAL, "rl_batch.reserved must be 0");
-  if (!e->d_rules) rl_load_rules(e, nullptr, 0);
-  e->begin_submit();
-  int rc = e->run_pipeline(*b, d_out, d_req_throttle_ms, e->default_mode());
+  if (e->n_fl) return e->fail(RL_ESTATE, "rl_submit_device while a batch is in flight (call rl_wait)");
+  int rc = e->check_batch(b, false);
   if (rc) return rc;
-  e->dev_batch = *b;
-  e->pend_out_dev = d_out;
-  e->pend_thr_dev = d_req_throttle_ms;
-  e->pend_reply = nullptr;
-  e->host_path = false;
-  e->end_submit(false);
-  e->in_flight = true;
-  return 0;
+  return e->submit_common(*b, d_out, d_req_throttle_ms, nullptr, nullptr, false, false, nullptr, nullptr);
 }
 
 int rl_submit_pipelined(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t* d_req_throttle_ms) {
   if (!e || !b) return RL_EINVAL;
-  if (e->in_flight && e->n_next + 1 >= HSLOTS)
+  if (e->n_fl >= HSLOTS)
     return e->fail(RL_ESTATE, "rl_submit_pipelined with %d batches in flight (call rl_wait)", HSLOTS);
-  const rl_config& c = e->cfg;
-  if (b->n_desc > c.max_batch_desc || b->n_req > c.max_batch_req)
-    return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req)", c.max_batch_desc,
-                   c.max_batch_req);
-  if (b->reserved) return e->fail(RL_EINVAL, "rl_batch.reserved must be 0");
-  const bool second = e->in_flight;
-  if (second && e->default_mode() != MODE_V4)
-    return e->fail(RL_ESTATE, "a second batch in flight needs the v4 pipeline (call rl_wait)");
-  bool shared = second && (e->pend_out_dev == d_out || e->pend_thr_dev == d_req_throttle_ms);
-  for (int q = 0; second && q < e->n_next; ++q)
-    shared |= e->nxt[q].out == d_out || e->nxt[q].thr == d_req_throttle_ms;
-  if (shared) return e->fail(RL_EINVAL, "batches in flight together need distinct output buffers");
-  if (!e->d_rules) rl_load_rules(e, nullptr, 0);
-  e->begin_submit();
-  e->inputs_ready = true;
-  const uint32_t slot = (uint32_t)(e->sub_seq % HSLOTS);
-  const bool want = e->want_cand;
-  int rc = e->run_pipeline(*b, d_out, d_req_throttle_ms, e->default_mode());
+  int rc = e->check_batch(b, false);
   if (rc) return rc;
-  if (second) {
-    rl_engine::Flight& n = e->nxt[e->n_next];
-    n = rl_engine::Flight{};
-    n.b = *b;
-    n.out = d_out;
-    n.thr = d_req_throttle_ms;
-    n.slot = slot;
-    n.want_cand = want;
-    e->n_next += 1;
-  } else {
-    e->dev_batch = *b;
-    e->pend_out_dev = d_out;
-    e->pend_thr_dev = d_req_throttle_ms;
-    e->pend_reply = nullptr;
-    e->host_path = false;
-    e->in_flight = true;
-  }
-  e->end_submit(second);
-  return 0;
+  if (e->n_fl && e->default_mode() != MODE_V4)
+    return e->fail(RL_ESTATE, "a second batch in flight needs the v4 pipeline (call rl_wait)");
+  for (int q = 0; q < e->n_fl; ++q)
+    if (e->fl[q].out == d_out || e->fl[q].thr == d_req_throttle_ms)
+      return e->fail(RL_EINVAL, "batches in flight together need distinct output buffers");
+  return e->submit_common(*b, d_out, d_req_throttle_ms, nullptr, nullptr, true, false, nullptr, nullptr);
 }
 
 void* rl_stream(rl_engine* e) { return e ? (void*)e->stream : nullptr; }
 
 int rl_set_stream(rl_engine* e, void* hip_stream) {
   if (!e) return RL_EINVAL;
-  if (e->in_flight) return e->fail(RL_ESTATE, "rl_set_stream while a batch is in flight");
+  if (e->n_fl) return e->fail(RL_ESTATE, "rl_set_stream while a batch is in flight");
   hipError_t he = hipStreamSynchronize(e->stream);  // work already queued finishes first
   if (he != hipSuccess) return e->hip_fail(he, "hipStreamSynchronize");
   e->stream = hip_stream ? (hipStream_t)hip_stream : e->own_stream;
@@ -1328,7 +1127,7 @@ int rl_set_stream(rl_engine* e, void* hip_stream) {
 int rl_route_pack(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_shards, void* d_send,
                   uint32_t* d_send_counts, uint32_t* d_perm, uint32_t* h_send_counts) {
   if (!e || !b) return RL_EINVAL;
-  if (e->in_flight) return e->fail(RL_ESTATE, "rl_route_pack while a batch is in flight (call rl_wait)");
+  if (e->n_fl) return e->fail(RL_ESTATE, "rl_route_pack while a batch is in flight (call rl_wait)");
   if (n_shards == 0 || n_shards > ROUTE_MAX_SHARDS || origin >= ROUTE_MAX_SHARDS)
     return e->fail(RL_EINVAL, "n_shards must be 1..%u and origin < %u", ROUTE_MAX_SHARDS, ROUTE_MAX_SHARDS);
   if (b->n_desc > e->cfg.max_batch_desc) return e->fail(RL_ECAPACITY, "batch exceeds engine capacity");
@@ -1357,22 +1156,25 @@ int rl_route_pack(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_s
   chk(hipStreamSynchronize(e->stream));
   if (he != hipSuccess) return e->hip_fail(he, "rl_route_pack");
   const uint32_t errs = e->h_route[0];
-  if (errs & ERR_BAD_INPUT) return e->fail(RL_EINVAL, "batch references an unknown rule id or request index");
-  if (errs & ERR_BAD_TIME) return e->fail(RL_EINVAL, "request time outside [0, 2^32) unix seconds");
+  if (errs & ERR_BAD_INPUT)
+    return e->fail(RL_EINVAL, "batch references an unknown rule id or request index, or malformed prefix offsets");
+  if (errs & ERR_BAD_TIME) return e->fail(RL_EINVAL, "request time outside [0, 0xFFFD0000] unix seconds");
   memcpy(h_send_counts, e->h_route + 1, n_shards * 4);
   return 0;
 }
 
 int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_reply) {
   if (!e) return RL_EINVAL;
-  if (e->in_flight) return e->fail(RL_ESTATE, "rl_submit_routed while a batch is in flight (call rl_wait)");
+  if (e->n_fl) return e->fail(RL_ESTATE, "rl_submit_routed while a batch is in flight (call rl_wait)");
   if (n > e->cfg.max_batch_desc)
     return e->fail(RL_ECAPACITY, "routed batch of %u records exceeds engine capacity (%u desc)", n,
                    e->cfg.max_batch_desc);
   if (n && (!d_records || !d_reply)) return e->fail(RL_EINVAL, "null routed buffer");
   if (!e->d_rules) rl_load_rules(e, nullptr, 0);
   if (!e->r_thr) {
-    hipError_t he = hipMalloc(&e->r_thr, (size_t)(e->cfg.max_batch_desc ? e->cfg.max_batch_desc : 1) * 4);
+    const size_t N = e->cfg.max_batch_desc ? e->cfg.max_batch_desc : 1;
+    hipError_t he = hipMalloc(&e->r_thr, N * 4 + 64);
+    if (he == hipSuccess) he = hipMalloc(&e->r_out, N * sizeof(rl_status) + 64);
     if (he != hipSuccess) return e->hip_fail(he, "router scratch allocation");
   }
   rl_batch b{};
@@ -1380,24 +1182,14 @@ int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_re
   b.n_req = n;  // every record has its own ThrottleMillis slot
   b.reserved = RL_BATCH_ROUTED;
   b.prefix_blob = reinterpret_cast<const uint8_t*>(d_records);
-  e->begin_submit();
-  int rc = e->run_pipeline(b, e->d_out, e->r_thr, e->default_mode());
-  if (rc) return rc;
-  launch_route_reply(e->stream, n, e->d_out, e->r_thr, reinterpret_cast<RReply*>(d_reply));
-  e->dev_batch = b;
-  e->pend_out_dev = e->d_out;
-  e->pend_thr_dev = e->r_thr;
-  e->pend_reply = reinterpret_cast<RReply*>(d_reply);
-  e->host_path = false;
-  e->end_submit(false);
-  e->in_flight = true;
-  return 0;
+  return e->submit_common(b, e->r_out, e->r_thr, reinterpret_cast<RReply*>(d_reply), nullptr, false, false, nullptr,
+                          nullptr);
 }
 
 int rl_route_unpack(rl_engine* e, const rl_batch* b, const uint32_t* d_perm, const void* d_reply, rl_status* d_out,
                     uint32_t* d_req_throttle_ms) {
   if (!e || !b) return RL_EINVAL;
-  if (e->in_flight) return e->fail(RL_ESTATE, "rl_route_unpack while a batch is in flight (call rl_wait)");
+  if (e->n_fl) return e->fail(RL_ESTATE, "rl_route_unpack while a batch is in flight (call rl_wait)");
   if (b->n_desc && (!d_perm || !d_out || !b->req_of)) return e->fail(RL_EINVAL, "null routing buffer");
   if (b->n_req && !d_req_throttle_ms) return e->fail(RL_EINVAL, "null throttle buffer");
   hipError_t he = hipSuccess;
@@ -1412,14 +1204,16 @@ int rl_route_unpack(rl_engine* e, const rl_batch* b, const uint32_t* d_perm, con
 
 int rl_reset(rl_engine* e) {
   if (!e) return RL_EINVAL;
-  if (e->in_flight) return e->fail(RL_ESTATE, "rl_reset while a batch is in flight");
+  if (e->n_fl) return e->fail(RL_ESTATE, "rl_reset while a batch is in flight");
   e->hot.clear();
   e->hot_dirty = true;
   e->cand_pending = false;
   e->cand_stash.clear();
   hipError_t he = hipMemsetAsync(e->table, 0, e->table_slots * sizeof(Slot), e->stream);
   if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
-  return he == hipSuccess ? 0 : e->hip_fail(he, "rl_reset");
+  if (he != hipSuccess) return e->hip_fail(he, "rl_reset");
+  e->st.live_keys = 0;
+  return e->reset_occ();
 }
 
 int rl_get_stats(rl_engine* e, rl_engine_stats* s) {
@@ -1428,9 +1222,20 @@ int rl_get_stats(rl_engine* e, rl_engine_stats* s) {
   return 0;
 }
 
+int rl_get_occupancy(rl_engine* e, rl_occupancy* o) {
+  if (!e || !o) return RL_EINVAL;
+  for (int r = 0; r < 8; ++r) {
+    o->gen[r] = e->occ[r].gen;
+    o->live[r] = e->occ[r].live;
+    o->limit[r] = e->occ[r].limit;
+    o->slots[r] = 1u << e->tab.region_log2[r];
+  }
+  return 0;
+}
+
 int rl_set_timing(rl_engine* e, int on) {
   if (!e) return RL_EINVAL;
-  if (e->in_flight) return e->fail(RL_ESTATE, "rl_set_timing while a batch is in flight");
+  if (e->n_fl) return e->fail(RL_ESTATE, "rl_set_timing while a batch is in flight");
   e->timing = on != 0;
   for (int k = 0; k < KT_COUNT; ++k) { e->kt_ms[k] = 0; e->kt_n[k] = 0; }
   return 0;
@@ -1458,13 +1263,9 @@ int rl_last_batch_info(rl_engine* e, uint64_t* unique_keys, uint64_t* n_desc, ui
   return 0;
 }
 
-}  // extern "C"
-
-extern "C" {
-
 int rl_load_tree(rl_engine* e, const rl_tree_node* nodes, uint32_t n_nodes, const uint8_t* names, uint32_t names_len) {
   if (!e) return RL_EINVAL;
-  if (e->in_flight) return e->fail(RL_ESTATE, "rl_load_tree while a batch is in flight");
+  if (e->n_fl) return e->fail(RL_ESTATE, "rl_load_tree while a batch is in flight");
   if ((n_nodes && !nodes) || (names_len && !names)) return e->fail(RL_EINVAL, "null tree array");
   std::vector<TreeNodeDev> hn;
   std::vector<uint32_t> hs;
@@ -1520,7 +1321,7 @@ int rl_resolve_device(rl_engine* e, const rl_resolve_batch* b, uint32_t* d_rule_
 
 int rl_resolve(rl_engine* e, const rl_resolve_batch* b, uint32_t* rule_out) {
   if (!e || !b) return RL_EINVAL;
-  if (e->in_flight) return e->fail(RL_ESTATE, "rl_resolve while a batch is in flight");
+  if (e->n_fl) return e->fail(RL_ESTATE, "rl_resolve while a batch is in flight");
   if (!e->has_tree) return e->fail(RL_ESTATE, "rl_resolve without a tree (rl_load_tree)");
   if (b->reserved) return e->fail(RL_EINVAL, "rl_resolve_batch.reserved must be 0");
   const uint32_t n = b->n_desc, ne = b->n_entries;

@@ -33,24 +33,39 @@ __device__ uint64_t g_stamps[4096][8];
 #define STAMP(k) do { } while (0)
 #endif
 
+// Window start, table place and fingerprint of one valid descriptor (both loaders).
+RL_DEV void fp_place(const FpState& s, int64_t now, const DevRule& R, uint64_t& key, ItemRec& rec, uint32_t& region,
+                     uint32_t& uw) {
+  const int64_t widx = div_const(now, R.unit);
+  const uint32_t ws = (uint32_t)(widx * (int64_t)R.div);  // (now/divider)*divider  cache_key.go:66-68
+  const Place pl = place_of(ws);
+  uint64_t hi, lo;
+  fp_final(s, (uint64_t)ws, hi, lo);
+  region = pl.region;
+  key = make_sort_key(region, hi);
+  rec.fp_lo = lo;
+  rec.now_mod = (int32_t)(now - (int64_t)ws);
+  rec.gen = pl.gen;
+  uw = (R.unit - 1u) * 2u + (uint32_t)(widx & 1);
+}
+
 __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
                                                      uint64_t seed, uint64_t* __restrict__ keys_orig,
                                                      ItemRec* __restrict__ recs, rl_status* __restrict__ out,
                                                      uint32_t* __restrict__ req_thr, uint32_t* __restrict__ fpart,
                                                      EngineCtl* ctl) {
-  __shared__ uint32_t sh_nil;
+  __shared__ uint32_t sh_f[FP_PART_WORDS];  // FP_* layout; gmin holds ~min (zero-init max)
   __shared__ uint32_t sh_err;
-  __shared__ uint32_t sh_gmin[8], sh_gmax[8];  // gmin holds ~min (zero-init max)
   const uint32_t tid = threadIdx.x;
-  if (tid < 8) { sh_gmin[tid] = 0; sh_gmax[tid] = 0; }
-  if (tid == 0) { sh_nil = 0; sh_err = 0; }
+  if (tid < FP_PART_WORDS) sh_f[tid] = 0;
+  if (tid == 0) sh_err = 0;
   __syncthreads();
 
   const uint32_t i = blockIdx.x * 256 + tid;
   uint32_t err = 0;
   bool nil = true;
   uint64_t key = NIL_KEY;
-  uint32_t region = 8, gen = 0;
+  uint32_t region = 8, gen = 0, uw = 8;
   if (i < in.n_desc && in.recs) {
     // Routed record (multi-GPU owner): the key prefix arrives as its fingerprint lane state.
     const RRec x = in.recs[i];
@@ -65,17 +80,10 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
     rec.pad = 0;
     if (x.rule >= n_rules) {
       err |= ERR_BAD_INPUT;
+    } else if ((int64_t)x.now > MAX_NOW) {
+      err |= ERR_BAD_TIME;
     } else {
-      const DevRule R = rules[x.rule];
-      const int64_t widx = div_const((int64_t)x.now, R.unit);
-      const int64_t ws = widx * (int64_t)R.div;
-      uint64_t hi, lo;
-      fp_final(FpState{x.a, x.b}, (uint64_t)ws, hi, lo);
-      region = (R.unit - 1u) * 2u + (uint32_t)(widx & 1);
-      key = make_sort_key(region, hi);
-      rec.fp_lo = lo;
-      rec.now_mod = (int32_t)((int64_t)x.now - ws);
-      rec.gen = (uint32_t)widx + 1u;
+      fp_place(FpState{x.a, x.b}, (int64_t)x.now, rules[x.rule], key, rec, region, uw);
       gen = rec.gen;
       nil = false;
     }
@@ -104,24 +112,20 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
     rec.now_mod = 0;
     rec.gen = 0;
     rec.pad = 0;
+    // batch layout checks (the device validates every submit form): prefix offsets in
+    // order and inside the blob, request indices non-decreasing
+    const uint32_t o0 = in.off[i], o1 = in.off[i + 1];
+    const bool layout_ok = o0 <= o1 && o1 <= in.blob_bytes && (i == 0 || in.req_of[i - 1] <= q);
+    if (!layout_ok) err |= ERR_BAD_INPUT;
     if (r != RL_NIL_RULE && (r >= n_rules || !q_ok)) err |= ERR_BAD_INPUT;
-    if (r != RL_NIL_RULE && r < n_rules && q_ok) {
-      if (now < 0 || now > 0xFFFFFFF0ll) {
+    if (r != RL_NIL_RULE && r < n_rules && q_ok && layout_ok) {
+      if (now < 0 || now > MAX_NOW) {
         err |= ERR_BAD_TIME;
       } else {
         const DevRule R = rules[r];
-        const int64_t widx = div_const(now, R.unit);
-        const int64_t ws = widx * (int64_t)R.div;  // (now/divider)*divider  cache_key.go:66-68
-        const uint32_t o0 = in.off[i], o1 = in.off[i + 1];
-        FpState s = fp_init(o1 - o0, R.unit, seed);
+        FpState s = fp_init(o1 - o0, seed);
         hash_prefix(in.blob, o0, o1 - o0, s);
-        uint64_t hi, lo;
-        fp_final(s, (uint64_t)ws, hi, lo);
-        region = (R.unit - 1u) * 2u + (uint32_t)(widx & 1);
-        key = make_sort_key(region, hi);
-        rec.fp_lo = lo;
-        rec.now_mod = (int32_t)(now - ws);
-        rec.gen = (uint32_t)widx + 1u;
+        fp_place(s, now, R, key, rec, region, uw);
         gen = rec.gen;
         nil = false;
       }
@@ -142,24 +146,24 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
   // Per-wave reductions, then one LDS op per wave.
   const uint64_t nilmask = __ballot(i < in.n_desc && nil);
   const uint32_t lane = __lane_id();
-  if (lane == 0 && nilmask) atomicAdd(&sh_nil, (uint32_t)__popcll(nilmask));
+  if (lane == 0 && nilmask) atomicAdd(&sh_f[FP_NIL], (uint32_t)__popcll(nilmask));
   for (uint32_t rg = 0; rg < 8; ++rg) {
     const bool mine = region == rg;
-    if (!__ballot(mine)) continue;
+    const uint64_t m = __ballot(mine);
+    if (!m) continue;
     const uint32_t mn = wave_min_u32(mine ? gen : 0xFFFFFFFFu);
     const uint32_t mx = wave_max_u32(mine ? gen : 0u);
     if (lane == 0) {
-      atomicMax(&sh_gmin[rg], ~mn);
-      atomicMax(&sh_gmax[rg], mx);
+      atomicMax(&sh_f[FP_GMIN + rg], ~mn);
+      atomicMax(&sh_f[FP_GMAX + rg], mx);
+      atomicAdd(&sh_f[FP_CNT + rg], (uint32_t)__popcll(m));
     }
   }
   if (err) atomicOr(&sh_err, err);
   __syncthreads();
-  // Block partials (plain stores); k_hist_scan's last block reduces them.
+  // Block partials (plain stores); k_histogram folds them, k_hist_scan's last block reduces.
   uint32_t* fp = fpart + (size_t)blockIdx.x * FP_PART_WORDS;
-  if (tid < 8) fp[tid] = sh_gmin[tid];
-  else if (tid < 16) fp[tid] = sh_gmax[tid - 8];
-  else if (tid == 16) fp[16] = sh_nil;
+  if (tid < FP_PART_WORDS) fp[tid] = sh_f[tid];
   if (tid == 0 && sh_err) atomicOr(&ctl->err, sh_err);
 }
 
@@ -186,7 +190,7 @@ __global__ __launch_bounds__(1024) void k_histogram(const uint64_t* __restrict__
     uint32_t v = 0;
     for (uint32_t f = f0; f < f1; ++f) {
       const uint32_t x = fpart[(size_t)f * FP_PART_WORDS + tid];
-      v = tid < 16 ? (x > v ? x : v) : v + x;
+      v = fp_is_max((int)tid) ? (x > v ? x : v) : v + x;
     }
     fpart2[(size_t)blockIdx.x * FP_PART_WORDS + tid] = v;
   }
@@ -197,11 +201,11 @@ __global__ __launch_bounds__(1024) void k_histogram(const uint64_t* __restrict__
 
 // Block (p, q), q < HIST_SUB: sum slice q of pass p's partial histograms -> sub[p][q][256].
 // Last block (if fp_blocks): reduce the folded fingerprint partials into ctl (the only
-// writer of gen_min / gen_max / n_nil).
+// writer of gen_min / gen_max / n_nil) and run the capacity check before any table write.
 __global__ __launch_bounds__(256) void k_hist_scan(const uint32_t* __restrict__ part, uint32_t nblocks,
                                                    uint32_t* __restrict__ sub, int npasses,
                                                    const uint32_t* __restrict__ fpart2, uint32_t fp_blocks,
-                                                   EngineCtl* ctl) {
+                                                   const RegionOcc* __restrict__ occ, EngineCtl* ctl) {
   const uint32_t tid = threadIdx.x;
   if ((int)blockIdx.x == npasses * HIST_SUB) {
     __shared__ uint32_t shm[FP_PART_WORDS][256];
@@ -209,7 +213,7 @@ __global__ __launch_bounds__(256) void k_hist_scan(const uint32_t* __restrict__ 
       uint32_t v = 0;
       for (uint32_t g = tid; g < fp_blocks; g += 256) {
         const uint32_t x = fpart2[(size_t)g * FP_PART_WORDS + w];
-        v = w < 16 ? (x > v ? x : v) : v + x;
+        v = fp_is_max(w) ? (x > v ? x : v) : v + x;
       }
       shm[w][tid] = v;
     }
@@ -218,13 +222,21 @@ __global__ __launch_bounds__(256) void k_hist_scan(const uint32_t* __restrict__ 
       if (tid < (uint32_t)d)
         for (int w = 0; w < FP_PART_WORDS; ++w) {
           const uint32_t a = shm[w][tid], c = shm[w][tid + d];
-          shm[w][tid] = w < 16 ? (a > c ? a : c) : a + c;
+          shm[w][tid] = fp_is_max(w) ? (a > c ? a : c) : a + c;
         }
       __syncthreads();
     }
-    if (tid < 8) ctl->gen_min[tid] = ~shm[tid][0];  // partials hold ~min
-    else if (tid < 16) ctl->gen_max[tid - 8] = shm[tid][0];
-    else if (tid == 16) ctl->n_nil = shm[16][0];
+    if (tid < 8) ctl->gen_min[tid] = ~shm[FP_GMIN + tid][0];  // partials hold ~min
+    else if (tid < 16) ctl->gen_max[tid - 8] = shm[FP_GMAX + tid - 8][0];
+    else if (tid == 16) ctl->n_nil = shm[FP_NIL][0];
+    else if (tid == 17) {
+      uint32_t gmax[8], cnt[8];
+      for (int r = 0; r < 8; ++r) {
+        gmax[r] = shm[FP_GMAX + r][0];
+        cnt[r] = shm[FP_CNT + r][0];
+      }
+      if (!capacity_ok(occ, gmax, cnt)) atomicOr(&ctl->err, ERR_TABLE_FULL);
+    }
     return;
   }
   const uint32_t p = blockIdx.x / HIST_SUB, q = blockIdx.x % HIST_SUB;
@@ -471,7 +483,6 @@ __global__ __launch_bounds__(256) void k_sort_pass(const uint64_t* __restrict__ 
 #endif
 constexpr int SCAN_IPT = RL_SCAN_IPT;
 constexpr int SCAN_TILE = 256 * SCAN_IPT;
-constexpr int LB_WIN = 8;
 constexpr uint64_t LB64_AGG = 1ull << 62;
 constexpr uint64_t LB64_INC = 2ull << 62;
 constexpr uint64_t LB64_FLAGS = 3ull << 62;
@@ -703,9 +714,9 @@ __global__ __launch_bounds__(256) void k_scan(const uint64_t* __restrict__ skeys
 // ---------------------------------------------------------------------------
 // k_leader — one thread per unique key (segment tail).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ skeys, const SortedRec* __restrict__ srec,
+__global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ skeys, SortedRec* __restrict__ srec,
                                                 const ItemRec* __restrict__ recs, const DevRule* __restrict__ rules,
-                                                uint32_t n_all, TableDesc tab, int local_cache,
+                                                uint32_t n_all, TableDesc tab,
                                                 SegInfo* __restrict__ seg, const uint32_t* __restrict__ tile_heads,
                                                 uint32_t n_scan_tiles, HotCand* __restrict__ cand, EngineCtl* ctl) {
   if (blockIdx.x == 0) {
@@ -722,7 +733,9 @@ __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ ske
     if (threadIdx.x == 0) ctl->n_segments = sh_u[0];
   }
   const uint32_t errs = ctl->err;  // flags of earlier launches
-  if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_BAD_INPUT | ERR_WINDOW_SPAN | ERR_V2_FALLBACK)) return;
+  if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_BAD_INPUT | ERR_WINDOW_SPAN | ERR_FALLBACK |
+              ERR_TABLE_FULL))
+    return;
   const uint32_t n = n_all - ctl->n_nil;  // written by an earlier launch
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
@@ -732,7 +745,7 @@ __global__ __launch_bounds__(256) void k_leader(const uint64_t* __restrict__ ske
   const bool mixed_rule = (tail.head & HEAD_MIXED_RULE) != 0;
   if (j - hp + 1 >= HOT_CAND_MIN && !mixed_rule)  // hot-set candidate for the bucketed pipeline
     emit_candidate(ctl, cand, tail.rule, j - hp + 1, srec[hp].idx);
-  leader_segment(hp, j, tail, mixed_rule, skeys, srec, recs, rules, tab, local_cache, seg, ctl);
+  leader_segment(hp, j, tail, mixed_rule, skeys, srec, recs, rules, tab, seg, ctl);
 }
 
 // ---------------------------------------------------------------------------
@@ -746,12 +759,53 @@ __global__ __launch_bounds__(256) void k_decide(const SortedRec* __restrict__ sr
                                                 int routed, EngineCtl* ctl) {
   const uint32_t errs = ctl->err;  // flags of earlier launches
   if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_TABLE_FULL | ERR_BAD_INPUT | ERR_WINDOW_SPAN |
-              ERR_V2_FALLBACK))
+              ERR_FALLBACK))
     return;
   const uint32_t n = n_all - ctl->n_nil;  // written by k_fingerprint (earlier launch)
   const uint32_t j = blockIdx.x * 256 + threadIdx.x;
   if (j >= n) return;
   decide_pos(j, srec, seg, rules, out, req_thr, routed);
+}
+
+// k_cand_state — hot-set candidates reported by k_leader carry the arrival index of their
+// key's first descriptor: fill in the key-prefix lane state and the unit (one thread each).
+__global__ __launch_bounds__(256) void k_cand_state(DevBatch in, const DevRule* __restrict__ rules, uint64_t seed,
+                                                    HotCand* __restrict__ cand, EngineCtl* ctl) {
+  const uint32_t nc = min((uint32_t)CAND_MAX, ctl->tile_ctr[CAND_CTR][0]);
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= nc) return;
+  HotCand c = cand[i];
+  if (c.first_idx == 0xFFFFFFFFu) return;
+  const uint32_t d = c.first_idx;
+  if (in.recs) {  // routed batch: the record already carries the prefix state
+    c.a = in.recs[d].a;
+    c.b = in.recs[d].b;
+  } else {
+    const uint32_t o0 = in.off[d], o1 = in.off[d + 1];
+    FpState st = fp_init(o1 - o0, seed);
+    hash_prefix(in.blob, o0, o1 - o0, st);
+    c.a = st.a;
+    c.b = st.b;
+  }
+  c.unit = rules[c.rule].unit;
+  cand[i] = c;
+}
+
+// k_occ_update — one thread: the batch's new slots per region into the occupancy counts
+// (the LSD pipeline; v4's last k4_group block does the same).
+__global__ void k_occ_update(RegionOcc* __restrict__ occ, EngineCtl* ctl) {
+  const uint32_t errs = ctl->err;
+  if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_BAD_INPUT | ERR_WINDOW_SPAN | ERR_FALLBACK |
+              ERR_TABLE_FULL))
+    return;
+  uint32_t ins[8], n = 0;
+  for (int r = 0; r < 8; ++r) {
+    ins[r] = ctl->tile_ctr[INS_CTR0 + r][0];
+    ctl->ins[r] = ins[r];
+    n += ins[r];
+  }
+  ctl->n_inserted = n;
+  occ_update(occ, ctl->gen_max, ins);
 }
 
 // ---------------------------------------------------------------------------
@@ -772,10 +826,10 @@ void launch_histogram(hipStream_t st, const uint64_t* keys, uint32_t n, int lo_b
                      fpart2);
 }
 void launch_hist_scan(hipStream_t st, const uint32_t* part, uint32_t n, uint32_t* sub, int npasses,
-                      const uint32_t* fpart2, EngineCtl* ctl) {
+                      const uint32_t* fpart2, const RegionOcc* occ, EngineCtl* ctl) {
   const uint32_t fpb = fpart2 ? hist_blocks(n) : 0;
   hipLaunchKernelGGL(k_hist_scan, dim3(npasses * HIST_SUB + (fpb ? 1 : 0)), dim3(256), 0, st, part, hist_blocks(n),
-                     sub, npasses, fpart2, fpb, ctl);
+                     sub, npasses, fpart2, fpb, occ, ctl);
 }
 uint32_t hist_sub_words() { return HIST_SUB * RADIX; }
 void launch_fallback_lo_keys(hipStream_t st, const ItemRec* recs, const uint64_t* keys_orig, uint32_t n,
@@ -799,11 +853,18 @@ void launch_scan(hipStream_t st, const uint64_t* skeys, const uint32_t* svals, c
   hipLaunchKernelGGL(k_scan, dim3(scan_tiles(n)), dim3(256), 0, st, skeys, svals, recs, n, lo_bit, check_mixed, srec,
                      lb_sum, lb_head, tile_ctr, tile_heads, ctl);
 }
-void launch_leader(hipStream_t st, const uint64_t* skeys, const SortedRec* srec, const ItemRec* recs,
-                   const DevRule* rules, uint32_t n, const TableDesc& tab, int local_cache, SegInfo* seg,
+void launch_leader(hipStream_t st, const uint64_t* skeys, SortedRec* srec, const ItemRec* recs,
+                   const DevRule* rules, uint32_t n, const TableDesc& tab, SegInfo* seg,
                    const uint32_t* heads, uint32_t n_heads, HotCand* cand, EngineCtl* ctl) {
   hipLaunchKernelGGL(k_leader, dim3((n + 255) / 256), dim3(256), 0, st, skeys, srec, recs, rules, n, tab,
-                     local_cache, seg, heads, n_heads, cand, ctl);
+                     seg, heads, n_heads, cand, ctl);
+}
+void launch_cand_state(hipStream_t st, const rl_batch& b, const DevRule* rules, uint64_t seed, HotCand* cand,
+                       EngineCtl* ctl) {
+  hipLaunchKernelGGL(k_cand_state, dim3(CAND_MAX / 256), dim3(256), 0, st, make_dev_batch(b), rules, seed, cand, ctl);
+}
+void launch_occ_update(hipStream_t st, RegionOcc* occ, EngineCtl* ctl) {
+  hipLaunchKernelGGL(k_occ_update, dim3(1), dim3(1), 0, st, occ, ctl);
 }
 void launch_decide(hipStream_t st, const SortedRec* srec, const SegInfo* seg, const DevRule* rules, uint32_t n,
                    rl_status* out, uint32_t* req_thr, int routed, EngineCtl* ctl) {

@@ -31,20 +31,20 @@
 #include "rl_common.h"
 #include "rl_decide.h"
 #include "rl_device.h"
-#include "rl_v3_dev.h"
+#include "rl_tile.h"
 
 namespace rlhip {
 namespace v4 {
 
-using v3::D3;
-using v3::NT;
-using v3::R;
-using v3::SegEl;
-using v3::T;
-using v3::W;
-using v3::BKT_NONE;
+using tile::D3;
+using tile::NT;
+using tile::R;
+using tile::SegEl;
+using tile::T;
+using tile::W;
+using tile::BKT_NONE;
 
-constexpr int ROW = V3_ROW16;  // u16 bucket starts per tile (entries [0, NBUCKETS] used)
+constexpr int ROW = V4_ROW16;  // u16 bucket starts per tile (entries [0, NBUCKETS] used)
 static_assert(ROW >= NBUCKETS + 1, "row holds every bucket start and the end");
 constexpr int GBLOCKS = 1024;              // k4_group blocks (at least; 4 per CU, one round)
 constexpr int MSD_GROUPS = MSD_BUCKETS / 64;  // k4_scan blocks of MSD buckets (one range list each)
@@ -58,7 +58,6 @@ constexpr int R_BPRE = R_START + MSD_GROUPS * (RANGE_MAX + 1);
 constexpr int R_GTOT = R_BPRE + MSD_BUCKETS;
 constexpr int R_BTOT = R_GTOT + MSD_GROUPS;  // per MSD bucket its batch total (k4_scan block pair hand-off)
 constexpr int RANGE_WORDS = R_BTOT + MSD_BUCKETS;
-constexpr int HOT_HALF = HOT_BUCKETS / 2;  // hot buckets per k4_group hot part
 constexpr int DONE_CTR = 27;               // EngineCtl::tile_ctr[DONE_CTR][0]: k4_group blocks done
 constexpr int G_NT = 256;
 constexpr int G_W = G_NT / 64;
@@ -73,11 +72,11 @@ constexpr int G_IPT = 3;        // positions per thread kept in registers (table
 constexpr int GS_HASH = 2048;   // global-scratch hash slots (> BUCKET_CAP)
 constexpr uint32_t G_EMPTY = 0xFFFFFFFFu;
 static_assert(G_CAP <= G_NT * G_IPT && G_HASH > G_CAP && GS_HASH > BUCKET_CAP, "k4_group geometry");
-static_assert(DONE_CTR != DFR_CTR && DONE_CTR != SCAN_CTR && DONE_CTR != CAND_CTR &&
+static_assert(DONE_CTR != DFR_CTR && DONE_CTR != CAND_CTR &&
                   (DONE_CTR < INS_CTR0 || DONE_CTR >= INS_CTR0 + INS_LINES),
               "control-block rows");
 
-RL_DEV uint32_t rule_of(uint32_t rn) { return rn & (V3_MAX_RULES - 1u); }
+using tile::rule_of;
 
 #ifdef RL_STAMPS
 // Diagnostic build only (tools/stamps4.py): per-block phase timestamps (s_memrealtime, 100 MHz)
@@ -126,6 +125,12 @@ RL_DEV void emit_cand_sc1(EngineCtl* ctl, HotCand* __restrict__ cand, uint32_t r
   }
 }
 static_assert(sizeof(HotCand) == 32 && sizeof(Deferred) == 32, "32-B hand-off records");
+static_assert(sizeof(HotBucket) == 64, "HotBucket is one 64-B line");
+// The counter a hot key's INCRBYs go to: the main store's, or the per-second store's.
+RL_DEV uint32_t* hot_counter(const HotBucket& x) {
+  Slot* s = reinterpret_cast<Slot*>(x.slot);
+  return (x.flags & HB_PS) ? &s->pcount : &s->count;
+}
 constexpr int SHARD_CTR0 = 0;  // EngineCtl::tile_ctr[0..7][0]: k4_group blocks done, by blockIdx & 7
 
 // ---------------------------------------------------------------------------
@@ -152,7 +157,7 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t tile = blockIdx.x, ntiles = gridDim.x;
   const uint32_t t0 = tile * T;
-  v3::load_hot_table(hot, sh_hot);
+  tile::load_hot_table(hot, sh_hot);
   for (int b = tid; b < ROW / 2; b += NT) reinterpret_cast<uint32_t*>(sh_cnt)[b] = 0;
   for (int b = tid; b < HOT_BUCKETS; b += NT) sh_hs[b] = 0;
   if (tid < FP_PART_WORDS) sh_f[tid] = 0;
@@ -167,12 +172,10 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   D3 d[R];
   uint32_t err = 0;
   if (ROUTED)
-    v3::load_routed(in, rules, n_rules, sh_hot, t0, d, err);
+    tile::load_routed(in, rules, n_rules, sh_hot, t0, d, err);
   else
-    v3::load_descs(in, rules, n_rules, seed, sh_hot, t0, d, err);
-  uint32_t gmin[8], gmax[8], nil = 0;
-#pragma unroll
-  for (int rg = 0; rg < 8; ++rg) { gmin[rg] = 0xFFFFFFFFu; gmax[rg] = 0; }
+    tile::load_descs(in, rules, n_rules, seed, sh_hot, t0, d, err);
+  uint32_t nil = 0;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint32_t o = r * NT + tid;
@@ -180,37 +183,52 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
     s_d[o] = (uint16_t)b;
     s_h[o] = d[r].h;
     s_pa[o] = (uint16_t)o;
-    if (b < NIL_BUCKET) {
-      const uint32_t region = key_region(d[r].key);
-#pragma unroll
-      for (int rg = 0; rg < 8; ++rg)  // static register indexing
-        if ((uint32_t)rg == region) {
-          gmin[rg] = d[r].gen < gmin[rg] ? d[r].gen : gmin[rg];
-          gmax[rg] = d[r].gen > gmax[rg] ? d[r].gen : gmax[rg];
-        }
-    } else if (b == NIL_BUCKET) {
-      ++nil;
-    }
+    nil += b == NIL_BUCKET;
   }
+  // Per-region generation range and descriptor count; per (unit, parity) the unit window of
+  // hot descriptors. Reductions run only for regions / windows present in the wave.
 #pragma unroll
   for (int rg = 0; rg < 8; ++rg) {
-    const uint32_t mx = wave_max_u32(gmax[rg]);
-    if (mx) {  // wave-uniform
-      const uint32_t mn = wave_min_u32(gmin[rg]);
-      if (lane == 0) {
-        atomicMax(&sh_f[rg], ~mn);
-        atomicMax(&sh_f[8 + rg], mx);
+    uint32_t mn = 0xFFFFFFFFu, mx = 0, c = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool m = d[r].bucket < NIL_BUCKET && key_region(d[r].key) == (uint32_t)rg;
+      c += (uint32_t)__popcll(__ballot(m));
+      if (m) {
+        mn = d[r].gen < mn ? d[r].gen : mn;
+        mx = d[r].gen > mx ? d[r].gen : mx;
       }
     }
+    if (c) {  // wave-uniform
+      mn = wave_min_u32(mn);
+      mx = wave_max_u32(mx);
+      if (lane == 0) {
+        atomicMax(&sh_f[FP_GMIN + rg], ~mn);
+        atomicMax(&sh_f[FP_GMAX + rg], mx);
+        atomicAdd(&sh_f[FP_CNT + rg], c);
+      }
+    }
+    uint32_t um = 0;
+    uint64_t any = 0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const bool m = d[r].bucket < (uint32_t)HOT_BUCKETS && d[r].uw == (uint32_t)rg;
+      any |= __ballot(m);
+      if (m) um = d[r].uwv > um ? d[r].uwv : um;
+    }
+    if (any) {
+      um = wave_max_u32(um);
+      if (lane == 0) atomicMax(&sh_f[FP_UW + rg], um);
+    }
   }
-  nil = v3::wave_sum(nil);
-  if (lane == 0 && nil) atomicAdd(&sh_f[16], nil);
+  nil = tile::wave_sum(nil);
+  if (lane == 0 && nil) atomicAdd(&sh_f[FP_NIL], nil);
   if (err) atomicOr(&sh_err, err);
   // Stable sort of the tile by bucket, then a segmented scan in sorted order:
   // hot -> inclusive prefix of h inside (tile, bucket); each bucket's last descriptor ->
   // the bucket's count (and h sum) in this tile.
-  v3::tile_digit_pass(s_d, s_pa, s_pb, 0, s_cnt, sh_w);  // includes barriers
-  v3::tile_digit_pass(s_d, s_pb, s_pa, 6, s_cnt, sh_w);
+  tile::tile_digit_pass(s_d, s_pa, s_pb, 0, s_cnt, sh_w);  // includes barriers
+  tile::tile_digit_pass(s_d, s_pb, s_pa, 6, s_cnt, sh_w);
   {
     const uint32_t s0 = tid * R;
     uint32_t od[R], dd[R], fl[R];
@@ -227,7 +245,7 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
       fl[q] = dv != prev_d;
       hv[q] = s_h[o];
       prev_d = dv;
-      t = v3::seg_op(t, SegEl{fl[q], s0 + q, hv[q]});
+      t = tile::seg_op(t, SegEl{fl[q], s0 + q, hv[q]});
     }
     SegEl incl = t;
 #pragma unroll
@@ -236,7 +254,7 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
       y.f = __shfl_up(incl.f, s, 64);
       y.hp = __shfl_up(incl.hp, s, 64);
       y.s = __shfl_up(incl.s, s, 64);
-      if (lane >= (uint32_t)s) incl = v3::seg_op(y, incl);
+      if (lane >= (uint32_t)s) incl = tile::seg_op(y, incl);
     }
     if (lane == 63) s_agg[wave] = incl;
     SegEl wex;
@@ -249,12 +267,12 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
 #pragma unroll
     for (int w = 0; w < W - 1; ++w) {
       const SegEl a = s_agg[w];  // wave-uniform LDS read
-      if ((uint32_t)w < wave) run = v3::seg_op(run, a);
+      if ((uint32_t)w < wave) run = tile::seg_op(run, a);
     }
-    run = v3::seg_op(run, wex);
+    run = tile::seg_op(run, wex);
 #pragma unroll
     for (int q = 0; q < R; ++q) {
-      run = v3::seg_op(run, SegEl{fl[q], s0 + q, hv[q]});
+      run = tile::seg_op(run, SegEl{fl[q], s0 + q, hv[q]});
       const uint32_t b = dd[q];
       if (b < (uint32_t)HOT_BUCKETS) s_res[od[q]] = run.s;
       s_pb[od[q]] = (uint16_t)(s0 + q);  // sorted position of descriptor od[q]
@@ -277,7 +295,7 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
       sum += v[k];
     }
     uint32_t total;
-    uint32_t run = v3::block_excl_scan<NT>(sum, sh_w, total);
+    uint32_t run = tile::block_excl_scan<NT>(sum, sh_w, total);
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const uint32_t e = tid * PER + k;
@@ -311,7 +329,7 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
     m.idx = i;
     m.req = x.req;
     m.h = x.h;
-    m.rn = rule_of(x.rule) | (x.now_mod << V3_RULE_BITS);
+    m.rn = rule_of(x.rule) | (x.now_mod << V4_RULE_BITS);
     srec[t0 + s_pb[o]] = m;
   }
   __syncthreads();
@@ -341,9 +359,8 @@ constexpr int SCAN_Q = 16;  // MSD column entries per lane kept in registers
 // tile) are pulled by 32 CUs, 8 tiles per lane at config 3.
 constexpr int HOT_PER_BLOCK = 16;
 constexpr int HOT_SCAN_BLOCKS = HOT_BUCKETS / HOT_PER_BLOCK;
-constexpr int HOT_SLICES = SCAN_NT / HOT_PER_BLOCK;
 constexpr int HOT_Q = 16;   // hot column entries per lane kept in registers
-static_assert(HOT_BUCKETS % 64 == 0 && V3_SCAN_BUCKETS % 64 == 0, "bucket blocks");
+static_assert(HOT_BUCKETS % 64 == 0 && MSD_BUCKETS % 64 == 0, "bucket blocks");
 static_assert(T < 65536 && SCAN_Q % 2 == 0, "per-tile counts pack in u16 pairs");
 static_assert(MSD_GROUPS <= 64 && PAIR_CTR != DONE_CTR && PAIR_CTR != DFR_CTR && PAIR_CTR != CAND_CTR &&
                   (PAIR_CTR < INS_CTR0 || PAIR_CTR >= INS_CTR0 + INS_LINES) && PAIR_CTR >= SHARD_CTR0 + 8,
@@ -375,11 +392,13 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
                                                    const unsigned long long* __restrict__ thsum, uint32_t ntiles,
                                                    unsigned long long* __restrict__ hoff,
                                                    const uint32_t* __restrict__ fpart,
-                                                   const HotEntry* __restrict__ hot_list, HotBucket3* __restrict__ hb,
-                                                   TableDesc tab, int local_cache, HotCand* __restrict__ cand,
-                                                   uint32_t* __restrict__ heads_out, uint16_t* __restrict__ toff,
-                                                   uint32_t* __restrict__ ranges, const uint32_t* __restrict__ poison,
-                                                   EngineCtl* ctl) {
+                                                   const HotEntry* __restrict__ hot_list, HotBucket* __restrict__ hb,
+                                                   TableDesc tab, HotCand* __restrict__ cand,
+                                                   uint32_t* __restrict__ heads_out, uint32_t* __restrict__ ins_out,
+                                                   uint16_t* __restrict__ toff, uint32_t* __restrict__ ranges,
+                                                   const uint32_t* __restrict__ poison,
+                                                   const RegionOcc* __restrict__ occ, EngineCtl* ctl) {
+  const uint32_t local_cache = tab.local_cache;
   __shared__ uint32_t s_f[FP_PART_WORDS];
   __shared__ uint32_t s_pc[SCAN_W][64];
   __shared__ unsigned long long s_ph[SCAN_W][64];
@@ -387,7 +406,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
   // A batch submitted behind a refused one (two batches in flight) is refused too, before
   // anything touches the table: the engine reruns both, in order (rl_engine::settle).
   if (*poison) {
-    if (blockIdx.x == 0 && tid == 0) atomicOr(&ctl->err, ERR_V2_FALLBACK);
+    if (blockIdx.x == 0 && tid == 0) atomicOr(&ctl->err, ERR_FALLBACK);
     return;
   }
   ST5(0);
@@ -456,21 +475,21 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     }
   }
   s_pc[wave][lane] = c;
-  bool span = false;
+  bool span = false, cap_ok = true;
   if (hotb) {
     s_ph[wave][lane] = hs;
     for (uint32_t g = tid + SCAN_NT; g < ntiles; g += SCAN_NT) {  // batches over SCAN_NT tiles
 #pragma unroll
       for (int w = 0; w < FP_PART_WORDS; ++w) {
         const uint32_t x = fpart[(size_t)g * FP_PART_WORDS + w];
-        fv[w] = w < 16 ? (x > fv[w] ? x : fv[w]) : fv[w] + x;
+        fv[w] = fp_is_max(w) ? (x > fv[w] ? x : fv[w]) : fv[w] + x;
       }
     }
 #pragma unroll
     for (int w = 0; w < FP_PART_WORDS; ++w) {
-      const uint32_t x = w < 16 ? wave_max_u32(fv[w]) : v3::wave_sum(fv[w]);
+      const uint32_t x = fp_is_max(w) ? wave_max_u32(fv[w]) : tile::wave_sum(fv[w]);
       if (lane == 0 && x) {
-        if (w < 16) atomicMax(&s_f[w], x);
+        if (fp_is_max(w)) atomicMax(&s_f[w], x);
         else atomicAdd(&s_f[w], x);
       }
     }
@@ -482,14 +501,18 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     // a region's generations share its parity, so a valid batch has ONE generation per region.
 #pragma unroll
     for (int rg = 0; rg < 8; ++rg) {
-      const uint32_t mx = s_f[8 + rg], mn = ~s_f[rg];
+      const uint32_t mx = s_f[FP_GMAX + rg], mn = ~s_f[FP_GMIN + rg];
       span |= mx != 0 && mx - mn > 1u;
     }
+    // Capacity (before any table write): every hot block computes the same verdict and
+    // claims nothing when it fails; block 0 refuses the batch.
+    cap_ok = capacity_ok(occ, &s_f[FP_GMAX], &s_f[FP_CNT]);
     if (blockIdx.x == 0) {
-      if (tid < 8) ctl->gen_min[tid] = ~s_f[tid];
-      else if (tid < 16) ctl->gen_max[tid - 8] = s_f[tid];
-      else if (tid == 16) ctl->n_nil = s_f[16];
+      if (tid < 8) ctl->gen_min[tid] = ~s_f[FP_GMIN + tid];
+      else if (tid < 16) ctl->gen_max[tid - 8] = s_f[FP_GMAX + tid - 8];
+      else if (tid == 16) ctl->n_nil = s_f[FP_NIL];
       if (tid == 0 && span) atomicOr(&ctl->err, ERR_WINDOW_SPAN);
+      if (tid == 0 && !cap_ok) atomicOr(&ctl->err, ERR_TABLE_FULL);
     }
   }
   uint32_t ctot = 0, crun = 0;
@@ -550,7 +573,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     // Hand-off inside the pair: this block's 32 bucket totals (lanes 0..31 = slice 0), then
     // the pair counter; the second block to arrive reads both halves and packs the group.
     if (lane < (uint32_t)MSD_HALF) {
-      if (ctot > (uint32_t)BUCKET_CAP) atomicOr(&ctl->err, ERR_V2_FALLBACK);
+      if (ctot > (uint32_t)BUCKET_CAP) atomicOr(&ctl->err, ERR_FALLBACK);
       st_relaxed(&ranges[R_BTOT + mb], ctot);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -559,7 +582,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     if (__builtin_amdgcn_readfirstlane(arrived) == 0u) return;  // the other block packs
     ctot = ld_relaxed(&ranges[R_BTOT + m * 64 + lane]);  // bucket lane of the group
     const uint32_t g = m;
-    const uint32_t incl = v3::wave_incl_scan<uint32_t>(ctot);
+    const uint32_t incl = tile::wave_incl_scan<uint32_t>(ctot);
     ranges[R_BPRE + m * 64 + lane] = incl - ctot;
     if (lane == 63) ranges[R_GTOT + g] = incl;
     // Pack the group's 64 buckets greedily into k4_group ranges of whole buckets holding at
@@ -623,53 +646,68 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     ST5(3);
     // Hot key leader: find or claim the key's slot and read the counter before this batch. A
     // claimed slot starts at count 0, which is invisible if the batch is later rejected.
-    HotBucket3 x;
+    HotBucket x;
     x.key = x.fp_lo = x.base = x.slot = x.total = 0;
     x.rule = 0;
     x.flags = 0;
     x.rstar = 0xFFFFFFFFu;
-    x.pad[0] = x.pad[1] = x.pad[2] = 0;
+    x.ws = x.t_all = x.t_rstar = 0;
     const uint32_t errs = ctl->err;  // flags of k4_hist
     uint32_t heads = 0;
+    uint32_t ins_region = 8;  // region of a newly claimed slot
     // lanes 0..15 of wave 0 (slice 0) lead the block's 16 hot buckets
-    if (lane < (uint32_t)HOT_PER_BLOCK && ctot && !span &&
-        !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME | ERR_V2_FALLBACK))) {
+    if (lane < (uint32_t)HOT_PER_BLOCK && ctot && !span && cap_ok &&
+        !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME | ERR_FALLBACK))) {
       const HotEntry he = hot_list[b >> 1];
-      const uint32_t region = (he.unit - 1u) * 2u + (b & 1u);
-      const uint32_t gen = s_f[8 + region];  // the region's one generation in this batch
-      const uint64_t ws = (uint64_t)(gen - 1u) * unit_div(he.unit);
+      // the key string's window: the hot prefix's unit window of this parity
+      const uint32_t uwv = s_f[FP_UW + (he.unit - 1u) * 2u + (b & 1u)];
+      const uint32_t div = unit_div(he.unit);
+      const uint32_t ws = (uwv - 1u) * div;
+      const Place pl = place_of(ws);
       uint64_t hi, lo;
       fp_final(FpState{he.a, he.b}, ws, hi, lo);
-      x.key = make_sort_key(region, hi);
+      x.key = make_sort_key(pl.region, hi);
       x.fp_lo = lo;
       x.rule = he.rule;
       x.total = htot;
+      x.ws = ws;
       Slot* slot = nullptr;
       bool existed = false;
-      if (!table_claim(tab, x.key, lo, gen, slot, existed)) {
-        atomicOr(&ctl->err, ERR_TABLE_FULL);
+      if (!table_claim(tab, x.key, lo, pl.gen, slot, existed)) {
+        atomicOr(&ctl->err, ERR_TABLE_FULL);  // unreachable below the load limit
       } else {
-        if (existed) {
-          x.base = slot->count;
-          x.flags = (slot->flags & SLOT_FROZEN) ? HB_FROZEN_PRE : 0u;
+        if (!existed) {
+          slot_reset(slot, x.key);
+          ins_region = pl.region;
+        }
+        const KeyState ks = existed ? read_state(slot) : KeyState{0, 0, 0, 0};
+        const bool ps = per_second_store(tab, he.unit);
+        bool frozen_pre = false;
+        if (!fast_state(ks, ps, local_cache != 0, ws, div, x.base, frozen_pre)) {
+          // an expiry falls among this batch's touches of a shared string: exact path
+          atomicOr(&ctl->err, ERR_FALLBACK);
         } else {
-          slot->key = x.key;
-          slot->fp_lo_hi = (uint32_t)(lo >> 32);
-          slot->count = 0;
-          slot->flags = 0;
+          // an expired main counter restarts at 0 before the atomicMax updates of k4_place
+          if (!ps && ks.exp <= ws && ks.count) slot->count = 0;
+          x.flags = (frozen_pre ? HB_FROZEN_PRE : 0u) | (ps ? HB_PS : 0u);
         }
         x.slot = (uint64_t)(uintptr_t)slot;
         // The local-cache freeze point is found from a monotone INCRBY sequence; a batch whose
         // counter would pass 2^32 goes to the LSD pipeline (uint32 wraparound, R10).
         if (local_cache && !(x.flags & HB_FROZEN_PRE) && x.base + htot >= (1ull << 32))
-          atomicOr(&ctl->err, ERR_V2_FALLBACK);
+          atomicOr(&ctl->err, ERR_FALLBACK);
         heads = 1;
       }
-      if (slot != nullptr && !existed) heads |= 1u << 16;  // a new table slot
       if (ctot >= HOT_CAND_MIN) emit_candidate(ctl, cand, he.rule, ctot, 0xFFFFFFFFu, he.a, he.b, he.unit);
     }
+    // new slots per region of this block (the last k4_group block adds them to RegionOcc)
+#pragma unroll
+    for (int rg = 0; rg < 8; ++rg) {
+      const uint64_t m = __ballot(ins_region == (uint32_t)rg);
+      if (lane == 0) ins_out[blockIdx.x * 8 + rg] = (uint32_t)__popcll(m);
+    }
     if (lane < (uint32_t)HOT_PER_BLOCK) hb[b] = x;
-    heads = v3::wave_sum(heads);
+    heads = tile::wave_sum(heads);
     if (lane == 0) heads_out[blockIdx.x] = heads;
     ST5(4);
   }
@@ -811,51 +849,88 @@ RL_DEV void g_scan(const GS& g, uint32_t m, LSeg* s_agg, LSeg* s_carry) {
 
 RL_DEV uint32_t g_tail(const GS& g, uint32_t k) { return g.list[g.end[g.grp[k]] - 1u]; }
 
+// The exact sequential path of a key (rare: a string shared by units of different sizes
+// whose expiry falls inside the batch), run by its leader in a pass after the leaders' so
+// its registers are not live across the fast path's. rec[k].key holds the key's slot.
+constexpr uint32_t SEG_EXOTIC_PENDING = 0xFFFFFFFCu;
+RL_DEV void g_lead_exotic(const GS& g, uint32_t k, const DevRule* __restrict__ rules, const TableDesc& tab,
+                          EngineCtl* ctl) {
+  Slot* slot = reinterpret_cast<Slot*>(g.rec[k].key);
+  const uint32_t s = g.grp[k];
+  const uint32_t n = g.cnt[s], e0 = g.end[s] - n;
+  const uint32_t region = key_region(slot->key);
+  const uint32_t ws = region_ws(region, ctl->gen_max[region]);
+  KeyState ks = read_state(slot);
+  exotic_sequence(
+      ks, tab, rules, n,
+      [&](uint32_t q) {
+        const MRec& m = g.rec[g.list[e0 + q]];
+        return SeqItem{m.req, ws + (m.rn >> V4_RULE_BITS), m.h, rule_of(m.rn)};
+      },
+      [&](uint32_t q, uint64_t v) { g.P[g.list[e0 + q]] = v; });
+  write_state(slot, ks);
+  g.rec[k].key = 0;
+  g.rec[k].fp_lo = SEG_EXOTIC;
+}
+
 // Run by the key's last record: table probe/claim, INCRBY of the key's whole sequence in
-// serial order, local-cache freeze (fixed_cache_impl.go:55-123, base_limiter.go:88-106).
-// Leaves the counter before the batch in rec[k].key and the freeze in rec[k].fp_lo.
-RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, const TableDesc& tab, int local_cache,
-                   HotCand* cand, EngineCtl* ctl, bool has_pre, const SlotView& pre, int cand_on, uint32_t& heads) {
+// serial order, EXPIRE, local-cache freeze (fixed_cache_impl.go:55-123, base_limiter.go:88-106).
+// Leaves the counter before the batch in rec[k].key and the freeze in rec[k].fp_lo; an exotic
+// key (a string shared by units of different sizes whose expiry falls inside the batch)
+// leaves per-position replies in P (SEG_EXOTIC). New slots are counted per region in ins[].
+RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, const TableDesc& tab, HotCand* cand,
+                   EngineCtl* ctl, bool has_pre, const SlotView& pre, int cand_on, uint32_t& heads, uint32_t* ins) {
   const uint64_t key = g.rec[k].key, lo = g.rec[k].fp_lo;
   const uint32_t rule = rule_of(g.rec[k].rn);
   const uint32_t s = g.grp[k];
   const uint32_t n = g.cnt[s], e1 = g.end[s], e0 = e1 - n;
   const uint64_t Pk = g.P[k];
-  bool mixed = false;
+  const DevRule R0 = rules[rule];
+  bool mixed = false, mixed_unit = false;
   heads += 1;
-  if ((cand_on && n >= HOT_MIN_SEG) || local_cache) {
-    for (uint32_t e = e0; e < e1; ++e) mixed |= rule_of(g.rec[g.list[e]].rn) != rule;
-    if (cand_on && n >= HOT_MIN_SEG && !mixed) emit_cand_sc1(ctl, cand, rule, n, g.rec[g.list[e0]].idx);
+  for (uint32_t e = e0; e < e1; ++e) {
+    const uint32_t r = rule_of(g.rec[g.list[e]].rn);
+    if (r != rule) {
+      mixed = true;
+      mixed_unit |= rules[r].unit != R0.unit;
+    }
   }
-  const uint32_t gen = ctl->gen_max[key_region(key)];  // the region's one generation (k4_scan)
+  if (cand_on && n >= HOT_MIN_SEG && !mixed) emit_cand_sc1(ctl, cand, rule, n, g.rec[g.list[e0]].idx);
+  const uint32_t region = key_region(key);
+  const uint32_t gen = ctl->gen_max[region];  // the region's one generation (k4_scan)
+  const uint32_t ws = region_ws(region, gen);
   Slot* slot = nullptr;
   bool existed = false;
-  uint64_t base = 0;
-  uint32_t sflags = 0;
-  const bool claimed = has_pre ? table_claim_pre(tab, key, lo, gen, pre, slot, existed, base, sflags)
+  KeyState ks{0, 0, 0, 0};
+  const bool claimed = has_pre ? table_claim_pre(tab, key, lo, gen, pre, slot, existed, ks)
                                : table_claim(tab, key, lo, gen, slot, existed);
   if (!claimed) {
-    atomicOr(&ctl->err, ERR_TABLE_FULL);
+    atomicOr(&ctl->err, ERR_TABLE_FULL);  // unreachable below the load limit
     g.rec[k].key = 0;
     g.rec[k].fp_lo = SEG_NO_FREEZE;
     return;
   }
-  if (existed && !has_pre) {
-    base = slot->count;
-    sflags = slot->flags;
-  }
-  const bool frozen_pre = existed && (sflags & SLOT_FROZEN) != 0;
+  if (existed && !has_pre) ks = read_state(slot);
   if (!existed) {
-    slot->key = key;
-    slot->fp_lo_hi = (uint32_t)(lo >> 32);
+    slot_reset(slot, key);
     heads += 1u << 16;
+    atomicAdd(&ins[region], 1u);
+  }
+  const bool ps = per_second_store(tab, R0.unit);
+  uint64_t base = 0;
+  bool frozen_pre = false;
+  if (mixed_unit || !fast_state(ks, ps, tab.local_cache != 0, ws, R0.div, base, frozen_pre)) {
+    // exact sequential path, in a pass of its own after the leaders (g_lead_exotic)
+    g.rec[k].key = (uint64_t)(uintptr_t)slot;
+    g.rec[k].fp_lo = SEG_EXOTIC_PENDING;
+    return;
   }
   uint32_t freeze = SEG_NO_FREEZE;
   uint64_t final_count = base + Pk;
+  uint32_t last = k;  // the key's last record whose INCRBY happens
   if (frozen_pre) {
     freeze = SEG_FROZEN_BEFORE;  // every descriptor is a local-cache hit: no INCRBY
-    final_count = base;
-  } else if (local_cache) {
+  } else if (tab.local_cache) {
     // the first record (arrival order) whose INCRBY reply exceeds its limit freezes the key;
     // the INCRBYs of its own request still happen (all lookups precede the Sets)
     const bool exact = !mixed && base + Pk < (1ull << 32);
@@ -865,17 +940,25 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
       const uint32_t L = rules[rule_of(g.rec[j].rn)].L;
       if (exact ? after > (uint64_t)L : (uint32_t)after > L) {
         const uint32_t rstar = g.rec[j].req;
-        uint64_t last = g.P[j];
-        for (uint32_t f = e + 1; f < e1 && g.rec[g.list[f]].req == rstar; ++f) last = g.P[g.list[f]];
+        last = j;
+        for (uint32_t f = e + 1; f < e1 && g.rec[g.list[f]].req == rstar; ++f) last = g.list[f];
         freeze = rstar;
-        final_count = base + last;
+        final_count = base + g.P[last];
         break;
       }
     }
   }
-  slot->count = final_count;
-  if (freeze != SEG_NO_FREEZE && freeze != SEG_FROZEN_BEFORE) slot->flags = SLOT_FROZEN;
-  else if (!existed) slot->flags = 0;
+  if (freeze != SEG_FROZEN_BEFORE) {
+    const uint32_t t_last = ws + (g.rec[last].rn >> V4_RULE_BITS);
+    if (ps) {
+      ks.pcount = (uint32_t)final_count;
+    } else {
+      ks.count = (uint32_t)final_count;
+      ks.exp = t_last + R0.div;  // EXPIRE key div of the last INCRBY (fixed_cache_impl.go:69-72)
+    }
+    if (freeze != SEG_NO_FREEZE) ks.frz = t_last + R0.div;  // freecache TTL (base_limiter.go:102)
+    write_state(slot, ks);
+  }
   g.rec[k].key = base;
   g.rec[k].fp_lo = freeze;
 }
@@ -884,9 +967,8 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
 // bits) and the new table slots claimed (high 16 bits) by this thread.
 template <bool LDS>
 RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__ rules, const TableDesc& tab,
-                            int local_cache, rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
-                            HotCand* cand, int cand_on, int routed, LSeg* s_agg, LSeg* s_carry, uint32_t* sh_w,
-                            EngineCtl* ctl) {
+                            rl_status* __restrict__ out, uint32_t* __restrict__ req_thr, HotCand* cand, int cand_on,
+                            int routed, LSeg* s_agg, LSeg* s_carry, uint32_t* sh_w, uint32_t* s_ins, EngineCtl* ctl) {
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
   uint32_t heads = 0;
   // The staging (and the hash-table reset before it) is complete: read each position's first
@@ -908,7 +990,7 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
     uint32_t sum = 0;
     for (uint32_t q = 0; q < spt; ++q) sum += g.cnt[s0 + q];
     uint32_t tot;
-    uint32_t run = v3::block_excl_scan<G_NT>(sum, sh_w, tot);
+    uint32_t run = tile::block_excl_scan<G_NT>(sum, sh_w, tot);
     for (uint32_t q = 0; q < spt; ++q) {
       g.end[s0 + q] = (uint16_t)run;
       run += g.cnt[s0 + q];
@@ -927,12 +1009,17 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
     for (int j = 0; j < G_IPT; ++j) {
       const uint32_t k = tid + j * G_NT;
       if (k < m && g_tail(g, k) == k)
-        g_lead(g, k, rules, tab, local_cache, cand, ctl, true, pre[j], cand_on, heads);
+        g_lead(g, k, rules, tab, cand, ctl, true, pre[j], cand_on, heads, s_ins);
     }
   } else {
     for (uint32_t k = tid; k < m; k += G_NT)
-      if (g_tail(g, k) == k) g_lead(g, k, rules, tab, local_cache, cand, ctl, false, SlotView{}, cand_on, heads);
+      if (g_tail(g, k) == k) g_lead(g, k, rules, tab, cand, ctl, false, SlotView{}, cand_on, heads, s_ins);
   }
+  __threadfence_block();
+  __syncthreads();
+  // exotic keys (rare): their leaders' sequential pass
+  for (uint32_t k = tid; k < m; k += G_NT)
+    if (g.rec[k].fp_lo == SEG_EXOTIC_PENDING && g_tail(g, k) == k) g_lead_exotic(g, k, rules, tab, ctl);
   __threadfence_block();
   __syncthreads();
   ST4(4);
@@ -940,7 +1027,7 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
     const MRec x = g.rec[k];
     const uint32_t t = g_tail(g, k);
     const MRec& lt = g.rec[t];
-    v3::decide_at(x.idx, x.req, rule_of(x.rn), x.h, x.rn >> V3_RULE_BITS, lt.key, g.P[k], (uint32_t)lt.fp_lo, rules,
+    tile::decide_at(x.idx, x.req, rule_of(x.rn), x.h, x.rn >> V4_RULE_BITS, lt.key, g.P[k], (uint32_t)lt.fp_lo, rules,
                   out, req_thr, routed);
   }
   return heads;
@@ -957,7 +1044,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
                                                const uint32_t* __restrict__ ranges,
                                                const DevRule* __restrict__ rules,
                                                const unsigned long long* __restrict__ hoff,
-                                               HotBucket3* __restrict__ hb, int local_cache,
+                                               HotBucket* __restrict__ hb, int local_cache,
                                                MRec* __restrict__ mrec, rl_status* __restrict__ out,
                                                uint32_t* __restrict__ req_thr, Deferred* __restrict__ dfr, int routed,
                                                uint32_t* __restrict__ poison, EngineCtl* ctl) {
@@ -977,23 +1064,23 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
   }
   if (tid < 64) {  // group bases: exclusive prefix of the group totals (one wave)
     const uint32_t v = tid < (uint32_t)MSD_GROUPS ? ranges[R_GTOT + tid] : 0u;
-    const uint32_t incl = v3::wave_incl_scan<uint32_t>(v);
+    const uint32_t incl = tile::wave_incl_scan<uint32_t>(v);
     if (tid < (uint32_t)MSD_GROUPS) s_gpre[tid] = incl - v;
   }
   if (local_cache)
     for (int b = tid; b < HOT_BUCKETS; b += NT) s_rstar[b] = 0xFFFFFFFFu;
   __syncthreads();
   // A batch the engine will rerun on the LSD pipeline poisons the next batch's k4_scan.
-  if (t == 0 && tid == 0 && (s_err & ERR_V2_FALLBACK) && !(s_err & (ERR_BAD_INPUT | ERR_BAD_TIME))) *poison = 1u;
+  if (t == 0 && tid == 0 && (s_err & ERR_FALLBACK) && !(s_err & (ERR_BAD_INPUT | ERR_BAD_TIME))) *poison = 1u;
   // Nothing is decided and nothing touches the table unless the whole batch is valid.
   if (s_err) return;
   // Hot keys without a freeze in this batch: the final counter is base + total (block 0).
   if (t == 0) {
     for (int b = tid; b < HOT_BUCKETS; b += NT) {
-      const HotBucket3 x = hb[b];
+      const HotBucket x = hb[b];
       if (!x.slot || (x.flags & HB_FROZEN_PRE)) continue;
       if (!local_cache || x.base + x.total <= (uint64_t)rules[x.rule].L)
-        reinterpret_cast<Slot*>(x.slot)->count = x.base + x.total;
+        *hot_counter(x) = (uint32_t)(x.base + x.total);
     }
   }
   const uint32_t nhot = s_row[HOT_BUCKETS], nrec = s_row[NIL_BUCKET];
@@ -1003,7 +1090,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
   // the tile's run in order)
   for (uint32_t p = nhot + tid; p < nrec; p += NT) {
     const MRec m = src[p];
-    const uint32_t mb = v3::msd_bucket(m.key);
+    const uint32_t mb = tile::msd_bucket(m.key);
     const uint32_t pos = s_gpre[mb >> 6] + ranges[R_BPRE + mb] + s_toff[mb] + (p - s_row[HOT_BUCKETS + mb]);
     mrec[pos] = m;
   }
@@ -1015,7 +1102,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
     for (uint32_t p = tid; p < nhot; p += NT) {
       const MRec a = src[p];
       const uint32_t b = (uint32_t)a.fp_lo;
-      const HotBucket3& x = hb[b];
+      const HotBucket& x = hb[b];
       if (x.flags & HB_FROZEN_PRE) continue;
       const uint64_t P = hrow[b] + a.key;
       const uint64_t after = x.base + P;
@@ -1023,7 +1110,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
       if (after > L && (after - a.h <= L || P == a.h)) {
         s_rstar[b] = a.req;
         hb[b].rstar = a.req;
-        reinterpret_cast<Slot*>(x.slot)->flags = SLOT_FROZEN;
+        hb[b].t_rstar = x.ws + (a.rn >> V4_RULE_BITS);  // the freecache Set's time (k4_group finalises)
       }
     }
     __syncthreads();
@@ -1032,31 +1119,31 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
   for (uint32_t p = tid; p < nhot; p += NT) {
     const MRec a = src[p];
     const uint32_t b = (uint32_t)a.fp_lo;
-    const uint32_t rule = rule_of(a.rn), now_mod = a.rn >> V3_RULE_BITS;
+    const uint32_t rule = rule_of(a.rn), now_mod = a.rn >> V4_RULE_BITS;
     const uint32_t i = a.idx;
     const unsigned long long P = hrow[b] + a.key;
-    const HotBucket3& hx = hb[b];
+    const HotBucket& hx = hb[b];
     const DevRule& rl = rules[rule];
     if (hx.flags & HB_FROZEN_PRE) {
-      out[i] = v3::local_hit_status(a.h, rl.div - now_mod);  // every descriptor is a local-cache hit
+      out[i] = tile::local_hit_status(a.h, rl.div - now_mod);  // every descriptor is a local-cache hit
       continue;
     }
     const uint64_t after = hx.base + P;
     if (!local_cache || after <= rl.L) {
-      v3::decide_at(i, a.req, rule, a.h, now_mod, hx.base, P, SEG_NO_FREEZE, rules, out, req_thr, routed);
+      tile::decide_at(i, a.req, rule, a.h, now_mod, hx.base, P, SEG_NO_FREEZE, rules, out, req_thr, routed);
+      if (P == hx.total) hb[b].t_all = hx.ws + now_mod;  // the key's last INCRBY (EXPIRE time)
       continue;
     }
     const uint32_t rs = s_rstar[b];
-    Slot* slot = reinterpret_cast<Slot*>(hx.slot);
     if (rs != 0xFFFFFFFFu) {  // the freezing descriptor is in this tile, at or before this one
       if (a.req > rs) {
-        out[i] = v3::local_hit_status(a.h, rl.div - now_mod);
+        out[i] = tile::local_hit_status(a.h, rl.div - now_mod);
       } else {  // same request as the freezing descriptor: its INCRBY still happens
-        v3::decide_at(i, a.req, rule, a.h, now_mod, hx.base, P, SEG_NO_FREEZE, rules, out, req_thr, routed);
-        atomicMax((unsigned long long*)&slot->count, (unsigned long long)after);
+        tile::decide_at(i, a.req, rule, a.h, now_mod, hx.base, P, SEG_NO_FREEZE, rules, out, req_thr, routed);
+        atomicMax(hot_counter(hx), (uint32_t)after);
       }
     } else if (a.req > q0) {  // froze in an earlier tile, in a request <= q0
-      out[i] = v3::local_hit_status(a.h, rl.div - now_mod);
+      out[i] = tile::local_hit_status(a.h, rl.div - now_mod);
     } else {  // a request that began in an earlier tile: decided by k4_group
       const uint32_t e = atomicAdd(&ctl->tile_ctr[DFR_CTR][0], 1u);
       Deferred df;
@@ -1089,14 +1176,16 @@ struct GScratch4 {
 };
 
 __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __restrict__ mrec,
-                                                 const DevRule* __restrict__ rules, TableDesc tab, int local_cache,
+                                                 const DevRule* __restrict__ rules, TableDesc tab,
                                                  rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
-                                                 const HotBucket3* __restrict__ hb, const Deferred* __restrict__ dfr,
+                                                 const HotBucket* __restrict__ hb, const Deferred* __restrict__ dfr,
                                                  HotCand* __restrict__ cand, int cand_on, uint64_t seed,
                                                  GScratch4 gs, uint32_t* __restrict__ wg_heads,
-                                                 const uint32_t* __restrict__ scan_heads, uint32_t n_scan_heads,
-                                                 const uint32_t* __restrict__ ranges, int routed, EngineCtl* ctl,
-                                                 EngineCtl* next_ctl) {
+                                                 uint32_t* __restrict__ wg_ins,
+                                                 const uint32_t* __restrict__ scan_heads,
+                                                 const uint32_t* __restrict__ scan_ins, uint32_t n_scan_heads,
+                                                 const uint32_t* __restrict__ ranges, int routed,
+                                                 RegionOcc* __restrict__ occ, EngineCtl* ctl, EngineCtl* next_ctl) {
   __shared__ MRec s_rec[G_CAP];
   __shared__ uint64_t s_P[G_CAP];
   __shared__ uint16_t s_list[G_CAP];
@@ -1109,13 +1198,15 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
   __shared__ uint32_t s_cursor, s_heads, s_last, s_err;
   __shared__ uint32_t s_rn[MSD_GROUPS + 1], s_gpre[MSD_GROUPS + 1];
   __shared__ uint32_t sh_w[G_W];
+  __shared__ uint32_t s_ins[8];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t j = blockIdx.x;
   uint32_t heads = 0;
+  if (tid < 8) s_ins[tid] = 0;
   if (tid < 64) {  // ranges per group and record bases of the groups: prefixes (one wave)
     const uint32_t v = tid < (uint32_t)MSD_GROUPS ? ranges[tid] : 0u;
     const uint32_t w = tid < (uint32_t)MSD_GROUPS ? ranges[R_GTOT + tid] : 0u;
-    const uint32_t iv = v3::wave_incl_scan<uint32_t>(v), iw = v3::wave_incl_scan<uint32_t>(w);
+    const uint32_t iv = tile::wave_incl_scan<uint32_t>(v), iw = tile::wave_incl_scan<uint32_t>(w);
     if (tid <= (uint32_t)MSD_GROUPS) {
       s_rn[tid] = iv - v;
       s_gpre[tid] = iw - w;
@@ -1133,13 +1224,13 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
     const uint32_t nd = ctl->tile_ctr[DFR_CTR][0];
     for (uint32_t e = j * G_NT + tid; e < nd; e += gridDim.x * G_NT) {
       const Deferred df = dfr[e];
-      const HotBucket3& x = hb[df.bucket];
+      const HotBucket& x = hb[df.bucket];
       if (df.req > x.rstar) {
-        out[df.idx] = v3::local_hit_status(df.h, rules[df.rule].div - df.now_mod);
+        out[df.idx] = tile::local_hit_status(df.h, rules[df.rule].div - df.now_mod);
       } else {
-        v3::decide_at(df.idx, df.req, df.rule, df.h, df.now_mod, x.base, df.P, SEG_NO_FREEZE, rules, out, req_thr,
+        tile::decide_at(df.idx, df.req, df.rule, df.h, df.now_mod, x.base, df.P, SEG_NO_FREEZE, rules, out, req_thr,
                       routed);
-        atomicMax((unsigned long long*)&reinterpret_cast<Slot*>(x.slot)->count, (unsigned long long)(x.base + df.P));
+        atomicMax(hot_counter(x), (uint32_t)(x.base + df.P));
       }
     }
     const uint32_t nr = s_rn[MSD_GROUPS];
@@ -1174,8 +1265,8 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
         ST4(2);
         const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
         {
-          const uint32_t hh = group_range<true>(gl, m, rules, tab, local_cache, out, req_thr, cand, cand_on, routed,
-                                                s_agg, &s_carry, sh_w, ctl);
+          const uint32_t hh = group_range<true>(gl, m, rules, tab, out, req_thr, cand, cand_on, routed, s_agg,
+                                                &s_carry, sh_w, s_ins, ctl);
           heads += hh;
           ST4X(0, m);
           ST4X(1, hh & 0xFFFFu);
@@ -1196,7 +1287,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
       uint32_t n0 = 0;
       for (int u = 0; u < SU; ++u) n0 += half_of(tid + u * G_NT) == 0u;
       uint32_t tot0;
-      v3::block_excl_scan<G_NT>(n0, sh_w, tot0);
+      tile::block_excl_scan<G_NT>(n0, sh_w, tot0);
       if (tot0 <= (uint32_t)G_CAP && m - tot0 <= (uint32_t)G_CAP) {
         // a split range takes its own half (the other half is another block's range)
         for (uint32_t part = split_half == 1 ? 1u : 0u; part < (split_half == 0 ? 1u : 2u); ++part) {
@@ -1212,7 +1303,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
             const uint32_t k = tid + u * G_NT;
             const bool mine = half_of(k) == part;
             uint32_t ct;
-            const uint32_t pos = mp + v3::block_excl_scan<G_NT>(mine ? 1u : 0u, sh_w, ct);
+            const uint32_t pos = mp + tile::block_excl_scan<G_NT>(mine ? 1u : 0u, sh_w, ct);
             if (mine) s_rec[pos] = src[k];
             mp += ct;
           }
@@ -1220,8 +1311,8 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
           __syncthreads();
           if (mp == 0) continue;
           const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
-          heads += group_range<true>(gl, mp, rules, tab, local_cache, out, req_thr, cand, cand_on, routed, s_agg,
-                                     &s_carry, sh_w, ctl);
+          heads += group_range<true>(gl, mp, rules, tab, out, req_thr, cand, cand_on, routed, s_agg, &s_carry,
+                                     sh_w, s_ins, ctl);
         }
       } else if (split_half != 1) {
         // grouped in place in bucket order (global scratch); for a split bucket by its half-0
@@ -1238,12 +1329,12 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
         if (tid == 0) *gg.cursor = 0;
         __threadfence_block();
         __syncthreads();
-        heads += group_range<false>(gg, m, rules, tab, local_cache, out, req_thr, cand, cand_on, routed, s_agg,
-                                    &s_carry, sh_w, ctl);
+        heads += group_range<false>(gg, m, rules, tab, out, req_thr, cand, cand_on, routed, s_agg, &s_carry,
+                                    sh_w, s_ins, ctl);
       }
     }
   }
-  heads = v3::wave_sum(heads);
+  heads = tile::wave_sum(heads);
   __syncthreads();
   if (lane == 0 && heads) atomicAdd(&s_heads, heads);
   __syncthreads();
@@ -1253,6 +1344,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
   // them), then one lane adds to the block's shard counter (blockIdx & 7); the last block of a
   // shard adds to the global counter; the last of those is the last block.
   if (tid == 0) st_relaxed(&wg_heads[j], s_heads);
+  if (tid < 8) st_relaxed(&wg_ins[j * 8 + tid], s_ins[tid]);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -1267,28 +1359,49 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
   }
   __syncthreads();
   if (!s_last) return;
-  // U = Σ per-block unique-key counts (this kernel and k4_scan's hot leaders)
+  // U = Σ per-block unique-key counts (this kernel and k4_scan's hot leaders); new slots per
+  // region into the occupancy counts (only for a batch that was applied)
   if (tid == 0) s_heads = 0;
-  if (tid == 1) s_cursor = 0;
+  if (tid < 8) s_ins[tid] = 0;
   __syncthreads();
   {
-    uint32_t u = 0, ins = 0;
-    for (uint32_t k = tid; k < gridDim.x + n_scan_heads; k += G_NT) {
-      const uint32_t v = k < gridDim.x ? ld_relaxed(&wg_heads[k]) : scan_heads[k - gridDim.x];
-      u += v & 0xFFFFu;
-      ins += v >> 16;
-    }
-    u = v3::wave_sum(u);
-    ins = v3::wave_sum(ins);
-    if (lane == 0) {
-      if (u) atomicAdd(&s_heads, u);
-      if (ins) atomicAdd(&s_cursor, ins);
-    }
+    uint32_t u = 0;
+    for (uint32_t k = tid; k < gridDim.x + n_scan_heads; k += G_NT)
+      u += (k < gridDim.x ? ld_relaxed(&wg_heads[k]) : scan_heads[k - gridDim.x]) & 0xFFFFu;
+    u = tile::wave_sum(u);
+    if (lane == 0 && u) atomicAdd(&s_heads, u);
+    // thread (block group, region): 32 groups x 8 regions
+    const uint32_t rg = tid & 7u;
+    uint32_t ins = 0;
+    for (uint32_t k = tid >> 3; k < gridDim.x + n_scan_heads; k += G_NT / 8)
+      ins += k < gridDim.x ? ld_relaxed(&wg_ins[k * 8 + rg]) : scan_ins[(k - gridDim.x) * 8 + rg];
+    if (ins) atomicAdd(&s_ins[rg], ins);
   }
   __syncthreads();
   if (tid == 0) {
     ctl->n_segments = s_heads;
-    ctl->tile_ctr[INS_CTR0][0] += s_cursor;  // new table slots (engine stats)
+    uint32_t n = 0;
+    for (int r = 0; r < 8; ++r) {
+      ctl->ins[r] = s_ins[r];
+      n += s_ins[r];
+    }
+    ctl->n_inserted = n;
+    // also for a refused batch: its hot keys may have claimed slots in k4_scan before the
+    // refusal (they hold the empty state; the rerun finds them)
+    occ_update(occ, ctl->gen_max, s_ins);
+  }
+  // Hot keys: EXPIRE and freecache TTLs from the time of the last INCRBY / the freezing
+  // request (fixed_cache_impl.go:69-72, base_limiter.go:102)
+  if (s_err == 0) {
+    for (uint32_t b = tid; b < (uint32_t)HOT_BUCKETS; b += G_NT) {
+      const HotBucket x = hb[b];
+      if (!x.slot || (x.flags & HB_FROZEN_PRE)) continue;
+      Slot* sl = reinterpret_cast<Slot*>(x.slot);
+      const uint32_t div = rules[x.rule].div;
+      const bool frozen = x.rstar != 0xFFFFFFFFu;
+      if (!(x.flags & HB_PS)) sl->exp = (frozen ? x.t_rstar : x.t_all) + div;
+      if (frozen) sl->frz = x.t_rstar + div;
+    }
   }
   // hot-set candidates found by leaders: their key-prefix state
   const uint32_t nc = min((uint32_t)CAND_MAX, ld_relaxed(&ctl->tile_ctr[CAND_CTR][0]));
@@ -1303,7 +1416,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
       c.b = in.recs[d].b;
     } else {
       const uint32_t o0 = in.off[d], o1 = in.off[d + 1];
-      const FpState st = v3::prefix_state(in.blob, o0, o1 - o0, unit, seed);
+      const FpState st = tile::prefix_state(in.blob, o0, o1 - o0, seed);
       c.a = st.a;
       c.b = st.b;
     }
@@ -1320,7 +1433,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-uint32_t v4_tiles(uint32_t n) { return n ? (n + V3_TILE - 1) / V3_TILE : 1; }
+uint32_t v4_tiles(uint32_t n) { return n ? (n + V4_TILE - 1) / V4_TILE : 1; }
 uint32_t v4_group_blocks(uint32_t) { return v4::GBLOCKS; }
 uint32_t v4_scan_blocks() { return v4::HOT_SCAN_BLOCKS + v4::MSD_SCAN_BLOCKS; }
 size_t v4_scratch_bytes() {
@@ -1338,31 +1451,32 @@ void launch_v4_hist(hipStream_t st, const rl_batch& b, const DevRule* rules, uin
                     unsigned long long* thsum, MRec* srec, rl_status* out, EngineCtl* ctl) {
   const DevBatch in = make_dev_batch(b);
   if (in.recs)
-    hipLaunchKernelGGL(v4::k4_hist<true>, dim3(v4_tiles(b.n_desc)), dim3(V3_THREADS), 0, st, in, rules, n_rules, seed,
+    hipLaunchKernelGGL(v4::k4_hist<true>, dim3(v4_tiles(b.n_desc)), dim3(V4_THREADS), 0, st, in, rules, n_rules, seed,
                        hot, req_thr, fpart, tstart, thsum, srec, out, ctl);
   else
-    hipLaunchKernelGGL(v4::k4_hist<false>, dim3(v4_tiles(b.n_desc)), dim3(V3_THREADS), 0, st, in, rules, n_rules,
+    hipLaunchKernelGGL(v4::k4_hist<false>, dim3(v4_tiles(b.n_desc)), dim3(V4_THREADS), 0, st, in, rules, n_rules,
                        seed, hot, req_thr, fpart, tstart, thsum, srec, out, ctl);
 }
 void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const unsigned long long* thsum,
-                    unsigned long long* hoff, const uint32_t* fpart, const HotEntry* hot_list, HotBucket3* hb,
-                    const TableDesc& tab, int local_cache, HotCand* cand, uint32_t* heads_out, uint16_t* toff,
-                    void* scratch, const uint32_t* poison, EngineCtl* ctl) {
+                    unsigned long long* hoff, const uint32_t* fpart, const HotEntry* hot_list, HotBucket* hb,
+                    const TableDesc& tab, HotCand* cand, uint32_t* heads_out, uint32_t* ins_out, uint16_t* toff,
+                    void* scratch, const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl) {
   hipLaunchKernelGGL(v4::k4_scan, dim3(v4_scan_blocks()), dim3(v4::SCAN_NT), 0, st, tstart, thsum, v4_tiles(n), hoff,
-                     fpart, hot_list, hb, tab, local_cache, cand, heads_out, toff, v4_ranges(scratch), poison, ctl);
+                     fpart, hot_list, hb, tab, cand, heads_out, ins_out, toff, v4_ranges(scratch), poison, occ, ctl);
 }
 void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart, const uint16_t* toff,
-                     void* scratch, const DevRule* rules, const unsigned long long* hoff, HotBucket3* hb,
+                     void* scratch, const DevRule* rules, const unsigned long long* hoff, HotBucket* hb,
                      int local_cache, MRec* mrec, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
                      uint32_t* poison, EngineCtl* ctl) {
-  hipLaunchKernelGGL(v4::k4_place, dim3(v4_tiles(b.n_desc)), dim3(V3_THREADS), 0, st, make_dev_batch(b), srec, tstart,
+  hipLaunchKernelGGL(v4::k4_place, dim3(v4_tiles(b.n_desc)), dim3(V4_THREADS), 0, st, make_dev_batch(b), srec, tstart,
                      toff, v4_ranges(scratch), rules, hoff, hb, local_cache, mrec, out, req_thr, dfr, routed, poison,
                      ctl);
 }
 void launch_v4_group(hipStream_t st, const rl_batch& b, MRec* mrec, const DevRule* rules, const TableDesc& tab,
-                     int local_cache, rl_status* out, uint32_t* req_thr, const HotBucket3* hb, const Deferred* dfr,
-                     HotCand* cand, int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads,
-                     const uint32_t* scan_heads, int routed, EngineCtl* ctl, EngineCtl* next_ctl) {
+                     rl_status* out, uint32_t* req_thr, const HotBucket* hb, const Deferred* dfr, HotCand* cand,
+                     int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads, uint32_t* wg_ins,
+                     const uint32_t* scan_heads, const uint32_t* scan_ins, int routed, RegionOcc* occ, EngineCtl* ctl,
+                     EngineCtl* next_ctl) {
   using namespace v4;
   uint8_t* p = reinterpret_cast<uint8_t*>(scratch);
   GScratch4 gs;
@@ -1379,9 +1493,9 @@ void launch_v4_group(hipStream_t st, const rl_batch& b, MRec* mrec, const DevRul
   gs.grp = reinterpret_cast<uint16_t*>(p);
   p += (size_t)GBLOCKS * BUCKET_CAP * 2;
   gs.end = reinterpret_cast<uint16_t*>(p);
-  hipLaunchKernelGGL(k4_group, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), mrec, rules, tab, local_cache, out,
-                     req_thr, hb, dfr, cand, cand_on, seed, gs, wg_heads, scan_heads, v4_scan_blocks(),
-                     v4_ranges(scratch), routed, ctl, next_ctl);
+  hipLaunchKernelGGL(k4_group, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), mrec, rules, tab, out, req_thr, hb,
+                     dfr, cand, cand_on, seed, gs, wg_heads, wg_ins, scan_heads, scan_ins, (uint32_t)HOT_SCAN_BLOCKS,
+                     v4_ranges(scratch), routed, occ, ctl, next_ctl);
 }
 
 }  // namespace rlhip

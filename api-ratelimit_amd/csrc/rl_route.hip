@@ -35,17 +35,18 @@ __global__ __launch_bounds__(NT) void k_route_hash(DevBatch in, const DevRule* _
   if (i < in.n_desc) {
     const uint32_t rule = in.rule[i], q = in.req_of[i];
     uint32_t err = 0, o = ROUTE_LOCAL;
-    if (rule != RL_NIL_RULE) {
+    const uint32_t o0 = in.off[i], o1 = in.off[i + 1];
+    if (o1 < o0 || o1 > in.blob_bytes || (i > 0 && in.req_of[i - 1] > q)) err |= ERR_BAD_INPUT;
+    if (rule != RL_NIL_RULE && !err) {
       if (rule >= n_rules || q >= in.n_req) {
         err |= ERR_BAD_INPUT;
       } else {
         const int64_t now = in.now[q];
-        if (now < 0 || now > 0xFFFFFFF0ll) {
+        if (now < 0 || now > MAX_NOW) {
           err |= ERR_BAD_TIME;
         } else {
-          const uint32_t unit = rules[rule].unit;
-          const uint32_t o0 = in.off[i], len = in.off[i + 1] - o0;
-          FpState s = fp_init(len, unit, seed);
+          const uint32_t len = o1 - o0;
+          FpState s = fp_init(len, seed);
           if (len) hash_prefix(in.blob, o0, len, s);
           const uint32_t ha = in.hits[q];
           RRec r;

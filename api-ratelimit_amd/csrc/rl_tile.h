@@ -1,7 +1,6 @@
-// rl_v3_dev.h — device helpers of the bucketed decision pipelines (v3 and v4):
-// descriptor loading + fingerprint, hot-set lookup, LDS tile sort, segmented scan element,
-// decisions of hot / local-cache-hit descriptors. Included by rl_kernels_v3.hip and
-// rl_kernels_v4.hip only.
+// rl_tile.h — device helpers of the bucketed (v4) decision pipeline: descriptor loading +
+// fingerprint, hot-set lookup, LDS tile sort, segmented scan element, decisions of hot /
+// local-cache-hit descriptors. Included by rl_kernels_v4.hip only.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -11,10 +10,10 @@
 #include "rl_device.h"
 
 namespace rlhip {
-namespace v3 {
+namespace tile {
 
-constexpr int T = V3_TILE;
-constexpr int NT = V3_THREADS;
+constexpr int T = V4_TILE;
+constexpr int NT = V4_THREADS;
 constexpr int R = T / NT;      // descriptors per thread
 constexpr int W = NT / 64;     // waves per tile block
 constexpr int PRE_DW = 8;      // blob dwords preloaded per descriptor (prefixes up to 24 B hash inline)
@@ -26,14 +25,15 @@ static_assert(T <= 65536, "u16 tile offsets");
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
 
 RL_DEV uint32_t msd_bucket(uint64_t key) { return (uint32_t)((key << 3) >> (64 - MSD_BITS)); }
-RL_DEV uint32_t rule_of(uint32_t rn) { return rn & (V3_MAX_RULES - 1u); }
+RL_DEV uint32_t rule_of(uint32_t rn) { return rn & (V4_MAX_RULES - 1u); }
 
-RL_DEV uint32_t hot_lookup(const HotEntry* sh_hot, uint64_t a, uint64_t b, uint32_t unit, uint32_t& rule) {
+// Hot entry of a key prefix (any unit: one prefix, one hot bucket pair), or ~0.
+RL_DEV uint32_t hot_lookup(const HotEntry* sh_hot, uint64_t a, uint64_t b, uint32_t& rule) {
   uint32_t s = (uint32_t)(a >> 40) & (HOT_SLOTS - 1);
   for (int probe = 0; probe < HOT_SLOTS; ++probe) {
     const HotEntry& e = sh_hot[s];
     if (e.idx == 0xFFFFFFFFu) return 0xFFFFFFFFu;
-    if (e.a == a && e.b == b && e.unit == unit) {
+    if (e.a == a && e.b == b) {
       rule = e.rule;
       return e.idx;
     }
@@ -87,6 +87,8 @@ RL_DEV uint32_t block_excl_scan(uint32_t v, uint32_t* sh_w, uint32_t& total) {
 struct D3 {
   uint64_t key, lo;
   uint32_t req, rule, h, now_mod, bucket, gen;
+  uint32_t uw;   // unit window slot (unit - 1) * 2 + parity, 8 = none
+  uint32_t uwv;  // unit window index + 1
 };
 
 // Words of a prefix beyond the preloaded dwords. p[0] = d0 is the dword holding the first
@@ -106,8 +108,8 @@ RL_DEV void hash_tail(const uint32_t* p, uint32_t d0, uint32_t sh, uint32_t rem,
 }
 
 // Prefix state (lanes a, b) of a byte string, reading only dwords that overlap it.
-RL_DEV FpState prefix_state(const uint8_t* blob, uint32_t off, uint32_t len, uint32_t unit, uint64_t seed) {
-  FpState s = fp_init(len, unit, seed);
+RL_DEV FpState prefix_state(const uint8_t* blob, uint32_t off, uint32_t len, uint64_t seed) {
+  FpState s = fp_init(len, seed);
   if (len) {
     const uint32_t* p = reinterpret_cast<const uint32_t*>(blob + (off & ~3u));
     hash_tail(p, p[0], off & 3u, len, s);
@@ -115,22 +117,28 @@ RL_DEV FpState prefix_state(const uint8_t* blob, uint32_t off, uint32_t len, uin
   return s;
 }
 
-// Window, sort key, gen and bucket of one valid descriptor from its prefix state.
+// Window, sort key, table place and bucket of one valid descriptor from its prefix state.
+// The key is the Redis key string (prefix, window start): its region and generation come
+// from the string's home unit, not the descriptor's (rl_common.h place_of).
 RL_DEV void key_of(D3& x, const FpState& s, int64_t now, const DevRule& rr, const HotEntry* sh_hot, uint32_t& err) {
   const uint32_t unit = rr.unit;
   const int64_t widx = div_const(now, unit);
-  const int64_t ws = widx * (int64_t)rr.div;  // (now/divider)*divider  cache_key.go:66-68
+  const uint32_t ws = (uint32_t)(widx * (int64_t)rr.div);  // (now/divider)*divider  cache_key.go:66-68
   uint32_t hot_rule = 0;
-  const uint32_t hidx = hot_lookup(sh_hot, s.a, s.b, unit, hot_rule);
+  const uint32_t hidx = hot_lookup(sh_hot, s.a, s.b, hot_rule);
   uint64_t hi, lo;
   fp_final(s, (uint64_t)ws, hi, lo);
-  const uint32_t region = (unit - 1u) * 2u + (uint32_t)(widx & 1);
-  x.key = make_sort_key(region, hi);
+  const Place pl = place_of(ws);
+  x.key = make_sort_key(pl.region, hi);
   x.lo = lo;
-  x.gen = (uint32_t)widx + 1u;
-  x.now_mod = (uint32_t)(now - ws);
+  x.gen = pl.gen;
+  x.now_mod = (uint32_t)(now - (int64_t)ws);
+  x.uw = (unit - 1u) * 2u + (uint32_t)(widx & 1);
+  x.uwv = (uint32_t)widx + 1u;
   if (hidx != 0xFFFFFFFFu) {
-    if (hot_rule != x.rule) err |= ERR_V2_FALLBACK;  // a hot bucket must hold one key under one rule
+    // a hot prefix takes every descriptor of the prefix under one rule, so a key string
+    // never splits between a hot bucket and an MSD bucket
+    if (hot_rule != x.rule) err |= ERR_FALLBACK;
     x.bucket = hidx * 2u + (uint32_t)(widx & 1);
   } else {
     x.bucket = HOT_BUCKETS + msd_bucket(x.key);
@@ -141,16 +149,22 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
                        const HotEntry* sh_hot, uint32_t t0, D3 (&d)[R], uint32_t& err) {
   const uint32_t tid = threadIdx.x;
   uint32_t rl[R], q[R], o0[R], len[R];
+  bool lay[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint32_t i = t0 + r * NT + tid;
     const bool v = i < in.n_desc;
     rl[r] = v ? in.rule[i] : RL_NIL_RULE;
     q[r] = v ? in.req_of[i] : 0u;
+    const uint32_t qp = (v && i > 0) ? in.req_of[i - 1] : 0u;
     const uint32_t a = v ? in.off[i] : 0u;
     const uint32_t b = v ? in.off[i + 1] : 0u;
+    // batch layout checks (the device validates every submit form): prefix offsets in order
+    // and inside the blob, request indices non-decreasing
+    lay[r] = a <= b && b <= in.blob_bytes && qp <= q[r];
+    if (v && !lay[r]) err |= ERR_BAD_INPUT;
     o0[r] = a;
-    len[r] = b - a;
+    len[r] = lay[r] ? b - a : 0u;
   }
   const uint32_t lim = (in.blob_bytes + 3u) & ~3u;
   int64_t now[R];
@@ -163,15 +177,10 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
     const uint32_t i = t0 + r * NT + tid;
     const bool v = i < in.n_desc;
     const bool q_ok = q[r] < in.n_req;
-    ok[r] = v && rl[r] != RL_NIL_RULE && rl[r] < n_rules && q_ok;
-    if (v && rl[r] != RL_NIL_RULE && !ok[r]) err |= ERR_BAD_INPUT;
-#ifdef RL_V_NOL2  // timing experiment only: no per-request loads
-    now[r] = in.now[0];
-    ha[r] = 1u;
-#else
+    ok[r] = v && rl[r] != RL_NIL_RULE && rl[r] < n_rules && q_ok && lay[r];
+    if (v && rl[r] != RL_NIL_RULE && (rl[r] >= n_rules || !q_ok)) err |= ERR_BAD_INPUT;
     now[r] = (v && q_ok) ? in.now[q[r]] : 0;
     ha[r] = (v && q_ok) ? in.hits[q[r]] : 1u;
-#endif
     if (ok[r]) {
       rr[r] = rules[rl[r]];
     } else {
@@ -180,11 +189,7 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
       rr[r].unit = RL_UNIT_SECOND;
     }
     const uint32_t a = o0[r] & ~3u;
-#ifdef RL_V_NOBLOB  // timing experiment only: no prefix bytes
-    const uint32_t need = 0;
-#else
     const uint32_t need = ok[r] ? (((o0[r] & 3u) + len[r] + 3u) & ~3u) : 0u;  // bytes from a
-#endif
 #pragma unroll
     for (int c = 0; c < PRE_DW / 4; ++c) {
       const uint32_t cb = a + 16u * c;
@@ -211,17 +216,18 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
     x.h = ha[r] > 1u ? ha[r] : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
     x.now_mod = 0;
     x.gen = 0;
+    x.uw = 8;
+    x.uwv = 0;
     x.key = NIL_KEY;
     x.lo = 0;
     x.bucket = i < in.n_desc ? NIL_BUCKET : BKT_NONE;
     if (!ok[r]) continue;
-    if (now[r] < 0 || now[r] > 0xFFFFFFF0ll) {
+    if (now[r] < 0 || now[r] > MAX_NOW) {
       err |= ERR_BAD_TIME;
       continue;
     }
-    const uint32_t unit = rr[r].unit;
     const uint32_t sh = o0[r] & 3u;
-    FpState s = fp_init(len[r], unit, seed);
+    FpState s = fp_init(len[r], seed);
     uint32_t rem = len[r];
 #pragma unroll
     for (int k = 0; k < (PRE_DW - 1) / 2; ++k) {
@@ -274,6 +280,8 @@ RL_DEV void load_routed(const DevBatch& in, const DevRule* __restrict__ rules, u
     x.h = rc[r].h > 1u ? rc[r].h : 1u;
     x.now_mod = 0;
     x.gen = 0;
+    x.uw = 8;
+    x.uwv = 0;
     x.key = NIL_KEY;
     x.lo = 0;
     x.bucket = i < in.n_desc ? NIL_BUCKET : BKT_NONE;
@@ -281,7 +289,7 @@ RL_DEV void load_routed(const DevBatch& in, const DevRule* __restrict__ rules, u
       if (i < in.n_desc && rc[r].rule != RL_NIL_RULE) err |= ERR_BAD_INPUT;
       continue;
     }
-    if (rc[r].now > 0xFFFFFFF0u) {
+    if ((int64_t)rc[r].now > MAX_NOW) {
       err |= ERR_BAD_TIME;
       continue;
     }
@@ -377,5 +385,5 @@ RL_DEV void decide_at(uint32_t idx, uint32_t req, uint32_t rule, uint32_t h, uin
   decide_one(o, si, rules[rule], out, req_thr, routed ? idx : req);
 }
 
-}  // namespace v3
+}  // namespace tile
 }  // namespace rlhip

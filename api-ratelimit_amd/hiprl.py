@@ -37,14 +37,16 @@ STATUS_DTYPE = np.dtype([("code_flags", "<u4"), ("limit_remaining", "<u4"), ("re
                          ("over_limit_delta", "<u4"), ("near_limit_delta", "<u4")])
 
 
-PIPELINE_FLAGS = {"v4": 0, "lsd": 1, "v2": 2, "v3": 4}  # rl_config.flags (RL_CFG_LSD_ONLY, RL_CFG_V2, RL_CFG_V3)
+PIPELINE_FLAGS = {"v4": 0, "lsd": 1}  # rl_config.flags (RL_CFG_LSD_ONLY)
+ABI_VERSION = 2
 
 
 class RlConfig(C.Structure):
     _fields_ = [("struct_size", C.c_uint32), ("device", C.c_int32), ("log2_slots", C.c_uint32 * 4),
                 ("near_limit_ratio", C.c_float), ("local_cache", C.c_uint32), ("per_second_split", C.c_uint32),
                 ("max_batch_desc", C.c_uint32), ("max_batch_req", C.c_uint32), ("max_blob_bytes", C.c_uint32),
-                ("sort_bits", C.c_uint32), ("flags", C.c_uint32), ("hash_seed", C.c_uint64)]
+                ("sort_bits", C.c_uint32), ("flags", C.c_uint32), ("hash_seed", C.c_uint64),
+                ("max_load_permille", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class RlRule(C.Structure):
@@ -73,7 +75,18 @@ MAX_IN_FLIGHT = 3  # RL_MAX_IN_FLIGHT: batches in flight at once through rl_subm
 
 class RlEngineStats(C.Structure):
     _fields_ = [("batches", C.c_uint64), ("descriptors", C.c_uint64), ("resorts", C.c_uint64),
-                ("live_slots_hint", C.c_uint64), ("lsd_fallbacks", C.c_uint64), ("hot_keys", C.c_uint64)]
+                ("inserted_keys", C.c_uint64), ("lsd_fallbacks", C.c_uint64), ("hot_keys", C.c_uint64),
+                ("live_keys", C.c_uint64), ("host_batches", C.c_uint64)]
+
+
+class RlOccupancy(C.Structure):
+    _fields_ = [("gen", C.c_uint32 * 8), ("live", C.c_uint32 * 8), ("limit", C.c_uint32 * 8), ("slots", C.c_uint32 * 8)]
+
+
+class RlHostBatch(C.Structure):
+    _fields_ = [("prefix_blob", C.c_void_p), ("prefix_off", C.c_void_p), ("rule_id", C.c_void_p),
+                ("req_of", C.c_void_p), ("now", C.c_void_p), ("hits_addend", C.c_void_p),
+                ("max_desc", C.c_uint32), ("max_req", C.c_uint32), ("max_blob", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 # (name, argtypes, restype) of every symbol include/rl_hip.h declares
@@ -83,13 +96,16 @@ ABI = [
     ("rl_last_error", [C.c_void_p], C.c_char_p),
     ("rl_abi_version", [], C.c_uint32),
     ("rl_load_rules", [C.c_void_p, C.POINTER(RlRule), C.c_uint32], C.c_int),
+    ("rl_host_acquire", [C.c_void_p, C.POINTER(RlHostBatch)], C.c_int),
     ("rl_submit", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
     ("rl_wait", [C.c_void_p], C.c_int),
+    ("rl_wait_into", [C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     ("rl_submit_device", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
     ("rl_submit_pipelined", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
     ("rl_stream", [C.c_void_p], C.c_void_p),
     ("rl_reset", [C.c_void_p], C.c_int),
     ("rl_get_stats", [C.c_void_p, C.POINTER(RlEngineStats)], C.c_int),
+    ("rl_get_occupancy", [C.c_void_p, C.POINTER(RlOccupancy)], C.c_int),
     ("rl_set_timing", [C.c_void_p, C.c_int], C.c_int),
     ("rl_kernel_times", [C.c_void_p, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
                          C.c_uint32, C.POINTER(C.c_uint32)], C.c_int),
@@ -219,11 +235,11 @@ class Engine:
                  local_cache: bool = False, per_second_split: bool = False, max_batch_desc: int = 1 << 16,
                  max_batch_req: Optional[int] = None, max_blob_bytes: Optional[int] = None, sort_bits: int = 48,
                  hash_seed: int = 0x5EE7AB1E5EED, lib_path: Optional[os.PathLike] = None, lsd_only: bool = False,
-                 pipeline: str = "v4"):
+                 pipeline: str = "v4", max_load_permille: int = 0):
         """pipeline: "v4" (default: tile-sorted records, hot keys decided in place, MSD buckets
-        gathered and grouped in LDS), "v3" / "v2" (earlier bucketed pipelines kept for
-        comparison) or "lsd" (radix-sort pipeline, also the fallback of the others).
-        lsd_only=True is pipeline="lsd"."""
+        gathered and grouped in LDS) or "lsd" (radix-sort pipeline, also v4's fallback).
+        lsd_only=True is pipeline="lsd". log2_slots: table slots per window generation for the
+        key strings whose home unit is SECOND/MINUTE/HOUR/DAY."""
         if lsd_only:
             pipeline = "lsd"
         if pipeline not in PIPELINE_FLAGS:
@@ -243,6 +259,7 @@ class Engine:
         cfg.sort_bits = sort_bits
         cfg.flags = PIPELINE_FLAGS[pipeline]
         cfg.hash_seed = hash_seed
+        cfg.max_load_permille = max_load_permille
         self.cfg = cfg
         h = C.c_void_p()
         rc = self.lib.rl_create(C.byref(cfg), C.byref(h))
@@ -275,13 +292,46 @@ class Engine:
         self._check(self.lib.rl_load_rules(self.h, arr, len(rules)), "rl_load_rules")
 
     def submit(self, b: Batch):
-        """Host batch -> (status[n_desc] structured array, throttle_ms[n_req])."""
-        out = np.zeros(b.n_desc, STATUS_DTYPE)
-        thr = np.zeros(b.n_req, np.uint32)
+        """Host batch -> (status[n_desc] structured array, throttle_ms[n_req]); one batch in flight."""
+        self.submit_host_async(b)
+        return self.wait_into(b.n_desc, b.n_req)
+
+    def submit_host_async(self, b: Batch):
+        """rl_submit of a host batch with no output pointers: up to MAX_IN_FLIGHT in flight, the
+        results wait in the engine's pinned memory until wait_into()."""
         s = _batch_struct(b)
-        self._check(self.lib.rl_submit(self.h, C.byref(s), _ptr(out) or None, _ptr(thr) or None), "rl_submit")
-        self._check(self.lib.rl_wait(self.h), "rl_wait")
+        self._check(self.lib.rl_submit(self.h, C.byref(s), None, None), "rl_submit")
+
+    def wait_into(self, n_desc: int, n_req: int):
+        """rl_wait_into: complete the oldest batch, copying its results out."""
+        out = np.zeros(n_desc, STATUS_DTYPE)
+        thr = np.zeros(n_req, np.uint32)
+        self._check(self.lib.rl_wait_into(self.h, _ptr(out) or None, _ptr(thr) or None), "rl_wait_into")
         return out, thr
+
+    def host_acquire(self) -> dict:
+        """rl_host_acquire: numpy views of the next free pinned staging slot (zero-copy submit)."""
+        hb = RlHostBatch()
+        self._check(self.lib.rl_host_acquire(self.h, C.byref(hb)), "rl_host_acquire")
+
+        def view(ptr, n, dt):
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(n,))
+        return dict(blob=view(hb.prefix_blob, hb.max_blob, np.uint8), off=view(hb.prefix_off, hb.max_desc + 1, np.uint32),
+                    rule=view(hb.rule_id, hb.max_desc, np.uint32), req_of=view(hb.req_of, hb.max_desc, np.uint32),
+                    now=view(hb.now, hb.max_req, np.int64), hits=view(hb.hits_addend, hb.max_req, np.uint32))
+
+    def submit_staged(self, n_desc: int, n_req: int, blob_bytes: int, staged: dict):
+        """rl_submit of a batch built in place in an acquired staging slot (no host copy)."""
+        s = RlBatch()
+        s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
+        s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = (
+            staged[k].ctypes.data for k in ("blob", "off", "rule", "req_of", "now", "hits"))
+        self._check(self.lib.rl_submit(self.h, C.byref(s), None, None), "rl_submit")
+
+    def occupancy(self) -> dict:
+        o = RlOccupancy()
+        self._check(self.lib.rl_get_occupancy(self.h, C.byref(o)), "rl_get_occupancy")
+        return {k: list(getattr(o, k)) for k in ("gen", "live", "limit", "slots")}
 
     def submit_device_async(self, n_desc: int, n_req: int, blob_bytes: int, ptrs, out_ptr: int, thr_ptr: int):
         s = RlBatch()

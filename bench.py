@@ -49,8 +49,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--no-kernel-times", action="store_true")
     ap.add_argument("--no-roofline-probe", action="store_true")
-    ap.add_argument("--pipeline", choices=["v4", "v3", "v2", "lsd"], default="v4",
-                    help="decision pipeline (v4 default; v3 / v2 = earlier bucketed pipelines; lsd = radix-sort only)")
+    ap.add_argument("--pipeline", choices=["v4", "lsd"], default="v4",
+                    help="decision pipeline (v4 default; lsd = radix-sort only)")
     ap.add_argument("--independent", action="store_true",
                     help="N>1: unrouted replicas (each rank its own key space) instead of RCCL routing")
     ap.add_argument("--json-out", type=str, default="")

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 1u
+#define RL_ABI_VERSION 2u
 
 /* rule id of a descriptor whose limit is nil ("don't check", src/limiter/cache.go:19-22) */
 #define RL_NIL_RULE 0xFFFFFFFFu
@@ -45,7 +45,8 @@ enum {
   RL_OK = 0,
   RL_EINVAL = -1,    /* bad argument / malformed batch */
   RL_EHIP = -2,      /* HIP runtime error */
-  RL_ENOSPC = -3,    /* a counter-table region is full (raise log2_slots) */
+  RL_ENOSPC = -3,    /* a counter-table region would pass its load limit: the batch was refused before
+                        any counter changed (raise log2_slots / max_load_permille) */
   RL_ECAPACITY = -4, /* batch larger than the engine was created for */
   RL_ESTATE = -5,    /* call out of order (e.g. rl_wait without rl_submit) */
   RL_EDEVICE = -6    /* device-side fault detected (bounded spin expired) */
@@ -57,24 +58,27 @@ typedef struct rl_engine rl_engine;
 typedef struct rl_config {
   uint32_t struct_size;        /* = sizeof(rl_config) */
   int32_t device;              /* HIP device ordinal (HIP_DEVICES) */
-  uint32_t log2_slots[4];      /* per unit SECOND/MINUTE/HOUR/DAY: slots per window generation (HIP_TABLE_SLOTS) */
+  uint32_t log2_slots[4];      /* table slots per window generation of the key strings whose home unit is
+                                  SECOND/MINUTE/HOUR/DAY (HIP_TABLE_SLOTS) */
   float near_limit_ratio;      /* NEAR_LIMIT_RATIO, default 0.8 (settings.go:44) */
   uint32_t local_cache;        /* 1 = local over-limit cache on (LOCAL_CACHE_SIZE_IN_BYTES > 0, settings.go:45) */
-  uint32_t per_second_split;   /* REDIS_PERSECOND (settings.go:35). The HIP table keeps every unit in its own
-                                  key space, i.e. it always behaves like the split configuration. */
+  uint32_t per_second_split;   /* REDIS_PERSECOND (settings.go:35): SECOND keys count in their own store; else
+                                  one store holds every unit and same-string keys share a counter */
   uint32_t max_batch_desc;     /* capacity: descriptors per batch (HIP_BATCH_LIMIT) */
   uint32_t max_batch_req;      /* capacity: requests per batch */
   uint32_t max_blob_bytes;     /* capacity: key-prefix bytes per batch */
   uint32_t sort_bits;          /* LSD pipeline: fingerprint bits radix-sorted per batch (8..64, multiple of 8; 0 = 48) */
   uint32_t flags;              /* RL_CFG_* */
-  uint64_t hash_seed;          /* fingerprint seed (randomise per process against hash flooding) */
+  uint64_t hash_seed;          /* fingerprint seed: one value for every engine of a deployment (multi-GPU
+                                  owners must agree), secret against hash flooding */
+  uint32_t max_load_permille;  /* load limit per table region, 100..950 (0 = 750): a batch that could push a
+                                  region past it is refused with RL_ENOSPC before anything changes */
+  uint32_t reserved;           /* 0 */
 } rl_config;
 
 /* rl_config.flags */
 enum {
-  RL_CFG_LSD_ONLY = 1u,  /* always use the LSD radix-sort pipeline (default: v4 pipeline, LSD as fallback) */
-  RL_CFG_V2 = 2u,        /* use the v2 bucketed pipeline (kept for comparison) */
-  RL_CFG_V3 = 4u         /* use the v3 pipeline (kept for comparison) */
+  RL_CFG_LSD_ONLY = 1u   /* always use the LSD radix-sort pipeline (default: v4 pipeline, LSD as fallback) */
 };
 
 /* One rate-limit rule: config.RateLimit.Limit (src/config/config.go:26-32). */
@@ -117,10 +121,20 @@ typedef struct rl_engine_stats {
   uint64_t batches;           /* batches completed */
   uint64_t descriptors;       /* descriptors decided */
   uint64_t resorts;           /* batches re-sorted on the full fingerprint after a sort-prefix collision */
-  uint64_t live_slots_hint;   /* keys inserted since creation (monotone; not a live count) */
+  uint64_t inserted_keys;     /* table slots claimed since creation (one per key string and window) */
   uint64_t lsd_fallbacks;     /* batches the bucketed pipeline handed to the LSD pipeline */
   uint64_t hot_keys;          /* size of the hot-key set used by the last batch */
+  uint64_t live_keys;         /* slots of the current window generations, all regions (after the last batch) */
+  uint64_t host_batches;      /* batches submitted from host memory (rl_submit) */
 } rl_engine_stats;
+
+/* Occupancy of the 8 table regions (home unit x window parity) after the last completed batch. */
+typedef struct rl_occupancy {
+  uint32_t gen[8];    /* window generation the count belongs to (home window index + 1; 0 = unused) */
+  uint32_t live[8];   /* slots claimed for that generation */
+  uint32_t limit[8];  /* load limit (slots) */
+  uint32_t slots[8];  /* region size */
+} rl_occupancy;
 
 int rl_create(const rl_config* cfg, rl_engine** out);
 void rl_destroy(rl_engine* e);
@@ -130,19 +144,43 @@ uint32_t rl_abi_version(void);
 /* Load (replace) the rule table. Rule ids index it. Must not be called while a batch is in flight. */
 int rl_load_rules(rl_engine* e, const rl_rule* rules, uint32_t n);
 
-/* Host-memory batch: copies in, runs the pipeline, copies back into out[n_desc] and
- * req_throttle_ms[n_req] (DoLimitResponse.ThrottleMillis, base_limiter.go:163-165).
- * Asynchronous: outputs are valid after rl_wait(). */
-int rl_submit(rl_engine* e, const rl_batch* batch, rl_status* out, uint32_t* req_throttle_ms);
-int rl_wait(rl_engine* e);
-
-/* Device-memory batch (inputs already resident in HBM; outputs stay in HBM). Ordered on
- * the engine's stream; rl_wait() or the stream synchronises. Used by the multi-GPU router
- * and by the benchmark. */
-int rl_submit_device(rl_engine* e, const rl_batch* device_batch, rl_status* d_out, uint32_t* d_req_throttle_ms);
-
-/* Batches that may be in flight at once through rl_submit_pipelined. */
+/* Batches that may be in flight at once (rl_submit, rl_submit_pipelined). */
 #define RL_MAX_IN_FLIGHT 3
+
+/* ---- Host-memory batches (the Go micro-batcher's path) ---------------------------------
+ * Up to RL_MAX_IN_FLIGHT host batches are in flight: each has its own pinned staging slot,
+ * its H2D copies run on a copy stream while the previous batch's kernels run, and its D2H
+ * copies on another while the next batch's run.
+ *
+ * rl_host_acquire returns the next free staging slot: pinned host arrays (C memory, so a cgo
+ * caller fills them through unsafe slices without passing Go pointers) with their
+ * capacities. rl_submit takes a batch whose arrays are that slot's (no copy) or any host
+ * memory (copied into the slot before rl_submit returns: the caller's arrays are free again).
+ * out[n_desc] / req_throttle_ms[n_req] (DoLimitResponse.ThrottleMillis, base_limiter.go:163-165)
+ * may be NULL: the results then stay in the engine until rl_wait_into copies them out
+ * (the cgo-safe form: Go memory is only touched during that call); non-NULL C memory is
+ * filled by rl_wait and must stay valid until then. Completion is in submission order. */
+typedef struct rl_host_batch {
+  uint8_t* prefix_blob;
+  uint32_t* prefix_off;
+  uint32_t* rule_id;
+  uint32_t* req_of;
+  int64_t* now;
+  uint32_t* hits_addend;
+  uint32_t max_desc, max_req, max_blob, reserved;
+} rl_host_batch;
+int rl_host_acquire(rl_engine* e, rl_host_batch* out);
+int rl_submit(rl_engine* e, const rl_batch* batch, rl_status* out, uint32_t* req_throttle_ms);
+/* Complete the oldest batch in flight (any submit form). */
+int rl_wait(rl_engine* e);
+/* Complete the oldest batch in flight, copying its results into out[n_desc] and
+ * req_throttle_ms[n_req] (a host batch's, or NULL to discard). */
+int rl_wait_into(rl_engine* e, rl_status* out, uint32_t* req_throttle_ms);
+
+/* Device-memory batch (inputs already resident in HBM; outputs stay in HBM), with nothing
+ * else in flight. Ordered on the engine's stream; rl_wait() completes it. Used by the
+ * multi-GPU router and by the benchmark. */
+int rl_submit_device(rl_engine* e, const rl_batch* device_batch, rl_status* d_out, uint32_t* d_req_throttle_ms);
 
 /* Device-memory batch whose inputs are complete when the call is made, submitted behind at
  * most RL_MAX_IN_FLIGHT - 1 batches still in flight (the micro-batcher's multi-buffering:
@@ -203,6 +241,8 @@ int rl_route_unpack(rl_engine* e, const rl_batch* device_batch, const uint32_t* 
 int rl_reset(rl_engine* e);
 
 int rl_get_stats(rl_engine* e, rl_engine_stats* s);
+/* Table occupancy (synchronises the engine's stream; not while a batch is in flight). */
+int rl_get_occupancy(rl_engine* e, rl_occupancy* o);
 
 /* Per-kernel timing with HIP events on the engine stream (off by default). When on, each
  * pipeline kernel is bracketed by an event pair; rl_kernel_times() returns the accumulated

@@ -49,14 +49,26 @@ def lib():
         L.rlo_decide.restype = None
         L.rlo_cache_key.argtypes = [C.c_char_p, u32, u32, i64, C.c_char_p, u32]
         L.rlo_cache_key.restype = u32
-        L.rlo_counter.argtypes = [vp, C.c_char_p, u32, C.c_int]
+        L.rlo_counter.argtypes = [vp, C.c_char_p, u32, C.c_int, i64]
         L.rlo_counter.restype = i64
-        L.rlo_local_cached.argtypes = [vp, C.c_char_p, u32]
+        L.rlo_local_cached.argtypes = [vp, C.c_char_p, u32, i64]
         L.rlo_local_cached.restype = C.c_int
         L.rlo_num_keys.argtypes = [vp]
         L.rlo_num_keys.restype = u64
-        L.rlo_fingerprint.argtypes = [C.c_char_p, u32, u64, u32, u64, C.POINTER(u64), C.POINTER(u64)]
+        L.rlo_num_strings.argtypes = [vp]
+        L.rlo_num_strings.restype = u64
+        L.rlo_fingerprint.argtypes = [C.c_char_p, u32, u64, u64, C.POINTER(u64), C.POINTER(u64)]
         L.rlo_fingerprint.restype = None
+        L.rlo_fingerprint_many.argtypes = [vp, vp, u32, u64, u64, vp, vp]
+        L.rlo_fingerprint_many.restype = None
+        L.rlo_place.argtypes = [u32, C.POINTER(u32), C.POINTER(u32)]
+        L.rlo_place.restype = None
+        L.rlo_prefix_lanes.argtypes = [C.c_char_p, u32, u64, C.POINTER(u64), C.POINTER(u64)]
+        L.rlo_prefix_lanes.restype = None
+        L.rlo_route_owner.argtypes = [u64, u64, u32]
+        L.rlo_route_owner.restype = u32
+        L.rlo_local_cache_stats.argtypes = [vp] + [C.POINTER(u64)] * 4
+        L.rlo_local_cache_stats.restype = None
         _lib = L
     return _lib
 
@@ -98,14 +110,25 @@ class Oracle:
             raise ValueError(f"rlo_submit: {rc}")
         return out, thr
 
-    def counter(self, key: bytes, per_second=False) -> int:
-        return self.L.rlo_counter(self.h, key, len(key), int(per_second))
+    def counter(self, key: bytes, now=None, per_second=False) -> int:
+        """Redis counter of a full key string at time `now` (-1: absent or expired); now=None
+        ignores expiry (the last value INCRBY left)."""
+        return self.L.rlo_counter(self.h, key, len(key), int(per_second), -(1 << 63) if now is None else now)
 
-    def local_cached(self, key: bytes) -> bool:
-        return bool(self.L.rlo_local_cached(self.h, key, len(key)))
+    def local_cached(self, key: bytes, now: int) -> bool:
+        return bool(self.L.rlo_local_cached(self.h, key, len(key), now))
 
     def num_keys(self) -> int:
         return self.L.rlo_num_keys(self.h)
+
+    def num_strings(self) -> int:
+        """Distinct key strings ever stored (one device table slot each per window)."""
+        return self.L.rlo_num_strings(self.h)
+
+    def local_cache_stats(self) -> dict:
+        v = [C.c_uint64() for _ in range(4)]
+        self.L.rlo_local_cache_stats(self.h, *[C.byref(x) for x in v])
+        return dict(zip(["hit", "miss", "lookup", "entries"], [x.value for x in v]))
 
 
 def decide(L_, unit, ratio, now, hits, after, local_hit=False, has_limit=True, before=None):
@@ -124,40 +147,36 @@ def cache_key(prefix: bytes, unit: int, now: int) -> bytes:
     return buf.raw[:n]
 
 
-def fingerprints(blob: np.ndarray, off: np.ndarray, window_start: int, unit: int, seed: int):
-    """Fingerprints (hi, lo uint64 arrays) of every prefix blob[off[i]:off[i+1]]."""
+def fingerprints(blob: np.ndarray, off: np.ndarray, window_start: int, seed: int):
+    """Fingerprints (hi uint64, lo = 32-bit tag) of every key string blob[off[i]:off[i+1]] || window_start."""
     n = len(off) - 1
     hi = np.zeros(n, np.uint64)
     lo = np.zeros(n, np.uint64)
-    L = lib()
-    L.rlo_fingerprint_many.restype = None
-    L.rlo_fingerprint_many.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64,
-                                       C.c_void_p, C.c_void_p]
     blob = np.ascontiguousarray(blob, np.uint8)
     off = np.ascontiguousarray(off, np.uint32)
-    L.rlo_fingerprint_many(_p(blob), _p(off), n, window_start, unit, seed, _p(hi), _p(lo))
+    lib().rlo_fingerprint_many(_p(blob), _p(off), n, window_start, seed, _p(hi), _p(lo))
     return hi, lo
 
 
-def prefix_lanes(prefix: bytes, unit: int, seed: int):
+def place(window_start: int):
+    """Table region (home unit x parity) and generation of a key string's window start."""
+    r, g = C.c_uint32(), C.c_uint32()
+    lib().rlo_place(window_start, C.byref(r), C.byref(g))
+    return r.value, g.value
+
+
+def prefix_lanes(prefix: bytes, seed: int):
     """Fingerprint lanes (a, b) of a key prefix before the window: the routed key identity."""
     a, b = C.c_uint64(), C.c_uint64()
-    L = lib()
-    L.rlo_prefix_lanes.argtypes = [C.c_char_p, C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint64),
-                                   C.POINTER(C.c_uint64)]
-    L.rlo_prefix_lanes.restype = None
-    L.rlo_prefix_lanes(prefix, len(prefix), unit, seed, C.byref(a), C.byref(b))
+    lib().rlo_prefix_lanes(prefix, len(prefix), seed, C.byref(a), C.byref(b))
     return a.value, b.value
 
 
 def route_owner(a: int, b: int, n_shards: int) -> int:
-    L = lib()
-    L.rlo_route_owner.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32]
-    L.rlo_route_owner.restype = C.c_uint32
-    return int(L.rlo_route_owner(a, b, n_shards))
+    return int(lib().rlo_route_owner(a, b, n_shards))
 
 
-def fingerprint(prefix: bytes, window_start: int, unit: int, seed: int):
+def fingerprint(prefix: bytes, window_start: int, seed: int):
     hi, lo = C.c_uint64(), C.c_uint64()
-    lib().rlo_fingerprint(prefix, len(prefix), window_start, unit, seed, C.byref(hi), C.byref(lo))
+    lib().rlo_fingerprint(prefix, len(prefix), window_start, seed, C.byref(hi), C.byref(lo))
     return hi.value, lo.value

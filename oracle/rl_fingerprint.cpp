@@ -18,10 +18,10 @@ inline uint64_t fmix(uint64_t x) {
 }  // namespace
 
 // Prefix lanes (a, b) before the window is folded in: also the routed record's key identity.
-extern "C" void rlo_prefix_lanes(const uint8_t* prefix, uint32_t len, uint32_t unit, uint64_t seed, uint64_t* a_out,
-                                 uint64_t* b_out) {
+// Unit-independent: one prefix + window start is one Redis key string whatever the rule.
+extern "C" void rlo_prefix_lanes(const uint8_t* prefix, uint32_t len, uint64_t seed, uint64_t* a_out, uint64_t* b_out) {
   uint64_t a = seed ^ 0x9E3779B97F4A7C15ull;
-  uint64_t b = (seed + 0xC2B2AE3D27D4EB4Full) ^ ((uint64_t)len << 32) ^ (uint64_t)unit;
+  uint64_t b = (seed + 0xC2B2AE3D27D4EB4Full) ^ ((uint64_t)len << 32);
   for (uint32_t o = 0; o < len; o += 8) {
     uint64_t w = 0;
     for (uint32_t k = 0; k < 8 && o + k < len; ++k) w |= (uint64_t)prefix[o + k] << (8 * k);
@@ -39,27 +39,27 @@ extern "C" uint32_t rlo_route_owner(uint64_t a, uint64_t b, uint32_t n_shards) {
   return (uint32_t)(((x >> 32) * (uint64_t)n_shards) >> 32);
 }
 
-extern "C" void rlo_fingerprint(const uint8_t* prefix, uint32_t len, uint64_t window_start, uint32_t region,
-                                uint64_t seed, uint64_t* hi, uint64_t* lo) {
-  // lanes: a = seed ^ K0, b = (seed + K1) ^ (len << 32) ^ unit
-  uint64_t a = seed ^ 0x9E3779B97F4A7C15ull;
-  uint64_t b = (seed + 0xC2B2AE3D27D4EB4Full) ^ ((uint64_t)len << 32) ^ (uint64_t)region;
-  for (uint32_t o = 0; o < len; o += 8) {
-    uint64_t w = 0;
-    for (uint32_t k = 0; k < 8 && o + k < len; ++k) w |= (uint64_t)prefix[o + k] << (8 * k);  // little-endian, zero pad
-    a = rotl((a ^ w) * 0x165667B19E3779F9ull, 31);
-    b = (b + w) * 0xD6E8FEB86659FD93ull;
-    b ^= b >> 29;
-  }
+extern "C" void rlo_fingerprint(const uint8_t* prefix, uint32_t len, uint64_t window_start, uint64_t seed,
+                                uint64_t* hi, uint64_t* lo) {
+  uint64_t a, b;
+  rlo_prefix_lanes(prefix, len, seed, &a, &b);
   a ^= window_start * 0xC2B2AE3D27D4EB4Full;
   b = (b ^ window_start) * 0x165667B19E3779F9ull;
   *hi = fmix(a + rotl(b, 23));
-  *lo = fmix(b ^ (a * 0xC4CEB9FE1A85EC53ull));
+  *lo = fmix(b ^ (a * 0xC4CEB9FE1A85EC53ull)) & 0xFFFFFFFFull;
+}
+
+// Home unit of a key string: the largest unit whose divider divides its window start; region
+// = (home - 1) * 2 + parity of the home window, gen = home window index + 1.
+extern "C" void rlo_place(uint32_t ws, uint32_t* region, uint32_t* gen) {
+  const uint32_t home = ws % 86400u == 0 ? 4u : ws % 3600u == 0 ? 3u : ws % 60u == 0 ? 2u : 1u;
+  const uint32_t div = home == 4u ? 86400u : home == 3u ? 3600u : home == 2u ? 60u : 1u;
+  *region = (home - 1u) * 2u + ((ws / div) & 1u);
+  *gen = ws / div + 1u;
 }
 
 // Batch form over a prefix blob (test-fixture generation: searching fingerprint collisions).
 extern "C" void rlo_fingerprint_many(const uint8_t* blob, const uint32_t* off, uint32_t n, uint64_t window_start,
-                                     uint32_t unit, uint64_t seed, uint64_t* hi, uint64_t* lo) {
-  for (uint32_t i = 0; i < n; ++i)
-    rlo_fingerprint(blob + off[i], off[i + 1] - off[i], window_start, unit, seed, hi + i, lo + i);
+                                     uint64_t seed, uint64_t* hi, uint64_t* lo) {
+  for (uint32_t i = 0; i < n; ++i) rlo_fingerprint(blob + off[i], off[i + 1] - off[i], window_start, seed, hi + i, lo + i);
 }

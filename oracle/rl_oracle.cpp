@@ -5,10 +5,13 @@
 // kentik/api-ratelimit tree). The Redis stand-in is a string-keyed map whose
 // INCRBY returns the post-increment int64 (Redis semantics; pinned by
 // test/redis/driver_impl_test.go:121-133, miniredis v2.11.4: INCRBY -> 1 then 2).
-// EXPIRE is modelled as "the key lives for the rest of its window": the key string
-// embeds the window start (cache_key.go:66-68), so with non-decreasing request time
-// a key is never referenced after its window ends and its TTL (div + jitter >= div,
-// fixed_cache_impl.go:69-72) never decides an outcome.
+// EXPIRE follows Redis: every INCRBY is followed by `EXPIRE key ttl` (fixed_cache_impl.go:
+// 26-29), ttl = UnitToDivider(unit) + jitter (:69-72; this restatement takes jitter 0 — with
+// jitter the reference itself is nondeterministic), the key is alive while now < expiry and
+// an expired key reads as missing (INCRBY starts from 0). Keys are exact strings, so a
+// MINUTE key "p_3600" and an HOUR key "p_3600" are one Redis key (one store) and one
+// freecache entry, whose TTL is the unit divider of the Set (base_limiter.go:102).
+// Time is integer seconds: a TTL that ends exactly at `now` has expired.
 #include "rl_oracle.h"
 
 #include <cmath>
@@ -48,6 +51,12 @@ void append_dec(std::string& s, int64_t v) {
 
 }  // namespace
 
+// A Redis key: INCRBY counter and EXPIRE deadline (unix seconds; alive while now < exp).
+struct RKey {
+  int64_t count;
+  int64_t exp;
+};
+
 struct rlo_engine {
   float near_ratio;
   bool local_cache;       // localCache != nil (base_limiter.go:58, :94)
@@ -55,9 +64,10 @@ struct rlo_engine {
   std::vector<rlo_rule> rules;
   std::vector<uint32_t> near_thr;  // per rule, base_limiter.go:86
   // Redis stand-ins: main client and per-second client (fixed_cache_impl.go:74-85).
-  std::unordered_map<std::string, int64_t> redis[2];
-  // freecache stand-in: set of over-limit keys (base_limiter.go:94-106).
-  std::unordered_set<std::string> lcache;
+  std::unordered_map<std::string, RKey> redis[2];
+  // freecache stand-in: over-limit keys and their expiry (base_limiter.go:94-106; freecache
+  // v1.1.0 Get misses once now >= expireAt).
+  std::unordered_map<std::string, int64_t> lcache;
   uint64_t lc_hit = 0, lc_miss = 0;
 };
 
@@ -205,14 +215,24 @@ uint32_t do_limit(rlo_engine* e, uint32_t d0, uint32_t d1, const uint8_t* blob, 
     if (!own(keys[k])) { skip[k] = 1; continue; }
     if (keys[k].key.empty()) continue;
     if (e->local_cache) {  // IsOverLimitWithLocalCache base_limiter.go:57-66
-      if (e->lcache.count(keys[k].key)) { ++e->lc_hit; local_hit[k] = 1; continue; }
+      auto it = e->lcache.find(keys[k].key);
+      if (it != e->lcache.end() && now < it->second) { ++e->lc_hit; local_hit[k] = 1; continue; }
       ++e->lc_miss;
     }
-    // INCRBY key h (post value, missing = 0) into results[i] as uint32; EXPIRE (TTL only).
-    const int store = (e->per_second_split && keys[k].per_second) ? 1 : 0;
-    int64_t& c = e->redis[store][keys[k].key];
-    c += (int64_t)h;
-    results[k] = (uint32_t)c;
+  }
+  // PipeDo of the main pipeline, then of the per-second one (:91-102): INCRBY key h (post value,
+  // a missing or expired key counts as 0) into results[i] as uint32, then EXPIRE key div.
+  for (int pass = 0; pass < 2; ++pass) {
+    for (size_t k = 0; k < keys.size(); ++k) {
+      if (skip[k] || local_hit[k] || keys[k].key.empty()) continue;
+      const int store = (e->per_second_split && keys[k].per_second) ? 1 : 0;
+      if (store != pass) continue;
+      RKey& c = e->redis[store][keys[k].key];  // a new key is {0, 0}: expired
+      if (now >= c.exp) c.count = 0;
+      c.count += (int64_t)h;
+      c.exp = now + unit_to_divider(e->rules[rule_id[keys[k].i]].unit);
+      results[k] = (uint32_t)c.count;
+    }
   }
   // HOT LOOP 2 :108-117
   uint32_t throttle_max = 0;
@@ -233,8 +253,8 @@ uint32_t do_limit(rlo_engine* e, uint32_t d0, uint32_t d1, const uint8_t* blob, 
     decide(L, near, div, now, h, results[k] - h, results[k], local_hit[k] != 0, has, &out[i], &thr);
     // response.ThrottleMillis = max(...)  base_limiter.go:163-165
     if (thr > throttle_max) throttle_max = thr;
-    // localCache.Set(key) on OVER_LIMIT from Redis  base_limiter.go:94-106
-    if (has && !local_hit[k] && e->local_cache && results[k] > L) e->lcache.insert(keys[k].key);
+    // localCache.Set(key, TTL = UnitToDivider(unit)) on OVER_LIMIT from Redis  base_limiter.go:94-106
+    if (has && !local_hit[k] && e->local_cache && results[k] > L) e->lcache[keys[k].key] = now + div;
   }
   return throttle_max;
 }
@@ -282,7 +302,7 @@ int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* 
   std::hash<std::string> H;
   for (int s = 0; s < 2; ++s)
     for (auto& kv : e->redis[s]) shard[H(kv.first) % T]->redis[s].emplace(kv.first, kv.second);
-  for (auto& k : e->lcache) shard[H(k) % T]->lcache.insert(k);
+  for (auto& kv : e->lcache) shard[H(kv.first) % T]->lcache.emplace(kv.first, kv.second);
   std::vector<std::vector<uint32_t>> thr(T, std::vector<uint32_t>(n_req, 0));
   std::vector<std::thread> th;
   for (int t = 0; t < T; ++t) {
@@ -317,17 +337,27 @@ int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* 
   return 0;
 }
 
-int64_t rlo_counter(rlo_engine* e, const char* key, uint32_t len, int per_second) {
+int64_t rlo_counter(rlo_engine* e, const char* key, uint32_t len, int per_second, int64_t now) {
   const int s = (e->per_second_split && per_second) ? 1 : 0;
   auto it = e->redis[s].find(std::string(key, len));
-  return it == e->redis[s].end() ? -1 : it->second;
+  if (it == e->redis[s].end() || now >= it->second.exp) return -1;
+  return it->second.count;
 }
 
-int rlo_local_cached(rlo_engine* e, const char* key, uint32_t len) {
-  return e->lcache.count(std::string(key, len)) ? 1 : 0;
+int rlo_local_cached(rlo_engine* e, const char* key, uint32_t len, int64_t now) {
+  auto it = e->lcache.find(std::string(key, len));
+  return (it != e->lcache.end() && now < it->second) ? 1 : 0;
 }
 
 uint64_t rlo_num_keys(rlo_engine* e) { return e->redis[0].size() + e->redis[1].size(); }
+
+uint64_t rlo_num_strings(rlo_engine* e) {
+  std::unordered_set<std::string> u;
+  for (int s = 0; s < 2; ++s)
+    for (auto& kv : e->redis[s]) u.insert(kv.first);
+  for (auto& kv : e->lcache) u.insert(kv.first);
+  return u.size();
+}
 
 void rlo_local_cache_stats(rlo_engine* e, uint64_t* hit, uint64_t* miss, uint64_t* lookup, uint64_t* entries) {
   *hit = e->lc_hit;
@@ -335,4 +365,3 @@ void rlo_local_cache_stats(rlo_engine* e, uint64_t* hit, uint64_t* miss, uint64_
   *lookup = e->lc_hit + e->lc_miss;
   *entries = e->lcache.size();
 }
-

@@ -83,24 +83,29 @@ void rlo_decide(uint32_t requests_per_unit, uint32_t unit, float near_limit_rati
  * Returns its length; writes at most cap bytes (no terminator). */
 uint32_t rlo_cache_key(const uint8_t* prefix, uint32_t len, uint32_t unit, int64_t now, char* out, uint32_t cap);
 
-/* Redis stand-in introspection: current counter for a full key string (-1 if absent),
- * and whether the local over-limit cache holds it. per_second selects the per-second store. */
-int64_t rlo_counter(rlo_engine* e, const char* key, uint32_t len, int per_second);
-int rlo_local_cached(rlo_engine* e, const char* key, uint32_t len);
-uint64_t rlo_num_keys(rlo_engine* e);
+/* Redis stand-in introspection at time `now`: counter of a full key string (-1 if absent or
+ * expired), and whether the local over-limit cache holds it. per_second selects the
+ * per-second store (when the split is on). */
+int64_t rlo_counter(rlo_engine* e, const char* key, uint32_t len, int per_second, int64_t now);
+int rlo_local_cached(rlo_engine* e, const char* key, uint32_t len, int64_t now);
+uint64_t rlo_num_keys(rlo_engine* e);     /* Redis keys ever created (both stores, expired included) */
+uint64_t rlo_num_strings(rlo_engine* e);  /* distinct key strings (both stores and the local cache) */
 
 /* Local-cache lookup statistics (freecache HitCount/MissCount/LookupCount/EntryCount). */
 void rlo_local_cache_stats(rlo_engine* e, uint64_t* hit, uint64_t* miss, uint64_t* lookup, uint64_t* entries);
 
-/* Deterministic 128-bit key fingerprint — restated here ONLY to test the product's
- * fingerprint kernel (tests/test_fingerprint*.py); decisions above never use it. */
-void rlo_fingerprint(const uint8_t* prefix, uint32_t len, uint64_t window_start, uint32_t region, uint64_t seed,
-                     uint64_t* hi, uint64_t* lo);
+/* Deterministic key fingerprint of the product (prefix bytes + window start)
+ * — restated here ONLY to test the product's fingerprint / placement; decisions above never
+ * use it. lo is the 32-bit tag. */
+void rlo_fingerprint(const uint8_t* prefix, uint32_t len, uint64_t window_start, uint64_t seed, uint64_t* hi,
+                     uint64_t* lo);
+/* Table place of a key string: region (home unit x window parity) and generation. */
+void rlo_place(uint32_t window_start, uint32_t* region, uint32_t* gen);
 /* Multi-GPU routing restated (tests of the router): prefix lanes and owner shard. */
-void rlo_prefix_lanes(const uint8_t* prefix, uint32_t len, uint32_t unit, uint64_t seed, uint64_t* a, uint64_t* b);
+void rlo_prefix_lanes(const uint8_t* prefix, uint32_t len, uint64_t seed, uint64_t* a, uint64_t* b);
 uint32_t rlo_route_owner(uint64_t a, uint64_t b, uint32_t n_shards);
-void rlo_fingerprint_many(const uint8_t* blob, const uint32_t* off, uint32_t n, uint64_t window_start, uint32_t unit,
-                          uint64_t seed, uint64_t* hi, uint64_t* lo);
+void rlo_fingerprint_many(const uint8_t* blob, const uint32_t* off, uint32_t n, uint64_t window_start, uint64_t seed,
+                          uint64_t* hi, uint64_t* lo);
 
 #ifdef __cplusplus
 }

@@ -1,5 +1,5 @@
 """Generate tests/golden/collisions.json: key prefixes whose fingerprints collide on the bits
-the bucketed pipeline groups by (see rl_kernels_v2.hip, k_bgroup), for the engine's default
+the v4 pipeline buckets and splits by (rl_kernels_v4.hip), for the engine's default
 hash seed. Uses the oracle's fingerprint restatement (pinned bit-exact to the device kernel
 by tests/test_gpu_golden.py). Run: python tests/golden/make_collisions.py
   - "g35": two keys equal on fingerprint hi bits 29..63 (grouping bits: regrouped in LDS)
@@ -24,7 +24,7 @@ UNIT = 1                 # SECOND: window start = NOW
 def find(shift, n):
     ids = np.arange(n, dtype=np.uint64)
     blob, off = workload.prefix_blob([b"coll_k_", ids, b"_"])
-    hi, _ = oracle.fingerprints(blob, off, NOW, UNIT, SEED)
+    hi, _ = oracle.fingerprints(blob, off, NOW, SEED)
     g = hi >> np.uint64(shift)
     order = np.argsort(g, kind="stable")
     gs = g[order]

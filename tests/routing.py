@@ -6,7 +6,7 @@
   perm / counts semantics of include/rl_hip.h) whose owner side is the CPU oracle, so the
   exchange protocol runs over gloo without a GPU. Records carry the oracle-restated prefix
   lanes (oracle.prefix_lanes) and owners (oracle.route_owner); the owner keys its oracle by
-  the 16 lane bytes, which identify (prefix, unit) exactly as the device does.
+  the 16 lane bytes, which identify the prefix exactly as the device does.
 - exchange_local: steps 2/3/5 of router.ShardRouter done by slicing, for G shards in one
   process (the GPU test drives G engines on one GPU through it).
 TEST INFRASTRUCTURE ONLY.
@@ -50,7 +50,7 @@ def owners_of(b, rules, n_shards, seed):
         r = int(b.rule[i])
         if r == hiprl.NIL_RULE:
             continue
-        a, bb = oracle.prefix_lanes(b.prefix(i), rules[r][1], seed)
+        a, bb = oracle.prefix_lanes(b.prefix(i), seed)
         own[i] = oracle.route_owner(a, bb, n_shards)
     return own
 
@@ -74,7 +74,7 @@ class OracleShard:
                 continue
             r = int(b.rule[i])
             q = int(b.req_of[i])
-            a, bb = oracle.prefix_lanes(b.prefix(i), self.rules[r][1], self.seed)
+            a, bb = oracle.prefix_lanes(b.prefix(i), self.seed)
             rec[i] = (a, bb, int(b.now[q]), r, max(1, int(b.hits[q])), (self.rank << REQ_BITS) | q)
         order = np.argsort(np.where(own < 0, self.world, own), kind="stable")
         counts = [int((own == s).sum()) for s in range(self.world)]

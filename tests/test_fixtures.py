@@ -15,7 +15,7 @@ def test_collision_fixture_collides():
     assert c["seed"] == inspect.signature(hiprl.Engine).parameters["hash_seed"].default
     for name, shift in (("g35", 29), ("g43", 21)):
         a, b = c[name]
-        ha, la = oracle.fingerprint(hiprl.cache_key_prefix("coll", [("k", a)]), c["now"], c["unit"], c["seed"])
-        hb, lb = oracle.fingerprint(hiprl.cache_key_prefix("coll", [("k", b)]), c["now"], c["unit"], c["seed"])
+        ha, la = oracle.fingerprint(hiprl.cache_key_prefix("coll", [("k", a)]), c["now"], c["seed"])
+        hb, lb = oracle.fingerprint(hiprl.cache_key_prefix("coll", [("k", b)]), c["now"], c["seed"])
         assert ha >> shift == hb >> shift, name
         assert (ha, la) != (hb, lb), name

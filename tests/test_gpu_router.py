@@ -4,8 +4,8 @@ G engines on cuda:0 stand in for G GPUs: each packs its own batch with rl_route_
 all-to-alls are done by slicing (tests/routing.exchange_local), every owner decides what it
 receives with rl_submit_routed, and each origin unpacks with rl_route_unpack. The outputs
 must equal one oracle replaying the origins' batches in rank order — bit-exact statuses,
-stat deltas and ThrottleMillis — for the v3 and LSD pipelines, local cache on and off, a
-skewed stream whose hot keys go through v3's hot buckets, and empty shards.
+stat deltas and ThrottleMillis — for the v4 and LSD pipelines, local cache on and off, a
+skewed stream whose hot keys go through v4 hot buckets, and empty shards.
 """
 import numpy as np
 import pytest
@@ -68,17 +68,17 @@ def stream_batches(G, steps, per, seed, keyspace=30):
     return out
 
 
-@pytest.mark.parametrize("pipeline", ["v4", "v3", "lsd"])
+@pytest.mark.parametrize("pipeline", ["v4", "lsd"])
 @pytest.mark.parametrize("local_cache", [False, True])
 @pytest.mark.parametrize("G", [2, 4])
 def test_routed_random_streams(G, local_cache, pipeline):
     run_routed(G, stream_batches(G, 4, 1500, seed=G), local_cache, pipeline)
 
 
-@pytest.mark.parametrize("pipeline", ["v4", "v3"])
+@pytest.mark.parametrize("pipeline", ["v4"])
 def test_routed_hot_keys(pipeline):
     """A few keys take most descriptors on every origin: the owners' hot sets form from
-    routed candidates and later steps decide those keys in v3's hot buckets."""
+    routed candidates and later steps decide those keys in v4's hot buckets."""
     G, steps = 3, 12
     rng = np.random.default_rng(3)
     out = []

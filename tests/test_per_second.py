@@ -1,16 +1,24 @@
-"""REDIS_PERSECOND: SECOND keys in their own store.
+"""Same-string keys of different units: REDIS_PERSECOND and the
+unsplit store.
 
-With `perSecondClient` set, a SECOND key and a MINUTE key with the same string are
-different counters (`src/redis/fixed_cache_impl.go:74-85`). The HIP table always keeps every
-unit in its own key space, so it reproduces the split configuration exactly:
-the GPU test drives same-string SECOND and MINUTE keys (window starts that coincide at a
-minute boundary) and checks bit-exactness against the oracle with the split on. Without the split,
-Redis shares such a counter and its TTL follows whichever EXPIRE came last (wall clock); the
-CPU test shows the oracle's shared-counter behaviour, which the device does not claim. The
-local over-limit cache is one freecache keyed by the key string for both clients
-(`src/limiter/base_limiter.go:57-66,94-106`), so with it on a SECOND key that goes over limit
-also freezes the MINUTE key of the same string; the device freezes per unit, so that case is
-outside the claim too (measured: 57 of the local-cache stream's statuses differ)."""
+A key is the exact string prefix + decimal window start (`src/limiter/cache_key.go:57-68`),
+so a SECOND key at t = 3600 and a MINUTE / HOUR key of the window starting at 3600 are one
+string. Without `REDIS_PERSECOND` (the default, `src/settings/settings.go:34`) they are one
+Redis counter whose TTL follows whichever `EXPIRE key div` came last
+(`src/redis/fixed_cache_impl.go:26-29,69-72`); with it, SECOND keys count in their own store
+(`:74-85`). MINUTE / HOUR / DAY keys always share the main store. Either way the local
+over-limit cache is one freecache keyed by the string, with the TTL of the unit that went
+over (`src/limiter/base_limiter.go:94-106`).
+
+The CPU tests pin the oracle's Redis/freecache TTL semantics on hand-derived sequences
+(Redis: INCRBY of a missing or expired key starts from 0; EXPIRE sets the deadline; a key is
+alive while now < deadline; freecache Get misses once now >= expireAt). The reference has no
+test of these interleavings, so parity beyond them is "unpinned" by a reference fixture: it
+rests on the documented Redis semantics, with EXPIRATION_JITTER_MAX_SECONDS = 0 (with jitter
+the reference itself is nondeterministic). The GPU tests check the device bit-exactly against
+that oracle on streams where such strings are frequent, split on and off, local cache on and
+off, on both pipelines.
+"""
 import numpy as np
 import pytest
 
@@ -18,25 +26,63 @@ import hiprl
 import oracle
 from streams import assert_same, batch_sizes, replay
 
-T0 = 1_699_999_200  # a multiple of 3600: SECOND, MINUTE and HOUR windows all start here
-RULES = [(5, hiprl.SECOND), (40, hiprl.MINUTE), (90, hiprl.HOUR)]
+T0 = 1_699_920_000  # a multiple of 86400: SECOND, MINUTE, HOUR and DAY windows all start here
+RULES = [(5, hiprl.SECOND), (40, hiprl.MINUTE), (90, hiprl.HOUR), (200, hiprl.DAY)]
+S, M, H, D = 0, 1, 2, 3
 
 
-def same_string_stream(seed, n_req=240):
-    rng = np.random.default_rng(seed)
-    reqs, t = [], T0
-    for q in range(n_req):
-        if q and q % 60 == 0:
-            t += 1  # the SECOND window moves on; MINUTE/HOUR keep the T0 string
-        descs, rules = [], []
-        for _ in range(int(rng.integers(1, 4))):
-            r = int(rng.integers(0, 3))
-            # SECOND and MINUTE share key strings; HOUR keys use their own (a MINUTE and an
-            # HOUR key with one string share a counter even with the split: not claimed)
-            descs.append([("k" if r < 2 else "h", f"v{int(rng.integers(0, 3))}")])
-            rules.append(r)
-        reqs.append(("dom", descs, rules, int(rng.integers(0, 4)), t))
-    return reqs
+def req(rule, t, h=1, key=("k", "v")):
+    return ("dom", [[key]], [rule], h, t)
+
+
+def statuses(reqs, split=False, local_cache=False, rules=RULES):
+    o = oracle.Oracle(per_second_split=split, local_cache=local_cache)
+    o.load_rules(rules)
+    st, thr = replay(o, reqs, [1] * len(reqs))
+    return o, st
+
+
+def remaining(st):
+    return [int(x) for x in st["limit_remaining"]]
+
+
+def test_shared_counter_ttl_follows_last_expire():
+    """Unsplit: SECOND + MINUTE at T0 share one counter; the last EXPIRE decides its life."""
+    # MINUTE then SECOND at T0: the last EXPIRE is 1 s, so at T0+1 the MINUTE key restarts
+    o, st = statuses([req(M, T0), req(S, T0), req(M, T0 + 1)])
+    assert remaining(st) == [39, 3, 39]  # post-values 1, 2, then 1 again
+    assert o.counter(b"dom_k_v_%d" % T0, T0 + 1) == 1
+    # SECOND then MINUTE at T0: the last EXPIRE is 60 s; the counter lives on
+    o, st = statuses([req(S, T0), req(M, T0), req(M, T0 + 1), req(M, T0 + 59), req(M, T0 + 60)])
+    assert remaining(st) == [4, 38, 37, 36, 39]  # T0+60 is the next MINUTE window: a new key
+    # HOUR after a MINUTE touch at T0+30: alive until T0+90 (EXPIRE 60 s), gone at T0+90
+    o, st = statuses([req(M, T0 + 30), req(H, T0 + 89), req(H, T0 + 90)])
+    assert remaining(st) == [39, 88, 87]  # the HOUR touch at T0+89 moved the deadline to T0+3689
+    o, st = statuses([req(M, T0 + 30), req(H, T0 + 90)])
+    assert remaining(st) == [39, 89]
+
+
+def test_split_store_keeps_second_keys_apart():
+    """REDIS_PERSECOND: the SECOND key counts in its own store; MINUTE/HOUR still share."""
+    o, st = statuses([req(S, T0), req(M, T0), req(S, T0), req(H, T0)], split=True)
+    assert remaining(st) == [4, 39, 3, 88]
+    key = b"dom_k_v_%d" % T0
+    assert o.counter(key, T0, per_second=True) == 2 and o.counter(key, T0) == 2
+
+
+def test_local_cache_freezes_the_string_for_the_unit_ttl():
+    """One freecache entry per string, TTL = divider of the unit that went over."""
+    rules = [(1, hiprl.SECOND), (40, hiprl.MINUTE)]
+    for split in (False, True):
+        # SECOND goes over at T0 (post 2 > 1): the string is frozen until T0+1 for every unit
+        reqs = [req(0, T0), req(0, T0), req(1, T0), req(1, T0 + 1)]
+        o, st = statuses(reqs, split=split, local_cache=True, rules=rules)
+        codes = [int(x) & 0xFF for x in st["code_flags"]]
+        local = [bool((int(x) >> 8) & hiprl.FLAG_LOCAL_CACHE_HIT) for x in st["code_flags"]]
+        assert codes == [1, 2, 2, 1] and local == [False, False, True, False], (split, codes, local)
+        # unsplit: SECOND's INCRBYs at T0 also counted in the shared key, which the MINUTE
+        # request at T0+1 finds expired (last EXPIRE 1 s at T0): post-value 1
+        assert remaining(st)[3] == 39
 
 
 def test_same_string_keys_split_vs_shared_oracle():
@@ -46,19 +92,64 @@ def test_same_string_keys_split_vs_shared_oracle():
     shared.load_rules(RULES)
     a = replay(split, reqs)
     b = replay(shared, reqs)
-    key = b"dom_k_v0_%d" % T0
-    # the split keeps the SECOND counter apart; the shared store sums every unit's hits
-    assert shared.counter(key) == split.counter(key) + split.counter(key, per_second=True)
-    assert not np.array_equal(a[0], b[0])
+    assert not np.array_equal(a[0], b[0])  # the stores really differ on this stream
+
+
+def same_string_stream(seed, n_req=3000, t0=T0 - 2):
+    """Requests around aligned windows: time moves 0-1 s every ~20 requests; each descriptor
+    takes a random unit, so strings at minute / hour / day boundaries are shared."""
+    rng = np.random.default_rng(seed)
+    reqs, t = [], t0
+    for q in range(n_req):
+        if rng.random() < 0.05:
+            t += int(rng.integers(0, 2)) + (58 if rng.random() < 0.02 else 0)
+        descs, rules = [], []
+        for _ in range(int(rng.integers(1, 4))):
+            descs.append([("k", f"v{int(rng.integers(0, 4))}")])
+            rules.append(int(rng.choice(4, p=[0.4, 0.3, 0.2, 0.1])))
+        reqs.append(("dom", descs, rules, int(rng.integers(0, 4)), t))
+    return reqs
+
+
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("local_cache", [False, True])
+def test_oracle_stream_self_consistent_across_batch_splits(split, local_cache):
+    """The oracle is serial per request, so batching cannot change it (sanity of the stream)."""
+    reqs = same_string_stream(3, 800)
+    o1 = oracle.Oracle(per_second_split=split, local_cache=local_cache)
+    o2 = oracle.Oracle(per_second_split=split, local_cache=local_cache)
+    o1.load_rules(RULES)
+    o2.load_rules(RULES)
+    assert_same(*replay(o1, reqs), *replay(o2, reqs, batch_sizes(reqs, np.random.default_rng(1), 50)))
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("local_cache", [False])
-def test_gpu_matches_split_oracle_on_same_string_keys(local_cache):
-    reqs = same_string_stream(2 + local_cache)
-    sizes = batch_sizes(reqs, np.random.default_rng(7), 50)
-    o = oracle.Oracle(local_cache=local_cache, per_second_split=True)
+@pytest.mark.parametrize("pipeline", ["v4", "lsd"])
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("local_cache", [False, True])
+def test_gpu_matches_oracle_on_same_string_keys(local_cache, split, pipeline):
+    reqs = same_string_stream(2 + 2 * local_cache + split)
+    sizes = batch_sizes(reqs, np.random.default_rng(7), 300)
+    o = oracle.Oracle(local_cache=local_cache, per_second_split=split)
     o.load_rules(RULES)
-    e = hiprl.Engine(local_cache=local_cache, per_second_split=True)
+    e = hiprl.Engine(local_cache=local_cache, per_second_split=split, pipeline=pipeline)
     e.load_rules(RULES)
-    assert_same(*replay(e, reqs, sizes), *replay(o, reqs, sizes), ctx=f"per-second split lc={local_cache}")
+    assert_same(*replay(e, reqs, sizes), *replay(o, reqs, sizes), ctx=f"split={split} lc={local_cache} {pipeline}")
+    assert e.stats()["inserted_keys"] == o.num_strings()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("local_cache", [False, True])
+def test_gpu_known_answers_shared_ttl(local_cache):
+    """The hand-derived sequences above, each request its own batch and all in one batch."""
+    seqs = [[req(M, T0), req(S, T0), req(M, T0 + 1)],
+            [req(S, T0), req(M, T0), req(M, T0 + 1), req(M, T0 + 59), req(M, T0 + 60)],
+            [req(M, T0 + 30), req(H, T0 + 89), req(H, T0 + 90)], [req(M, T0 + 30), req(H, T0 + 90)],
+            [req(0, T0), req(0, T0), req(1, T0), req(1, T0 + 1)]]
+    for reqs in seqs:
+        for sizes in ([1] * len(reqs), batch_sizes(reqs, np.random.default_rng(0), 8)):
+            o = oracle.Oracle(local_cache=local_cache)
+            o.load_rules(RULES)
+            e = hiprl.Engine(local_cache=local_cache)
+            e.load_rules(RULES)
+            assert_same(*replay(e, reqs, sizes), *replay(o, reqs, sizes), ctx=str(reqs))

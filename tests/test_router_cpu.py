@@ -99,6 +99,6 @@ def test_owner_partition_is_balanced_and_window_independent():
     rng = np.random.default_rng(0)
     prefixes = [f"dom_k_{int(x)}_".encode() for x in rng.integers(0, 1 << 40, 4000)]
     for g in (2, 3, 8):
-        own = np.array([oracle.route_owner(*oracle.prefix_lanes(p, hiprl.SECOND, 7), g) for p in prefixes])
+        own = np.array([oracle.route_owner(*oracle.prefix_lanes(p, 7), g) for p in prefixes])
         cnt = np.bincount(own, minlength=g)
         assert cnt.min() > 0.8 * len(prefixes) / g, cnt
