@@ -182,7 +182,7 @@ struct rl_engine {
   HotBucket* v4_hb = nullptr;                 // per hot bucket batch state
   void* v4_scratch = nullptr;                 // k4_group global scratch + k4_scan ranges
   uint32_t* v4_heads = nullptr;               // per-block unique-key counts (k4_group, then k4_scan)
-  uint32_t* v4_ins = nullptr;                 // per-block new slots per region (k4_group, then k4_scan)
+  uint32_t* v4_ins = nullptr;                 // per-block new slots per region, 16-bit pairs (k4_group, then k4_scan)
   EngineCtl* v4_ctl[3] = {};                  // control blocks rotate over three (k4_group clears batch k+2's)
   uint32_t* d_poison = nullptr;               // set by k4_place of a refused batch, read by k4_scan
 
@@ -387,7 +387,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     }
     timed(KT_V4_SCAN, [&] {
       launch_v4_scan(stream, n, v4_tcount[sl], v4_thsum[sl], v4_hoff, v4_fpart[sl], hot_t + HOT_SLOTS, v4_hb, tab,
-                     d_cand, v4_heads + ng, v4_ins + (size_t)ng * 8, v4_toff, v4_scratch, d_poison, d_occ, c4);
+                     d_cand, v4_heads + ng, v4_ins + (size_t)ng * 4, v4_toff, v4_scratch, d_poison, d_occ, c4);
     });
     timed(KT_V4_PLACE, [&] {
       launch_v4_place(stream, b, srt, v4_tcount[sl], v4_toff, v4_scratch, d_rules, v4_hoff, v4_hb, lc, v4_mrec, out,
@@ -395,7 +395,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     });
     timed(KT_V4_GROUP, [&] {
       launch_v4_group(stream, b, v4_mrec, d_rules, tab, out, thr, v4_hb, v4_dfr, d_cand, want_cand ? 1 : 0,
-                      cfg.hash_seed, v4_scratch, v4_heads, v4_ins, v4_heads + ng, v4_ins + (size_t)ng * 8, routed,
+                      cfg.hash_seed, v4_scratch, v4_heads, v4_ins, v4_heads + ng, v4_ins + (size_t)ng * 4, routed,
                       d_occ, c4, c4n);
     });
     e = hipGetLastError();
@@ -915,7 +915,7 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     chk(hipMalloc(&e->v4_hb, HOT_BUCKETS * sizeof(HotBucket)));
     const size_t nb = (size_t)v4_group_blocks((uint32_t)N) + v4_scan_blocks();
     chk(hipMalloc(&e->v4_heads, nb * 4 + 64));
-    chk(hipMalloc(&e->v4_ins, nb * 8 * 4 + 64));
+    chk(hipMalloc(&e->v4_ins, nb * 4 * 4 + 64));
     chk(hipMalloc(&e->v4_scratch, v4_scratch_bytes()));
     for (int k = 0; k < 3; ++k) {
       chk(hipMalloc(&e->v4_ctl[k], sizeof(EngineCtl)));

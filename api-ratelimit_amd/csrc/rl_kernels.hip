@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
   uint32_t err = 0;
   bool nil = true;
   uint64_t key = NIL_KEY;
-  uint32_t region = 8, gen = 0, uw = 8;
+  uint32_t region = 8, gen = 0, uw = 8;  // uw: unit window slot (v4 hot keys only; unused here)
   if (i < in.n_desc && in.recs) {
     // Routed record (multi-GPU owner): the key prefix arrives as its fingerprint lane state.
     const RRec x = in.recs[i];
@@ -149,14 +149,12 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
   if (lane == 0 && nilmask) atomicAdd(&sh_f[FP_NIL], (uint32_t)__popcll(nilmask));
   for (uint32_t rg = 0; rg < 8; ++rg) {
     const bool mine = region == rg;
-    const uint64_t m = __ballot(mine);
-    if (!m) continue;
+    if (!__ballot(mine)) continue;
     const uint32_t mn = wave_min_u32(mine ? gen : 0xFFFFFFFFu);
     const uint32_t mx = wave_max_u32(mine ? gen : 0u);
     if (lane == 0) {
       atomicMax(&sh_f[FP_GMIN + rg], ~mn);
       atomicMax(&sh_f[FP_GMAX + rg], mx);
-      atomicAdd(&sh_f[FP_CNT + rg], (uint32_t)__popcll(m));
     }
   }
   if (err) atomicOr(&sh_err, err);
@@ -205,7 +203,7 @@ __global__ __launch_bounds__(1024) void k_histogram(const uint64_t* __restrict__
 __global__ __launch_bounds__(256) void k_hist_scan(const uint32_t* __restrict__ part, uint32_t nblocks,
                                                    uint32_t* __restrict__ sub, int npasses,
                                                    const uint32_t* __restrict__ fpart2, uint32_t fp_blocks,
-                                                   const RegionOcc* __restrict__ occ, EngineCtl* ctl) {
+                                                   uint32_t n_all, const RegionOcc* __restrict__ occ, EngineCtl* ctl) {
   const uint32_t tid = threadIdx.x;
   if ((int)blockIdx.x == npasses * HIST_SUB) {
     __shared__ uint32_t shm[FP_PART_WORDS][256];
@@ -230,12 +228,9 @@ __global__ __launch_bounds__(256) void k_hist_scan(const uint32_t* __restrict__ 
     else if (tid < 16) ctl->gen_max[tid - 8] = shm[FP_GMAX + tid - 8][0];
     else if (tid == 16) ctl->n_nil = shm[FP_NIL][0];
     else if (tid == 17) {
-      uint32_t gmax[8], cnt[8];
-      for (int r = 0; r < 8; ++r) {
-        gmax[r] = shm[FP_GMAX + r][0];
-        cnt[r] = shm[FP_CNT + r][0];
-      }
-      if (!capacity_ok(occ, gmax, cnt)) atomicOr(&ctl->err, ERR_TABLE_FULL);
+      uint32_t gmax[8];
+      for (int r = 0; r < 8; ++r) gmax[r] = shm[FP_GMAX + r][0];
+      if (!capacity_ok(occ, gmax, n_all - shm[FP_NIL][0])) atomicOr(&ctl->err, ERR_TABLE_FULL);
     }
     return;
   }
@@ -829,7 +824,7 @@ void launch_hist_scan(hipStream_t st, const uint32_t* part, uint32_t n, uint32_t
                       const uint32_t* fpart2, const RegionOcc* occ, EngineCtl* ctl) {
   const uint32_t fpb = fpart2 ? hist_blocks(n) : 0;
   hipLaunchKernelGGL(k_hist_scan, dim3(npasses * HIST_SUB + (fpb ? 1 : 0)), dim3(256), 0, st, part, hist_blocks(n),
-                     sub, npasses, fpart2, fpb, occ, ctl);
+                     sub, npasses, fpart2, fpb, n, occ, ctl);
 }
 uint32_t hist_sub_words() { return HIST_SUB * RADIX; }
 void launch_fallback_lo_keys(hipStream_t st, const ItemRec* recs, const uint64_t* keys_orig, uint32_t n,

@@ -189,23 +189,23 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   // hot descriptors. Reductions run only for regions / windows present in the wave.
 #pragma unroll
   for (int rg = 0; rg < 8; ++rg) {
-    uint32_t mn = 0xFFFFFFFFu, mx = 0, c = 0;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0;
+    uint64_t any_r = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const bool m = d[r].bucket < NIL_BUCKET && key_region(d[r].key) == (uint32_t)rg;
-      c += (uint32_t)__popcll(__ballot(m));
+      any_r |= __ballot(m);
       if (m) {
         mn = d[r].gen < mn ? d[r].gen : mn;
         mx = d[r].gen > mx ? d[r].gen : mx;
       }
     }
-    if (c) {  // wave-uniform
+    if (any_r) {  // wave-uniform
       mn = wave_min_u32(mn);
       mx = wave_max_u32(mx);
       if (lane == 0) {
         atomicMax(&sh_f[FP_GMIN + rg], ~mn);
         atomicMax(&sh_f[FP_GMAX + rg], mx);
-        atomicAdd(&sh_f[FP_CNT + rg], c);
       }
     }
     uint32_t um = 0;
@@ -390,6 +390,7 @@ RL_DEV void column_counts(const uint16_t* __restrict__ tstart, uint32_t b, uint3
 
 __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ tstart,
                                                    const unsigned long long* __restrict__ thsum, uint32_t ntiles,
+                                                   uint32_t n_desc,
                                                    unsigned long long* __restrict__ hoff,
                                                    const uint32_t* __restrict__ fpart,
                                                    const HotEntry* __restrict__ hot_list, HotBucket* __restrict__ hb,
@@ -506,7 +507,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     }
     // Capacity (before any table write): every hot block computes the same verdict and
     // claims nothing when it fails; block 0 refuses the batch.
-    cap_ok = capacity_ok(occ, &s_f[FP_GMAX], &s_f[FP_CNT]);
+    cap_ok = capacity_ok(occ, &s_f[FP_GMAX], n_desc - s_f[FP_NIL]);
     if (blockIdx.x == 0) {
       if (tid < 8) ctl->gen_min[tid] = ~s_f[FP_GMIN + tid];
       else if (tid < 16) ctl->gen_max[tid - 8] = s_f[FP_GMAX + tid - 8];
@@ -700,11 +701,13 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
       }
       if (ctot >= HOT_CAND_MIN) emit_candidate(ctl, cand, he.rule, ctot, 0xFFFFFFFFu, he.a, he.b, he.unit);
     }
-    // new slots per region of this block (the last k4_group block adds them to RegionOcc)
+    // new slots per region of this block, two 16-bit counts a word (the last k4_group block
+    // adds them to RegionOcc)
 #pragma unroll
-    for (int rg = 0; rg < 8; ++rg) {
-      const uint64_t m = __ballot(ins_region == (uint32_t)rg);
-      if (lane == 0) ins_out[blockIdx.x * 8 + rg] = (uint32_t)__popcll(m);
+    for (int x = 0; x < 4; ++x) {
+      const uint32_t lo_n = (uint32_t)__popcll(__ballot(ins_region == (uint32_t)(2 * x)));
+      const uint32_t hi_n = (uint32_t)__popcll(__ballot(ins_region == (uint32_t)(2 * x + 1)));
+      if (lane == 0) ins_out[blockIdx.x * 4 + x] = lo_n | (hi_n << 16);
     }
     if (lane < (uint32_t)HOT_PER_BLOCK) hb[b] = x;
     heads = tile::wave_sum(heads);
@@ -742,17 +745,28 @@ RL_DEV void gbar() {
   }
 }
 
-RL_DEV void g_insert(const GS& g, uint32_t k) {
+// Hash slot counts: records of the key in the low 16 bits; CNT_MIXED when a record's rule
+// differs from the first record's, CNT_MIXED_UNIT when its unit does too (found here, in
+// parallel, instead of by a walk of the key's list).
+constexpr uint32_t CNT_MASK = 0xFFFFu, CNT_MIXED = 0x10000u, CNT_MIXED_UNIT = 0x20000u;
+RL_DEV void g_insert(const GS& g, uint32_t k, const DevRule* __restrict__ rules) {
   const uint64_t key = g.rec[k].key, lo = g.rec[k].fp_lo;
   const uint32_t hmask = g.hs - 1u;
   uint32_t s = (uint32_t)key & hmask;
+  uint32_t v;
   for (;;) {
-    const uint32_t v = atomicCAS(&g.slot[s], G_EMPTY, k);
+    v = atomicCAS(&g.slot[s], G_EMPTY, k);
     if (v == G_EMPTY || (g.rec[v].key == key && g.rec[v].fp_lo == lo)) break;
     s = (s + 1) & hmask;
   }
   g.grp[k] = (uint16_t)s;
-  atomicAdd(&g.cnt[s], 1u);
+  uint32_t inc = 1u;
+  if (v != G_EMPTY) {
+    const uint32_t r0 = rule_of(g.rec[v].rn), r1 = rule_of(g.rec[k].rn);
+    if (r0 != r1) inc |= rules[r0].unit != rules[r1].unit ? (CNT_MIXED | CNT_MIXED_UNIT) : CNT_MIXED;
+  }
+  if (inc == 1u) atomicAdd(&g.cnt[s], 1u);
+  else atomicOr(&g.cnt[s], inc & ~1u), atomicAdd(&g.cnt[s], 1u);
 }
 
 // One wave: each key's list in position order (positions [0, m), 64 at a time).
@@ -809,7 +823,7 @@ RL_DEV void g_scan(const GS& g, uint32_t m, LSeg* s_agg, LSeg* s_carry) {
         const uint32_t k = g.list[e];
         const uint32_t s = g.grp[k];
         pos[q] = k;
-        hd[q] = e == (uint32_t)g.end[s] - g.cnt[s];
+        hd[q] = e == (uint32_t)g.end[s] - (g.cnt[s] & CNT_MASK);
         hv[q] = g.rec[k].h;
         t = lseg_op(t, LSeg{hd[q], hv[q]});
       }
@@ -857,7 +871,7 @@ RL_DEV void g_lead_exotic(const GS& g, uint32_t k, const DevRule* __restrict__ r
                           EngineCtl* ctl) {
   Slot* slot = reinterpret_cast<Slot*>(g.rec[k].key);
   const uint32_t s = g.grp[k];
-  const uint32_t n = g.cnt[s], e0 = g.end[s] - n;
+  const uint32_t n = g.cnt[s] & CNT_MASK, e0 = g.end[s] - n;
   const uint32_t region = key_region(slot->key);
   const uint32_t ws = region_ws(region, ctl->gen_max[region]);
   KeyState ks = read_state(slot);
@@ -879,22 +893,16 @@ RL_DEV void g_lead_exotic(const GS& g, uint32_t k, const DevRule* __restrict__ r
 // key (a string shared by units of different sizes whose expiry falls inside the batch)
 // leaves per-position replies in P (SEG_EXOTIC). New slots are counted per region in ins[].
 RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, const TableDesc& tab, HotCand* cand,
-                   EngineCtl* ctl, bool has_pre, const SlotView& pre, int cand_on, uint32_t& heads, uint32_t* ins) {
+                   EngineCtl* ctl, bool has_pre, const SlotView& pre, int cand_on, uint32_t& heads, uint64_t& ins) {
   const uint64_t key = g.rec[k].key, lo = g.rec[k].fp_lo;
   const uint32_t rule = rule_of(g.rec[k].rn);
   const uint32_t s = g.grp[k];
-  const uint32_t n = g.cnt[s], e1 = g.end[s], e0 = e1 - n;
+  const uint32_t cw = g.cnt[s];
+  const uint32_t n = cw & CNT_MASK, e1 = g.end[s], e0 = e1 - n;
+  const bool mixed = (cw & CNT_MIXED) != 0, mixed_unit = (cw & CNT_MIXED_UNIT) != 0;
   const uint64_t Pk = g.P[k];
   const DevRule R0 = rules[rule];
-  bool mixed = false, mixed_unit = false;
   heads += 1;
-  for (uint32_t e = e0; e < e1; ++e) {
-    const uint32_t r = rule_of(g.rec[g.list[e]].rn);
-    if (r != rule) {
-      mixed = true;
-      mixed_unit |= rules[r].unit != R0.unit;
-    }
-  }
   if (cand_on && n >= HOT_MIN_SEG && !mixed) emit_cand_sc1(ctl, cand, rule, n, g.rec[g.list[e0]].idx);
   const uint32_t region = key_region(key);
   const uint32_t gen = ctl->gen_max[region];  // the region's one generation (k4_scan)
@@ -914,7 +922,7 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
   if (!existed) {
     slot_reset(slot, key);
     heads += 1u << 16;
-    atomicAdd(&ins[region], 1u);
+    ins += 1ull << (8 * region);  // per-region new-slot counts, 8 bits each (reduced per block)
   }
   const bool ps = per_second_store(tab, R0.unit);
   uint64_t base = 0;
@@ -933,19 +941,30 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
   } else if (tab.local_cache) {
     // the first record (arrival order) whose INCRBY reply exceeds its limit freezes the key;
     // the INCRBYs of its own request still happen (all lookups precede the Sets)
-    const bool exact = !mixed && base + Pk < (1ull << 32);
-    for (uint32_t e = e0; e < e1; ++e) {
-      const uint32_t j = g.list[e];
-      const uint64_t after = base + g.P[j];
-      const uint32_t L = rules[rule_of(g.rec[j].rn)].L;
-      if (exact ? after > (uint64_t)L : (uint32_t)after > L) {
-        const uint32_t rstar = g.rec[j].req;
-        last = j;
-        for (uint32_t f = e + 1; f < e1 && g.rec[g.list[f]].req == rstar; ++f) last = g.list[f];
-        freeze = rstar;
-        final_count = base + g.P[last];
-        break;
+    uint32_t estar = e1;
+    if (!mixed && base + Pk < (1ull << 32)) {
+      // one limit, no wrap: after = base + P rises along the list, binary search
+      if (base + Pk > (uint64_t)R0.L) {
+        uint32_t a = e0, b = e1 - 1;
+        while (a < b) {
+          const uint32_t mid = (a + b) >> 1;
+          if (base + g.P[g.list[mid]] > (uint64_t)R0.L) b = mid; else a = mid + 1;
+        }
+        estar = a;
       }
+    } else {
+      for (uint32_t e = e0; e < e1; ++e) {
+        const uint32_t j = g.list[e];
+        if ((uint32_t)(base + g.P[j]) > rules[rule_of(g.rec[j].rn)].L) { estar = e; break; }
+      }
+    }
+    if (estar < e1) {
+      const uint32_t rstar = g.rec[g.list[estar]].req;
+      uint32_t f = estar;
+      while (f + 1 < e1 && g.rec[g.list[f + 1]].req == rstar) ++f;
+      last = g.list[f];
+      freeze = rstar;
+      final_count = base + g.P[last];
     }
   }
   if (freeze != SEG_FROZEN_BEFORE) {
@@ -968,7 +987,7 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
 template <bool LDS>
 RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__ rules, const TableDesc& tab,
                             rl_status* __restrict__ out, uint32_t* __restrict__ req_thr, HotCand* cand, int cand_on,
-                            int routed, LSeg* s_agg, LSeg* s_carry, uint32_t* sh_w, uint32_t* s_ins, EngineCtl* ctl) {
+                            int routed, LSeg* s_agg, LSeg* s_carry, uint32_t* sh_w, uint64_t& ins, EngineCtl* ctl) {
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
   uint32_t heads = 0;
   // The staging (and the hash-table reset before it) is complete: read each position's first
@@ -981,19 +1000,19 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
       if (k < m) pre[j] = load_slot(slot_first(tab, g.rec[k].key));
     }
   }
-  for (uint32_t k = tid; k < m; k += G_NT) g_insert(g, k);
+  for (uint32_t k = tid; k < m; k += G_NT) g_insert(g, k, rules);
   gbar<LDS>();
   ST4(1);
   // each key's list start: exclusive prefix of the per-slot counts (hash-slot order)
   {
     const uint32_t spt = g.hs / G_NT, s0 = tid * spt;
     uint32_t sum = 0;
-    for (uint32_t q = 0; q < spt; ++q) sum += g.cnt[s0 + q];
+    for (uint32_t q = 0; q < spt; ++q) sum += g.cnt[s0 + q] & CNT_MASK;
     uint32_t tot;
     uint32_t run = tile::block_excl_scan<G_NT>(sum, sh_w, tot);
     for (uint32_t q = 0; q < spt; ++q) {
       g.end[s0 + q] = (uint16_t)run;
-      run += g.cnt[s0 + q];
+      run += g.cnt[s0 + q] & CNT_MASK;
     }
   }
   gbar<LDS>();
@@ -1009,11 +1028,11 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
     for (int j = 0; j < G_IPT; ++j) {
       const uint32_t k = tid + j * G_NT;
       if (k < m && g_tail(g, k) == k)
-        g_lead(g, k, rules, tab, cand, ctl, true, pre[j], cand_on, heads, s_ins);
+        g_lead(g, k, rules, tab, cand, ctl, true, pre[j], cand_on, heads, ins);
     }
   } else {
     for (uint32_t k = tid; k < m; k += G_NT)
-      if (g_tail(g, k) == k) g_lead(g, k, rules, tab, cand, ctl, false, SlotView{}, cand_on, heads, s_ins);
+      if (g_tail(g, k) == k) g_lead(g, k, rules, tab, cand, ctl, false, SlotView{}, cand_on, heads, ins);
   }
   __threadfence_block();
   __syncthreads();
@@ -1202,6 +1221,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t j = blockIdx.x;
   uint32_t heads = 0;
+  uint64_t ins = 0;  // new slots per region, 8 bits each
   if (tid < 8) s_ins[tid] = 0;
   if (tid < 64) {  // ranges per group and record bases of the groups: prefixes (one wave)
     const uint32_t v = tid < (uint32_t)MSD_GROUPS ? ranges[tid] : 0u;
@@ -1266,7 +1286,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
         const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
         {
           const uint32_t hh = group_range<true>(gl, m, rules, tab, out, req_thr, cand, cand_on, routed, s_agg,
-                                                &s_carry, sh_w, s_ins, ctl);
+                                                &s_carry, sh_w, ins, ctl);
           heads += hh;
           ST4X(0, m);
           ST4X(1, hh & 0xFFFFu);
@@ -1312,7 +1332,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
           if (mp == 0) continue;
           const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
           heads += group_range<true>(gl, mp, rules, tab, out, req_thr, cand, cand_on, routed, s_agg, &s_carry,
-                                     sh_w, s_ins, ctl);
+                                     sh_w, ins, ctl);
         }
       } else if (split_half != 1) {
         // grouped in place in bucket order (global scratch); for a split bucket by its half-0
@@ -1330,11 +1350,16 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
         __threadfence_block();
         __syncthreads();
         heads += group_range<false>(gg, m, rules, tab, out, req_thr, cand, cand_on, routed, s_agg, &s_carry,
-                                    sh_w, s_ins, ctl);
+                                    sh_w, ins, ctl);
       }
     }
   }
   heads = tile::wave_sum(heads);
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint32_t c = tile::wave_sum((uint32_t)(ins >> (8 * r)) & 0xFFu);
+    if (lane == 0 && c) atomicAdd(&s_ins[r], c);
+  }
   __syncthreads();
   if (lane == 0 && heads) atomicAdd(&s_heads, heads);
   __syncthreads();
@@ -1344,7 +1369,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
   // them), then one lane adds to the block's shard counter (blockIdx & 7); the last block of a
   // shard adds to the global counter; the last of those is the last block.
   if (tid == 0) st_relaxed(&wg_heads[j], s_heads);
-  if (tid < 8) st_relaxed(&wg_ins[j * 8 + tid], s_ins[tid]);
+  if (tid < 4) st_relaxed(&wg_ins[j * 4 + tid], s_ins[2 * tid] | (s_ins[2 * tid + 1] << 16));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
@@ -1370,12 +1395,33 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
       u += (k < gridDim.x ? ld_relaxed(&wg_heads[k]) : scan_heads[k - gridDim.x]) & 0xFFFFu;
     u = tile::wave_sum(u);
     if (lane == 0 && u) atomicAdd(&s_heads, u);
-    // thread (block group, region): 32 groups x 8 regions
-    const uint32_t rg = tid & 7u;
-    uint32_t ins = 0;
-    for (uint32_t k = tid >> 3; k < gridDim.x + n_scan_heads; k += G_NT / 8)
-      ins += k < gridDim.x ? ld_relaxed(&wg_ins[k * 8 + rg]) : scan_ins[(k - gridDim.x) * 8 + rg];
-    if (ins) atomicAdd(&s_ins[rg], ins);
+    // new slots per region: 4 words per block, two 16-bit region counts each; every thread
+    // sums whole blocks with its loads in flight together
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0;
+    const uint32_t nb = gridDim.x + n_scan_heads;
+    for (uint32_t k0 = tid * 4; k0 < nb; k0 += G_NT * 4) {
+      uint32_t w[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          const uint32_t k = k0 + q;
+          w[q][x] = k >= nb ? 0u : k < gridDim.x ? ld_relaxed(&wg_ins[k * 4 + x]) : scan_ins[(k - gridDim.x) * 4 + x];
+        }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        c0 += w[q][0] & 0xFFFFu; c1 += w[q][0] >> 16;
+        c2 += w[q][1] & 0xFFFFu; c3 += w[q][1] >> 16;
+        c4 += w[q][2] & 0xFFFFu; c5 += w[q][2] >> 16;
+        c6 += w[q][3] & 0xFFFFu; c7 += w[q][3] >> 16;
+      }
+    }
+    const uint32_t cs[8] = {c0, c1, c2, c3, c4, c5, c6, c7};
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const uint32_t c = tile::wave_sum(cs[r]);
+      if (lane == 0 && c) atomicAdd(&s_ins[r], c);
+    }
   }
   __syncthreads();
   if (tid == 0) {
@@ -1461,7 +1507,7 @@ void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const un
                     unsigned long long* hoff, const uint32_t* fpart, const HotEntry* hot_list, HotBucket* hb,
                     const TableDesc& tab, HotCand* cand, uint32_t* heads_out, uint32_t* ins_out, uint16_t* toff,
                     void* scratch, const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl) {
-  hipLaunchKernelGGL(v4::k4_scan, dim3(v4_scan_blocks()), dim3(v4::SCAN_NT), 0, st, tstart, thsum, v4_tiles(n), hoff,
+  hipLaunchKernelGGL(v4::k4_scan, dim3(v4_scan_blocks()), dim3(v4::SCAN_NT), 0, st, tstart, thsum, v4_tiles(n), n, hoff,
                      fpart, hot_list, hb, tab, cand, heads_out, ins_out, toff, v4_ranges(scratch), poison, occ, ctl);
 }
 void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart, const uint16_t* toff,

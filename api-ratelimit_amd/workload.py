@@ -134,28 +134,30 @@ class Workload:
 
 
 def config3_batch(b: int, d: int = 1_000_000, N: int = 100_000_000, s: float = 1.1, seed: int = 3,
-                  t0: int = 1_700_000_000) -> Batch:
+                  t0: int = 1_700_000_000, batches_per_s: int = 1) -> Batch:
     """Config 3: 1e8 keys Zipf(1.1), ranks through a fixed permutation, rule by rank % 3
-    (SECOND 10 / MINUTE 600 / HOUR 36000), 1 descriptor per request, h = 1, now = t0 + b."""
+    (SECOND 10 / MINUTE 600 / HOUR 36000), 1 descriptor per request, h = 1,
+    now = t0 + b // batches_per_s."""
     z = Zipf(N, s)
     rank = z.sample(seed, b, d) - 1
     key = permute(rank, N)
     rule = (rank % 3).astype(np.uint32)
     blob, off = prefix_blob([b"bench_k_", key, b"_"])
-    return Batch(blob, off, rule, np.arange(d, dtype=np.uint32), np.full(d, t0 + b, np.int64),
+    return Batch(blob, off, rule, np.arange(d, dtype=np.uint32), np.full(d, t0 + b // batches_per_s, np.int64),
                  np.ones(d, np.uint32))
 
 
 CONFIG3_RULES = [(10, SECOND), (600, MINUTE), (36000, HOUR)]
 
 
-def config2_batch(b: int, d: int = 1_000_000, N: int = 1_000_000, seed: int = 2, t0: int = 1_700_000_000) -> Batch:
-    """Config 2: 1e6 uniform keys, SECOND L=5, 1 descriptor per request, now advances 1 s per batch."""
+def config2_batch(b: int, d: int = 1_000_000, N: int = 1_000_000, seed: int = 2, t0: int = 1_700_000_000,
+                  batches_per_s: int = 1) -> Batch:
+    """Config 2: 1e6 uniform keys, SECOND L=5, 1 descriptor per request, now = t0 + b // batches_per_s."""
     u = uniform01(seed, b, 0, d)
     rank = np.minimum((u * N).astype(np.int64), N - 1)
     blob, off = prefix_blob([b"bench_k_", permute(rank, N), b"_"])
-    return Batch(blob, off, np.zeros(d, np.uint32), np.arange(d, dtype=np.uint32), np.full(d, t0 + b, np.int64),
-                 np.ones(d, np.uint32))
+    return Batch(blob, off, np.zeros(d, np.uint32), np.arange(d, dtype=np.uint32),
+                 np.full(d, t0 + b // batches_per_s, np.int64), np.ones(d, np.uint32))
 
 
 CONFIG2_RULES = [(5, SECOND)]

@@ -3,9 +3,16 @@
 
 Workload (N=1 line): BASELINE config 3 — 1e8 keys, Zipf s=1.1 over ranks mapped through a
 fixed permutation, rule by rank % 3 (SECOND 10 / MINUTE 600 / HOUR 36000), 1e6 descriptors
-per batch (one descriptor per request, hits_addend 1), `now` advancing 1 s per batch.
-A step = one batch through the whole device path (fingerprint, radix sort, segmented scan,
-table apply, decide). Inputs are resident in HBM before timing; outputs stay in HBM.
+per batch (one descriptor per request, hits_addend 1). `now` advances once every
+--batches-per-second batches (default 8000, i.e. the rate this path runs at), so one SECOND
+window holds thousands of batches and the table holds the live set a real deployment has:
+before timing, --prefill batches (default 1.5 s of traffic) fill it — every MINUTE/HOUR key
+drawn so far, the previous second's SECOND keys and half of the current second's — in
+regions sized for it (2^26 slots per home unit and parity, 12.9 GB). A step = one batch
+through the whole device path (fingerprint, bucket sort, segmented scan, table apply,
+decide); inputs are resident in HBM before timing, outputs stay in HBM. Batches are made on
+the device (tools/gen/workload_gen.hip, the workload.py construction) because one second of
+traffic is 8000 distinct 1e6-descriptor batches.
 
 Multi-GPU (torchrun, one rank per GPU): the key space is hash-sharded one
 shard per GPU. Every rank ingests its own 1e6-descriptor batch per step, routes each
@@ -14,14 +21,18 @@ decide, and the 24-B replies return with the reverse all-to-all (api-ratelimit_a
 — weak scaling. value = descriptors decided for all ranks / max-over-ranks time.
 --independent runs N unrouted replicas instead (each rank its own key space).
 
-Also reported (rank 0): per-kernel HIP-event times over an extra K steps, the roofline
-of the batch pipeline against §8(d)'s algorithmic bytes, and the CPU oracle timed on a
-bounded sample of the same stream (cpu_baseline).
+Also reported (rank 0): per-kernel HIP-event times over an extra K steps, the roofline of the
+dominant kernel and the SURVEY §8(d) random-access roofline, table occupancy, the host
+(PCIe) path end to end, and the CPU oracle timed on a bounded sample of the same stream on
+1 and on N host threads (cpu_baseline).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes as C
+import hashlib
 import json
+import math
 import os
 import sys
 import time
@@ -36,7 +47,19 @@ import hiprl  # noqa: E402
 import router  # noqa: E402
 import workload  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+T0 = 1_700_000_020      # not minute-aligned: SECOND / MINUTE / HOUR keys in their own home regions
+PMC_SUMMARY = ROOT / "profiles" / "r02_pmc_traffic.json"
+SOURCES = sorted((ROOT / "api-ratelimit_amd" / "csrc").glob("*.h*")) + sorted(
+    (ROOT / "api-ratelimit_amd" / "csrc").glob("*.cpp")) + [ROOT / "include" / "rl_hip.h"]
+
+
+def source_sha() -> str:
+    h = hashlib.sha256()
+    for p in SOURCES:
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()[:16]
 
 
 def parse():
@@ -44,28 +67,74 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3])
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3])
     ap.add_argument("--desc", type=int, default=1_000_000, help="descriptors per batch")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--batches-per-second", type=int, default=8000,
+                    help="batches per SECOND window (now advances once every K batches); 1 = round-1 mode")
+    ap.add_argument("--prefill", type=int, default=-1,
+                    help="untimed batches that fill the table before warmup (-1: 1.5 windows of K batches)")
+    ap.add_argument("--log2-slots", type=int, default=26, help="table slots per region (home unit x parity)")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample budget per leg (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="N-thread CPU baseline (0 = min(16, cpus))")
     ap.add_argument("--no-kernel-times", action="store_true")
     ap.add_argument("--no-roofline-probe", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true")
     ap.add_argument("--pipeline", choices=["v4", "lsd"], default="v4",
                     help="decision pipeline (v4 default; lsd = radix-sort only)")
     ap.add_argument("--independent", action="store_true",
                     help="N>1: unrouted replicas (each rank its own key space) instead of RCCL routing")
     ap.add_argument("--json-out", type=str, default="")
-    ap.add_argument("--depth", type=int, default=2,
-                    help="batches in flight through rl_submit_pipelined (2..3; --serial = 1). 2 is fastest "
-                         "at config 3: a third batch's k4_hist starts at the end of batch k-2 and takes the "
-                         "CUs the next k4_scan needs (DESIGN.md §3a)")
-    ap.add_argument("--serial", action="store_true",
-                    help="one batch in flight (rl_submit_device + rl_wait per step) instead of two (rl_submit_pipelined)")
+    ap.add_argument("--depth", type=int, default=2, help="batches in flight through rl_submit_pipelined (2..3)")
+    ap.add_argument("--serial", action="store_true", help="one batch in flight (rl_submit_device + rl_wait)")
     return ap.parse_args()
 
 
-def random_access_roofline(eng, alg_bytes, U, pipe_ms, step_ms):
-    import ctypes as C
+class DeviceGen:
+    """Config-2/3 batches made on the device (tools/gen/libworkload_gen.so) into DeviceBatch buffers."""
 
+    def __init__(self, config: int, d: int, seed: int, K: int, dev):
+        import torch
+
+        self.torch, self.d, self.seed, self.K, self.dev = torch, d, seed, K, dev
+        lib = C.CDLL(str(ROOT / "tools" / "gen" / "libworkload_gen.so"))
+        vp, u32, u64, dbl = C.c_void_p, C.c_uint32, C.c_uint64, C.c_double
+        lib.rlw_keys.argtypes = [C.c_int, u64, dbl, dbl, dbl, dbl, u64, u64, u64, u32, vp, vp, vp, vp]
+        lib.rlw_bytes.argtypes = [u32, vp, vp, vp, vp, vp]
+        self.lib = lib
+        if config == 3:
+            self.N, s, self.mode = 100_000_000, 1.1, 0
+            z = workload.Zipf(self.N, s)
+            self.z = (s, float(z.hx1), float(z.hN), float(z.sq))
+        else:
+            self.N, self.mode, self.z = 1_000_000, 1, (0.0, 0.0, 0.0, 0.0)
+        a = 2654435761
+        while math.gcd(a, self.N) != 1:
+            a += 2
+        self.mult = a  # workload.permute
+        self.key = torch.empty(d, dtype=torch.int64, device=dev)
+        self.len = torch.empty(d, dtype=torch.int32, device=dev)
+
+    def alloc(self):
+        t, d, dev = self.torch, self.d, self.dev
+        return router.DeviceBatch(t.empty(d * 17 + 64, dtype=t.uint8, device=dev), t.zeros(d + 1, dtype=t.int32, device=dev),
+                                  t.empty(d, dtype=t.int32, device=dev), t.empty(d, dtype=t.int32, device=dev),
+                                  t.empty(d, dtype=t.int64, device=dev), t.ones(d, dtype=t.int32, device=dev),
+                                  d * 17)
+
+    def fill(self, b: int, db):
+        """Batch b (counter stream b): now = T0 + b // K."""
+        t = self.torch
+        st = t.cuda.current_stream(self.dev).cuda_stream
+        rc = self.lib.rlw_keys(self.mode, self.N, *self.z, self.seed, b, self.mult, self.d, self.key.data_ptr(),
+                               db.rule.data_ptr(), self.len.data_ptr(), st)
+        t.cumsum(self.len, 0, dtype=t.int32, out=db.off[1:])
+        rc |= self.lib.rlw_bytes(self.d, self.key.data_ptr(), db.off.data_ptr(), db.blob.data_ptr(), db.req_of.data_ptr(), st)
+        db.now.fill_(T0 + b // self.K)
+        if rc:
+            raise RuntimeError("workload generator launch failed")
+
+
+def random_access_roofline(eng, alg_bytes, U, pipe_ms, step_ms):
     lp = ROOT / "tools" / "microbench" / "libroofline_probe.so"
     if not lp.exists() or U <= 0:
         return None
@@ -73,7 +142,7 @@ def random_access_roofline(eng, alg_bytes, U, pipe_ms, step_ms):
     lib.rl_probe_roofline.argtypes = [C.c_uint64, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_double),
                                       C.POINTER(C.c_double)]
     lib.rl_probe_roofline.restype = C.c_int
-    slots = sum(2 << int(x) for x in eng.cfg.log2_slots)  # 8 regions: unit x window parity
+    slots = sum(2 << int(x) for x in eng.cfg.log2_slots)  # 8 regions: home unit x window parity
     gbs, rate, rus = C.c_double(), C.c_double(), C.c_double()
     if lib.rl_probe_roofline(slots, U, C.byref(gbs), C.byref(rate), C.byref(rus)):
         return None
@@ -90,6 +159,52 @@ def random_access_roofline(eng, alg_bytes, U, pipe_ms, step_ms):
                           "frac = t_roof / t"}
 
 
+def pmc_traffic(dom: str):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc summary,
+    only if it was measured on these exact kernel sources."""
+    if not PMC_SUMMARY.exists():
+        return None, "no PMC summary committed"
+    try:
+        pm = json.loads(PMC_SUMMARY.read_text())
+    except Exception as ex:  # noqa: BLE001
+        return None, f"unreadable PMC summary: {ex}"
+    if pm.get("source_sha") != source_sha():
+        return None, f"PMC summary {PMC_SUMMARY.name} is for other kernel sources ({pm.get('source_sha')})"
+    k = pm.get("kernels", {}).get(dom)
+    return (k or {}).get("hbm_bytes_per_launch"), f"{PMC_SUMMARY.name} (source {pm['source_sha']})"
+
+
+def cpu_baseline(args, rules, d, seed, K, b0):
+    """The C++ oracle (serial DoLimit restatement) on host batches of the same stream (numpy
+    generator, batch indices from b0): 1 thread, then N key-sharded threads on the same batches."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle as orc
+
+    n_thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+    gen = workload.config3_batch if args.config == 3 else workload.config2_batch
+    hbs, legs = [], {}
+    for threads in (1, n_thr):
+        o = orc.Oracle()
+        o.load_rules(rules)
+        n_done, t_cpu, nb = 0, 0.0, 0
+        while t_cpu < args.cpu_seconds and nb < 64:
+            if nb == len(hbs):
+                hbs.append(gen(b0 + nb, d=d, seed=seed, batches_per_s=K, t0=T0))
+            t1 = time.perf_counter()
+            o.submit(hbs[nb], threads=threads)
+            t_cpu += time.perf_counter() - t1
+            n_done += d
+            nb += 1
+        legs[threads] = (n_done / t_cpu, nb, t_cpu)
+    v1, nb1, t1 = legs[1]
+    vn, nbn, tn = legs[n_thr]
+    return {"value": round(vn, 1), "unit": "descriptor decisions/s", "cores": n_thr, "kind": "port",
+            "sample": f"{nbn} batches ({nbn * d} descriptors) of the same stream (host-generated, cold table) through "
+                      f"the C++ oracle, key-sharded over {n_thr} threads, {tn:.1f} s",
+            "single_core": {"value": round(v1, 1), "cores": 1,
+                            "sample": f"{nb1} batches, serial DoLimit over an in-memory Redis stand-in, {t1:.1f} s"}}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -104,185 +219,221 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    d = args.desc
+    d, K = args.desc, max(1, args.batches_per_second)
+    lg = args.log2_slots
     if args.config == 3:
-        gen, rules, log2 = workload.config3_batch, workload.CONFIG3_RULES, (22, 24, 25, 12)
+        rules, log2 = workload.CONFIG3_RULES, (lg, lg, lg, 12)
         wl = "config3: 1e8 keys Zipf s=1.1, SECOND/MINUTE/HOUR by rank%3, 1 descriptor/request"
-    elif args.config == 2:
-        gen, rules, log2 = workload.config2_batch, workload.CONFIG2_RULES, (22, 12, 12, 12)
-        wl = "config2: 1e6 uniform keys, SECOND L=5, 1 descriptor/request"
     else:
-        gen, rules, log2 = workload.config1_batch, workload.CONFIG1_RULES, (16, 12, 12, 12)
-        wl = "config1: examples/ratelimit rules, 1e4 keys"
-    n_batches = args.warmup + args.steps * (1 if args.no_kernel_times else 2)
-    # Each rank is its own key shard: seed the stream by rank.
-    host_batches = []
-    t_gen = time.time()
-    for b in range(n_batches):
-        if args.config == 1:
-            hb = gen(b, d=d, seed=1 + 7919 * rank)
-        else:
-            hb = gen(b, d=d, seed=(3 if args.config == 3 else 2) + 7919 * rank)
-        host_batches.append(hb)
-    t_gen = time.time() - t_gen
-
+        rules, log2 = workload.CONFIG2_RULES, (lg, 12, 12, 12)
+        wl = "config2: 1e6 uniform keys, SECOND L=5, 1 descriptor/request"
+    prefill = args.prefill if args.prefill >= 0 else (K + K // 2 if K > 1 else 0)
+    seed = (3 if args.config == 3 else 2) + 7919 * rank  # each rank its own stream
     routed = world > 1 and not args.independent
     # an owner may receive up to every origin's batch (hot keys concentrate on their owner)
     cap = d * world if routed else d
     eng = hiprl.Engine(device=local, log2_slots=log2, max_batch_desc=cap, max_batch_req=cap,
-                       max_blob_bytes=max(int(hb.blob.shape[0]) for hb in host_batches) + 64, sort_bits=48,
-                       pipeline=args.pipeline)
+                       max_blob_bytes=cap * 17 + 64, sort_bits=48, pipeline=args.pipeline)
     eng.load_rules(rules)
-
-    dev_batches = [router.DeviceBatch.from_host(hb, dev) for hb in host_batches]
-    # two output buffers: with two batches in flight each needs its own
+    gen = DeviceGen(args.config, d, seed, K, dev)
+    rtr = router.ShardRouter(router.EngineShard(eng, rank, world, dev, d)) if routed else None
+    pipelined = rtr is None and not args.serial
+    DEPTH = min(args.depth, hiprl.MAX_IN_FLIGHT) if pipelined else 1
     outs = [torch.empty(d * 20, dtype=torch.uint8, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
     thrs = [torch.empty(d, dtype=torch.int32, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
-    rtr = None
-    if routed:
-        rtr = router.ShardRouter(router.EngineShard(eng, rank, world, dev, d))
-    torch.cuda.synchronize()
 
-    pipelined = rtr is None and not args.serial
-    # The rl_batch of every batch and the output pointers are marshalled once, outside the timed
-    # loop: a service's submitter builds them while the previous batch runs (Python ctypes
-    # marshalling would otherwise sit between rl_wait and the next submit).
-    DEPTH = min(args.depth, hiprl.MAX_IN_FLIGHT) if pipelined else 1
-    sub_args = [(hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs()),
-                 outs[b % DEPTH].data_ptr(), thrs[b % DEPTH].data_ptr()) for b, db in enumerate(dev_batches)]
-
-    def run(b0, b1):
-        """Batches [b0, b1): one step per batch. Pipelined: batch k+1 is submitted before batch k
-        is waited for (the micro-batcher's double buffering); every batch is complete on return."""
-        for j, b in enumerate(range(b0, b1)):
-            db = dev_batches[b]
+    def run(dbs, first=0):
+        """One step per batch. Pipelined: batch k+1 is submitted before batch k is waited for (the
+        micro-batcher's double buffering); every batch is complete on return."""
+        pend = 0
+        for j, db in enumerate(dbs):
             if rtr is not None:
                 rtr.step(db)
                 continue
+            sb = hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs())
+            o, t = outs[(first + j) % len(outs)].data_ptr(), thrs[(first + j) % len(thrs)].data_ptr()
             if pipelined:
-                eng.submit_pipelined_batch(*sub_args[b])  # output buffers rotate by batch
-                if j >= DEPTH - 1:
+                eng.submit_pipelined_batch(sb, o, t)
+                pend += 1
+                if pend == DEPTH:
                     eng.wait()
+                    pend -= 1
             else:
-                args_ = (db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), outs[j & 1].data_ptr(), thrs[j & 1].data_ptr())
-                eng.submit_device_async(*args_)
+                eng.submit_device_async(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), o, t)
                 eng.wait()
-        if pipelined:
-            for _ in range(min(DEPTH - 1, b1 - b0)):
-                eng.wait()
+        for _ in range(pend):
+            eng.wait()
 
-    run(0, args.warmup)
+    # Prefill (untimed): one batch generated at a time into a ring of buffers, the engine two
+    # batches behind (a buffer is refilled only after the batch that used it completed).
+    t_fill = time.time()
+    ring = [gen.alloc() for _ in range(4)]
+    pend = 0
+    for b in range(prefill):
+        db = ring[b % len(ring)]
+        gen.fill(b, db)
+        torch.cuda.current_stream(dev).synchronize()
+        if rtr is not None:
+            rtr.step(db)
+            continue
+        sb = hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs())
+        eng.submit_pipelined_batch(sb, outs[b % len(outs)].data_ptr(), thrs[b % len(thrs)].data_ptr())
+        pend += 1
+        if pend == 2:
+            eng.wait()
+            pend -= 1
+    for _ in range(pend):
+        eng.wait()
+    t_fill = time.time() - t_fill
+    fallbacks_prefill = eng.stats()["lsd_fallbacks"]
+    # Timed batches (and warmup and kernel-timing batches) resident before timing.
+    n_kt = 0 if args.no_kernel_times else args.steps
+    b0 = prefill
+    dbs = []
+    for j in range(args.warmup + args.steps + n_kt):
+        db = gen.alloc()
+        gen.fill(b0 + j, db)
+        dbs.append(db)
+    torch.cuda.synchronize()
+    run(dbs[:args.warmup])
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    fb0 = eng.stats()["lsd_fallbacks"]
     t0 = time.perf_counter()
-    run(args.warmup, args.warmup + args.steps)
+    run(dbs[args.warmup:args.warmup + args.steps], args.warmup)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    fb_timed = eng.stats()["lsd_fallbacks"] - fb0
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     total_desc = world * args.steps * d
     value = total_desc / elapsed
+    step_ms = elapsed / args.steps * 1e3
 
-    # Per-kernel HIP-event timing over another K steps of the same stream.
-    kernel = None
-    uniq = []
-    if not args.no_kernel_times:
+    # Per-kernel HIP-event timing over another K steps of the same stream (one stream, unoverlapped).
+    kernel, uniq = None, []
+    if n_kt:
         eng.set_timing(True)
-        for b in range(args.warmup + args.steps, args.warmup + 2 * args.steps):
-            run(b, b + 1)
+        for j in range(args.warmup + args.steps, len(dbs)):
+            run([dbs[j]], j)
             uniq.append(eng.last_batch_info()["unique_keys"])
         kt = eng.kernel_times()
         eng.set_timing(False)
         kernel = {k: dict(total_ms=v[0], launches=v[1]) for k, v in kt.items() if v[1]}
-    info = eng.last_batch_info()
     if not uniq:
-        uniq = [info["unique_keys"]]
+        uniq = [eng.last_batch_info()["unique_keys"]]
     stats = eng.stats()
+    occ = eng.occupancy()
+
+    # Host (PCIe) path: the timed batches from host memory through rl_submit, staged by the
+    # submitter in the engine's pinned slots (rl_host_acquire, as a Go micro-batcher builds
+    # batches in C memory), three in flight (H2D, kernels and D2H of different batches
+    # overlap), outputs copied out by rl_wait_into — what the Go side sees end to end.
+    host = None
+    if not args.no_host_path and rtr is None:
+        hbatches = []
+        for db in dbs[args.warmup:args.warmup + args.steps]:
+            n = int(db.off[-1].item())
+            hbatches.append(hiprl.Batch(db.blob[:n].cpu().numpy(), db.off.cpu().numpy().view(np.uint32),
+                                        db.rule.cpu().numpy().view(np.uint32), db.req_of.cpu().numpy().view(np.uint32),
+                                        db.now.cpu().numpy(), db.hits.cpu().numpy().view(np.uint32)))
+        out_h = np.empty(d, hiprl.STATUS_DTYPE)
+        thr_h = np.empty(d, np.uint32)
+
+        def host_round(bs):
+            pend = 0
+            for b in bs:
+                sl = eng.host_acquire()
+                n = int(b.blob.shape[0])
+                sl["blob"][:n] = b.blob
+                sl["off"][:b.n_desc + 1] = b.off
+                sl["rule"][:b.n_desc] = b.rule
+                sl["req_of"][:b.n_desc] = b.req_of
+                sl["now"][:b.n_req] = b.now
+                sl["hits"][:b.n_req] = b.hits
+                eng.submit_staged(b.n_desc, b.n_req, n, sl)
+                pend += 1
+                if pend == hiprl.MAX_IN_FLIGHT:
+                    eng._check(eng.lib.rl_wait_into(eng.h, out_h.ctypes.data, thr_h.ctypes.data), "rl_wait_into")
+                    pend -= 1
+            for _ in range(pend):
+                eng._check(eng.lib.rl_wait_into(eng.h, out_h.ctypes.data, thr_h.ctypes.data), "rl_wait_into")
+
+        host_round(hbatches[:2])
+        th = time.perf_counter()
+        host_round(hbatches)
+        t_host = time.perf_counter() - th
+        pcie = sum(int(b.blob.shape[0]) + 4 * (b.n_desc + 1) + 8 * b.n_desc + 12 * b.n_req + 20 * b.n_desc + 4 * b.n_req
+                   for b in hbatches)
+        host = {"value": round(len(hbatches) * d / t_host, 1), "unit": "descriptor decisions/s",
+                "ms_per_batch": round(t_host / len(hbatches) * 1e3, 4),
+                "pcie_GBps": round(pcie / t_host / 1e9, 2), "pcie_bytes_per_batch": pcie // len(hbatches),
+                "note": "same batches from host memory: staged into the engine's pinned slots (numpy copy, included), "
+                        "3 in flight, results copied out by rl_wait_into"}
 
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
 
-    # Roofline of the batch pipeline against §8(d) algorithmic bytes.
     U = float(np.mean(uniq))
-    hb_last = host_batches[-1]
-    alg_bytes = workload.algorithmic_bytes(hb_last, int(U))
+    nbytes = int(dbs[-1].off[-1].item())
+    alg_bytes = nbytes + 12 * d + 12 * d + 20 * d + 4 * d + 64 * int(U)  # workload.algorithmic_bytes, r = d
     roofline = None
     if kernel:
         per_batch_ms = {k: v["total_ms"] / args.steps for k, v in kernel.items()}
-        pipe_ms = sum(v for k, v in per_batch_ms.items())
+        pipe_ms = sum(per_batch_ms.values())
         dom = max((k for k in per_batch_ms if k != "memset"), key=lambda k: per_batch_ms[k])
-        achieved = alg_bytes / (pipe_ms * 1e-3) / 1e9
-        prof_dir = ROOT / "profiles"
-        traffic = None
-        # PMC traffic of this pipeline from the committed rocprofv3 --pmc passes (tools/profile_round.sh)
-        tf = prof_dir / {"v4": "r01_v7_pmc_traffic.json", "v3": "r01_v3_pmc_traffic.json", "v2": "r01_v2_pmc_traffic.json",
-                         "lsd": "r01_pmc_traffic.json"}[args.pipeline]
-        if tf.exists():
-            try:
-                traffic = json.loads(tf.read_text()).get("hbm_bytes_per_batch")
-            except Exception:
-                traffic = None
+        dom_us = kernel[dom]["total_ms"] * 1e3 / kernel[dom]["launches"]
+        # The dominant kernel priced at the batch's algorithmic bytes (SURVEY §8d's per-descriptor
+        # figure x the descriptors one launch processes): every kernel of a batch handles all of
+        # its descriptors, so each launch is held to the whole batch's bytes.
+        achieved = alg_bytes / (dom_us * 1e-6) / 1e9
+        traffic, tsrc = pmc_traffic(dom)
         roofline = {
-            "bound": "hbm", "kernel": "batch pipeline (all kernels of one batch, HIP events on the engine stream)",
+            "bound": "hbm", "kernel": dom,
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
             "algorithmic_bytes_per_batch": alg_bytes, "unique_keys_per_batch": int(U),
+            "dominant_kernel_avg_us": round(dom_us, 2),
             "pipeline_us_per_batch": round(pipe_ms * 1e3, 2),
-            "dominant_kernel": {"name": dom, "us_per_batch": round(per_batch_ms[dom] * 1e3, 2),
-                                "launches_per_batch": kernel[dom]["launches"] / args.steps,
-                                "avg_us_per_launch": round(kernel[dom]["total_ms"] * 1e3 / kernel[dom]["launches"], 2)},
+            "pipeline_achieved_GBps": round(alg_bytes / (pipe_ms * 1e-3) / 1e9, 1),
             "kernels_us_per_batch": {k: round(v * 1e3, 2) for k, v in per_batch_ms.items()},
+            "definition": "achieved = algorithmic bytes of one batch (SURVEY §8d: prefixes + 12 B/desc + 16 B/req "
+                          "+ 20 B/desc out + 64 B per unique key) / the dominant kernel's average launch time "
+                          "(HIP events on the engine stream, kernels unoverlapped)",
         }
-
-    # SURVEY.md §8d random-access roofline: t_roof = streaming bytes / copy bandwidth + U /
-    # random slot-RMW rate, both measured here on a table of the engine's size.
-    if roofline is not None and not args.no_roofline_probe:
-        ra = random_access_roofline(eng, alg_bytes, int(U), pipe_ms, elapsed / args.steps * 1e3)
-        if ra:
-            roofline["random_access"] = ra
+        if not args.no_roofline_probe:
+            ra = random_access_roofline(eng, alg_bytes, int(U), pipe_ms, step_ms)
+            if ra:
+                roofline["random_access"] = ra
 
     cpu = None
     if world == 1 and args.cpu_seconds > 0:
-        sys.path.insert(0, str(ROOT / "oracle"))
-        import oracle as orc
+        cpu = cpu_baseline(args, rules, d, seed, K, b0)
 
-        o = orc.Oracle()
-        o.load_rules(rules)
-        n_done, t_cpu, nb = 0, 0.0, 0
-        for hb in host_batches:
-            t1 = time.perf_counter()
-            o.submit(hb)
-            t_cpu += time.perf_counter() - t1
-            n_done += hb.n_desc
-            nb += 1
-            if t_cpu >= args.cpu_seconds:
-                break
-        cpu = {"value": round(n_done / t_cpu, 1), "unit": "descriptor decisions/s", "cores": 1, "kind": "port",
-               "sample": f"first {nb} batches ({n_done} descriptors) of the same stream through the C++ oracle "
-                         f"(serial DoLimit over an in-memory Redis stand-in), {t_cpu:.1f} s"}
-
+    live_frac = [round(occ["live"][r] / occ["slots"][r], 4) for r in range(8)]
     line = {
         "metric": "descriptor decisions/sec, 100M keys Zipf, 1-8 GPUs; % of HBM peak" if args.config == 3
-        else f"descriptor decisions/sec (config {args.config})",
+        else "descriptor decisions/sec (config 2)",
         "value": round(value, 1),
         "unit": "descriptor decisions/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "ms_per_step": round(step_ms, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u64",
-        "data": "synthetic (seeded splitmix64 / bounded Zipf stream, generated on host, resident in HBM)",
+        "dtype": "u32",
+        "data": "synthetic (seeded splitmix64 / bounded Zipf stream, generated on the device, resident in HBM)",
         "config": {"workload": wl, "descriptors_per_batch": d, "requests_per_batch": d,
+                   "batches_per_second_window": K, "prefill_batches": prefill,
                    "parallelism": (f"key-sharded x{world}, RCCL all-to-all routing (32-B records out, 24-B replies back)"
                                    if routed else "single shard" if world == 1
                                    else f"x{world} independent replicas (no collective)"),
@@ -290,8 +441,12 @@ def main():
                    "unique_keys_per_batch": int(U)},
         "roofline": roofline,
         "cpu_baseline": cpu,
-        "engine": {"resorts": stats["resorts"], "lsd_fallbacks": stats["lsd_fallbacks"], "hot_keys": stats["hot_keys"],
-                   "batches": stats["batches"], "gen_s": round(t_gen, 1)},
+        "host_path": host,
+        "table": {"live_keys": stats["live_keys"], "region_live_fraction": live_frac, "region_slots": occ["slots"],
+                  "bytes": int(sum(occ["slots"])) * 32},
+        "engine": {"resorts": stats["resorts"], "lsd_fallbacks_prefill": fallbacks_prefill,
+                   "lsd_fallbacks_timed": fb_timed, "hot_keys": stats["hot_keys"], "batches": stats["batches"],
+                   "prefill_s": round(t_fill, 1), "source_sha": source_sha()},
     }
     s = json.dumps(line)
     print(s, flush=True)

@@ -69,7 +69,23 @@ struct rlo_engine {
   // v1.1.0 Get misses once now >= expireAt).
   std::unordered_map<std::string, int64_t> lcache;
   uint64_t lc_hit = 0, lc_miss = 0;
+  // rlo_submit_mt: the state lives in key shards between multi-threaded calls
+  std::vector<rlo_engine*> shards;
 };
+
+namespace {
+// Move the key shards' state back into the engine (before any serial use of it).
+void merge_shards(rlo_engine* e) {
+  for (rlo_engine* sh : e->shards) {
+    for (int s = 0; s < 2; ++s) e->redis[s].insert(sh->redis[s].begin(), sh->redis[s].end());
+    e->lcache.insert(sh->lcache.begin(), sh->lcache.end());
+    e->lc_hit += sh->lc_hit;
+    e->lc_miss += sh->lc_miss;
+    delete sh;
+  }
+  e->shards.clear();
+}
+}  // namespace
 
 // C linkage comes from the declarations in rl_oracle.h.
 
@@ -81,7 +97,10 @@ rlo_engine* rlo_create(float near_limit_ratio, int local_cache, int per_second_s
   return e;
 }
 
-void rlo_destroy(rlo_engine* e) { delete e; }
+void rlo_destroy(rlo_engine* e) {
+  merge_shards(e);
+  delete e;
+}
 
 int rlo_load_rules(rlo_engine* e, const rlo_rule* rules, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i)
@@ -186,17 +205,10 @@ int validate(const rlo_engine* e, uint32_t n_desc, const uint32_t* prefix_off, c
   return 0;
 }
 
-// One request: fixedRateLimitCacheImpl.DoLimit, fixed_cache_impl.go:31-123.
-// Descriptors [d0, d1) of the batch; `own` filters descriptors to a key shard
-// (nullptr = all). Returns the request's ThrottleMillis contribution.
-template <class Own>
-uint32_t do_limit(rlo_engine* e, uint32_t d0, uint32_t d1, const uint8_t* blob, const uint32_t* off,
-                  const uint32_t* rule_id, int64_t now, uint32_t hits_addend, rlo_status* out, Own own) {
-  // hitsAddend := utils.Max(1, request.HitsAddend)  :39
-  const uint32_t h = umax(1u, hits_addend);
-  // GenerateCacheKeys (one `now` per request, base_limiter.go:43) :42
-  std::vector<Desc> keys;
-  keys.reserve(d1 - d0);
+// The cache keys of descriptors [d0, d1) of one request (GenerateCacheKeys, one `now` per
+// request, base_limiter.go:39-54; GenerateCacheKey, cache_key.go:43-73).
+void build_keys(const rlo_engine* e, uint32_t d0, uint32_t d1, const uint8_t* blob, const uint32_t* off,
+                const uint32_t* rule_id, int64_t now, std::vector<Desc>& keys) {
   for (uint32_t i = d0; i < d1; ++i) {
     Desc d{i, std::string(), false};
     const uint32_t r = rule_id[i];
@@ -208,11 +220,19 @@ uint32_t do_limit(rlo_engine* e, uint32_t d0, uint32_t d1, const uint8_t* blob, 
     }
     keys.push_back(std::move(d));
   }
+}
+
+// One request: fixedRateLimitCacheImpl.DoLimit, fixed_cache_impl.go:31-123, over the given
+// descriptors of the request (all of them, or one key shard's). Returns the request's
+// ThrottleMillis contribution.
+uint32_t do_limit(rlo_engine* e, const std::vector<Desc>& keys, const uint32_t* rule_id, int64_t now,
+                  uint32_t hits_addend, rlo_status* out) {
+  // hitsAddend := utils.Max(1, request.HitsAddend)  :39
+  const uint32_t h = umax(1u, hits_addend);
   // HOT LOOP 1 :55-86 — local-cache lookups for every descriptor precede any Set.
-  std::vector<char> local_hit(keys.size(), 0), skip(keys.size(), 0);
+  std::vector<char> local_hit(keys.size(), 0);
   std::vector<uint32_t> results(keys.size(), 0);
   for (size_t k = 0; k < keys.size(); ++k) {
-    if (!own(keys[k])) { skip[k] = 1; continue; }
     if (keys[k].key.empty()) continue;
     if (e->local_cache) {  // IsOverLimitWithLocalCache base_limiter.go:57-66
       auto it = e->lcache.find(keys[k].key);
@@ -224,7 +244,7 @@ uint32_t do_limit(rlo_engine* e, uint32_t d0, uint32_t d1, const uint8_t* blob, 
   // a missing or expired key counts as 0) into results[i] as uint32, then EXPIRE key div.
   for (int pass = 0; pass < 2; ++pass) {
     for (size_t k = 0; k < keys.size(); ++k) {
-      if (skip[k] || local_hit[k] || keys[k].key.empty()) continue;
+      if (local_hit[k] || keys[k].key.empty()) continue;
       const int store = (e->per_second_split && keys[k].per_second) ? 1 : 0;
       if (store != pass) continue;
       RKey& c = e->redis[store][keys[k].key];  // a new key is {0, 0}: expired
@@ -237,7 +257,6 @@ uint32_t do_limit(rlo_engine* e, uint32_t d0, uint32_t d1, const uint8_t* blob, 
   // HOT LOOP 2 :108-117
   uint32_t throttle_max = 0;
   for (size_t k = 0; k < keys.size(); ++k) {
-    if (skip[k]) continue;
     const uint32_t i = keys[k].i;
     const uint32_t r = rule_id[i];
     const bool has = !keys[k].key.empty();
@@ -266,18 +285,25 @@ int rlo_submit(rlo_engine* e, uint32_t n_desc, const uint8_t* prefix_blob, const
                const uint32_t* hits_addend, rlo_status* out, uint32_t* req_throttle_ms) {
   int rc = validate(e, n_desc, prefix_off, rule_id, req_of, n_req);
   if (rc) return rc;
-  for (uint32_t r = 0; r < n_req; ++r) req_throttle_ms[r] = 0;
+  merge_shards(e);
+  std::vector<Desc> keys;
   uint32_t d = 0;
   for (uint32_t r = 0; r < n_req; ++r) {
     uint32_t d1 = d;
     while (d1 < n_desc && req_of[d1] == r) ++d1;
-    req_throttle_ms[r] = do_limit(e, d, d1, prefix_blob, prefix_off, rule_id, now[r], hits_addend[r], out,
-                                  [](const Desc&) { return true; });
+    keys.clear();
+    build_keys(e, d, d1, prefix_blob, prefix_off, rule_id, now[r], keys);
+    req_throttle_ms[r] = do_limit(e, keys, rule_id, now[r], hits_addend[r], out);
     d = d1;
   }
   return 0;
 }
 
+// Key-sharded over n_threads host threads (the N-core CPU baseline): (1) threads build the
+// key strings of contiguous request ranges and partition the descriptors by key shard,
+// (2) each shard's thread applies its descriptors request by request in serial order with its
+// own Redis / local-cache shard. Per-key serial order is kept (a key lives in one shard), so the
+// outputs equal rlo_submit's.
 int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* prefix_blob,
                   const uint32_t* prefix_off, const uint32_t* rule_id, const uint32_t* req_of, uint32_t n_req,
                   const int64_t* now, const uint32_t* hits_addend, rlo_status* out, uint32_t* req_throttle_ms) {
@@ -286,49 +312,82 @@ int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* 
                       req_throttle_ms);
   int rc = validate(e, n_desc, prefix_off, rule_id, req_of, n_req);
   if (rc) return rc;
-  // Key-sharded: each thread owns keys with hash % n_threads == t and its own Redis /
-  // local-cache shard. Per-key serial order is kept, so outputs equal rlo_submit's.
   const int T = n_threads;
-  std::vector<rlo_engine*> shard(T);
+  std::hash<std::string> H;
+  // key k lives in shard H(k) % T; the shards persist across calls with the same T
+  if ((int)e->shards.size() != T) {
+    merge_shards(e);
+    e->shards.resize(T);
+    for (int t = 0; t < T; ++t) {
+      e->shards[t] = new rlo_engine();
+      e->shards[t]->near_ratio = e->near_ratio;
+      e->shards[t]->local_cache = e->local_cache;
+      e->shards[t]->per_second_split = e->per_second_split;
+    }
+    for (int s = 0; s < 2; ++s)
+      for (auto& kv : e->redis[s]) e->shards[H(kv.first) % T]->redis[s].emplace(kv.first, kv.second);
+    for (auto& kv : e->lcache) e->shards[H(kv.first) % T]->lcache.emplace(kv.first, kv.second);
+    e->redis[0].clear();
+    e->redis[1].clear();
+    e->lcache.clear();
+  }
+  std::vector<rlo_engine*>& shard = e->shards;
   for (int t = 0; t < T; ++t) {
-    shard[t] = new rlo_engine();
-    shard[t]->near_ratio = e->near_ratio;
-    shard[t]->local_cache = e->local_cache;
-    shard[t]->per_second_split = e->per_second_split;
     shard[t]->rules = e->rules;
     shard[t]->near_thr = e->near_thr;
   }
-  // Move existing state into shards.
-  std::hash<std::string> H;
-  for (int s = 0; s < 2; ++s)
-    for (auto& kv : e->redis[s]) shard[H(kv.first) % T]->redis[s].emplace(kv.first, kv.second);
-  for (auto& kv : e->lcache) shard[H(kv.first) % T]->lcache.emplace(kv.first, kv.second);
-  std::vector<std::vector<uint32_t>> thr(T, std::vector<uint32_t>(n_req, 0));
+  // (1) keys and shard lists per request range
+  struct Item { uint32_t req; Desc d; };
+  std::vector<std::vector<std::vector<Item>>> lists(T, std::vector<std::vector<Item>>(T));
+  std::vector<uint32_t> r_lo(T + 1);
+  for (int t = 0; t <= T; ++t) r_lo[t] = (uint32_t)((uint64_t)n_req * t / T);
+  std::vector<uint32_t> d_lo(T + 1, n_desc);
+  {
+    uint32_t d = 0;
+    for (int t = 0; t < T; ++t) {
+      while (d < n_desc && req_of[d] < r_lo[t]) ++d;
+      d_lo[t] = d;
+    }
+  }
   std::vector<std::thread> th;
   for (int t = 0; t < T; ++t) {
     th.emplace_back([&, t] {
-      uint32_t d = 0;
-      for (uint32_t r = 0; r < n_req; ++r) {
+      std::vector<Desc> keys;
+      uint32_t d = d_lo[t];
+      for (uint32_t r = r_lo[t]; r < r_lo[t + 1]; ++r) {
         uint32_t d1 = d;
         while (d1 < n_desc && req_of[d1] == r) ++d1;
-        // nil-limit descriptors (empty key) go to shard 0
-        thr[t][r] = do_limit(shard[t], d, d1, prefix_blob, prefix_off, rule_id, now[r], hits_addend[r], out,
-                             [&](const Desc& k) { return (int)(k.key.empty() ? 0 : H(k.key) % T) == t; });
+        keys.clear();
+        build_keys(e, d, d1, prefix_blob, prefix_off, rule_id, now[r], keys);
+        for (auto& k : keys) {
+          const int o = k.key.empty() ? 0 : (int)(H(k.key) % T);  // nil-limit descriptors go to shard 0
+          lists[t][o].push_back(Item{r, std::move(k)});
+        }
         d = d1;
       }
     });
   }
   for (auto& x : th) x.join();
-  e->redis[0].clear();
-  e->redis[1].clear();
-  e->lcache.clear();
-  for (int t = 0; t < T; ++t) {
-    for (int s = 0; s < 2; ++s) e->redis[s].insert(shard[t]->redis[s].begin(), shard[t]->redis[s].end());
-    e->lcache.insert(shard[t]->lcache.begin(), shard[t]->lcache.end());
-    e->lc_hit += shard[t]->lc_hit;
-    e->lc_miss += shard[t]->lc_miss;
-    delete shard[t];
+  th.clear();
+  // (2) every shard applies its descriptors, request by request, in serial order
+  std::vector<std::vector<uint32_t>> thr(T, std::vector<uint32_t>(n_req, 0));
+  for (int o = 0; o < T; ++o) {
+    th.emplace_back([&, o] {
+      std::vector<Desc> keys;
+      for (int t = 0; t < T; ++t) {
+        auto& L = lists[t][o];
+        for (size_t a = 0; a < L.size();) {
+          size_t b = a;
+          keys.clear();
+          while (b < L.size() && L[b].req == L[a].req) keys.push_back(std::move(L[b++].d));
+          const uint32_t r = L[a].req;
+          thr[o][r] = do_limit(shard[o], keys, rule_id, now[r], hits_addend[r], out);
+          a = b;
+        }
+      }
+    });
   }
+  for (auto& x : th) x.join();
   for (uint32_t r = 0; r < n_req; ++r) {
     uint32_t m = 0;
     for (int t = 0; t < T; ++t) m = thr[t][r] > m ? thr[t][r] : m;
@@ -338,6 +397,7 @@ int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* 
 }
 
 int64_t rlo_counter(rlo_engine* e, const char* key, uint32_t len, int per_second, int64_t now) {
+  merge_shards(e);
   const int s = (e->per_second_split && per_second) ? 1 : 0;
   auto it = e->redis[s].find(std::string(key, len));
   if (it == e->redis[s].end() || now >= it->second.exp) return -1;
@@ -345,13 +405,15 @@ int64_t rlo_counter(rlo_engine* e, const char* key, uint32_t len, int per_second
 }
 
 int rlo_local_cached(rlo_engine* e, const char* key, uint32_t len, int64_t now) {
+  merge_shards(e);
   auto it = e->lcache.find(std::string(key, len));
   return (it != e->lcache.end() && now < it->second) ? 1 : 0;
 }
 
-uint64_t rlo_num_keys(rlo_engine* e) { return e->redis[0].size() + e->redis[1].size(); }
+uint64_t rlo_num_keys(rlo_engine* e) { merge_shards(e); return e->redis[0].size() + e->redis[1].size(); }
 
 uint64_t rlo_num_strings(rlo_engine* e) {
+  merge_shards(e);
   std::unordered_set<std::string> u;
   for (int s = 0; s < 2; ++s)
     for (auto& kv : e->redis[s]) u.insert(kv.first);
@@ -360,6 +422,7 @@ uint64_t rlo_num_strings(rlo_engine* e) {
 }
 
 void rlo_local_cache_stats(rlo_engine* e, uint64_t* hit, uint64_t* miss, uint64_t* lookup, uint64_t* entries) {
+  merge_shards(e);
   *hit = e->lc_hit;
   *miss = e->lc_miss;
   *lookup = e->lc_hit + e->lc_miss;
