@@ -1,14 +1,13 @@
 #!/bin/bash
-# Build timing variants of the HIP library (tools only; not used by the product).
-# Usage: tools/build_variants.sh "NAME:-DFLAG ..." ...
+# Build timing / diagnostic variants of the HIP library (tools only; not used by the product).
+# Usage: tools/build_variants.sh "NAME:-DFLAG ..." ...   -> tools/variants/lib_NAME.so
 set -e
 cd "$(dirname "$0")/../api-ratelimit_amd/csrc"
 mkdir -p ../../tools/variants
-rm -f ../../tools/variants/lib_v_*.so
 for v in "$@"; do
   name=${v%%:*}; flags=${v#*:}
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I../../include -Wno-unused-result $flags -shared \
-     -o ../../tools/variants/lib_$name.so rl_kernels.hip rl_kernels_v2.hip rl_kernels_v3.hip rl_kernels_v4.hip rl_route.hip rl_resolve.hip rl_engine.cpp rl_cache.cpp -lpthread &
+     -o ../../tools/variants/lib_$name.so rl_kernels.hip rl_kernels_v4.hip rl_route.hip rl_resolve.hip rl_engine.cpp rl_cache.cpp -lpthread &
 done
 wait
 ls ../../tools/variants
