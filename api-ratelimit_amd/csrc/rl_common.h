@@ -178,10 +178,10 @@ constexpr int INS_CTR0 = 16;
 constexpr int INS_LINES = 8;
 
 // Per-block fingerprint partials: ~min / max home generation per region, nil count,
-// max unit window + 1 per (unit, window parity) (hot keys).
-constexpr int FP_GMIN = 0, FP_GMAX = 8, FP_NIL = 16, FP_UW = 17;
-constexpr int FP_PART_WORDS = 25;
-__host__ __device__ __forceinline__ bool fp_is_max(int w) { return w != FP_NIL; }
+// max unit window + 1 per (unit, window parity) (hot keys), descriptors per region.
+constexpr int FP_GMIN = 0, FP_GMAX = 8, FP_NIL = 16, FP_UW = 17, FP_CNT = 25;
+constexpr int FP_PART_WORDS = 33;
+__host__ __device__ __forceinline__ bool fp_is_max(int w) { return w < FP_NIL || (w >= FP_UW && w < FP_CNT); }
 
 // Counter table: 8 regions (home unit x window parity), region r has 2^region_log2[r] slots.
 struct TableDesc {

@@ -219,18 +219,18 @@ RL_DEV void exotic_sequence(KeyState& s, const TableDesc& tab, const DevRule* __
 }
 
 // Capacity check, before any table write: every region the batch touches must
-// stay within its load limit even if each of the batch's descriptors claimed a new slot in
-// it. Counts are per window generation: a newer generation finds the region empty (its older
-// slots are free for it). gmax: the batch's generation per region (0 = untouched); n: the
-// batch's non-nil descriptors.
+// stay within its load limit even if each of its descriptors in that region claimed a new
+// slot. Counts are per window generation: a newer generation finds the region empty (its
+// older slots are free for it). gmax / cnt: the batch's generation and descriptor count per
+// region (0 = untouched).
 RL_DEV uint32_t region_live(const RegionOcc& o, uint32_t gen) { return (o.gen < gen) ? 0u : o.live; }
-RL_DEV bool capacity_ok(const RegionOcc* __restrict__ occ, const uint32_t* gmax, uint32_t n) {
+RL_DEV bool capacity_ok(const RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* cnt) {
   bool ok = true;
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    if (!gmax[r]) continue;
+    if (!cnt[r]) continue;
     const RegionOcc o = occ[r];
-    ok &= (uint64_t)region_live(o, gmax[r]) + n <= (uint64_t)o.limit;
+    ok &= (uint64_t)region_live(o, gmax[r]) + cnt[r] <= (uint64_t)o.limit;
   }
   return ok;
 }

@@ -149,12 +149,14 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
   if (lane == 0 && nilmask) atomicAdd(&sh_f[FP_NIL], (uint32_t)__popcll(nilmask));
   for (uint32_t rg = 0; rg < 8; ++rg) {
     const bool mine = region == rg;
-    if (!__ballot(mine)) continue;
+    const uint64_t m = __ballot(mine);
+    if (!m) continue;
     const uint32_t mn = wave_min_u32(mine ? gen : 0xFFFFFFFFu);
     const uint32_t mx = wave_max_u32(mine ? gen : 0u);
     if (lane == 0) {
       atomicMax(&sh_f[FP_GMIN + rg], ~mn);
       atomicMax(&sh_f[FP_GMAX + rg], mx);
+      atomicAdd(&sh_f[FP_CNT + rg], (uint32_t)__popcll(m));
     }
   }
   if (err) atomicOr(&sh_err, err);
@@ -228,9 +230,12 @@ __global__ __launch_bounds__(256) void k_hist_scan(const uint32_t* __restrict__ 
     else if (tid < 16) ctl->gen_max[tid - 8] = shm[FP_GMAX + tid - 8][0];
     else if (tid == 16) ctl->n_nil = shm[FP_NIL][0];
     else if (tid == 17) {
-      uint32_t gmax[8];
-      for (int r = 0; r < 8; ++r) gmax[r] = shm[FP_GMAX + r][0];
-      if (!capacity_ok(occ, gmax, n_all - shm[FP_NIL][0])) atomicOr(&ctl->err, ERR_TABLE_FULL);
+      uint32_t gmax[8], cnt[8];
+      for (int r = 0; r < 8; ++r) {
+        gmax[r] = shm[FP_GMAX + r][0];
+        cnt[r] = shm[FP_CNT + r][0];
+      }
+      if (!capacity_ok(occ, gmax, cnt)) atomicOr(&ctl->err, ERR_TABLE_FULL);
     }
     return;
   }

@@ -88,7 +88,10 @@ __device__ uint64_t g_st4[4096][8];
 #define ST4X(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_st4[3072 + blockIdx.x][k] += (v); } while (0)
 // k4_scan blocks stamp rows 2048 + block (thread 0).
 #define ST5(k) do { if (threadIdx.x == 0) g_st4[2048 + blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// the last k4_group block's epilogue: row 4000
+#define STL(k) do { if (threadIdx.x == 0) g_st4[4000][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
+#define STL(k) do { } while (0)
 #define ST5(k) do { } while (0)
 #define ST4(k) do { } while (0)
 #define ST4V(k, v) do { } while (0)
@@ -189,23 +192,23 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   // hot descriptors. Reductions run only for regions / windows present in the wave.
 #pragma unroll
   for (int rg = 0; rg < 8; ++rg) {
-    uint32_t mn = 0xFFFFFFFFu, mx = 0;
-    uint64_t any_r = 0;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0, c = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const bool m = d[r].bucket < NIL_BUCKET && key_region(d[r].key) == (uint32_t)rg;
-      any_r |= __ballot(m);
+      c += (uint32_t)__popcll(__ballot(m));
       if (m) {
         mn = d[r].gen < mn ? d[r].gen : mn;
         mx = d[r].gen > mx ? d[r].gen : mx;
       }
     }
-    if (any_r) {  // wave-uniform
+    if (c) {  // wave-uniform
       mn = wave_min_u32(mn);
       mx = wave_max_u32(mx);
       if (lane == 0) {
         atomicMax(&sh_f[FP_GMIN + rg], ~mn);
         atomicMax(&sh_f[FP_GMAX + rg], mx);
+        atomicAdd(&sh_f[FP_CNT + rg], c);
       }
     }
     uint32_t um = 0;
@@ -507,7 +510,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     }
     // Capacity (before any table write): every hot block computes the same verdict and
     // claims nothing when it fails; block 0 refuses the batch.
-    cap_ok = capacity_ok(occ, &s_f[FP_GMAX], n_desc - s_f[FP_NIL]);
+    cap_ok = capacity_ok(occ, &s_f[FP_GMAX], &s_f[FP_CNT]);
     if (blockIdx.x == 0) {
       if (tid < 8) ctl->gen_min[tid] = ~s_f[FP_GMIN + tid];
       else if (tid < 16) ctl->gen_max[tid - 8] = s_f[FP_GMAX + tid - 8];
@@ -749,7 +752,7 @@ RL_DEV void gbar() {
 // differs from the first record's, CNT_MIXED_UNIT when its unit does too (found here, in
 // parallel, instead of by a walk of the key's list).
 constexpr uint32_t CNT_MASK = 0xFFFFu, CNT_MIXED = 0x10000u, CNT_MIXED_UNIT = 0x20000u;
-RL_DEV void g_insert(const GS& g, uint32_t k, const DevRule* __restrict__ rules) {
+RL_DEV bool g_insert(const GS& g, uint32_t k, const DevRule* __restrict__ rules) {
   const uint64_t key = g.rec[k].key, lo = g.rec[k].fp_lo;
   const uint32_t hmask = g.hs - 1u;
   uint32_t s = (uint32_t)key & hmask;
@@ -767,6 +770,7 @@ RL_DEV void g_insert(const GS& g, uint32_t k, const DevRule* __restrict__ rules)
   }
   if (inc == 1u) atomicAdd(&g.cnt[s], 1u);
   else atomicOr(&g.cnt[s], inc & ~1u), atomicAdd(&g.cnt[s], 1u);
+  return v == G_EMPTY;  // this position claimed the hash slot: it leads the key
 }
 
 // One wave: each key's list in position order (positions [0, m), 64 at a time).
@@ -894,13 +898,16 @@ RL_DEV void g_lead_exotic(const GS& g, uint32_t k, const DevRule* __restrict__ r
 // leaves per-position replies in P (SEG_EXOTIC). New slots are counted per region in ins[].
 RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, const TableDesc& tab, HotCand* cand,
                    EngineCtl* ctl, bool has_pre, const SlotView& pre, int cand_on, uint32_t& heads, uint64_t& ins) {
+  // k: the position that claimed the key's hash slot (any record of the key); the key's
+  // results go to its last record (tail), where the decisions read them
   const uint64_t key = g.rec[k].key, lo = g.rec[k].fp_lo;
   const uint32_t rule = rule_of(g.rec[k].rn);
   const uint32_t s = g.grp[k];
   const uint32_t cw = g.cnt[s];
   const uint32_t n = cw & CNT_MASK, e1 = g.end[s], e0 = e1 - n;
+  const uint32_t tail = g.list[e1 - 1];
   const bool mixed = (cw & CNT_MIXED) != 0, mixed_unit = (cw & CNT_MIXED_UNIT) != 0;
-  const uint64_t Pk = g.P[k];
+  const uint64_t Pk = g.P[tail];
   const DevRule R0 = rules[rule];
   heads += 1;
   if (cand_on && n >= HOT_MIN_SEG && !mixed) emit_cand_sc1(ctl, cand, rule, n, g.rec[g.list[e0]].idx);
@@ -914,8 +921,8 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
                                : table_claim(tab, key, lo, gen, slot, existed);
   if (!claimed) {
     atomicOr(&ctl->err, ERR_TABLE_FULL);  // unreachable below the load limit
-    g.rec[k].key = 0;
-    g.rec[k].fp_lo = SEG_NO_FREEZE;
+    g.rec[tail].key = 0;
+    g.rec[tail].fp_lo = SEG_NO_FREEZE;
     return;
   }
   if (existed && !has_pre) ks = read_state(slot);
@@ -929,13 +936,13 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
   bool frozen_pre = false;
   if (mixed_unit || !fast_state(ks, ps, tab.local_cache != 0, ws, R0.div, base, frozen_pre)) {
     // exact sequential path, in a pass of its own after the leaders (g_lead_exotic)
-    g.rec[k].key = (uint64_t)(uintptr_t)slot;
-    g.rec[k].fp_lo = SEG_EXOTIC_PENDING;
+    g.rec[tail].key = (uint64_t)(uintptr_t)slot;
+    g.rec[tail].fp_lo = SEG_EXOTIC_PENDING;
     return;
   }
   uint32_t freeze = SEG_NO_FREEZE;
   uint64_t final_count = base + Pk;
-  uint32_t last = k;  // the key's last record whose INCRBY happens
+  uint32_t last = tail;  // the key's last record whose INCRBY happens
   if (frozen_pre) {
     freeze = SEG_FROZEN_BEFORE;  // every descriptor is a local-cache hit: no INCRBY
   } else if (tab.local_cache) {
@@ -978,8 +985,8 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
     if (freeze != SEG_NO_FREEZE) ks.frz = t_last + R0.div;  // freecache TTL (base_limiter.go:102)
     write_state(slot, ks);
   }
-  g.rec[k].key = base;
-  g.rec[k].fp_lo = freeze;
+  g.rec[tail].key = base;
+  g.rec[tail].fp_lo = freeze;
 }
 
 // All phases of one staged range of m records (whole keys). Returns the keys led (low 16
@@ -990,17 +997,23 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
                             int routed, LSeg* s_agg, LSeg* s_carry, uint32_t* sh_w, uint64_t& ins, EngineCtl* ctl) {
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
   uint32_t heads = 0;
-  // The staging (and the hash-table reset before it) is complete: read each position's first
-  // table slot ahead, so the leaders' probes overlap the grouping.
+  // Insert every position into the LDS hash; the position that claims a key's hash slot leads
+  // the key and reads its first table slot right away, so the leader's probe overlaps the
+  // grouping (one table read-ahead per key, not per record).
+  constexpr int KPT = (BUCKET_CAP + G_NT - 1) / G_NT;  // positions per thread (global path)
+  static_assert(KPT <= 8 && G_IPT <= KPT, "owner bits");
+  uint32_t own = 0;  // bit j: position tid + j * G_NT leads its key
   SlotView pre[G_IPT];
-  if constexpr (LDS) {
 #pragma unroll
-    for (int j = 0; j < G_IPT; ++j) {
-      const uint32_t k = tid + j * G_NT;
-      if (k < m) pre[j] = load_slot(slot_first(tab, g.rec[k].key));
+  for (int j = 0; j < KPT; ++j) {
+    const uint32_t k = tid + j * G_NT;
+    if (k < m && g_insert(g, k, rules)) {
+      own |= 1u << j;
+      if constexpr (LDS) {
+        if (j < G_IPT) pre[j] = load_slot(slot_first(tab, g.rec[k].key));
+      }
     }
   }
-  for (uint32_t k = tid; k < m; k += G_NT) g_insert(g, k, rules);
   gbar<LDS>();
   ST4(1);
   // each key's list start: exclusive prefix of the per-slot counts (hash-slot order)
@@ -1025,14 +1038,12 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
   ST4(3);
   if constexpr (LDS) {
 #pragma unroll
-    for (int j = 0; j < G_IPT; ++j) {
-      const uint32_t k = tid + j * G_NT;
-      if (k < m && g_tail(g, k) == k)
-        g_lead(g, k, rules, tab, cand, ctl, true, pre[j], cand_on, heads, ins);
-    }
+    for (int j = 0; j < G_IPT; ++j)
+      if ((own >> j) & 1u) g_lead(g, tid + j * G_NT, rules, tab, cand, ctl, true, pre[j], cand_on, heads, ins);
   } else {
-    for (uint32_t k = tid; k < m; k += G_NT)
-      if (g_tail(g, k) == k) g_lead(g, k, rules, tab, cand, ctl, false, SlotView{}, cand_on, heads, ins);
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      if ((own >> j) & 1u) g_lead(g, tid + j * G_NT, rules, tab, cand, ctl, false, SlotView{}, cand_on, heads, ins);
   }
   __threadfence_block();
   __syncthreads();
@@ -1238,6 +1249,19 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
   }
   __syncthreads();
   ST4(0);
+  if (s_err == 0 && j < (uint32_t)(HOT_BUCKETS / G_NT)) {
+    // Hot keys (decided by k4_place): EXPIRE and freecache TTLs from the time of the last
+    // INCRBY / of the freezing request (fixed_cache_impl.go:69-72, base_limiter.go:102). The
+    // deferred hot descriptors below only raise the counter word.
+    const HotBucket x = hb[j * G_NT + tid];
+    if (x.slot && !(x.flags & HB_FROZEN_PRE)) {
+      Slot* sl = reinterpret_cast<Slot*>(x.slot);
+      const uint32_t div = rules[x.rule].div;
+      const bool frozen = x.rstar != 0xFFFFFFFFu;
+      if (!(x.flags & HB_PS)) sl->exp = (frozen ? x.t_rstar : x.t_all) + div;
+      if (frozen) sl->frz = x.t_rstar + div;
+    }
+  }
   if (s_err == 0) {
     // Hot descriptors of a request that began before the tile where their key froze
     // (k4_place, a previous launch, recorded them and the freezing requests).
@@ -1384,6 +1408,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
   }
   __syncthreads();
   if (!s_last) return;
+  STL(0);
   // U = Σ per-block unique-key counts (this kernel and k4_scan's hot leaders); new slots per
   // region into the occupancy counts (only for a batch that was applied)
   if (tid == 0) s_heads = 0;
@@ -1424,31 +1449,29 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
     }
   }
   __syncthreads();
-  if (tid == 0) {
+  if (tid < 8) {
+    // one thread per region; also for a refused batch: its hot keys may have claimed slots in
+    // k4_scan before the refusal (they hold the empty state; the rerun finds them)
+    const uint32_t r = tid, g = ctl->gen_max[r];
+    ctl->ins[r] = s_ins[r];
+    if (g) {
+      RegionOcc o = occ[r];
+      if (o.gen < g) {
+        o.gen = g;
+        o.live = s_ins[r];
+      } else {
+        o.live += s_ins[r];
+      }
+      occ[r] = o;
+    }
+  }
+  if (tid == 8) {
     ctl->n_segments = s_heads;
     uint32_t n = 0;
-    for (int r = 0; r < 8; ++r) {
-      ctl->ins[r] = s_ins[r];
-      n += s_ins[r];
-    }
+    for (int r = 0; r < 8; ++r) n += s_ins[r];
     ctl->n_inserted = n;
-    // also for a refused batch: its hot keys may have claimed slots in k4_scan before the
-    // refusal (they hold the empty state; the rerun finds them)
-    occ_update(occ, ctl->gen_max, s_ins);
   }
-  // Hot keys: EXPIRE and freecache TTLs from the time of the last INCRBY / the freezing
-  // request (fixed_cache_impl.go:69-72, base_limiter.go:102)
-  if (s_err == 0) {
-    for (uint32_t b = tid; b < (uint32_t)HOT_BUCKETS; b += G_NT) {
-      const HotBucket x = hb[b];
-      if (!x.slot || (x.flags & HB_FROZEN_PRE)) continue;
-      Slot* sl = reinterpret_cast<Slot*>(x.slot);
-      const uint32_t div = rules[x.rule].div;
-      const bool frozen = x.rstar != 0xFFFFFFFFu;
-      if (!(x.flags & HB_PS)) sl->exp = (frozen ? x.t_rstar : x.t_all) + div;
-      if (frozen) sl->frz = x.t_rstar + div;
-    }
-  }
+  STL(1);
   // hot-set candidates found by leaders: their key-prefix state
   const uint32_t nc = min((uint32_t)CAND_MAX, ld_relaxed(&ctl->tile_ctr[CAND_CTR][0]));
   for (uint32_t i = tid; i < nc; i += G_NT) {
@@ -1471,7 +1494,9 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
   }
   uint32_t* z = reinterpret_cast<uint32_t*>(next_ctl);
   constexpr uint32_t words = sizeof(EngineCtl) / 4;
+  STL(2);
   for (uint32_t w = tid; w < words; w += G_NT) z[w] = 0;
+  STL(3);
 }
 
 }  // namespace v4

@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--json-out", type=str, default="")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight through rl_submit_pipelined (2..3)")
     ap.add_argument("--serial", action="store_true", help="one batch in flight (rl_submit_device + rl_wait)")
+    ap.add_argument("--lib", type=str, default="", help=argparse.SUPPRESS)  # diagnostics: a variant library
+    ap.add_argument("--dump-stamps", type=str, default="", help=argparse.SUPPRESS)  # -DRL_STAMPS variant: raw stamps
     return ap.parse_args()
 
 
@@ -233,7 +235,8 @@ def main():
     # an owner may receive up to every origin's batch (hot keys concentrate on their owner)
     cap = d * world if routed else d
     eng = hiprl.Engine(device=local, log2_slots=log2, max_batch_desc=cap, max_batch_req=cap,
-                       max_blob_bytes=cap * 17 + 64, sort_bits=48, pipeline=args.pipeline)
+                       max_blob_bytes=cap * 17 + 64, sort_bits=48, pipeline=args.pipeline,
+                       lib_path=(ROOT / args.lib) if args.lib else None)
     eng.load_rules(rules)
     gen = DeviceGen(args.config, d, seed, K, dev)
     rtr = router.ShardRouter(router.EngineShard(eng, rank, world, dev, d)) if routed else None
@@ -327,6 +330,11 @@ def main():
         kernel = {k: dict(total_ms=v[0], launches=v[1]) for k, v in kt.items() if v[1]}
     if not uniq:
         uniq = [eng.last_batch_info()["unique_keys"]]
+    if args.dump_stamps:  # diagnostic build: per-block phase stamps of the last batch
+        st4 = np.zeros((4096, 8), np.uint64)
+        eng.lib.rl_debug_st4.argtypes = [C.c_void_p]
+        eng.lib.rl_debug_st4(st4.ctypes.data)
+        np.save(args.dump_stamps, st4)
     stats = eng.stats()
     occ = eng.occupancy()
 
