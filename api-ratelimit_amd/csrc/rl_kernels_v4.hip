@@ -90,7 +90,10 @@ __device__ uint64_t g_st4[4096][8];
 #define ST5(k) do { if (threadIdx.x == 0) g_st4[2048 + blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 // the last k4_group block's epilogue: row 4000
 #define STL(k) do { if (threadIdx.x == 0) g_st4[4000][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+// k4_hist tiles: rows 1024 + tile
+#define STH(k) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_st4[1024 + blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
+#define STH(k) do { } while (0)
 #define STL(k) do { } while (0)
 #define ST5(k) do { } while (0)
 #define ST4(k) do { } while (0)
@@ -160,6 +163,7 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t tile = blockIdx.x, ntiles = gridDim.x;
   const uint32_t t0 = tile * T;
+  STH(0);
   tile::load_hot_table(hot, sh_hot);
   for (int b = tid; b < ROW / 2; b += NT) reinterpret_cast<uint32_t*>(sh_cnt)[b] = 0;
   for (int b = tid; b < HOT_BUCKETS; b += NT) sh_hs[b] = 0;
@@ -172,12 +176,14 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
     for (uint32_t q = r0 + tid; q < r1; q += NT) req_thr[q] = 0;
   }
   __syncthreads();
+  STH(1);
   D3 d[R];
   uint32_t err = 0;
   if (ROUTED)
     tile::load_routed(in, rules, n_rules, sh_hot, t0, d, err);
   else
     tile::load_descs(in, rules, n_rules, seed, sh_hot, t0, d, err);
+  STH(2);
   uint32_t nil = 0;
 #pragma unroll
   for (int r = 0; r < R; ++r) {
@@ -230,8 +236,11 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   // Stable sort of the tile by bucket, then a segmented scan in sorted order:
   // hot -> inclusive prefix of h inside (tile, bucket); each bucket's last descriptor ->
   // the bucket's count (and h sum) in this tile.
+  STH(3);
   tile::tile_digit_pass(s_d, s_pa, s_pb, 0, s_cnt, sh_w);  // includes barriers
+  STH(4);
   tile::tile_digit_pass(s_d, s_pb, s_pa, 6, s_cnt, sh_w);
+  STH(5);
   {
     const uint32_t s0 = tid * R;
     uint32_t od[R], dd[R], fl[R];
@@ -306,6 +315,7 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
       run += v[k];
     }
   }
+  STH(6);
   // Records in bucket order. A hot record carries its in-tile INCRBY prefix and its bucket;
   // an MSD record its sort key and fp_lo; a nil-limit descriptor is decided here.
 #pragma unroll
@@ -342,6 +352,8 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   for (int b = tid; b < HOT_BUCKETS; b += NT) hrow[b] = sh_hs[b];
   if (tid < FP_PART_WORDS) fpart[(size_t)tile * FP_PART_WORDS + tid] = sh_f[tid];
   if (tid == 0 && sh_err) atomicOr(&ctl->err, sh_err);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  STH(7);
 }
 
 // ---------------------------------------------------------------------------

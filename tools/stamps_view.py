@@ -24,3 +24,15 @@ s5 = st[2048:2048 + 96]
 s5 = s5[s5[:, 0] > 0]
 if len(s5):
     print(f"k4_scan: {len(s5)} blocks, entry..end {(s5[:, 0].min() - t0) / 100:.1f}..{(s5[:, 4].max() - t0) / 100:.1f} us (k4_group t0)")
+h = st[1024:2048]
+h = h[h[:, 7] > 0]
+if len(h):
+    t0h = h[:, 0].min()
+    rel = (h - t0h) / 100.0
+    nm = ["entry", "hot table", "descs+hash", "partials", "digit pass 1", "digit pass 2", "scan+starts", "written"]
+    print(f"k4_hist {len(h)} tiles; entry spread {rel[:, 0].max():.1f} us, last end {rel[:, 7].max():.1f} us, "
+          f"end p50 {np.median(rel[:, 7]):.1f}")
+    dd = np.diff(rel, axis=1)
+    for j in range(7):
+        print(f"   {nm[j]:>12s}->{nm[j + 1]:<12s} median {np.median(dd[:, j]):6.2f}  p90 {np.percentile(dd[:, j], 90):6.2f}"
+              f"  max {dd[:, j].max():6.2f}")
