@@ -745,6 +745,9 @@ int rl_engine::check_batch(const rl_batch* b, bool host) {
   if (b->reserved) return fail(RL_EINVAL, "rl_batch.reserved must be 0");
   if (b->n_desc && (!b->prefix_off || !b->rule_id || !b->req_of)) return fail(RL_EINVAL, "null descriptor array");
   if (b->n_req && (!b->now || !b->hits_addend)) return fail(RL_EINVAL, "null request array");
+  if (b->n_desc && !b->n_req) return fail(RL_EINVAL, "descriptors without requests");
+  if (b->n_desc && !b->prefix_blob && (!host || b->blob_bytes))
+    return fail(RL_EINVAL, "null prefix_blob (a device blob must be readable even when empty)");
   if (!d_rules) {
     int rc = rl_load_rules(this, nullptr, 0);
     if (rc) return rc;
@@ -858,7 +861,7 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   if (he == hipSuccess) chk(hipMemcpy(e->d_occ, e->occ, sizeof e->occ, hipMemcpyHostToDevice));
   const size_t N = c.max_batch_desc, R = c.max_batch_req, B = c.max_blob_bytes;
   // host staging: blob | off | rule | req | now | hits (same layout on host and device)
-  e->o_off = align_up(B + 16, 256);
+  e->o_off = align_up(B + RL_BLOB_SLACK, 256);
   e->o_rule = e->o_off + align_up((N + 1) * 4, 256);
   e->o_req = e->o_rule + align_up(N * 4, 256);
   e->o_now = e->o_req + align_up(N * 4, 256);
@@ -1058,12 +1061,12 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
       {b->now, e->o_now, (size_t)b->n_req * 8}, {b->hits_addend, e->o_hits, (size_t)b->n_req * 4}};
   for (auto& a : arrs)
     if (a.n && a.src != h + a.o) memcpy(h + a.o, a.src, a.n);
-  memset(h + b->blob_bytes, 0, 16);  // slack for the device's 16-B word reads
+  memset(h + b->blob_bytes, 0, RL_BLOB_SLACK);  // the device reads prefixes in 16-B words
   e->acquired = -1;
   hipError_t he = hipSuccess;
   // Copy only the used extents of each array, on the copy-in stream: the previous batch's
   // kernels keep running meanwhile.
-  const size_t ext[] = {(size_t)b->blob_bytes + 16, arrs[1].n, arrs[2].n, arrs[3].n, arrs[4].n, arrs[5].n};
+  const size_t ext[] = {(size_t)b->blob_bytes + RL_BLOB_SLACK, arrs[1].n, arrs[2].n, arrs[3].n, arrs[4].n, arrs[5].n};
   for (int k = 0; k < 6 && he == hipSuccess; ++k)
     if (ext[k]) he = hipMemcpyAsync(g.d_in + arrs[k].o, h + arrs[k].o, ext[k], hipMemcpyHostToDevice, e->xin);
   if (he == hipSuccess) he = hipEventRecord(e->ev_in[s], e->xin);

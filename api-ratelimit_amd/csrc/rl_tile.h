@@ -107,6 +107,27 @@ RL_DEV void hash_tail(const uint32_t* p, uint32_t d0, uint32_t sh, uint32_t rem,
   }
 }
 
+// Words of a prefix beyond the preloaded dwords, 32 bytes (three words) per pair of 16-B
+// loads. p = dword holding the next word's first byte; the blob is readable 32 B past its end.
+RL_DEV void hash_tail32(const uint32_t* p, uint32_t sh, uint32_t rem, FpState& s) {
+  while (rem > 0) {
+    const u32x4 x0 = *reinterpret_cast<const u32x4*>(p), x1 = *reinterpret_cast<const u32x4*>(p + 4);
+    const uint32_t dw[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (rem > 0) {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(dw[2 * k + 1], dw[2 * k], sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(dw[2 * k + 2], dw[2 * k + 1], sh);
+        uint64_t w = ((uint64_t)hi << 32) | lo;
+        if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
+        fp_word(s, w);
+        rem = rem > 8 ? rem - 8 : 0;
+      }
+    }
+    p += 6;
+  }
+}
+
 // Prefix state (lanes a, b) of a byte string, reading only dwords that overlap it.
 RL_DEV FpState prefix_state(const uint8_t* blob, uint32_t off, uint32_t len, uint64_t seed) {
   FpState s = fp_init(len, seed);
@@ -147,73 +168,57 @@ RL_DEV void key_of(D3& x, const FpState& s, int64_t now, const DevRule& rr, cons
 
 RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, uint32_t n_rules, uint64_t seed,
                        const HotEntry* sh_hot, uint32_t t0, D3 (&d)[R], uint32_t& err) {
+  // Every load is unconditional at a clamped index, so each of the two dependent levels (the
+  // descriptor arrays; then now / hits / the rule / the prefix's first 32 bytes) issues as one
+  // run of loads and waits once. A load behind a per-lane condition made the compiler wait
+  // after each one. Clamped reads stay inside the arrays (n_desc >= 1 here: a tile exists only
+  // for a non-empty batch; n_req >= 1 and the rule table holds >= 1 entry, both host-checked)
+  // and inside the blob's 32 readable bytes of slack (rl_hip.h, rl_batch.prefix_blob).
   const uint32_t tid = threadIdx.x;
-  uint32_t rl[R], q[R], o0[R], len[R];
-  bool lay[R];
+  const uint32_t last = in.n_desc - 1u;
+  uint32_t rl[R], q[R], qp[R], oa[R], ob[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const uint32_t i = t0 + r * NT + tid;
-    const bool v = i < in.n_desc;
-    rl[r] = v ? in.rule[i] : RL_NIL_RULE;
-    q[r] = v ? in.req_of[i] : 0u;
-    const uint32_t qp = (v && i > 0) ? in.req_of[i - 1] : 0u;
-    const uint32_t a = v ? in.off[i] : 0u;
-    const uint32_t b = v ? in.off[i + 1] : 0u;
-    // batch layout checks (the device validates every submit form): prefix offsets in order
-    // and inside the blob, request indices non-decreasing
-    lay[r] = a <= b && b <= in.blob_bytes && qp <= q[r];
-    if (v && !lay[r]) err |= ERR_BAD_INPUT;
-    o0[r] = a;
-    len[r] = lay[r] ? b - a : 0u;
+    const uint32_t i = min(t0 + r * NT + tid, last);
+    rl[r] = in.rule[i];
+    q[r] = in.req_of[i];
+    qp[r] = in.req_of[i ? i - 1u : 0u];
+    oa[r] = in.off[i];
+    ob[r] = in.off[i + 1u];
   }
-  const uint32_t lim = (in.blob_bytes + 3u) & ~3u;
+  uint32_t o0[R], len[R];
+  bool ok[R];
   int64_t now[R];
   uint32_t ha[R];
   DevRule rr[R];
-  bool ok[R];
-  uint32_t dw[R][PRE_DW];
+  u32x4 w0[R], w1[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    const uint32_t i = t0 + r * NT + tid;
-    const bool v = i < in.n_desc;
-    const bool q_ok = q[r] < in.n_req;
-    ok[r] = v && rl[r] != RL_NIL_RULE && rl[r] < n_rules && q_ok && lay[r];
-    if (v && rl[r] != RL_NIL_RULE && (rl[r] >= n_rules || !q_ok)) err |= ERR_BAD_INPUT;
-    now[r] = (v && q_ok) ? in.now[q[r]] : 0;
-    ha[r] = (v && q_ok) ? in.hits[q[r]] : 1u;
-    if (ok[r]) {
-      rr[r] = rules[rl[r]];
-    } else {
-      rr[r].L = rr[r].near = 0;
-      rr[r].div = 1;
-      rr[r].unit = RL_UNIT_SECOND;
-    }
-    const uint32_t a = o0[r] & ~3u;
-    const uint32_t need = ok[r] ? (((o0[r] & 3u) + len[r] + 3u) & ~3u) : 0u;  // bytes from a
-#pragma unroll
-    for (int c = 0; c < PRE_DW / 4; ++c) {
-      const uint32_t cb = a + 16u * c;
-      if (16u * c < need && cb + 16u <= lim) {
-        const u32x4 x = *reinterpret_cast<const u32x4*>(in.blob + cb);
-        dw[r][4 * c] = x.x;
-        dw[r][4 * c + 1] = x.y;
-        dw[r][4 * c + 2] = x.z;
-        dw[r][4 * c + 3] = x.w;
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          dw[r][4 * c + k] =
-              16u * c + 4u * k < need ? *reinterpret_cast<const uint32_t*>(in.blob + cb + 4u * k) : 0u;
-      }
-    }
+    const bool v = t0 + r * NT + tid < in.n_desc;
+    // batch layout checks (the device validates every submit form): prefix offsets in order
+    // and inside the blob, request indices non-decreasing and in range, known rule ids
+    const bool lay = oa[r] <= ob[r] && ob[r] <= in.blob_bytes && qp[r] <= q[r];
+    const bool q_ok = q[r] < in.n_req, rule_ok = rl[r] < n_rules, nil = rl[r] == RL_NIL_RULE;
+    if (v && (!lay || (!nil && (!rule_ok || !q_ok)))) err |= ERR_BAD_INPUT;
+    ok[r] = v && !nil && rule_ok && q_ok && lay;
+    o0[r] = ok[r] ? oa[r] : 0u;
+    len[r] = ok[r] ? ob[r] - oa[r] : 0u;
+    const uint32_t qc = q_ok ? q[r] : 0u;
+    now[r] = in.now[qc];
+    ha[r] = in.hits[qc];
+    rr[r] = rules[rule_ok ? rl[r] : 0u];
+    const u32x4* p = reinterpret_cast<const u32x4*>(in.blob + (o0[r] & ~3u));
+    w0[r] = p[0];
+    w1[r] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint32_t*>(p) + 4);
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint32_t i = t0 + r * NT + tid;
     D3& x = d[r];
-    x.req = q[r];
-    x.rule = rl[r];
-    x.h = ha[r] > 1u ? ha[r] : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
+    x.req = i < in.n_desc ? q[r] : 0u;
+    x.rule = i < in.n_desc ? rl[r] : RL_NIL_RULE;
+    // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
+    x.h = i < in.n_desc && q[r] < in.n_req && ha[r] > 1u ? ha[r] : 1u;
     x.now_mod = 0;
     x.gen = 0;
     x.uw = 8;
@@ -226,14 +231,15 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
       err |= ERR_BAD_TIME;
       continue;
     }
+    const uint32_t dw[PRE_DW + 1] = {w0[r].x, w0[r].y, w0[r].z, w0[r].w, w1[r].x, w1[r].y, w1[r].z, w1[r].w, 0u};
     const uint32_t sh = o0[r] & 3u;
     FpState s = fp_init(len[r], seed);
     uint32_t rem = len[r];
 #pragma unroll
     for (int k = 0; k < (PRE_DW - 1) / 2; ++k) {
       if (rem > 0) {
-        const uint32_t lo = __builtin_amdgcn_alignbyte(dw[r][2 * k + 1], dw[r][2 * k], sh);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(dw[r][2 * k + 2], dw[r][2 * k + 1], sh);
+        const uint32_t lo = __builtin_amdgcn_alignbyte(dw[2 * k + 1], dw[2 * k], sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(dw[2 * k + 2], dw[2 * k + 1], sh);
         uint64_t w = ((uint64_t)hi << 32) | lo;
         if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
         fp_word(s, w);
@@ -241,8 +247,7 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
       }
     }
     constexpr int DONE_DW = 2 * ((PRE_DW - 1) / 2);  // dword holding the next word's first byte
-    if (rem)
-      hash_tail(reinterpret_cast<const uint32_t*>(in.blob + (o0[r] & ~3u)) + DONE_DW, dw[r][DONE_DW], sh, rem, s);
+    if (rem) hash_tail32(reinterpret_cast<const uint32_t*>(in.blob + (o0[r] & ~3u)) + DONE_DW, sh, rem, s);
     key_of(x, s, now[r], rr[r], sh_hot, err);
   }
 }

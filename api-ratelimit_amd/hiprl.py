@@ -70,6 +70,7 @@ class RlResolveBatch(C.Structure):
 
 
 TREE_ROOT = 0xFFFFFFFF
+BLOB_SLACK = 32  # RL_BLOB_SLACK: a device prefix_blob is readable this many bytes past its end
 MAX_IN_FLIGHT = 3  # RL_MAX_IN_FLIGHT: batches in flight at once through rl_submit_pipelined
 
 

@@ -58,8 +58,8 @@ class DeviceBatch:
         import numpy as np
 
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
-        # the device path reads prefix bytes as 16-B loads: keep 16 B of slack past the end
-        blob = np.zeros(int(b.blob.shape[0]) + 16, np.uint8)
+        # the device reads prefix bytes as 16-B loads: the blob is readable RL_BLOB_SLACK bytes past its end
+        blob = np.zeros(int(b.blob.shape[0]) + hiprl.BLOB_SLACK, np.uint8)
         blob[:b.blob.shape[0]] = b.blob
         return cls(t(blob), t(b.off.view(np.int32)), t(b.rule.view(np.int32)), t(b.req_of.view(np.int32)),
                    t(b.now), t(b.hits.view(np.int32)), int(b.off[-1]))

@@ -165,15 +165,16 @@ def pmc_traffic(dom: str):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc summary,
     only if it was measured on these exact kernel sources."""
     if not PMC_SUMMARY.exists():
-        return None, "no PMC summary committed"
+        return None, "no PMC summary committed", None
     try:
         pm = json.loads(PMC_SUMMARY.read_text())
     except Exception as ex:  # noqa: BLE001
-        return None, f"unreadable PMC summary: {ex}"
+        return None, f"unreadable PMC summary: {ex}", None
     if pm.get("source_sha") != source_sha():
-        return None, f"PMC summary {PMC_SUMMARY.name} is for other kernel sources ({pm.get('source_sha')})"
+        return None, f"PMC summary {PMC_SUMMARY.name} is for other kernel sources ({pm.get('source_sha')})", None
     k = pm.get("kernels", {}).get(dom)
-    return (k or {}).get("hbm_bytes_per_launch"), f"{PMC_SUMMARY.name} (source {pm['source_sha']})"
+    return ((k or {}).get("hbm_bytes_per_launch"), f"{PMC_SUMMARY.name} (source {pm['source_sha']})",
+            pm.get("hbm_bytes_per_batch"))
 
 
 def cpu_baseline(args, rules, d, seed, K, b0):
@@ -402,11 +403,13 @@ def main():
         # figure x the descriptors one launch processes): every kernel of a batch handles all of
         # its descriptors, so each launch is held to the whole batch's bytes.
         achieved = alg_bytes / (dom_us * 1e-6) / 1e9
-        traffic, tsrc = pmc_traffic(dom)
+        traffic, tsrc, traffic_batch = pmc_traffic(dom)
         roofline = {
             "bound": "hbm", "kernel": dom,
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+            "traffic_per_batch": traffic_batch,
+            "traffic_over_algorithmic": round(traffic_batch / alg_bytes, 3) if traffic_batch else None,
             "algorithmic_bytes_per_batch": alg_bytes, "unique_keys_per_batch": int(U),
             "dominant_kernel_avg_us": round(dom_us, 2),
             "pipeline_us_per_batch": round(pipe_ms * 1e3, 2),

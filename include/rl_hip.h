@@ -92,7 +92,12 @@ typedef struct rl_rule {
  *   domain '_' key1 '_' value1 '_' ... keyN '_' valueN '_'
  * of GenerateCacheKey (src/limiter/cache_key.go:57-65) without the window timestamp, which
  * the device appends (cache_key.go:66-68): bytes prefix_blob[prefix_off[i] .. prefix_off[i+1]).
- * The same struct carries host pointers (rl_submit) or device pointers (rl_submit_device). */
+ * The same struct carries host pointers (rl_submit) or device pointers (rl_submit_device).
+ * A device prefix_blob must be readable (not meaningful) for RL_BLOB_SLACK bytes past
+ * blob_bytes, non-null even when every prefix is empty: the device reads prefixes in 16-B
+ * words. Host batches need no slack (rl_submit stages them with it). A batch with
+ * descriptors has at least one request. */
+#define RL_BLOB_SLACK 32
 typedef struct rl_batch {
   uint32_t n_desc;
   uint32_t n_req;

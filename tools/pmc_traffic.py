@@ -1,47 +1,75 @@
-"""HBM traffic per batch from rocprofv3 --pmc passes (tools/profile_round.sh output).
+"""Per-kernel HBM traffic from rocprofv3 --pmc passes (tools/pmc_round.sh output).
 
-FETCH_SIZE / WRITE_SIZE are in KiB per dispatch. Per MI355X_MICROARCH.md §HBM, gfx950's
-FETCH_SIZE counts half of the bytes of a wide coalesced read (TCC_EA0_RDREQ x 64 B for
-128-B requests), so the read side is reported raw and x2-corrected; WRITE_SIZE is exact
-for 16-B-per-lane stores and uncalibrated for narrower ones."""
+usage: pmc_traffic.py <pmc dir> <out.json> <timed steps> [tag]
+
+Only the last <timed steps> dispatches of each kernel are used: the bench's timed region
+(prefill and warmup dispatches run at other table fills and are skipped). FETCH_SIZE and
+WRITE_SIZE are KiB per dispatch. Per MI355X_MICROARCH.md §HBM, gfx950's FETCH_SIZE counts half
+the bytes of a wide coalesced read, so hbm_bytes_per_launch = 2 x FETCH + WRITE. Random 32-B
+slot traffic is calibrated separately on tools/microbench/table_rmw (random 32-B probe reads
+and 32-B read-modify-writes of known count on an 8 GiB table): the calibration block reports
+counter bytes per operation for those access shapes, so the reader can see how the counters
+tally the table's random accesses. The summary carries bench.source_sha(), so bench.py uses
+it only for the kernel sources it was measured on."""
 import collections
 import csv
 import glob
 import json
+import os
 import sys
 
-root, out = sys.argv[1], sys.argv[2]
-steps = int(sys.argv[3]) if len(sys.argv) > 3 else 7  # warmup + steps of the pmc runs
-vals = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob(f"{root}/p*/run_counter_collection.csv"):
-    for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].split("::")[-1].replace("void ", "")
-        vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-per_kernel = {}
-fetch_raw = write = 0.0
-for k, c in vals.items():
-    if not k.startswith(("k_", "k3_", "k4_")):
+root, out, steps = sys.argv[1], sys.argv[2], int(sys.argv[3])
+tag = sys.argv[4] if len(sys.argv) > 4 else ""
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from bench import source_sha  # noqa: E402
+
+
+def load(pattern):
+    """kernel -> counter -> [values in dispatch order]"""
+    rows = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(pattern):
+        recs = list(csv.DictReader(open(f)))
+        recs.sort(key=lambda r: int(r.get("Dispatch_Id", 0) or 0))
+        for r in recs:
+            k = r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1].replace("void ", "").strip()
+            rows[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return rows
+
+
+def mean_last(v, n):
+    v = v[-n:] if n else v
+    return sum(v) / len(v) if v else 0.0
+
+
+bench_rows = load(f"{root}/p*/run_counter_collection.csv")
+kernels = {}
+for k, c in sorted(bench_rows.items()):
+    if not k.startswith(("k_", "k4_")):
         continue
-    n_fetch = len(c.get("FETCH_SIZE", []))
-    per_batch = n_fetch / steps if n_fetch else 0
-    f = sum(c.get("FETCH_SIZE", [0])) / max(1, n_fetch) * 1024
-    w = sum(c.get("WRITE_SIZE", [0])) / max(1, len(c.get("WRITE_SIZE", [1]))) * 1024
-    per_kernel[k] = {"launches_per_batch": per_batch, "fetch_bytes_raw": f, "write_bytes": w,
-                     "atomics": sum(c.get("TCC_EA0_ATOMIC_sum", [0])) / max(1, len(c.get("TCC_EA0_ATOMIC_sum", [1]))),
-                     "l2_hit_rate": (sum(c.get("TCC_HIT_sum", [0])) /
-                                     max(1.0, sum(c.get("TCC_HIT_sum", [0])) + sum(c.get("TCC_MISS_sum", [0]))))}
-    fetch_raw += f * per_batch
-    write += w * per_batch
-# steady state: kernels that run every batch (the LSD fallback of the first batch, before a
-# hot set exists, runs once per process and is reported per kernel only)
-ss_f = sum(v["fetch_bytes_raw"] * v["launches_per_batch"] for v in per_kernel.values() if v["launches_per_batch"] >= 0.9)
-ss_w = sum(v["write_bytes"] * v["launches_per_batch"] for v in per_kernel.values() if v["launches_per_batch"] >= 0.9)
-res = {"hbm_bytes_per_batch": ss_f * 2 + ss_w, "steady_state_fetch_bytes_raw": ss_f, "steady_state_write_bytes": ss_w,
-       "all_kernels_hbm_bytes_per_batch": fetch_raw * 2 + write, "fetch_bytes_raw_per_batch": fetch_raw,
-       "fetch_bytes_x2_per_batch": fetch_raw * 2, "write_bytes_per_batch": write,
-       "note": "FETCH_SIZE x2 per MI355X_MICROARCH.md gfx950 correction; WRITE_SIZE uncorrected",
-       "per_kernel_per_launch": per_kernel}
+    n = len(c.get("FETCH_SIZE", []))
+    f = mean_last(c.get("FETCH_SIZE", []), steps) * 1024
+    w = mean_last(c.get("WRITE_SIZE", []), steps) * 1024
+    hit, miss = mean_last(c.get("TCC_HIT_sum", []), steps), mean_last(c.get("TCC_MISS_sum", []), steps)
+    kernels[k] = {"dispatches_seen": n, "fetch_size_bytes": round(f), "write_size_bytes": round(w),
+                  "hbm_bytes_per_launch": round(2 * f + w),
+                  "tcc_ea0_atomic": round(mean_last(c.get("TCC_EA0_ATOMIC_sum", []), steps)),
+                  "l2_hit_rate": round(hit / (hit + miss), 4) if hit + miss else None}
+cal_rows = load(f"{root}/c*/run_counter_collection.csv")
+U = 230000
+cal = {}
+for k, c in cal_rows.items():
+    if k not in ("k_probe_read", "k_rmw", "k_copy"):
+        continue
+    # table_rmw launches each kernel 1 + reps times; every launch touches the same U slots
+    f = mean_last(c.get("FETCH_SIZE", []), 0) * 1024
+    w = mean_last(c.get("WRITE_SIZE", []), 0) * 1024
+    cal[k] = {"fetch_size_bytes_per_op": round(f / U, 2), "write_size_bytes_per_op": round(w / U, 2)}
+cal["note"] = ("k_probe_read: one random 16-B load per op inside a 32-B slot; k_rmw: random 32-B slot "
+               "load + store per op (two 16-B lanes); U = 230000 ops per launch on 2^28 slots")
+res = {"tag": tag, "source_sha": source_sha(), "timed_steps": steps,
+       "hbm_bytes_per_batch": sum(v["hbm_bytes_per_launch"] for v in kernels.values() if v["dispatches_seen"] >= steps),
+       "definition": "hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md gfx950 FETCH_SIZE "
+                     "correction), mean over the last timed_steps dispatches of each kernel",
+       "kernels": kernels, "calibration_table_rmw": cal}
 json.dump(res, open(out, "w"), indent=1)
-print(json.dumps({k: v for k, v in res.items() if k != "per_kernel_per_launch"}, indent=1))
-for k, v in per_kernel.items():
-    print(f"{k:16s} x{v['launches_per_batch']:.0f}  fetch {v['fetch_bytes_raw']/1e6:8.2f} MB  write {v['write_bytes']/1e6:8.2f} MB  atomics {v['atomics']:.0f}  L2hit {v['l2_hit_rate']:.2f}")
+print(json.dumps(res, indent=1))
