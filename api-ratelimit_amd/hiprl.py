@@ -31,7 +31,8 @@ UNIT_DIVIDER = {SECOND: 1, MINUTE: 60, HOUR: 3600, DAY: 86400}
 CODE_UNKNOWN, CODE_OK, CODE_OVER_LIMIT = 0, 1, 2
 FLAG_HAS_LIMIT, FLAG_LOCAL_CACHE_HIT = 1, 2
 
-RL_ERRORS = {-1: "RL_EINVAL", -2: "RL_EHIP", -3: "RL_ENOSPC", -4: "RL_ECAPACITY", -5: "RL_ESTATE", -6: "RL_EDEVICE"}
+RL_ERRORS = {-1: "RL_EINVAL", -2: "RL_EHIP", -3: "RL_ENOSPC", -4: "RL_ECAPACITY", -5: "RL_ESTATE", -6: "RL_EDEVICE",
+             -7: "RL_EPEER", -8: "RL_ECOMM"}
 
 STATUS_DTYPE = np.dtype([("code_flags", "<u4"), ("limit_remaining", "<u4"), ("reset_s", "<u4"),
                          ("over_limit_delta", "<u4"), ("near_limit_delta", "<u4")])
@@ -91,6 +92,20 @@ class RlHostBatch(C.Structure):
 
 
 # (name, argtypes, restype) of every symbol include/rl_hip.h declares
+class RlRouterConfig(C.Structure):
+    _fields_ = [("struct_size", C.c_uint32), ("n_shards", C.c_uint32), ("rank", C.c_uint32), ("max_desc", C.c_uint32),
+                ("rccl_id", C.c_void_p)]
+
+
+class RlRouterStats(C.Structure):
+    _fields_ = [("steps", C.c_uint64), ("n_shards", C.c_uint32), ("status", C.c_int32 * 16), ("recv", C.c_uint32 * 16),
+                ("sent", C.c_uint32 * 16), ("pack_us", C.c_double), ("exchange_us", C.c_double),
+                ("decide_us", C.c_double), ("decide_max_us", C.c_double), ("reply_us", C.c_double),
+                ("unpack_us", C.c_double), ("step_us", C.c_double)]
+
+
+ROUTER_ID_BYTES = 128
+
 ABI = [
     ("rl_create", [C.POINTER(RlConfig), C.POINTER(C.c_void_p)], C.c_int),
     ("rl_destroy", [C.c_void_p], None),
@@ -120,6 +135,12 @@ ABI = [
     ("rl_load_tree", [C.c_void_p, C.POINTER(RlTreeNode), C.c_uint32, C.c_void_p, C.c_uint32], C.c_int),
     ("rl_resolve", [C.c_void_p, C.POINTER(RlResolveBatch), C.c_void_p], C.c_int),
     ("rl_resolve_device", [C.c_void_p, C.POINTER(RlResolveBatch), C.c_void_p], C.c_int),
+    ("rl_router_unique_id", [C.c_void_p], C.c_int),
+    ("rl_router_create", [C.POINTER(RlRouterConfig), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
+    ("rl_router_step", [C.c_void_p, C.POINTER(RlBatch), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
+    ("rl_router_get_stats", [C.c_void_p, C.POINTER(RlRouterStats)], C.c_int),
+    ("rl_router_last_error", [C.c_void_p], C.c_char_p),
+    ("rl_router_destroy", [C.c_void_p], None),
 ]
 
 # multi-GPU router record sizes (include/rl_hip.h RL_ROUTE_*)
@@ -150,7 +171,12 @@ def load_library(path: Optional[os.PathLike] = None) -> C.CDLL:
 
 
 class RedisError(RuntimeError):
-    """redis.RedisError — the backend's only recoverable failure (service/ratelimit.go:276-281)."""
+    """redis.RedisError — the backend's only recoverable failure (service/ratelimit.go:276-281).
+    `code` is the RL_E* return code when the error came from the C ABI."""
+
+    def __init__(self, msg: str, code: Optional[int] = None):
+        super().__init__(msg)
+        self.code = code
 
 
 # ---------------------------------------------------------------------------
@@ -283,7 +309,7 @@ class Engine:
     def _check(self, rc: int, what: str):
         if rc:
             msg = self.lib.rl_last_error(self.h).decode()
-            raise RedisError(f"{what}: {RL_ERRORS.get(rc, rc)}: {msg}")
+            raise RedisError(f"{what}: {RL_ERRORS.get(rc, rc)}: {msg}", rc)
 
     def load_rules(self, rules: Sequence[tuple]):
         arr = (RlRule * max(1, len(rules)))()
@@ -428,6 +454,70 @@ class Engine:
         s.req_of = req_of_ptr
         self._check(self.lib.rl_route_unpack(self.h, C.byref(s), perm_ptr, reply_ptr, out_ptr, thr_ptr),
                     "rl_route_unpack")
+
+
+class Router:
+    """The routed step owned by the C ABI (rl_router_*): G engines in this process (local
+    transport) or this rank's engine over an RCCL communicator (rccl_id from
+    router_unique_id() on one rank, shared out of band)."""
+
+    def __init__(self, engines, max_desc: int, n_shards: Optional[int] = None, rank: int = 0,
+                 rccl_id: Optional[bytes] = None):
+        self.lib = engines[0].lib
+        self.engines = list(engines)
+        cfg = RlRouterConfig()
+        cfg.struct_size = C.sizeof(RlRouterConfig)
+        cfg.n_shards = n_shards if n_shards is not None else len(engines)
+        cfg.rank = rank
+        cfg.max_desc = max_desc
+        self._id = None
+        if rccl_id is not None:
+            self._id = C.create_string_buffer(bytes(rccl_id), ROUTER_ID_BYTES)
+            cfg.rccl_id = C.cast(self._id, C.c_void_p)
+        arr = (C.c_void_p * len(engines))(*[e.h for e in engines])
+        self.h = C.c_void_p()
+        rc = self.lib.rl_router_create(C.byref(cfg), arr, C.byref(self.h))
+        if rc:
+            raise RedisError(f"rl_router_create failed: {RL_ERRORS.get(rc, rc)}")
+        self.n = len(engines)
+
+    @staticmethod
+    def unique_id(lib=None) -> bytes:
+        lib = lib or load_library()
+        buf = C.create_string_buffer(ROUTER_ID_BYTES)
+        rc = lib.rl_router_unique_id(buf)
+        if rc:
+            raise RedisError(f"rl_router_unique_id: {RL_ERRORS.get(rc, rc)}")
+        return buf.raw
+
+    def step(self, batches, out_ptrs, thr_ptrs):
+        """batches: RlBatch per engine (device pointers); outputs: device pointers per engine."""
+        arr = (RlBatch * self.n)(*batches)
+        o = (C.c_void_p * self.n)(*out_ptrs)
+        t = (C.c_void_p * self.n)(*thr_ptrs)
+        rc = self.lib.rl_router_step(self.h, arr, o, t)
+        if rc:
+            raise RedisError(f"rl_router_step: {RL_ERRORS.get(rc, rc)}: {self.lib.rl_router_last_error(self.h).decode()}",
+                             rc)
+
+    def stats(self) -> dict:
+        s = RlRouterStats()
+        self.lib.rl_router_get_stats(self.h, C.byref(s))
+        d = {k: getattr(s, k) for k, _ in RlRouterStats._fields_}
+        for k in ("status", "recv", "sent"):
+            d[k] = list(d[k])[:s.n_shards]
+        return d
+
+    def close(self):
+        if self.h:
+            self.lib.rl_router_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 # ---------------------------------------------------------------------------

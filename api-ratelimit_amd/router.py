@@ -13,6 +13,12 @@ src/redis/driver_impl.go:56-90). One step of a rank:
   5. all-to-all of the 24-B replies (reverse splits)
   6. unpack    replies -> rl_status[n_desc] and ThrottleMillis[n_req] in its own order
 
+A shard whose pack or decide fails still takes part in every exchange of the step: the
+counts all-to-all carries each origin's pack status next to its counts, and a status
+all-to-all after the owners decide carries each owner's. Every rank then raises together
+(its own error, or RL_EPEER naming the failed shard), so one bad batch cannot leave the
+other GPUs blocked in a collective.
+
 The exchange is plain torch.distributed (RCCL over xGMI for "nccl", gloo on CPU for the
 tests); the shard object does steps 1, 4 and 6. EngineShard is the product shard (HIP
 engine, device tensors); a test shard with the same byte layouts can stand in on CPU.
@@ -126,6 +132,11 @@ class EngineShard:
         return out, thr
 
 
+def _code(ex: Exception) -> int:
+    c = getattr(ex, "code", None)
+    return int(c) if c else -1  # RL_EINVAL for errors without a C code
+
+
 class ShardRouter:
     """Steps 2, 3 and 5 of the routed step over a torch.distributed group."""
 
@@ -133,19 +144,50 @@ class ShardRouter:
         self.shard = shard
         self.group = group
         self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
         self.last_recv = 0  # records this rank decided as owner in the last step
+        self.last_status = [0] * self.world  # per shard: pack / decide status of the last step
+
+    def _raise(self, phase: str, status, own: Exception | None):
+        self.last_status = status
+        if own is not None:
+            raise own
+        bad = [j for j, c in enumerate(status) if c]
+        raise hiprl.RedisError(f"routed step: RL_EPEER: shard {bad[0]} failed to {phase} "
+                               f"({hiprl.RL_ERRORS.get(status[bad[0]], status[bad[0]])})", -7)
 
     def step(self, b):
         sh = self.shard
-        send, counts_t, counts, perm = sh.pack(b)
-        rcounts_t = torch.empty_like(counts_t)
-        dist.all_to_all_single(rcounts_t, counts_t, group=self.group)
-        rcounts = [int(x) for x in rcounts_t.tolist()]
+        own = None
+        try:
+            send, counts_t, counts, perm = sh.pack(b)
+        except hiprl.RedisError as ex:
+            own, counts_t, counts, perm = ex, None, [0] * self.world, None
+            send = sh.empty(0)
+        dev = send.device
+        err = _code(own) if own is not None else 0
+        x = torch.tensor([v for c in counts for v in (c, err)], dtype=torch.int32, device=dev)
+        rx = torch.empty_like(x)
+        dist.all_to_all_single(rx, x, group=self.group)
+        rv = [int(v) for v in rx.tolist()]
+        rcounts, status = rv[0::2], rv[1::2]
+        if any(status):
+            self._raise("pack its batch", status, own)
         n_in = sum(rcounts)
         recv = sh.empty(n_in * REC)
         dist.all_to_all_single(recv, send, [c * REC for c in rcounts], [c * REC for c in counts], group=self.group)
-        reply = sh.decide(recv, n_in)
+        try:
+            reply = sh.decide(recv, n_in)
+        except hiprl.RedisError as ex:
+            own, reply = ex, sh.empty(n_in * REP)
+        e = torch.full((self.world,), _code(own) if own is not None else 0, dtype=torch.int32, device=dev)
+        re_ = torch.empty_like(e)
+        dist.all_to_all_single(re_, e, group=self.group)
+        status = [int(v) for v in re_.tolist()]
+        if any(status):
+            self._raise("decide its records", status, own)
         back = sh.empty(sum(counts) * REP)
         dist.all_to_all_single(back, reply, [c * REP for c in counts], [c * REP for c in rcounts], group=self.group)
         self.last_recv = n_in
+        self.last_status = [0] * self.world
         return sh.unpack(b, perm, back)

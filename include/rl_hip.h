@@ -49,7 +49,9 @@ enum {
                         any counter changed (raise log2_slots / max_load_permille) */
   RL_ECAPACITY = -4, /* batch larger than the engine was created for */
   RL_ESTATE = -5,    /* call out of order (e.g. rl_wait without rl_submit) */
-  RL_EDEVICE = -6    /* device-side fault detected (bounded spin expired) */
+  RL_EDEVICE = -6,   /* device-side fault detected (bounded spin expired) */
+  RL_EPEER = -7,     /* rl_router_step: another shard failed this step (its code in rl_router_stats) */
+  RL_ECOMM = -8      /* rl_router: RCCL error */
 };
 
 typedef struct rl_engine rl_engine;
@@ -241,6 +243,54 @@ int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_re
  * Ordered on the engine stream; no host synchronisation. */
 int rl_route_unpack(rl_engine* e, const rl_batch* device_batch, const uint32_t* d_perm, const void* d_reply,
                     rl_status* d_out, uint32_t* d_req_throttle_ms);
+
+/* ---- Router object: the routed step above behind one call ------------------------------
+ * Owns the exchange buffers and the transport, so a non-Python host (the Go service over cgo)
+ * can route without torch.distributed:
+ *   RCCL transport  (rccl_id != NULL): one process per GPU, engines[0] = this rank's engine;
+ *                   counts, records and replies move by ncclAllToAll / ncclAllToAllv over the
+ *                   communicator the router owns (xGMI between GPUs of a node). rank 0 makes the
+ *                   id with rl_router_unique_id and hands it to the others out of band.
+ *   local transport (rccl_id == NULL): n_shards engines in this process (logical shards, one
+ *                   device or several); the exchanges are device-to-device copies.
+ * Every shard finishes every exchange of a step even when one fails, then all of them return
+ * the failure: the failing shard its own code, the others RL_EPEER. The counts exchange
+ * carries each origin's pack status, the reply exchange each owner's decide status, so a bad
+ * batch on one GPU cannot leave its peers blocked in a collective. A refused owner batch
+ * (RL_ENOSPC, RL_ECAPACITY) leaves that owner's table unchanged; other owners of the step
+ * have applied theirs (per-shard atomicity, as a Redis cluster pipeline gives per-node). */
+#define RL_ROUTER_ID_BYTES 128u
+typedef struct rl_router rl_router;
+
+typedef struct rl_router_config {
+  uint32_t struct_size; /* sizeof(rl_router_config) */
+  uint32_t n_shards;    /* 1..RL_ROUTE_MAX_SHARDS */
+  uint32_t rank;        /* RCCL transport: this process's shard; local transport: 0 */
+  uint32_t max_desc;    /* descriptors per origin batch (an owner can receive n_shards x this) */
+  const uint8_t* rccl_id; /* RL_ROUTER_ID_BYTES from rl_router_unique_id, or NULL: local transport */
+} rl_router_config;
+
+typedef struct rl_router_stats {
+  uint64_t steps;
+  uint32_t n_shards;
+  int32_t status[RL_ROUTE_MAX_SHARDS]; /* last step: each shard's pack / decide status (0 = ok) */
+  uint32_t recv[RL_ROUTE_MAX_SHARDS];  /* last step: records each owner decided (RCCL: this rank's only) */
+  uint32_t sent[RL_ROUTE_MAX_SHARDS];  /* last step: records origin 0 (RCCL: this rank) sent each owner */
+  double pack_us, exchange_us, decide_us, decide_max_us, reply_us, unpack_us, step_us; /* last step, host clock */
+} rl_router_stats;
+
+/* A fresh RCCL unique id (ncclGetUniqueId), RL_ROUTER_ID_BYTES bytes. */
+int rl_router_unique_id(uint8_t* id_out);
+/* engines: n_shards engines (local transport) or 1 (RCCL transport). The router does not own
+ * them; they must outlive it and be used by nothing else while a step runs. */
+int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_router** out);
+/* One routed step, synchronous. batches / d_out / d_req_throttle_ms: one per engine passed at
+ * create (device pointers; the same layouts as rl_submit_device). Decisions equal one engine
+ * deciding the origins' batches one after another in shard order (include above). */
+int rl_router_step(rl_router* r, const rl_batch* batches, rl_status* const* d_out, uint32_t* const* d_req_throttle_ms);
+int rl_router_get_stats(const rl_router* r, rl_router_stats* out);
+const char* rl_router_last_error(const rl_router* r);
+void rl_router_destroy(rl_router* r);
 
 /* Clear the counter table and local-cache state (FLUSHALL analogue; tests and restarts). */
 int rl_reset(rl_engine* e);

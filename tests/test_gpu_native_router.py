@@ -1,0 +1,132 @@
+"""The routed step owned by the C ABI (rl_router_*, csrc/rl_router.cpp) vs the serial oracle.
+
+Local transport: G engines on cuda:0 stand in for G GPUs (exchanges by device copies).
+RCCL transport: a one-rank communicator on cuda:0 (the collectives run for real, each rank
+sending to itself). Decisions must equal one oracle replaying the origins' batches in shard
+order, bit-exact. Error steps: a bad batch on one origin and an owner that cannot take its
+records make every shard's step fail (its own code or RL_EPEER), and the router keeps working.
+Reference: src/redis/fixed_cache_impl.go:31-123 per key on the server that owns it
+(driver_impl.go:84-110 pipelines per server).
+"""
+import numpy as np
+import pytest
+import torch
+
+import hiprl
+import oracle
+import router
+import routing
+import streams
+from test_gpu_router import DEV, stream_batches
+
+pytestmark = pytest.mark.gpu
+
+
+def _engines(G, local_cache, cap):
+    es = []
+    for _ in range(G):
+        e = hiprl.Engine(local_cache=local_cache, max_batch_desc=cap)
+        e.load_rules(streams.RULES)
+        es.append(e)
+    return es
+
+
+def _step(r, batches):
+    dbs = [router.DeviceBatch.from_host(b, DEV) for b in batches]
+    outs = [torch.empty(max(1, b.n_desc) * 20, dtype=torch.uint8, device=DEV) for b in batches]
+    thrs = [torch.empty(max(1, b.n_req), dtype=torch.int32, device=DEV) for b in batches]
+    torch.cuda.synchronize()
+    r.step([hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs()) for db in dbs],
+           [o.data_ptr() for o in outs], [t.data_ptr() for t in thrs])
+    return [(o.cpu().numpy().view(hiprl.STATUS_DTYPE)[:b.n_desc], t.cpu().numpy().view(np.uint32)[:b.n_req])
+            for o, t, b in zip(outs, thrs, batches)]
+
+
+def _check(o, batches, got, ctx):
+    est, ethr = o.submit(routing.concat_batches(batches))
+    d0 = r0 = 0
+    for g, (b, (st, thr)) in enumerate(zip(batches, got)):
+        streams.assert_same(est[d0:d0 + b.n_desc], ethr[r0:r0 + b.n_req], st, thr, f"{ctx} origin={g}")
+        d0 += b.n_desc
+        r0 += b.n_req
+
+
+@pytest.mark.parametrize("local_cache", [False, True])
+@pytest.mark.parametrize("G", [1, 3, 4])
+def test_local_transport_matches_serial_oracle(G, local_cache):
+    per = 1500  # requests per origin batch (1-3 descriptors each)
+    es = _engines(G, local_cache, 4 * per * G)
+    r = hiprl.Router(es, max_desc=4 * per)
+    o = oracle.Oracle(local_cache=local_cache)
+    o.load_rules(streams.RULES)
+    for s, batches in enumerate(stream_batches(G, 4, per, seed=40 + G)):
+        got = _step(r, batches)
+        _check(o, batches, got, f"G={G} step={s}")
+        st = r.stats()
+        routed = sum(int((b.rule != hiprl.NIL_RULE).sum()) for b in batches)
+        assert sum(st["recv"]) == routed and st["status"] == [0] * G, st
+        own0 = routing.owners_of(batches[0], streams.RULES, G, 0x5EE7AB1E5EED)
+        assert st["sent"] == [int((own0 == j).sum()) for j in range(G)]
+
+
+def test_rccl_transport_one_rank(monkeypatch):
+    monkeypatch.setenv("NCCL_SOCKET_IFNAME", "lo")
+    per = 1500
+    es = _engines(1, True, 4 * per)
+    r = hiprl.Router(es, max_desc=4 * per, n_shards=1, rank=0, rccl_id=hiprl.Router.unique_id())
+    o = oracle.Oracle(local_cache=True)
+    o.load_rules(streams.RULES)
+    for s, batches in enumerate(stream_batches(1, 3, per, seed=9)):
+        _check(o, batches, _step(r, batches), f"rccl step={s}")
+    assert r.stats()["steps"] == 3
+    r.close()
+
+
+def test_local_transport_errors_fail_every_shard():
+    G, per = 3, 1000
+    es = _engines(G, True, 4 * per * G)
+    r = hiprl.Router(es, max_desc=4 * per)
+    o = oracle.Oracle(local_cache=True)
+    o.load_rules(streams.RULES)
+    steps = stream_batches(G, 3, per, seed=77)
+    _check(o, steps[0], _step(r, steps[0]), "before")
+    bad = list(steps[1])
+    b1 = bad[1]
+    rule = b1.rule.copy()
+    rule[len(rule) // 2] = 99  # unknown rule id on origin 1
+    bad[1] = hiprl.Batch(b1.blob, b1.off, rule, b1.req_of, b1.now, b1.hits)
+    with pytest.raises(hiprl.RedisError, match="shard 1 \\(pack\\)") as ex:
+        _step(r, bad)
+    assert ex.value.code == -1 and r.stats()["status"][1] == -1
+    # the failed step changed nothing: the next one equals the oracle without it
+    _check(o, steps[2], _step(r, steps[2]), "after")
+
+
+def test_owner_over_capacity_fails_every_shard():
+    """Owner 1 can decide at most 2000 records; both origins send it more (requests picked so
+    that all their descriptors route to shard 1): the step fails on both shards."""
+    G, per = 2, 1500
+    batches = []
+    for g in range(G):
+        reqs = [(d, de, ru, h, 1_700_000_000) for d, de, ru, h, _ in
+                streams.make_stream(300 + g, 4000, t0=1_700_000_000, keyspace=400, dt_max=1)]
+        b = hiprl.build_batch(reqs)
+        own = routing.owners_of(b, streams.RULES, G, 0x5EE7AB1E5EED)
+        to1 = np.ones(b.n_req, bool)
+        np.logical_and.at(to1, b.req_of, own != 0)
+        keep = [q for q in range(b.n_req) if to1[q]]
+        sel, n = [], 0
+        for q in keep:
+            n += len(reqs[q][1])
+            if n > per:
+                break
+            sel.append(reqs[q])
+        batches.append(hiprl.build_batch(sel))
+    assert all(600 < b.n_desc <= per for b in batches)
+    es = [hiprl.Engine(local_cache=True, max_batch_desc=c) for c in (per * G, 2000)]
+    for e in es:
+        e.load_rules(streams.RULES)
+    r = hiprl.Router(es, max_desc=per)
+    with pytest.raises(hiprl.RedisError, match="shard 1 \\(decide\\)") as ex:
+        _step(r, batches)
+    assert ex.value.code == -4 and r.stats()["status"] == [0, -4], r.stats()

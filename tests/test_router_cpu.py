@@ -102,3 +102,72 @@ def test_owner_partition_is_balanced_and_window_independent():
         own = np.array([oracle.route_owner(*oracle.prefix_lanes(p, 7), g) for p in prefixes])
         cnt = np.bincount(own, minlength=g)
         assert cnt.min() > 0.8 * len(prefixes) / g, cnt
+
+
+class FailingShard(routing.OracleShard):
+    """An OracleShard that fails to pack at (rank, step) pack_at and to decide at decide_at."""
+
+    def __init__(self, *a, pack_at=None, decide_at=None, **kw):
+        super().__init__(*a, **kw)
+        self.step_no, self.pack_at, self.decide_at = 0, pack_at, decide_at
+
+    def pack(self, b):
+        self.step_no += 1
+        if self.pack_at == self.step_no - 1:
+            raise hiprl.RedisError("rl_route_pack: RL_EINVAL: injected bad batch", -1)
+        return super().pack(b)
+
+    def decide(self, recv, n):
+        if self.decide_at == self.step_no - 1:
+            raise hiprl.RedisError("rl_wait: RL_ENOSPC: injected full region", -3)
+        return super().decide(recv, n)
+
+
+def _fail_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+
+    import router
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        sh = FailingShard(rank, world, streams.RULES, local_cache=True,
+                          pack_at=1 if rank == 1 else None, decide_at=3 if rank == 0 else None)
+        r = router.ShardRouter(sh)
+        res = {}
+        for s, b in enumerate(rank_batches(rank, True)):
+            try:
+                st, thr = r.step(b)
+                res[f"st{s}"], res[f"thr{s}"] = st, thr
+                res[f"err{s}"] = np.array([0])
+            except hiprl.RedisError as ex:
+                res[f"err{s}"] = np.array([ex.code])
+            res[f"status{s}"] = np.array(r.last_status)
+        dist.barrier()  # every rank left every step: nobody is stuck in a collective
+        np.savez(os.path.join(outdir, f"rank{rank}.npz"), **res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_errors_reach_every_rank(tmp_path):
+    """Rank 1 fails to pack at step 1 and rank 0 fails to decide at step 3: every rank raises at
+    both steps (the failing one its own code, the other RL_EPEER) and no collective hangs;
+    steps 0 and 2 still equal the serial oracle (a pack failure changes no owner's state)."""
+    world = 2
+    mp.spawn(_fail_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    got = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    assert [int(got[r]["err1"][0]) for r in range(world)] == [-7, -1]
+    assert [int(got[r]["err3"][0]) for r in range(world)] == [-3, -7]
+    assert list(got[0]["status1"]) == [0, -1] and list(got[1]["status3"]) == [-3, 0]
+    per_rank = [rank_batches(r, True) for r in range(world)]
+    o = oracle.Oracle(local_cache=True)
+    o.load_rules(streams.RULES)
+    for s in (0, 2):
+        est, ethr = o.submit(routing.concat_batches([per_rank[r][s] for r in range(world)]))
+        d0 = r0 = 0
+        for r in range(world):
+            b = per_rank[r][s]
+            assert int(got[r][f"err{s}"][0]) == 0
+            streams.assert_same(est[d0:d0 + b.n_desc], ethr[r0:r0 + b.n_req], got[r][f"st{s}"], got[r][f"thr{s}"],
+                                f"step={s} rank={r}")
+            d0 += b.n_desc
+            r0 += b.n_req
