@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--json-out", type=str, default="")
     ap.add_argument("--depth", type=int, default=2, help="batches in flight through rl_submit_pipelined (2..3)")
     ap.add_argument("--serial", action="store_true", help="one batch in flight (rl_submit_device + rl_wait)")
+    ap.add_argument("--logical-shards", type=int, default=0,
+                    help="G > 0: one GPU, G engines as G logical shards behind the C-ABI router (rl_router, local "
+                         "transport): G origin batches per step, records per owner and the step breakdown")
     ap.add_argument("--lib", type=str, default="", help=argparse.SUPPRESS)  # diagnostics: a variant library
     ap.add_argument("--dump-stamps", type=str, default="", help=argparse.SUPPRESS)  # -DRL_STAMPS variant: raw stamps
     return ap.parse_args()
@@ -208,8 +211,70 @@ def cpu_baseline(args, rules, d, seed, K, b0):
                             "sample": f"{nb1} batches, serial DoLimit over an in-memory Redis stand-in, {t1:.1f} s"}}
 
 
+def logical_shards_main(args):
+    """G logical shards on one GPU (SURVEY.md §8e readiness without a multi-GPU box): every
+    origin draws its batch from the same Zipf key distribution, so each hot key lands on one
+    owner from every origin. Reports records per owner (max / mean) and the router's step
+    breakdown; decide_max_us is the owners' critical path when each owner has its own GPU."""
+    import torch
+
+    G, d, K = args.logical_shards, args.desc, max(1, args.batches_per_second)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    lg = args.log2_slots - int(math.ceil(math.log2(G)))  # each shard holds 1/G of the live set
+    rules = workload.CONFIG3_RULES if args.config == 3 else workload.CONFIG2_RULES
+    engines = []
+    for _ in range(G):
+        e = hiprl.Engine(device=0, log2_slots=(lg, lg, lg, 12), max_batch_desc=G * d, max_batch_req=G * d,
+                         max_blob_bytes=G * d * 17 + 64, sort_bits=48, pipeline=args.pipeline)
+        e.load_rules(rules)
+        engines.append(e)
+    r = hiprl.Router(engines, max_desc=d)
+    gens = [DeviceGen(args.config, d, (3 if args.config == 3 else 2) + 7919 * g, K, dev) for g in range(G)]
+    bufs = [[gen.alloc() for gen in gens] for _ in range(2)]
+    outs = [torch.empty(d * 20, dtype=torch.uint8, device=dev) for _ in range(G)]
+    thrs = [torch.empty(d, dtype=torch.int32, device=dev) for _ in range(G)]
+    prefill = args.prefill if args.prefill >= 0 else 64
+
+    def step(b):
+        dbs = bufs[b % 2]
+        for gen, db in zip(gens, dbs):
+            gen.fill(b, db)
+        torch.cuda.synchronize()
+        r.step([hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs()) for db in dbs],
+               [o.data_ptr() for o in outs], [t.data_ptr() for t in thrs])
+        return r.stats()
+
+    for b in range(prefill + args.warmup):
+        step(b)
+    rows = [step(prefill + args.warmup + j) for j in range(args.steps)]
+    rec = np.array([x["recv"] for x in rows], np.float64)  # steps x owners
+    mean_owner = rec.mean(axis=1)
+    keys = ["pack_us", "exchange_us", "decide_us", "decide_max_us", "reply_us", "unpack_us", "step_us"]
+    br = {k: round(float(np.mean([x[k] for x in rows])), 1) for k in keys}
+    # G real GPUs: packs, decides and unpacks run side by side; the exchanges are the same bytes
+    est = br["pack_us"] / G + br["exchange_us"] + br["decide_max_us"] + br["reply_us"] + br["unpack_us"] / G
+    line = {"mode": "logical_shards", "n_shards": G, "descriptors_per_origin_batch": d, "steps": args.steps,
+            "prefill_steps": prefill, "config": args.config, "log2_slots_per_shard": lg,
+            "records_per_owner_mean": round(float(mean_owner.mean()), 1),
+            "records_per_owner_max": int(rec.max()),
+            "owner_imbalance_max_over_mean": round(float((rec.max(axis=1) / mean_owner).mean()), 3),
+            "records_per_owner_last_step": [int(x) for x in rows[-1]["recv"]],
+            "step_breakdown_us": br,
+            "estimated_step_us_on_G_gpus": round(est, 1),
+            "estimated_desc_per_s_on_G_gpus": round(G * d / (est * 1e-6), 1),
+            "note": "one GPU, G engines (local transport: exchanges are device copies); estimate = pack/G + "
+                    "exchange + max owner decide + reply + unpack/G"}
+    print(json.dumps(line), flush=True)
+    if args.json_out:
+        Path(args.json_out).write_text(json.dumps(line) + "\n")
+    r.close()
+
+
 def main():
     args = parse()
+    if args.logical_shards:
+        return logical_shards_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
