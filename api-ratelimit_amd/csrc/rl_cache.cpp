@@ -65,6 +65,7 @@ HipRateLimitCache::HipRateLimitCache(const HipSettings& s, std::shared_ptr<TimeS
   c.max_batch_req = s.batch_limit + 4096;
   c.max_blob_bytes = (s.batch_limit + 4096) * 128u;
   c.hash_seed = s.hash_seed;
+  c.max_load_permille = s.max_load_permille;
   int rc = rl_create(&c, &eng_);
   if (rc) throw RedisError("rl_create failed: " + std::to_string(rc));
   thr_ = std::thread([this] { submitter(); });

@@ -144,7 +144,8 @@ struct HipSettings {
   bool per_second_split = false;          // REDIS_PERSECOND
   uint32_t batch_window_us = 75;          // HIP_BATCH_WINDOW
   uint32_t batch_limit = 1u << 16;        // HIP_BATCH_LIMIT (descriptors)
-  uint64_t hash_seed = 0x5ee7ab1e5eedull;
+  uint64_t hash_seed = 0x5ee7ab1e5eedull;  // HIP_HASH_SEED: the same in every process of a deployment
+  uint32_t max_load_permille = 750;        // HIP_TABLE_MAX_LOAD: refuse a batch past this region load
 };
 
 // The HIP backend. Equivalent of redis.NewFixedRateLimitCacheImpl + fixedRateLimitCacheImpl.

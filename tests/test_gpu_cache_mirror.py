@@ -1,0 +1,132 @@
+"""The C++ host-side mirror of the reference's RateLimitCache (api-ratelimit_amd/csrc/rl_cache.hpp,
+HipRateLimitCache: DoLimit micro-batched onto the engine by a submitter thread) through a test
+shim (tests/cshim), on the reference's integration streams (test/integration/
+integration_test.go, tests/golden/reference_vectors.json) and on concurrent callers whose
+requests share batches. Statuses, ThrottleMillis and the per-rule stats counters must equal
+the reference's expectations / the serial oracle."""
+import ctypes as C
+import threading
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import hiprl
+import oracle
+import streams
+
+pytestmark = pytest.mark.gpu
+SHIM = Path(__file__).resolve().parent / "cshim" / "librl_cache_shim.so"
+
+
+def _lib():
+    if not SHIM.exists():
+        raise RuntimeError(f"{SHIM} missing (built by __graft_entry__.build())")
+    lib = C.CDLL(str(SHIM))
+    vp, u32, i64 = C.c_void_p, C.c_uint32, C.c_int64
+    lib.rlc_create.argtypes, lib.rlc_create.restype = [C.c_int, C.c_float, C.c_int, u32], vp
+    lib.rlc_destroy.argtypes = [vp]
+    lib.rlc_set_time.argtypes = [vp, i64]
+    lib.rlc_add_rule.argtypes, lib.rlc_add_rule.restype = [vp, u32, u32, C.c_char_p], C.c_int
+    lib.rlc_do_limit.argtypes = [vp, C.c_char_p, u32, vp, vp, vp, vp, u32, vp, vp]
+    lib.rlc_do_limit.restype = C.c_int
+    lib.rlc_stats.argtypes = [vp, C.c_int, vp]
+    lib.rlc_error.argtypes, lib.rlc_error.restype = [vp], C.c_char_p
+    lib.rlc_flush.argtypes = [vp]
+    return lib
+
+
+class Mirror:
+    def __init__(self, local_cache, window_us=0, ratio=0.8):
+        self.lib = _lib()
+        self.h = self.lib.rlc_create(int(local_cache), ratio, 0, window_us)
+        assert self.h, "HipRateLimitCache construction failed"
+
+    def add_rule(self, rpu, unit, key):
+        return self.lib.rlc_add_rule(self.h, rpu, unit, key.encode())
+
+    def do_limit(self, domain, descs, rules, hits):
+        n = len(descs)
+        ne = (C.c_uint32 * max(1, n))(*[len(d) for d in descs])
+        flat = [e for d in descs for e in d]
+        keys = (C.c_char_p * max(1, len(flat)))(*[k.encode() for k, _ in flat])
+        vals = (C.c_char_p * max(1, len(flat)))(*[v.encode() for _, v in flat])
+        rl = (C.c_int32 * max(1, n))(*[-1 if r is None or r == streams.NIL else r for r in rules])
+        out = (C.c_uint32 * (4 * max(1, n)))()
+        thr = C.c_uint32()
+        rc = self.lib.rlc_do_limit(self.h, domain.encode(), n, ne, keys, vals, rl, hits, out, C.byref(thr))
+        if rc:
+            raise hiprl.RedisError(self.lib.rlc_error(self.h).decode())
+        return [tuple(out[4 * i:4 * i + 4]) for i in range(n)], thr.value
+
+    def stats(self, rule):
+        o = (C.c_uint64 * 4)()
+        self.lib.rlc_stats(self.h, rule, o)
+        return dict(total_hits=o[0], over_limit=o[1], near_limit=o[2], over_limit_with_local_cache=o[3])
+
+    def close(self):
+        self.lib.rlc_destroy(self.h)
+
+
+def test_integration_streams_through_cpp_mirror(golden):
+    for s in golden["streams"]:
+        m = Mirror(s["local_cache"])
+        ids = [m.add_rule(L, u, s["stat_keys"][k]) for k, (L, u) in enumerate(s["rules"])]
+        for req, exp in zip(s["requests"], s["expect"]):
+            m.lib.rlc_set_time(m.h, req["now"])
+            descs = [[tuple(e) for e in d] for d in req["descriptors"]]
+            rules = [None if r is None else ids[r] for r in req["rules"]]
+            got, _ = m.do_limit(req["domain"], descs, rules, req["hits"])
+            for k, ((code, rem, has_limit, _), want) in enumerate(zip(got, exp["statuses"])):
+                assert [code, rem, bool(has_limit)] == [want[0], want[1], want[2]], (exp["src"], k)
+            for name, want in exp["stats"].items():
+                got_st = m.stats(s["stat_keys"].index(name))
+                for key, v in want.items():
+                    assert got_st[key] == v, (exp["src"], name, key)
+        m.close()
+
+
+@pytest.mark.parametrize("local_cache", [False, True])
+def test_concurrent_callers_share_batches(local_cache):
+    """8 threads, 150 requests each on keys of their own, one shared time: requests of
+    different threads land in the same batches (2 ms window); each thread's results equal a
+    serial oracle of its own requests, and the stats counters add up."""
+    T, n = 8, 150
+    rules = [(20, hiprl.SECOND), (60, hiprl.MINUTE)]
+    m = Mirror(local_cache, window_us=2000)
+    ids = [m.add_rule(L, u, f"rule{k}") for k, (L, u) in enumerate(rules)]
+    now = 1_700_000_000
+    m.lib.rlc_set_time(m.h, now)
+    rng = np.random.default_rng(11)
+    per = []
+    for t in range(T):
+        reqs = []
+        for _ in range(n):
+            k = int(rng.integers(0, 6))
+            r = int(rng.integers(0, 2))
+            reqs.append((f"dom{t}", [[("k", str(k))]], [r], int(rng.integers(0, 3)), now))
+        per.append(reqs)
+    res = [None] * T
+
+    def run(t):
+        res[t] = [m.do_limit(d, de, [ids[x] for x in ru], h) for d, de, ru, h, _ in per[t]]
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    tot = {0: 0, 1: 0}
+    for t in range(T):
+        o = oracle.Oracle(local_cache=local_cache)
+        o.load_rules(rules)
+        st, thr = streams.replay(o, per[t], [1] * n)
+        for q, ((got, gthr), (_, _, ru, h, _)) in enumerate(zip(res[t], per[t])):
+            code, rem, has_limit, reset = got[0]
+            assert (code, rem, reset) == (int(st["code_flags"][q]) & 0xFF, int(st["limit_remaining"][q]),
+                                          int(st["reset_s"][q])), (t, q)
+            assert gthr == int(thr[q])
+            tot[ru[0]] += max(1, h)
+    for r in (0, 1):
+        assert m.stats(ids[r])["total_hits"] == tot[r]
+    m.close()
