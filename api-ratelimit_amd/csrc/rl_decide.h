@@ -225,13 +225,13 @@ RL_DEV void exotic_sequence(KeyState& s, const TableDesc& tab, const DevRule* __
 // region (0 = untouched).
 RL_DEV uint32_t region_live(const RegionOcc& o, uint32_t gen) { return (o.gen < gen) ? 0u : o.live; }
 RL_DEV bool capacity_ok(const RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* cnt) {
+  RegionOcc o[8];  // all eight loads in flight together (no load behind a branch)
+#pragma unroll
+  for (int r = 0; r < 8; ++r) o[r] = occ[r];
   bool ok = true;
 #pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    if (!cnt[r]) continue;
-    const RegionOcc o = occ[r];
-    ok &= (uint64_t)region_live(o, gmax[r]) + cnt[r] <= (uint64_t)o.limit;
-  }
+  for (int r = 0; r < 8; ++r)
+    ok &= !cnt[r] || (uint64_t)region_live(o[r], gmax[r]) + cnt[r] <= (uint64_t)o[r].limit;
   return ok;
 }
 // After the batch: add its new slots (one thread).

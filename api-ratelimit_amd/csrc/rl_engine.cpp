@@ -63,7 +63,7 @@ void launch_v4_place(hipStream_t, const rl_batch&, const MRec*, const uint16_t*,
                      Deferred*, int, uint32_t*, EngineCtl*);
 void launch_v4_group(hipStream_t, const rl_batch&, MRec*, const DevRule*, const TableDesc&, rl_status*, uint32_t*,
                      const HotBucket*, const Deferred*, HotCand*, int, uint64_t, void*, uint32_t*, uint32_t*,
-                     const uint32_t*, const uint32_t*, int, RegionOcc*, EngineCtl*, EngineCtl*);
+                     const uint32_t*, const uint32_t*, int, RegionOcc*, EngineCtl*, EngineCtl*, EngineCtl*, HotCand*);
 }  // namespace rlhip
 
 using namespace rlhip;
@@ -190,6 +190,9 @@ struct rl_engine {
   EngineCtl* h_ctl = nullptr;
   EngineCtl* h_ctl_s[HSLOTS] = {};
   hipEvent_t ev_done[HSLOTS] = {};            // the slot's batch complete (outputs copied, for host batches)
+  hipEvent_t ev_dd[HSLOTS] = {};              // device batch complete: device-scope release only (no
+                                              // system-scope cache write-back between batches)
+  hipEvent_t done_ev[HSLOTS] = {};            // the completion event recorded for the slot's batch
   hipEvent_t ev_in[HSLOTS] = {};              // host path: the slot's inputs copied in
   hipEvent_t ev_kern[HSLOTS] = {};            // host path: the slot's kernels done (D2H may start)
   hipEvent_t ev_front[2] = {};                // k4_hist of the device slot done (on front)
@@ -348,11 +351,12 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     EngineCtl* c4n = v4_ctl[(sub_seq + 2) % 3];  // batch seq+2's control block (k4_group clears it)
     // k4_hist runs on the front stream while the previous batch is still being decided (a
     // submit behind a batch in flight); otherwise, or when kernels are timed, on the engine stream
-    const bool split = !timing && n_fl > 0;
+    static const bool no_split = getenv("RL_DIAG_NO_SPLIT") != nullptr;  // diagnostics
+    const bool split = !timing && n_fl > 0 && !no_split;
     hipStream_t fs = split ? front : stream;
     if (split) {
       // slot buffers and control block free: batch seq-2 done
-      hipStreamWaitEvent(front, ev_done[(sub_seq + HSLOTS - 2) % HSLOTS], 0);
+      hipStreamWaitEvent(front, done_ev[(sub_seq + HSLOTS - 2) % HSLOTS], 0);
       if (in_ev) {
         hipStreamWaitEvent(front, in_ev, 0);
       } else if (!inputs_ready) {  // inputs come from work queued on the stream
@@ -396,14 +400,11 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     timed(KT_V4_GROUP, [&] {
       launch_v4_group(stream, b, v4_mrec, d_rules, tab, out, thr, v4_hb, v4_dfr, d_cand, want_cand ? 1 : 0,
                       cfg.hash_seed, v4_scratch, v4_heads, v4_ins, v4_heads + ng, v4_ins + (size_t)ng * 4, routed,
-                      d_occ, c4, c4n);
+                      d_occ, c4, c4n, h_ctl, want_cand ? h_cand : nullptr);
     });
+    // k4_group's last block writes the summary into h_ctl / h_cand (pinned host memory)
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
-    e = hipMemcpyAsync(h_ctl, c4, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
-    if (e == hipSuccess && want_cand)
-      e = hipMemcpyAsync(h_cand, d_cand, sizeof(HotCand) * CAND_MAX, hipMemcpyDeviceToHost, stream);
-    if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(ctl)");
     return 0;
   }
   if (in_ev) hipStreamWaitEvent(stream, in_ev, 0);
@@ -619,7 +620,7 @@ int rl_engine::enqueue_d2h(const Flight& f, hipStream_t s) {
 int rl_engine::settle(Flight& f) {
   h_ctl = h_ctl_s[f.slot];
   h_cand = h_cand_s[f.slot];
-  hipError_t e = timing ? hipStreamSynchronize(stream) : wait_event_polling(ev_done[f.slot]);
+  hipError_t e = timing ? hipStreamSynchronize(stream) : wait_event_polling(done_ev[f.slot]);
   if (e == hipSuccess && timing && f.host) e = hipStreamSynchronize(xout);
   if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
   uint32_t errs = h_ctl->err;
@@ -784,8 +785,13 @@ int rl_engine::submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, R
     if (e != hipSuccess) return hip_fail(e, "host path events");
     if ((rc = enqueue_d2h(f, xout)) != 0) return rc;
     e = hipEventRecord(ev_done[s], xout);
+    done_ev[s] = ev_done[s];
   } else {
-    e = hipEventRecord(ev_done[s], stream);
+    // outputs stay in device memory; the host summary was written with a system-scope
+    // release by k4_group (or copied by the LSD path's own D2H copy, ordered before this)
+    const bool dev_only = default_mode() == MODE_V4 && !reply && d.n_desc;
+    done_ev[s] = dev_only ? ev_dd[s] : ev_done[s];
+    e = hipEventRecord(done_ev[s], stream);
   }
   if (e != hipSuccess) return hip_fail(e, "hipEventRecord(done)");
   fl[n_fl++] = f;
@@ -937,6 +943,10 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     chk(hipEventCreateWithFlags(ev, hipEventDisableTiming));
     if (he == hipSuccess) chk(hipEventRecord(*ev, e->stream));
   }
+  for (int k = 0; k < HSLOTS; ++k) {
+    chk(hipEventCreateWithFlags(&e->ev_dd[k], hipEventDisableTiming | hipEventReleaseToDevice));
+    e->done_ev[k] = e->ev_done[k];
+  }
   if (he == hipSuccess) chk(hipMemset(e->zero_block, 0, e->zero_cap));
   if (he == hipSuccess) chk(hipDeviceSynchronize());
   if (he != hipSuccess) {
@@ -955,7 +965,7 @@ void rl_destroy(rl_engine* e) {
   for (hipEvent_t ev : {e->ev_front[0], e->ev_front[1], e->ev_ready, e->ev_hot})
     if (ev) hipEventDestroy(ev);
   for (int k = 0; k < HSLOTS; ++k) {
-    for (hipEvent_t ev : {e->ev_done[k], e->ev_in[k], e->ev_kern[k]})
+    for (hipEvent_t ev : {e->ev_done[k], e->ev_dd[k], e->ev_in[k], e->ev_kern[k]})
       if (ev) hipEventDestroy(ev);
     hipFree(e->d_hot_buf[k]);
     hipHostFree(e->h_cand_s[k]);

@@ -350,7 +350,8 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   for (int b = tid; b < ROW / 2; b += NT) trow[b] = reinterpret_cast<const uint32_t*>(sh_cnt)[b];
   unsigned long long* hrow = thsum + (size_t)tile * HOT_BUCKETS;
   for (int b = tid; b < HOT_BUCKETS; b += NT) hrow[b] = sh_hs[b];
-  if (tid < FP_PART_WORDS) fpart[(size_t)tile * FP_PART_WORDS + tid] = sh_f[tid];
+  // word-major ([word][tile]): k4_scan's hot blocks read each word of every tile coalesced
+  if (tid < FP_PART_WORDS) fpart[(size_t)tid * ntiles + tile] = sh_f[tid];
   if (tid == 0 && sh_err) atomicOr(&ctl->err, sh_err);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   STH(7);
@@ -435,7 +436,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
   uint32_t fv[FP_PART_WORDS];
 #pragma unroll
   for (int w = 0; w < FP_PART_WORDS; ++w)
-    fv[w] = hotb && tid < ntiles ? fpart[(size_t)tid * FP_PART_WORDS + w] : 0u;
+    fv[w] = hotb && tid < ntiles ? fpart[(size_t)w * ntiles + tid] : 0u;
   // Column pass. MSD blocks: bucket b = lane, tiles [wave*Q, wave*Q + Q). Hot blocks: bucket
   // b = lane % 16 of the block's 16, tile slice wave * 4 + lane / 16.
   const uint32_t m2 = blockIdx.x - HOT_SCAN_BLOCKS;  // MSD block: half m2 & 1 of group m2 / 2
@@ -497,7 +498,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     for (uint32_t g = tid + SCAN_NT; g < ntiles; g += SCAN_NT) {  // batches over SCAN_NT tiles
 #pragma unroll
       for (int w = 0; w < FP_PART_WORDS; ++w) {
-        const uint32_t x = fpart[(size_t)g * FP_PART_WORDS + w];
+        const uint32_t x = fpart[(size_t)w * ntiles + g];
         fv[w] = fp_is_max(w) ? (x > fv[w] ? x : fv[w]) : fv[w] + x;
       }
     }
@@ -1227,7 +1228,8 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
                                                  const uint32_t* __restrict__ scan_heads,
                                                  const uint32_t* __restrict__ scan_ins, uint32_t n_scan_heads,
                                                  const uint32_t* __restrict__ ranges, int routed,
-                                                 RegionOcc* __restrict__ occ, EngineCtl* ctl, EngineCtl* next_ctl) {
+                                                 RegionOcc* __restrict__ occ, EngineCtl* ctl, EngineCtl* next_ctl,
+                                                 EngineCtl* hctl, HotCand* hcand) {
   __shared__ MRec s_rec[G_CAP];
   __shared__ uint64_t s_P[G_CAP];
   __shared__ uint16_t s_list[G_CAP];
@@ -1489,7 +1491,10 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
   for (uint32_t i = tid; i < nc; i += G_NT) {
     HotCand c;
     ld_sc1_32B(&c, &cand[i]);
-    if (c.first_idx == 0xFFFFFFFFu) continue;  // a hot key: state already known
+    if (c.first_idx == 0xFFFFFFFFu) {  // a hot key: state already known
+      if (hcand) hcand[i] = c;
+      continue;
+    }
     const uint32_t d = c.first_idx;
     const uint32_t unit = rules[c.rule].unit;
     if (in.recs) {  // routed batch: the record already carries the prefix state
@@ -1503,6 +1508,18 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
     }
     c.unit = unit;
     cand[i] = c;
+    if (hcand) hcand[i] = c;
+  }
+  // The batch's summary straight into the host's pinned control block (header words and the
+  // candidate count): no device-to-host copy between this batch and the next one's kernels.
+  __syncthreads();  // ins / n_segments / n_inserted written above by threads 0..8
+  if (hctl) {
+    constexpr uint32_t HEAD = offsetof(EngineCtl, tile_ctr) / 4;
+    const uint32_t* cw = reinterpret_cast<const uint32_t*>(ctl);
+    uint32_t* hw = reinterpret_cast<uint32_t*>(hctl);
+    if (tid < HEAD) hw[tid] = ld_relaxed(&cw[tid]);
+    if (tid == HEAD) hctl->tile_ctr[CAND_CTR][0] = nc;
+    __threadfence_system();
   }
   uint32_t* z = reinterpret_cast<uint32_t*>(next_ctl);
   constexpr uint32_t words = sizeof(EngineCtl) / 4;
@@ -1559,7 +1576,7 @@ void launch_v4_group(hipStream_t st, const rl_batch& b, MRec* mrec, const DevRul
                      rl_status* out, uint32_t* req_thr, const HotBucket* hb, const Deferred* dfr, HotCand* cand,
                      int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads, uint32_t* wg_ins,
                      const uint32_t* scan_heads, const uint32_t* scan_ins, int routed, RegionOcc* occ, EngineCtl* ctl,
-                     EngineCtl* next_ctl) {
+                     EngineCtl* next_ctl, EngineCtl* hctl, HotCand* hcand) {
   using namespace v4;
   uint8_t* p = reinterpret_cast<uint8_t*>(scratch);
   GScratch4 gs;
@@ -1578,7 +1595,7 @@ void launch_v4_group(hipStream_t st, const rl_batch& b, MRec* mrec, const DevRul
   gs.end = reinterpret_cast<uint16_t*>(p);
   hipLaunchKernelGGL(k4_group, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), mrec, rules, tab, out, req_thr, hb,
                      dfr, cand, cand_on, seed, gs, wg_heads, wg_ins, scan_heads, scan_ins, (uint32_t)HOT_SCAN_BLOCKS,
-                     v4_ranges(scratch), routed, occ, ctl, next_ctl);
+                     v4_ranges(scratch), routed, occ, ctl, next_ctl, hctl, hcand);
 }
 
 }  // namespace rlhip

@@ -9,7 +9,7 @@
 #   4. tools/pmc_traffic.py -> gpurun_out/<tag>/pmc_traffic.json (per-kernel bytes per launch
 #      over the timed dispatches, tagged with bench.source_sha()).
 # Raw CSVs stay under /tmp on the box; only summaries come back.
-# usage (on the GPU box, from the repo root): tools/pmc_round.sh <tag> [steps]
+# usage (on the GPU box, from the repo root): tools/pmc_round.sh <tag> [steps] [trace-only]
 set -u
 TAG=$1
 STEPS=${2:-20}
@@ -25,6 +25,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $P/trace -o run --output-f
   > "$OUT/trace.json" 2> "$OUT/trace.err" || { echo "trace rc=$?"; tail -5 "$OUT/trace.err"; exit 1; }
 cp $P/trace/run_kernel_stats.csv "$OUT/kernel_stats.csv"
 python3 $R/tools/trace_summary.py $P/trace/run_kernel_trace.csv "$OUT/trace.json" $STEPS "$OUT/kernel_trace_summary.json" > /dev/null
+[ "${3:-}" = "trace-only" ] && exit 0
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum"; do
   i=$((i+1))
