@@ -63,7 +63,7 @@ void launch_v4_place(hipStream_t, const rl_batch&, const MRec*, const uint16_t*,
                      Deferred*, int, uint32_t*, EngineCtl*);
 void launch_v4_group(hipStream_t, const rl_batch&, MRec*, const DevRule*, const TableDesc&, rl_status*, uint32_t*,
                      const HotBucket*, const Deferred*, HotCand*, int, uint64_t, void*, uint32_t*, uint32_t*,
-                     const uint32_t*, const uint32_t*, int, RegionOcc*, EngineCtl*, EngineCtl*, EngineCtl*, HotCand*);
+                     const uint32_t*, const uint32_t*, int, RegionOcc*, EngineCtl*, EngineCtl*, EngineCtl*, HotCand*, const MRec*, const uint16_t*);
 }  // namespace rlhip
 
 using namespace rlhip;
@@ -400,7 +400,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     timed(KT_V4_GROUP, [&] {
       launch_v4_group(stream, b, v4_mrec, d_rules, tab, out, thr, v4_hb, v4_dfr, d_cand, want_cand ? 1 : 0,
                       cfg.hash_seed, v4_scratch, v4_heads, v4_ins, v4_heads + ng, v4_ins + (size_t)ng * 4, routed,
-                      d_occ, c4, c4n, h_ctl, want_cand ? h_cand : nullptr);
+                      d_occ, c4, c4n, h_ctl, want_cand ? h_cand : nullptr, srt, v4_tcount[sl]);
     });
     // k4_group's last block writes the summary into h_ctl / h_cand (pinned host memory)
     e = hipGetLastError();

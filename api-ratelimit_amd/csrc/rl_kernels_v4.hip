@@ -1091,24 +1091,16 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
                                                MRec* __restrict__ mrec, rl_status* __restrict__ out,
                                                uint32_t* __restrict__ req_thr, Deferred* __restrict__ dfr, int routed,
                                                uint32_t* __restrict__ poison, EngineCtl* ctl) {
-  __shared__ uint16_t s_row[ROW];
-  __shared__ uint16_t s_toff[MSD_BUCKETS];
-  __shared__ uint32_t s_gpre[MSD_GROUPS];
+  __shared__ __attribute__((aligned(16))) uint16_t s_row[HOT_BUCKETS + 8];
   __shared__ uint32_t s_rstar[HOT_BUCKETS];
   __shared__ uint32_t s_err;
   const uint32_t tid = threadIdx.x;
   const uint32_t t = blockIdx.x, t0 = t * T;
   if (tid == 0) s_err = ctl->err;
-  {
+  {  // the hot part of the tile's row of bucket starts (MSD records stay where k4_hist put
+     // them: k4_group gathers its ranges from the tile-sorted records)
     const uint32_t* rsrc = reinterpret_cast<const uint32_t*>(tstart + (size_t)t * ROW);
-    for (int k = tid; k < ROW / 2; k += NT) reinterpret_cast<uint32_t*>(s_row)[k] = rsrc[k];
-    const uint32_t* osrc = reinterpret_cast<const uint32_t*>(toff + (size_t)t * MSD_BUCKETS);
-    for (int k = tid; k < MSD_BUCKETS / 2; k += NT) reinterpret_cast<uint32_t*>(s_toff)[k] = osrc[k];
-  }
-  if (tid < 64) {  // group bases: exclusive prefix of the group totals (one wave)
-    const uint32_t v = tid < (uint32_t)MSD_GROUPS ? ranges[R_GTOT + tid] : 0u;
-    const uint32_t incl = tile::wave_incl_scan<uint32_t>(v);
-    if (tid < (uint32_t)MSD_GROUPS) s_gpre[tid] = incl - v;
+    for (int k = tid; k < (HOT_BUCKETS + 8) / 2; k += NT) reinterpret_cast<uint32_t*>(s_row)[k] = rsrc[k];
   }
   if (local_cache)
     for (int b = tid; b < HOT_BUCKETS; b += NT) s_rstar[b] = 0xFFFFFFFFu;
@@ -1126,17 +1118,9 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
         *hot_counter(x) = (uint32_t)(x.base + x.total);
     }
   }
-  const uint32_t nhot = s_row[HOT_BUCKETS], nrec = s_row[NIL_BUCKET];
+  const uint32_t nhot = s_row[HOT_BUCKETS];
   const MRec* src = srec + t0;
   const unsigned long long* hrow = hoff + (size_t)t * HOT_BUCKETS;
-  // MSD records: scattered to bucket order (arrival order inside a bucket: tiles in order,
-  // the tile's run in order)
-  for (uint32_t p = nhot + tid; p < nrec; p += NT) {
-    const MRec m = src[p];
-    const uint32_t mb = tile::msd_bucket(m.key);
-    const uint32_t pos = s_gpre[mb >> 6] + ranges[R_BPRE + mb] + s_toff[mb] + (p - s_row[HOT_BUCKETS + mb]);
-    mrec[pos] = m;
-  }
   if (nhot == 0) return;  // block-uniform
   if (local_cache) {
     // The descriptor whose INCRBY reply first exceeds the limit freezes the key
@@ -1209,6 +1193,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
 // the hot-set candidates and clears the next batch's control block.
 // ---------------------------------------------------------------------------
 struct GScratch4 {
+  MRec* rec;       // [GBLOCKS][BUCKET_CAP] an oversized bucket's records, gathered
   uint64_t* P;     // [GBLOCKS][BUCKET_CAP]
   uint16_t* list;  // [GBLOCKS][BUCKET_CAP]
   uint16_t* grp;   // [GBLOCKS][BUCKET_CAP]
@@ -1217,6 +1202,64 @@ struct GScratch4 {
   uint16_t* end;   // [GBLOCKS][GS_HASH]
   uint32_t* cursor;  // [GBLOCKS]
 };
+
+// The records of MSD buckets [B0, B1) in arrival order, gathered straight from the
+// tile-sorted records k4_hist wrote: inside a tile the range is one contiguous run, and runs
+// taken tile by tile keep every key's records in arrival order (a key lives in one bucket).
+// dst[0, m): the LDS stage or a block's global scratch. GATHER_T tiles per chunk: their run
+// starts and exclusive prefix in LDS, then every output position finds its tile by binary
+// search and all of a thread's record loads are in flight together.
+constexpr int GATHER_T = 512;
+constexpr int GATHER_TPT = GATHER_T / G_NT;
+constexpr int GATHER_PPT = (BUCKET_CAP + G_NT - 1) / G_NT;  // output positions per thread
+RL_DEV void gather_runs(const MRec* __restrict__ srec, const uint16_t* __restrict__ tstart, uint32_t ntiles,
+                        uint32_t B0, uint32_t B1, MRec* dst, uint16_t* s_ra, uint16_t* s_pre, uint32_t* sh_w) {
+  const uint32_t tid = threadIdx.x;
+  uint32_t done = 0;
+  for (uint32_t c0 = 0; c0 < ntiles; c0 += GATHER_T) {
+    const uint32_t nt = min((uint32_t)GATHER_T, ntiles - c0);
+    uint32_t a[GATHER_TPT], l[GATHER_TPT], sum = 0;
+#pragma unroll
+    for (int q = 0; q < GATHER_TPT; ++q) {
+      const uint32_t t = tid * GATHER_TPT + q;
+      const uint16_t* row = tstart + (size_t)(c0 + min(t, nt - 1u)) * ROW;
+      const uint32_t x0 = row[B0], x1 = row[B1];
+      a[q] = x0;
+      l[q] = t < nt ? x1 - x0 : 0u;
+      sum += l[q];
+    }
+    uint32_t tot;
+    uint32_t run = tile::block_excl_scan<G_NT>(sum, sh_w, tot);
+#pragma unroll
+    for (int q = 0; q < GATHER_TPT; ++q) {
+      s_ra[tid * GATHER_TPT + q] = (uint16_t)a[q];
+      s_pre[tid * GATHER_TPT + q] = (uint16_t)run;
+      run += l[q];
+    }
+    __syncthreads();
+    if (tot) {  // block-uniform
+      MRec v[GATHER_PPT];
+      uint32_t ps[GATHER_PPT];
+#pragma unroll
+      for (int u = 0; u < GATHER_PPT; ++u) {
+        const uint32_t p = min(tid + u * G_NT, tot - 1u);
+        uint32_t lo = 0, hi = GATHER_T;  // last tile whose prefix is <= p (its run holds p)
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (s_pre[mid] <= p) lo = mid;
+          else hi = mid;
+        }
+        ps[u] = p;
+        v[u] = srec[(size_t)(c0 + lo) * T + s_ra[lo] + (p - s_pre[lo])];
+      }
+#pragma unroll
+      for (int u = 0; u < GATHER_PPT; ++u)
+        if (tid + u * G_NT < tot) dst[done + ps[u]] = v[u];
+    }
+    done += tot;
+    __syncthreads();  // s_ra / s_pre of the next chunk
+  }
+}
 
 __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __restrict__ mrec,
                                                  const DevRule* __restrict__ rules, TableDesc tab,
@@ -1229,9 +1272,14 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
                                                  const uint32_t* __restrict__ scan_ins, uint32_t n_scan_heads,
                                                  const uint32_t* __restrict__ ranges, int routed,
                                                  RegionOcc* __restrict__ occ, EngineCtl* ctl, EngineCtl* next_ctl,
-                                                 EngineCtl* hctl, HotCand* hcand) {
+                                                 EngineCtl* hctl, HotCand* hcand,
+                                                 const MRec* __restrict__ srec, const uint16_t* __restrict__ tstart,
+                                                 uint32_t ntiles) {
   __shared__ MRec s_rec[G_CAP];
   __shared__ uint64_t s_P[G_CAP];
+  static_assert(sizeof(uint64_t) * G_CAP >= 4 * GATHER_T, "the gather's run tables alias s_P");
+  uint16_t* const s_ra = reinterpret_cast<uint16_t*>(s_P);  // only while a range is gathered
+  uint16_t* const s_pre = s_ra + GATHER_T;
   __shared__ uint16_t s_list[G_CAP];
   __shared__ uint16_t s_grp[G_CAP];
   __shared__ uint32_t s_slot[G_HASH];
@@ -1306,6 +1354,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
       const uint32_t r1 = k1 == 64u ? s_gpre[g + 1] : s_gpre[g] + ranges[R_BPRE + g * 64 + k1];
       const uint32_t m = r1 - r0;
       if (m == 0) continue;
+      const uint32_t B0 = HOT_BUCKETS + g * 64u + k0, B1 = HOT_BUCKETS + g * 64u + k1;
       __syncthreads();  // the previous range is done with LDS
       if (m <= (uint32_t)G_CAP && split_half < 0) {
         for (uint32_t s = tid; s < (uint32_t)G_HASH; s += G_NT) {
@@ -1313,12 +1362,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
           s_cnt[s] = 0;
         }
         if (tid == 0) s_cursor = 0;
-        const MRec* src = mrec + r0;
-#pragma unroll
-        for (int u = 0; u < G_IPT; ++u) {
-          const uint32_t k = tid + u * G_NT;
-          if (k < m) s_rec[k] = src[k];
-        }
+        gather_runs(srec, tstart, ntiles, B0, B1, s_rec, s_ra, s_pre, sh_w);
         __syncthreads();
         ST4(2);
         const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
@@ -1338,7 +1382,10 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
       ST4X(0, m);
       constexpr int SPLIT_BIT = 64 - 3 - MSD_BITS - 1;
       constexpr int SU = BUCKET_CAP / G_NT;
-      const MRec* src = mrec + r0;
+      MRec* const src = gs.rec + (size_t)j * BUCKET_CAP;  // the bucket, gathered (<= BUCKET_CAP records)
+      gather_runs(srec, tstart, ntiles, B0, B1, src, s_ra, s_pre, sh_w);
+      __threadfence_block();
+      __syncthreads();
       auto half_of = [&](uint32_t k) -> uint32_t {
         return k < m ? (uint32_t)(__builtin_nontemporal_load(&src[k].key) >> SPLIT_BIT) & 1u : 2u;
       };
@@ -1375,7 +1422,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
       } else if (split_half != 1) {
         // grouped in place in bucket order (global scratch); for a split bucket by its half-0
         // range's block (the half-1 block has nothing to do)
-        const GS gg{mrec + r0,                        gs.P + (size_t)j * BUCKET_CAP,
+        const GS gg{src,                              gs.P + (size_t)j * BUCKET_CAP,
                     gs.list + (size_t)j * BUCKET_CAP,  gs.grp + (size_t)j * BUCKET_CAP,
                     gs.slot + (size_t)j * GS_HASH,     gs.cnt + (size_t)j * GS_HASH,
                     gs.end + (size_t)j * GS_HASH,      gs.cursor + j,
@@ -1538,8 +1585,8 @@ uint32_t v4_group_blocks(uint32_t) { return v4::GBLOCKS; }
 uint32_t v4_scan_blocks() { return v4::HOT_SCAN_BLOCKS + v4::MSD_SCAN_BLOCKS; }
 size_t v4_scratch_bytes() {
   using namespace v4;
-  return (size_t)GBLOCKS * BUCKET_CAP * (8 + 2 + 2) + (size_t)GBLOCKS * GS_HASH * (4 + 4 + 2) + (size_t)GBLOCKS * 4 +
-         RANGE_WORDS * 4 + 1024;
+  return (size_t)GBLOCKS * BUCKET_CAP * (sizeof(MRec) + 8 + 2 + 2) + (size_t)GBLOCKS * GS_HASH * (4 + 4 + 2) +
+         (size_t)GBLOCKS * 4 + RANGE_WORDS * 4 + 1024;
 }
 static uint32_t* v4_ranges(void* scratch) {  // the last RANGE_WORDS words (+ slack) of the scratch
   return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(scratch) + v4_scratch_bytes() - 1024 -
@@ -1576,10 +1623,13 @@ void launch_v4_group(hipStream_t st, const rl_batch& b, MRec* mrec, const DevRul
                      rl_status* out, uint32_t* req_thr, const HotBucket* hb, const Deferred* dfr, HotCand* cand,
                      int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads, uint32_t* wg_ins,
                      const uint32_t* scan_heads, const uint32_t* scan_ins, int routed, RegionOcc* occ, EngineCtl* ctl,
-                     EngineCtl* next_ctl, EngineCtl* hctl, HotCand* hcand) {
+                     EngineCtl* next_ctl, EngineCtl* hctl, HotCand* hcand, const MRec* srec,
+                     const uint16_t* tstart) {
   using namespace v4;
   uint8_t* p = reinterpret_cast<uint8_t*>(scratch);
   GScratch4 gs;
+  gs.rec = reinterpret_cast<MRec*>(p);
+  p += (size_t)GBLOCKS * BUCKET_CAP * sizeof(MRec);
   gs.P = reinterpret_cast<uint64_t*>(p);
   p += (size_t)GBLOCKS * BUCKET_CAP * 8;
   gs.slot = reinterpret_cast<uint32_t*>(p);
@@ -1595,7 +1645,7 @@ void launch_v4_group(hipStream_t st, const rl_batch& b, MRec* mrec, const DevRul
   gs.end = reinterpret_cast<uint16_t*>(p);
   hipLaunchKernelGGL(k4_group, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), mrec, rules, tab, out, req_thr, hb,
                      dfr, cand, cand_on, seed, gs, wg_heads, wg_ins, scan_heads, scan_ins, (uint32_t)HOT_SCAN_BLOCKS,
-                     v4_ranges(scratch), routed, occ, ctl, next_ctl, hctl, hcand);
+                     v4_ranges(scratch), routed, occ, ctl, next_ctl, hctl, hcand, srec, tstart, v4_tiles(b.n_desc));
 }
 
 }  // namespace rlhip
