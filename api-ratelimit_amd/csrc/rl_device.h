@@ -87,23 +87,42 @@ RL_DEV int64_t div_const(int64_t now, uint32_t unit) {
   }
 }
 
-RL_DEV uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t o = __shfl_xor(v, d, 64);
-    v = o < v ? o : v;
-  }
-  return v;
+// Whole-wave reductions and scans with DPP lane moves (VALU, no LDS round trip per step):
+// quad swaps, row_shr 4 / 8 (bound_ctrl: out-of-row lanes read 0), then row_bcast 15 / 31 over
+// the rows; the result is in lane 63. All 64 lanes must be active.
+template <int CTRL, int ROWM = 0xF, bool BOUND0 = true>
+RL_DEV uint32_t dpp_mov(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWM, 0xF, BOUND0);
 }
 RL_DEV uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t o = __shfl_xor(v, d, 64);
-    v = o > v ? o : v;
-  }
+  v = max(v, dpp_mov<0xB1>(v));  // quad_perm [1,0,3,2]
+  v = max(v, dpp_mov<0x4E>(v));  // quad_perm [2,3,0,1]
+  v = max(v, dpp_mov<0x114>(v));  // row_shr:4
+  v = max(v, dpp_mov<0x118>(v));  // row_shr:8
+  v = max(v, dpp_mov<0x142, 0xA, false>(v));  // row_bcast:15 into rows 1, 3
+  v = max(v, dpp_mov<0x143, 0xC, false>(v));  // row_bcast:31 into rows 2, 3
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+RL_DEV uint32_t wave_min_u32(uint32_t v) { return ~wave_max_u32(~v); }
+RL_DEV uint32_t wave_sum_u32(uint32_t v) {
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
+  v += dpp_mov<0x114>(v);
+  v += dpp_mov<0x118>(v);
+  v += dpp_mov<0x142, 0xA, false>(v);
+  v += dpp_mov<0x143, 0xC, false>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// Inclusive scan: row_shr 1, 2, 4, 8 inside each row of 16, then the row carries.
+RL_DEV uint32_t wave_incl_scan_u32(uint32_t v) {
+  v += dpp_mov<0x111>(v);
+  v += dpp_mov<0x112>(v);
+  v += dpp_mov<0x114>(v);
+  v += dpp_mov<0x118>(v);
+  v += dpp_mov<0x142, 0xA, false>(v);
+  v += dpp_mov<0x143, 0xC, false>(v);
   return v;
 }
-
 
 RL_DEV void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 

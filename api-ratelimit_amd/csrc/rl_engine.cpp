@@ -55,15 +55,20 @@ uint32_t v4_scan_blocks();
 size_t v4_scratch_bytes();
 void launch_v4_hist(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, const HotEntry*, uint32_t*,
                     uint32_t*, uint16_t*, unsigned long long*, MRec*, rl_status*, EngineCtl*);
-void launch_v4_scan(hipStream_t, uint32_t, const uint16_t*, const unsigned long long*, unsigned long long*,
-                    const uint32_t*, const HotEntry*, HotBucket*, const TableDesc&, HotCand*, uint32_t*, uint32_t*,
-                    uint16_t*, void*, const uint32_t*, const RegionOcc*, EngineCtl*);
-void launch_v4_place(hipStream_t, const rl_batch&, const MRec*, const uint16_t*, const uint16_t*, void*,
-                     const DevRule*, const unsigned long long*, HotBucket*, int, MRec*, rl_status*, uint32_t*,
-                     Deferred*, int, uint32_t*, EngineCtl*);
-void launch_v4_group(hipStream_t, const rl_batch&, MRec*, const DevRule*, const TableDesc&, rl_status*, uint32_t*,
-                     const HotBucket*, const Deferred*, HotCand*, int, uint64_t, void*, uint32_t*, uint32_t*,
-                     const uint32_t*, const uint32_t*, int, RegionOcc*, EngineCtl*, EngineCtl*, EngineCtl*, HotCand*, const MRec*, const uint16_t*);
+void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const unsigned long long* thsum,
+                    unsigned long long* hoff, const uint32_t* fpart, const HotEntry* hot_list, HotBucket* hb,
+                    const TableDesc& tab, HotCand* cand, uint32_t* heads_out, uint32_t* ins_out, void* scratch,
+                    const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl);
+void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart,
+                     void* scratch, const DevRule* rules, const unsigned long long* hoff, HotBucket* hb,
+                     int local_cache, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
+                     uint32_t* poison, EngineCtl* ctl);
+void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, const TableDesc& tab,
+                     rl_status* out, uint32_t* req_thr, const HotBucket* hb, const Deferred* dfr, HotCand* cand,
+                     int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads, uint32_t* wg_ins,
+                     const uint32_t* scan_heads, const uint32_t* scan_ins, int routed, RegionOcc* occ, EngineCtl* ctl,
+                     EngineCtl* next_ctl, EngineCtl* hctl, HotCand* hcand, const MRec* srec,
+                     const uint16_t* tstart);
 }  // namespace rlhip
 
 using namespace rlhip;
@@ -175,9 +180,7 @@ struct rl_engine {
   unsigned long long* v4_thsum[2] = {};       // [tile][HOT_BUCKETS] hot h sums
   MRec* v4_srt[2] = {};                       // tile-sorted records
   uint32_t* v4_fpart[2] = {};                 // per-tile fingerprint partials
-  uint16_t* v4_toff = nullptr;                // [tile][MSD_BUCKETS] records of the bucket in earlier tiles
   unsigned long long* v4_hoff = nullptr;      // [tile][HOT_BUCKETS] exclusive h prefix over tiles
-  MRec* v4_mrec = nullptr;                    // MSD records in bucket order
   Deferred* v4_dfr = nullptr;                 // deferred hot descriptors
   HotBucket* v4_hb = nullptr;                 // per hot bucket batch state
   void* v4_scratch = nullptr;                 // k4_group global scratch + k4_scan ranges
@@ -391,14 +394,14 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     }
     timed(KT_V4_SCAN, [&] {
       launch_v4_scan(stream, n, v4_tcount[sl], v4_thsum[sl], v4_hoff, v4_fpart[sl], hot_t + HOT_SLOTS, v4_hb, tab,
-                     d_cand, v4_heads + ng, v4_ins + (size_t)ng * 4, v4_toff, v4_scratch, d_poison, d_occ, c4);
+                     d_cand, v4_heads + ng, v4_ins + (size_t)ng * 4, v4_scratch, d_poison, d_occ, c4);
     });
     timed(KT_V4_PLACE, [&] {
-      launch_v4_place(stream, b, srt, v4_tcount[sl], v4_toff, v4_scratch, d_rules, v4_hoff, v4_hb, lc, v4_mrec, out,
+      launch_v4_place(stream, b, srt, v4_tcount[sl], v4_scratch, d_rules, v4_hoff, v4_hb, lc, out,
                       thr, v4_dfr, routed, d_poison, c4);
     });
     timed(KT_V4_GROUP, [&] {
-      launch_v4_group(stream, b, v4_mrec, d_rules, tab, out, thr, v4_hb, v4_dfr, d_cand, want_cand ? 1 : 0,
+      launch_v4_group(stream, b, d_rules, tab, out, thr, v4_hb, v4_dfr, d_cand, want_cand ? 1 : 0,
                       cfg.hash_seed, v4_scratch, v4_heads, v4_ins, v4_heads + ng, v4_ins + (size_t)ng * 4, routed,
                       d_occ, c4, c4n, h_ctl, want_cand ? h_cand : nullptr, srt, v4_tcount[sl]);
     });
@@ -917,9 +920,7 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
       chk(hipMalloc(&e->v4_srt[k], N * sizeof(MRec) + 64));
       chk(hipMalloc(&e->v4_fpart[k], T4 * FP_PART_WORDS * 4 + 64));
     }
-    chk(hipMalloc(&e->v4_toff, T4 * MSD_BUCKETS * 2));
     chk(hipMalloc(&e->v4_hoff, T4 * HOT_BUCKETS * 8));
-    chk(hipMalloc(&e->v4_mrec, N * sizeof(MRec) + 64));
     chk(hipMalloc(&e->v4_dfr, N * sizeof(Deferred) + 64));
     chk(hipMalloc(&e->v4_hb, HOT_BUCKETS * sizeof(HotBucket)));
     const size_t nb = (size_t)v4_group_blocks((uint32_t)N) + v4_scan_blocks();
@@ -986,7 +987,7 @@ void rl_destroy(rl_engine* e) {
     hipFree(e->v4_fpart[k]);
   }
   for (int k = 0; k < 3; ++k) hipFree(e->v4_ctl[k]);
-  for (void* p : {(void*)e->v4_toff, (void*)e->v4_hoff, (void*)e->v4_mrec, (void*)e->v4_dfr, (void*)e->v4_hb,
+  for (void* p : {(void*)e->v4_hoff, (void*)e->v4_dfr, (void*)e->v4_hb,
                   (void*)e->v4_heads, (void*)e->v4_ins, e->v4_scratch, (void*)e->d_poison, (void*)e->d_tree_nodes,
                   (void*)e->d_tree_slots, (void*)e->d_tree_names, (void*)e->d_res, (void*)e->table, (void*)e->d_occ,
                   (void*)e->d_rules, (void*)e->keys_orig, (void*)e->keys_a, (void*)e->keys_b, (void*)e->vals_a,

@@ -391,16 +391,16 @@ RL_DEV void column_counts(const uint16_t* __restrict__ tstart, uint32_t b, uint3
   const uint32_t lane = threadIdx.x & 63;
   uint32_t e[SCAN_Q];
 #pragma unroll
-  for (int u = 0; u < SCAN_Q; ++u) {
-    const uint16_t* row = tstart + (size_t)(tb + u) * ROW;
-    const bool v = tb + u < te;
-    cq[u] = v ? (uint32_t)row[b] : 0u;
-    e[u] = v ? (uint32_t)row[b0 + MSD_HALF] : 0u;
+  for (int u = 0; u < SCAN_Q; ++u) {  // clamped tiles: all loads in flight together
+    const uint16_t* row = tstart + (size_t)min(tb + u, te - 1u) * ROW;
+    cq[u] = row[b];
+    e[u] = row[b0 + MSD_HALF];
   }
 #pragma unroll
   for (int u = 0; u < SCAN_Q; ++u) {
     const uint32_t nx = __shfl_down(cq[u], 1, MSD_HALF);
-    cq[u] = ((lane & (MSD_HALF - 1u)) < MSD_HALF - 1u ? nx : e[u]) - cq[u];
+    const uint32_t d = ((lane & (MSD_HALF - 1u)) < MSD_HALF - 1u ? nx : e[u]) - cq[u];
+    cq[u] = tb + u < te ? d : 0u;
   }
 }
 
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
                                                    const HotEntry* __restrict__ hot_list, HotBucket* __restrict__ hb,
                                                    TableDesc tab, HotCand* __restrict__ cand,
                                                    uint32_t* __restrict__ heads_out, uint32_t* __restrict__ ins_out,
-                                                   uint16_t* __restrict__ toff, uint32_t* __restrict__ ranges,
+                                                   uint32_t* __restrict__ ranges,
                                                    const uint32_t* __restrict__ poison,
                                                    const RegionOcc* __restrict__ occ, EngineCtl* ctl) {
   const uint32_t local_cache = tab.local_cache;
@@ -454,26 +454,31 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
   // Columns up to SCAN_Q (MSD) / HOT_Q (hot) tiles per lane are loaded once, all loads in
   // flight together, and kept in registers for the prefix pass below.
   const bool in_regs = Q <= (uint32_t)(hotb ? HOT_Q : SCAN_Q);  // block-uniform
-  uint32_t cpk[SCAN_Q / 2];  // MSD: counts (<= T each) packed in u16 pairs
   unsigned long long hq[HOT_Q];  // hot: h sums
   if (in_regs && hotb) {
+    // every load at a clamped tile, so all of them are in flight together (a load behind a
+    // per-lane condition waits for the one before it)
+    uint32_t r0[HOT_Q], r1[HOT_Q];
 #pragma unroll
     for (int u = 0; u < HOT_Q; ++u) {
-      const uint32_t t = tb + u;
+      const uint32_t t = min(tb + u, ntiles - 1u);
       const uint16_t* row = tstart + (size_t)t * ROW + b;
-      const bool v = t < te;
-      c += v ? (uint32_t)row[1] - (uint32_t)row[0] : 0u;
-      hq[u] = v ? thsum[(size_t)t * HOT_BUCKETS + b] : 0ull;
+      r0[u] = row[0];
+      r1[u] = row[1];
+      hq[u] = thsum[(size_t)t * HOT_BUCKETS + b];
     }
 #pragma unroll
-    for (int u = 0; u < HOT_Q; ++u) hs += hq[u];
+    for (int u = 0; u < HOT_Q; ++u) {
+      const bool v = tb + u < te;
+      c += v ? r1[u] - r0[u] : 0u;
+      hq[u] = v ? hq[u] : 0ull;
+      hs += hq[u];
+    }
   } else if (in_regs) {
     uint32_t cq[SCAN_Q];
     column_counts(tstart, b, mb0, tb, te, cq);
 #pragma unroll
     for (int u = 0; u < SCAN_Q; ++u) c += cq[u];
-#pragma unroll
-    for (int u = 0; u < SCAN_Q / 2; ++u) cpk[u] = cq[2 * u] | (cq[2 * u + 1] << 16);
   } else {
     for (uint32_t t = tb; t < te; t += SCAN_U) {
       uint32_t cv[SCAN_U];
@@ -532,7 +537,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
       if (tid == 0 && !cap_ok) atomicOr(&ctl->err, ERR_TABLE_FULL);
     }
   }
-  uint32_t ctot = 0, crun = 0;
+  uint32_t ctot = 0;
   unsigned long long hrun = 0, htot = 0;
   if (hotb) {  // bucket totals over the 64 slices; h sums of the slices before this lane's
 #pragma unroll
@@ -547,43 +552,17 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
         hrun += sl < slice ? y : 0ull;
       }
     }
-  } else {  // bucket totals over the 32 slices; counts of the slices before this lane's
+  } else {  // bucket totals over the 32 slices
 #pragma unroll
     for (int w = 0; w < SCAN_W; ++w) {
 #pragma unroll
-      for (int q = 0; q < 64 / MSD_HALF; ++q) {
-        const uint32_t sl = (uint32_t)(w * (64 / MSD_HALF) + q);
-        const uint32_t x = s_pc[w][q * MSD_HALF + bb];
-        ctot += x;
-        crun += sl < slice ? x : 0u;
-      }
+      for (int q = 0; q < 64 / MSD_HALF; ++q) ctot += s_pc[w][q * MSD_HALF + bb];
     }
   }
   if (!hotb) {
-    // per (tile, MSD bucket): the records of the bucket in earlier tiles (u16: a bucket holds
-    // at most BUCKET_CAP records on this path; a larger one sends the batch to the LSD pipeline
-    // before anything touches the table)
+    // (no per-tile offsets: k4_group gathers a range's records from each tile's run. A bucket
+    // over BUCKET_CAP records sends the batch to the LSD pipeline before the table is touched.)
     const uint32_t mb = b - HOT_BUCKETS;
-    if (in_regs) {
-#pragma unroll
-      for (int u = 0; u < SCAN_Q; ++u) {
-        if (tb + u < te) toff[(size_t)(tb + u) * MSD_BUCKETS + mb] = (uint16_t)crun;
-        crun += (cpk[u >> 1] >> (16 * (u & 1))) & 0xFFFFu;
-      }
-    }
-    for (uint32_t t = in_regs ? te : tb; t < te; t += SCAN_U) {
-      uint32_t cv[SCAN_U];
-#pragma unroll
-      for (int u = 0; u < SCAN_U; ++u) {
-        const uint16_t* row = tstart + (size_t)(t + u) * ROW + b;
-        cv[u] = t + u < te ? (uint32_t)row[1] - (uint32_t)row[0] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < SCAN_U; ++u) {
-        if (t + u < te) toff[(size_t)(t + u) * MSD_BUCKETS + mb] = (uint16_t)crun;
-        crun += cv[u];
-      }
-    }
     if (wave != 0) return;
     ST5(3);
     if (lane == 0) heads_out[blockIdx.x] = 0;
@@ -1083,12 +1062,11 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restrict__ srec,
                                                const uint16_t* __restrict__ tstart,
-                                               const uint16_t* __restrict__ toff,
                                                const uint32_t* __restrict__ ranges,
                                                const DevRule* __restrict__ rules,
                                                const unsigned long long* __restrict__ hoff,
                                                HotBucket* __restrict__ hb, int local_cache,
-                                               MRec* __restrict__ mrec, rl_status* __restrict__ out,
+                                               rl_status* __restrict__ out,
                                                uint32_t* __restrict__ req_thr, Deferred* __restrict__ dfr, int routed,
                                                uint32_t* __restrict__ poison, EngineCtl* ctl) {
   __shared__ __attribute__((aligned(16))) uint16_t s_row[HOT_BUCKETS + 8];
@@ -1211,7 +1189,7 @@ struct GScratch4 {
 // search and all of a thread's record loads are in flight together.
 constexpr int GATHER_T = 512;
 constexpr int GATHER_TPT = GATHER_T / G_NT;
-constexpr int GATHER_PPT = (BUCKET_CAP + G_NT - 1) / G_NT;  // output positions per thread
+template <int PPT>  // output positions per thread: m <= PPT * G_NT
 RL_DEV void gather_runs(const MRec* __restrict__ srec, const uint16_t* __restrict__ tstart, uint32_t ntiles,
                         uint32_t B0, uint32_t B1, MRec* dst, uint16_t* s_ra, uint16_t* s_pre, uint32_t* sh_w) {
   const uint32_t tid = threadIdx.x;
@@ -1220,7 +1198,7 @@ RL_DEV void gather_runs(const MRec* __restrict__ srec, const uint16_t* __restric
     const uint32_t nt = min((uint32_t)GATHER_T, ntiles - c0);
     uint32_t a[GATHER_TPT], l[GATHER_TPT], sum = 0;
 #pragma unroll
-    for (int q = 0; q < GATHER_TPT; ++q) {
+    for (int q = 0; q < GATHER_TPT; ++q) {  // clamped tiles: the loads go out together
       const uint32_t t = tid * GATHER_TPT + q;
       const uint16_t* row = tstart + (size_t)(c0 + min(t, nt - 1u)) * ROW;
       const uint32_t x0 = row[B0], x1 = row[B1];
@@ -1238,30 +1216,31 @@ RL_DEV void gather_runs(const MRec* __restrict__ srec, const uint16_t* __restric
     }
     __syncthreads();
     if (tot) {  // block-uniform
-      MRec v[GATHER_PPT];
-      uint32_t ps[GATHER_PPT];
+      // the last tile whose prefix is <= p holds p (zero-length runs share a prefix with the
+      // next tile); all PPT searches step together, one LDS read each per halving
+      uint32_t p[PPT], lo[PPT];
 #pragma unroll
-      for (int u = 0; u < GATHER_PPT; ++u) {
-        const uint32_t p = min(tid + u * G_NT, tot - 1u);
-        uint32_t lo = 0, hi = GATHER_T;  // last tile whose prefix is <= p (its run holds p)
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (s_pre[mid] <= p) lo = mid;
-          else hi = mid;
-        }
-        ps[u] = p;
-        v[u] = srec[(size_t)(c0 + lo) * T + s_ra[lo] + (p - s_pre[lo])];
+      for (int u = 0; u < PPT; ++u) {
+        p[u] = min(tid + u * G_NT, tot - 1u);
+        lo[u] = 0;
       }
 #pragma unroll
-      for (int u = 0; u < GATHER_PPT; ++u)
-        if (tid + u * G_NT < tot) dst[done + ps[u]] = v[u];
+      for (uint32_t step = GATHER_T / 2; step >= 1; step >>= 1)
+#pragma unroll
+        for (int u = 0; u < PPT; ++u) lo[u] = s_pre[lo[u] + step] <= p[u] ? lo[u] + step : lo[u];
+      MRec v[PPT];
+#pragma unroll
+      for (int u = 0; u < PPT; ++u) v[u] = srec[(size_t)(c0 + lo[u]) * T + s_ra[lo[u]] + (p[u] - s_pre[lo[u]])];
+#pragma unroll
+      for (int u = 0; u < PPT; ++u)
+        if (tid + u * G_NT < tot) dst[done + p[u]] = v[u];
     }
     done += tot;
     __syncthreads();  // s_ra / s_pre of the next chunk
   }
 }
 
-__global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __restrict__ mrec,
+__global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
                                                  const DevRule* __restrict__ rules, TableDesc tab,
                                                  rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
                                                  const HotBucket* __restrict__ hb, const Deferred* __restrict__ dfr,
@@ -1362,7 +1341,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
           s_cnt[s] = 0;
         }
         if (tid == 0) s_cursor = 0;
-        gather_runs(srec, tstart, ntiles, B0, B1, s_rec, s_ra, s_pre, sh_w);
+        gather_runs<G_IPT>(srec, tstart, ntiles, B0, B1, s_rec, s_ra, s_pre, sh_w);
         __syncthreads();
         ST4(2);
         const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
@@ -1383,7 +1362,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in, MRec* __
       constexpr int SPLIT_BIT = 64 - 3 - MSD_BITS - 1;
       constexpr int SU = BUCKET_CAP / G_NT;
       MRec* const src = gs.rec + (size_t)j * BUCKET_CAP;  // the bucket, gathered (<= BUCKET_CAP records)
-      gather_runs(srec, tstart, ntiles, B0, B1, src, s_ra, s_pre, sh_w);
+      gather_runs<BUCKET_CAP / G_NT>(srec, tstart, ntiles, B0, B1, src, s_ra, s_pre, sh_w);
       __threadfence_block();
       __syncthreads();
       auto half_of = [&](uint32_t k) -> uint32_t {
@@ -1606,20 +1585,20 @@ void launch_v4_hist(hipStream_t st, const rl_batch& b, const DevRule* rules, uin
 }
 void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const unsigned long long* thsum,
                     unsigned long long* hoff, const uint32_t* fpart, const HotEntry* hot_list, HotBucket* hb,
-                    const TableDesc& tab, HotCand* cand, uint32_t* heads_out, uint32_t* ins_out, uint16_t* toff,
-                    void* scratch, const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl) {
+                    const TableDesc& tab, HotCand* cand, uint32_t* heads_out, uint32_t* ins_out, void* scratch,
+                    const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl) {
   hipLaunchKernelGGL(v4::k4_scan, dim3(v4_scan_blocks()), dim3(v4::SCAN_NT), 0, st, tstart, thsum, v4_tiles(n), n, hoff,
-                     fpart, hot_list, hb, tab, cand, heads_out, ins_out, toff, v4_ranges(scratch), poison, occ, ctl);
+                     fpart, hot_list, hb, tab, cand, heads_out, ins_out, v4_ranges(scratch), poison, occ, ctl);
 }
-void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart, const uint16_t* toff,
+void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart,
                      void* scratch, const DevRule* rules, const unsigned long long* hoff, HotBucket* hb,
-                     int local_cache, MRec* mrec, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
+                     int local_cache, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
                      uint32_t* poison, EngineCtl* ctl) {
   hipLaunchKernelGGL(v4::k4_place, dim3(v4_tiles(b.n_desc)), dim3(V4_THREADS), 0, st, make_dev_batch(b), srec, tstart,
-                     toff, v4_ranges(scratch), rules, hoff, hb, local_cache, mrec, out, req_thr, dfr, routed, poison,
+                     v4_ranges(scratch), rules, hoff, hb, local_cache, out, req_thr, dfr, routed, poison,
                      ctl);
 }
-void launch_v4_group(hipStream_t st, const rl_batch& b, MRec* mrec, const DevRule* rules, const TableDesc& tab,
+void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, const TableDesc& tab,
                      rl_status* out, uint32_t* req_thr, const HotBucket* hb, const Deferred* dfr, HotCand* cand,
                      int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads, uint32_t* wg_ins,
                      const uint32_t* scan_heads, const uint32_t* scan_ins, int routed, RegionOcc* occ, EngineCtl* ctl,
@@ -1643,7 +1622,7 @@ void launch_v4_group(hipStream_t st, const rl_batch& b, MRec* mrec, const DevRul
   gs.grp = reinterpret_cast<uint16_t*>(p);
   p += (size_t)GBLOCKS * BUCKET_CAP * 2;
   gs.end = reinterpret_cast<uint16_t*>(p);
-  hipLaunchKernelGGL(k4_group, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), mrec, rules, tab, out, req_thr, hb,
+  hipLaunchKernelGGL(k4_group, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), rules, tab, out, req_thr, hb,
                      dfr, cand, cand_on, seed, gs, wg_heads, wg_ins, scan_heads, scan_ins, (uint32_t)HOT_SCAN_BLOCKS,
                      v4_ranges(scratch), routed, occ, ctl, next_ctl, hctl, hcand, srec, tstart, v4_tiles(b.n_desc));
 }

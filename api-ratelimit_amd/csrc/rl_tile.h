@@ -44,13 +44,18 @@ RL_DEV uint32_t hot_lookup(const HotEntry* sh_hot, uint64_t a, uint64_t b, uint3
 
 template <class V>
 RL_DEV V wave_sum(V x) {
+  if constexpr (sizeof(V) == 4) {
+    return (V)wave_sum_u32((uint32_t)x);
+  } else {
 #pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-  return x;
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+  }
 }
 
 template <class V>
 RL_DEV V wave_incl_scan(V x) {
+  if constexpr (sizeof(V) == 4) return (V)wave_incl_scan_u32((uint32_t)x);
   const uint32_t lane = __lane_id();
 #pragma unroll
   for (int s = 1; s < 64; s <<= 1) {
