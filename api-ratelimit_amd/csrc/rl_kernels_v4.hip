@@ -1455,33 +1455,32 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   if (tid < 8) s_ins[tid] = 0;
   __syncthreads();
   {
-    uint32_t u = 0;
-    for (uint32_t k = tid; k < gridDim.x + n_scan_heads; k += G_NT)
-      u += (k < gridDim.x ? ld_relaxed(&wg_heads[k]) : scan_heads[k - gridDim.x]) & 0xFFFFu;
-    u = tile::wave_sum(u);
-    if (lane == 0 && u) atomicAdd(&s_heads, u);
-    // new slots per region: 4 words per block, two 16-bit region counts each; every thread
-    // sums whole blocks with its loads in flight together
-    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0;
+    // k4_scan's hot blocks wrote their words right behind this kernel's (the engine passes
+    // scan_heads = wg_heads + gridDim.x, scan_ins = wg_ins + 4 * gridDim.x): every thread loads
+    // all of its blocks' five words at once (clamped indices), then DPP sums per wave
+    constexpr int EPI = (GBLOCKS + HOT_SCAN_BLOCKS + G_NT - 1) / G_NT;
     const uint32_t nb = gridDim.x + n_scan_heads;
-    for (uint32_t k0 = tid * 4; k0 < nb; k0 += G_NT * 4) {
-      uint32_t w[4][4];
+    uint32_t hv[EPI], w[EPI][4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+    for (int e = 0; e < EPI; ++e) {
+      const uint32_t k = min(tid + e * G_NT, nb - 1u);
+      hv[e] = ld_relaxed(&wg_heads[k]);
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          const uint32_t k = k0 + q;
-          w[q][x] = k >= nb ? 0u : k < gridDim.x ? ld_relaxed(&wg_ins[k * 4 + x]) : scan_ins[(k - gridDim.x) * 4 + x];
-        }
+      for (int x = 0; x < 4; ++x) w[e][x] = ld_relaxed(&wg_ins[k * 4 + x]);
+    }
+    uint32_t u = 0, cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        c0 += w[q][0] & 0xFFFFu; c1 += w[q][0] >> 16;
-        c2 += w[q][1] & 0xFFFFu; c3 += w[q][1] >> 16;
-        c4 += w[q][2] & 0xFFFFu; c5 += w[q][2] >> 16;
-        c6 += w[q][3] & 0xFFFFu; c7 += w[q][3] >> 16;
+    for (int e = 0; e < EPI; ++e) {
+      if (tid + e * G_NT >= nb) continue;
+      u += hv[e] & 0xFFFFu;
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        cs[2 * x] += w[e][x] & 0xFFFFu;
+        cs[2 * x + 1] += w[e][x] >> 16;
       }
     }
-    const uint32_t cs[8] = {c0, c1, c2, c3, c4, c5, c6, c7};
+    u = tile::wave_sum(u);
+    if (lane == 0 && u) atomicAdd(&s_heads, u);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const uint32_t c = tile::wave_sum(cs[r]);
@@ -1493,9 +1492,9 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
     // one thread per region; also for a refused batch: its hot keys may have claimed slots in
     // k4_scan before the refusal (they hold the empty state; the rerun finds them)
     const uint32_t r = tid, g = ctl->gen_max[r];
+    RegionOcc o = occ[r];  // loaded with gen_max, not behind it
     ctl->ins[r] = s_ins[r];
     if (g) {
-      RegionOcc o = occ[r];
       if (o.gen < g) {
         o.gen = g;
         o.live = s_ins[r];

@@ -8,7 +8,7 @@ per batch (one descriptor per request, hits_addend 1). `now` advances once every
 window holds thousands of batches and the table holds the live set a real deployment has:
 before timing, --prefill batches (default 1.5 s of traffic) fill it — every MINUTE/HOUR key
 drawn so far, the previous second's SECOND keys and half of the current second's — in
-regions sized for it (2^26 slots per home unit and parity, 12.9 GB). A step = one batch
+regions sized for it (2^27 slots per home unit and parity, 25.8 GB). A step = one batch
 through the whole device path (fingerprint, bucket sort, segmented scan, table apply,
 decide); inputs are resident in HBM before timing, outputs stay in HBM. Batches are made on
 the device (tools/gen/workload_gen.hip, the workload.py construction) because one second of
@@ -73,7 +73,9 @@ def parse():
                     help="batches per SECOND window (now advances once every K batches); 1 = round-1 mode")
     ap.add_argument("--prefill", type=int, default=-1,
                     help="untimed batches that fill the table before warmup (-1: 1.5 windows of K batches)")
-    ap.add_argument("--log2-slots", type=int, default=26, help="table slots per region (home unit x parity)")
+    ap.add_argument("--log2-slots", type=int, default=27,
+                    help="table slots per region (home unit x parity); 2^27 x 32 B x 6 regions = 25.8 GB, ~23 %% load "
+                         "at config 3's live set (shorter probe chains than 2^26 at ~46 %%)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample budget per leg (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="N-thread CPU baseline (0 = min(16, cpus))")
     ap.add_argument("--no-kernel-times", action="store_true")
