@@ -1,11 +1,11 @@
 // rl_kernels_v4.hip — the default decision pipeline: four launches per batch.
 //
-// Same contract and outputs as the LSD pipeline (rl_kernels.hip) and v3. Compared with v3
-// each tile writes its descriptors ONCE, already sorted by bucket, and a row of bucket starts
-// per tile; the MSD records then move once more, from the tile-sorted runs to bucket order
-// (k4_place), and there is no bucket-base pass and no tail launch. k4_hist needs nothing
-// from the table, so with two batches in flight it runs for batch k+1 on a second stream
-// while batch k is decided (rl_engine.cpp, rl_submit_pipelined).
+// Same contract and outputs as the LSD pipeline (rl_kernels.hip). Each tile writes its
+// descriptors ONCE, already sorted by bucket, with a row of bucket starts per tile; k4_group
+// gathers each range of MSD buckets straight from those tile-sorted runs (one run per tile),
+// so MSD records are written once and read once. k4_hist needs nothing from the table, so
+// with two batches in flight it runs for batch k+1 on a second stream while batch k is
+// decided (rl_engine.cpp, rl_submit_pipelined).
 //
 //   k4_hist    per 2048-descriptor tile: fingerprint (fixed_cache_impl.go:43-53 via
 //              cache_key.go:57-68), hot-set lookup, bucket; stable LDS sort of the tile by
@@ -13,14 +13,14 @@
 //              hot record carries its in-tile INCRBY prefix), the row of bucket starts, the
 //              hot buckets' h sums; nil-limit descriptors decided (base_limiter.go:72-75)
 //   k4_scan    per hot bucket: exclusive scan of the h sums over tiles, table claim and the
-//              counter before the batch; per MSD bucket: the records in earlier tiles, the
-//              batch total (size check), and per group of 64 MSD buckets the k4_group ranges
+//              counter before the batch; per MSD bucket the batch total (size check), and
+//              per group of 64 MSD buckets the k4_group ranges
 //              (whole buckets packed up to the LDS stage) — all before any table write, so a
 //              refused batch leaves the table untouched
 //   k4_place   per tile: hot descriptors decided in place (post-value = base + tile prefix +
-//              in-tile prefix; local-cache freezes of requests that straddle tiles deferred);
-//              MSD records scattered from the tile's runs to their bucket position
-//   k4_group   per MSD range: records into LDS (bucket order = arrival order inside a key),
+//              in-tile prefix; local-cache freezes of requests that straddle tiles deferred)
+//   k4_group   per MSD range: records gathered into LDS from every tile's run (tile order =
+//              arrival order inside a key),
 //              grouped by full fingerprint, segmented INCRBY prefix, one leader per key
 //              (table probe/claim, serial-order INCRBY, local-cache freeze), decisions. The
 //              last block to finish decides the deferred hot descriptors, counts U, fills
@@ -46,7 +46,15 @@ using tile::BKT_NONE;
 
 constexpr int ROW = V4_ROW16;  // u16 bucket starts per tile (entries [0, NBUCKETS] used)
 static_assert(ROW >= NBUCKETS + 1, "row holds every bucket start and the end");
-constexpr int GBLOCKS = 1024;              // k4_group blocks (at least; 4 per CU, one round)
+#ifndef RL_G_CAP
+// 896 records (two average config-3 buckets) per LDS stage at 3 blocks per CU (50 KB LDS,
+// 152 VGPRs, no spills) measured 114.5 us/step against 118.5 for 640 x 4 blocks (spilling at
+// 128 VGPRs) and 134.6 for 1024 x 2 (tools/build_variants.sh, bench --lib, one box)
+#define RL_G_CAP 896
+#define RL_G_HASH 1024
+#define RL_G_OCC 3
+#endif
+constexpr int GBLOCKS = 256 * RL_G_OCC;    // k4_group blocks: RL_G_OCC per CU, one round
 constexpr int MSD_GROUPS = MSD_BUCKETS / 64;  // k4_scan blocks of MSD buckets (one range list each)
 constexpr int RANGE_MAX = 128;             // ranges per MSD group (two per bucket at most)
 // k4_scan -> k4_place / k4_group, one array of words: [0, MSD_GROUPS) ranges per group;
@@ -61,14 +69,9 @@ constexpr int RANGE_WORDS = R_BTOT + MSD_BUCKETS;
 constexpr int DONE_CTR = 27;               // EngineCtl::tile_ctr[DONE_CTR][0]: k4_group blocks done
 constexpr int G_NT = 256;
 constexpr int G_W = G_NT / 64;
-#ifndef RL_G_CAP
-#define RL_G_CAP 640
-#define RL_G_HASH 1024
-#define RL_G_OCC 4
-#endif
 constexpr int G_CAP = RL_G_CAP;    // records grouped in LDS (a larger pair runs bucket by bucket)
 constexpr int G_HASH = RL_G_HASH;  // LDS hash slots (power of two > G_CAP)
-constexpr int G_IPT = 3;        // positions per thread kept in registers (table read-ahead)
+constexpr int G_IPT = (G_CAP + G_NT - 1) / G_NT;  // positions per thread in registers (table read-ahead)
 constexpr int GS_HASH = 2048;   // global-scratch hash slots (> BUCKET_CAP)
 constexpr uint32_t G_EMPTY = 0xFFFFFFFFu;
 static_assert(G_CAP <= G_NT * G_IPT && G_HASH > G_CAP && GS_HASH > BUCKET_CAP, "k4_group geometry");
@@ -1056,9 +1059,8 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// k4_place — per tile (tile-sorted records): hot descriptors decided in place (v3's k3_place
-// hot branch), MSD records scattered to their bucket position (bucket base + records of the
-// bucket in earlier tiles + rank inside the tile's run).
+// k4_place — per tile (tile-sorted records): hot descriptors decided in place. MSD records
+// stay where k4_hist wrote them; k4_group gathers its ranges from the tile runs.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restrict__ srec,
                                                const uint16_t* __restrict__ tstart,
@@ -1165,8 +1167,9 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
 }
 
 // ---------------------------------------------------------------------------
-// k4_group — one block per range of whole MSD buckets (k4_scan packs them to fit LDS; a range
-// of one bucket larger than the stage runs on the block's global scratch). Every block also
+// k4_group — one block per range of whole MSD buckets (k4_scan packs them to fit LDS; a
+// bucket larger than the stage is gathered into the block's global scratch and grouped there
+// by fingerprint half). Every block also
 // decides a share of the deferred hot descriptors; the last block to finish counts U, fills
 // the hot-set candidates and clears the next batch's control block.
 // ---------------------------------------------------------------------------
