@@ -148,8 +148,18 @@ RL_DEV FpState prefix_state(const uint8_t* blob, uint32_t off, uint32_t len, uin
 // from the string's home unit, not the descriptor's (rl_common.h place_of).
 RL_DEV void key_of(D3& x, const FpState& s, int64_t now, const DevRule& rr, const HotEntry* sh_hot, uint32_t& err) {
   const uint32_t unit = rr.unit;
-  const int64_t widx = div_const(now, unit);
-  const uint32_t ws = (uint32_t)(widx * (int64_t)rr.div);  // (now/divider)*divider  cache_key.go:66-68
+  // now / divider for now in [0, MAX_NOW] (checked by the caller): 32-bit multiply-high by the
+  // divider's magic number, branch-free across lanes of different units (exact for every
+  // 32-bit now: 60 -> 0x88888889 >> 37, 3600 -> 0x91A2B3C5 >> 43, 86400 = 2^7 * 675 ->
+  // 0xC22E4507 >> 41 on now >> 7)
+  const uint32_t n32 = (uint32_t)now;
+  const uint32_t q60 = __umulhi(n32, 0x88888889u) >> 5, q3600 = __umulhi(n32, 0x91A2B3C5u) >> 11,
+                 q86400 = __umulhi(n32 >> 7, 0xC22E4507u) >> 9;
+  const uint32_t widx = unit == RL_UNIT_SECOND ? n32
+                        : unit == RL_UNIT_MINUTE ? q60
+                        : unit == RL_UNIT_HOUR   ? q3600
+                                                 : q86400;
+  const uint32_t ws = widx * rr.div;  // (now/divider)*divider  cache_key.go:66-68
   uint32_t hot_rule = 0;
   const uint32_t hidx = hot_lookup(sh_hot, s.a, s.b, hot_rule);
   uint64_t hi, lo;
@@ -158,14 +168,14 @@ RL_DEV void key_of(D3& x, const FpState& s, int64_t now, const DevRule& rr, cons
   x.key = make_sort_key(pl.region, hi);
   x.lo = lo;
   x.gen = pl.gen;
-  x.now_mod = (uint32_t)(now - (int64_t)ws);
-  x.uw = (unit - 1u) * 2u + (uint32_t)(widx & 1);
-  x.uwv = (uint32_t)widx + 1u;
+  x.now_mod = n32 - ws;
+  x.uw = (unit - 1u) * 2u + (widx & 1u);
+  x.uwv = widx + 1u;
   if (hidx != 0xFFFFFFFFu) {
     // a hot prefix takes every descriptor of the prefix under one rule, so a key string
     // never splits between a hot bucket and an MSD bucket
     if (hot_rule != x.rule) err |= ERR_FALLBACK;
-    x.bucket = hidx * 2u + (uint32_t)(widx & 1);
+    x.bucket = hidx * 2u + (widx & 1u);
   } else {
     x.bucket = HOT_BUCKETS + msd_bucket(x.key);
   }

@@ -369,8 +369,9 @@ int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* 
   }
   for (auto& x : th) x.join();
   th.clear();
-  // (2) every shard applies its descriptors, request by request, in serial order
-  std::vector<std::vector<uint32_t>> thr(T, std::vector<uint32_t>(n_req, 0));
+  // (2) every shard applies its descriptors, request by request, in serial order; each records
+  // (request, ThrottleMillis) for the requests it saw, merged by max below
+  std::vector<std::vector<std::pair<uint32_t, uint32_t>>> thr(T);
   for (int o = 0; o < T; ++o) {
     th.emplace_back([&, o] {
       std::vector<Desc> keys;
@@ -381,18 +382,16 @@ int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* 
           keys.clear();
           while (b < L.size() && L[b].req == L[a].req) keys.push_back(std::move(L[b++].d));
           const uint32_t r = L[a].req;
-          thr[o][r] = do_limit(shard[o], keys, rule_id, now[r], hits_addend[r], out);
+          thr[o].emplace_back(r, do_limit(shard[o], keys, rule_id, now[r], hits_addend[r], out));
           a = b;
         }
       }
     });
   }
   for (auto& x : th) x.join();
-  for (uint32_t r = 0; r < n_req; ++r) {
-    uint32_t m = 0;
-    for (int t = 0; t < T; ++t) m = thr[t][r] > m ? thr[t][r] : m;
-    req_throttle_ms[r] = m;
-  }
+  if (n_req) memset(req_throttle_ms, 0, (size_t)n_req * 4);
+  for (int t = 0; t < T; ++t)
+    for (const auto& x : thr[t]) req_throttle_ms[x.first] = std::max(req_throttle_ms[x.first], x.second);
   return 0;
 }
 
