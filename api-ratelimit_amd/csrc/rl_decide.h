@@ -5,53 +5,6 @@
 
 namespace rlhip {
 
-// Find the slot of (key, fp_lo) for window generation G in its region, or claim an empty one
-// (a slot whose generation is older than G is empty for this window: window expiry). The
-// capacity check (RegionOcc, before any table write) keeps every region below its load
-// limit, so a free slot always exists within the region: the probe is bounded by its size.
-// A claimed slot is reset by the caller (slot_reset) before anything reads it: a key's slot
-// is only ever looked up by the key's one leader of the batch.
-RL_DEV bool table_claim(const TableDesc& tab, uint64_t key, uint64_t fp_lo, uint32_t G, Slot*& slot_out,
-                        bool& existed_out) {
-  const uint32_t region = key_region(key);
-  const uint32_t lg = tab.region_log2[region];
-  const uint64_t mask = (1ull << lg) - 1ull;
-  Slot* rbase = tab.slots + tab.region_base[region];
-  uint64_t pos = (key << 3) >> (64 - lg);  // top lg bits below the region bits
-  const uint32_t tag = (uint32_t)fp_lo;
-  Slot* slot = nullptr;
-  bool existed = false;
-  for (uint64_t probe = 0; probe <= mask;) {
-    Slot* s = rbase + (pos & mask);
-    // ctrl by an L1-bypassing atomic load (it may be CASed concurrently); the key word is
-    // written by earlier batches, or by a concurrent claimer of a different key, which can
-    // never match.
-    const uint64_t c = ld_relaxed64(&s->ctrl);
-    const uint64_t skey = s->key;
-    const uint32_t g = (uint32_t)c;
-    if (g == G && (uint32_t)(c >> 32) == tag && skey == key) {
-      slot = s;
-      existed = true;
-      break;
-    }
-    if (g < G) {
-      // empty for this window generation: claim it
-      const unsigned long long want = ((unsigned long long)tag << 32) | G;
-      const unsigned long long old = atomicCAS((unsigned long long*)&s->ctrl, (unsigned long long)c, want);
-      if (old == c) {
-        slot = s;
-        break;
-      }
-      continue;  // lost the race: re-examine this slot
-    }
-    ++pos;
-    ++probe;
-  }
-  slot_out = slot;
-  existed_out = existed;
-  return slot != nullptr;
-}
-
 // First probe slot of a key in its region.
 RL_DEV Slot* slot_first(const TableDesc& tab, uint64_t key) {
   const uint32_t region = key_region(key);
@@ -97,7 +50,13 @@ RL_DEV void slot_reset(Slot* s, uint64_t key) {
   write_state(s, KeyState{0, 0, 0, 0});
 }
 
-// table_claim with the first probe slot already read (pre). The read-ahead may predate a
+// Find the slot of (key, fp_lo) for window generation G in its region, or claim an empty one
+// (a slot whose generation is older than G is empty for this window: window expiry). The
+// capacity check (RegionOcc, before any table write) keeps every region below its load
+// limit, so a free slot always exists within the region: the probe is bounded by its size.
+// A claimed slot is reset by the caller (slot_reset) before anything reads it: a key's slot
+// is only ever looked up by the key's one leader of the batch.
+// table_claim_pre: with the first probe slot already read (pre). The read-ahead may predate a
 // concurrent claim of that slot by another key: a claim is permanent for the window
 // generation, so a stale "taken by another key" stays true, a stale "free" makes the CAS
 // fail and the slot is re-read. A key's own slot is only claimed by its own leader, and
@@ -111,42 +70,42 @@ RL_DEV bool table_claim_pre(const TableDesc& tab, uint64_t key, uint64_t fp_lo, 
   Slot* rbase = tab.slots + tab.region_base[region];
   uint64_t pos = (key << 3) >> (64 - lg);
   const uint32_t tag = (uint32_t)fp_lo;
-  bool use_pre = true;
   slot_out = nullptr;
   existed_out = false;
   st_out = KeyState{0, 0, 0, 0};
+  SlotView cur = pre;
   for (uint64_t probe = 0; probe <= mask;) {
     Slot* s = rbase + (pos & mask);
-    uint64_t c, skey;
-    if (use_pre) {
-      c = pre.ctrl;
-      skey = pre.key;
-    } else {
-      c = ld_relaxed64(&s->ctrl);
-      skey = s->key;
-    }
-    const uint32_t g = (uint32_t)c;
-    if (g == G && (uint32_t)(c >> 32) == tag && skey == key) {
+    const uint32_t g = (uint32_t)cur.ctrl;
+    if (g == G && (uint32_t)(cur.ctrl >> 32) == tag && cur.key == key) {
       slot_out = s;
       existed_out = true;
-      st_out = use_pre ? pre.st : read_state(s);
+      st_out = cur.st;
       return true;
     }
     if (g < G) {  // empty for this window generation: claim it
       const unsigned long long want = ((unsigned long long)tag << 32) | G;
-      const unsigned long long old = atomicCAS((unsigned long long*)&s->ctrl, (unsigned long long)c, want);
-      if (old == c) {
+      const unsigned long long old = atomicCAS((unsigned long long*)&s->ctrl, (unsigned long long)cur.ctrl, want);
+      if (old == cur.ctrl) {
         slot_out = s;
         return true;
       }
-      use_pre = false;
-      continue;  // lost the race (or a stale read-ahead): re-examine this slot
+      // lost the race, or the read was stale: the CAS returned the slot's claim word, which
+      // now belongs to another key of this generation (a key is claimed only by its own
+      // leader) or is still older; re-examine the slot with it
+      cur.ctrl = old;
+      continue;
     }
-    use_pre = false;
     ++pos;
     ++probe;
+    cur = load_slot(rbase + (pos & mask));  // the whole next slot in one round trip
   }
   return false;
+}
+// table_claim from the key's first slot, read here; returns the state of an existing slot.
+RL_DEV bool table_claim(const TableDesc& tab, uint64_t key, uint64_t fp_lo, uint32_t G, Slot*& slot_out,
+                        bool& existed_out, KeyState& st_out) {
+  return table_claim_pre(tab, key, fp_lo, G, load_slot(slot_first(tab, key)), slot_out, existed_out, st_out);
 }
 
 // Fast-path state of a key all of whose descriptors in the batch have one unit (one store),
@@ -294,13 +253,13 @@ RL_DEV void leader_segment(uint32_t hp, uint32_t j, const SortedRec& tail, bool 
   }
   Slot* slot = nullptr;
   bool existed = false;
-  if (!table_claim(tab, key, rec.fp_lo, rec.gen, slot, existed)) {
+  KeyState ks{0, 0, 0, 0};
+  if (!table_claim(tab, key, rec.fp_lo, rec.gen, slot, existed, ks)) {
     atomicOr(&ctl->err, ERR_TABLE_FULL);  // unreachable below the load limit
     return;
   }
   if (!existed) slot_reset(slot, key);
   count_inserts(!existed, region, ctl);
-  KeyState ks = existed ? read_state(slot) : KeyState{0, 0, 0, 0};
   const uint32_t ws = region_ws(region, rec.gen);
   const DevRule R0 = rules[tail.rule];
   bool exotic = false;

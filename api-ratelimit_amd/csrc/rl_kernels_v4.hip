@@ -440,6 +440,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
 #pragma unroll
   for (int w = 0; w < FP_PART_WORDS; ++w)
     fv[w] = hotb && tid < ntiles ? fpart[(size_t)w * ntiles + tid] : 0u;
+
   // Column pass. MSD blocks: bucket b = lane, tiles [wave*Q, wave*Q + Q). Hot blocks: bucket
   // b = lane % 16 of the block's 16, tile slice wave * 4 + lane / 16.
   const uint32_t m2 = blockIdx.x - HOT_SCAN_BLOCKS;  // MSD block: half m2 & 1 of group m2 / 2
@@ -672,14 +673,14 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
       x.ws = ws;
       Slot* slot = nullptr;
       bool existed = false;
-      if (!table_claim(tab, x.key, lo, pl.gen, slot, existed)) {
+      KeyState ks{0, 0, 0, 0};
+      if (!table_claim(tab, x.key, lo, pl.gen, slot, existed, ks)) {
         atomicOr(&ctl->err, ERR_TABLE_FULL);  // unreachable below the load limit
       } else {
         if (!existed) {
           slot_reset(slot, x.key);
           ins_region = pl.region;
         }
-        const KeyState ks = existed ? read_state(slot) : KeyState{0, 0, 0, 0};
         const bool ps = per_second_store(tab, he.unit);
         bool frozen_pre = false;
         if (!fast_state(ks, ps, local_cache != 0, ws, div, x.base, frozen_pre)) {
@@ -913,14 +914,13 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
   bool existed = false;
   KeyState ks{0, 0, 0, 0};
   const bool claimed = has_pre ? table_claim_pre(tab, key, lo, gen, pre, slot, existed, ks)
-                               : table_claim(tab, key, lo, gen, slot, existed);
+                               : table_claim(tab, key, lo, gen, slot, existed, ks);
   if (!claimed) {
     atomicOr(&ctl->err, ERR_TABLE_FULL);  // unreachable below the load limit
     g.rec[tail].key = 0;
     g.rec[tail].fp_lo = SEG_NO_FREEZE;
     return;
   }
-  if (existed && !has_pre) ks = read_state(slot);
   if (!existed) {
     slot_reset(slot, key);
     heads += 1u << 16;
@@ -1089,14 +1089,12 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
   if (t == 0 && tid == 0 && (s_err & ERR_FALLBACK) && !(s_err & (ERR_BAD_INPUT | ERR_BAD_TIME))) *poison = 1u;
   // Nothing is decided and nothing touches the table unless the whole batch is valid.
   if (s_err) return;
-  // Hot keys without a freeze in this batch: the final counter is base + total (block 0).
-  if (t == 0) {
-    for (int b = tid; b < HOT_BUCKETS; b += NT) {
-      const HotBucket x = hb[b];
-      if (!x.slot || (x.flags & HB_FROZEN_PRE)) continue;
-      if (!local_cache || x.base + x.total <= (uint64_t)rules[x.rule].L)
-        *hot_counter(x) = (uint32_t)(x.base + x.total);
-    }
+  // Hot keys without a freeze in this batch: the final counter is base + total (spread over
+  // the blocks, about one bucket each, so no block carries the whole loop).
+  for (uint32_t b = t + tid * gridDim.x; b < (uint32_t)HOT_BUCKETS; b += NT * gridDim.x) {
+    const HotBucket x = hb[b];
+    if (!x.slot || (x.flags & HB_FROZEN_PRE)) continue;
+    if (!local_cache || x.base + x.total <= (uint64_t)rules[x.rule].L) *hot_counter(x) = (uint32_t)(x.base + x.total);
   }
   const uint32_t nhot = s_row[HOT_BUCKETS];
   const MRec* src = srec + t0;
