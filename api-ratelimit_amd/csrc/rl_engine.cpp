@@ -709,7 +709,7 @@ int rl_engine::finish(rl_status* out_into, uint32_t* thr_into, bool into) {
   if (errs & ERR_TABLE_FULL)
     return fail(RL_ENOSPC, "counter table region would pass its load limit; batch refused before any update "
                            "(raise log2_slots or max_load_permille)");
-  if (errs & ERR_SPIN) return fail(RL_EDEVICE, "device look-back spin limit exceeded");
+  if (errs & ERR_SPIN) return fail(RL_EDEVICE, "device spin limit exceeded or range invariant violated");
   if (errs & ERR_NEED_RESORT) return fail(RL_EDEVICE, "full-fingerprint re-sort still found a mixed run");
   // Hot-set maintenance costs host time between batches: every batch while the set is
   // empty or after a fallback, else every 8th batch (a skewed stream's head moves slowly).

@@ -59,8 +59,7 @@ constexpr int MSD_GROUPS = MSD_BUCKETS / 64;  // k4_scan blocks of MSD buckets (
 constexpr int RANGE_MAX = 128;             // ranges per MSD group (two per bucket at most)
 // k4_scan -> k4_place / k4_group, one array of words: [0, MSD_GROUPS) ranges per group;
 // R_START: per group RANGE_MAX + 1 range entries (bucket << 1 | half inside the group, last = 128);
-// R_BPRE: per MSD bucket the exclusive prefix of bucket totals inside its group;
-// R_GTOT: per group its record total.
+// R_BPRE / R_GTOT: unused (reserved words of the layout).
 constexpr int R_START = MSD_GROUPS;
 constexpr int R_BPRE = R_START + MSD_GROUPS * (RANGE_MAX + 1);
 constexpr int R_GTOT = R_BPRE + MSD_BUCKETS;
@@ -582,9 +581,6 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     if (__builtin_amdgcn_readfirstlane(arrived) == 0u) return;  // the other block packs
     ctot = ld_relaxed(&ranges[R_BTOT + m * 64 + lane]);  // bucket lane of the group
     const uint32_t g = m;
-    const uint32_t incl = tile::wave_incl_scan<uint32_t>(ctot);
-    ranges[R_BPRE + m * 64 + lane] = incl - ctot;
-    if (lane == 63) ranges[R_GTOT + g] = incl;
     // Pack the group's 64 buckets greedily into k4_group ranges of whole buckets holding at
     // most G_CAP records (a single larger bucket is a range of its own). The walk is
     // wave-uniform over the lanes' totals (readlane: no LDS round trip per bucket); lane 0
@@ -1190,9 +1186,9 @@ struct GScratch4 {
 // search and all of a thread's record loads are in flight together.
 constexpr int GATHER_T = 512;
 constexpr int GATHER_TPT = GATHER_T / G_NT;
-template <int PPT>  // output positions per thread: m <= PPT * G_NT
-RL_DEV void gather_runs(const MRec* __restrict__ srec, const uint16_t* __restrict__ tstart, uint32_t ntiles,
-                        uint32_t B0, uint32_t B1, MRec* dst, uint16_t* s_ra, uint16_t* s_pre, uint32_t* sh_w) {
+template <int PPT, int CAP>  // output positions per thread; dst holds CAP <= PPT * G_NT records
+RL_DEV uint32_t gather_runs(const MRec* __restrict__ srec, const uint16_t* __restrict__ tstart, uint32_t ntiles,
+                            uint32_t B0, uint32_t B1, MRec* dst, uint16_t* s_ra, uint16_t* s_pre, uint32_t* sh_w) {
   const uint32_t tid = threadIdx.x;
   uint32_t done = 0;
   for (uint32_t c0 = 0; c0 < ntiles; c0 += GATHER_T) {
@@ -1234,11 +1230,12 @@ RL_DEV void gather_runs(const MRec* __restrict__ srec, const uint16_t* __restric
       for (int u = 0; u < PPT; ++u) v[u] = srec[(size_t)(c0 + lo[u]) * T + s_ra[lo[u]] + (p[u] - s_pre[lo[u]])];
 #pragma unroll
       for (int u = 0; u < PPT; ++u)
-        if (tid + u * G_NT < tot) dst[done + p[u]] = v[u];
+        if (tid + u * G_NT < tot && done + p[u] < (uint32_t)CAP) dst[done + p[u]] = v[u];
     }
     done += tot;
     __syncthreads();  // s_ra / s_pre of the next chunk
   }
+  return done;
 }
 
 __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
@@ -1268,7 +1265,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   __shared__ LSeg s_agg[G_W];
   __shared__ LSeg s_carry;
   __shared__ uint32_t s_cursor, s_heads, s_last, s_err;
-  __shared__ uint32_t s_rn[MSD_GROUPS + 1], s_gpre[MSD_GROUPS + 1];
+  __shared__ uint32_t s_rq[6];  // this block's group: range count, entries of its first two ranges; deferred count
   __shared__ uint32_t sh_w[G_W];
   __shared__ uint32_t s_ins[8];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1276,14 +1273,17 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   uint32_t heads = 0;
   uint64_t ins = 0;  // new slots per region, 8 bits each
   if (tid < 8) s_ins[tid] = 0;
-  if (tid < 64) {  // ranges per group and record bases of the groups: prefixes (one wave)
-    const uint32_t v = tid < (uint32_t)MSD_GROUPS ? ranges[tid] : 0u;
-    const uint32_t w = tid < (uint32_t)MSD_GROUPS ? ranges[R_GTOT + tid] : 0u;
-    const uint32_t iv = tile::wave_incl_scan<uint32_t>(v), iw = tile::wave_incl_scan<uint32_t>(w);
-    if (tid <= (uint32_t)MSD_GROUPS) {
-      s_rn[tid] = iv - v;
-      s_gpre[tid] = iw - w;
-    }
+  // Block j takes ranges q = j / MSD_GROUPS, + RPG, ... of MSD group g = j % MSD_GROUPS (no
+  // prefix over the groups first): the group's range count and the entries of the block's
+  // first two ranges are loaded together with the error word and the deferred count.
+  constexpr uint32_t RPG = GBLOCKS / MSD_GROUPS;
+  static_assert(GBLOCKS % MSD_GROUPS == 0, "blocks per MSD group");
+  const uint32_t g = j % MSD_GROUPS, q0 = j / MSD_GROUPS;
+  const uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
+  if (tid < 6) {
+    const uint32_t i2 = min(q0 + RPG, (uint32_t)RANGE_MAX - 1u);
+    s_rq[tid] = tid == 0 ? ranges[g] : tid == 1 ? rb[q0] : tid == 2 ? rb[q0 + 1] : tid == 3 ? rb[i2]
+              : tid == 4 ? rb[i2 + 1] : ctl->tile_ctr[DFR_CTR][0];
   }
   if (tid == 0) {
     s_heads = 0;
@@ -1307,7 +1307,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   if (s_err == 0) {
     // Hot descriptors of a request that began before the tile where their key froze
     // (k4_place, a previous launch, recorded them and the freezing requests).
-    const uint32_t nd = ctl->tile_ctr[DFR_CTR][0];
+    const uint32_t nd = s_rq[5];
     for (uint32_t e = j * G_NT + tid; e < nd; e += gridDim.x * G_NT) {
       const Deferred df = dfr[e];
       const HotBucket& x = hb[df.bucket];
@@ -1319,30 +1319,28 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
         atomicMax(hot_counter(x), (uint32_t)(x.base + df.P));
       }
     }
-    const uint32_t nr = s_rn[MSD_GROUPS];
-    for (uint32_t r = j; j < (uint32_t)GBLOCKS && r < nr; r += GBLOCKS) {
-      uint32_t g = 0;
-      while (g + 1 < (uint32_t)MSD_GROUPS && s_rn[g + 1] <= r) ++g;
-      const uint32_t q = r - s_rn[g];
-      const uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
+    const uint32_t nq = s_rq[0];  // ranges of group g
+    for (uint32_t q = q0, it = 0; q < nq; q += RPG, ++it) {
       // Range entries are bucket << 1 | half (see k4_scan): [e0, e1) is whole buckets, or one
       // fingerprint half of an oversized bucket (e0 odd: half 1; e1 == e0 | 1: half 0).
-      const uint32_t e0 = rb[q], e1 = rb[q + 1];
+      const uint32_t e0 = it == 0 ? s_rq[1] : it == 1 ? s_rq[3] : rb[q];
+      const uint32_t e1 = it == 0 ? s_rq[2] : it == 1 ? s_rq[4] : rb[q + 1];
       const int split_half = (e0 & 1u) ? 1 : (e1 == (e0 | 1u) ? 0 : -1);
       const uint32_t k0 = e0 >> 1, k1 = split_half >= 0 ? k0 + 1u : e1 >> 1;
-      const uint32_t r0 = s_gpre[g] + ranges[R_BPRE + g * 64 + k0];
-      const uint32_t r1 = k1 == 64u ? s_gpre[g + 1] : s_gpre[g] + ranges[R_BPRE + g * 64 + k1];
-      const uint32_t m = r1 - r0;
-      if (m == 0) continue;
       const uint32_t B0 = HOT_BUCKETS + g * 64u + k0, B1 = HOT_BUCKETS + g * 64u + k1;
       __syncthreads();  // the previous range is done with LDS
-      if (m <= (uint32_t)G_CAP && split_half < 0) {
+      if (split_half < 0) {  // whole buckets: at most G_CAP records (k4_scan's packing)
         for (uint32_t s = tid; s < (uint32_t)G_HASH; s += G_NT) {
           s_slot[s] = G_EMPTY;
           s_cnt[s] = 0;
         }
         if (tid == 0) s_cursor = 0;
-        gather_runs<G_IPT>(srec, tstart, ntiles, B0, B1, s_rec, s_ra, s_pre, sh_w);
+        const uint32_t m = gather_runs<G_IPT, G_CAP>(srec, tstart, ntiles, B0, B1, s_rec, s_ra, s_pre, sh_w);
+        if (m == 0) continue;  // block-uniform
+        if (m > (uint32_t)G_CAP) {  // unreachable: k4_scan packs whole buckets up to G_CAP
+          if (tid == 0) atomicOr(&ctl->err, ERR_SPIN);
+          continue;
+        }
         __syncthreads();
         ST4(2);
         const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
@@ -1359,11 +1357,11 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
       // One bucket larger than the LDS stage. Its keys split by the fingerprint bit below the
       // bucket bits into two halves of whole keys; each half that fits is grouped in LDS.
       ST4X(3, 1);
-      ST4X(0, m);
       constexpr int SPLIT_BIT = 64 - 3 - MSD_BITS - 1;
       constexpr int SU = BUCKET_CAP / G_NT;
       MRec* const src = gs.rec + (size_t)j * BUCKET_CAP;  // the bucket, gathered (<= BUCKET_CAP records)
-      gather_runs<BUCKET_CAP / G_NT>(srec, tstart, ntiles, B0, B1, src, s_ra, s_pre, sh_w);
+      const uint32_t m = gather_runs<BUCKET_CAP / G_NT, BUCKET_CAP>(srec, tstart, ntiles, B0, B1, src, s_ra, s_pre, sh_w);
+      ST4X(0, m);
       __threadfence_block();
       __syncthreads();
       auto half_of = [&](uint32_t k) -> uint32_t {
