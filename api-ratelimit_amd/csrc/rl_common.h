@@ -214,7 +214,15 @@ struct __attribute__((aligned(32))) HotEntry {
   uint32_t pad;
 };
 constexpr int HOT_MAX = 256;              // hot prefixes per batch
-constexpr int HOT_SLOTS = 512;            // open-addressing table of HotEntry (device + LDS copy)
+// Hot-set table (device + LDS copy in k4_hist): HOT_TAGS u32 tag words (open addressing from
+// the prefix state's low bits, load <= 1/8), in the space of HOT_SLOTS HotEntry units, then
+// the HOT_MAX entries by hot index. Tag word = (a >> 32) with its low 9 bits replaced by
+// hot index + 1 (0 = empty); a tag match is confirmed on the entry's full (a, b).
+constexpr int HOT_SLOTS = 256;
+constexpr int HOT_TAGS = HOT_SLOTS * 32 / 4;
+constexpr uint32_t HOT_TAG_MASK = ~0x1FFu;
+__host__ __device__ __forceinline__ uint32_t hot_tag(uint64_t a) { return (uint32_t)(a >> 32) & HOT_TAG_MASK; }
+__host__ __device__ __forceinline__ uint32_t hot_home(uint64_t a) { return (uint32_t)a & (HOT_TAGS - 1); }
 constexpr int HOT_BUCKETS = 2 * HOT_MAX;  // hot prefix x window parity
 constexpr int MSD_BITS = 11;
 constexpr int MSD_BUCKETS = 1 << MSD_BITS;   // 11 fingerprint bits below the region bits

@@ -162,7 +162,7 @@ struct rl_engine {
   size_t zero_cap = 0;
 
   // hot set (both pipelines)
-  HotEntry* d_hot = nullptr;                  // device hot-key table (HOT_SLOTS) + list by hot index (HOT_MAX)
+  HotEntry* d_hot = nullptr;                  // device hot-key table: tag words (HOT_SLOTS units) + list by hot index (HOT_MAX)
   HotEntry* d_hot_buf[HSLOTS] = {};           // d_hot = d_hot_buf[hot_ver]; one per batch in flight
   int hot_ver = 0;
   HotEntry* h_hot_stage = nullptr;            // pinned upload staging
@@ -503,8 +503,8 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   return 0;
 }
 
-// Upload the hot-key set: an open-addressing table (slot = a>>40 mod HOT_SLOTS) followed by
-// the entries in hot-index order.
+// Upload the hot-key set: open-addressed tag words (rl_common.h HOT_TAGS; home = hot_home(a),
+// word = hot_tag(a) | index + 1) followed by the entries in hot-index order.
 int rl_engine::upload_hot(hipStream_t us) {
   std::vector<HotEntry> t(HOT_SLOTS + HOT_MAX);
   for (auto& x : t) {
@@ -513,6 +513,8 @@ int rl_engine::upload_hot(hipStream_t us) {
     x.idx = 0xFFFFFFFFu;
     x.pad = 0;
   }
+  std::vector<uint32_t> tags(HOT_TAGS, 0u);
+  static_assert(HOT_MAX < 512 && (size_t)HOT_TAGS * 4 == HOT_SLOTS * sizeof(HotEntry), "hot tag words");
   for (size_t i = 0; i < hot.size(); ++i) {
     HotEntry he;
     he.a = hot[i].a;
@@ -521,11 +523,12 @@ int rl_engine::upload_hot(hipStream_t us) {
     he.rule = hot[i].rule;
     he.idx = (uint32_t)i;
     he.pad = 0;
-    uint32_t s = (uint32_t)(he.a >> 40) & (HOT_SLOTS - 1);
-    while (t[s].idx != 0xFFFFFFFFu) s = (s + 1) & (HOT_SLOTS - 1);
-    t[s] = he;
+    uint32_t s = hot_home(he.a);
+    while (tags[s]) s = (s + 1) & (HOT_TAGS - 1);
+    tags[s] = hot_tag(he.a) | (uint32_t)(i + 1);
     t[HOT_SLOTS + i] = he;
   }
+  memcpy(t.data(), tags.data(), (size_t)HOT_TAGS * 4);
   // Into the version no in-flight batch reads, through a pinned staging buffer whose last
   // copy is done.
   hipError_t e = hipEventSynchronize(ev_hot);

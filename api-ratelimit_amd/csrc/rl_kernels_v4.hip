@@ -81,9 +81,8 @@ static_assert(DONE_CTR != DFR_CTR && DONE_CTR != CAND_CTR &&
 using tile::rule_of;
 
 #ifdef RL_STAMPS
-// Diagnostic build only (tools/stamps4.py): per-block phase timestamps (s_memrealtime, 100 MHz)
-// of wave 0 of k4_group blocks.
-__device__ uint64_t g_st4[4096][8];
+// Diagnostic build only (tools/stamps_view.py): per-block phase timestamps (s_memrealtime,
+// 100 MHz) of wave 0 of k4_group blocks. g_st4 is defined in rl_tile.h.
 #define ST4(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_st4[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define ST4V(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_st4[blockIdx.x][k] = (v); } while (0)
 // k4_group per-block facts in rows 3072 + block: [0] records grouped, [1] keys led, [2] ranges, [3] split ranges
@@ -93,7 +92,12 @@ __device__ uint64_t g_st4[4096][8];
 // the last k4_group block's epilogue: row 4000
 #define STL(k) do { if (threadIdx.x == 0) g_st4[4000][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 // k4_hist tiles: rows 1024 + tile
+#ifdef RL_HIST_FINE  // load_descs stamps its two load levels into columns 2 and 3 (rl_tile.h)
+#define STH(k) do { if ((k) < 2 || (k) > 5 || (k) == 2 || (k) == 3) { constexpr int c_ = (k) == 2 ? 4 : (k) == 3 ? 5 : (k); \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) g_st4[1024 + blockIdx.x][c_] = __builtin_amdgcn_s_memrealtime(); } } while (0)
+#else
 #define STH(k) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_st4[1024 + blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#endif
 #else
 #define STH(k) do { } while (0)
 #define STL(k) do { } while (0)
@@ -150,7 +154,7 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
                                               uint32_t* __restrict__ req_thr, uint32_t* __restrict__ fpart,
                                               uint16_t* __restrict__ tstart, unsigned long long* __restrict__ thsum,
                                               MRec* __restrict__ srec, rl_status* __restrict__ out, EngineCtl* ctl) {
-  __shared__ HotEntry sh_hot[HOT_SLOTS];
+  __shared__ HotEntry sh_hot[HOT_SLOTS + HOT_MAX];  // tag words, then the entries (rl_common.h)
   __shared__ uint16_t sh_cnt[ROW];
   __shared__ unsigned long long sh_hs[HOT_BUCKETS];
   __shared__ uint16_t s_d[T];
@@ -1629,7 +1633,7 @@ void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, co
 
 #ifdef RL_STAMPS
 extern "C" int rl_debug_st4(uint64_t* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(rlhip::v4::g_st4), sizeof(uint64_t) * 4096 * 8, 0,
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(rlhip::g_st4), sizeof(uint64_t) * 4096 * 8, 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif

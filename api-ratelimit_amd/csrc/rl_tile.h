@@ -10,6 +10,15 @@
 #include "rl_device.h"
 
 namespace rlhip {
+#ifdef RL_STAMPS
+__device__ uint64_t g_st4[4096][8];  // diagnostic phase stamps (rl_kernels_v4.hip)
+#endif
+#ifdef RL_HIST_FINE
+#define HSTF(k) do { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+  if (threadIdx.x == 0 && blockIdx.x < 1024) g_st4[1024 + blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define HSTF(k) do { } while (0)
+#endif
 namespace tile {
 
 constexpr int T = V4_TILE;
@@ -27,17 +36,26 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
 RL_DEV uint32_t msd_bucket(uint64_t key) { return (uint32_t)((key << 3) >> (64 - MSD_BITS)); }
 RL_DEV uint32_t rule_of(uint32_t rn) { return rn & (V4_MAX_RULES - 1u); }
 
-// Hot entry of a key prefix (any unit: one prefix, one hot bucket pair), or ~0.
+// Hot entry of a key prefix (any unit: one prefix, one hot bucket pair), or ~0. sh_hot = the
+// table (rl_common.h HOT_TAGS): u32 tag words, then the entries by hot index. With at most
+// 256 keys in 2048 words a miss ends after ~1.1 probes of one LDS word each; the per-slot
+// 32-B entry probe it replaces walked clusters at load 1/2 (7 us of k4_hist at config 3).
 RL_DEV uint32_t hot_lookup(const HotEntry* sh_hot, uint64_t a, uint64_t b, uint32_t& rule) {
-  uint32_t s = (uint32_t)(a >> 40) & (HOT_SLOTS - 1);
-  for (int probe = 0; probe < HOT_SLOTS; ++probe) {
-    const HotEntry& e = sh_hot[s];
-    if (e.idx == 0xFFFFFFFFu) return 0xFFFFFFFFu;
-    if (e.a == a && e.b == b) {
-      rule = e.rule;
-      return e.idx;
+  const uint32_t* tags = reinterpret_cast<const uint32_t*>(sh_hot);
+  const HotEntry* list = sh_hot + HOT_SLOTS;
+  const uint32_t t = hot_tag(a);
+  uint32_t s = hot_home(a);
+  for (int probe = 0; probe < HOT_TAGS; ++probe) {
+    const uint32_t w = tags[s];
+    if (w == 0u) return 0xFFFFFFFFu;
+    if ((w & HOT_TAG_MASK) == t) {
+      const HotEntry& e = list[(w & ~HOT_TAG_MASK) - 1u];
+      if (e.a == a && e.b == b) {
+        rule = e.rule;
+        return e.idx;
+      }
     }
-    s = (s + 1) & (HOT_SLOTS - 1);
+    s = (s + 1) & (HOT_TAGS - 1);
   }
   return 0xFFFFFFFFu;
 }
@@ -201,6 +219,7 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
     oa[r] = in.off[i];
     ob[r] = in.off[i + 1u];
   }
+  HSTF(2);
   uint32_t o0[R], len[R];
   bool ok[R];
   int64_t now[R];
@@ -226,6 +245,7 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
     w0[r] = p[0];
     w1[r] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint32_t*>(p) + 4);
   }
+  HSTF(3);
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint32_t i = t0 + r * NT + tid;
@@ -318,7 +338,7 @@ RL_DEV void load_routed(const DevBatch& in, const DevRule* __restrict__ rules, u
 }
 
 RL_DEV void load_hot_table(const HotEntry* __restrict__ hot, HotEntry* sh_hot) {
-  for (int k = threadIdx.x; k < HOT_SLOTS; k += blockDim.x) sh_hot[k] = hot[k];
+  for (int k = threadIdx.x; k < HOT_SLOTS + HOT_MAX; k += blockDim.x) sh_hot[k] = hot[k];
 }
 
 // One stable LDS counting pass over 64 digits of the tile: src -> dst by (s_d[x] >> shift) & 63.

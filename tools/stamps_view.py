@@ -7,6 +7,8 @@ import numpy as np
 st = np.load(sys.argv[1]).astype(np.int64)
 a = st[:1024]
 a = a[a[:, 2] > 0]
+if not len(a):  # no k4_group work in the dumped batch (e.g. it fell back): hist rows only
+    a = st[:1]
 t0 = a[:, 0].min()
 names = ["entry", "staged", "inserted", "reserved", "laidout", "scanned", "led", "done"]
 rel = (a[:, [0, 2, 1, 6, 7, 3, 4, 5]] - t0) / 100.0
@@ -30,6 +32,8 @@ if len(h):
     t0h = h[:, 0].min()
     rel = (h - t0h) / 100.0
     nm = ["entry", "hot table", "descs+hash", "partials", "digit pass 1", "digit pass 2", "scan+starts", "written"]
+    if len(sys.argv) > 2 and sys.argv[2] == "fine":  # -DRL_HIST_FINE build
+        nm = ["entry", "hot table", "level 1", "level 2", "hash+key", "partials", "sort+scan", "written"]
     print(f"k4_hist {len(h)} tiles; entry spread {rel[:, 0].max():.1f} us, last end {rel[:, 7].max():.1f} us, "
           f"end p50 {np.median(rel[:, 7]):.1f}")
     dd = np.diff(rel, axis=1)
