@@ -56,6 +56,8 @@ static_assert(ROW >= NBUCKETS + 1, "row holds every bucket start and the end");
 #endif
 constexpr int GBLOCKS = 256 * RL_G_OCC;    // k4_group blocks: RL_G_OCC per CU, one round
 constexpr int MSD_GROUPS = MSD_BUCKETS / 64;  // k4_scan blocks of MSD buckets (one range list each)
+constexpr uint32_t RPG = GBLOCKS / MSD_GROUPS;  // k4_group blocks per MSD group
+static_assert(GBLOCKS % MSD_GROUPS == 0, "blocks per MSD group");
 constexpr int RANGE_MAX = 128;             // ranges per MSD group (two per bucket at most)
 // k4_scan -> k4_place / k4_group, one array of words: [0, MSD_GROUPS) ranges per group;
 // R_START: per group RANGE_MAX + 1 range entries (bucket << 1 | half inside the group, last = 128);
@@ -85,7 +87,8 @@ using tile::rule_of;
 // 100 MHz) of wave 0 of k4_group blocks. g_st4 is defined in rl_tile.h.
 #define ST4(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_st4[blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #define ST4V(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g_st4[blockIdx.x][k] = (v); } while (0)
-// k4_group per-block facts in rows 3072 + block: [0] records grouped, [1] keys led, [2] ranges, [3] split ranges
+// k4_group per-block facts of the batch in rows 3072 + block: [0] records grouped, [1] keys led,
+// [2] ranges, [3] split ranges
 #define ST4X(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_st4[3072 + blockIdx.x][k] += (v); } while (0)
 // k4_scan blocks stamp rows 2048 + block (thread 0).
 #define ST5(k) do { if (threadIdx.x == 0) g_st4[2048 + blockIdx.x][k] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -585,13 +588,24 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     if (__builtin_amdgcn_readfirstlane(arrived) == 0u) return;  // the other block packs
     ctot = ld_relaxed(&ranges[R_BTOT + m * 64 + lane]);  // bucket lane of the group
     const uint32_t g = m;
-    // Pack the group's 64 buckets greedily into k4_group ranges of whole buckets holding at
-    // most G_CAP records (a single larger bucket is a range of its own). The walk is
-    // wave-uniform over the lanes' totals (readlane: no LDS round trip per bucket); lane 0
-    // stores.
+    // Pack the group's 64 buckets into k4_group ranges of whole buckets, at most G_CAP records
+    // each (a single larger bucket: two half ranges of its own), balanced over the group's RPG
+    // blocks: a range closes before a bucket whose midpoint would pass the even share of what
+    // is left (a k4_group block's time grows with its range's records, and the kernel lasts
+    // as long as its largest range). The walk is wave-uniform over the lanes' totals (readlane:
+    // no LDS round trip per bucket); lane 0 stores.
     uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
     uint32_t nr = 0, cur = 0, last = 0;  // last = rb[nr]
+    uint32_t rem = tile::wave_sum(ctot), left = RPG;  // records not in closed ranges; ranges to form
     if (lane == 0) rb[0] = 0;
+    auto close = [&](uint32_t e) {
+      ++nr;
+      if (lane == 0) rb[nr] = e;
+      last = e;
+      rem -= cur;
+      left = left > 1u ? left - 1u : 1u;
+      cur = 0;
+    };
 #pragma unroll
     for (int k = 0; k < 64; ++k) {
       const uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)ctot, k);
@@ -599,22 +613,15 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
       if (cb > (uint32_t)G_CAP) {
         // Oversized bucket (<= BUCKET_CAP): two ranges of its own, one per fingerprint half
         // (entries ek and ek | 1), grouped by two blocks; the next bucket starts a range.
-        if (last != ek) {
-          ++nr;
-          if (lane == 0) rb[nr] = ek;
-        }
+        if (last != ek) close(ek);
         ++nr;
         if (lane == 0) rb[nr] = ek | 1u;
         last = ek | 1u;
+        left = left > 1u ? left - 1u : 1u;
         cur = cb;
         continue;
       }
-      if (cur && cur + cb > (uint32_t)G_CAP) {
-        ++nr;
-        if (lane == 0) rb[nr] = ek;
-        last = ek;
-        cur = 0;
-      }
+      if (cur && (cur + cb > (uint32_t)G_CAP || (2u * cur + cb) * left > 2u * rem)) close(ek);
       cur += cb;
     }
     ++nr;
@@ -1280,8 +1287,6 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   // Block j takes ranges q = j / MSD_GROUPS, + RPG, ... of MSD group g = j % MSD_GROUPS (no
   // prefix over the groups first): the group's range count and the entries of the block's
   // first two ranges are loaded together with the error word and the deferred count.
-  constexpr uint32_t RPG = GBLOCKS / MSD_GROUPS;
-  static_assert(GBLOCKS % MSD_GROUPS == 0, "blocks per MSD group");
   const uint32_t g = j % MSD_GROUPS, q0 = j / MSD_GROUPS;
   const uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
   if (tid < 6) {
@@ -1295,6 +1300,9 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   }
   __syncthreads();
   ST4(0);
+#ifdef RL_STAMPS
+  if (tid == 0 && j < 1024) for (int k = 0; k < 8; ++k) g_st4[3072 + j][k] = 0;  // this batch's facts only
+#endif
   if (s_err == 0 && j < (uint32_t)(HOT_BUCKETS / G_NT)) {
     // Hot keys (decided by k4_place): EXPIRE and freecache TTLs from the time of the last
     // INCRBY / of the freezing request (fixed_cache_impl.go:69-72, base_limiter.go:102). The

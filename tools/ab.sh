@@ -12,6 +12,7 @@ for t in $vars; do
   python - "$t" <<'PY'
 import json, sys
 d = json.loads(open("gpurun_out/ab.log").read().strip().splitlines()[-1])
-print(sys.argv[1], d["ms_per_step"], d["config"].get("batches_in_flight"))
+k = (d.get("roofline") or {}).get("kernels_us_per_batch") or {}
+print(sys.argv[1], d["ms_per_step"], d["config"].get("batches_in_flight"), " ".join(f"{n}={v}" for n, v in k.items()))
 PY
 done
