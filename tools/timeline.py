@@ -37,3 +37,7 @@ print(f"  scan end -> place start {np.mean(pl[:, 0] - sc[:, 1]):.1f};  place end
 # hist of batch k+1 relative to batch k's scan (the last B hists belong to batches one ahead)
 print(f"  hist start - scan start (same step) {np.mean(hi[-B + 1:, 0] - sc[-B:-1, 0]):.1f}; "
       f"hist end - group start {np.mean(hi[-B + 1:, 1] - g[-B:-1, 0]):.1f}")
+# slot reuse: batch k's k4_hist writes the device slot of batch k-2, so it must start after
+# batch k-2's k4_group ended (the front stream waits for that batch's completion event)
+gap2 = hi[2:, 0] - g[:-2, 1]
+print(f"  hist(k) start - group(k-2) end: min {gap2.min():.1f} (must be >= 0), mean {gap2.mean():.1f}")
