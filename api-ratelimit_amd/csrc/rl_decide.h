@@ -6,10 +6,24 @@
 namespace rlhip {
 
 // First probe slot of a key in its region.
+// A region's first slot offset and log2 size by a select chain over constant indices: the
+// kernel argument words stay in scalar registers. A dynamic index into the by-value TableDesc
+// compiled to vector loads from the argument segment whose waits (vmcnt) also drained every
+// table read-ahead issued before them.
+RL_DEV void region_geom(const TableDesc& tab, uint32_t region, uint64_t& rb, uint32_t& lg) {
+  rb = tab.region_base[0];
+  lg = tab.region_log2[0];
+#pragma unroll
+  for (int r = 1; r < 8; ++r) {
+    rb = region == (uint32_t)r ? tab.region_base[r] : rb;
+    lg = region == (uint32_t)r ? tab.region_log2[r] : lg;
+  }
+}
 RL_DEV Slot* slot_first(const TableDesc& tab, uint64_t key) {
-  const uint32_t region = key_region(key);
-  const uint32_t lg = tab.region_log2[region];
-  return tab.slots + tab.region_base[region] + (((key << 3) >> (64 - lg)) & ((1ull << lg) - 1ull));
+  uint64_t rb;
+  uint32_t lg;
+  region_geom(tab, key_region(key), rb, lg);
+  return tab.slots + rb + (((key << 3) >> (64 - lg)) & ((1ull << lg) - 1ull));
 }
 
 // The per-key state of a slot: both stores' counters, the main counter's expiry and the
@@ -64,10 +78,11 @@ RL_DEV void slot_reset(Slot* s, uint64_t key) {
 // current. Returns the state of an existing slot (zeros for a claimed one).
 RL_DEV bool table_claim_pre(const TableDesc& tab, uint64_t key, uint64_t fp_lo, uint32_t G, const SlotView pre,
                             Slot*& slot_out, bool& existed_out, KeyState& st_out) {
-  const uint32_t region = key_region(key);
-  const uint32_t lg = tab.region_log2[region];
+  uint64_t rb;
+  uint32_t lg;
+  region_geom(tab, key_region(key), rb, lg);
   const uint64_t mask = (1ull << lg) - 1ull;
-  Slot* rbase = tab.slots + tab.region_base[region];
+  Slot* rbase = tab.slots + rb;
   uint64_t pos = (key << 3) >> (64 - lg);
   const uint32_t tag = (uint32_t)fp_lo;
   slot_out = nullptr;

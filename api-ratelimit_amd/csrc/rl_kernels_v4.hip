@@ -760,11 +760,24 @@ RL_DEV bool g_insert(const GS& g, uint32_t k, const DevRule* __restrict__ rules)
   const uint32_t hmask = g.hs - 1u;
   uint32_t s = (uint32_t)key & hmask;
   uint32_t v;
+#ifdef RL_PROBE_STATS  // diagnostics: probes and inserts per k4_group block (stamp rows 3072 + block)
+  uint32_t probes = 0;
+#endif
   for (;;) {
     v = atomicCAS(&g.slot[s], G_EMPTY, k);
+#ifdef RL_PROBE_STATS
+    ++probes;
+#endif
     if (v == G_EMPTY || (g.rec[v].key == key && g.rec[v].fp_lo == lo)) break;
     s = (s + 1) & hmask;
   }
+#ifdef RL_PROBE_STATS
+  if (blockIdx.x < 1024) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&g_st4[3072 + blockIdx.x][4]), (unsigned long long)probes);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&g_st4[3072 + blockIdx.x][5]), 1ull);
+    if (v == G_EMPTY) atomicAdd(reinterpret_cast<unsigned long long*>(&g_st4[3072 + blockIdx.x][6]), 1ull);
+  }
+#endif
   g.grp[k] = (uint16_t)s;
   uint32_t inc = 1u;
   if (v != G_EMPTY) {
@@ -1009,11 +1022,17 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     const uint32_t k = tid + j * G_NT;
-    if (k < m && g_insert(g, k, rules)) {
-      own |= 1u << j;
-      if constexpr (LDS) {
-        if (j < G_IPT) pre[j] = load_slot(slot_first(tab, g.rec[k].key));
-      }
+    if (k < m && g_insert(g, k, rules)) own |= 1u << j;
+  }
+  if constexpr (LDS) {
+    // every thread issues G_IPT slot loads at once, a position that leads no key reading the
+    // table's first slot instead (no branch around a load: a load under a condition made the
+    // compiler wait for it at the merge point, one table round trip per position)
+#pragma unroll
+    for (int j = 0; j < G_IPT; ++j) {
+      const uint32_t k = min(tid + (uint32_t)j * G_NT, (uint32_t)G_CAP - 1u);
+      const Slot* a = ((own >> j) & 1u) ? slot_first(tab, g.rec[k].key) : tab.slots;
+      pre[j] = load_slot(a);
     }
   }
   gbar<LDS>();
