@@ -123,12 +123,12 @@ DoLimitResponse HipRateLimitCache::DoLimit(const RateLimitRequest& request,
   return std::move(call->resp);
 }
 
-uint32_t HipRateLimitCache::rule_id(const RateLimitLimit& l) {
-  auto k = std::make_pair(l.RequestsPerUnit, (uint32_t)l.unit);
+uint32_t HipRateLimitCache::rule_id(const RateLimitLimit& l, bool shadow) {
+  auto k = std::make_pair(l.RequestsPerUnit, (uint32_t)l.unit | (shadow ? RL_RULE_SHADOW : 0u));
   auto it = rule_ids_.find(k);
   if (it != rule_ids_.end()) return it->second;
   const uint32_t id = (uint32_t)rules_.size();
-  rules_.push_back(rl_rule{l.RequestsPerUnit, (uint32_t)l.unit});
+  rules_.push_back(rl_rule{l.RequestsPerUnit, k.second});
   rule_ids_.emplace(k, id);
   rules_dirty_ = true;
   return id;
@@ -193,7 +193,7 @@ void HipRateLimitCache::run_batch(std::vector<std::shared_ptr<Call>>& calls) {
       const auto& lim = (*c.limits)[i];
       blob.insert(blob.end(), c.prefix[i].begin(), c.prefix[i].end());
       off.push_back((uint32_t)blob.size());
-      rule.push_back(lim ? rule_id(lim->Limit) : RL_NIL_RULE);
+      rule.push_back(lim ? rule_id(lim->Limit, lim->ShadowMode) : RL_NIL_RULE);
       req_of.push_back((uint32_t)r);
     }
   }
@@ -245,6 +245,7 @@ void HipRateLimitCache::run_batch(std::vector<std::shared_ptr<Call>>& calls) {
         if (s.over_limit_delta) lim->Stats->OverLimit.Add(s.over_limit_delta);
         if (fl & RL_FLAG_LOCAL_CACHE_HIT) lim->Stats->OverLimitWithLocalCache.Add(s.over_limit_delta);
         if (s.near_limit_delta) lim->Stats->NearLimit.Add(s.near_limit_delta);
+        if (fl & RL_FLAG_SHADOW) lim->Stats->ShadowMode.Add(1);
       }
     }
     c.done.set_value();

@@ -48,6 +48,7 @@ class Counter {
 // config.RateLimitStats  src/config/config.go:18-23
 struct RateLimitStats {
   Counter TotalHits, OverLimit, NearLimit, OverLimitWithLocalCache;
+  Counter ShadowMode;  // extension (rl_hip.h RL_RULE_SHADOW): over-limit decisions reported as OK
 };
 
 // Stats scope: counters are shared by name (`<FullKey>.total_hits` ...), like
@@ -74,6 +75,7 @@ struct RateLimit {
   RateLimitLimit Limit;
   bool SleepOnThrottle = false;
   bool ReportDetails = false;
+  bool ShadowMode = false;  // extension (rl_hip.h RL_RULE_SHADOW); the fork's config has no shadow_mode key
 };
 // config.NewRateLimit  src/config/config_impl.go:79-89
 std::shared_ptr<RateLimit> NewRateLimit(uint32_t requests_per_unit, Unit unit, const std::string& key,
@@ -162,7 +164,7 @@ class HipRateLimitCache : public RateLimitCache {
  private:
   struct Call;
   void submitter();
-  uint32_t rule_id(const RateLimitLimit& l);
+  uint32_t rule_id(const RateLimitLimit& l, bool shadow);
   void run_batch(std::vector<std::shared_ptr<Call>>& calls);
 
   HipSettings s_;

@@ -145,7 +145,16 @@ struct __attribute__((aligned(16))) DevRule {
   uint32_t near;     // uint32(floor(float64(float32(L) * ratio)))  base_limiter.go:86
   uint32_t div;      // UnitToDivider
   uint32_t unit;
+  uint32_t shadow;   // 1: RL_RULE_SHADOW (OVER_LIMIT reported as OK + RL_FLAG_SHADOW)
+  uint32_t pad[3];
 };
+
+// Shadow mode (rl_hip.h RL_RULE_SHADOW): an OVER_LIMIT code becomes OK with RL_FLAG_SHADOW.
+__host__ __device__ inline uint32_t shadow_code(uint32_t code_flags, uint32_t shadow) {
+  return (shadow && (code_flags & 0xFFu) == RL_CODE_OVER_LIMIT)
+             ? ((code_flags & ~0xFFu) | RL_CODE_OK | (RL_FLAG_SHADOW << 8))
+             : code_flags;
+}
 
 // Device error flags (bitmask in EngineCtl.err).
 enum : uint32_t {

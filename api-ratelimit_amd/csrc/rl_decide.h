@@ -398,6 +398,7 @@ RL_DEV void decide_one(const SortedRec& r, const SegInfo& si, const DevRule& R, 
       }
     }
   }
+  st.code_flags = shadow_code(st.code_flags, R.shadow);
   out[r.idx] = st;
   if (throttle) atomicMax(&req_thr[thr_idx], throttle);
 }

@@ -1011,9 +1011,12 @@ int rl_load_rules(rl_engine* e, const rl_rule* rules, uint32_t n) {
   if (e->n_fl) return e->fail(RL_ESTATE, "rl_load_rules while a batch is in flight");
   std::vector<DevRule> h(n);
   for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t u = rules[i].unit;
+    const uint32_t u = rules[i].unit & ~RL_RULE_SHADOW;
     if (u < RL_UNIT_SECOND || u > RL_UNIT_DAY)
-      return e->fail(RL_EINVAL, "rule %u: unit %u is not SECOND/MINUTE/HOUR/DAY (utilities.go:31 panics)", i, u);
+      return e->fail(RL_EINVAL, "rule %u: unit %u is not SECOND/MINUTE/HOUR/DAY (utilities.go:31 panics)", i,
+                     rules[i].unit);
+    h[i] = DevRule{};
+    h[i].shadow = (rules[i].unit & RL_RULE_SHADOW) ? 1u : 0u;
     h[i].L = rules[i].requests_per_unit;
     // nearLimitThreshold = uint32(math.Floor(float64(float32(L) * nearLimitRatio)))  base_limiter.go:86
     const float p = (float)rules[i].requests_per_unit * e->cfg.near_limit_ratio;

@@ -1156,7 +1156,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
     const HotBucket& hx = hb[b];
     const DevRule& rl = rules[rule];
     if (hx.flags & HB_FROZEN_PRE) {
-      out[i] = tile::local_hit_status(a.h, rl.div - now_mod);  // every descriptor is a local-cache hit
+      out[i] = tile::local_hit_status(a.h, rl.div - now_mod, rl.shadow);  // every descriptor is a local-cache hit
       continue;
     }
     const uint64_t after = hx.base + P;
@@ -1168,13 +1168,13 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
     const uint32_t rs = s_rstar[b];
     if (rs != 0xFFFFFFFFu) {  // the freezing descriptor is in this tile, at or before this one
       if (a.req > rs) {
-        out[i] = tile::local_hit_status(a.h, rl.div - now_mod);
+        out[i] = tile::local_hit_status(a.h, rl.div - now_mod, rl.shadow);
       } else {  // same request as the freezing descriptor: its INCRBY still happens
         tile::decide_at(i, a.req, rule, a.h, now_mod, hx.base, P, SEG_NO_FREEZE, rules, out, req_thr, routed);
         atomicMax(hot_counter(hx), (uint32_t)after);
       }
     } else if (a.req > q0) {  // froze in an earlier tile, in a request <= q0
-      out[i] = tile::local_hit_status(a.h, rl.div - now_mod);
+      out[i] = tile::local_hit_status(a.h, rl.div - now_mod, rl.shadow);
     } else {  // a request that began in an earlier tile: decided by k4_group
       const uint32_t e = atomicAdd(&ctl->tile_ctr[DFR_CTR][0], 1u);
       Deferred df;
@@ -1343,7 +1343,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
       const Deferred df = dfr[e];
       const HotBucket& x = hb[df.bucket];
       if (df.req > x.rstar) {
-        out[df.idx] = tile::local_hit_status(df.h, rules[df.rule].div - df.now_mod);
+        out[df.idx] = tile::local_hit_status(df.h, rules[df.rule].div - df.now_mod, rules[df.rule].shadow);
       } else {
         tile::decide_at(df.idx, df.req, df.rule, df.h, df.now_mod, x.base, df.P, SEG_NO_FREEZE, rules, out, req_thr,
                       routed);

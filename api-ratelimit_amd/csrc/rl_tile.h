@@ -394,10 +394,10 @@ RL_DEV SegEl seg_op(const SegEl a, const SegEl b) {
 }
 
 
-RL_DEV rl_status local_hit_status(uint32_t h, uint32_t reset) {
+RL_DEV rl_status local_hit_status(uint32_t h, uint32_t reset, uint32_t shadow) {
   // base_limiter.go:76-81: OVER_LIMIT from the local cache, no INCRBY
   rl_status st;
-  st.code_flags = RL_CODE_OVER_LIMIT | ((RL_FLAG_HAS_LIMIT | RL_FLAG_LOCAL_CACHE_HIT) << 8);
+  st.code_flags = shadow_code(RL_CODE_OVER_LIMIT | ((RL_FLAG_HAS_LIMIT | RL_FLAG_LOCAL_CACHE_HIT) << 8), shadow);
   st.limit_remaining = 0;
   st.reset_s = reset;
   st.over_limit_delta = h;

@@ -29,7 +29,8 @@ UNIT_UNKNOWN, SECOND, MINUTE, HOUR, DAY = 0, 1, 2, 3, 4
 UNIT_NAMES = {SECOND: "SECOND", MINUTE: "MINUTE", HOUR: "HOUR", DAY: "DAY"}
 UNIT_DIVIDER = {SECOND: 1, MINUTE: 60, HOUR: 3600, DAY: 86400}
 CODE_UNKNOWN, CODE_OK, CODE_OVER_LIMIT = 0, 1, 2
-FLAG_HAS_LIMIT, FLAG_LOCAL_CACHE_HIT = 1, 2
+FLAG_HAS_LIMIT, FLAG_LOCAL_CACHE_HIT, FLAG_SHADOW = 1, 2, 4
+RULE_SHADOW = 0x100  # RL_RULE_SHADOW: shadow-mode rule (extension; rl_hip.h)
 
 RL_ERRORS = {-1: "RL_EINVAL", -2: "RL_EHIP", -3: "RL_ENOSPC", -4: "RL_ECAPACITY", -5: "RL_ESTATE", -6: "RL_EDEVICE",
              -7: "RL_EPEER", -8: "RL_ECOMM"}
@@ -312,10 +313,11 @@ class Engine:
             raise RedisError(f"{what}: {RL_ERRORS.get(rc, rc)}: {msg}", rc)
 
     def load_rules(self, rules: Sequence[tuple]):
+        """rules: (requests_per_unit, unit) or (requests_per_unit, unit, shadow_mode)."""
         arr = (RlRule * max(1, len(rules)))()
-        for i, (L, u) in enumerate(rules):
-            arr[i].requests_per_unit = L
-            arr[i].unit = u
+        for i, r in enumerate(rules):
+            arr[i].requests_per_unit = r[0]
+            arr[i].unit = r[1] | (RULE_SHADOW if len(r) > 2 and r[2] else 0)
         self._check(self.lib.rl_load_rules(self.h, arr, len(rules)), "rl_load_rules")
 
     def submit(self, b: Batch):
@@ -540,6 +542,7 @@ class RateLimitStats:
     OverLimit: Counter = field(default_factory=Counter)
     NearLimit: Counter = field(default_factory=Counter)
     OverLimitWithLocalCache: Counter = field(default_factory=Counter)
+    ShadowMode: Counter = field(default_factory=Counter)  # extension (RULE_SHADOW)
 
 
 class StatsStore:
@@ -565,12 +568,14 @@ class RateLimit:
     Limit: RateLimitLimit
     SleepOnThrottle: bool = False
     ReportDetails: bool = False
+    ShadowMode: bool = False  # extension: the fork's config has no shadow_mode (config_impl.go:49-59)
 
 
 def NewRateLimit(requests_per_unit: int, unit: int, key: str, scope: StatsStore, sleep_on_throttle=False,
-                 report_details=False) -> RateLimit:
-    """config.NewRateLimit  src/config/config_impl.go:79-89"""
-    return RateLimit(key, scope.get(key), RateLimitLimit(requests_per_unit, unit), sleep_on_throttle, report_details)
+                 report_details=False, shadow_mode=False) -> RateLimit:
+    """config.NewRateLimit  src/config/config_impl.go:79-89 (+ shadow_mode, an extension)"""
+    return RateLimit(key, scope.get(key), RateLimitLimit(requests_per_unit, unit), sleep_on_throttle, report_details,
+                     shadow_mode)
 
 
 @dataclass
@@ -618,8 +623,8 @@ class HipRateLimitCache:
         self.rules = []
         self.dirty = False
 
-    def _rule(self, lim: RateLimitLimit) -> int:
-        k = (lim.RequestsPerUnit, lim.Unit)
+    def _rule(self, lim: RateLimitLimit, shadow: bool = False) -> int:
+        k = (lim.RequestsPerUnit, lim.Unit, bool(shadow))
         if k not in self.rule_ids:
             self.rule_ids[k] = len(self.rules)
             self.rules.append(k)
@@ -645,7 +650,7 @@ class HipRateLimitCache:
                 if lim is None:
                     rules.append(NIL_RULE)
                 else:
-                    rules.append(self._rule(lim.Limit))
+                    rules.append(self._rule(lim.Limit, lim.ShadowMode))
                     lim.Stats.TotalHits.Add(h)  # base_limiter.go:49-51
             reqs.append((request.Domain, request.Descriptors, rules, request.HitsAddend, now))
         if self.dirty:
@@ -669,5 +674,7 @@ class HipRateLimitCache:
                 if fl & FLAG_LOCAL_CACHE_HIT:
                     lim.Stats.OverLimitWithLocalCache.Add(int(s["over_limit_delta"]))
                 lim.Stats.NearLimit.Add(int(s["near_limit_delta"]))
+                if fl & FLAG_SHADOW:
+                    lim.Stats.ShadowMode.Add(1)
             out.append(DoLimitResponse(sts, int(thr[r])))
         return out

@@ -36,8 +36,11 @@ enum { RL_CODE_UNKNOWN = 0, RL_CODE_OK = 1, RL_CODE_OVER_LIMIT = 2 };
 /* rl_status.code_flags bits 8.. */
 enum {
   RL_FLAG_HAS_LIMIT = 1u,       /* DescriptorStatus.CurrentLimit != nil and DurationUntilReset set */
-  RL_FLAG_LOCAL_CACHE_HIT = 2u  /* over limit via the local cache: add over_limit_delta to
+  RL_FLAG_LOCAL_CACHE_HIT = 2u, /* over limit via the local cache: add over_limit_delta to
                                    OverLimitWithLocalCache too (base_limiter.go:76-81) */
+  RL_FLAG_SHADOW = 4u           /* extension (rule with RL_RULE_SHADOW): the descriptor was over its limit
+                                   and is reported OK; add 1 to Stats.ShadowMode. Counters, local cache,
+                                   limit_remaining and the over/near deltas are those of the OVER_LIMIT decision */
 };
 
 /* error codes */
@@ -86,8 +89,15 @@ enum {
 /* One rate-limit rule: config.RateLimit.Limit (src/config/config.go:26-32). */
 typedef struct rl_rule {
   uint32_t requests_per_unit;
-  uint32_t unit; /* RL_UNIT_SECOND..RL_UNIT_DAY; anything else is RL_EINVAL (utilities.go:31 panics) */
+  uint32_t unit; /* RL_UNIT_SECOND..RL_UNIT_DAY, optionally | RL_RULE_SHADOW; anything else is RL_EINVAL
+                    (utilities.go:31 panics) */
 } rl_rule;
+/* Shadow mode (BASELINE config 4; an extension: this fork has none, config_impl.go:49-59 rejects a
+ * shadow_mode key). A rule whose unit carries this bit never answers OVER_LIMIT: such a decision
+ * is reported as RL_CODE_OK with RL_FLAG_SHADOW, everything else unchanged (envoyproxy/ratelimit's
+ * later `shadow_mode`: counters still increment, the local cache still freezes the key, over/near
+ * stats still count). Parity unpinned by a reference fixture. */
+#define RL_RULE_SHADOW 0x100u
 
 /* A batch of requests in serial (enqueue) order. Descriptor i belongs to request req_of[i]
  * (non-decreasing). Its cache-key prefix is the exact byte string

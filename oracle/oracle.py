@@ -92,7 +92,9 @@ class Oracle:
             pass
 
     def load_rules(self, rules):
-        arr = np.array([(L_, u) for L_, u in rules], dtype=np.uint32).reshape(-1, 2)
+        # (L, unit) or (L, unit, shadow_mode): shadow rides in the unit's RLO_RULE_SHADOW bit
+        arr = np.array([(r[0], r[1] | (0x100 if len(r) > 2 and r[2] else 0)) for r in rules],
+                       dtype=np.uint32).reshape(-1, 2)
         rc = self.L.rlo_load_rules(self.h, _p(arr), len(rules))
         if rc:
             raise ValueError(f"rlo_load_rules: {rc}")

@@ -63,6 +63,7 @@ struct rlo_engine {
   bool per_second_split;  // perSecondClient != nil (fixed_cache_impl.go:75)
   std::vector<rlo_rule> rules;
   std::vector<uint32_t> near_thr;  // per rule, base_limiter.go:86
+  std::vector<char> shadow;        // per rule: RLO_RULE_SHADOW (extension, do_limit)
   // Redis stand-ins: main client and per-second client (fixed_cache_impl.go:74-85).
   std::unordered_map<std::string, RKey> redis[2];
   // freecache stand-in: over-limit keys and their expiry (base_limiter.go:94-106; freecache
@@ -104,10 +105,13 @@ void rlo_destroy(rlo_engine* e) {
 
 int rlo_load_rules(rlo_engine* e, const rlo_rule* rules, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i)
-    if (unit_to_divider(rules[i].unit) == 0) return -2;
+    if (unit_to_divider(rules[i].unit & ~RLO_RULE_SHADOW) == 0) return -2;
   e->rules.assign(rules, rules + n);
   e->near_thr.resize(n);
+  e->shadow.resize(n);
   for (uint32_t i = 0; i < n; ++i) {
+    e->shadow[i] = (rules[i].unit & RLO_RULE_SHADOW) != 0;
+    e->rules[i].unit &= ~RLO_RULE_SHADOW;
     // nearLimitThreshold = uint32(math.Floor(float64(float32(L) * ratio)))  base_limiter.go:86
     float p = (float)rules[i].requests_per_unit * e->near_ratio;  // float32 * float32
     e->near_thr[i] = (uint32_t)std::floor((double)p);
@@ -270,6 +274,13 @@ uint32_t do_limit(rlo_engine* e, const std::vector<Desc>& keys, const uint32_t* 
     uint32_t thr = 0;
     // limitBeforeIncrease := limitAfterIncrease - hitsAddend (uint32 wrap)  fixed_cache_impl.go:109-110
     decide(L, near, div, now, h, results[k] - h, results[k], local_hit[k] != 0, has, &out[i], &thr);
+    // Shadow mode — an extension: this fork has none (config_impl.go:49-59 rejects the key).
+    // Restated from envoyproxy/ratelimit's later GetResponseDescriptorStatus: an OVER_LIMIT
+    // decision (from Redis or the local cache) is answered OK and counted in Stats.ShadowMode;
+    // the INCRBY, the local-cache Set below and the over/near stats are unchanged. Parity
+    // unpinned (no reference fixture).
+    if (has && e->shadow[r] && (out[i].code_flags & 0xFFu) == RLO_CODE_OVER_LIMIT)
+      out[i].code_flags = (out[i].code_flags & ~0xFFu) | RLO_CODE_OK | (RLO_FLAG_SHADOW << 8);
     // response.ThrottleMillis = max(...)  base_limiter.go:163-165
     if (thr > throttle_max) throttle_max = thr;
     // localCache.Set(key, TTL = UnitToDivider(unit)) on OVER_LIMIT from Redis  base_limiter.go:94-106
@@ -335,6 +346,7 @@ int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* 
   for (int t = 0; t < T; ++t) {
     shard[t]->rules = e->rules;
     shard[t]->near_thr = e->near_thr;
+    shard[t]->shadow = e->shadow;
   }
   // (1) keys and shard lists per request range
   struct Item { uint32_t req; Desc d; };

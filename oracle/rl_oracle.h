@@ -35,9 +35,12 @@ enum { RLO_UNIT_UNKNOWN = 0, RLO_UNIT_SECOND = 1, RLO_UNIT_MINUTE = 2, RLO_UNIT_
 /* envoy.service.ratelimit.v3.RateLimitResponse.Code */
 enum { RLO_CODE_UNKNOWN = 0, RLO_CODE_OK = 1, RLO_CODE_OVER_LIMIT = 2 };
 /* status flags */
-enum { RLO_FLAG_HAS_LIMIT = 1u, RLO_FLAG_LOCAL_CACHE_HIT = 2u };
+enum { RLO_FLAG_HAS_LIMIT = 1u, RLO_FLAG_LOCAL_CACHE_HIT = 2u, RLO_FLAG_SHADOW = 4u };
 
+/* unit may carry RLO_RULE_SHADOW (= RL_RULE_SHADOW): shadow mode, an extension the fork does not
+ * have (see rl_oracle.cpp do_limit) */
 typedef struct { uint32_t requests_per_unit; uint32_t unit; } rlo_rule;
+#define RLO_RULE_SHADOW 0x100u
 
 /* One descriptor's outcome. Layout-identical to rl_status in include/rl_hip.h. */
 typedef struct {

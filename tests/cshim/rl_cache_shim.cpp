@@ -49,10 +49,12 @@ void rlc_destroy(void* p) { delete static_cast<Shim*>(p); }
 
 void rlc_set_time(void* p, int64_t now) { static_cast<Shim*>(p)->ts->t.store(now); }
 
-// config.NewRateLimit(rpu, unit, key, scope): the rule's index, for rlc_do_limit / rlc_stats
+// config.NewRateLimit(rpu, unit, key, scope): the rule's index, for rlc_do_limit / rlc_stats;
+// unit | RL_RULE_SHADOW sets RateLimit.ShadowMode (extension)
 int rlc_add_rule(void* p, uint32_t rpu, uint32_t unit, const char* key) {
   auto* s = static_cast<Shim*>(p);
-  s->rules.push_back(NewRateLimit(rpu, (Unit)unit, key, s->store, false, false));
+  s->rules.push_back(NewRateLimit(rpu, (Unit)(unit & ~RL_RULE_SHADOW), key, s->store, false, false));
+  s->rules.back()->ShadowMode = (unit & RL_RULE_SHADOW) != 0;
   return (int)s->rules.size() - 1;
 }
 
@@ -98,6 +100,7 @@ void rlc_stats(void* p, int rule, uint64_t* out) {
   out[1] = st.OverLimit.Value();
   out[2] = st.NearLimit.Value();
   out[3] = st.OverLimitWithLocalCache.Value();
+  out[4] = st.ShadowMode.Value();
 }
 
 const char* rlc_error(void* p) { return static_cast<Shim*>(p)->err.c_str(); }

@@ -60,9 +60,10 @@ class Mirror:
         return [tuple(out[4 * i:4 * i + 4]) for i in range(n)], thr.value
 
     def stats(self, rule):
-        o = (C.c_uint64 * 4)()
+        o = (C.c_uint64 * 5)()
         self.lib.rlc_stats(self.h, rule, o)
-        return dict(total_hits=o[0], over_limit=o[1], near_limit=o[2], over_limit_with_local_cache=o[3])
+        return dict(total_hits=o[0], over_limit=o[1], near_limit=o[2], over_limit_with_local_cache=o[3],
+                    shadow_mode=o[4])
 
     def close(self):
         self.lib.rlc_destroy(self.h)
@@ -129,4 +130,22 @@ def test_concurrent_callers_share_batches(local_cache):
             tot[ru[0]] += max(1, h)
     for r in (0, 1):
         assert m.stats(ids[r])["total_hits"] == tot[r]
+    m.close()
+
+
+def test_shadow_rule_through_cpp_mirror():
+    """RateLimit.ShadowMode (extension, rl_hip.h RL_RULE_SHADOW) through the C++ DoLimit mirror:
+    over-limit answers OK, Stats.ShadowMode counts them, the other stats match the enforced twin."""
+    m = Mirror(True)
+    sh = m.add_rule(2, hiprl.SECOND | hiprl.RULE_SHADOW, "shadow")
+    en = m.add_rule(2, hiprl.SECOND, "enforced")
+    m.lib.rlc_set_time(m.h, 1_700_000_000)
+    codes = []
+    for _ in range(5):
+        got, _ = m.do_limit("d", [[("a", "b")], [("c", "d")]], [sh, en], 1)
+        codes.append([g[0] for g in got])
+    assert codes == [[1, 1]] * 2 + [[1, 2]] * 3
+    s, e = m.stats(sh), m.stats(en)
+    assert s["shadow_mode"] == 3 and e["shadow_mode"] == 0
+    assert {k: v for k, v in s.items() if k != "shadow_mode"} == {k: v for k, v in e.items() if k != "shadow_mode"}
     m.close()

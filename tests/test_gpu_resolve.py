@@ -95,20 +95,27 @@ def test_resolve_empty_and_errors_gpu():
         eng.load_tree(fwd, names)
 
 
+@pytest.mark.parametrize("shadow", [False, True])
 @pytest.mark.parametrize("local_cache", [False, True])
-def test_config4_stream_resolved_on_device_gpu(local_cache):
+def test_config4_stream_resolved_on_device_gpu(local_cache, shadow):
     """Config 4's shape end to end at test size: 4-entry descriptors, device GetLimit, then
     device decisions; the oracle gets the oracle's resolution. Several descriptors per
-    request, h in 0..8, the local over-limit cache on and off."""
+    request, h in 0..8, the local over-limit cache on and off, and (config 4's shadow mode, an
+    extension: tests/test_shadow.py) every other rule of the tree in shadow mode."""
     y = workload.config4_yaml(4)
     orc_cfg = config_oracle.Config([("c4.yaml", y)])
     cfg = rl_config.RateLimitConfig([("c4.yaml", y)])
     eng = hiprl.Engine(local_cache=local_cache)
     cfg.install(eng)
+    rules = [tuple(r) for r in cfg.rule_table()]
+    if shadow:
+        rules = [(r[0], r[1], k % 2 == 0) for k, r in enumerate(rules)]
+        eng.load_rules(rules)
     o = oracle.Oracle(near_limit_ratio=0.8, local_cache=local_cache)
-    o.load_rules(cfg.rule_table())
+    o.load_rules(rules)
     rng = np.random.default_rng(40)
     t = 1_700_000_000
+    n_sh = 0
     for batch in range(6):
         descs = workload.config4_descriptors(100 + batch, 6000, values=40)
         rid = eng.resolve(rl_config.ResolveBatch([(d, e, None) for d, e in descs]))
@@ -124,7 +131,11 @@ def test_config4_stream_resolved_on_device_gpu(local_cache):
         b = hiprl.build_batch(reqs)
         st, thr = eng.submit(b)
         ost, othr = o.submit(b)
-        streams.assert_same(st, thr, ost, othr, f"config4 batch {batch}")
+        streams.assert_same(st, thr, ost, othr, f"config4 batch {batch} shadow={shadow}")
+        if shadow:
+            n_sh += int(((st["code_flags"] >> 8) & hiprl.FLAG_SHADOW).astype(bool).sum())
+    if shadow:
+        assert n_sh > 0
 
 
 @pytest.mark.parametrize("local_cache", [False, True])
