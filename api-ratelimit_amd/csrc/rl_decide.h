@@ -198,15 +198,18 @@ RL_DEV void exotic_sequence(KeyState& s, const TableDesc& tab, const DevRule* __
 // older slots are free for it). gmax / cnt: the batch's generation and descriptor count per
 // region (0 = untouched).
 RL_DEV uint32_t region_live(const RegionOcc& o, uint32_t gen) { return (o.gen < gen) ? 0u : o.live; }
-RL_DEV bool capacity_ok(const RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* cnt) {
-  RegionOcc o[8];  // all eight loads in flight together (no load behind a branch)
-#pragma unroll
-  for (int r = 0; r < 8; ++r) o[r] = occ[r];
+RL_DEV bool capacity_ok(const RegionOcc (&o)[8], const uint32_t* gmax, const uint32_t* cnt) {
   bool ok = true;
 #pragma unroll
   for (int r = 0; r < 8; ++r)
     ok &= !cnt[r] || (uint64_t)region_live(o[r], gmax[r]) + cnt[r] <= (uint64_t)o[r].limit;
   return ok;
+}
+RL_DEV bool capacity_ok(const RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* cnt) {
+  RegionOcc o[8];  // all eight loads in flight together (no load behind a branch)
+#pragma unroll
+  for (int r = 0; r < 8; ++r) o[r] = occ[r];
+  return capacity_ok(o, gmax, cnt);
 }
 // After the batch: add its new slots (one thread).
 RL_DEV void occ_update(RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* ins) {

@@ -394,7 +394,8 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     }
     timed(KT_V4_SCAN, [&] {
       launch_v4_scan(stream, n, v4_tcount[sl], v4_thsum[sl], v4_hoff, v4_fpart[sl], hot_t + HOT_SLOTS, v4_hb, tab,
-                     d_cand, v4_heads + ng, v4_ins + (size_t)ng * 4, v4_scratch, d_poison, d_occ, c4);
+                     want_cand ? d_cand : nullptr, v4_heads + ng, v4_ins + (size_t)ng * 4, v4_scratch, d_poison,
+                     d_occ, c4);
     });
     timed(KT_V4_PLACE, [&] {
       launch_v4_place(stream, b, srt, v4_tcount[sl], v4_scratch, d_rules, v4_hoff, v4_hb, lc, out,

@@ -372,13 +372,13 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
 constexpr int SCAN_NT = 1024;
 constexpr int SCAN_W = SCAN_NT / 64;
 constexpr int SCAN_U = 16;  // column loads in flight per lane (columns longer than SCAN_Q)
-// MSD blocks come in pairs per group of 64 buckets: 32 buckets each over 32 tile slices
-// (lane = slice % 2 * 32 + bucket, wave = slice / 2), so 64 CUs pull the MSD columns; the
-// second block of a pair to finish packs the group's ranges from both blocks' totals.
-constexpr int MSD_HALF = 32;
-constexpr int MSD_SCAN_BLOCKS = 2 * MSD_GROUPS;
-constexpr int PAIR_CTR = 8;  // EngineCtl::tile_ctr[PAIR_CTR][g]: blocks of MSD group g done
-constexpr int SCAN_Q = 16;  // MSD column entries per lane kept in registers
+// One MSD block per group of 64 buckets (lane = bucket, wave = tile slice, up to SCAN_Q tiles
+// per lane in registers): the block holds the group's 64 bucket totals itself and packs the
+// group's k4_group ranges right away (a pair of 32-bucket blocks needed a hand-off through
+// global memory and a pair counter: three more round trips on k4_scan's critical path).
+constexpr int MSD_PER_BLOCK = 64;
+constexpr int MSD_SCAN_BLOCKS = MSD_GROUPS;
+constexpr int SCAN_Q = 32;  // MSD column entries per lane kept in registers (16 slices x 32 = 512 tiles)
 // Hot blocks take 16 buckets each over 64 tile slices (lane = slice % 4 * 16 + bucket, wave =
 // slice / 4): 32 blocks instead of 8, so the hot columns (u16 starts + u64 h sums of every
 // tile) are pulled by 32 CUs, 8 tiles per lane at config 3.
@@ -386,31 +386,33 @@ constexpr int HOT_PER_BLOCK = 16;
 constexpr int HOT_SCAN_BLOCKS = HOT_BUCKETS / HOT_PER_BLOCK;
 constexpr int HOT_Q = 16;   // hot column entries per lane kept in registers
 static_assert(HOT_BUCKETS % 64 == 0 && MSD_BUCKETS % 64 == 0, "bucket blocks");
-static_assert(T < 65536 && SCAN_Q % 2 == 0, "per-tile counts pack in u16 pairs");
-static_assert(MSD_GROUPS <= 64 && PAIR_CTR != DONE_CTR && PAIR_CTR != DFR_CTR && PAIR_CTR != CAND_CTR &&
-                  (PAIR_CTR < INS_CTR0 || PAIR_CTR >= INS_CTR0 + INS_LINES) && PAIR_CTR >= SHARD_CTR0 + 8,
-              "pair counters: one control-block row of their own");
+static_assert(T < 65536 && MSD_GROUPS <= 64, "k4_scan geometry");
 
-// Counts of bucket b (= this lane's) in tiles [tb, tb + SCAN_Q) ∩ [tb, te), for 32-lane
-// segments of 32 consecutive buckets starting at b0: each lane loads its bucket's start and
-// takes the next bucket's start from the next lane; the segment's last lane takes entry 32
-// of the row segment.
-RL_DEV void column_counts(const uint16_t* __restrict__ tstart, uint32_t b, uint32_t b0, uint32_t tb, uint32_t te,
-                          uint32_t (&cq)[SCAN_Q]) {
+// Records of the group's bucket b0 + lane in tiles [tb, te) ∩ [tb, tb + SCAN_Q): one dword of
+// the tile's row per lane and tile, so each bucket start is loaded once. Lane l reads dword
+// (l + 1) / 2 of the group's row segment: an even lane holds its bucket's start and end, an
+// odd lane its bucket's end and the next one's (its start is the even lane below's high
+// half; lane 63 reads entry 64 of the segment). Sums of the low and high halves over the
+// tiles first, then one shuffle.
+static_assert(ROW % 2 == 0 && HOT_BUCKETS % 2 == 0 && NBUCKETS + 1 <= ROW, "dword-aligned row segments");
+RL_DEV uint32_t column_total(const uint16_t* __restrict__ tstart, uint32_t b0, uint32_t tb, uint32_t te) {
   const uint32_t lane = threadIdx.x & 63;
-  uint32_t e[SCAN_Q];
+  const uint32_t di = (lane + 1u) >> 1;
+  uint32_t d[SCAN_Q];
 #pragma unroll
   for (int u = 0; u < SCAN_Q; ++u) {  // clamped tiles: all loads in flight together
-    const uint16_t* row = tstart + (size_t)min(tb + u, te - 1u) * ROW;
-    cq[u] = row[b];
-    e[u] = row[b0 + MSD_HALF];
+    const uint32_t* row = reinterpret_cast<const uint32_t*>(tstart + (size_t)min(tb + u, te - 1u) * ROW + b0);
+    d[u] = row[di];
   }
+  uint32_t slo = 0, shi = 0;
 #pragma unroll
   for (int u = 0; u < SCAN_Q; ++u) {
-    const uint32_t nx = __shfl_down(cq[u], 1, MSD_HALF);
-    const uint32_t d = ((lane & (MSD_HALF - 1u)) < MSD_HALF - 1u ? nx : e[u]) - cq[u];
-    cq[u] = tb + u < te ? d : 0u;
+    const uint32_t x = tb + u < te ? d[u] : 0u;
+    slo += x & 0xFFFFu;
+    shi += x >> 16;
   }
+  const uint32_t shi_prev = __shfl_up(shi, 1, 64);
+  return (lane & 1u) ? slo - shi_prev : shi - slo;
 }
 
 __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ tstart,
@@ -437,25 +439,40 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
   }
   ST5(0);
   const bool hotb = blockIdx.x < (uint32_t)HOT_SCAN_BLOCKS;  // block-uniform
+  const uint32_t errs = ctl->err;
+  const HotEntry he = hot_list[((blockIdx.x % (uint32_t)HOT_SCAN_BLOCKS) * HOT_PER_BLOCK + (lane & 15u)) >> 1];
+  RegionOcc oc[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) oc[r] = occ[r];
   // Hot blocks fold the per-tile partials (generation range per region, nil count; the hot
   // claims need the generations, block 0 publishes them). The partials' loads are issued
   // here and reduced after the column pass, so the two latencies overlap; MSD blocks need
   // none of it.
-  if (tid < FP_PART_WORDS) s_f[tid] = 0;
-  uint32_t fv[FP_PART_WORDS];
+  // Partials: wave v folds words v, v + 16, v + 32 over the tiles (lane = tile mod 64, FPT
+  // tiles a lane in registers, loaded here at clamped indices, all in flight together), one
+  // wave reduction per word instead of one per word in every wave.
+  constexpr int FPW = (FP_PART_WORDS + SCAN_W - 1) / SCAN_W;
+  constexpr int FPT = 8;
+  uint32_t fl[FPW][FPT];
+  if (hotb) {
 #pragma unroll
-  for (int w = 0; w < FP_PART_WORDS; ++w)
-    fv[w] = hotb && tid < ntiles ? fpart[(size_t)w * ntiles + tid] : 0u;
+    for (int q = 0; q < FPW; ++q)
+#pragma unroll
+      for (int u = 0; u < FPT; ++u) {
+        const uint32_t w = min(wave + (uint32_t)q * SCAN_W, (uint32_t)FP_PART_WORDS - 1u);
+        const uint32_t t = min(lane + (uint32_t)u * 64u, ntiles - 1u);
+        fl[q][u] = fpart[(size_t)w * ntiles + t];
+      }
+  }
 
   // Column pass. MSD blocks: bucket b = lane, tiles [wave*Q, wave*Q + Q). Hot blocks: bucket
   // b = lane % 16 of the block's 16, tile slice wave * 4 + lane / 16.
-  const uint32_t m2 = blockIdx.x - HOT_SCAN_BLOCKS;  // MSD block: half m2 & 1 of group m2 / 2
-  const uint32_t m = m2 >> 1, mh = m2 & 1u;
-  const uint32_t bpb = hotb ? HOT_PER_BLOCK : MSD_HALF;  // buckets per block
+  const uint32_t m = blockIdx.x - HOT_SCAN_BLOCKS;  // MSD block: group m
+  const uint32_t bpb = hotb ? HOT_PER_BLOCK : MSD_PER_BLOCK;  // buckets per block
   const uint32_t bb = lane & (bpb - 1u);
   const uint32_t nsl = SCAN_NT / bpb;  // tile slices
   const uint32_t slice = wave * (64 / bpb) + lane / bpb;
-  const uint32_t mb0 = HOT_BUCKETS + m * 64 + mh * MSD_HALF;  // MSD: first bucket of the block
+  const uint32_t mb0 = HOT_BUCKETS + m * 64;  // MSD: first bucket of the block
   const uint32_t b = hotb ? blockIdx.x * HOT_PER_BLOCK + bb : mb0 + bb;
   const uint32_t Q = (ntiles + nsl - 1) / nsl;
   const uint32_t tb = min(ntiles, slice * Q), te = min(ntiles, tb + Q);
@@ -485,10 +502,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
       hs += hq[u];
     }
   } else if (in_regs) {
-    uint32_t cq[SCAN_Q];
-    column_counts(tstart, b, mb0, tb, te, cq);
-#pragma unroll
-    for (int u = 0; u < SCAN_Q; ++u) c += cq[u];
+    c = column_total(tstart, mb0, tb, te);
   } else {
     for (uint32_t t = tb; t < te; t += SCAN_U) {
       uint32_t cv[SCAN_U];
@@ -510,20 +524,23 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
   bool span = false, cap_ok = true;
   if (hotb) {
     s_ph[wave][lane] = hs;
-    for (uint32_t g = tid + SCAN_NT; g < ntiles; g += SCAN_NT) {  // batches over SCAN_NT tiles
 #pragma unroll
-      for (int w = 0; w < FP_PART_WORDS; ++w) {
-        const uint32_t x = fpart[(size_t)w * ntiles + g];
-        fv[w] = fp_is_max(w) ? (x > fv[w] ? x : fv[w]) : fv[w] + x;
-      }
-    }
+    for (int q = 0; q < FPW; ++q) {
+      const uint32_t w = wave + (uint32_t)q * SCAN_W;
+      if (w >= (uint32_t)FP_PART_WORDS) break;  // wave-uniform
+      const bool mx = fp_is_max((int)w);
+      uint32_t v = 0;
 #pragma unroll
-    for (int w = 0; w < FP_PART_WORDS; ++w) {
-      const uint32_t x = fp_is_max(w) ? wave_max_u32(fv[w]) : tile::wave_sum(fv[w]);
-      if (lane == 0 && x) {
-        if (fp_is_max(w)) atomicMax(&s_f[w], x);
-        else atomicAdd(&s_f[w], x);
+      for (int u = 0; u < FPT; ++u) {
+        const uint32_t x = lane + (uint32_t)u * 64u < ntiles ? fl[q][u] : 0u;
+        v = mx ? max(v, x) : v + x;
       }
+      for (uint32_t t = 64u * FPT + lane; t < ntiles + lane; t += 64u) {  // more than 64 x FPT tiles
+        const uint32_t x = t < ntiles ? fpart[(size_t)w * ntiles + t] : 0u;
+        v = mx ? max(v, x) : v + x;
+      }
+      v = mx ? wave_max_u32(v) : tile::wave_sum(v);
+      if (lane == 0) s_f[w] = v;
     }
   }
   __syncthreads();
@@ -538,7 +555,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     }
     // Capacity (before any table write): every hot block computes the same verdict and
     // claims nothing when it fails; block 0 refuses the batch.
-    cap_ok = capacity_ok(occ, &s_f[FP_GMAX], &s_f[FP_CNT]);
+    cap_ok = capacity_ok(oc, &s_f[FP_GMAX], &s_f[FP_CNT]);
     if (blockIdx.x == 0) {
       if (tid < 8) ctl->gen_min[tid] = ~s_f[FP_GMIN + tid];
       else if (tid < 16) ctl->gen_max[tid - 8] = s_f[FP_GMAX + tid - 8];
@@ -562,72 +579,88 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
         hrun += sl < slice ? y : 0ull;
       }
     }
-  } else {  // bucket totals over the 32 slices
+  } else {  // bucket totals over the 16 slices
 #pragma unroll
-    for (int w = 0; w < SCAN_W; ++w) {
-#pragma unroll
-      for (int q = 0; q < 64 / MSD_HALF; ++q) ctot += s_pc[w][q * MSD_HALF + bb];
-    }
+    for (int w = 0; w < SCAN_W; ++w) ctot += s_pc[w][bb];
   }
   if (!hotb) {
     // (no per-tile offsets: k4_group gathers a range's records from each tile's run. A bucket
     // over BUCKET_CAP records sends the batch to the LSD pipeline before the table is touched.)
-    const uint32_t mb = b - HOT_BUCKETS;
     if (wave != 0) return;
     ST5(3);
     if (lane == 0) heads_out[blockIdx.x] = 0;
-    // Hand-off inside the pair: this block's 32 bucket totals (lanes 0..31 = slice 0), then
-    // the pair counter; the second block to arrive reads both halves and packs the group.
-    if (lane < (uint32_t)MSD_HALF) {
-      if (ctot > (uint32_t)BUCKET_CAP) atomicOr(&ctl->err, ERR_FALLBACK);
-      st_relaxed(&ranges[R_BTOT + mb], ctot);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t arrived = 0;
-    if (lane == 0) arrived = atomicAdd(&ctl->tile_ctr[PAIR_CTR][m], 1u);
-    if (__builtin_amdgcn_readfirstlane(arrived) == 0u) return;  // the other block packs
-    ctot = ld_relaxed(&ranges[R_BTOT + m * 64 + lane]);  // bucket lane of the group
+    if (ctot > (uint32_t)BUCKET_CAP) atomicOr(&ctl->err, ERR_FALLBACK);
     const uint32_t g = m;
     // Pack the group's 64 buckets into k4_group ranges of whole buckets, at most G_CAP records
     // each (a single larger bucket: two half ranges of its own), balanced over the group's RPG
-    // blocks: a range closes before a bucket whose midpoint would pass the even share of what
-    // is left (a k4_group block's time grows with its range's records, and the kernel lasts
-    // as long as its largest range). The walk is wave-uniform over the lanes' totals (readlane:
-    // no LDS round trip per bucket); lane 0 stores.
+    // blocks (a k4_group block's time grows with its range's records, and the kernel lasts as
+    // long as its largest range). Entries are marked in two masks: bit k of ev = entry 2k (a
+    // range starts at bucket k), of od = entry 2k | 1 (the second half of oversized bucket k);
+    // the lanes then store the entries in order in one step.
+    //   Common case, in parallel: bucket k joins range floor((E_k + c_k / 2) / t), E_k its
+    // exclusive prefix, t = ceil(total / RPG): a range closes before a bucket whose midpoint
+    // passes the next multiple of the even share. Taken when no bucket is oversized and every
+    // range fits the stage; otherwise a sequential walk (a range closes before a bucket whose
+    // midpoint would pass the even share of what is left), ~5 us of scalar code per group.
     uint32_t* rb = ranges + R_START + g * (RANGE_MAX + 1);
-    uint32_t nr = 0, cur = 0, last = 0;  // last = rb[nr]
-    uint32_t rem = tile::wave_sum(ctot), left = RPG;  // records not in closed ranges; ranges to form
-    if (lane == 0) rb[0] = 0;
-    auto close = [&](uint32_t e) {
-      ++nr;
-      if (lane == 0) rb[nr] = e;
-      last = e;
-      rem -= cur;
-      left = left > 1u ? left - 1u : 1u;
-      cur = 0;
-    };
-#pragma unroll
-    for (int k = 0; k < 64; ++k) {
-      const uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)ctot, k);
-      const uint32_t ek = (uint32_t)k << 1;
-      if (cb > (uint32_t)G_CAP) {
-        // Oversized bucket (<= BUCKET_CAP): two ranges of its own, one per fingerprint half
-        // (entries ek and ek | 1), grouped by two blocks; the next bucket starts a range.
-        if (last != ek) close(ek);
-        ++nr;
-        if (lane == 0) rb[nr] = ek | 1u;
-        last = ek | 1u;
-        left = left > 1u ? left - 1u : 1u;
-        cur = cb;
-        continue;
+    uint64_t ev = 0, od = 0;
+    const uint32_t rem0 = tile::wave_sum(ctot);
+    const uint32_t excl = wave_incl_scan_u32(ctot) - ctot;
+    const uint32_t t_share = max(rem0 / RPG + (rem0 % RPG != 0u ? 1u : 0u), 1u);
+    const uint32_t rid = min((excl + ctot / 2u) / t_share, RPG - 1u);
+    const uint32_t rid_prev = __shfl_up(rid, 1, 64);
+    const bool starts = lane == 0 || rid != rid_prev;
+    const uint64_t smask = __ballot(starts);
+    const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
+    const uint32_t nxt = (smask & above) ? (uint32_t)__ffsll((unsigned long long)(smask & above)) - 1u : 64u;
+    const uint32_t e_next = __shfl(excl, nxt & 63u, 64);
+    const uint32_t rsize = (nxt < 64u ? e_next : rem0) - excl;
+    const bool fits = __ballot(ctot > (uint32_t)G_CAP || (starts && rsize > (uint32_t)G_CAP)) == 0ull;
+    if (fits) {
+      ev = smask & ~1ull;
+    } else {
+      uint32_t cur = 0, last = 0;  // last = the latest entry
+      uint32_t rem = rem0, left = RPG;  // records not in closed ranges; ranges to form
+#pragma unroll 1
+      for (int k = 0; k < 64; ++k) {
+        const uint32_t cb = (uint32_t)__builtin_amdgcn_readlane((int)ctot, k);
+        const uint32_t ek = (uint32_t)k << 1;
+        if (cb > (uint32_t)G_CAP) {
+          // Oversized bucket (<= BUCKET_CAP): two ranges of its own, one per fingerprint half
+          // (entries ek and ek | 1), grouped by two blocks; the next bucket starts a range.
+          if (last != ek) {
+            ev |= 1ull << k;
+            rem -= cur;
+            left = left > 1u ? left - 1u : 1u;
+          }
+          od |= 1ull << k;
+          last = ek | 1u;
+          left = left > 1u ? left - 1u : 1u;
+          cur = cb;
+          continue;
+        }
+        if (cur && (cur + cb > (uint32_t)G_CAP || (2u * cur + cb) * left > 2u * rem)) {
+          ev |= 1ull << k;
+          last = ek;
+          rem -= cur;
+          left = left > 1u ? left - 1u : 1u;
+          cur = 0;
+        }
+        cur += cb;
       }
-      if (cur && (cur + cb > (uint32_t)G_CAP || (2u * cur + cb) * left > 2u * rem)) close(ek);
-      cur += cb;
     }
-    ++nr;
-    if (lane == 0) {
-      rb[nr] = 64u << 1;
-      ranges[g] = nr;
+    {
+      const uint64_t below = lanemask_lt();
+      const uint32_t has_ev = (uint32_t)(ev >> lane) & 1u, has_od = (uint32_t)(od >> lane) & 1u;
+      const uint32_t p_ev = 1u + (uint32_t)__popcll(ev & below) + (uint32_t)__popcll(od & below);
+      if (has_ev) rb[p_ev] = lane << 1;
+      if (has_od) rb[p_ev + has_ev] = (lane << 1) | 1u;
+      const uint32_t nr = (uint32_t)__popcll(ev) + (uint32_t)__popcll(od) + 1u;
+      if (lane == 0) {
+        rb[0] = 0;
+        rb[nr] = 64u << 1;
+        ranges[g] = nr;
+      }
     }
     ST5(4);
     return;
@@ -649,6 +682,12 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
       hrun += hv[u];
     }
   }
+  const bool lead = wave == 0 && lane < (uint32_t)HOT_PER_BLOCK && ctot && !span && cap_ok &&
+                    !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME | ERR_FALLBACK));
+  // (cand = nullptr: no candidates wanted for this batch, the engine samples every 8th)
+  const uint64_t cmask = __ballot(lead && ctot >= HOT_CAND_MIN && cand != nullptr);
+  uint32_t cbase = 0;  // lane 0: the first reserved slot (read where it is used)
+  if (wave == 0 && lane == 0 && cmask) cbase = atomicAdd(&ctl->tile_ctr[CAND_CTR][0], (uint32_t)__popcll(cmask));
   if (wave == 0) {
     ST5(3);
     // Hot key leader: find or claim the key's slot and read the counter before this batch. A
@@ -659,13 +698,11 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     x.flags = 0;
     x.rstar = 0xFFFFFFFFu;
     x.ws = x.t_all = x.t_rstar = 0;
-    const uint32_t errs = ctl->err;  // flags of k4_hist
     uint32_t heads = 0;
     uint32_t ins_region = 8;  // region of a newly claimed slot
     // lanes 0..15 of wave 0 (slice 0) lead the block's 16 hot buckets
     if (lane < (uint32_t)HOT_PER_BLOCK && ctot && !span && cap_ok &&
         !(errs & (ERR_BAD_INPUT | ERR_BAD_TIME | ERR_FALLBACK))) {
-      const HotEntry he = hot_list[b >> 1];
       // the key string's window: the hot prefix's unit window of this parity
       const uint32_t uwv = s_f[FP_UW + (he.unit - 1u) * 2u + (b & 1u)];
       const uint32_t div = unit_div(he.unit);
@@ -705,7 +742,14 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
           atomicOr(&ctl->err, ERR_FALLBACK);
         heads = 1;
       }
-      if (ctot >= HOT_CAND_MIN) emit_candidate(ctl, cand, he.rule, ctot, 0xFFFFFFFFu, he.a, he.b, he.unit);
+      if (cand && ctot >= HOT_CAND_MIN) {
+        const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cbase, 0) + (uint32_t)__popcll(cmask & lanemask_lt());
+        if (c < (uint32_t)CAND_MAX) {
+          HotCand hc;
+          hc.a = he.a; hc.b = he.b; hc.unit = he.unit; hc.rule = he.rule; hc.count = ctot; hc.first_idx = 0xFFFFFFFFu;
+          cand[c] = hc;
+        }
+      }
     }
     // new slots per region of this block, two 16-bit counts a word (the last k4_group block
     // adds them to RegionOcc)
@@ -913,7 +957,8 @@ RL_DEV void g_lead_exotic(const GS& g, uint32_t k, const DevRule* __restrict__ r
 // key (a string shared by units of different sizes whose expiry falls inside the batch)
 // leaves per-position replies in P (SEG_EXOTIC). New slots are counted per region in ins[].
 RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, const TableDesc& tab, HotCand* cand,
-                   EngineCtl* ctl, bool has_pre, const SlotView& pre, int cand_on, uint32_t& heads, uint64_t& ins) {
+                   EngineCtl* ctl, const uint32_t* s_gen, bool has_pre, const SlotView& pre, int cand_on,
+                   uint32_t& heads, uint64_t& ins) {
   // k: the position that claimed the key's hash slot (any record of the key); the key's
   // results go to its last record (tail), where the decisions read them
   const uint64_t key = g.rec[k].key, lo = g.rec[k].fp_lo;
@@ -928,7 +973,7 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
   heads += 1;
   if (cand_on && n >= HOT_MIN_SEG && !mixed) emit_cand_sc1(ctl, cand, rule, n, g.rec[g.list[e0]].idx);
   const uint32_t region = key_region(key);
-  const uint32_t gen = ctl->gen_max[region];  // the region's one generation (k4_scan)
+  const uint32_t gen = s_gen[region];  // the region's one generation (k4_scan; staged in LDS)
   const uint32_t ws = region_ws(region, gen);
   Slot* slot = nullptr;
   bool existed = false;
@@ -1009,7 +1054,8 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
 template <bool LDS>
 RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__ rules, const TableDesc& tab,
                             rl_status* __restrict__ out, uint32_t* __restrict__ req_thr, HotCand* cand, int cand_on,
-                            int routed, LSeg* s_agg, LSeg* s_carry, uint32_t* sh_w, uint64_t& ins, EngineCtl* ctl) {
+                            int routed, LSeg* s_agg, LSeg* s_carry, uint32_t* sh_w, uint64_t& ins, EngineCtl* ctl,
+                            const uint32_t* s_gen) {
   const uint32_t tid = threadIdx.x, wave = tid >> 6;
   uint32_t heads = 0;
   // Insert every position into the LDS hash; the position that claims a key's hash slot leads
@@ -1060,11 +1106,12 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
   if constexpr (LDS) {
 #pragma unroll
     for (int j = 0; j < G_IPT; ++j)
-      if ((own >> j) & 1u) g_lead(g, tid + j * G_NT, rules, tab, cand, ctl, true, pre[j], cand_on, heads, ins);
+      if ((own >> j) & 1u) g_lead(g, tid + j * G_NT, rules, tab, cand, ctl, s_gen, true, pre[j], cand_on, heads, ins);
   } else {
 #pragma unroll
     for (int j = 0; j < KPT; ++j)
-      if ((own >> j) & 1u) g_lead(g, tid + j * G_NT, rules, tab, cand, ctl, false, SlotView{}, cand_on, heads, ins);
+      if ((own >> j) & 1u)
+        g_lead(g, tid + j * G_NT, rules, tab, cand, ctl, s_gen, false, SlotView{}, cand_on, heads, ins);
   }
   __threadfence_block();
   __syncthreads();
@@ -1298,6 +1345,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   __shared__ uint32_t s_rq[6];  // this block's group: range count, entries of its first two ranges; deferred count
   __shared__ uint32_t sh_w[G_W];
   __shared__ uint32_t s_ins[8];
+  __shared__ uint32_t s_gen[8];  // per region the batch's window generation (k4_scan)
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t j = blockIdx.x;
   uint32_t heads = 0;
@@ -1317,6 +1365,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
     s_heads = 0;
     s_err = ld_relaxed(&ctl->err);
   }
+  if (tid >= 8 && tid < 16) s_gen[tid - 8] = ctl->gen_max[tid - 8];
   __syncthreads();
   ST4(0);
 #ifdef RL_STAMPS
@@ -1377,7 +1426,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
         const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
         {
           const uint32_t hh = group_range<true>(gl, m, rules, tab, out, req_thr, cand, cand_on, routed, s_agg,
-                                                &s_carry, sh_w, ins, ctl);
+                                                &s_carry, sh_w, ins, ctl, s_gen);
           heads += hh;
           ST4X(0, m);
           ST4X(1, hh & 0xFFFFu);
@@ -1426,7 +1475,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
           if (mp == 0) continue;
           const GS gl{s_rec, s_P, s_list, s_grp, s_slot, s_cnt, s_end, &s_cursor, G_HASH};
           heads += group_range<true>(gl, mp, rules, tab, out, req_thr, cand, cand_on, routed, s_agg, &s_carry,
-                                     sh_w, ins, ctl);
+                                     sh_w, ins, ctl, s_gen);
         }
       } else if (split_half != 1) {
         // grouped in place in bucket order (global scratch); for a split bucket by its half-0
@@ -1444,7 +1493,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
         __threadfence_block();
         __syncthreads();
         heads += group_range<false>(gg, m, rules, tab, out, req_thr, cand, cand_on, routed, s_agg, &s_carry,
-                                    sh_w, ins, ctl);
+                                    sh_w, ins, ctl, s_gen);
       }
     }
   }
@@ -1480,24 +1529,42 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   if (!s_last) return;
   STL(0);
   // U = Σ per-block unique-key counts (this kernel and k4_scan's hot leaders); new slots per
-  // region into the occupancy counts (only for a batch that was applied)
+  // region into the occupancy counts (only for a batch that was applied); the hot-set
+  // candidates' prefix states. Every load the epilogue needs goes out first, in three
+  // dependent levels: (block words, candidates, occupancy) -> (candidates' prefix offsets or
+  // routed records) -> (prefix bytes).
   if (tid == 0) s_heads = 0;
   if (tid < 8) s_ins[tid] = 0;
-  __syncthreads();
+  constexpr int EPI = (GBLOCKS + HOT_SCAN_BLOCKS + G_NT - 1) / G_NT;
+  constexpr int CPT = CAND_MAX / G_NT;  // candidate entries per thread
+  static_assert(CAND_MAX % G_NT == 0, "candidates per thread");
+  const uint32_t nb = gridDim.x + n_scan_heads;
+  uint32_t hv[EPI], w[EPI][4];
+  HotCand cc[CPT];
+  // k4_scan's hot blocks wrote their words right behind this kernel's (the engine passes
+  // scan_heads = wg_heads + gridDim.x, scan_ins = wg_ins + 4 * gridDim.x): every thread loads
+  // all of its blocks' five words at once (clamped indices), then DPP sums per wave
+#pragma unroll
+  for (int e = 0; e < EPI; ++e) {
+    const uint32_t k = min(tid + e * G_NT, nb - 1u);
+    hv[e] = ld_relaxed(&wg_heads[k]);
+#pragma unroll
+    for (int x = 0; x < 4; ++x) w[e][x] = ld_relaxed(&wg_ins[k * 4 + x]);
+  }
+  // candidates only for a batch whose candidates the host wants (hcand set: every 8th batch)
+  const bool do_cand = hcand != nullptr;  // kernel-uniform
+  if (do_cand) {
+#pragma unroll
+    for (int e = 0; e < CPT; ++e) ld_sc1_32B(&cc[e], &cand[tid + e * G_NT]);  // unused entries: stale
+  }
+  const uint32_t nc = min((uint32_t)CAND_MAX, ld_relaxed(&ctl->tile_ctr[CAND_CTR][0]));
+  const uint32_t gm = ctl->gen_max[tid & 7u];
+  RegionOcc ro = occ[tid & 7u];
+  // the control block's header words for the host's copy (k4_scan's and the blocks' words are
+  // final: every block's stores completed before it counted itself done)
+  const uint32_t hdr = ld_relaxed(reinterpret_cast<const uint32_t*>(ctl) + (tid & 63u));
+  __syncthreads();  // s_heads / s_ins cleared
   {
-    // k4_scan's hot blocks wrote their words right behind this kernel's (the engine passes
-    // scan_heads = wg_heads + gridDim.x, scan_ins = wg_ins + 4 * gridDim.x): every thread loads
-    // all of its blocks' five words at once (clamped indices), then DPP sums per wave
-    constexpr int EPI = (GBLOCKS + HOT_SCAN_BLOCKS + G_NT - 1) / G_NT;
-    const uint32_t nb = gridDim.x + n_scan_heads;
-    uint32_t hv[EPI], w[EPI][4];
-#pragma unroll
-    for (int e = 0; e < EPI; ++e) {
-      const uint32_t k = min(tid + e * G_NT, nb - 1u);
-      hv[e] = ld_relaxed(&wg_heads[k]);
-#pragma unroll
-      for (int x = 0; x < 4; ++x) w[e][x] = ld_relaxed(&wg_ins[k * 4 + x]);
-    }
     uint32_t u = 0, cs[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int e = 0; e < EPI; ++e) {
@@ -1517,21 +1584,39 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
       if (lane == 0 && c) atomicAdd(&s_ins[r], c);
     }
   }
+  // candidates found by k4_group leaders carry their first descriptor: its prefix offsets (or
+  // the routed record's prefix state), all loads in flight together
+  uint32_t po[CPT] = {}, pl[CPT] = {};
+  uint64_t ra[CPT] = {}, rbv[CPT] = {};
+  const bool any_cand = do_cand && nc > 0 && in.n_desc > 0;  // block-uniform
+#pragma unroll
+  for (int e = 0; e < CPT && any_cand; ++e) {
+    const uint32_t i = tid + e * G_NT;
+    const uint32_t d = i < nc && cc[e].first_idx != 0xFFFFFFFFu ? min(cc[e].first_idx, in.n_desc - 1u) : 0u;
+    if (in.recs) {  // routed batch (kernel-uniform)
+      ra[e] = in.recs[d].a;
+      rbv[e] = in.recs[d].b;
+      po[e] = pl[e] = 0;
+    } else {
+      po[e] = in.off[d];
+      pl[e] = in.off[d + 1u] - po[e];
+      ra[e] = rbv[e] = 0;
+    }
+  }
   __syncthreads();
   if (tid < 8) {
     // one thread per region; also for a refused batch: its hot keys may have claimed slots in
     // k4_scan before the refusal (they hold the empty state; the rerun finds them)
-    const uint32_t r = tid, g = ctl->gen_max[r];
-    RegionOcc o = occ[r];  // loaded with gen_max, not behind it
+    const uint32_t r = tid;
     ctl->ins[r] = s_ins[r];
-    if (g) {
-      if (o.gen < g) {
-        o.gen = g;
-        o.live = s_ins[r];
+    if (gm) {
+      if (ro.gen < gm) {
+        ro.gen = gm;
+        ro.live = s_ins[r];
       } else {
-        o.live += s_ins[r];
+        ro.live += s_ins[r];
       }
-      occ[r] = o;
+      occ[r] = ro;
     }
   }
   if (tid == 8) {
@@ -1541,28 +1626,32 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
     ctl->n_inserted = n;
   }
   STL(1);
-  // hot-set candidates found by leaders: their key-prefix state
-  const uint32_t nc = min((uint32_t)CAND_MAX, ld_relaxed(&ctl->tile_ctr[CAND_CTR][0]));
-  for (uint32_t i = tid; i < nc; i += G_NT) {
-    HotCand c;
-    ld_sc1_32B(&c, &cand[i]);
-    if (c.first_idx == 0xFFFFFFFFu) {  // a hot key: state already known
-      if (hcand) hcand[i] = c;
-      continue;
+  if (any_cand && !in.recs) {
+    tile::u32x4 b0[CPT], b1[CPT];
+#pragma unroll
+    for (int e = 0; e < CPT; ++e) {
+      const tile::u32x4* q = reinterpret_cast<const tile::u32x4*>(in.blob + (po[e] & ~3u));
+      b0[e] = q[0];
+      b1[e] = q[1];
     }
-    const uint32_t d = c.first_idx;
-    const uint32_t unit = rules[c.rule].unit;
-    if (in.recs) {  // routed batch: the record already carries the prefix state
-      c.a = in.recs[d].a;
-      c.b = in.recs[d].b;
-    } else {
-      const uint32_t o0 = in.off[d], o1 = in.off[d + 1];
-      const FpState st = tile::prefix_state(in.blob, o0, o1 - o0, seed);
-      c.a = st.a;
-      c.b = st.b;
+#pragma unroll
+    for (int e = 0; e < CPT; ++e) {
+      const FpState st = tile::prefix_state_pre(b0[e], b1[e], in.blob, po[e], pl[e], seed);
+      ra[e] = st.a;
+      rbv[e] = st.b;
     }
-    c.unit = unit;
-    cand[i] = c;
+  }
+#pragma unroll
+  for (int e = 0; e < CPT && do_cand; ++e) {
+    const uint32_t i = tid + e * G_NT;
+    if (i >= nc) continue;
+    HotCand c = cc[e];
+    if (c.first_idx != 0xFFFFFFFFu) {  // a hot key's candidate already carries its state
+      c.a = ra[e];
+      c.b = rbv[e];
+      c.unit = rules[c.rule].unit;
+      cand[i] = c;
+    }
     if (hcand) hcand[i] = c;
   }
   // The batch's summary straight into the host's pinned control block (header words and the
@@ -1570,9 +1659,20 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   __syncthreads();  // ins / n_segments / n_inserted written above by threads 0..8
   if (hctl) {
     constexpr uint32_t HEAD = offsetof(EngineCtl, tile_ctr) / 4;
-    const uint32_t* cw = reinterpret_cast<const uint32_t*>(ctl);
+    static_assert(HEAD == 64 && offsetof(EngineCtl, n_segments) == 8 && offsetof(EngineCtl, n_inserted) == 12,
+                  "header words");
+    constexpr uint32_t INS0 = offsetof(EngineCtl, ins) / 4;
     uint32_t* hw = reinterpret_cast<uint32_t*>(hctl);
-    if (tid < HEAD) hw[tid] = ld_relaxed(&cw[tid]);
+    if (tid < HEAD) {
+      uint32_t v = hdr;
+      if (tid == 2) v = s_heads;
+      if (tid == 3) {
+        v = 0;
+        for (int r = 0; r < 8; ++r) v += s_ins[r];
+      }
+      if (tid >= INS0 && tid < INS0 + 8) v = s_ins[tid - INS0];
+      hw[tid] = v;
+    }
     if (tid == HEAD) hctl->tile_ctr[CAND_CTR][0] = nc;
     __threadfence_system();
   }

@@ -161,6 +161,31 @@ RL_DEV FpState prefix_state(const uint8_t* blob, uint32_t off, uint32_t len, uin
   return s;
 }
 
+// Prefix state of blob[o0, o0 + len) whose first 32 bytes from the dword at o0 & ~3 are
+// already loaded (w0, w1); longer prefixes read the rest 32 bytes a step (the blob is
+// readable 32 bytes past its end).
+RL_DEV FpState prefix_state_pre(const u32x4 w0, const u32x4 w1, const uint8_t* blob, uint32_t o0, uint32_t len,
+                                uint64_t seed) {
+  const uint32_t dw[PRE_DW + 1] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, 0u};
+  const uint32_t sh = o0 & 3u;
+  FpState s = fp_init(len, seed);
+  uint32_t rem = len;
+#pragma unroll
+  for (int k = 0; k < (PRE_DW - 1) / 2; ++k) {
+    if (rem > 0) {
+      const uint32_t lo = __builtin_amdgcn_alignbyte(dw[2 * k + 1], dw[2 * k], sh);
+      const uint32_t hi = __builtin_amdgcn_alignbyte(dw[2 * k + 2], dw[2 * k + 1], sh);
+      uint64_t w = ((uint64_t)hi << 32) | lo;
+      if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
+      fp_word(s, w);
+      rem = rem > 8 ? rem - 8 : 0;
+    }
+  }
+  constexpr int DONE_DW = 2 * ((PRE_DW - 1) / 2);  // dword holding the next word's first byte
+  if (rem) hash_tail32(reinterpret_cast<const uint32_t*>(blob + (o0 & ~3u)) + DONE_DW, sh, rem, s);
+  return s;
+}
+
 // Window, sort key, table place and bucket of one valid descriptor from its prefix state.
 // The key is the Redis key string (prefix, window start): its region and generation come
 // from the string's home unit, not the descriptor's (rl_common.h place_of).
@@ -266,23 +291,7 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
       err |= ERR_BAD_TIME;
       continue;
     }
-    const uint32_t dw[PRE_DW + 1] = {w0[r].x, w0[r].y, w0[r].z, w0[r].w, w1[r].x, w1[r].y, w1[r].z, w1[r].w, 0u};
-    const uint32_t sh = o0[r] & 3u;
-    FpState s = fp_init(len[r], seed);
-    uint32_t rem = len[r];
-#pragma unroll
-    for (int k = 0; k < (PRE_DW - 1) / 2; ++k) {
-      if (rem > 0) {
-        const uint32_t lo = __builtin_amdgcn_alignbyte(dw[2 * k + 1], dw[2 * k], sh);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(dw[2 * k + 2], dw[2 * k + 1], sh);
-        uint64_t w = ((uint64_t)hi << 32) | lo;
-        if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
-        fp_word(s, w);
-        rem = rem > 8 ? rem - 8 : 0;
-      }
-    }
-    constexpr int DONE_DW = 2 * ((PRE_DW - 1) / 2);  // dword holding the next word's first byte
-    if (rem) hash_tail32(reinterpret_cast<const uint32_t*>(in.blob + (o0[r] & ~3u)) + DONE_DW, sh, rem, s);
+    const FpState s = prefix_state_pre(w0[r], w1[r], in.blob, o0[r], len[r], seed);
     key_of(x, s, now[r], rr[r], sh_hot, err);
   }
 }
