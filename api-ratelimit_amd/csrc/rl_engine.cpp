@@ -60,10 +60,10 @@ void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const un
                     const TableDesc& tab, HotCand* cand, uint32_t* heads_out, uint32_t* ins_out, void* scratch,
                     const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl);
 void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart,
-                     void* scratch, const DevRule* rules, const unsigned long long* hoff, HotBucket* hb,
+                     void* scratch, const DevRule* rules, uint32_t n_rules, const unsigned long long* hoff, HotBucket* hb,
                      int local_cache, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
                      uint32_t* poison, EngineCtl* ctl);
-void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, const TableDesc& tab,
+void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, const TableDesc& tab,
                      rl_status* out, uint32_t* req_thr, const HotBucket* hb, const Deferred* dfr, HotCand* cand,
                      int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads, uint32_t* wg_ins,
                      const uint32_t* scan_heads, const uint32_t* scan_ins, int routed, RegionOcc* occ, EngineCtl* ctl,
@@ -398,11 +398,11 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
                      d_occ, c4);
     });
     timed(KT_V4_PLACE, [&] {
-      launch_v4_place(stream, b, srt, v4_tcount[sl], v4_scratch, d_rules, v4_hoff, v4_hb, lc, out,
+      launch_v4_place(stream, b, srt, v4_tcount[sl], v4_scratch, d_rules, n_rules, v4_hoff, v4_hb, lc, out,
                       thr, v4_dfr, routed, d_poison, c4);
     });
     timed(KT_V4_GROUP, [&] {
-      launch_v4_group(stream, b, d_rules, tab, out, thr, v4_hb, v4_dfr, d_cand, want_cand ? 1 : 0,
+      launch_v4_group(stream, b, d_rules, n_rules, tab, out, thr, v4_hb, v4_dfr, d_cand, want_cand ? 1 : 0,
                       cfg.hash_seed, v4_scratch, v4_heads, v4_ins, v4_heads + ng, v4_ins + (size_t)ng * 4, routed,
                       d_occ, c4, c4n, h_ctl, want_cand ? h_cand : nullptr, srt, v4_tcount[sl]);
     });

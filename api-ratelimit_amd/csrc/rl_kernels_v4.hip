@@ -1135,10 +1135,14 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
 // k4_place — per tile (tile-sorted records): hot descriptors decided in place. MSD records
 // stay where k4_hist wrote them; k4_group gathers its ranges from the tile runs.
 // ---------------------------------------------------------------------------
+// LR: the rule table (n_rules <= LDS_RULES) is staged in LDS (every hot descriptor's decision
+// reads its rule).
+constexpr uint32_t LDS_RULES = 32;
+template <bool LR>
 __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restrict__ srec,
                                                const uint16_t* __restrict__ tstart,
                                                const uint32_t* __restrict__ ranges,
-                                               const DevRule* __restrict__ rules,
+                                               const DevRule* __restrict__ rules_g, uint32_t n_rules,
                                                const unsigned long long* __restrict__ hoff,
                                                HotBucket* __restrict__ hb, int local_cache,
                                                rl_status* __restrict__ out,
@@ -1147,9 +1151,12 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
   __shared__ __attribute__((aligned(16))) uint16_t s_row[HOT_BUCKETS + 8];
   __shared__ uint32_t s_rstar[HOT_BUCKETS];
   __shared__ uint32_t s_err;
+  __shared__ DevRule s_rules[LR ? LDS_RULES : 1];
+  const DevRule* __restrict__ rules = LR ? s_rules : rules_g;
   const uint32_t tid = threadIdx.x;
   const uint32_t t = blockIdx.x, t0 = t * T;
   if (tid == 0) s_err = ctl->err;
+  if (LR && tid >= 64 && tid < 64 + n_rules) s_rules[tid - 64] = rules_g[tid - 64];
   {  // the hot part of the tile's row of bucket starts (MSD records stay where k4_hist put
      // them: k4_group gathers its ranges from the tile-sorted records)
     const uint32_t* rsrc = reinterpret_cast<const uint32_t*>(tstart + (size_t)t * ROW);
@@ -1315,8 +1322,11 @@ RL_DEV uint32_t gather_runs(const MRec* __restrict__ srec, const uint16_t* __res
   return done;
 }
 
+// LR: the rule table (n_rules <= LDS_RULES) is staged in LDS; the leaders and the decisions
+// read a rule per key / per record.
+template <bool LR>
 __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
-                                                 const DevRule* __restrict__ rules, TableDesc tab,
+                                                 const DevRule* __restrict__ rules_g, TableDesc tab,
                                                  rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
                                                  const HotBucket* __restrict__ hb, const Deferred* __restrict__ dfr,
                                                  HotCand* __restrict__ cand, int cand_on, uint64_t seed,
@@ -1328,7 +1338,9 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
                                                  RegionOcc* __restrict__ occ, EngineCtl* ctl, EngineCtl* next_ctl,
                                                  EngineCtl* hctl, HotCand* hcand,
                                                  const MRec* __restrict__ srec, const uint16_t* __restrict__ tstart,
-                                                 uint32_t ntiles) {
+                                                 uint32_t ntiles, uint32_t n_rules) {
+  __shared__ DevRule s_rules[LR ? LDS_RULES : 1];
+  const DevRule* __restrict__ rules = LR ? s_rules : rules_g;
   __shared__ MRec s_rec[G_CAP];
   __shared__ uint64_t s_P[G_CAP];
   static_assert(sizeof(uint64_t) * G_CAP >= 4 * GATHER_T, "the gather's run tables alias s_P");
@@ -1366,6 +1378,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
     s_err = ld_relaxed(&ctl->err);
   }
   if (tid >= 8 && tid < 16) s_gen[tid - 8] = ctl->gen_max[tid - 8];
+  if (LR && tid >= 32 && tid < 32 + n_rules) s_rules[tid - 32] = rules_g[tid - 32];
   __syncthreads();
   ST4(0);
 #ifdef RL_STAMPS
@@ -1720,14 +1733,19 @@ void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const un
                      fpart, hot_list, hb, tab, cand, heads_out, ins_out, v4_ranges(scratch), poison, occ, ctl);
 }
 void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart,
-                     void* scratch, const DevRule* rules, const unsigned long long* hoff, HotBucket* hb,
-                     int local_cache, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
+                     void* scratch, const DevRule* rules, uint32_t n_rules, const unsigned long long* hoff,
+                     HotBucket* hb, int local_cache, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
                      uint32_t* poison, EngineCtl* ctl) {
-  hipLaunchKernelGGL(v4::k4_place, dim3(v4_tiles(b.n_desc)), dim3(V4_THREADS), 0, st, make_dev_batch(b), srec, tstart,
-                     v4_ranges(scratch), rules, hoff, hb, local_cache, out, req_thr, dfr, routed, poison,
-                     ctl);
+  if (n_rules <= v4::LDS_RULES)
+    hipLaunchKernelGGL(v4::k4_place<true>, dim3(v4_tiles(b.n_desc)), dim3(V4_THREADS), 0, st, make_dev_batch(b), srec,
+                       tstart, v4_ranges(scratch), rules, n_rules, hoff, hb, local_cache, out, req_thr, dfr, routed,
+                       poison, ctl);
+  else
+    hipLaunchKernelGGL(v4::k4_place<false>, dim3(v4_tiles(b.n_desc)), dim3(V4_THREADS), 0, st, make_dev_batch(b), srec,
+                       tstart, v4_ranges(scratch), rules, n_rules, hoff, hb, local_cache, out, req_thr, dfr, routed,
+                       poison, ctl);
 }
-void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, const TableDesc& tab,
+void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, const TableDesc& tab,
                      rl_status* out, uint32_t* req_thr, const HotBucket* hb, const Deferred* dfr, HotCand* cand,
                      int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads, uint32_t* wg_ins,
                      const uint32_t* scan_heads, const uint32_t* scan_ins, int routed, RegionOcc* occ, EngineCtl* ctl,
@@ -1751,9 +1769,16 @@ void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, co
   gs.grp = reinterpret_cast<uint16_t*>(p);
   p += (size_t)GBLOCKS * BUCKET_CAP * 2;
   gs.end = reinterpret_cast<uint16_t*>(p);
-  hipLaunchKernelGGL(k4_group, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), rules, tab, out, req_thr, hb,
-                     dfr, cand, cand_on, seed, gs, wg_heads, wg_ins, scan_heads, scan_ins, (uint32_t)HOT_SCAN_BLOCKS,
-                     v4_ranges(scratch), routed, occ, ctl, next_ctl, hctl, hcand, srec, tstart, v4_tiles(b.n_desc));
+  if (n_rules <= LDS_RULES)
+    hipLaunchKernelGGL(k4_group<true>, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), rules, tab, out, req_thr,
+                       hb, dfr, cand, cand_on, seed, gs, wg_heads, wg_ins, scan_heads, scan_ins,
+                       (uint32_t)HOT_SCAN_BLOCKS, v4_ranges(scratch), routed, occ, ctl, next_ctl, hctl, hcand, srec,
+                       tstart, v4_tiles(b.n_desc), n_rules);
+  else
+    hipLaunchKernelGGL(k4_group<false>, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), rules, tab, out, req_thr,
+                       hb, dfr, cand, cand_on, seed, gs, wg_heads, wg_ins, scan_heads, scan_ins,
+                       (uint32_t)HOT_SCAN_BLOCKS, v4_ranges(scratch), routed, occ, ctl, next_ctl, hctl, hcand, srec,
+                       tstart, v4_tiles(b.n_desc), n_rules);
 }
 
 }  // namespace rlhip
