@@ -78,6 +78,58 @@ RL_DEV void hash_prefix(const uint8_t* blob, uint32_t off, uint32_t len, FpState
   }
 }
 
+// Prefix hashing from a preload of the prefix's first 32 bytes (two 16-B loads from the dword
+// at off & ~3, issued with the descriptor's other loads): prefixes up to 24 B hash inline.
+constexpr int PREFIX_PRE_DW = 8;
+static_assert(PREFIX_PRE_DW % 4 == 0, "the preload is whole 16-B loads");
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// Words of a prefix beyond the preloaded dwords, 32 bytes (three words) per pair of 16-B
+// loads. p = dword holding the next word's first byte; the blob is readable 32 B past its end.
+RL_DEV void hash_tail32(const uint32_t* p, uint32_t sh, uint32_t rem, FpState& s) {
+  while (rem > 0) {
+    const u32x4 x0 = *reinterpret_cast<const u32x4*>(p), x1 = *reinterpret_cast<const u32x4*>(p + 4);
+    const uint32_t dw[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (rem > 0) {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(dw[2 * k + 1], dw[2 * k], sh);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(dw[2 * k + 2], dw[2 * k + 1], sh);
+        uint64_t w = ((uint64_t)hi << 32) | lo;
+        if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
+        fp_word(s, w);
+        rem = rem > 8 ? rem - 8 : 0;
+      }
+    }
+    p += 6;
+  }
+}
+
+// Prefix state of blob[o0, o0 + len) whose first 32 bytes from the dword at o0 & ~3 are
+// already loaded (w0, w1); longer prefixes read the rest 32 bytes a step (the blob is
+// readable 32 bytes past its end).
+RL_DEV FpState prefix_state_pre(const u32x4 w0, const u32x4 w1, const uint8_t* blob, uint32_t o0, uint32_t len,
+                                uint64_t seed) {
+  const uint32_t dw[PREFIX_PRE_DW + 1] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, 0u};
+  const uint32_t sh = o0 & 3u;
+  FpState s = fp_init(len, seed);
+  uint32_t rem = len;
+#pragma unroll
+  for (int k = 0; k < (PREFIX_PRE_DW - 1) / 2; ++k) {
+    if (rem > 0) {
+      const uint32_t lo = __builtin_amdgcn_alignbyte(dw[2 * k + 1], dw[2 * k], sh);
+      const uint32_t hi = __builtin_amdgcn_alignbyte(dw[2 * k + 2], dw[2 * k + 1], sh);
+      uint64_t w = ((uint64_t)hi << 32) | lo;
+      if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
+      fp_word(s, w);
+      rem = rem > 8 ? rem - 8 : 0;
+    }
+  }
+  constexpr int DONE_DW = 2 * ((PREFIX_PRE_DW - 1) / 2);  // dword holding the next word's first byte
+  if (rem) hash_tail32(reinterpret_cast<const uint32_t*>(blob + (o0 & ~3u)) + DONE_DW, sh, rem, s);
+  return s;
+}
+
 RL_DEV int64_t div_const(int64_t now, uint32_t unit) {
   switch (unit) {
     case RL_UNIT_SECOND: return now;

@@ -1640,16 +1640,16 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   }
   STL(1);
   if (any_cand && !in.recs) {
-    tile::u32x4 b0[CPT], b1[CPT];
+    u32x4 b0[CPT], b1[CPT];
 #pragma unroll
     for (int e = 0; e < CPT; ++e) {
-      const tile::u32x4* q = reinterpret_cast<const tile::u32x4*>(in.blob + (po[e] & ~3u));
+      const u32x4* q = reinterpret_cast<const u32x4*>(in.blob + (po[e] & ~3u));
       b0[e] = q[0];
       b1[e] = q[1];
     }
 #pragma unroll
     for (int e = 0; e < CPT; ++e) {
-      const FpState st = tile::prefix_state_pre(b0[e], b1[e], in.blob, po[e], pl[e], seed);
+      const FpState st = prefix_state_pre(b0[e], b1[e], in.blob, po[e], pl[e], seed);
       ra[e] = st.a;
       rbv[e] = st.b;
     }

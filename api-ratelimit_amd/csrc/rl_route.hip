@@ -33,33 +33,37 @@ __global__ __launch_bounds__(NT) void k_route_hash(DevBatch in, const DevRule* _
   if (tid < NS) s_cnt[tid] = 0;
   __syncthreads();
   if (i < in.n_desc) {
-    const uint32_t rule = in.rule[i], q = in.req_of[i];
-    uint32_t err = 0, o = ROUTE_LOCAL;
+    // two levels of loads, each issued together (clamped indices; the blob is readable
+    // RL_BLOB_SLACK bytes past its end): (rule, request, prefix offsets), then (now, hits, the
+    // prefix's first 32 bytes)
+    const uint32_t rule = in.rule[i], q = in.req_of[i], qp = in.req_of[i ? i - 1u : 0u];
     const uint32_t o0 = in.off[i], o1 = in.off[i + 1];
-    if (o1 < o0 || o1 > in.blob_bytes || (i > 0 && in.req_of[i - 1] > q)) err |= ERR_BAD_INPUT;
-    if (rule != RL_NIL_RULE && !err) {
-      if (rule >= n_rules || q >= in.n_req) {
-        err |= ERR_BAD_INPUT;
+    uint32_t err = 0, o = ROUTE_LOCAL;
+    if (o1 < o0 || o1 > in.blob_bytes || qp > q) err |= ERR_BAD_INPUT;
+    const bool nil = rule == RL_NIL_RULE;
+    if (!nil && !err && (rule >= n_rules || q >= in.n_req)) err |= ERR_BAD_INPUT;
+    const uint32_t qc = q < in.n_req ? q : 0u;
+    const uint32_t oc = err ? 0u : o0;
+    const int64_t now = in.now[qc];
+    const uint32_t ha = in.hits[qc];
+    const u32x4* pw = reinterpret_cast<const u32x4*>(in.blob + (oc & ~3u));
+    const u32x4 w0 = pw[0];
+    const u32x4 w1 = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint32_t*>(pw) + 4);
+    if (!nil && !err) {
+      if (now < 0 || now > MAX_NOW) {
+        err |= ERR_BAD_TIME;
       } else {
-        const int64_t now = in.now[q];
-        if (now < 0 || now > MAX_NOW) {
-          err |= ERR_BAD_TIME;
-        } else {
-          const uint32_t len = o1 - o0;
-          FpState s = fp_init(len, seed);
-          if (len) hash_prefix(in.blob, o0, len, s);
-          const uint32_t ha = in.hits[q];
-          RRec r;
-          r.a = s.a;
-          r.b = s.b;
-          r.now = (uint32_t)now;
-          r.rule = rule;
-          r.h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
-          r.greq = (origin << ROUTE_REQ_BITS) | q;
-          tmp[i] = r;
-          o = route_owner(s.a, s.b, n_shards);
-          atomicAdd(&s_cnt[o], 1u);
-        }
+        const FpState s = prefix_state_pre(w0, w1, in.blob, o0, o1 - o0, seed);
+        RRec r;
+        r.a = s.a;
+        r.b = s.b;
+        r.now = (uint32_t)now;
+        r.rule = rule;
+        r.h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
+        r.greq = (origin << ROUTE_REQ_BITS) | q;
+        tmp[i] = r;
+        o = route_owner(s.a, s.b, n_shards);
+        atomicAdd(&s_cnt[o], 1u);
       }
     }
     own[i] = (uint8_t)o;

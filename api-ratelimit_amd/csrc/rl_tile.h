@@ -25,13 +25,11 @@ constexpr int T = V4_TILE;
 constexpr int NT = V4_THREADS;
 constexpr int R = T / NT;      // descriptors per thread
 constexpr int W = NT / 64;     // waves per tile block
-constexpr int PRE_DW = 8;      // blob dwords preloaded per descriptor (prefixes up to 24 B hash inline)
-static_assert(PRE_DW % 4 == 0, "the preload is whole 16-B loads");
+constexpr int PRE_DW = PREFIX_PRE_DW;  // blob dwords preloaded per descriptor (rl_device.h)
 constexpr uint32_t BKT_NONE = 4095;  // past the end of the batch (sorts last in 12 bits)
 static_assert(NBUCKETS <= 4095, "bucket ids are 12-bit");
 static_assert(T <= 65536, "u16 tile offsets");
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4), aligned(4)));
 
 RL_DEV uint32_t msd_bucket(uint64_t key) { return (uint32_t)((key << 3) >> (64 - MSD_BITS)); }
 RL_DEV uint32_t rule_of(uint32_t rn) { return rn & (V4_MAX_RULES - 1u); }
@@ -130,27 +128,6 @@ RL_DEV void hash_tail(const uint32_t* p, uint32_t d0, uint32_t sh, uint32_t rem,
   }
 }
 
-// Words of a prefix beyond the preloaded dwords, 32 bytes (three words) per pair of 16-B
-// loads. p = dword holding the next word's first byte; the blob is readable 32 B past its end.
-RL_DEV void hash_tail32(const uint32_t* p, uint32_t sh, uint32_t rem, FpState& s) {
-  while (rem > 0) {
-    const u32x4 x0 = *reinterpret_cast<const u32x4*>(p), x1 = *reinterpret_cast<const u32x4*>(p + 4);
-    const uint32_t dw[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      if (rem > 0) {
-        const uint32_t lo = __builtin_amdgcn_alignbyte(dw[2 * k + 1], dw[2 * k], sh);
-        const uint32_t hi = __builtin_amdgcn_alignbyte(dw[2 * k + 2], dw[2 * k + 1], sh);
-        uint64_t w = ((uint64_t)hi << 32) | lo;
-        if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
-        fp_word(s, w);
-        rem = rem > 8 ? rem - 8 : 0;
-      }
-    }
-    p += 6;
-  }
-}
-
 // Prefix state (lanes a, b) of a byte string, reading only dwords that overlap it.
 RL_DEV FpState prefix_state(const uint8_t* blob, uint32_t off, uint32_t len, uint64_t seed) {
   FpState s = fp_init(len, seed);
@@ -158,31 +135,6 @@ RL_DEV FpState prefix_state(const uint8_t* blob, uint32_t off, uint32_t len, uin
     const uint32_t* p = reinterpret_cast<const uint32_t*>(blob + (off & ~3u));
     hash_tail(p, p[0], off & 3u, len, s);
   }
-  return s;
-}
-
-// Prefix state of blob[o0, o0 + len) whose first 32 bytes from the dword at o0 & ~3 are
-// already loaded (w0, w1); longer prefixes read the rest 32 bytes a step (the blob is
-// readable 32 bytes past its end).
-RL_DEV FpState prefix_state_pre(const u32x4 w0, const u32x4 w1, const uint8_t* blob, uint32_t o0, uint32_t len,
-                                uint64_t seed) {
-  const uint32_t dw[PRE_DW + 1] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, 0u};
-  const uint32_t sh = o0 & 3u;
-  FpState s = fp_init(len, seed);
-  uint32_t rem = len;
-#pragma unroll
-  for (int k = 0; k < (PRE_DW - 1) / 2; ++k) {
-    if (rem > 0) {
-      const uint32_t lo = __builtin_amdgcn_alignbyte(dw[2 * k + 1], dw[2 * k], sh);
-      const uint32_t hi = __builtin_amdgcn_alignbyte(dw[2 * k + 2], dw[2 * k + 1], sh);
-      uint64_t w = ((uint64_t)hi << 32) | lo;
-      if (rem < 8) w &= (~0ull) >> (64 - 8 * rem);
-      fp_word(s, w);
-      rem = rem > 8 ? rem - 8 : 0;
-    }
-  }
-  constexpr int DONE_DW = 2 * ((PRE_DW - 1) / 2);  // dword holding the next word's first byte
-  if (rem) hash_tail32(reinterpret_cast<const uint32_t*>(blob + (o0 & ~3u)) + DONE_DW, sh, rem, s);
   return s;
 }
 

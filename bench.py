@@ -228,7 +228,8 @@ def logical_shards_main(args):
     engines = []
     for _ in range(G):
         e = hiprl.Engine(device=0, log2_slots=(lg, lg, lg, 12), max_batch_desc=G * d, max_batch_req=G * d,
-                         max_blob_bytes=G * d * 17 + 64, sort_bits=48, pipeline=args.pipeline)
+                         max_blob_bytes=G * d * 17 + 64, sort_bits=48, pipeline=args.pipeline,
+                         lib_path=(ROOT / args.lib) if args.lib else None)
         e.load_rules(rules)
         engines.append(e)
     r = hiprl.Router(engines, max_desc=d)
