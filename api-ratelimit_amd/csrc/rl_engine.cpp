@@ -1168,12 +1168,11 @@ int rl_route_pack(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_s
     chk(hipHostMalloc(&e->h_route, 64 * 4, hipHostMallocDefault));
     if (he != hipSuccess) return e->hip_fail(he, "router scratch allocation");
   }
-  chk(hipMemsetAsync(e->r_ctl, 0, sizeof(EngineCtl), e->stream));
+  // k_route_scan writes the error word and the owner totals into r_ctl's first words: one copy
   launch_route_pack(e->stream, *b, e->d_rules, e->n_rules, e->cfg.hash_seed, origin, n_shards, e->r_tmp, e->r_own,
                     e->r_bcnt, reinterpret_cast<RRec*>(d_send), d_send_counts, d_perm, e->r_ctl);
   chk(hipGetLastError());
-  chk(hipMemcpyAsync(e->h_route, e->r_ctl, 4, hipMemcpyDeviceToHost, e->stream));
-  chk(hipMemcpyAsync(e->h_route + 1, d_send_counts, n_shards * 4, hipMemcpyDeviceToHost, e->stream));
+  chk(hipMemcpyAsync(e->h_route, e->r_ctl, (1 + n_shards) * 4, hipMemcpyDeviceToHost, e->stream));
   chk(hipStreamSynchronize(e->stream));
   if (he != hipSuccess) return e->hip_fail(he, "rl_route_pack");
   const uint32_t errs = e->h_route[0];

@@ -29,8 +29,10 @@ __global__ __launch_bounds__(NT) void k_route_hash(DevBatch in, const DevRule* _
                                                     RRec* __restrict__ tmp, uint8_t* __restrict__ own,
                                                     uint32_t* __restrict__ bcnt, EngineCtl* ctl) {
   __shared__ uint32_t s_cnt[NS];
+  __shared__ uint32_t s_err;
   const uint32_t tid = threadIdx.x, i = blockIdx.x * NT + tid;
   if (tid < NS) s_cnt[tid] = 0;
+  if (tid == 0) s_err = 0;
   __syncthreads();
   if (i < in.n_desc) {
     // two levels of loads, each issued together (clamped indices; the blob is readable
@@ -67,47 +69,83 @@ __global__ __launch_bounds__(NT) void k_route_hash(DevBatch in, const DevRule* _
       }
     }
     own[i] = (uint8_t)o;
-    if (err) atomicOr(&ctl->err, err);
+    if (err) atomicOr(&s_err, err);
   }
   __syncthreads();
   if (tid < NS) bcnt[blockIdx.x * NS + tid] = s_cnt[tid];
+  // the block's error flags after every block's counts (k_route_scan folds them: no atomic,
+  // no memset of the error word before the launch)
+  if (tid == 0) bcnt[gridDim.x * NS + blockIdx.x] = s_err;
 }
 
-// One block: wave w < n_shards scans column w over the blocks (exclusive, in place), then
-// owner totals are scanned into owner offsets and added to every entry.
+// One block: wave w < n_shards scans column w over the blocks (exclusive, in place), in
+// chunks of 64 x RPL blocks: lane l holds RPL consecutive blocks' counts in registers (all
+// loads in flight together, clamped), one DPP scan of the lanes' sums, then the lane writes
+// its run's prefixes. Owner totals are scanned into owner offsets in between (a second
+// read of the column is cheap: it is in the L2). The blocks' error flags are folded into
+// ctl->err; ctl words 1..n_shards get the owner totals too, so the host reads both in one copy.
+constexpr int RPL = 32;
 __global__ __launch_bounds__(SCAN_NT) void k_route_scan(uint32_t* __restrict__ bcnt, uint32_t nb, uint32_t n_shards,
-                                                        uint32_t* __restrict__ send_counts) {
-  __shared__ uint32_t s_tot[NS], s_off[NS];
+                                                        uint32_t* __restrict__ send_counts, EngineCtl* ctl) {
+  __shared__ uint32_t s_tot[NS], s_off[NS], s_err;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (w < n_shards) {
-    uint32_t carry = 0;
-    for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
-      const uint32_t b = b0 + lane;
-      const uint32_t v = b < nb ? bcnt[b * NS + w] : 0u;
-      uint32_t x = v;
+  static_assert(SCAN_NT / 64 >= NS, "one wave per shard column");
+  if (tid == 0) s_err = 0;
+  __syncthreads();
+  constexpr uint32_t CH = 64u * RPL;  // blocks per chunk
+  // pass 1: column totals
+  if (w < n_shards) {  // wave-uniform
+    uint32_t tot = 0;
+    for (uint32_t c0 = 0; c0 < nb; c0 += CH) {
+      uint32_t v[RPL];
 #pragma unroll
-      for (int s = 1; s < 64; s <<= 1) {
-        const uint32_t y = __shfl_up(x, s, 64);
-        if (lane >= (uint32_t)s) x += y;
-      }
-      if (b < nb) bcnt[b * NS + w] = carry + x - v;
-      carry += __shfl(x, 63, 64);
+      for (int u = 0; u < RPL; ++u) v[u] = bcnt[(size_t)min(c0 + lane * RPL + u, nb - 1u) * NS + w];
+      uint32_t sum = 0;
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) sum += c0 + lane * RPL + u < nb ? v[u] : 0u;
+      tot += wave_sum_u32(sum);
     }
-    if (lane == 0) s_tot[w] = carry;
+    if (lane == 0) s_tot[w] = tot;
   }
+  uint32_t err = 0;
+  for (uint32_t b = tid; b < nb; b += SCAN_NT) err |= bcnt[(size_t)nb * NS + b];
+  if (err) atomicOr(&s_err, err);
   __syncthreads();
   if (tid == 0) {
     uint32_t acc = 0;
-    for (uint32_t s = 0; s < n_shards; ++s) {
-      s_off[s] = acc;
-      send_counts[s] = s_tot[s];
-      acc += s_tot[s];
+    uint32_t* cw = reinterpret_cast<uint32_t*>(ctl);
+    for (uint32_t s2 = 0; s2 < n_shards; ++s2) {
+      s_off[s2] = acc;
+      send_counts[s2] = s_tot[s2];
+      cw[1 + s2] = s_tot[s2];
+      acc += s_tot[s2];
     }
+    cw[0] = s_err;
   }
   __syncthreads();
-  for (uint32_t k = tid; k < nb * NS; k += SCAN_NT) {
-    const uint32_t s = k % NS;
-    if (s < n_shards) bcnt[k] += s_off[s];
+  // pass 2: exclusive prefixes + the owner's offset
+  if (w < n_shards) {
+    uint32_t carry = s_off[w];
+    for (uint32_t c0 = 0; c0 < nb; c0 += CH) {
+      uint32_t v[RPL];
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) v[u] = bcnt[(size_t)min(c0 + lane * RPL + u, nb - 1u) * NS + w];
+      uint32_t sum = 0;
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) {
+        v[u] = c0 + lane * RPL + u < nb ? v[u] : 0u;
+        sum += v[u];
+      }
+      const uint32_t incl = wave_incl_scan_u32(sum);
+      uint32_t run = carry + incl - sum;
+#pragma unroll
+      for (int u = 0; u < RPL; ++u) {
+        const uint32_t b = c0 + lane * RPL + u;
+        if (b < nb) bcnt[(size_t)b * NS + w] = run;
+        run += v[u];
+      }
+      carry += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
   }
 }
 
@@ -184,7 +222,7 @@ __global__ __launch_bounds__(NT) void k_route_unpack(uint32_t n, const uint32_t*
 }  // namespace route
 
 static uint32_t route_blocks(uint32_t n) { return n ? (n + route::NT - 1) / route::NT : 1; }
-uint32_t route_bcnt_words(uint32_t n) { return route_blocks(n) * route::NS; }
+uint32_t route_bcnt_words(uint32_t n) { return route_blocks(n) * (route::NS + 1); }  // counts, then errors
 
 void launch_route_pack(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
                        uint32_t origin, uint32_t n_shards, RRec* tmp, uint8_t* own, uint32_t* bcnt, RRec* send,
@@ -192,7 +230,7 @@ void launch_route_pack(hipStream_t st, const rl_batch& b, const DevRule* rules, 
   const uint32_t nb = route_blocks(b.n_desc);
   hipLaunchKernelGGL(route::k_route_hash, dim3(nb), dim3(route::NT), 0, st, make_dev_batch(b), rules, n_rules, seed,
                      origin, n_shards, tmp, own, bcnt, ctl);
-  hipLaunchKernelGGL(route::k_route_scan, dim3(1), dim3(route::SCAN_NT), 0, st, bcnt, nb, n_shards, send_counts);
+  hipLaunchKernelGGL(route::k_route_scan, dim3(1), dim3(route::SCAN_NT), 0, st, bcnt, nb, n_shards, send_counts, ctl);
   hipLaunchKernelGGL(route::k_route_scatter, dim3(nb), dim3(route::NT), 0, st, b.n_desc, tmp, own, bcnt, send,
                      perm);
 }
