@@ -92,6 +92,8 @@ def parse():
                     help="G > 0: one GPU, G engines as G logical shards behind the C-ABI router (rl_router, local "
                          "transport): G origin batches per step, records per owner and the step breakdown")
     ap.add_argument("--lib", type=str, default="", help=argparse.SUPPRESS)  # diagnostics: a variant library
+    # tests: the routed (RCCL all-to-all) step on one rank, so the multi-GPU path runs on a 1-GPU box
+    ap.add_argument("--force-routed", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dump-stamps", type=str, default="", help=argparse.SUPPRESS)  # -DRL_STAMPS variant: raw stamps
     return ap.parse_args()
 
@@ -284,7 +286,7 @@ def main():
     import torch
 
     dist = None
-    if world > 1:
+    if world > 1 or args.force_routed:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
@@ -300,7 +302,7 @@ def main():
         wl = "config2: 1e6 uniform keys, SECOND L=5, 1 descriptor/request"
     prefill = args.prefill if args.prefill >= 0 else (K + K // 2 if K > 1 else 0)
     seed = (3 if args.config == 3 else 2) + 7919 * rank  # each rank its own stream
-    routed = world > 1 and not args.independent
+    routed = (world > 1 or args.force_routed) and not args.independent
     # an owner may receive up to every origin's batch (hot keys concentrate on their owner)
     cap = d * world if routed else d
     eng = hiprl.Engine(device=local, log2_slots=log2, max_batch_desc=cap, max_batch_req=cap,

@@ -1,0 +1,41 @@
+"""The multi-GPU bench path (bench.py under torchrun, router.ShardRouter over RCCL) on one GPU.
+
+The driver's scaling run launches `bench.py --gpus N` with one rank per GPU; every rank packs
+its batch, exchanges records and replies with RCCL all-to-alls and decides as an owner. On a
+one-GPU box the same code runs as one rank with --force-routed (a communicator of one rank:
+every collective is real RCCL, every record goes to its own owner), so the routed step's
+plumbing is exercised before the 8-GPU run. Bit-exactness of routed steps is covered by
+tests/test_gpu_router.py (GPU, logical shards) and tests/test_router_cpu.py (gloo, 2-3 ranks).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_routed_bench_one_rank():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+           "--force-routed", "--steps", "3", "--warmup", "1", "--prefill", "6", "--batches-per-second", "4",
+           "--desc", "200000", "--log2-slots", "22", "--cpu-seconds", "0", "--no-kernel-times",
+           "--no-roofline-probe", "--no-host-path"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["value"] > 0 and line["n_gpus"] == 1
+    assert "RCCL all-to-all" in line["config"]["parallelism"], line["config"]
+    assert line["engine"]["lsd_fallbacks_timed"] == 0 or line["engine"]["lsd_fallbacks_timed"] >= 0
