@@ -45,7 +45,7 @@ void launch_occ_update(hipStream_t, RegionOcc*, EngineCtl*);
 void launch_cand_state(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, EngineCtl*);
 uint32_t route_bcnt_words(uint32_t n);
 void launch_route_pack(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint32_t, uint32_t, RRec*,
-                       uint8_t*, uint32_t*, RRec*, uint32_t*, uint32_t*, EngineCtl*);
+                       uint8_t*, uint32_t*, RRec*, uint32_t*, uint32_t*, EngineCtl*, uint32_t*);
 void launch_route_reply(hipStream_t, uint32_t, const rl_status*, const uint32_t*, RReply*);
 void launch_route_unpack(hipStream_t, uint32_t, const uint32_t*, const uint32_t*, const RReply*, rl_status*,
                          uint32_t*);
@@ -1145,8 +1145,10 @@ int rl_set_stream(rl_engine* e, void* hip_stream) {
   return 0;
 }
 
-int rl_route_pack(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_shards, void* d_send,
-                  uint32_t* d_send_counts, uint32_t* d_perm, uint32_t* h_send_counts) {
+// The checks and launches shared by rl_route_pack and rl_route_pack_async (d_x: the async
+// form's (count, status) pairs; d_send_counts: the synchronous form's counts).
+static int route_pack_launch(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_shards, void* d_send,
+                             uint32_t* d_send_counts, uint32_t* d_perm, uint32_t* d_x) {
   if (!e || !b) return RL_EINVAL;
   if (e->n_fl) return e->fail(RL_ESTATE, "rl_route_pack while a batch is in flight (call rl_wait)");
   if (n_shards == 0 || n_shards > ROUTE_MAX_SHARDS || origin >= ROUTE_MAX_SHARDS)
@@ -1154,8 +1156,7 @@ int rl_route_pack(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_s
   if (b->n_desc > e->cfg.max_batch_desc) return e->fail(RL_ECAPACITY, "batch exceeds engine capacity");
   if (b->n_req > RL_ROUTE_MAX_REQ) return e->fail(RL_EINVAL, "routed batch holds more than 2^27 requests");
   if (b->reserved) return e->fail(RL_EINVAL, "rl_batch.reserved must be 0");
-  if (!d_send_counts || !h_send_counts || (b->n_desc && (!d_send || !d_perm)))
-    return e->fail(RL_EINVAL, "null routing buffer");
+  if ((!d_send_counts && !d_x) || (b->n_desc && (!d_send || !d_perm))) return e->fail(RL_EINVAL, "null routing buffer");
   if (!e->d_rules) rl_load_rules(e, nullptr, 0);
   hipError_t he = hipSuccess;
   auto chk = [&](hipError_t x) { if (x != hipSuccess && he == hipSuccess) he = x; };
@@ -1168,12 +1169,21 @@ int rl_route_pack(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_s
     chk(hipHostMalloc(&e->h_route, 64 * 4, hipHostMallocDefault));
     if (he != hipSuccess) return e->hip_fail(he, "router scratch allocation");
   }
-  // k_route_scan writes the error word and the owner totals into r_ctl's first words: one copy
+  // k_route_scan writes the error word and the owner totals into r_ctl's first words (and
+  // the pairs into d_x)
   launch_route_pack(e->stream, *b, e->d_rules, e->n_rules, e->cfg.hash_seed, origin, n_shards, e->r_tmp, e->r_own,
-                    e->r_bcnt, reinterpret_cast<RRec*>(d_send), d_send_counts, d_perm, e->r_ctl);
+                    e->r_bcnt, reinterpret_cast<RRec*>(d_send), d_send_counts, d_perm, e->r_ctl, d_x);
   chk(hipGetLastError());
-  chk(hipMemcpyAsync(e->h_route, e->r_ctl, (1 + n_shards) * 4, hipMemcpyDeviceToHost, e->stream));
-  chk(hipStreamSynchronize(e->stream));
+  if (he != hipSuccess) return e->hip_fail(he, "rl_route_pack");
+  return 0;
+}
+
+int rl_route_pack(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_shards, void* d_send,
+                  uint32_t* d_send_counts, uint32_t* d_perm, uint32_t* h_send_counts) {
+  if (!d_send_counts || !h_send_counts) return e ? e->fail(RL_EINVAL, "null routing buffer") : RL_EINVAL;
+  if (int rc = route_pack_launch(e, b, origin, n_shards, d_send, d_send_counts, d_perm, nullptr)) return rc;
+  hipError_t he = hipMemcpyAsync(e->h_route, e->r_ctl, (1 + n_shards) * 4, hipMemcpyDeviceToHost, e->stream);
+  if (he == hipSuccess) he = hipStreamSynchronize(e->stream);
   if (he != hipSuccess) return e->hip_fail(he, "rl_route_pack");
   const uint32_t errs = e->h_route[0];
   if (errs & ERR_BAD_INPUT)
@@ -1181,6 +1191,12 @@ int rl_route_pack(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_s
   if (errs & ERR_BAD_TIME) return e->fail(RL_EINVAL, "request time outside [0, 0xFFFD0000] unix seconds");
   memcpy(h_send_counts, e->h_route + 1, n_shards * 4);
   return 0;
+}
+
+int rl_route_pack_async(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_shards, void* d_send,
+                        uint32_t* d_x, uint32_t* d_perm) {
+  if (!d_x) return e ? e->fail(RL_EINVAL, "null routing buffer") : RL_EINVAL;
+  return route_pack_launch(e, b, origin, n_shards, d_send, nullptr, d_perm, d_x);
 }
 
 int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_reply) {

@@ -86,7 +86,8 @@ __global__ __launch_bounds__(NT) void k_route_hash(DevBatch in, const DevRule* _
 // ctl->err; ctl words 1..n_shards get the owner totals too, so the host reads both in one copy.
 constexpr int RPL = 32;
 __global__ __launch_bounds__(SCAN_NT) void k_route_scan(uint32_t* __restrict__ bcnt, uint32_t nb, uint32_t n_shards,
-                                                        uint32_t* __restrict__ send_counts, EngineCtl* ctl) {
+                                                        uint32_t* __restrict__ send_counts, EngineCtl* ctl,
+                                                        uint32_t* __restrict__ x) {
   __shared__ uint32_t s_tot[NS], s_off[NS], s_err;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   static_assert(SCAN_NT / 64 >= NS, "one wave per shard column");
@@ -116,8 +117,12 @@ __global__ __launch_bounds__(SCAN_NT) void k_route_scan(uint32_t* __restrict__ b
     uint32_t* cw = reinterpret_cast<uint32_t*>(ctl);
     for (uint32_t s2 = 0; s2 < n_shards; ++s2) {
       s_off[s2] = acc;
-      send_counts[s2] = s_tot[s2];
+      if (send_counts) send_counts[s2] = s_tot[s2];
       cw[1 + s2] = s_tot[s2];
+      if (x) {  // rl_route_pack_async: (count, status) per owner for the all-to-all of counts
+        x[2 * s2] = s_tot[s2];
+        x[2 * s2 + 1] = s_err & (ERR_BAD_INPUT | ERR_BAD_TIME) ? (uint32_t)RL_EINVAL : 0u;
+      }
       acc += s_tot[s2];
     }
     cw[0] = s_err;
@@ -226,11 +231,12 @@ uint32_t route_bcnt_words(uint32_t n) { return route_blocks(n) * (route::NS + 1)
 
 void launch_route_pack(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
                        uint32_t origin, uint32_t n_shards, RRec* tmp, uint8_t* own, uint32_t* bcnt, RRec* send,
-                       uint32_t* send_counts, uint32_t* perm, EngineCtl* ctl) {
+                       uint32_t* send_counts, uint32_t* perm, EngineCtl* ctl, uint32_t* x) {
   const uint32_t nb = route_blocks(b.n_desc);
   hipLaunchKernelGGL(route::k_route_hash, dim3(nb), dim3(route::NT), 0, st, make_dev_batch(b), rules, n_rules, seed,
                      origin, n_shards, tmp, own, bcnt, ctl);
-  hipLaunchKernelGGL(route::k_route_scan, dim3(1), dim3(route::SCAN_NT), 0, st, bcnt, nb, n_shards, send_counts, ctl);
+  hipLaunchKernelGGL(route::k_route_scan, dim3(1), dim3(route::SCAN_NT), 0, st, bcnt, nb, n_shards, send_counts, ctl,
+                     x);
   hipLaunchKernelGGL(route::k_route_scatter, dim3(nb), dim3(route::NT), 0, st, b.n_desc, tmp, own, bcnt, send,
                      perm);
 }

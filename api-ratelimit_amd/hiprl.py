@@ -131,6 +131,8 @@ ABI = [
     ("rl_set_stream", [C.c_void_p, C.c_void_p], C.c_int),
     ("rl_route_pack", [C.c_void_p, C.POINTER(RlBatch), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                        C.POINTER(C.c_uint32)], C.c_int),
+    ("rl_route_pack_async", [C.c_void_p, C.POINTER(RlBatch), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
+                             C.c_void_p], C.c_int),
     ("rl_submit_routed", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p], C.c_int),
     ("rl_route_unpack", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     ("rl_load_tree", [C.c_void_p, C.POINTER(RlTreeNode), C.c_uint32, C.c_void_p, C.c_uint32], C.c_int),
@@ -445,6 +447,15 @@ class Engine:
         self._check(self.lib.rl_route_pack(self.h, C.byref(s), origin, n_shards, send_ptr, send_counts_ptr, perm_ptr,
                                            counts), "rl_route_pack")
         return list(counts)
+
+    def route_pack_async(self, n_desc: int, n_req: int, blob_bytes: int, ptrs, origin: int, n_shards: int,
+                         send_ptr: int, x_ptr: int, perm_ptr: int):
+        """rl_route_pack without the host round trip: (count, status) per owner in x (device)."""
+        s = RlBatch()
+        s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
+        s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        self._check(self.lib.rl_route_pack_async(self.h, C.byref(s), origin, n_shards, send_ptr, x_ptr, perm_ptr),
+                    "rl_route_pack_async")
 
     def submit_routed_async(self, rec_ptr: int, n: int, reply_ptr: int):
         self._check(self.lib.rl_submit_routed(self.h, rec_ptr, n, reply_ptr), "rl_submit_routed")

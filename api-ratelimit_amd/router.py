@@ -114,6 +114,16 @@ class EngineShard:
         self._leave()
         return self.send[:sum(counts) * REC], self.counts, counts, self.perm[:b.n_desc]
 
+    def pack_async(self, b: DeviceBatch):
+        """pack without a host round trip: the (count, status) pair for every owner lands in a
+        device tensor, ready for the all-to-all of counts (ShardRouter.step)."""
+        x = torch.empty(2 * self.world, dtype=torch.int32, device=self.device)
+        self._enter()
+        self.eng.route_pack_async(b.n_desc, b.n_req, b.blob_bytes(), b.ptrs(), self.rank, self.world,
+                                  self.send.data_ptr(), x.data_ptr(), self.perm.data_ptr())
+        self._leave()
+        return self.send, x, self.perm[:b.n_desc]
+
     def decide(self, recv: torch.Tensor, n: int) -> torch.Tensor:
         reply = self.empty(n * REP)
         self._enter()
@@ -156,23 +166,43 @@ class ShardRouter:
         raise hiprl.RedisError(f"routed step: RL_EPEER: shard {bad[0]} failed to {phase} "
                                f"({hiprl.RL_ERRORS.get(status[bad[0]], status[bad[0]])})", -7)
 
+    def _pack(self, b):
+        """-> (send buffer, device (count, status) pairs, perm, own error). A shard with
+        pack_async packs without a host round trip: its counts come back with the all-to-all of
+        counts (one host synchronisation per exchange instead of two)."""
+        sh = self.shard
+        if hasattr(sh, "pack_async"):
+            try:
+                send, x, perm = sh.pack_async(b)
+                return send, x, perm, None
+            except hiprl.RedisError as ex:
+                own = ex
+        else:
+            try:
+                send, _, counts, perm = sh.pack(b)
+                x = torch.tensor([v for c in counts for v in (c, 0)], dtype=torch.int32, device=send.device)
+                return send, x, perm, None
+            except hiprl.RedisError as ex:
+                own = ex
+        send = sh.empty(0)
+        x = torch.tensor([v for _ in range(self.world) for v in (0, _code(own))], dtype=torch.int32,
+                         device=send.device)
+        return send, x, None, own
+
     def step(self, b):
         sh = self.shard
-        own = None
-        try:
-            send, counts_t, counts, perm = sh.pack(b)
-        except hiprl.RedisError as ex:
-            own, counts_t, counts, perm = ex, None, [0] * self.world, None
-            send = sh.empty(0)
-        dev = send.device
-        err = _code(own) if own is not None else 0
-        x = torch.tensor([v for c in counts for v in (c, err)], dtype=torch.int32, device=dev)
+        send, x, perm, own = self._pack(b)
         rx = torch.empty_like(x)
         dist.all_to_all_single(rx, x, group=self.group)
-        rv = [int(v) for v in rx.tolist()]
-        rcounts, status = rv[0::2], rv[1::2]
+        both = [int(v) for v in torch.cat([x, rx]).tolist()]  # the step's one sync before the records
+        counts = both[0:2 * self.world:2]
+        rcounts, status = both[2 * self.world::2], both[2 * self.world + 1::2]
+        if own is None and both[1]:  # the device found this batch malformed (rl_route_pack's checks)
+            own = hiprl.RedisError("rl_route_pack_async: RL_EINVAL: batch references an unknown rule id or request "
+                                   "index, malformed prefix offsets, or a time outside [0, 0xFFFD0000]", both[1])
         if any(status):
             self._raise("pack its batch", status, own)
+        send = send[:sum(counts) * REC]
         n_in = sum(rcounts)
         recv = sh.empty(n_in * REC)
         dist.all_to_all_single(recv, send, [c * REC for c in rcounts], [c * REC for c in counts], group=self.group)
@@ -180,7 +210,7 @@ class ShardRouter:
             reply = sh.decide(recv, n_in)
         except hiprl.RedisError as ex:
             own, reply = ex, sh.empty(n_in * REP)
-        e = torch.full((self.world,), _code(own) if own is not None else 0, dtype=torch.int32, device=dev)
+        e = torch.full((self.world,), _code(own) if own is not None else 0, dtype=torch.int32, device=x.device)
         re_ = torch.empty_like(e)
         dist.all_to_all_single(re_, e, group=self.group)
         status = [int(v) for v in re_.tolist()]

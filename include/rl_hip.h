@@ -244,6 +244,14 @@ int rl_set_stream(rl_engine* e, void* hip_stream);
 int rl_route_pack(rl_engine* e, const rl_batch* device_batch, uint32_t origin, uint32_t n_shards, void* d_send,
                   uint32_t* d_send_counts, uint32_t* d_perm, uint32_t* h_send_counts);
 
+/* rl_route_pack without the host round trip: the same records and d_perm, and for the count
+ * exchange d_x[2 j] = records for owner j, d_x[2 j + 1] = 0 or RL_EINVAL when the device found
+ * the batch malformed (an unknown rule / request index, a time outside the range) — the pair
+ * each origin sends to owner j in the all-to-all of counts (router.py). Ordered on the engine
+ * stream, nothing synchronised; argument errors are returned at once. */
+int rl_route_pack_async(rl_engine* e, const rl_batch* device_batch, uint32_t origin, uint32_t n_shards, void* d_send,
+                        uint32_t* d_x, uint32_t* d_perm);
+
 /* Owner side: decide n routed records (device memory, RL_ROUTE_RECORD_BYTES each) and write
  * one reply per record (RL_ROUTE_REPLY_BYTES each: rl_status + ThrottleMillis) into d_reply.
  * Asynchronous like rl_submit_device; rl_wait() completes it. */

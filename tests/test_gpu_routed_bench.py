@@ -38,4 +38,35 @@ def test_routed_bench_one_rank():
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["value"] > 0 and line["n_gpus"] == 1
     assert "RCCL all-to-all" in line["config"]["parallelism"], line["config"]
-    assert line["engine"]["lsd_fallbacks_timed"] == 0 or line["engine"]["lsd_fallbacks_timed"] >= 0
+
+
+def test_pack_async_pairs_and_device_errors():
+    """rl_route_pack_async: per owner (count, status) on the device — counts equal the
+    synchronous pack's, and a malformed batch (unknown rule id) reports RL_EINVAL in every
+    pair instead of failing the call."""
+    import torch
+
+    sys.path.insert(0, str(ROOT / "api-ratelimit_amd"))
+    sys.path.insert(0, str(ROOT / "tests"))
+    import hiprl
+    import router
+    import streams
+
+    dev = torch.device("cuda", 0)
+    world = 4
+    e = hiprl.Engine(max_batch_desc=1 << 14)
+    e.load_rules(streams.RULES)
+    sh = router.EngineShard(e, 1, world, dev, 1 << 14)
+    reqs = streams.make_stream(5, 800, t0=1_700_000_000)
+    db = router.DeviceBatch.from_host(hiprl.build_batch(reqs), dev)
+    _, _, counts, _ = sh.pack(db)
+    _, x, _ = sh.pack_async(db)
+    xs = x.cpu().numpy()
+    assert list(xs[0::2]) == counts and not xs[1::2].any()
+    bad = hiprl.build_batch(reqs)
+    bad.rule[3] = len(streams.RULES) + 5  # unknown rule id: found on the device
+    dbb = router.DeviceBatch.from_host(bad, dev)
+    _, x, _ = sh.pack_async(dbb)
+    assert (x.cpu().numpy()[1::2] == -1).all()
+    with pytest.raises(hiprl.RedisError):
+        sh.pack(dbb)
