@@ -15,9 +15,11 @@ src/redis/driver_impl.go:56-90). One step of a rank:
 
 A shard whose pack or decide fails still takes part in every exchange of the step: the
 counts all-to-all carries each origin's pack status next to its counts, and a status
-all-to-all after the owners decide carries each owner's. Every rank then raises together
-(its own error, or RL_EPEER naming the failed shard), so one bad batch cannot leave the
-other GPUs blocked in a collective.
+all-to-all after the owners decide carries each owner's (the replies are exchanged and
+unpacked either way). Every rank then raises together (its own error, or RL_EPEER naming
+the failed shard), so one bad batch cannot leave the other GPUs blocked in a collective.
+A step synchronises the host twice: once for the counts (send and receive sizes of the
+record exchange), once for the owners' statuses at its end.
 
 The exchange is plain torch.distributed (RCCL over xGMI for "nccl", gloo on CPU for the
 tests); the shard object does steps 1, 4 and 6. EngineShard is the product shard (HIP
@@ -210,14 +212,18 @@ class ShardRouter:
             reply = sh.decide(recv, n_in)
         except hiprl.RedisError as ex:
             own, reply = ex, sh.empty(n_in * REP)
+        # The owners' statuses, the replies and the unpack are all enqueued before the host
+        # waits once, at the end: a failed owner still sends (meaningless) replies of the agreed
+        # sizes, and every rank raises after the exchanges, so no rank is left in a collective.
         e = torch.full((self.world,), _code(own) if own is not None else 0, dtype=torch.int32, device=x.device)
         re_ = torch.empty_like(e)
         dist.all_to_all_single(re_, e, group=self.group)
+        back = sh.empty(sum(counts) * REP)
+        dist.all_to_all_single(back, reply, [c * REP for c in counts], [c * REP for c in rcounts], group=self.group)
+        out = sh.unpack(b, perm, back)
         status = [int(v) for v in re_.tolist()]
         if any(status):
             self._raise("decide its records", status, own)
-        back = sh.empty(sum(counts) * REP)
-        dist.all_to_all_single(back, reply, [c * REP for c in counts], [c * REP for c in rcounts], group=self.group)
         self.last_recv = n_in
         self.last_status = [0] * self.world
-        return sh.unpack(b, perm, back)
+        return out
