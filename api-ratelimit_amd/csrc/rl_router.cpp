@@ -13,8 +13,8 @@
 // status word per shard through each exchange, so every shard completes every collective of
 // a step and then all of them fail together.
 //
-// Ordering is host-synchronous between phases: rl_route_pack synchronises the engine stream;
-// each exchange is synchronised on the router stream before the next phase reads its result.
+// Local transport: host-synchronous between phases. RCCL transport: three host waits per
+// step (counts, the owner's decide, the end), the two streams ordered by events otherwise.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -59,7 +59,8 @@ struct rl_router {
   hipStream_t rs = nullptr;  // exchanges
   std::vector<ShardBufs> sh;
   int32_t* d_x = nullptr;    // RCCL: [2G] send + [2G] receive status/count words
-  int32_t* h_x = nullptr;    // pinned mirror of d_x
+  int32_t* h_x = nullptr;    // pinned mirror of d_x + [G] owner statuses
+  hipEvent_t ev = nullptr;   // orders the router and engine streams
   rl_router_stats st{};
   std::string err;
 
@@ -93,6 +94,8 @@ void rl_router::free_all() {
   if (h_x) (void)hipHostFree(h_x);
   if (comm) (void)ncclCommDestroy(comm);
   if (rs) (void)hipStreamDestroy(rs);
+  if (ev) (void)hipEventDestroy(ev);
+  ev = nullptr;
   d_x = nullptr;
   h_x = nullptr;
   comm = nullptr;
@@ -187,32 +190,51 @@ int rl_router::step_local(const rl_batch* b, rl_status* const* out, uint32_t* co
 
 // RCCL transport: this rank's batch; counts + status, records, replies + status over the
 // communicator. Every rank runs all three exchanges whatever its own status.
+//
+// Three host waits per step: the counts (the record exchange's split sizes), the owner's
+// decide (its status), and the end of the step. rl_route_pack_async writes the (count, status)
+// pairs on the device, so the pack needs no wait of its own; the router stream and the engine
+// stream are ordered by events around the record exchange and the unpack. The unpack runs
+// before the owners' statuses are read: when a step fails, out and thr hold garbage.
 int rl_router::step_rccl(const rl_batch* b, rl_status* out, uint32_t* thr) {
   const uint32_t G = cfg.n_shards, me = cfg.rank;
   ShardBufs& s = sh[0];
+  hipStream_t es = (hipStream_t)rl_stream(s.e);
   const double t0 = now_us();
   int rc_pack = RL_ECAPACITY;
   std::string pack_msg = "batch exceeds the router's max_desc";
   if (b->n_desc <= cfg.max_desc) {
-    rc_pack = rl_route_pack(s.e, b, me, G, s.send, s.d_cnt, s.perm, s.cnt);
+    rc_pack = rl_route_pack_async(s.e, b, me, G, s.send, reinterpret_cast<uint32_t*>(d_x), s.perm);
     pack_msg = rc_pack ? rl_last_error(s.e) : "";
   }
-  int32_t* hs = h_x;           // [2G] to send
+  int32_t* hs = h_x;           // [2G] sent
   int32_t* hr = h_x + 2 * G;   // [2G] received
-  for (uint32_t j = 0; j < G; ++j) {
-    hs[2 * j] = rc_pack ? 0 : (int32_t)s.cnt[j];
-    hs[2 * j + 1] = rc_pack;
+  hipError_t he;
+  if (rc_pack) {  // found on the host: no pairs on the device, send (0, rc_pack) to every owner
+    for (uint32_t j = 0; j < G; ++j) {
+      hs[2 * j] = 0;
+      hs[2 * j + 1] = rc_pack;
+    }
+    he = hipMemcpyAsync(d_x, hs, 8 * G, hipMemcpyHostToDevice, rs);
+  } else {
+    he = hipEventRecord(ev, es);
+    if (he == hipSuccess) he = hipStreamWaitEvent(rs, ev, 0);
   }
-  hipError_t he = hipMemcpyAsync(d_x, hs, 8 * G, hipMemcpyHostToDevice, rs);
   if (int rc = hip(he, "counts upload")) return rc;
   if (int rc = nccl(ncclAllToAll(d_x, d_x + 2 * G, 2, ncclInt32, comm, rs), "ncclAllToAll(counts)")) return rc;
-  he = hipMemcpyAsync(hr, d_x + 2 * G, 8 * G, hipMemcpyDeviceToHost, rs);
+  he = hipMemcpyAsync(h_x, d_x, 16 * G, hipMemcpyDeviceToHost, rs);  // sent and received pairs
   if (he == hipSuccess) he = hipStreamSynchronize(rs);
   if (int rc = hip(he, "counts exchange")) return rc;
+  if (!rc_pack && hs[1]) {  // the device found the batch malformed (rl_route_pack's checks)
+    rc_pack = hs[1];
+    pack_msg = "rl_route_pack_async: batch references an unknown rule id or request index, malformed prefix "
+               "offsets, or a time outside [0, 0xFFFD0000]";
+  }
   const double t1 = now_us();
   st.pack_us = t1 - t0;
   int first_err = 0;
   for (uint32_t j = 0; j < G; ++j) {
+    s.cnt[j] = rc_pack ? 0u : (uint32_t)hs[2 * j];
     st.status[j] = hr[2 * j + 1];
     if (hr[2 * j + 1] && !first_err) first_err = j == me ? hr[2 * j + 1] : RL_EPEER;
   }
@@ -236,15 +258,20 @@ int rl_router::step_rccl(const rl_batch* b, rl_status* out, uint32_t* thr) {
   if (int rc = nccl(ncclAllToAllv(s.send, sc.data(), sd.data(), s.recv, rc_.data(), rd.data(), ncclUint8, comm, rs),
                     "ncclAllToAllv(records)"))
     return rc;
-  if (int rc = hip(hipStreamSynchronize(rs), "record exchange")) return rc;
+  he = hipEventRecord(ev, rs);  // the owner's decide reads the received records
+  if (he == hipSuccess) he = hipStreamWaitEvent(es, ev, 0);
+  if (int rc = hip(he, "record exchange")) return rc;
   const double t2 = now_us();
-  st.exchange_us = t2 - t1;
+  st.exchange_us = t2 - t1;  // enqueue only: the exchange's time is inside decide_us
   int rc_dec = 0;
   if (n_in) {
     rc_dec = rl_submit_routed(s.e, s.recv, n_in, s.reply);
     if (!rc_dec) rc_dec = rl_wait(s.e);
   }
   std::string dec_msg = rc_dec ? rl_last_error(s.e) : "";
+  if (!n_in) {  // nothing decided: the exchange still has to be complete before the replies
+    if (int rc = hip(hipStreamSynchronize(es), "record exchange")) return rc;
+  }
   const double t3 = now_us();
   st.decide_us = st.decide_max_us = t3 - t2;
   for (uint32_t j = 0; j < G; ++j) hs[j] = rc_dec;
@@ -268,23 +295,27 @@ int rl_router::step_rccl(const rl_batch* b, rl_status* out, uint32_t* thr) {
     nr = ncclAllToAllv(s.reply, sc.data(), sd.data(), s.back, rc_.data(), rd.data(), ncclUint8, comm, rs);
   const ncclResult_t ne = ncclGroupEnd();
   if (int rc = nccl(nr != ncclSuccess ? nr : ne, "ncclAllToAll(replies)")) return rc;
-  he = hipMemcpyAsync(hr, d_x + 2 * G, 4 * G, hipMemcpyDeviceToHost, rs);
-  if (he == hipSuccess) he = hipStreamSynchronize(rs);
+  int32_t* hst = h_x + 4 * G;  // the owners' statuses (own pinned words: hs is still being uploaded)
+  he = hipMemcpyAsync(hst, d_x + 2 * G, 4 * G, hipMemcpyDeviceToHost, rs);
+  if (he == hipSuccess) he = hipEventRecord(ev, rs);
+  if (he == hipSuccess) he = hipStreamWaitEvent(es, ev, 0);
   if (int rc = hip(he, "reply exchange")) return rc;
-  const double t4 = now_us();
-  st.reply_us = t4 - t3;
+  int rc = rl_route_unpack(s.e, b, s.perm, s.back, out, thr);
+  if (rc) {
+    (void)hipStreamSynchronize(rs);  // the exchange is complete before the error returns
+    return fail(rc, "shard %u (unpack): %s", me, rl_last_error(s.e));
+  }
+  if ((rc = hip(hipStreamSynchronize(es), "reply exchange and unpack"))) return rc;
+  st.reply_us = now_us() - t3;
+  st.unpack_us = 0;  // inside reply_us
   for (uint32_t j = 0; j < G; ++j) {
-    st.status[j] = hr[j];
-    if (hr[j] && !first_err) first_err = j == me ? hr[j] : RL_EPEER;
+    st.status[j] = hst[j];
+    if (hst[j] && !first_err) first_err = j == me ? hst[j] : RL_EPEER;
   }
   if (first_err) {
     if (rc_dec) return fail(rc_dec, "shard %u (decide): %s", me, dec_msg.c_str());
     return fail(RL_EPEER, "a peer shard failed to decide its records (see rl_router_stats.status)");
   }
-  int rc = rl_route_unpack(s.e, b, s.perm, s.back, out, thr);
-  if (rc) return fail(rc, "shard %u (unpack): %s", me, rl_last_error(s.e));
-  if ((rc = hip(hipStreamSynchronize((hipStream_t)rl_stream(s.e)), "unpack"))) return rc;
-  st.unpack_us = now_us() - t4;
   return 0;
 }
 
@@ -334,7 +365,8 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
   }
   if (he == hipSuccess && rccl) {
     he = hipMalloc(&r->d_x, 4 * G * 4);
-    if (he == hipSuccess) he = hipHostMalloc(&r->h_x, 4 * G * 4, hipHostMallocDefault);
+    if (he == hipSuccess) he = hipHostMalloc(&r->h_x, 5 * G * 4, hipHostMallocDefault);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&r->ev, hipEventDisableTiming);
   }
   if (he != hipSuccess) return bail(he);
   if (rccl) {

@@ -94,6 +94,9 @@ def parse():
     ap.add_argument("--lib", type=str, default="", help=argparse.SUPPRESS)  # diagnostics: a variant library
     # tests: the routed (RCCL all-to-all) step on one rank, so the multi-GPU path runs on a 1-GPU box
     ap.add_argument("--force-routed", action="store_true", help=argparse.SUPPRESS)
+    # routed steps through the C-ABI router (rl_router_step, RCCL transport: the Go host's path)
+    # instead of router.ShardRouter; torch.distributed (gloo) only shares the RCCL id and times
+    ap.add_argument("--native-router", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--dump-stamps", type=str, default="", help=argparse.SUPPRESS)  # -DRL_STAMPS variant: raw stamps
     return ap.parse_args()
 
@@ -288,7 +291,10 @@ def main():
     dist = None
     if world > 1 or args.force_routed:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.native_router:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -310,8 +316,14 @@ def main():
                        lib_path=(ROOT / args.lib) if args.lib else None)
     eng.load_rules(rules)
     gen = DeviceGen(args.config, d, seed, K, dev)
-    rtr = router.ShardRouter(router.EngineShard(eng, rank, world, dev, d)) if routed else None
-    pipelined = rtr is None and not args.serial
+    rtr = nrt = None
+    if routed and args.native_router:
+        ids = [hiprl.Router.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=0)
+        nrt = hiprl.Router([eng], max_desc=d, n_shards=world, rank=rank, rccl_id=ids[0])
+    elif routed:
+        rtr = router.ShardRouter(router.EngineShard(eng, rank, world, dev, d))
+    pipelined = not routed and not args.serial
     DEPTH = min(args.depth, hiprl.MAX_IN_FLIGHT) if pipelined else 1
     outs = [torch.empty(d * 20, dtype=torch.uint8, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
     thrs = [torch.empty(d, dtype=torch.int32, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
@@ -326,6 +338,9 @@ def main():
                 continue
             sb = hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs())
             o, t = outs[(first + j) % len(outs)].data_ptr(), thrs[(first + j) % len(thrs)].data_ptr()
+            if nrt is not None:
+                nrt.step([sb], [o], [t])
+                continue
             if pipelined:
                 eng.submit_pipelined_batch(sb, o, t)
                 pend += 1
@@ -351,6 +366,9 @@ def main():
             rtr.step(db)
             continue
         sb = hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs())
+        if nrt is not None:
+            nrt.step([sb], [outs[b % len(outs)].data_ptr()], [thrs[b % len(thrs)].data_ptr()])
+            continue
         eng.submit_pipelined_batch(sb, outs[b % len(outs)].data_ptr(), thrs[b % len(thrs)].data_ptr())
         pend += 1
         if pend == 2:
@@ -382,7 +400,7 @@ def main():
     elapsed = time.perf_counter() - t0
     fb_timed = eng.stats()["lsd_fallbacks"] - fb0
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.native_router else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     total_desc = world * args.steps * d
@@ -414,7 +432,7 @@ def main():
     # batches in C memory), three in flight (H2D, kernels and D2H of different batches
     # overlap), outputs copied out by rl_wait_into — what the Go side sees end to end.
     host = None
-    if not args.no_host_path and rtr is None:
+    if not args.no_host_path and not routed:
         hbatches = []
         for db in dbs[args.warmup:args.warmup + args.steps]:
             n = int(db.off[-1].item())
@@ -516,6 +534,7 @@ def main():
         "config": {"workload": wl, "descriptors_per_batch": d, "requests_per_batch": d,
                    "batches_per_second_window": K, "prefill_batches": prefill,
                    "parallelism": (f"key-sharded x{world}, RCCL all-to-all routing (32-B records out, 24-B replies back)"
+                                   + (", C-ABI router (rl_router_step)" if nrt is not None else "")
                                    if routed else "single shard" if world == 1
                                    else f"x{world} independent replicas (no collective)"),
                    "pipeline": args.pipeline, "batches_in_flight": DEPTH,

@@ -130,3 +130,33 @@ def test_owner_over_capacity_fails_every_shard():
     with pytest.raises(hiprl.RedisError, match="shard 1 \\(decide\\)") as ex:
         _step(r, batches)
     assert ex.value.code == -4 and r.stats()["status"] == [0, -4], r.stats()
+
+
+def test_rccl_transport_one_rank_errors(monkeypatch):
+    """RCCL transport error steps: a batch the device finds malformed (unknown rule id: the
+    pack's status rides in the counts exchange) and a batch over max_desc (found on the host)
+    (an owner that cannot take its records is covered on the local transport above: at one
+    rank the pack's capacity check comes first) fail the step with the shard's own code, and the
+    router keeps working: the next step equals the oracle without the failed ones."""
+    monkeypatch.setenv("NCCL_SOCKET_IFNAME", "lo")
+    per = 1200
+    e = hiprl.Engine(local_cache=True, max_batch_desc=4 * per)
+    e.load_rules(streams.RULES)
+    r = hiprl.Router([e], max_desc=4 * per, n_shards=1, rank=0, rccl_id=hiprl.Router.unique_id())
+    o = oracle.Oracle(local_cache=True)
+    o.load_rules(streams.RULES)
+    steps = stream_batches(1, 3, per, seed=31)
+    _check(o, steps[0], _step(r, steps[0]), "before")
+    b = steps[1][0]
+    rule = b.rule.copy()
+    rule[len(rule) // 3] = 77
+    with pytest.raises(hiprl.RedisError, match="shard 0 \\(pack\\)") as ex:
+        _step(r, [hiprl.Batch(b.blob, b.off, rule, b.req_of, b.now, b.hits)])
+    assert ex.value.code == -1 and r.stats()["status"][0] == -1
+    big = routing.concat_batches(stream_batches(1, 5, per, seed=32)[0] * 5)
+    assert big.n_desc > 4 * per
+    with pytest.raises(hiprl.RedisError, match="shard 0 \\(pack\\)") as ex:
+        _step(r, [big])
+    assert ex.value.code == -4
+    _check(o, steps[2], _step(r, steps[2]), "after")
+    r.close()
