@@ -17,8 +17,10 @@ traffic is 8000 distinct 1e6-descriptor batches.
 Multi-GPU (torchrun, one rank per GPU): the key space is hash-sharded one
 shard per GPU. Every rank ingests its own 1e6-descriptor batch per step, routes each
 descriptor to the GPU owning its key with an RCCL all-to-all (32-B records), the owners
-decide, and the 24-B replies return with the reverse all-to-all (api-ratelimit_amd/router.py)
-— weak scaling. value = descriptors decided for all ranks / max-over-ranks time.
+decide, and the 24-B replies return with the reverse all-to-all — weak scaling. The step
+runs through the C-ABI router (rl_router_step, csrc/rl_router.cpp: the Go host's entry point,
+its own RCCL communicator); --torch-router runs it through api-ratelimit_amd/router.py
+(torch.distributed) instead. value = descriptors decided for all ranks / max-over-ranks time.
 --independent runs N unrouted replicas instead (each rank its own key space).
 
 Also reported (rank 0): per-kernel HIP-event times over an extra K steps, the roofline of the
@@ -94,9 +96,9 @@ def parse():
     ap.add_argument("--lib", type=str, default="", help=argparse.SUPPRESS)  # diagnostics: a variant library
     # tests: the routed (RCCL all-to-all) step on one rank, so the multi-GPU path runs on a 1-GPU box
     ap.add_argument("--force-routed", action="store_true", help=argparse.SUPPRESS)
-    # routed steps through the C-ABI router (rl_router_step, RCCL transport: the Go host's path)
-    # instead of router.ShardRouter; torch.distributed (gloo) only shares the RCCL id and times
-    ap.add_argument("--native-router", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--torch-router", action="store_true",
+                    help="routed steps through router.ShardRouter (torch.distributed over RCCL) instead of the "
+                         "C-ABI router rl_router_step (the Go host's path, the default)")
     ap.add_argument("--dump-stamps", type=str, default="", help=argparse.SUPPRESS)  # -DRL_STAMPS variant: raw stamps
     return ap.parse_args()
 
@@ -289,8 +291,13 @@ def main():
     import torch
 
     dist = None
+    args.native_router = not args.torch_router
     if world > 1 or args.force_routed:
         import torch.distributed as dist
+        # the C-ABI router's own communicator bootstraps over loopback (one node); torch.distributed
+        # (gloo) only shares its id and carries the barrier and the max over ranks of the time
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         if args.native_router:
             dist.init_process_group("gloo")
         else:

@@ -3,7 +3,8 @@
 The driver's scaling run launches `bench.py --gpus N` with one rank per GPU; every rank packs
 its batch, exchanges records and replies with RCCL all-to-alls and decides as an owner. On a
 one-GPU box the same code runs as one rank with --force-routed (a communicator of one rank:
-every collective is real RCCL, every record goes to its own owner), so the routed step's
+every collective is real RCCL, every record goes to its own owner), through the C-ABI router
+(the default) and through router.ShardRouter (--torch-router), so the routed step's
 plumbing is exercised before the 8-GPU run. Bit-exactness of routed steps is covered by
 tests/test_gpu_router.py (GPU, logical shards) and tests/test_router_cpu.py (gloo, 2-3 ranks).
 """
@@ -26,18 +27,20 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_routed_bench_one_rank():
+@pytest.mark.parametrize("mode", [[], ["--torch-router"]], ids=["c_abi_router", "torch_router"])
+def test_routed_bench_one_rank(mode):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
            "--force-routed", "--steps", "3", "--warmup", "1", "--prefill", "6", "--batches-per-second", "4",
            "--desc", "200000", "--log2-slots", "22", "--cpu-seconds", "0", "--no-kernel-times",
-           "--no-roofline-probe", "--no-host-path"]
+           "--no-roofline-probe", "--no-host-path"] + mode
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["value"] > 0 and line["n_gpus"] == 1
     assert "RCCL all-to-all" in line["config"]["parallelism"], line["config"]
+    assert ("C-ABI router" in line["config"]["parallelism"]) == (not mode), line["config"]
 
 
 def test_pack_async_pairs_and_device_errors():
