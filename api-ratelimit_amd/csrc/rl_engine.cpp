@@ -44,6 +44,8 @@ void launch_decide(hipStream_t, const SortedRec*, const SegInfo*, const DevRule*
 void launch_occ_update(hipStream_t, RegionOcc*, EngineCtl*);
 void launch_cand_state(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, EngineCtl*);
 uint32_t route_bcnt_words(uint32_t n);
+void launch_route_pack_strided(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint32_t, uint32_t,
+                               uint32_t, RRec*, uint32_t*, uint32_t*, uint32_t*);
 void launch_route_pack(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint32_t, uint32_t, RRec*,
                        uint8_t*, uint32_t*, RRec*, uint32_t*, uint32_t*, EngineCtl*, uint32_t*);
 void launch_route_reply(hipStream_t, uint32_t, const rl_status*, const uint32_t*, RReply*);
@@ -1164,7 +1166,7 @@ static int route_pack_launch(rl_engine* e, const rl_batch* b, uint32_t origin, u
   if (!e->r_tmp) {
     chk(hipMalloc(&e->r_tmp, N * sizeof(RRec)));
     chk(hipMalloc(&e->r_own, N));
-    chk(hipMalloc(&e->r_bcnt, (size_t)route_bcnt_words((uint32_t)N) * 4));
+    if (!e->r_bcnt) chk(hipMalloc(&e->r_bcnt, (size_t)route_bcnt_words((uint32_t)N) * 4));  // (strided pack)
     chk(hipMalloc(&e->r_ctl, sizeof(EngineCtl)));
     chk(hipHostMalloc(&e->h_route, 64 * 4, hipHostMallocDefault));
     if (he != hipSuccess) return e->hip_fail(he, "router scratch allocation");
@@ -1197,6 +1199,33 @@ int rl_route_pack_async(rl_engine* e, const rl_batch* b, uint32_t origin, uint32
                         uint32_t* d_x, uint32_t* d_perm) {
   if (!d_x) return e ? e->fail(RL_EINVAL, "null routing buffer") : RL_EINVAL;
   return route_pack_launch(e, b, origin, n_shards, d_send, nullptr, d_perm, d_x);
+}
+
+int rl_route_pack_strided(rl_engine* e, const rl_batch* b, uint32_t origin, uint32_t n_shards, uint32_t stride,
+                          void* d_send, uint32_t* d_x, uint32_t* d_perm) {
+  if (!d_x) return e ? e->fail(RL_EINVAL, "null routing buffer") : RL_EINVAL;
+  if (!e || !b) return RL_EINVAL;
+  if (b->n_desc > stride) return e->fail(RL_ECAPACITY, "batch of %u descriptors exceeds the owner stride %u", b->n_desc, stride);
+  if (stride > RL_ROUTE_MAX_REQ) return e->fail(RL_EINVAL, "owner stride above 2^27 records");
+  // the same checks and scratch as the three-kernel pack; its launches are replaced below
+  if (e->n_fl) return e->fail(RL_ESTATE, "rl_route_pack while a batch is in flight (call rl_wait)");
+  if (n_shards == 0 || n_shards > ROUTE_MAX_SHARDS || origin >= ROUTE_MAX_SHARDS)
+    return e->fail(RL_EINVAL, "n_shards must be 1..%u and origin < %u", ROUTE_MAX_SHARDS, ROUTE_MAX_SHARDS);
+  if (b->n_desc > e->cfg.max_batch_desc) return e->fail(RL_ECAPACITY, "batch exceeds engine capacity");
+  if (b->n_req > RL_ROUTE_MAX_REQ) return e->fail(RL_EINVAL, "routed batch holds more than 2^27 requests");
+  if (b->reserved) return e->fail(RL_EINVAL, "rl_batch.reserved must be 0");
+  if (b->n_desc && (!d_send || !d_perm)) return e->fail(RL_EINVAL, "null routing buffer");
+  if (!e->d_rules) rl_load_rules(e, nullptr, 0);
+  const size_t N = e->cfg.max_batch_desc ? e->cfg.max_batch_desc : 1;
+  hipError_t he = hipSuccess;
+  if (!e->r_bcnt) he = hipMalloc(&e->r_bcnt, (size_t)route_bcnt_words((uint32_t)N) * 4);
+  if (he == hipSuccess) he = hipMemsetAsync(e->r_bcnt, 0, (size_t)route_bcnt_words(b->n_desc) * 4, e->stream);
+  if (he == hipSuccess) {
+    launch_route_pack_strided(e->stream, *b, e->d_rules, e->n_rules, e->cfg.hash_seed, origin, n_shards, stride,
+                              reinterpret_cast<RRec*>(d_send), d_perm, e->r_bcnt, d_x);
+    he = hipGetLastError();
+  }
+  return he == hipSuccess ? 0 : e->hip_fail(he, "rl_route_pack_strided");
 }
 
 int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_reply) {

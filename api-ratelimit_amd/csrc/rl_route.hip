@@ -190,6 +190,163 @@ __global__ __launch_bounds__(NT) void k_route_scatter(uint32_t n, const RRec* __
   perm[i] = pos;
 }
 
+// One-pass pack into a strided send buffer (owner j's records at [j * stride, j * stride +
+// count_j)): hash and owner as k_route_hash, ranks inside the block as k_route_scatter, and
+// each block's offset per owner from a decoupled look-back over the blocks before it, so the
+// records are written once, straight to their place (no tmp records, no scan launch). lb
+// holds one word per (block, owner), block-major: each block's words in a line of their own
+// (owner-major, 32 blocks share a line and their publishing stores from every XCD contend
+// for it: 66 us per 10^6 descriptors against 32): flag in the top two bits (A = the block's own count, P =
+// inclusive prefix), zeroed before the launch together with gerr. Workgroups are dispatched
+// in blockIdx order, so every block looked at is resident or done; the spin is bounded all
+// the same (ERR_SPIN -> RL_EDEVICE in the pairs). The last block writes the (count, status)
+// pair of every owner. Every block ORs its error flags into gerr before it publishes, and the
+// look-back acquires what the blocks before it released, so the last block's read of gerr
+// sees every block's flags. The look-back words are self-contained (flag and value in one
+// word), so they are read and written relaxed at agent scope: acquire loads and release
+// stores would invalidate / write back the XCD's L2 on every block (738 us per 10^6
+// descriptors measured with them, against the three-kernel pack's 42). The look-back is wave-wide (64 blocks per read): one lane walking
+// back one block at a time took 2 ms per 10^6 descriptors.
+constexpr uint32_t LB_A = 1u << 30, LB_P = 2u << 30, LB_V = (1u << 30) - 1u;
+constexpr uint32_t LB_SPIN_LIMIT = 1u << 22;
+constexpr int LB_U = 1;  // look-back words per lane per read (4: 52 us, every extra word a line)
+__global__ __launch_bounds__(NT) void k_route_pack1(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
+                                                     uint64_t seed, uint32_t origin, uint32_t n_shards, uint32_t stride,
+                                                     RRec* __restrict__ send, uint32_t* __restrict__ perm,
+                                                     uint32_t* lb, uint32_t* gerr, uint32_t* __restrict__ x) {
+  constexpr int W = NT / 64;
+  __shared__ uint32_t s_wc[W][NS + 1];
+  __shared__ uint32_t s_base[NS];
+  __shared__ uint32_t s_err;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6, i = blockIdx.x * NT + tid;
+  for (uint32_t k = tid; k < W * (NS + 1); k += NT) (&s_wc[0][0])[k] = 0;
+  if (tid == 0) s_err = 0;
+  __syncthreads();
+  RRec r{};
+  uint32_t o = ROUTE_LOCAL, err = 0;
+  if (i < in.n_desc) {
+    const uint32_t rule = in.rule[i], q = in.req_of[i], qp = in.req_of[i ? i - 1u : 0u];
+    const uint32_t o0 = in.off[i], o1 = in.off[i + 1];
+    if (o1 < o0 || o1 > in.blob_bytes || qp > q) err |= ERR_BAD_INPUT;
+    const bool nil = rule == RL_NIL_RULE;
+    if (!nil && !err && (rule >= n_rules || q >= in.n_req)) err |= ERR_BAD_INPUT;
+    const uint32_t qc = q < in.n_req ? q : 0u;
+    const uint32_t oc = err ? 0u : o0;
+    const int64_t now = in.now[qc];
+    const uint32_t ha = in.hits[qc];
+    const u32x4* pw = reinterpret_cast<const u32x4*>(in.blob + (oc & ~3u));
+    const u32x4 w0 = pw[0];
+    const u32x4 w1 = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint32_t*>(pw) + 4);
+    if (!nil && !err) {
+      if (now < 0 || now > MAX_NOW) {
+        err |= ERR_BAD_TIME;
+      } else {
+        const FpState fs = prefix_state_pre(w0, w1, in.blob, o0, o1 - o0, seed);
+        r.a = fs.a;
+        r.b = fs.b;
+        r.now = (uint32_t)now;
+        r.rule = rule;
+        r.h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
+        r.greq = (origin << ROUTE_REQ_BITS) | q;
+        o = route_owner(fs.a, fs.b, n_shards);
+      }
+    }
+  }
+  const uint32_t d = o == ROUTE_LOCAL ? (uint32_t)NS : o;  // 0..16
+  uint64_t m = ~0ull;
+#pragma unroll
+  for (int bt = 0; bt < 5; ++bt) {
+    const bool bit = (d >> bt) & 1u;
+    const uint64_t bal = __ballot(bit);
+    m &= bit ? bal : ~bal;
+  }
+  const uint32_t rank = (uint32_t)__popcll(m & lanemask_lt());
+  if (lane == (uint32_t)__ffsll((unsigned long long)m) - 1u) s_wc[w][d] = (uint32_t)__popcll(m);
+  if (err) atomicOr(&s_err, err);
+  __syncthreads();
+  if (tid == 0 && s_err) {  // before any owner's word of this block is published
+    atomicOr(gerr, s_err);
+    __threadfence();
+  }
+  __syncthreads();
+  // wave w publishes and looks back for owners w, w + W, ...: the wave reads the 64 blocks
+  // before the window's end at once (LB_U per lane), stops at the nearest P (summing the A's before it) or
+  // moves 64 blocks back when all are A; it waits only for blocks nearer than that P
+  const uint32_t bi = blockIdx.x;
+  for (uint32_t j = w; j < n_shards; j += W) {  // wave-uniform
+    uint32_t agg = 0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) agg += s_wc[k][j];
+    if (lane == 0)
+      __hip_atomic_store(&lb[(size_t)bi * NS + j], (bi ? LB_A : LB_P) | agg, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t excl = 0;
+    if (bi) {
+      int32_t end = (int32_t)bi - 1;
+      uint32_t spun = 0;
+      for (;;) {
+        // lane l reads blocks end - LB_U l - u: distance t = LB_U l + u
+        uint32_t v[LB_U];
+#pragma unroll
+        for (int u = 0; u < LB_U; ++u) {
+          const int32_t k = end - (int32_t)(lane * LB_U + u);
+          v[u] = k >= 0 ? __hip_atomic_load(&lb[(size_t)k * NS + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : LB_P;  // before block 0: an inclusive prefix of 0
+        }
+        uint32_t up = LB_U, un = LB_U;  // the lane's first P and first unpublished word
+#pragma unroll
+        for (int u = LB_U - 1; u >= 0; --u) {
+          if ((v[u] >> 30) == 2u) up = u;
+          if ((v[u] >> 30) == 0u) un = u;
+        }
+        const uint64_t pm = __ballot(up < LB_U);
+        const uint32_t lp = pm ? (uint32_t)__ffsll((unsigned long long)pm) - 1u : 64u;  // lane of the first P
+        // waiting: an unpublished word nearer than the first P
+        const bool wait = lane < lp ? un < LB_U : lane == lp ? un < up : false;
+        if (__ballot(wait)) {
+          if (++spun > LB_SPIN_LIMIT) {
+            if (lane == 0) atomicOr(gerr, (uint32_t)ERR_SPIN);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        uint32_t part = 0;
+#pragma unroll
+        for (int u = 0; u < LB_U; ++u)
+          part += lane < lp || (lane == lp && (uint32_t)u <= up) ? v[u] & LB_V : 0u;
+        excl += wave_sum_u32(part);
+        if (pm) break;
+        end -= 64 * LB_U;
+      }
+      if (lane == 0)
+        __hip_atomic_store(&lb[(size_t)bi * NS + j], LB_P | ((excl + agg) & LB_V), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      s_base[j] = excl;
+      if (bi == gridDim.x - 1u) {  // the last block: every owner's total and the batch's status
+        const uint32_t e = __hip_atomic_load(gerr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        x[2 * j] = excl + agg;
+        x[2 * j + 1] = e & ERR_SPIN ? (uint32_t)RL_EDEVICE
+                       : e & (ERR_BAD_INPUT | ERR_BAD_TIME) ? (uint32_t)RL_EINVAL : 0u;
+      }
+    }
+  }
+  __syncthreads();
+  if (i >= in.n_desc) return;
+  if (d == (uint32_t)NS) {
+    perm[i] = RL_ROUTE_LOCAL;
+    return;
+  }
+  uint32_t before = 0;
+#pragma unroll
+  for (int k = 0; k < W; ++k) before += (uint32_t)k < w ? s_wc[k][d] : 0u;
+  const uint32_t pos = d * stride + s_base[d] + before + rank;
+  send[pos] = r;
+  perm[i] = pos;
+}
+
 __global__ __launch_bounds__(NT) void k_route_reply(uint32_t n, const rl_status* __restrict__ out,
                                                      const uint32_t* __restrict__ thr, RReply* __restrict__ reply) {
   const uint32_t i = blockIdx.x * NT + threadIdx.x;
@@ -239,6 +396,14 @@ void launch_route_pack(hipStream_t st, const rl_batch& b, const DevRule* rules, 
                      x);
   hipLaunchKernelGGL(route::k_route_scatter, dim3(nb), dim3(route::NT), 0, st, b.n_desc, tmp, own, bcnt, send,
                      perm);
+}
+
+void launch_route_pack_strided(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules,
+                               uint64_t seed, uint32_t origin, uint32_t n_shards, uint32_t stride, RRec* send,
+                               uint32_t* perm, uint32_t* lb, uint32_t* x) {
+  const uint32_t nb = route_blocks(b.n_desc);  // lb: nb * NS look-back words + the error word, zeroed
+  hipLaunchKernelGGL(route::k_route_pack1, dim3(nb), dim3(route::NT), 0, st, make_dev_batch(b), rules, n_rules, seed,
+                     origin, n_shards, stride, send, perm, lb, lb + (size_t)nb * route::NS, x);
 }
 
 void launch_route_reply(hipStream_t st, uint32_t n, const rl_status* out, const uint32_t* thr, RReply* reply) {

@@ -204,7 +204,7 @@ int rl_router::step_rccl(const rl_batch* b, rl_status* out, uint32_t* thr) {
   int rc_pack = RL_ECAPACITY;
   std::string pack_msg = "batch exceeds the router's max_desc";
   if (b->n_desc <= cfg.max_desc) {
-    rc_pack = rl_route_pack_async(s.e, b, me, G, s.send, reinterpret_cast<uint32_t*>(d_x), s.perm);
+    rc_pack = rl_route_pack_strided(s.e, b, me, G, cfg.max_desc, s.send, reinterpret_cast<uint32_t*>(d_x), s.perm);
     pack_msg = rc_pack ? rl_last_error(s.e) : "";
   }
   int32_t* hs = h_x;           // [2G] sent
@@ -244,10 +244,10 @@ int rl_router::step_rccl(const rl_batch* b, rl_status* out, uint32_t* thr) {
   }
   std::vector<size_t> sc(G), sd(G), rc_(G), rd(G);
   uint64_t so = 0, ro = 0;
+  const size_t D = cfg.max_desc;  // owner stride of the send and back buffers (rl_route_pack_strided)
   for (uint32_t j = 0; j < G; ++j) {
     sc[j] = (size_t)s.cnt[j] * REC;
-    sd[j] = so;
-    so += sc[j];
+    sd[j] = j * D * REC;
     rc_[j] = (size_t)(uint32_t)hr[2 * j] * REC;
     rd[j] = ro;
     ro += rc_[j];
@@ -282,12 +282,11 @@ int rl_router::step_rccl(const rl_batch* b, rl_status* out, uint32_t* thr) {
     sc[j] = (size_t)(uint32_t)hr[2 * j] * REP;  // to origin j: the replies to its records
     rc_[j] = (size_t)s.cnt[j] * REP;
   }
-  so = ro = 0;
+  so = 0;
   for (uint32_t j = 0; j < G; ++j) {
     sd[j] = so;
     so += sc[j];
-    rd[j] = ro;
-    ro += rc_[j];
+    rd[j] = j * D * REP;  // perm[i] = owner * D + position
   }
   ncclResult_t nr = ncclGroupStart();
   if (nr == ncclSuccess) nr = ncclAllToAll(d_x, d_x + 2 * G, 1, ncclInt32, comm, rs);
@@ -356,12 +355,13 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
   for (uint32_t s = 0; s < n_eng && he == hipSuccess; ++s) {
     ShardBufs& b = r->sh[s];
     b.e = engines[s];
-    he = hipMalloc(&b.send, D * REC);
+    // RCCL transport: owner-strided send / back buffers (rl_route_pack_strided); local: compact
+    he = hipMalloc(&b.send, D * (rccl ? G : 1) * REC);
     if (he == hipSuccess) he = hipMalloc(&b.d_cnt, MAXS * 4);
     if (he == hipSuccess) he = hipMalloc(&b.perm, D * 4);
     if (he == hipSuccess) he = hipMalloc(&b.recv, D * G * REC);
     if (he == hipSuccess) he = hipMalloc(&b.reply, D * G * REP);
-    if (he == hipSuccess) he = hipMalloc(&b.back, D * REP);
+    if (he == hipSuccess) he = hipMalloc(&b.back, D * (rccl ? G : 1) * REP);
   }
   if (he == hipSuccess && rccl) {
     he = hipMalloc(&r->d_x, 4 * G * 4);

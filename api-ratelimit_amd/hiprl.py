@@ -133,6 +133,8 @@ ABI = [
                        C.POINTER(C.c_uint32)], C.c_int),
     ("rl_route_pack_async", [C.c_void_p, C.POINTER(RlBatch), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
                              C.c_void_p], C.c_int),
+    ("rl_route_pack_strided", [C.c_void_p, C.POINTER(RlBatch), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
+                               C.c_void_p, C.c_void_p], C.c_int),
     ("rl_submit_routed", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p], C.c_int),
     ("rl_route_unpack", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     ("rl_load_tree", [C.c_void_p, C.POINTER(RlTreeNode), C.c_uint32, C.c_void_p, C.c_uint32], C.c_int),
@@ -456,6 +458,15 @@ class Engine:
         s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
         self._check(self.lib.rl_route_pack_async(self.h, C.byref(s), origin, n_shards, send_ptr, x_ptr, perm_ptr),
                     "rl_route_pack_async")
+
+    def route_pack_strided(self, n_desc: int, n_req: int, blob_bytes: int, ptrs, origin: int, n_shards: int,
+                           stride: int, send_ptr: int, x_ptr: int, perm_ptr: int):
+        """rl_route_pack_strided: one-kernel pack, owner j's records at send[j * stride ...]."""
+        s = RlBatch()
+        s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
+        s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        self._check(self.lib.rl_route_pack_strided(self.h, C.byref(s), origin, n_shards, stride, send_ptr, x_ptr,
+                                                   perm_ptr), "rl_route_pack_strided")
 
     def submit_routed_async(self, rec_ptr: int, n: int, reply_ptr: int):
         self._check(self.lib.rl_submit_routed(self.h, rec_ptr, n, reply_ptr), "rl_submit_routed")

@@ -252,6 +252,14 @@ int rl_route_pack(rl_engine* e, const rl_batch* device_batch, uint32_t origin, u
 int rl_route_pack_async(rl_engine* e, const rl_batch* device_batch, uint32_t origin, uint32_t n_shards, void* d_send,
                         uint32_t* d_x, uint32_t* d_perm);
 
+/* rl_route_pack_async into a strided send buffer, in one kernel: owner j's records at
+ * d_send[j * stride ...] (d_send holds n_shards * stride records), d_perm[i] = j * stride +
+ * position, pairs in d_x as above (status RL_EDEVICE if the device's look-back spin expired).
+ * For transports that take per-peer displacements (ncclAllToAllv; rl_router_step uses it):
+ * no temporary records, no separate scan. n_desc must be <= stride <= 2^27. */
+int rl_route_pack_strided(rl_engine* e, const rl_batch* device_batch, uint32_t origin, uint32_t n_shards,
+                          uint32_t stride, void* d_send, uint32_t* d_x, uint32_t* d_perm);
+
 /* Owner side: decide n routed records (device memory, RL_ROUTE_RECORD_BYTES each) and write
  * one reply per record (RL_ROUTE_REPLY_BYTES each: rl_status + ThrottleMillis) into d_reply.
  * Asynchronous like rl_submit_device; rl_wait() completes it. */
