@@ -83,7 +83,7 @@ HipRateLimitCache::~HipRateLimitCache() {
 
 void HipRateLimitCache::Flush() {
   std::unique_lock<std::mutex> g(mu_);
-  idle_cv_.wait(g, [&] { return q_.empty() && inflight_ == 0; });
+  idle_cv_.wait(g, [&] { return inflight_ == 0; });
 }
 
 DoLimitResponse HipRateLimitCache::DoLimit(const RateLimitRequest& request,
@@ -117,6 +117,7 @@ DoLimitResponse HipRateLimitCache::DoLimit(const RateLimitRequest& request,
   {
     std::lock_guard<std::mutex> g(mu_);
     q_.push_back(call);
+    ++inflight_;  // until its batch is decided (Flush waits for 0)
   }
   cv_.notify_one();
   f.get();  // rethrows RedisError
@@ -134,105 +135,116 @@ uint32_t HipRateLimitCache::rule_id(const RateLimitLimit& l, bool shadow) {
   return id;
 }
 
-void HipRateLimitCache::submitter() {
-  const size_t cap_desc = s_.batch_limit + 4096, cap_blob = (size_t)(s_.batch_limit + 4096) * 128u;
-  for (;;) {
-    std::vector<std::shared_ptr<Call>> batch;
-    {
-      std::unique_lock<std::mutex> g(mu_);
-      cv_.wait(g, [&] { return stop_ || !q_.empty(); });
-      if (stop_ && q_.empty()) return;
-      // Gather for up to batch_window_us or batch_limit descriptors (implicit pipelining
-      // analogue, src/redis/driver_impl.go:84-89). A batch may straddle at most one window
-      // boundary of a unit, so it is cut when request times are 2 s or more apart.
-      const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(s_.batch_window_us);
-      size_t nd = 0, nb = 0;
-      int64_t tmin = 0, tmax = 0;
-      for (;;) {
-        while (!q_.empty()) {
-          auto& c = q_.front();
-          const size_t d = c->prefix.size();
-          if (!batch.empty()) {
-            const int64_t lo = c->now < tmin ? c->now : tmin, hi = c->now > tmax ? c->now : tmax;
-            if (nd + d > s_.batch_limit || nd + d > cap_desc || nb + c->blob_bytes > cap_blob || hi - lo >= 2)
-              goto full;
-          }
-          if (batch.empty()) tmin = tmax = c->now;
-          tmin = c->now < tmin ? c->now : tmin;
-          tmax = c->now > tmax ? c->now : tmax;
-          nd += d;
-          nb += c->blob_bytes;
-          batch.push_back(c);
-          q_.pop_front();
-        }
-        if (stop_ || nd >= s_.batch_limit) break;
-        if (cv_.wait_until(g, deadline) == std::cv_status::timeout && q_.empty()) break;
-        if (std::chrono::steady_clock::now() >= deadline) break;
-      }
-    full:
-      inflight_ += batch.size();
-    }
-    run_batch(batch);
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      inflight_ -= batch.size();
-    }
-    idle_cv_.notify_all();
-  }
+// The batch being built in one of the engine's pinned staging slots (rl_host_acquire): calls
+// are written straight into C memory, the way the Go batcher does.
+struct HipRateLimitCache::Staged {
+  std::vector<std::shared_ptr<Call>> calls;
+  rl_host_batch hb{};
+  uint32_t nd = 0, nr = 0, nb = 0;
+  int64_t tmin = 0, tmax = 0;
+  bool failed = false;  // refused at submit: its callers already have the error
+};
+
+bool HipRateLimitCache::fits(const Staged& st, const Call& c) const {
+  if (st.calls.empty()) return true;
+  const int64_t lo = c.now < st.tmin ? c.now : st.tmin, hi = c.now > st.tmax ? c.now : st.tmax;
+  // A batch may straddle at most one window boundary of a unit (rl_submit refuses a SECOND key
+  // spanning three windows), so it is cut before a request 2 s or more from the others; and
+  // before one the slot cannot hold, or past HIP_BATCH_LIMIT descriptors.
+  return hi - lo < 2 && st.nd + c.prefix.size() <= s_.batch_limit && st.nd + c.prefix.size() <= st.hb.max_desc &&
+         st.nr + 1 <= st.hb.max_req && st.nb + c.blob_bytes <= st.hb.max_blob;
 }
 
-void HipRateLimitCache::run_batch(std::vector<std::shared_ptr<Call>>& calls) {
-  std::vector<uint8_t> blob;
-  std::vector<uint32_t> off{0}, rule, req_of, hits;
-  std::vector<int64_t> now;
-  for (size_t r = 0; r < calls.size(); ++r) {
-    Call& c = *calls[r];
-    now.push_back(c.now);
-    hits.push_back(c.hits);
-    for (size_t i = 0; i < c.prefix.size(); ++i) {
-      const auto& lim = (*c.limits)[i];
-      blob.insert(blob.end(), c.prefix[i].begin(), c.prefix[i].end());
-      off.push_back((uint32_t)blob.size());
-      rule.push_back(lim ? rule_id(lim->Limit, lim->ShadowMode) : RL_NIL_RULE);
-      req_of.push_back((uint32_t)r);
-    }
+// One request into the slot: GenerateCacheKey's bytes before the timestamp per descriptor with
+// a limit (cache_key.go:57-65), the rule id, the request index; now and the raw HitsAddend.
+void HipRateLimitCache::add(Staged& st, const std::shared_ptr<Call>& cp) {
+  Call& c = *cp;
+  if (st.calls.empty()) st.tmin = st.tmax = c.now;
+  st.tmin = c.now < st.tmin ? c.now : st.tmin;
+  st.tmax = c.now > st.tmax ? c.now : st.tmax;
+  const uint32_t r = st.nr++;
+  st.hb.now[r] = c.now;
+  st.hb.hits_addend[r] = c.req->HitsAddend;
+  st.hb.prefix_off[0] = 0;
+  for (size_t i = 0; i < c.prefix.size(); ++i) {
+    const auto& lim = (*c.limits)[i];
+    memcpy(st.hb.prefix_blob + st.nb, c.prefix[i].data(), c.prefix[i].size());
+    st.nb += (uint32_t)c.prefix[i].size();
+    st.hb.rule_id[st.nd] = lim ? rule_id(lim->Limit, lim->ShadowMode) : RL_NIL_RULE;
+    st.hb.req_of[st.nd] = r;
+    ++st.nd;
+    st.hb.prefix_off[st.nd] = st.nb;
   }
-  std::vector<rl_status> st(rule.size());
-  std::vector<uint32_t> thr(calls.size());
+  st.calls.push_back(cp);
+}
+
+void HipRateLimitCache::fail(std::vector<std::shared_ptr<Call>>& calls) {
+  // checkError -> panic(RedisError(...))  src/redis/driver_impl.go:50-54
+  const std::string msg = std::string("hip backend: ") + rl_last_error(eng_);
+  for (auto& c : calls) c->done.set_exception(std::make_exception_ptr(RedisError(msg)));
+  done_calls(calls.size());
+  calls.clear();
+}
+
+void HipRateLimitCache::done_calls(size_t n) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    inflight_ -= n;
+  }
+  idle_cv_.notify_all();
+}
+
+// Hand the slot's batch to the engine. New (L, unit) rules are appended to the device table
+// first: that is allowed while the previous batch is in flight (rule ids keep their meaning,
+// rl_hip.h rl_load_rules), and a refusal fails this batch's calls, keeping the table dirty.
+void HipRateLimitCache::submit(Staged& st) {
   int rc = 0;
   if (rules_dirty_) {
     rc = rl_load_rules(eng_, rules_.data(), (uint32_t)rules_.size());
-    rules_dirty_ = rc != 0;
+    if (!rc) {
+      rules_dirty_ = false;
+      n_loads_ += 1;
+      if (n_inflight_batches_) n_loads_inflight_ += 1;
+    }
   }
   if (!rc) {
     rl_batch b;
     memset(&b, 0, sizeof b);
-    b.n_desc = (uint32_t)rule.size();
-    b.n_req = (uint32_t)calls.size();
-    b.blob_bytes = (uint32_t)blob.size();
-    b.prefix_blob = blob.data();
-    b.prefix_off = off.data();
-    b.rule_id = rule.data();
-    b.req_of = req_of.data();
-    b.now = now.data();
-    b.hits_addend = hits.data();
-    rc = rl_submit(eng_, &b, st.data(), thr.data());
-    if (!rc) rc = rl_wait(eng_);
+    b.n_desc = st.nd;
+    b.n_req = st.nr;
+    b.blob_bytes = st.nb;
+    b.prefix_blob = st.hb.prefix_blob;  // the slot's own arrays: rl_submit does not copy them
+    b.prefix_off = st.hb.prefix_off;
+    b.rule_id = st.hb.rule_id;
+    b.req_of = st.hb.req_of;
+    b.now = st.hb.now;
+    b.hits_addend = st.hb.hits_addend;
+    rc = rl_submit(eng_, &b, nullptr, nullptr);  // results stay in the engine until rl_wait_into
+    if (!rc) n_batches_ += 1;
   }
   if (rc) {
-    // checkError -> panic(RedisError(...))  src/redis/driver_impl.go:50-54
-    const std::string msg = std::string("hip backend: ") + rl_last_error(eng_);
-    for (auto& c : calls) c->done.set_exception(std::make_exception_ptr(RedisError(msg)));
+    fail(st.calls);
+    st.failed = true;
+  }
+}
+
+// Collect the oldest batch in flight: rl_wait_into copies its results out during the call.
+void HipRateLimitCache::finish(Staged& st) {
+  if (st.failed) return;
+  std::vector<rl_status> out(st.nd);
+  std::vector<uint32_t> thr(st.nr);
+  if (rl_wait_into(eng_, out.data(), thr.data())) {
+    fail(st.calls);
     return;
   }
   size_t d = 0;
-  for (size_t r = 0; r < calls.size(); ++r) {
-    Call& c = *calls[r];
+  for (size_t r = 0; r < st.calls.size(); ++r) {
+    Call& c = *st.calls[r];
     c.resp.DescriptorStatuses.resize(c.prefix.size());
     c.resp.ThrottleMillis = thr[r];
     for (size_t i = 0; i < c.prefix.size(); ++i, ++d) {
       const auto& lim = (*c.limits)[i];
-      const rl_status& s = st[d];
+      const rl_status& s = out[d];
       DescriptorStatus& o = c.resp.DescriptorStatuses[i];
       o.code = (Code)(s.code_flags & 0xFF);
       o.LimitRemaining = s.limit_remaining;
@@ -250,6 +262,76 @@ void HipRateLimitCache::run_batch(std::vector<std::shared_ptr<Call>>& calls) {
     }
     c.done.set_value();
   }
+  done_calls(st.calls.size());
+}
+
+// The submitter thread owns the engine (rl_hip.h: one thread per engine) and keeps two batches
+// in flight, as the Go batcher does: batch k+1 is gathered, built in its
+// pinned slot and submitted (its H2D copy and fingerprint overlap batch k's kernels) before
+// batch k's results are collected; with nothing queued it finishes what is in flight instead
+// of waiting. Gathering lasts up to batch_window_us (implicit pipelining analogue,
+// src/redis/driver_impl.go:84-89).
+void HipRateLimitCache::submitter() {
+  std::deque<Staged> inflight;
+  std::shared_ptr<Call> carry;
+  for (;;) {
+    std::shared_ptr<Call> first = std::move(carry);
+    carry.reset();
+    if (!first) {
+      std::unique_lock<std::mutex> g(mu_);
+      if (!inflight.empty() && q_.empty()) {
+        g.unlock();
+        finish(inflight.front());
+        inflight.pop_front();
+        n_inflight_batches_ = inflight.size();
+        continue;
+      }
+      cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+      if (q_.empty()) break;  // stopping
+      first = q_.front();
+      q_.pop_front();
+    }
+    Staged st;
+    if (rl_host_acquire(eng_, &st.hb)) {
+      std::vector<std::shared_ptr<Call>> one{first};
+      fail(one);
+      continue;
+    }
+    if (first->prefix.size() > st.hb.max_desc || first->blob_bytes > st.hb.max_blob) {
+      first->done.set_exception(std::make_exception_ptr(RedisError("hip backend: request larger than a batch")));
+      done_calls(1);
+      continue;
+    }
+    add(st, first);
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(s_.batch_window_us);
+      for (;;) {
+        while (!q_.empty()) {
+          std::shared_ptr<Call> c = q_.front();
+          q_.pop_front();
+          if (!fits(st, *c)) {
+            carry = std::move(c);  // starts the next batch
+            goto full;
+          }
+          add(st, c);
+        }
+        if (stop_ || st.nd >= s_.batch_limit) break;
+        if (cv_.wait_until(g, deadline) == std::cv_status::timeout && q_.empty()) break;
+        if (std::chrono::steady_clock::now() >= deadline) break;
+      }
+    full:;
+    }
+    submit(st);
+    inflight.push_back(std::move(st));
+    n_inflight_batches_ = inflight.size();
+    if (inflight.size() == 2) {
+      finish(inflight.front());
+      inflight.pop_front();
+    }
+    n_inflight_batches_ = inflight.size();
+  }
+  for (auto& st : inflight) finish(st);
 }
 
 }  // namespace ratelimit

@@ -161,11 +161,24 @@ class HipRateLimitCache : public RateLimitCache {
   // waits until every enqueued call has been decided.
   void Flush() override;
 
+  // Batcher counters (tests): batches submitted, rule-table loads, and loads made while an
+  // earlier batch was still in flight (append-only rule table, rl_hip.h rl_load_rules).
+  struct BatcherStats {
+    uint64_t batches, rule_loads, rule_loads_in_flight;
+  };
+  BatcherStats batcher_stats() const { return {n_batches_.load(), n_loads_.load(), n_loads_inflight_.load()}; }
+
  private:
   struct Call;
+  struct Staged;
   void submitter();
   uint32_t rule_id(const RateLimitLimit& l, bool shadow);
-  void run_batch(std::vector<std::shared_ptr<Call>>& calls);
+  bool fits(const Staged& st, const Call& c) const;
+  void add(Staged& st, const std::shared_ptr<Call>& c);
+  void submit(Staged& st);
+  void finish(Staged& st);
+  void fail(std::vector<std::shared_ptr<Call>>& calls);
+  void done_calls(size_t n);
 
   HipSettings s_;
   std::shared_ptr<TimeSource> ts_;
@@ -173,13 +186,16 @@ class HipRateLimitCache : public RateLimitCache {
   std::mutex mu_;
   std::condition_variable cv_, idle_cv_;
   std::deque<std::shared_ptr<Call>> q_;
-  size_t inflight_ = 0;
+  size_t inflight_ = 0;  // calls enqueued and not yet answered
   bool stop_ = false;
   std::thread thr_;
-  // rule registry (submitter thread only)
+  // rule registry (submitter thread only): append-only, so ids keep their meaning while
+  // batches that use them are in flight
   std::map<std::pair<uint32_t, uint32_t>, uint32_t> rule_ids_;
   std::vector<rl_rule> rules_;
   bool rules_dirty_ = false;
+  size_t n_inflight_batches_ = 0;  // submitter thread only
+  std::atomic<uint64_t> n_batches_{0}, n_loads_{0}, n_loads_inflight_{0};
 };
 
 }  // namespace ratelimit

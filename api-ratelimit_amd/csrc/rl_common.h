@@ -281,12 +281,25 @@ struct RReply {
   uint32_t thr;
 };
 static_assert(sizeof(RReply) == 24, "RReply is 6 words");
+// Raw reply of an owner to an origin (8 B, the combining router): the INCRBY
+// post-value the record's key saw (Redis' reply to the record's INCRBY, uint32 as
+// fixed_cache_impl.go:51 decodes it) or a local-cache hit; the origin makes the decisions.
+struct RawReply {
+  uint32_t after;
+  uint32_t flags;  // RAW_*
+};
+constexpr uint32_t RAW_LOCAL_HIT = 1u;  // the key was in the local over-limit cache: no INCRBY
+constexpr uint32_t RAW_NIL = 2u;        // a record without a limit (never sent by rl_route_pack)
+// How a pipeline writes its decisions: per descriptor statuses (+ ThrottleMillis per request),
+// routed statuses (+ ThrottleMillis per record), or raw replies (RawReply per record).
+constexpr int OUT_STATUS = 0, OUT_ROUTED = 1, OUT_RAW = 2;
 constexpr int ROUTE_REQ_BITS = 27;
 constexpr uint32_t ROUTE_MAX_SHARDS = 16;
 constexpr uint8_t ROUTE_LOCAL = 0xFF;  // descriptor decided at the origin (nil limit)
 // rl_batch.reserved bit: prefix_blob holds RRec records (rl_submit_routed), n_req = n_desc and
 // every record has its own ThrottleMillis slot.
 constexpr uint32_t RL_BATCH_ROUTED = 1u;
+constexpr uint32_t RL_BATCH_RAW = 2u;  // with RL_BATCH_ROUTED: raw replies (RawReply) instead of statuses
 
 // MSD descriptor record (32 B): tile-sorted (k4_hist) and in bucket order (k4_place,
 // grouped by k4_group). A hot record carries its in-tile INCRBY prefix in `key` and its hot

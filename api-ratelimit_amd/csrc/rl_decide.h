@@ -356,23 +356,23 @@ RL_DEV void leader_segment(uint32_t hp, uint32_t j, const SortedRec& tail, bool 
 // GetResponseDescriptorStatus + checkOverLimitThreshold + checkNearLimitThreshold +
 // CalculateReset (base_limiter.go:70-195, utilities.go:34-38) for one descriptor.
 // thr_idx: the ThrottleMillis slot (the request index; a routed record's own position).
-RL_DEV void decide_one(const SortedRec& r, const SegInfo& si, const DevRule& R, rl_status* __restrict__ out,
-                       uint32_t* __restrict__ req_thr, uint32_t thr_idx) {
-  const uint32_t h = r.h;
-  const uint32_t reset = R.div - (uint32_t)r.now_mod;  // div - now % div
-  rl_status st;
+// A raw reply (OUT_RAW): the post-value or the local-cache hit, for the origin to decide.
+RL_DEV void emit_raw(rl_status* __restrict__ out, uint32_t idx, uint32_t after, uint32_t flags) {
+  RawReply r;
+  r.after = after;
+  r.flags = flags;
+  reinterpret_cast<RawReply*>(out)[idx] = r;
+}
+
+// The decision from the INCRBY reply (after) or a local-cache hit: GetResponseDescriptorStatus
+// + checkOverLimitThreshold + checkNearLimitThreshold + CalculateReset (base_limiter.go:70-195,
+// utilities.go:34-38). Returns the ThrottleMillis contribution (0 = none).
+RL_DEV uint32_t decide_status(uint32_t after, bool local_hit, uint32_t h, uint32_t now_mod, const DevRule& R,
+                              rl_status& st) {
+  const uint32_t reset = R.div - now_mod;  // div - now % div
   st.reset_s = reset;
   st.over_limit_delta = 0;
   st.near_limit_delta = 0;
-  bool local_hit;
-  uint32_t after;
-  if (si.freeze == SEG_EXOTIC) {
-    local_hit = (r.P & P_LOCAL_HIT) != 0;
-    after = (uint32_t)r.P;
-  } else {
-    local_hit = si.freeze == SEG_FROZEN_BEFORE || (si.freeze != SEG_NO_FREEZE && r.req > si.freeze);
-    after = (uint32_t)(si.base + r.P);
-  }
   uint32_t throttle = 0;
   if (local_hit) {
     st.code_flags = RL_CODE_OVER_LIMIT | ((RL_FLAG_HAS_LIMIT | RL_FLAG_LOCAL_CACHE_HIT) << 8);
@@ -402,15 +402,38 @@ RL_DEV void decide_one(const SortedRec& r, const SegInfo& si, const DevRule& R, 
     }
   }
   st.code_flags = shadow_code(st.code_flags, R.shadow);
+  return throttle;
+}
+
+// One descriptor of a segment: its post-value from the segment's state, then the decision
+// (or the raw reply). thr_idx: the ThrottleMillis slot (the request; a routed record's own
+// position).
+RL_DEV void decide_one(const SortedRec& r, const SegInfo& si, const DevRule& R, rl_status* __restrict__ out,
+                       uint32_t* __restrict__ req_thr, uint32_t thr_idx, int mode) {
+  bool local_hit;
+  uint32_t after;
+  if (si.freeze == SEG_EXOTIC) {
+    local_hit = (r.P & P_LOCAL_HIT) != 0;
+    after = (uint32_t)r.P;
+  } else {
+    local_hit = si.freeze == SEG_FROZEN_BEFORE || (si.freeze != SEG_NO_FREEZE && r.req > si.freeze);
+    after = (uint32_t)(si.base + r.P);
+  }
+  if (mode == OUT_RAW) {
+    emit_raw(out, r.idx, local_hit ? 0u : after, local_hit ? RAW_LOCAL_HIT : 0u);
+    return;
+  }
+  rl_status st;
+  const uint32_t throttle = decide_status(after, local_hit, r.h, (uint32_t)r.now_mod, R, st);
   out[r.idx] = st;
   if (throttle) atomicMax(&req_thr[thr_idx], throttle);
 }
 
 RL_DEV void decide_pos(uint32_t j, const SortedRec* __restrict__ srec, const SegInfo* __restrict__ seg,
                        const DevRule* __restrict__ rules, rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
-                       int routed) {
+                       int mode) {
   const SortedRec r = srec[j];
-  decide_one(r, seg[r.head & ~HEAD_MIXED_RULE], rules[r.rule], out, req_thr, routed ? r.idx : r.req);
+  decide_one(r, seg[r.head & ~HEAD_MIXED_RULE], rules[r.rule], out, req_thr, mode != OUT_STATUS ? r.idx : r.req, mode);
 }
 
 }  // namespace rlhip

@@ -165,6 +165,15 @@ RL_DEV uint32_t wave_sum_u32(uint32_t v) {
   v += dpp_mov<0x143, 0xC, false>(v);
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
+RL_DEV uint32_t wave_or_u32(uint32_t v) {
+  v |= dpp_mov<0xB1>(v);
+  v |= dpp_mov<0x4E>(v);
+  v |= dpp_mov<0x114>(v);
+  v |= dpp_mov<0x118>(v);
+  v |= dpp_mov<0x142, 0xA, false>(v);
+  v |= dpp_mov<0x143, 0xC, false>(v);
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
 // Inclusive scan: row_shr 1, 2, 4, 8 inside each row of 16, then the row carries.
 RL_DEV uint32_t wave_incl_scan_u32(uint32_t v) {
   v += dpp_mov<0x111>(v);

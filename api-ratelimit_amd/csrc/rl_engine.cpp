@@ -19,6 +19,7 @@
 
 #include "rl_common.h"
 #include "rl_hip.h"
+#include "rl_internal.h"
 #include "rl_resolve.h"
 
 namespace rlhip {
@@ -87,12 +88,6 @@ const char* const kKernelNames[KT_COUNT] = {"k_fingerprint", "k_histogram", "k_h
 
 enum Mode { MODE_LSD = 1, MODE_LSD_FULL = 2, MODE_V4 = 4 };
 
-// Hot-key set kept on the host between batches.
-struct HotKey {
-  uint64_t a, b;
-  uint32_t unit, rule, count;
-};
-
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // Wait for an event by polling. A blocking wait wakes the submitter thread ≈20 µs after the
@@ -135,6 +130,7 @@ struct rl_engine {
   // rules
   DevRule* d_rules = nullptr;
   uint32_t n_rules = 0, rules_cap = 0;
+  std::vector<DevRule> h_rules;      // what d_rules[0, n_rules) holds
 
   // host staging (rl_submit): per host slot one pinned input region with the device layout,
   // its device twin, device outputs and pinned outputs
@@ -348,7 +344,8 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   uint64_t* lb_sum = reinterpret_cast<uint64_t*>(zero_block + z.lb_sum);
   uint64_t* lb_head = reinterpret_cast<uint64_t*>(zero_block + z.lb_head);
   const size_t lb_pass_stride = (size_t)sort_tiles(n > 0 ? n : 1) * RADIX;  // per-digit look-back words
-  const int routed = (b.reserved & RL_BATCH_ROUTED) ? 1 : 0;
+  // how decisions are written (rl_common.h OUT_*): statuses, routed statuses, raw replies
+  const int routed = (b.reserved & RL_BATCH_ROUTED) ? ((b.reserved & RL_BATCH_RAW) ? OUT_RAW : OUT_ROUTED) : OUT_STATUS;
   hipError_t e;
   if (mode == MODE_V4) {
     const uint32_t sl = (uint32_t)(sub_seq & 1u);
@@ -372,7 +369,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
       hipStreamWaitEvent(stream, in_ev, 0);
     }
     if (n == 0) {
-      hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
+      if (thr && b.n_req) hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
       hipMemsetAsync(c4, 0, sizeof(EngineCtl), stream);
       hipMemsetAsync(c4n, 0, sizeof(EngineCtl), stream);
       e = hipMemcpyAsync(h_ctl, c4, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
@@ -417,7 +414,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   timed(KT_MEMSET, [&] {
     hipMemsetAsync(zero_block, 0, z.total, stream);
     // request throttles are zeroed by k_fingerprint; only an empty batch needs a memset
-    if (b.n_req && n == 0) hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
+    if (thr && b.n_req && n == 0) hipMemsetAsync(thr, 0, (size_t)b.n_req * 4, stream);
   });
   if (n == 0) {
     e = hipMemcpyAsync(h_ctl, ctl, sizeof(EngineCtl), hipMemcpyDeviceToHost, stream);
@@ -509,29 +506,8 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
 // Upload the hot-key set: open-addressed tag words (rl_common.h HOT_TAGS; home = hot_home(a),
 // word = hot_tag(a) | index + 1) followed by the entries in hot-index order.
 int rl_engine::upload_hot(hipStream_t us) {
-  std::vector<HotEntry> t(HOT_SLOTS + HOT_MAX);
-  for (auto& x : t) {
-    x.a = x.b = 0;
-    x.unit = x.rule = 0;
-    x.idx = 0xFFFFFFFFu;
-    x.pad = 0;
-  }
-  std::vector<uint32_t> tags(HOT_TAGS, 0u);
-  static_assert(HOT_MAX < 512 && (size_t)HOT_TAGS * 4 == HOT_SLOTS * sizeof(HotEntry), "hot tag words");
-  for (size_t i = 0; i < hot.size(); ++i) {
-    HotEntry he;
-    he.a = hot[i].a;
-    he.b = hot[i].b;
-    he.unit = hot[i].unit;
-    he.rule = hot[i].rule;
-    he.idx = (uint32_t)i;
-    he.pad = 0;
-    uint32_t s = hot_home(he.a);
-    while (tags[s]) s = (s + 1) & (HOT_TAGS - 1);
-    tags[s] = hot_tag(he.a) | (uint32_t)(i + 1);
-    t[HOT_SLOTS + i] = he;
-  }
-  memcpy(t.data(), tags.data(), (size_t)HOT_TAGS * 4);
+  std::vector<HotEntry> t;
+  build_hot_table(hot, t);
   // Into the version no in-flight batch reads, through a pinned staging buffer whose last
   // copy is done.
   hipError_t e = hipEventSynchronize(ev_hot);
@@ -816,6 +792,24 @@ int rl_engine::submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, R
   return 0;
 }
 
+namespace rlhip {
+int rlx_engine_view(rl_engine* e, EngineView* v) {
+  if (!e || !v) return RL_EINVAL;
+  if (!e->d_rules) {
+    int rc = rl_load_rules(e, nullptr, 0);
+    if (rc) return rc;
+  }
+  v->rules = e->d_rules;
+  v->n_rules = e->n_rules;
+  v->seed = e->cfg.hash_seed;
+  v->local_cache = e->cfg.local_cache ? 1 : 0;
+  v->device = e->cfg.device;
+  v->max_batch_desc = e->cfg.max_batch_desc;
+  return 0;
+}
+void rlx_engine_hot(rl_engine* e, std::vector<HotKey>& out) { out = e->hot; }
+}  // namespace rlhip
+
 extern "C" {
 
 uint32_t rl_abi_version(void) { return RL_ABI_VERSION; }
@@ -1011,7 +1005,7 @@ void rl_destroy(rl_engine* e) {
 
 int rl_load_rules(rl_engine* e, const rl_rule* rules, uint32_t n) {
   if (!e) return RL_EINVAL;
-  if (e->n_fl) return e->fail(RL_ESTATE, "rl_load_rules while a batch is in flight");
+  if (n && !rules) return e->fail(RL_EINVAL, "null rule array");
   std::vector<DevRule> h(n);
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t u = rules[i].unit & ~RL_RULE_SHADOW;
@@ -1027,18 +1021,44 @@ int rl_load_rules(rl_engine* e, const rl_rule* rules, uint32_t n) {
     h[i].div = unit_div(u);
     h[i].unit = u;
   }
+  // Rule ids never change meaning while batches are in flight: a batch reads rules by id (its
+  // launch validated ids against the n_rules of that moment), so a table that keeps the loaded
+  // prefix and appends rules can be loaded at any time — the micro-batcher registers the
+  // (L, unit) of a new config.RateLimit, e.g. a descriptor.Limit override
+  // (config_impl.go:281-289), while earlier batches are still being decided. Only the appended
+  // entries are copied, into slots no in-flight batch reads, with a blocking copy that is
+  // complete before any later launch. A table that changes or drops a loaded rule, or that
+  // must grow the device allocation, needs nothing in flight.
+  const uint32_t n_old = e->n_rules;
+  if (e->n_fl) {
+    bool prefix = n >= n_old;
+    for (uint32_t i = 0; prefix && i < n_old; ++i) prefix = memcmp(&h[i], &e->h_rules[i], sizeof(DevRule)) == 0;
+    if (!prefix)
+      return e->fail(RL_ESTATE, "rl_load_rules while a batch is in flight may only append rules (ids keep their meaning)");
+    if (n > e->rules_cap || (n > V4_MAX_RULES) != (n_old > V4_MAX_RULES))
+      return e->fail(RL_ESTATE, "rl_load_rules: %u rules need a larger table; call rl_wait until nothing is in flight", n);
+  }
+  const uint32_t first = e->n_fl ? n_old : 0u;  // entries to copy
   if (n > e->rules_cap || !e->d_rules) {
     hipFree(e->d_rules);
     e->d_rules = nullptr;
-    const uint32_t cap = n < 16 ? 16 : n;
+    // room for the v4 pipeline's whole rule-id space, so appends never reallocate
+    const uint32_t cap = n < V4_MAX_RULES ? V4_MAX_RULES : n;
     hipError_t he = hipMalloc(&e->d_rules, (size_t)cap * sizeof(DevRule));
-    if (he != hipSuccess) return e->hip_fail(he, "hipMalloc(rules)");
+    if (he != hipSuccess) {
+      e->rules_cap = 0;
+      e->n_rules = 0;
+      e->h_rules.clear();
+      return e->hip_fail(he, "hipMalloc(rules)");
+    }
     e->rules_cap = cap;
   }
-  if (n) {
-    hipError_t he = hipMemcpy(e->d_rules, h.data(), (size_t)n * sizeof(DevRule), hipMemcpyHostToDevice);
+  if (n > first) {
+    hipError_t he = hipMemcpy(e->d_rules + first, h.data() + first, (size_t)(n - first) * sizeof(DevRule),
+                              hipMemcpyHostToDevice);
     if (he != hipSuccess) return e->hip_fail(he, "hipMemcpy(rules)");
   }
+  e->h_rules = std::move(h);
   e->n_rules = n;
   return 0;
 }
@@ -1249,6 +1269,36 @@ int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_re
   b.prefix_blob = reinterpret_cast<const uint8_t*>(d_records);
   return e->submit_common(b, e->r_out, e->r_thr, reinterpret_cast<RReply*>(d_reply), nullptr, false, false, nullptr,
                           nullptr);
+}
+
+int rl_submit_routed_async(rl_engine* e, const void* d_records, uint32_t n, void* d_reply, uint32_t flags,
+                           void* ready_event) {
+  if (!e) return RL_EINVAL;
+  if (flags & ~RL_ROUTED_RAW) return e->fail(RL_EINVAL, "unknown rl_submit_routed_async flags 0x%x", flags);
+  if (!(flags & RL_ROUTED_RAW)) {
+    if (ready_event) return e->fail(RL_EINVAL, "rl_submit_routed_async: status replies need ready_event == NULL");
+    return rl_submit_routed(e, d_records, n, d_reply);
+  }
+  if (e->n_fl >= HSLOTS)
+    return e->fail(RL_ESTATE, "rl_submit_routed_async with %d batches in flight (call rl_wait)", HSLOTS);
+  if (e->n_fl && e->default_mode() != MODE_V4)
+    return e->fail(RL_ESTATE, "a second batch in flight needs the v4 pipeline (call rl_wait)");
+  if (n > e->cfg.max_batch_desc)
+    return e->fail(RL_ECAPACITY, "routed batch of %u records exceeds engine capacity (%u desc)", n,
+                   e->cfg.max_batch_desc);
+  if (n && (!d_records || !d_reply)) return e->fail(RL_EINVAL, "null routed buffer");
+  for (int q = 0; q < e->n_fl; ++q)
+    if (e->fl[q].out == reinterpret_cast<rl_status*>(d_reply))
+      return e->fail(RL_EINVAL, "batches in flight together need distinct reply buffers");
+  if (!e->d_rules) rl_load_rules(e, nullptr, 0);
+  rl_batch b{};
+  b.n_desc = n;
+  b.n_req = n;
+  b.reserved = RL_BATCH_ROUTED | RL_BATCH_RAW;
+  b.prefix_blob = reinterpret_cast<const uint8_t*>(d_records);
+  // the replies are the pipeline's output array (RawReply per record); no ThrottleMillis slots
+  return e->submit_common(b, reinterpret_cast<rl_status*>(d_reply), nullptr, nullptr,
+                          reinterpret_cast<hipEvent_t>(ready_event), false, false, nullptr, nullptr);
 }
 
 int rl_route_unpack(rl_engine* e, const rl_batch* b, const uint32_t* d_perm, const void* d_reply, rl_status* d_out,

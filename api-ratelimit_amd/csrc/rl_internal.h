@@ -1,0 +1,86 @@
+// rl_internal.h — host-side pieces shared by the engine (rl_engine.cpp) and the router
+// (rl_router.cpp) inside libratelimit_hip.so; not part of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "rl_common.h"
+#include "rl_hip.h"
+
+namespace rlhip {
+
+// A hot key prefix (host side): fingerprint lanes after the prefix bytes, its unit and rule,
+// and how many descriptors carried it in the batch it was counted on.
+struct HotKey {
+  uint64_t a, b;
+  uint32_t unit, rule, count;
+};
+
+// The device hot-set table (rl_common.h HOT_TAGS): open-addressed tag words (home =
+// hot_home(a), word = hot_tag(a) | index + 1) followed by the entries in index order.
+inline void build_hot_table(const std::vector<HotKey>& hot, std::vector<HotEntry>& t) {
+  t.assign(HOT_SLOTS + HOT_MAX, HotEntry{});
+  for (auto& x : t) x.idx = 0xFFFFFFFFu;
+  std::vector<uint32_t> tags(HOT_TAGS, 0u);
+  static_assert(HOT_MAX < 512 && (size_t)HOT_TAGS * 4 == HOT_SLOTS * sizeof(HotEntry), "hot tag words");
+  for (size_t i = 0; i < hot.size() && i < (size_t)HOT_MAX; ++i) {
+    HotEntry he{};
+    he.a = hot[i].a;
+    he.b = hot[i].b;
+    he.unit = hot[i].unit;
+    he.rule = hot[i].rule;
+    he.idx = (uint32_t)i;
+    uint32_t s = hot_home(he.a);
+    while (tags[s]) s = (s + 1) & (HOT_TAGS - 1);
+    tags[s] = hot_tag(he.a) | (uint32_t)(i + 1);
+    t[HOT_SLOTS + i] = he;
+  }
+  memcpy(t.data(), tags.data(), (size_t)HOT_TAGS * 4);
+}
+
+// What the router needs from an engine (rl_engine.cpp).
+struct EngineView {
+  const DevRule* rules;
+  uint32_t n_rules;
+  uint64_t seed;
+  int local_cache;
+  int device;
+  uint32_t max_batch_desc;
+};
+int rlx_engine_view(rl_engine* e, EngineView* v);
+// The engine's current hot set (keys it owns that arrive with many descriptors per batch).
+void rlx_engine_hot(rl_engine* e, std::vector<HotKey>& out);
+
+// ---- combining route kernels (rl_route.hip) ----------------------------------------------
+// Per origin batch of a routed step: records grouped by owner in a strided send buffer
+// (owner j at [j * stride, ...)), cold descriptors one record each in arrival order, then one
+// combined record per hot prefix group (the hot set's prefixes, when combining is on and the
+// batch's hot descriptors share one request time); per owner (count, status) pairs in x.
+struct RoutePackBufs {
+  RRec* send;          // n_shards * stride records
+  uint32_t* perm;      // per descriptor: record position | PERM_HOT group code | RL_ROUTE_LOCAL
+  uint32_t* x;         // [2 * n_shards]: (count, status) per owner
+  uint32_t* lb;        // look-back words + error word, two areas (pack, repack), zeroed by the caller
+  uint32_t* bhs;       // [blocks][HOT_MAX] hot h sums per block -> exclusive prefixes over blocks
+  uint32_t* bstat;     // [blocks][4] per block: ~min now, max now, flags of its hot descriptors
+  uint32_t* rctl;      // [16] step words: [0] repack (combining refused), [1] combined records, [2] done ctr
+  uint32_t* hot_pos;   // [HOT_MAX] record position of each hot group's combined record
+  uint32_t* hot_tot;   // [HOT_MAX] its sum of hits_addend
+};
+uint32_t route2_blocks(uint32_t n);
+size_t route2_lb_words(uint32_t n);     // one area
+size_t route2_bhs_words(uint32_t n);
+// hot == nullptr: no combining
+void launch_route_pack2(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
+                        uint32_t origin, uint32_t n_shards, uint32_t stride, const HotEntry* hot,
+                        const RoutePackBufs& o);
+// Origin: raw replies (back, strided like send) -> statuses and ThrottleMillis (the decisions).
+void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* rules, const RoutePackBufs& o,
+                             const RawReply* back, rl_status* out, uint32_t* thr);
+constexpr uint32_t ROUTE2_BLOCK = 1024;  // descriptors per pack block
+constexpr uint32_t PERM_HOT = 0x80000000u;
+constexpr int PERM_HOT_PRE_BITS = 22;
+
+}  // namespace rlhip

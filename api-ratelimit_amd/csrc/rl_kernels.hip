@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
   if (i < in.n_desc && in.recs) {
     // Routed record (multi-GPU owner): the key prefix arrives as its fingerprint lane state.
     const RRec x = in.recs[i];
-    req_thr[i] = 0;  // one ThrottleMillis slot per record
+    if (req_thr) req_thr[i] = 0;  // one ThrottleMillis slot per record (none for raw replies)
     ItemRec rec;
     rec.rule = x.rule;
     rec.req = x.greq;

@@ -182,7 +182,8 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   {
     const uint32_t per = (in.n_req + ntiles - 1) / ntiles;
     const uint32_t r0 = tile * per, r1 = min(in.n_req, r0 + per);
-    for (uint32_t q = r0 + tid; q < r1; q += NT) req_thr[q] = 0;
+    if (req_thr)  // (raw replies: no ThrottleMillis slots)
+      for (uint32_t q = r0 + tid; q < r1; q += NT) req_thr[q] = 0;
   }
   __syncthreads();
   STH(1);
@@ -334,6 +335,10 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
     const D3& x = d[r];
     if (x.bucket == BKT_NONE) continue;
     if (x.bucket == NIL_BUCKET) {
+      if (ROUTED && !req_thr) {  // raw replies (a routed batch never carries a nil limit)
+        emit_raw(out, i, 0u, RAW_NIL);
+        continue;
+      }
       // GetResponseDescriptorStatus("" key) -> {OK, nil limit, 0}  base_limiter.go:72-75
       rl_status st;
       st.code_flags = RL_CODE_OK;
@@ -1210,7 +1215,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
     const HotBucket& hx = hb[b];
     const DevRule& rl = rules[rule];
     if (hx.flags & HB_FROZEN_PRE) {
-      out[i] = tile::local_hit_status(a.h, rl.div - now_mod, rl.shadow);  // every descriptor is a local-cache hit
+      tile::emit_local_hit(out, i, a.h, rl.div - now_mod, rl.shadow, routed);  // every descriptor is a local-cache hit
       continue;
     }
     const uint64_t after = hx.base + P;
@@ -1222,13 +1227,13 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
     const uint32_t rs = s_rstar[b];
     if (rs != 0xFFFFFFFFu) {  // the freezing descriptor is in this tile, at or before this one
       if (a.req > rs) {
-        out[i] = tile::local_hit_status(a.h, rl.div - now_mod, rl.shadow);
+        tile::emit_local_hit(out, i, a.h, rl.div - now_mod, rl.shadow, routed);
       } else {  // same request as the freezing descriptor: its INCRBY still happens
         tile::decide_at(i, a.req, rule, a.h, now_mod, hx.base, P, SEG_NO_FREEZE, rules, out, req_thr, routed);
         atomicMax(hot_counter(hx), (uint32_t)after);
       }
     } else if (a.req > q0) {  // froze in an earlier tile, in a request <= q0
-      out[i] = tile::local_hit_status(a.h, rl.div - now_mod, rl.shadow);
+      tile::emit_local_hit(out, i, a.h, rl.div - now_mod, rl.shadow, routed);
     } else {  // a request that began in an earlier tile: decided by k4_group
       const uint32_t e = atomicAdd(&ctl->tile_ctr[DFR_CTR][0], 1u);
       Deferred df;
@@ -1405,7 +1410,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
       const Deferred df = dfr[e];
       const HotBucket& x = hb[df.bucket];
       if (df.req > x.rstar) {
-        out[df.idx] = tile::local_hit_status(df.h, rules[df.rule].div - df.now_mod, rules[df.rule].shadow);
+        tile::emit_local_hit(out, df.idx, df.h, rules[df.rule].div - df.now_mod, rules[df.rule].shadow, routed);
       } else {
         tile::decide_at(df.idx, df.req, df.rule, df.h, df.now_mod, x.base, df.P, SEG_NO_FREEZE, rules, out, req_thr,
                       routed);

@@ -15,7 +15,9 @@
 //   k_route_reply   owner: (out, thr) of the routed batch -> RReply records
 //   k_route_unpack  origin: replies -> out[i], max into ThrottleMillis of req_of[i]
 #include "rl_common.h"
+#include "rl_decide.h"
 #include "rl_device.h"
+#include "rl_internal.h"
 
 namespace rlhip {
 namespace route {
@@ -305,7 +307,10 @@ __global__ __launch_bounds__(NT) void k_route_pack1(DevBatch in, const DevRule* 
         const bool wait = lane < lp ? un < LB_U : lane == lp ? un < up : false;
         if (__ballot(wait)) {
           if (++spun > LB_SPIN_LIMIT) {
-            if (lane == 0) atomicOr(gerr, (uint32_t)ERR_SPIN);
+            if (lane == 0) {
+              atomicOr(gerr, (uint32_t)ERR_SPIN);
+              __threadfence();  // the flag is visible before the (wrong) prefix below is published
+            }
             break;
           }
           __builtin_amdgcn_s_sleep(1);
@@ -325,15 +330,21 @@ __global__ __launch_bounds__(NT) void k_route_pack1(DevBatch in, const DevRule* 
     }
     if (lane == 0) {
       s_base[j] = excl;
-      if (bi == gridDim.x - 1u) {  // the last block: every owner's total and the batch's status
-        const uint32_t e = __hip_atomic_load(gerr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        x[2 * j] = excl + agg;
-        x[2 * j + 1] = e & ERR_SPIN ? (uint32_t)RL_EDEVICE
-                       : e & (ERR_BAD_INPUT | ERR_BAD_TIME) ? (uint32_t)RL_EINVAL : 0u;
-      }
+      if (bi == gridDim.x - 1u) x[2 * j] = excl + agg;  // the last block: every owner's total
     }
   }
   __syncthreads();
+  // The last block writes the batch's status into every owner's pair, from ONE read of gerr
+  // after all of its look-backs: every rank then receives the same status from this origin and
+  // all of them take the same exit (rl_router.cpp). Every block ORed its flags (and a timed-out
+  // look-back its ERR_SPIN) into gerr before publishing the words this block has read.
+  if (bi == gridDim.x - 1u && tid == 0) {
+    __threadfence();
+    const uint32_t e = __hip_atomic_load(gerr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t status = e & ERR_SPIN ? (uint32_t)RL_EDEVICE
+                            : e & (ERR_BAD_INPUT | ERR_BAD_TIME) ? (uint32_t)RL_EINVAL : 0u;
+    for (uint32_t j = 0; j < n_shards; ++j) x[2 * j + 1] = status;
+  }
   if (i >= in.n_desc) return;
   if (d == (uint32_t)NS) {
     perm[i] = RL_ROUTE_LOCAL;
@@ -381,6 +392,486 @@ __global__ __launch_bounds__(NT) void k_route_unpack(uint32_t n, const uint32_t*
   if (r.thr) atomicMax(&req_thr[req_of[i]], r.thr);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Combining router (rl_router.cpp). Under a skewed key distribution the hottest
+// keys arrive from every origin at their one owner (Zipf 1.1: the top 256 prefixes are about
+// half of all descriptors), so per-descriptor records overload that owner. An origin combines
+// its descriptors of a hot prefix into ONE record carrying their sum of hits_addend: a run of
+// INCRBYs of one key string at one request time is one INCRBY of the sum (no EXPIRE can fall
+// between them, and the local cache is off when combining is on). The owner answers every
+// record with its raw INCRBY post-value (rl_raw_reply); the origin rebuilds each descriptor's
+// post-value as (record post-value - record sum + the descriptor's inclusive prefix of h inside
+// its group, in arrival order) and makes the decisions itself.
+//
+//   k_route_pack2     hash, owner, hot-set lookup (tags in LDS); cold descriptors ranked
+//                     stably per owner (block ranks + decoupled look-back, as k_route_pack1)
+//                     and written once to the strided send buffer; hot descriptors: per-block
+//                     h sums per group and each descriptor's exclusive prefix inside its block
+//   k_route_hot_scan  per group: exclusive prefix of the block sums over blocks, the group's
+//                     total; the last block checks the batch (one request time over all hot
+//                     descriptors, every hot descriptor with its entry's rule, sums in range)
+//                     and appends one combined record per group to its owner's section, or
+//                     asks for a repack without combining
+//   k_route_pack2<repack>  the pack again without combining, only when asked (else it returns)
+//   k_route_unpack_raw     origin: raw replies -> each descriptor's post-value -> decision
+// ---------------------------------------------------------------------------------------------
+constexpr int PR = 4;                   // descriptors per thread
+constexpr int PBLK = NT * PR;           // per block
+constexpr int PW = NT / 64;             // waves per block
+constexpr int PV = PR * PW;             // virtual waves per block, (round, wave) in arrival order
+static_assert(PBLK == (int)ROUTE2_BLOCK, "pack block");
+constexpr uint32_t RF_MISMATCH = 1u, RF_OVERFLOW = 2u, RF_HOT = 4u;
+constexpr uint32_t CAT_LOCAL = NS, CAT_HOT = NS + 1;
+constexpr uint32_t HOT_PRE_MAX = (1u << PERM_HOT_PRE_BITS) - 1u;
+constexpr uint32_t HOT_H_MAX = 4095u;   // a combined descriptor's h: 1024 x 4095 < 2^22
+static_assert(HOT_MAX <= 256, "hot group index in 8 perm bits");
+
+RL_DEV uint32_t route_hot_lookup(const uint32_t* s_tags, const HotEntry* __restrict__ ent, uint64_t a, uint64_t b,
+                                 uint32_t& rule) {
+  const uint32_t t = hot_tag(a);
+  uint32_t s = hot_home(a);
+  for (int probe = 0; probe < HOT_TAGS; ++probe) {
+    const uint32_t w = s_tags[s];
+    if (w == 0u) return 0xFFFFFFFFu;
+    if ((w & HOT_TAG_MASK) == t) {
+      const HotEntry e = ent[(w & ~HOT_TAG_MASK) - 1u];
+      if (e.a == a && e.b == b) {
+        rule = e.rule;
+        return e.idx;
+      }
+    }
+    s = (s + 1) & (HOT_TAGS - 1);
+  }
+  return 0xFFFFFFFFu;
+}
+
+// Decoupled look-back of one owner's count over the blocks before this one (k_route_pack1's,
+// run by one wave): returns the exclusive prefix and publishes the inclusive one.
+RL_DEV uint32_t lookback_owner(uint32_t* lb, uint32_t* gerr, uint32_t bi, uint32_t j, uint32_t agg) {
+  const uint32_t lane = threadIdx.x & 63;
+  if (lane == 0)
+    __hip_atomic_store(&lb[(size_t)bi * NS + j], (bi ? LB_A : LB_P) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t excl = 0;
+  if (bi) {
+    int32_t end = (int32_t)bi - 1;
+    uint32_t spun = 0;
+    for (;;) {
+      const int32_t k = end - (int32_t)lane;
+      const uint32_t v = k >= 0 ? __hip_atomic_load(&lb[(size_t)k * NS + j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : LB_P;
+      const uint64_t pm = __ballot((v >> 30) == 2u);
+      const uint32_t lp = pm ? (uint32_t)__ffsll((unsigned long long)pm) - 1u : 64u;
+      const bool wait = lane <= lp && lane < 64u && (v >> 30) == 0u;
+      if (__ballot(wait)) {
+        if (++spun > LB_SPIN_LIMIT) {
+          if (lane == 0) {
+            atomicOr(gerr, (uint32_t)ERR_SPIN);
+            __threadfence();
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      excl += wave_sum_u32(lane <= lp ? v & LB_V : 0u);
+      if (pm) break;
+      end -= 64;
+    }
+    if (lane == 0)
+      __hip_atomic_store(&lb[(size_t)bi * NS + j], LB_P | ((excl + agg) & LB_V), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return excl;
+}
+
+template <bool COMBINE, bool REPACK>
+__global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
+                                                     uint64_t seed, uint32_t origin, uint32_t n_shards, uint32_t stride,
+                                                     const HotEntry* __restrict__ hot, RRec* __restrict__ send,
+                                                     uint32_t* __restrict__ perm, uint32_t* lb, uint32_t* gerr,
+                                                     uint32_t* __restrict__ x, uint32_t* __restrict__ bhs,
+                                                     uint32_t* __restrict__ bstat, const uint32_t* __restrict__ rctl) {
+  __shared__ uint32_t s_wc[PR][PW][NS + 2];
+  __shared__ uint32_t s_tot[NS], s_base[NS];
+  __shared__ uint32_t s_err;
+  __shared__ uint32_t s_tags[COMBINE ? HOT_TAGS : 1];
+  __shared__ uint32_t s_hw[COMBINE ? PV : 1][COMBINE ? HOT_MAX : 1];
+  __shared__ uint32_t s_st[3];  // the block's hot descriptors: ~min now, max now, RF_* flags
+  if (REPACK && rctl[0] == 0u) return;  // combining was accepted: nothing to redo
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6, bi = blockIdx.x;
+  for (uint32_t k = tid; k < PR * PW * (NS + 2); k += NT) (&s_wc[0][0][0])[k] = 0;
+  if constexpr (COMBINE) {
+    const uint32_t* tg = reinterpret_cast<const uint32_t*>(hot);
+    for (uint32_t k = tid; k < (uint32_t)HOT_TAGS; k += NT) s_tags[k] = tg[k];
+    for (uint32_t k = tid; k < (uint32_t)(PV * HOT_MAX); k += NT) (&s_hw[0][0])[k] = 0;
+  }
+  if (tid == 0) s_err = 0;
+  if (tid < 3) s_st[tid] = 0;
+  __syncthreads();
+  const uint32_t i0 = bi * PBLK, last = in.n_desc - 1u;  // n_desc >= 1, n_req >= 1 (host-checked)
+  // two levels of loads, each issued together at clamped indices (k_route_pack1)
+  uint32_t rl[PR], q[PR], qp[PR], oa[PR], ob[PR];
+#pragma unroll
+  for (int r = 0; r < PR; ++r) {
+    const uint32_t i = min(i0 + r * NT + tid, last);
+    rl[r] = in.rule[i];
+    q[r] = in.req_of[i];
+    qp[r] = in.req_of[i ? i - 1u : 0u];
+    oa[r] = in.off[i];
+    ob[r] = in.off[i + 1u];
+  }
+  bool okv[PR];
+  int64_t nowv[PR];
+  uint32_t hav[PR];
+  u32x4 w0[PR], w1[PR];
+  uint32_t err = 0;
+#pragma unroll
+  for (int r = 0; r < PR; ++r) {
+    const bool v = i0 + r * NT + tid < in.n_desc;
+    const bool lay = oa[r] <= ob[r] && ob[r] <= in.blob_bytes && qp[r] <= q[r];
+    const bool nil = rl[r] == RL_NIL_RULE, q_ok = q[r] < in.n_req, rule_ok = rl[r] < n_rules;
+    if (v && (!lay || (!nil && (!rule_ok || !q_ok)))) err |= ERR_BAD_INPUT;
+    okv[r] = v && !nil && lay && rule_ok && q_ok;
+    const uint32_t qc = q_ok ? q[r] : 0u;
+    nowv[r] = in.now[qc];
+    hav[r] = in.hits[qc];
+    const u32x4* pw = reinterpret_cast<const u32x4*>(in.blob + ((okv[r] ? oa[r] : 0u) & ~3u));
+    w0[r] = pw[0];
+    w1[r] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const uint32_t*>(pw) + 4);
+  }
+  RRec rec[PR];
+  uint32_t cat[PR], hix[PR], stf = 0;
+#pragma unroll
+  for (int r = 0; r < PR; ++r) {
+    cat[r] = CAT_LOCAL;
+    hix[r] = 0;
+    rec[r].a = rec[r].b = 0;
+    rec[r].now = rec[r].rule = rec[r].h = rec[r].greq = 0;
+    if (!okv[r]) continue;
+    if (nowv[r] < 0 || nowv[r] > MAX_NOW) {
+      err |= ERR_BAD_TIME;
+      continue;
+    }
+    const FpState fs = prefix_state_pre(w0[r], w1[r], in.blob, oa[r], ob[r] - oa[r], seed);
+    rec[r].a = fs.a;
+    rec[r].b = fs.b;
+    rec[r].now = (uint32_t)nowv[r];
+    rec[r].rule = rl[r];
+    rec[r].h = hav[r] > 1u ? hav[r] : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
+    rec[r].greq = (origin << ROUTE_REQ_BITS) | q[r];
+    cat[r] = route_owner(fs.a, fs.b, n_shards);
+    if constexpr (COMBINE) {
+      uint32_t hr = 0;
+      const uint32_t hx = route_hot_lookup(s_tags, hot + HOT_SLOTS, fs.a, fs.b, hr);
+      if (hx != 0xFFFFFFFFu) {
+        cat[r] = CAT_HOT;
+        hix[r] = hx;
+        // the group is one key string only if every descriptor has the entry's rule
+        if (hr != rl[r]) stf |= RF_MISMATCH;
+        if (rec[r].h > HOT_H_MAX) stf |= RF_OVERFLOW;
+      }
+    }
+  }
+  // stable ranks per owner: (round, wave, lane) is arrival order inside the block
+  const uint64_t lt = lanemask_lt();
+  uint32_t rank[PR];
+#pragma unroll
+  for (int r = 0; r < PR; ++r) {
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (int bt = 0; bt < 5; ++bt) {
+      const bool bit = (cat[r] >> bt) & 1u;
+      const uint64_t bal = __ballot(bit);
+      m &= bit ? bal : ~bal;
+    }
+    rank[r] = (uint32_t)__popcll(m & lt);
+    if (lane == (uint32_t)__ffsll((unsigned long long)m) - 1u) s_wc[r][w][cat[r]] = (uint32_t)__popcll(m);
+  }
+  uint32_t hex[PR];  // hot: exclusive prefix of h among the wave's descriptors of the same group
+#pragma unroll
+  for (int r = 0; r < PR; ++r) hex[r] = 0;
+  if constexpr (COMBINE) {
+    uint32_t mn = 0xFFFFFFFFu, mx = 0;
+#pragma unroll
+    for (int r = 0; r < PR; ++r) {
+      uint64_t todo = __ballot(cat[r] == CAT_HOT);
+      while (todo) {  // one group of the wave per iteration (wave-uniform)
+        const uint32_t ld = (uint32_t)__ffsll((unsigned long long)todo) - 1u;
+        const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)hix[r], (int)ld);
+        const bool mine = cat[r] == CAT_HOT && hix[r] == hl;
+        const uint64_t m = __ballot(mine);
+        const uint32_t v = mine ? rec[r].h : 0u;
+        const uint32_t incl = wave_incl_scan_u32(v);
+        if (mine) hex[r] = incl - v;
+        if (lane == ld) s_hw[r * PW + w][hl] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        todo &= ~m;
+      }
+      if (cat[r] == CAT_HOT) {
+        mn = min(mn, rec[r].now);
+        mx = max(mx, rec[r].now);
+      }
+    }
+    if (__ballot(mx != 0u || mn != 0xFFFFFFFFu)) {  // the wave has hot descriptors (wave-uniform)
+      mn = wave_min_u32(mn);
+      mx = wave_max_u32(mx);
+      if (lane == 0) {
+        atomicMax(&s_st[0], ~mn);
+        atomicMax(&s_st[1], mx);
+        atomicOr(&s_st[2], RF_HOT);
+      }
+    }
+    if (stf) atomicOr(&s_st[2], stf);
+  }
+  if (err) atomicOr(&s_err, err);
+  __syncthreads();
+  if (tid < NS) {  // per owner: exclusive offsets of the (round, wave) runs, block total
+    uint32_t run = 0;
+#pragma unroll
+    for (int r = 0; r < PR; ++r)
+#pragma unroll
+      for (int v = 0; v < PW; ++v) {
+        const uint32_t c = s_wc[r][v][tid];
+        s_wc[r][v][tid] = run;
+        run += c;
+      }
+    s_tot[tid] = run;
+  }
+  if constexpr (COMBINE) {
+    for (uint32_t hl = tid; hl < (uint32_t)HOT_MAX; hl += NT) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int v = 0; v < PV; ++v) t += s_hw[v][hl];
+      bhs[(size_t)bi * HOT_MAX + hl] = t;
+      if (t > HOT_PRE_MAX) atomicOr(&s_st[2], RF_OVERFLOW);
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && s_err) {  // before any owner's word of this block is published
+    atomicOr(gerr, s_err);
+    __threadfence();
+  }
+  if (COMBINE && tid < 3) bstat[(size_t)bi * 4 + tid] = s_st[tid];
+  __syncthreads();
+  for (uint32_t j = w; j < n_shards; j += PW) {  // wave-uniform
+    const uint32_t excl = lookback_owner(lb, gerr, bi, j, s_tot[j]);
+    if (lane == 0) {
+      s_base[j] = excl;
+      if (bi == gridDim.x - 1u) x[2 * j] = excl + s_tot[j];  // the last block: every owner's cold total
+    }
+  }
+  __syncthreads();
+  if (bi == gridDim.x - 1u && tid == 0) {  // one status for every owner (k_route_pack1)
+    __threadfence();
+    const uint32_t e = __hip_atomic_load(gerr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t status = e & ERR_SPIN ? (uint32_t)RL_EDEVICE
+                            : e & (ERR_BAD_INPUT | ERR_BAD_TIME) ? (uint32_t)RL_EINVAL : 0u;
+    for (uint32_t j = 0; j < n_shards; ++j) x[2 * j + 1] = status;
+  }
+#pragma unroll
+  for (int r = 0; r < PR; ++r) {
+    const uint32_t i = i0 + r * NT + tid;
+    if (i >= in.n_desc) continue;
+    if (cat[r] == CAT_LOCAL) {
+      perm[i] = RL_ROUTE_LOCAL;
+    } else if (COMBINE && cat[r] == CAT_HOT) {
+      uint32_t pre = hex[r];
+      const uint32_t v0 = (uint32_t)(r * PW) + w;
+      for (uint32_t v = 0; v < v0; ++v) pre += s_hw[v][hix[r]];
+      perm[i] = PERM_HOT | (hix[r] << PERM_HOT_PRE_BITS) | (pre & HOT_PRE_MAX);
+    } else {
+      const uint32_t d = cat[r];
+      const uint32_t pos = d * stride + s_base[d] + s_wc[r][w][d] + rank[r];
+      send[pos] = rec[r];
+      perm[i] = pos;
+    }
+  }
+}
+
+constexpr int HS_NT = 1024, HS_COLS = 16, HS_SLICES = HS_NT / HS_COLS, HS_Q = 16;
+static_assert(HOT_MAX % HS_COLS == 0, "hot scan columns");
+__global__ __launch_bounds__(HS_NT) void k_route_hot_scan(uint32_t nb, uint32_t n_shards, uint32_t origin,
+                                                           uint32_t stride, const HotEntry* __restrict__ hot,
+                                                           uint32_t* __restrict__ bhs, const uint32_t* bstat,
+                                                           RRec* __restrict__ send, uint32_t* x, uint32_t* rctl,
+                                                           uint32_t* __restrict__ hot_pos,
+                                                           uint32_t* __restrict__ hot_tot,
+                                                           unsigned long long* tot64, const uint32_t* gerr) {
+  __shared__ unsigned long long s_sl[HS_SLICES][HS_COLS];
+  __shared__ uint32_t s_last, s_mn, s_mx, s_fl, s_bad;
+  __shared__ uint32_t s_oc[4][NS + 1];
+  const uint32_t tid = threadIdx.x, c = tid % HS_COLS, sl = tid / HS_COLS;
+  const uint32_t col = blockIdx.x * HS_COLS + c;
+  const uint32_t Q = (nb + HS_SLICES - 1) / HS_SLICES;
+  const uint32_t r0 = min(nb, sl * Q), r1 = min(nb, r0 + Q);
+  unsigned long long sum = 0;
+  for (uint32_t rr = r0; rr < r1; rr += HS_Q) {
+    uint32_t v[HS_Q];
+#pragma unroll
+    for (int u = 0; u < HS_Q; ++u) v[u] = bhs[(size_t)min(rr + u, r1 - 1u) * HOT_MAX + col];
+#pragma unroll
+    for (int u = 0; u < HS_Q; ++u) sum += rr + u < r1 ? v[u] : 0u;
+  }
+  s_sl[sl][c] = sum;
+  __syncthreads();
+  unsigned long long run = 0, tot = 0;
+  for (uint32_t k = 0; k < (uint32_t)HS_SLICES; ++k) {
+    const unsigned long long y = s_sl[k][c];
+    run += k < sl ? y : 0ull;
+    tot += y;
+  }
+  for (uint32_t rr = r0; rr < r1; rr += HS_Q) {  // the same rows again (L2): exclusive prefixes in place
+    uint32_t v[HS_Q];
+#pragma unroll
+    for (int u = 0; u < HS_Q; ++u) v[u] = bhs[(size_t)min(rr + u, r1 - 1u) * HOT_MAX + col];
+#pragma unroll
+    for (int u = 0; u < HS_Q; ++u)
+      if (rr + u < r1) {
+        bhs[(size_t)(rr + u) * HOT_MAX + col] = (uint32_t)run;
+        run += v[u];
+      }
+  }
+  if (sl == 0) tot64[col] = tot;
+  // hand-off to the last block (MI355X_MICROARCH.md, inter-workgroup visibility): every storing
+  // wave drains, barrier, one lane's release + counter; the last arriver's lane acquires
+  drain_vmem();
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    s_last = atomicAdd(&rctl[2], 1u) == gridDim.x - 1u;
+    if (s_last) __threadfence();
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the last block: the batch's verdict, then one combined record per group
+  if (tid == 0) {
+    s_mn = 0;
+    s_mx = 0;
+    s_fl = 0;
+    s_bad = 0;
+  }
+  if (tid < 4 * (NS + 1)) (&s_oc[0][0])[tid] = 0;
+  __syncthreads();
+  {
+    uint32_t mn = 0, mx = 0, fl = 0;
+    for (uint32_t b = tid; b < nb; b += HS_NT) {
+      mn = max(mn, bstat[(size_t)b * 4]);
+      mx = max(mx, bstat[(size_t)b * 4 + 1]);
+      fl |= bstat[(size_t)b * 4 + 2];
+    }
+    mn = wave_max_u32(mn);
+    mx = wave_max_u32(mx);
+    fl = wave_or_u32(fl);
+    if ((tid & 63) == 0) {
+      atomicMax(&s_mn, mn);
+      atomicMax(&s_mx, mx);
+      atomicOr(&s_fl, fl);
+    }
+  }
+  unsigned long long t = 0;
+  HotEntry e{};
+  if (tid < (uint32_t)HOT_MAX) {
+    t = tot64[tid];
+    e = hot[HOT_SLOTS + tid];
+    if (t >= (1ull << 32)) atomicOr(&s_bad, 1u);
+  }
+  __syncthreads();
+  const uint32_t fl = s_fl, now_min = ~s_mn, now_max = s_mx;
+  if (*gerr) return;  // the batch is refused (its status is in x): nothing to add
+  const bool ok = !s_bad && !(fl & (RF_MISMATCH | RF_OVERFLOW)) && (!(fl & RF_HOT) || now_min == now_max);
+  if (!ok) {
+    if (tid == 0) rctl[0] = 1u;  // k_route_pack2<repack> redoes the batch without combining
+    return;
+  }
+  // rank of each non-empty group among its owner's groups (index order), per wave then over waves
+  const uint32_t lane = tid & 63, w = tid >> 6;
+  const bool act = tid < (uint32_t)HOT_MAX && t > 0;
+  const uint32_t o = act ? route_owner(e.a, e.b, n_shards) : (uint32_t)NS;
+  uint32_t rank = 0;
+  if (tid < (uint32_t)HOT_MAX) {
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (int bt = 0; bt < 5; ++bt) {
+      const bool bit = (o >> bt) & 1u;
+      const uint64_t bal = __ballot(bit);
+      m &= bit ? bal : ~bal;
+    }
+    rank = (uint32_t)__popcll(m & lanemask_lt());
+    if (lane == (uint32_t)__ffsll((unsigned long long)m) - 1u) s_oc[w][o] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  uint32_t before = 0, cnt = 0;
+  if (act) {
+    for (uint32_t k = 0; k < 4; ++k) before += k < w ? s_oc[k][o] : 0u;
+    const uint32_t pos = o * stride + x[2 * o] + before + rank;
+    RRec r;
+    r.a = e.a;
+    r.b = e.b;
+    r.now = now_min;
+    r.rule = e.rule;
+    r.h = (uint32_t)t;
+    r.greq = origin << ROUTE_REQ_BITS;
+    send[pos] = r;
+    hot_pos[tid] = pos;
+    hot_tot[tid] = (uint32_t)t;
+  }
+  if (tid < NS) {
+    for (uint32_t k = 0; k < 4; ++k) cnt += s_oc[k][tid];
+  }
+  __syncthreads();  // every group read x[] above
+  if (tid < n_shards) x[2 * tid] += cnt;
+  if (tid == 0) rctl[1] = 1u;  // combining applied
+}
+
+// Origin: every descriptor's decision from its owner's raw reply.
+__global__ __launch_bounds__(NT) void k_route_unpack_raw(DevBatch in, const DevRule* __restrict__ rules,
+                                                          const uint32_t* __restrict__ perm,
+                                                          const RawReply* __restrict__ back,
+                                                          const uint32_t* __restrict__ boff,
+                                                          const uint32_t* __restrict__ hot_pos,
+                                                          const uint32_t* __restrict__ hot_tot,
+                                                          rl_status* __restrict__ out, uint32_t* __restrict__ req_thr) {
+  const uint32_t i = blockIdx.x * NT + threadIdx.x;
+  if (i >= in.n_desc) return;
+  const uint32_t p = perm[i];
+  if (p == RL_ROUTE_LOCAL) {
+    // GetResponseDescriptorStatus("" key) -> {OK, nil limit, 0}  base_limiter.go:72-75
+    rl_status st;
+    st.code_flags = RL_CODE_OK;
+    st.limit_remaining = 0;
+    st.reset_s = 0;
+    st.over_limit_delta = 0;
+    st.near_limit_delta = 0;
+    out[i] = st;
+    return;
+  }
+  const uint32_t rule = in.rule[i], q = in.req_of[i];
+  const int64_t now = in.now[q];
+  const uint32_t ha = in.hits[q];
+  const uint32_t h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
+  const DevRule R = rules[rule];
+  uint32_t after, fl;
+  if (p & PERM_HOT) {
+    // post-value of this descriptor's INCRBY inside its combined group: the group's reply minus
+    // the group's sum plus the inclusive prefix of h up to this descriptor (arrival order)
+    const uint32_t hl = (p >> PERM_HOT_PRE_BITS) & (uint32_t)(HOT_MAX - 1);
+    const uint32_t P = boff[(size_t)(i / PBLK) * HOT_MAX + hl] + (p & HOT_PRE_MAX) + h;
+    const RawReply rr = back[hot_pos[hl]];
+    after = rr.after - hot_tot[hl] + P;
+    fl = rr.flags;
+  } else {
+    const RawReply rr = back[p];
+    after = rr.after;
+    fl = rr.flags;
+  }
+  const uint32_t now_mod = (uint32_t)now % R.div;  // now - (now / div) * div
+  rl_status st;
+  const uint32_t thr = decide_status(after, (fl & RAW_LOCAL_HIT) != 0u, h, now_mod, R, st);
+  out[i] = st;
+  // DoLimitResponse.ThrottleMillis = max over the request's descriptors  base_limiter.go:163-165
+  if (thr) atomicMax(&req_thr[q], thr);
+}
+
 }  // namespace route
 
 static uint32_t route_blocks(uint32_t n) { return n ? (n + route::NT - 1) / route::NT : 1; }
@@ -404,6 +895,40 @@ void launch_route_pack_strided(hipStream_t st, const rl_batch& b, const DevRule*
   const uint32_t nb = route_blocks(b.n_desc);  // lb: nb * NS look-back words + the error word, zeroed
   hipLaunchKernelGGL(route::k_route_pack1, dim3(nb), dim3(route::NT), 0, st, make_dev_batch(b), rules, n_rules, seed,
                      origin, n_shards, stride, send, perm, lb, lb + (size_t)nb * route::NS, x);
+}
+
+uint32_t route2_blocks(uint32_t n) { return n ? (n + ROUTE2_BLOCK - 1) / ROUTE2_BLOCK : 1; }
+size_t route2_lb_words(uint32_t n) { return ((size_t)route2_blocks(n) * route::NS + 1 + 63) / 64 * 64; }
+size_t route2_bhs_words(uint32_t n) { return (size_t)route2_blocks(n) * HOT_MAX; }
+
+void launch_route_pack2(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
+                        uint32_t origin, uint32_t n_shards, uint32_t stride, const HotEntry* hot,
+                        const RoutePackBufs& o) {
+  const uint32_t nb = route2_blocks(b.n_desc);
+  const DevBatch in = make_dev_batch(b);
+  const size_t area = route2_lb_words(b.n_desc);
+  uint32_t* lb1 = o.lb;
+  uint32_t* lb2 = o.lb + area;
+  const size_t gw = (size_t)nb * route::NS;  // the error word follows the look-back words
+  if (!hot) {
+    hipLaunchKernelGGL((route::k_route_pack2<false, false>), dim3(nb), dim3(route::NT), 0, st, in, rules, n_rules, seed,
+                       origin, n_shards, stride, hot, o.send, o.perm, lb1, lb1 + gw, o.x, o.bhs, o.bstat, o.rctl);
+    return;
+  }
+  hipLaunchKernelGGL((route::k_route_pack2<true, false>), dim3(nb), dim3(route::NT), 0, st, in, rules, n_rules, seed,
+                     origin, n_shards, stride, hot, o.send, o.perm, lb1, lb1 + gw, o.x, o.bhs, o.bstat, o.rctl);
+  hipLaunchKernelGGL(route::k_route_hot_scan, dim3(HOT_MAX / route::HS_COLS), dim3(route::HS_NT), 0, st, nb, n_shards,
+                     origin, stride, hot, o.bhs, o.bstat, o.send, o.x, o.rctl, o.hot_pos, o.hot_tot,
+                     reinterpret_cast<unsigned long long*>(o.rctl + 16), lb1 + gw);
+  hipLaunchKernelGGL((route::k_route_pack2<false, true>), dim3(nb), dim3(route::NT), 0, st, in, rules, n_rules, seed,
+                     origin, n_shards, stride, hot, o.send, o.perm, lb2, lb2 + gw, o.x, o.bhs, o.bstat, o.rctl);
+}
+
+void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* rules, const RoutePackBufs& o,
+                             const RawReply* back, rl_status* out, uint32_t* thr) {
+  if (!b.n_desc) return;
+  hipLaunchKernelGGL(route::k_route_unpack_raw, dim3(route_blocks(b.n_desc)), dim3(route::NT), 0, st, make_dev_batch(b),
+                     rules, o.perm, back, o.bhs, o.hot_pos, o.hot_tot, out, thr);
 }
 
 void launch_route_reply(hipStream_t st, uint32_t n, const rl_status* out, const uint32_t* thr, RReply* reply) {

@@ -1,66 +1,148 @@
-// rl_router.cpp — the routed DoLimit step behind one C call (include/rl_hip.h
-// "Router object").
+// rl_router.cpp — the routed DoLimit step behind the C ABI (include/rl_hip.h
+// "Router object", DESIGN.md §5).
 //
 // The reference sends each key's INCRBY to the Redis server that holds it and pipelines the
 // commands of a request (src/redis/fixed_cache_impl.go:66-80, src/redis/driver_impl.go:84-110).
-// Here GPU s owns the keys whose prefix fingerprint maps to s (route_owner); one step of a
-// shard packs its origin batch by owner (rl_route_pack), exchanges per-owner counts and then
-// the 32-B records, decides what it received as owner (rl_submit_routed, origin-major), sends
-// the 24-B replies back and unpacks them (rl_route_unpack).
+// Here GPU s owns the keys whose prefix fingerprint maps to s (route_owner). One step:
+//   origin   pack its batch by owner into a strided send buffer: one record per descriptor,
+//            except hot prefixes (the shard's route hot set), whose descriptors travel as ONE
+//            combined record per prefix carrying their sum of hits_addend (rl_route.hip)
+//   exchange per-owner (count, status) pairs, then the records (all-to-all)
+//   owner    decide the records received from every origin, in origin order, answering each
+//            with its raw INCRBY post-value (rl_submit_routed_async, RL_ROUTED_RAW)
+//   exchange the owners' statuses and the raw replies (reverse all-to-all)
+//   origin   every descriptor's post-value from its record's reply (and, inside a combined
+//            record, its prefix of hits_addend), then its decision (k_route_unpack_raw)
 //
-// Transports: RCCL (one process per GPU, ncclAllToAll / ncclAllToAllv on a stream the router
-// owns) or local (n_shards engines in one process, device-to-device copies). Both carry a
-// status word per shard through each exchange, so every shard completes every collective of
-// a step and then all of them fail together.
+// Transports: RCCL (one process per GPU, ncclAllToAll / ncclAllToAllv / ncclAllGather on a
+// stream the router owns) or local (n_shards engines in one process, device copies). Status
+// words ride in the counts exchange (pack) and the reply exchange (decide, and any local HIP
+// failure after the counts), so every shard completes every collective of a step and all of
+// them fail together.
 //
-// Local transport: host-synchronous between phases. RCCL transport: three host waits per
-// step (counts, the owner's decide, the end), the two streams ordered by events otherwise.
+// Two steps may be in flight (rl_router_submit / rl_router_wait): step k+1's pack, counts and
+// record exchange run on the origin and exchange streams while step k's owner batch is decided
+// on the engine's streams (the engine pipelines routed batches like rl_submit_pipelined).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
+#include "rl_common.h"
 #include "rl_hip.h"
+#include "rl_internal.h"
+
+using namespace rlhip;
 
 namespace {
 
-constexpr uint32_t REC = RL_ROUTE_RECORD_BYTES;
-constexpr uint32_t REP = RL_ROUTE_REPLY_BYTES;
+constexpr uint32_t REC = sizeof(RRec);
+constexpr uint32_t RAWB = sizeof(RawReply);
 constexpr uint32_t MAXS = RL_ROUTE_MAX_SHARDS;
+constexpr int NSLOT = 2;                   // steps in flight
+constexpr uint64_t ROUTE_HOT_EVERY = 8;    // route hot set refresh period (steps)
+constexpr uint32_t ROUTE_HOT_KEEP = 64;    // a group stays while its origin sends it >= this sum of hits per step
+static_assert(REC == RL_ROUTE_RECORD_BYTES && RAWB == sizeof(rl_raw_reply), "record layouts");
+constexpr uint32_t HX_HOT = 8 * MAXS;      // pinned mirror: hot sums, then the control words
 
 double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// Per-shard exchange buffers (device): an origin's records by owner and its reply area, an
-// owner's received records and replies.
-struct ShardBufs {
-  rl_engine* e = nullptr;
-  void* send = nullptr;       // max_desc records, grouped by owner
-  uint32_t* d_cnt = nullptr;  // per-owner counts (rl_route_pack)
-  uint32_t* perm = nullptr;   // max_desc
-  void* recv = nullptr;       // n_shards * max_desc records
-  void* reply = nullptr;      // n_shards * max_desc replies
-  void* back = nullptr;       // max_desc replies (origin side)
+// Fault injection for the tests (RL_ROUTER_FAULT="phase:shard", read at create, fires once):
+// the shard behaves as if a HIP call of that phase failed.
+enum Phase { PH_NONE = 0, PH_PACK, PH_RECORDS, PH_DECIDE, PH_REPLIES, PH_UNPACK };
+
+// One hot-set entry as exchanged between ranks (32 B): an owner's hot prefix.
+struct AgEntry {
+  uint64_t a, b;
+  uint32_t unit, rule, count, pad;
+};
+static_assert(sizeof(AgEntry) == 32, "allgather entry");
+
+// Pinned + device staging of one shard's host batch (RL_ROUTER_HOST), the engine's layout.
+struct HostStage {
+  uint8_t* h_in = nullptr;
+  uint8_t* d_in = nullptr;
+  rl_status* d_out = nullptr;
+  rl_status* h_out = nullptr;
+  uint32_t* d_thr = nullptr;
+  uint32_t* h_thr = nullptr;
+};
+
+// One shard's part of one step in flight.
+struct ShardStep {
+  RoutePackBufs pb{};
+  uint8_t* zero = nullptr;    // look-back areas + control words, zeroed per step
+  size_t zero_bytes = 0;
+  RRec* recv = nullptr;       // owner: records from every origin
+  RawReply* reply = nullptr;  // owner: one raw reply per received record
+  RawReply* back = nullptr;   // origin: replies to its records, strided like send
+  int32_t* d_x = nullptr;     // [2G] pairs sent | [2G] received | [G] statuses sent | [G] received
+  int32_t* h_x = nullptr;     // pinned mirror; at HX_HOT the hot sums, then the control words
+  HostStage hs;
+  rl_batch b{};               // the origin batch (device pointers)
+  rl_status* out = nullptr;
+  uint32_t* thr = nullptr;
   uint32_t cnt[MAXS] = {};    // records this origin sends each owner
+  uint32_t rcv[MAXS] = {};    // records this owner receives from each origin
+  uint32_t n_in = 0;
+  int rc_pack = 0, rc_dec = 0, rc_local = 0;
+  std::string msg;
+  const char* phase = "";     // where msg comes from: pack, records, decide, replies, unpack
+  bool submitted = false;     // owner batch handed to the engine (rl_wait pending)
+  bool combined = false;
+};
+
+struct Shard {
+  rl_engine* e = nullptr;
+  EngineView v{};
+  hipStream_t os = nullptr;   // origin work: staging copies, pack, hot scan, unpack
+  hipEvent_t ev = nullptr;    // os -> exchange stream
+  ShardStep st[NSLOT];
+  // route hot set (this shard as origin)
+  std::vector<HotKey> hot;
+  HotEntry* d_hot = nullptr;
+  HotEntry* h_hot = nullptr;
+  hipEvent_t ev_hot = nullptr;
+  uint32_t last_tot[HOT_MAX] = {};  // sums of hits per group, last step that combined
+  bool last_valid = false;
+  bool repacked = false;            // since the last refresh
+};
+
+struct StepSlot {
+  bool busy = false;
+  bool host = false;
+  bool counts_failed = false;  // every shard left after the counts exchange
+  double t0 = 0;
+  int32_t status[MAXS] = {};   // per shard (RCCL: as received from every origin / owner)
 };
 
 }  // namespace
 
 struct rl_router {
   rl_router_config cfg{};
-  bool rccl = false;
+  bool rccl = false, broken = false;
   ncclComm_t comm = nullptr;
   hipStream_t rs = nullptr;  // exchanges
-  std::vector<ShardBufs> sh;
-  int32_t* d_x = nullptr;    // RCCL: [2G] send + [2G] receive status/count words
-  int32_t* h_x = nullptr;    // pinned mirror of d_x + [G] owner statuses
-  hipEvent_t ev = nullptr;   // orders the router and engine streams
+  hipEvent_t ev_rs = nullptr;
+  std::vector<Shard> sh;
+  StepSlot slot[NSLOT];
+  uint64_t seq = 0, done = 0;
+  double t_pack0 = 0;        // start of the current submit's packs (host clock)
+  size_t in_bytes = 0, o_off = 0, o_rule = 0, o_req = 0, o_now = 0, o_hits = 0;  // host staging layout
+  AgEntry* d_ag = nullptr;   // RCCL hot-set allgather: [HOT_MAX] send | [G * HOT_MAX] receive
+  AgEntry* h_ag = nullptr;
+  int fault_phase = PH_NONE;
+  uint32_t fault_shard = 0;
   rl_router_stats st{};
   std::string err;
 
@@ -73,249 +155,687 @@ struct rl_router {
     err = buf;
     return code;
   }
-  int hip(hipError_t he, const char* what) {
-    return he == hipSuccess ? 0 : fail(RL_EHIP, "%s: %s", what, hipGetErrorString(he));
+  // RCCL failure: abort the communicator (its peers' collectives return), every later call fails
+  int nccl_fail(ncclResult_t nr, const char* what) {
+    if (comm) (void)ncclCommAbort(comm);
+    comm = nullptr;
+    broken = true;
+    return fail(RL_ECOMM, "%s: %s (communicator aborted)", what, ncclGetErrorString(nr));
   }
-  int nccl(ncclResult_t nr, const char* what) {
-    return nr == ncclSuccess ? 0 : fail(RL_ECOMM, "%s: %s", what, ncclGetErrorString(nr));
+  bool fault(int phase, uint32_t s) {
+    if (fault_phase != phase || fault_shard != s) return false;
+    fault_phase = PH_NONE;
+    return true;
   }
-  int step_local(const rl_batch* b, rl_status* const* out, uint32_t* const* thr);
-  int step_rccl(const rl_batch* b, rl_status* out, uint32_t* thr);
+  uint32_t n_local() const { return (uint32_t)sh.size(); }
+  uint32_t shard_id(uint32_t s) const { return rccl ? cfg.rank : s; }
+
+  int alloc_shard(Shard& s);
   void free_all();
+  int validate(const rl_batch& b) const;
+  int stage_host(uint32_t s, uint32_t k, const rl_batch& hb, rl_batch& db);
+  void pack(uint32_t s, uint32_t k);
+  void note_combine(uint32_t s, uint32_t k);
+  void refresh_hot();
+  int submit(const rl_batch* batches, rl_status* const* out, uint32_t* const* thr, bool host);
+  int wait(rl_status* const* out, uint32_t* const* thr, bool into);
+  int submit_rccl(uint32_t k);
+  int submit_local(uint32_t k);
+  void wait_rccl(uint32_t k);
+  void wait_local(uint32_t k);
+  int step_result(uint32_t k);
 };
 
 void rl_router::free_all() {
-  for (ShardBufs& s : sh) {
-    for (void* p : {s.send, (void*)s.d_cnt, (void*)s.perm, s.recv, s.reply, s.back})
-      if (p) (void)hipFree(p);
+  for (Shard& s : sh) {
+    for (ShardStep& t : s.st) {
+      for (void* p : {(void*)t.pb.send, (void*)t.pb.perm, (void*)t.pb.bhs, (void*)t.pb.bstat, (void*)t.zero,
+                      (void*)t.pb.hot_pos, (void*)t.recv, (void*)t.reply, (void*)t.back, (void*)t.d_x,
+                      (void*)t.hs.d_in, (void*)t.hs.d_out, (void*)t.hs.d_thr})
+        if (p) (void)hipFree(p);
+      for (void* p : {(void*)t.h_x, (void*)t.hs.h_in, (void*)t.hs.h_out, (void*)t.hs.h_thr})
+        if (p) (void)hipHostFree(p);
+    }
+    if (s.d_hot) (void)hipFree(s.d_hot);
+    if (s.h_hot) (void)hipHostFree(s.h_hot);
+    if (s.ev_hot) (void)hipEventDestroy(s.ev_hot);
+    if (s.ev) (void)hipEventDestroy(s.ev);
+    if (s.os) (void)hipStreamDestroy(s.os);
   }
   sh.clear();
-  if (d_x) (void)hipFree(d_x);
-  if (h_x) (void)hipHostFree(h_x);
+  if (d_ag) (void)hipFree(d_ag);
+  if (h_ag) (void)hipHostFree(h_ag);
   if (comm) (void)ncclCommDestroy(comm);
+  if (ev_rs) (void)hipEventDestroy(ev_rs);
   if (rs) (void)hipStreamDestroy(rs);
-  if (ev) (void)hipEventDestroy(ev);
-  ev = nullptr;
-  d_x = nullptr;
-  h_x = nullptr;
+  d_ag = nullptr;
+  h_ag = nullptr;
   comm = nullptr;
+  ev_rs = nullptr;
   rs = nullptr;
 }
 
-// Local transport: every shard's batch, all exchanges by copies on the router stream.
-int rl_router::step_local(const rl_batch* b, rl_status* const* out, uint32_t* const* thr) {
+int rl_router::alloc_shard(Shard& s) {
   const uint32_t G = cfg.n_shards;
-  const double t0 = now_us();
-  int first_err = 0;
-  for (uint32_t s = 0; s < G; ++s) {
-    const int rc = rl_route_pack(sh[s].e, &b[s], s, G, sh[s].send, sh[s].d_cnt, sh[s].perm, sh[s].cnt);
-    st.status[s] = rc;
-    if (rc && !first_err) {
-      first_err = rc;
-      fail(rc, "shard %u (pack): %s", s, rl_last_error(sh[s].e));
-    }
-  }
-  const double t1 = now_us();
-  st.pack_us = t1 - t0;
-  if (first_err) return first_err;
-  for (uint32_t j = 0; j < G; ++j) st.sent[j] = sh[0].cnt[j];
-  // records: owner j receives origin 0's group j, then origin 1's, ...
-  std::vector<uint64_t> sdis(G * G), rdis(G * G);  // [i*G+j]: record offset of (origin i, owner j)
-  for (uint32_t i = 0; i < G; ++i) {
-    uint64_t o = 0;
-    for (uint32_t j = 0; j < G; ++j) {
-      sdis[i * G + j] = o;
-      o += sh[i].cnt[j];
-    }
-  }
-  for (uint32_t j = 0; j < G; ++j) {
-    uint64_t o = 0;
-    for (uint32_t i = 0; i < G; ++i) {
-      rdis[i * G + j] = o;
-      o += sh[i].cnt[j];
-    }
-    st.recv[j] = (uint32_t)o;
-  }
+  const size_t D = cfg.max_desc;
   hipError_t he = hipSuccess;
-  for (uint32_t i = 0; i < G && he == hipSuccess; ++i)
-    for (uint32_t j = 0; j < G && he == hipSuccess; ++j)
-      if (sh[i].cnt[j])
-        he = hipMemcpyAsync(static_cast<uint8_t*>(sh[j].recv) + rdis[i * G + j] * REC,
-                            static_cast<const uint8_t*>(sh[i].send) + sdis[i * G + j] * REC, (size_t)sh[i].cnt[j] * REC,
-                            hipMemcpyDeviceToDevice, rs);
-  if (he == hipSuccess) he = hipStreamSynchronize(rs);
-  if (int rc = hip(he, "record exchange")) return rc;
-  const double t2 = now_us();
-  st.exchange_us = t2 - t1;
-  // owners decide one after another (logical shards share the device; each alone is the
-  // model of one GPU, so decide_max_us is the step's critical path on G real GPUs)
-  st.decide_max_us = 0;
-  for (uint32_t j = 0; j < G; ++j) {
-    const double a = now_us();
-    int rc = 0;
-    if (st.recv[j]) {
-      rc = rl_submit_routed(sh[j].e, sh[j].recv, st.recv[j], sh[j].reply);
-      if (!rc) rc = rl_wait(sh[j].e);
-    }
-    const double d = now_us() - a;
-    st.decide_max_us = d > st.decide_max_us ? d : st.decide_max_us;
-    st.status[j] = rc;
-    if (rc && !first_err) {
-      first_err = rc;
-      fail(rc, "shard %u (decide): %s", j, rl_last_error(sh[j].e));
+  auto chk = [&](hipError_t x) { if (x != hipSuccess && he == hipSuccess) he = x; };
+  chk(hipStreamCreateWithFlags(&s.os, hipStreamNonBlocking));
+  chk(hipEventCreateWithFlags(&s.ev, hipEventDisableTiming));
+  chk(hipEventCreateWithFlags(&s.ev_hot, hipEventDisableTiming));
+  chk(hipMalloc(&s.d_hot, sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX)));
+  chk(hipHostMalloc(&s.h_hot, sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX), hipHostMallocDefault));
+  if (he == hipSuccess) chk(hipEventRecord(s.ev_hot, s.os));
+  const size_t lbw = route2_lb_words((uint32_t)D);
+  for (ShardStep& t : s.st) {
+    chk(hipMalloc(&t.pb.send, D * G * REC));
+    chk(hipMalloc(&t.pb.perm, D * 4 + 64));
+    chk(hipMalloc(&t.pb.bhs, route2_bhs_words((uint32_t)D) * 4 + 64));
+    chk(hipMalloc(&t.pb.bstat, (size_t)route2_blocks((uint32_t)D) * 16 + 64));
+    chk(hipMalloc(&t.pb.hot_pos, (size_t)HOT_MAX * 8));  // hot_pos | hot_tot
+    t.pb.hot_tot = t.pb.hot_pos + HOT_MAX;
+    // zeroed per step: two look-back areas and the control words; the hot scan's u64 sums follow
+    t.zero_bytes = (2 * lbw + 16) * 4;
+    chk(hipMalloc(&t.zero, t.zero_bytes + (size_t)HOT_MAX * 8 + 64));
+    t.pb.lb = reinterpret_cast<uint32_t*>(t.zero);
+    t.pb.rctl = t.pb.lb + 2 * lbw;
+    chk(hipMalloc(&t.recv, D * G * REC));
+    chk(hipMalloc(&t.reply, D * G * RAWB));
+    chk(hipMalloc(&t.back, D * G * RAWB));
+    chk(hipMalloc(&t.d_x, 8 * MAXS * 4));
+    chk(hipHostMalloc(&t.h_x, (HX_HOT + HOT_MAX + 16) * 4, hipHostMallocDefault));
+    t.pb.x = reinterpret_cast<uint32_t*>(t.d_x);
+    if (cfg.flags & RL_ROUTER_HOST) {
+      chk(hipMalloc(&t.hs.d_in, in_bytes));
+      chk(hipHostMalloc(&t.hs.h_in, in_bytes, hipHostMallocDefault));
+      chk(hipMalloc(&t.hs.d_out, D * sizeof(rl_status) + 64));
+      chk(hipHostMalloc(&t.hs.h_out, D * sizeof(rl_status) + 64, hipHostMallocDefault));
+      chk(hipMalloc(&t.hs.d_thr, D * 4 + 64));
+      chk(hipHostMalloc(&t.hs.h_thr, D * 4 + 64, hipHostMallocDefault));
     }
   }
-  const double t3 = now_us();
-  st.decide_us = t3 - t2;
-  if (first_err) return first_err;
-  for (uint32_t i = 0; i < G && he == hipSuccess; ++i)
-    for (uint32_t j = 0; j < G && he == hipSuccess; ++j)
-      if (sh[i].cnt[j])
-        he = hipMemcpyAsync(static_cast<uint8_t*>(sh[i].back) + sdis[i * G + j] * REP,
-                            static_cast<const uint8_t*>(sh[j].reply) + rdis[i * G + j] * REP,
-                            (size_t)sh[i].cnt[j] * REP, hipMemcpyDeviceToDevice, rs);
-  if (he == hipSuccess) he = hipStreamSynchronize(rs);
-  if (int rc = hip(he, "reply exchange")) return rc;
-  const double t4 = now_us();
-  st.reply_us = t4 - t3;
-  for (uint32_t i = 0; i < G; ++i) {
-    int rc = rl_route_unpack(sh[i].e, &b[i], sh[i].perm, sh[i].back, out[i], thr[i]);
-    if (!rc) rc = hip(hipStreamSynchronize((hipStream_t)rl_stream(sh[i].e)), "unpack");
-    else fail(rc, "shard %u (unpack): %s", i, rl_last_error(sh[i].e));
-    if (rc) return rc;
-  }
-  st.unpack_us = now_us() - t4;
+  return he == hipSuccess ? 0 : fail(RL_EHIP, "router allocation: %s", hipGetErrorString(he));
+}
+
+int rl_router::validate(const rl_batch& b) const {
+  if (b.n_desc > cfg.max_desc) return RL_ECAPACITY;
+  if (b.reserved || b.n_req > RL_ROUTE_MAX_REQ || (b.n_desc && !b.n_req)) return RL_EINVAL;
+  if (b.n_desc && (!b.prefix_blob || !b.prefix_off || !b.rule_id || !b.req_of)) return RL_EINVAL;
+  if (b.n_req && (!b.now || !b.hits_addend)) return RL_EINVAL;
   return 0;
 }
 
-// RCCL transport: this rank's batch; counts + status, records, replies + status over the
-// communicator. Every rank runs all three exchanges whatever its own status.
-//
-// Three host waits per step: the counts (the record exchange's split sizes), the owner's
-// decide (its status), and the end of the step. rl_route_pack_async writes the (count, status)
-// pairs on the device, so the pack needs no wait of its own; the router stream and the engine
-// stream are ordered by events around the record exchange and the unpack. The unpack runs
-// before the owners' statuses are read: when a step fails, out and thr hold garbage.
-int rl_router::step_rccl(const rl_batch* b, rl_status* out, uint32_t* thr) {
-  const uint32_t G = cfg.n_shards, me = cfg.rank;
-  ShardBufs& s = sh[0];
-  hipStream_t es = (hipStream_t)rl_stream(s.e);
-  const double t0 = now_us();
-  int rc_pack = RL_ECAPACITY;
-  std::string pack_msg = "batch exceeds the router's max_desc";
-  if (b->n_desc <= cfg.max_desc) {
-    rc_pack = rl_route_pack_strided(s.e, b, me, G, cfg.max_desc, s.send, reinterpret_cast<uint32_t*>(d_x), s.perm);
-    pack_msg = rc_pack ? rl_last_error(s.e) : "";
-  }
-  int32_t* hs = h_x;           // [2G] sent
-  int32_t* hr = h_x + 2 * G;   // [2G] received
-  hipError_t he;
-  if (rc_pack) {  // found on the host: no pairs on the device, send (0, rc_pack) to every owner
+// Host batch -> the slot's pinned staging (unless the caller built it there) -> device, on the
+// shard's origin stream ahead of its pack.
+int rl_router::stage_host(uint32_t s, uint32_t k, const rl_batch& b, rl_batch& d) {
+  ShardStep& t = sh[s].st[k];
+  uint8_t* h = t.hs.h_in;
+  if ((size_t)b.blob_bytes + RL_BLOB_SLACK > o_off || b.n_desc > cfg.max_desc || b.n_req > cfg.max_desc)
+    return RL_ECAPACITY;
+  struct Arr { const void* src; size_t o, n; } arrs[] = {
+      {b.prefix_blob, 0, b.blob_bytes}, {b.prefix_off, o_off, b.n_desc ? ((size_t)b.n_desc + 1) * 4 : 0},
+      {b.rule_id, o_rule, (size_t)b.n_desc * 4}, {b.req_of, o_req, (size_t)b.n_desc * 4},
+      {b.now, o_now, (size_t)b.n_req * 8}, {b.hits_addend, o_hits, (size_t)b.n_req * 4}};
+  for (auto& a : arrs)
+    if (a.n && a.src != h + a.o) memcpy(h + a.o, a.src, a.n);
+  memset(h + b.blob_bytes, 0, RL_BLOB_SLACK);  // the device reads prefixes in 16-B words
+  const size_t ext[] = {(size_t)b.blob_bytes + RL_BLOB_SLACK, arrs[1].n, arrs[2].n, arrs[3].n, arrs[4].n, arrs[5].n};
+  hipError_t he = hipSuccess;
+  for (int q = 0; q < 6 && he == hipSuccess; ++q)
+    if (ext[q]) he = hipMemcpyAsync(t.hs.d_in + arrs[q].o, h + arrs[q].o, ext[q], hipMemcpyHostToDevice, sh[s].os);
+  if (he != hipSuccess) return RL_EHIP;
+  d = b;
+  d.prefix_blob = t.hs.d_in;
+  d.prefix_off = reinterpret_cast<const uint32_t*>(t.hs.d_in + o_off);
+  d.rule_id = reinterpret_cast<const uint32_t*>(t.hs.d_in + o_rule);
+  d.req_of = reinterpret_cast<const uint32_t*>(t.hs.d_in + o_req);
+  d.now = reinterpret_cast<const int64_t*>(t.hs.d_in + o_now);
+  d.hits_addend = reinterpret_cast<const uint32_t*>(t.hs.d_in + o_hits);
+  return 0;
+}
+
+// Origin pack of shard s for slot k on its origin stream: the (count, status) pairs land in
+// d_x[0, 2G) and, with combining, the groups' sums and the control words in the pinned mirror.
+void rl_router::pack(uint32_t s, uint32_t k) {
+  Shard& S = sh[s];
+  ShardStep& t = S.st[k];
+  const uint32_t G = cfg.n_shards;
+  t.combined = false;
+  auto send_status = [&](int32_t rc) {  // pairs (0, rc) to every owner
     for (uint32_t j = 0; j < G; ++j) {
-      hs[2 * j] = 0;
-      hs[2 * j + 1] = rc_pack;
+      t.h_x[2 * j] = 0;
+      t.h_x[2 * j + 1] = rc;
     }
-    he = hipMemcpyAsync(d_x, hs, 8 * G, hipMemcpyHostToDevice, rs);
+    (void)hipMemcpyAsync(t.d_x, t.h_x, 8 * G, hipMemcpyHostToDevice, S.os);
+  };
+  if (t.rc_pack || !t.b.n_desc) {
+    send_status(t.rc_pack);
+    return;
+  }
+  const bool combine = !(cfg.flags & RL_ROUTER_NO_COMBINE) && !S.v.local_cache && !S.hot.empty();
+  (void)hipMemsetAsync(t.zero, 0, t.zero_bytes, S.os);
+  launch_route_pack2(S.os, t.b, S.v.rules, S.v.n_rules, S.v.seed, shard_id(s), G, cfg.max_desc,
+                     combine ? S.d_hot : nullptr, t.pb);
+  t.combined = combine;
+  if (combine) {
+    (void)hipMemcpyAsync(t.h_x + HX_HOT, t.pb.hot_tot, HOT_MAX * 4, hipMemcpyDeviceToHost, S.os);
+    (void)hipMemcpyAsync(t.h_x + HX_HOT + HOT_MAX, t.pb.rctl, 4 * 4, hipMemcpyDeviceToHost, S.os);
+  }
+  const hipError_t he = hipGetLastError();
+  if (he != hipSuccess || fault(PH_PACK, s)) {  // the pack cannot be trusted: fail the step everywhere
+    t.rc_pack = RL_EHIP;
+    t.msg = he != hipSuccess ? std::string("route pack: ") + hipGetErrorString(he) : "injected fault (pack)";
+    t.phase = "pack";
+    t.combined = false;
+    send_status(RL_EHIP);
+  }
+}
+
+// After the counts: did shard s's pack combine (its groups' sums keep the route hot set), or
+// did its batch need the repack (a hot group was not one key string)?
+void rl_router::note_combine(uint32_t s, uint32_t k) {
+  ShardStep& t = sh[s].st[k];
+  if (!t.combined) return;
+  const uint32_t* ctl = reinterpret_cast<const uint32_t*>(t.h_x + HX_HOT + HOT_MAX);
+  if (ctl[0]) {
+    if (s == 0) ++st.repacks;
+    sh[s].repacked = true;
+    t.combined = false;
   } else {
-    he = hipEventRecord(ev, es);
-    if (he == hipSuccess) he = hipStreamWaitEvent(rs, ev, 0);
+    memcpy(sh[s].last_tot, t.h_x + HX_HOT, sizeof sh[s].last_tot);
+    sh[s].last_valid = true;
+    if (s == 0) ++st.combined_steps;
   }
-  if (int rc = hip(he, "counts upload")) return rc;
-  if (int rc = nccl(ncclAllToAll(d_x, d_x + 2 * G, 2, ncclInt32, comm, rs), "ncclAllToAll(counts)")) return rc;
-  he = hipMemcpyAsync(h_x, d_x, 16 * G, hipMemcpyDeviceToHost, rs);  // sent and received pairs
+}
+
+// Route hot set refresh (every ROUTE_HOT_EVERY steps, at the same step on every shard): keep the
+// groups this origin still sends with >= ROUTE_HOT_KEEP hits per step, add the owners' hot keys
+// (each engine's own hot set: prefixes that reach it with many records per batch; over RCCL
+// gathered from every rank), up to HOT_MAX. A shard that had to repack starts over.
+void rl_router::refresh_hot() {
+  std::vector<HotKey> cand;
+  if (rccl) {
+    std::vector<HotKey> mine;
+    rlx_engine_hot(sh[0].e, mine);
+    for (uint32_t i = 0; i < HOT_MAX; ++i) {
+      AgEntry& a = h_ag[i];
+      memset(&a, 0, sizeof a);
+      if (i < mine.size()) a = AgEntry{mine[i].a, mine[i].b, mine[i].unit, mine[i].rule, std::max(1u, mine[i].count), 0};
+    }
+    const size_t n = HOT_MAX * sizeof(AgEntry);
+    hipError_t he = hipMemcpyAsync(d_ag, h_ag, n, hipMemcpyHostToDevice, rs);
+    const ncclResult_t nr = ncclAllGather(d_ag, d_ag + HOT_MAX, n, ncclUint8, comm, rs);
+    if (nr != ncclSuccess) {
+      nccl_fail(nr, "ncclAllGather(hot sets)");
+      return;
+    }
+    if (he == hipSuccess) he = hipMemcpyAsync(h_ag + HOT_MAX, d_ag + HOT_MAX, n * cfg.n_shards, hipMemcpyDeviceToHost, rs);
+    if (he == hipSuccess) he = hipStreamSynchronize(rs);
+    if (he != hipSuccess) return;  // keep the current sets (decisions do not depend on them)
+    for (uint32_t i = 0; i < HOT_MAX * cfg.n_shards; ++i) {
+      const AgEntry& a = h_ag[HOT_MAX + i];
+      if (a.count) cand.push_back(HotKey{a.a, a.b, a.unit, a.rule, a.count});
+    }
+  } else {
+    for (Shard& s : sh) {
+      std::vector<HotKey> h;
+      rlx_engine_hot(s.e, h);
+      cand.insert(cand.end(), h.begin(), h.end());
+    }
+  }
+  std::stable_sort(cand.begin(), cand.end(), [](const HotKey& x, const HotKey& y) { return x.count > y.count; });
+  for (Shard& s : sh) {
+    std::vector<HotKey> next;
+    std::unordered_set<uint64_t> seen;
+    if (!s.repacked && s.last_valid)
+      for (size_t i = 0; i < s.hot.size(); ++i)
+        if (s.last_tot[i] >= ROUTE_HOT_KEEP) {
+          HotKey k = s.hot[i];
+          k.count = s.last_tot[i];
+          seen.insert(k.a);
+          next.push_back(k);
+        }
+    for (const HotKey& c : cand) {
+      if (next.size() >= (size_t)HOT_MAX) break;
+      if (!seen.insert(c.a).second) continue;  // (a prefix seen with a second rule: the pack repacks)
+      next.push_back(c);
+    }
+    s.repacked = false;
+    bool same = next.size() == s.hot.size();
+    for (size_t i = 0; same && i < next.size(); ++i)
+      same = next[i].a == s.hot[i].a && next[i].b == s.hot[i].b && next[i].rule == s.hot[i].rule;
+    if (same) continue;
+    std::vector<HotEntry> t;
+    build_hot_table(next, t);
+    // the staging's previous copy is done; the next pack is ordered behind this copy on os
+    if (hipEventSynchronize(s.ev_hot) != hipSuccess) continue;
+    memcpy(s.h_hot, t.data(), sizeof(HotEntry) * t.size());
+    if (hipMemcpyAsync(s.d_hot, s.h_hot, sizeof(HotEntry) * t.size(), hipMemcpyHostToDevice, s.os) != hipSuccess)
+      continue;
+    (void)hipEventRecord(s.ev_hot, s.os);
+    s.hot = std::move(next);
+    s.last_valid = false;
+  }
+}
+
+// RCCL: counts (+ pack statuses), then records; the owner batch is handed to the engine.
+int rl_router::submit_rccl(uint32_t k) {
+  const uint32_t G = cfg.n_shards, me = cfg.rank;
+  Shard& S = sh[0];
+  ShardStep& t = S.st[k];
+  const double t0 = t_pack0;
+  hipError_t he = hipEventRecord(S.ev, S.os);
+  if (he == hipSuccess) he = hipStreamWaitEvent(rs, S.ev, 0);
+  ncclResult_t nr = ncclAllToAll(t.d_x, t.d_x + 2 * G, 2, ncclInt32, comm, rs);
+  if (nr != ncclSuccess) return nccl_fail(nr, "ncclAllToAll(counts)");
+  if (he == hipSuccess) he = hipMemcpyAsync(t.h_x, t.d_x, 16 * G, hipMemcpyDeviceToHost, rs);
   if (he == hipSuccess) he = hipStreamSynchronize(rs);
-  if (int rc = hip(he, "counts exchange")) return rc;
-  if (!rc_pack && hs[1]) {  // the device found the batch malformed (rl_route_pack's checks)
-    rc_pack = hs[1];
-    pack_msg = "rl_route_pack_async: batch references an unknown rule id or request index, malformed prefix "
-               "offsets, or a time outside [0, 0xFFFD0000]";
+  if (he != hipSuccess) {  // the counts are unknown: nobody can take part in the record exchange
+    broken = true;
+    if (comm) (void)ncclCommAbort(comm);
+    comm = nullptr;
+    return fail(RL_ECOMM, "counts exchange: %s (communicator aborted)", hipGetErrorString(he));
   }
-  const double t1 = now_us();
-  st.pack_us = t1 - t0;
-  int first_err = 0;
+  const int32_t* hs = t.h_x;
+  const int32_t* hr = t.h_x + 2 * G;
+  if (!t.rc_pack && hs[1]) {  // the device refused the pack (one status in every owner's pair)
+    t.rc_pack = hs[1];
+    t.msg = t.rc_pack == RL_EDEVICE ? "route pack: the device's look-back spin limit expired (device fault)"
+                                    : "route pack: batch references an unknown rule id or request index, malformed "
+                                      "prefix offsets, or a time outside [0, 0xFFFD0000]";
+    t.phase = "pack";
+  }
+  st.pack_us = now_us() - t0;
+  bool any = false;
   for (uint32_t j = 0; j < G; ++j) {
-    s.cnt[j] = rc_pack ? 0u : (uint32_t)hs[2 * j];
-    st.status[j] = hr[2 * j + 1];
-    if (hr[2 * j + 1] && !first_err) first_err = j == me ? hr[2 * j + 1] : RL_EPEER;
+    t.cnt[j] = t.rc_pack ? 0u : (uint32_t)hs[2 * j];
+    t.rcv[j] = (uint32_t)hr[2 * j];
+    slot[k].status[j] = hr[2 * j + 1];
+    any |= hr[2 * j + 1] != 0;
   }
-  if (first_err) {  // every rank saw the same status words: all leave here together
-    if (rc_pack) return fail(rc_pack, "shard %u (pack): %s", me, pack_msg.c_str());
-    return fail(RL_EPEER, "a peer shard failed to pack its batch (see rl_router_stats.status)");
+  if (any) {  // every rank saw the same status words: all leave after this exchange
+    slot[k].counts_failed = true;
+    return 0;
   }
-  std::vector<size_t> sc(G), sd(G), rc_(G), rd(G);
-  uint64_t so = 0, ro = 0;
-  const size_t D = cfg.max_desc;  // owner stride of the send and back buffers (rl_route_pack_strided)
+  note_combine(0, k);
+  // records: to owner j this origin's section j (stride D); from origin j its count, compact
+  const size_t D = cfg.max_desc;
+  std::vector<size_t> sc(G), sd(G), rc(G), rd(G);
+  uint64_t ro = 0;
   for (uint32_t j = 0; j < G; ++j) {
-    sc[j] = (size_t)s.cnt[j] * REC;
+    sc[j] = (size_t)t.cnt[j] * REC;
     sd[j] = j * D * REC;
-    rc_[j] = (size_t)(uint32_t)hr[2 * j] * REC;
+    rc[j] = (size_t)t.rcv[j] * REC;
     rd[j] = ro;
-    ro += rc_[j];
-    st.sent[j] = s.cnt[j];
+    ro += rc[j];
+    st.sent[j] = t.cnt[j];
   }
-  const uint32_t n_in = (uint32_t)(ro / REC);
-  for (uint32_t j = 0; j < G; ++j) st.recv[j] = j == me ? n_in : 0;
-  if (int rc = nccl(ncclAllToAllv(s.send, sc.data(), sd.data(), s.recv, rc_.data(), rd.data(), ncclUint8, comm, rs),
-                    "ncclAllToAllv(records)"))
-    return rc;
-  he = hipEventRecord(ev, rs);  // the owner's decide reads the received records
-  if (he == hipSuccess) he = hipStreamWaitEvent(es, ev, 0);
-  if (int rc = hip(he, "record exchange")) return rc;
-  const double t2 = now_us();
-  st.exchange_us = t2 - t1;  // enqueue only: the exchange's time is inside decide_us
-  int rc_dec = 0;
-  if (n_in) {
-    rc_dec = rl_submit_routed(s.e, s.recv, n_in, s.reply);
-    if (!rc_dec) rc_dec = rl_wait(s.e);
+  t.n_in = (uint32_t)(ro / REC);
+  for (uint32_t j = 0; j < G; ++j) st.recv[j] = j == me ? t.n_in : 0;
+  nr = ncclAllToAllv(t.pb.send, sc.data(), sd.data(), t.recv, rc.data(), rd.data(), ncclUint8, comm, rs);
+  if (nr != ncclSuccess) return nccl_fail(nr, "ncclAllToAllv(records)");
+  const double t1 = now_us();
+  he = hipEventRecord(ev_rs, rs);
+  if (fault(PH_RECORDS, 0)) he = hipErrorUnknown;
+  if (he != hipSuccess) {  // keep going: the failure travels in the reply exchange
+    t.rc_local = RL_EHIP;
+    t.msg = std::string("record exchange: ") + (he == hipErrorUnknown ? "injected fault (records)" : hipGetErrorString(he));
+    t.phase = "records";
+  } else if (t.n_in) {
+    ShardStep& prev = S.st[k ^ 1u];
+    t.rc_dec = rl_submit_routed_async(S.e, t.recv, t.n_in, t.reply, RL_ROUTED_RAW, ev_rs);
+    if (t.rc_dec == RL_ESTATE && prev.submitted) {
+      // an engine that cannot pipeline (LSD only): finish the previous owner batch first
+      const int rp = rl_wait(S.e);
+      if (rp) {
+        prev.rc_dec = rp;
+        prev.msg = rl_last_error(S.e);
+        prev.phase = "decide";
+      }
+      prev.submitted = false;
+      t.rc_dec = rl_submit_routed_async(S.e, t.recv, t.n_in, t.reply, RL_ROUTED_RAW, ev_rs);
+    }
+    if (t.rc_dec) {
+      t.msg = rl_last_error(S.e);
+      t.phase = "decide";
+    }
+    t.submitted = t.rc_dec == 0;
   }
-  std::string dec_msg = rc_dec ? rl_last_error(s.e) : "";
-  if (!n_in) {  // nothing decided: the exchange still has to be complete before the replies
-    if (int rc = hip(hipStreamSynchronize(es), "record exchange")) return rc;
+  st.exchange_us = now_us() - t1;
+  return 0;
+}
+
+// Local transport: every shard's counts on the host, records by device copies; the owners
+// decide one after another, each timed alone (each models one GPU: decide_max_us is the step's
+// critical path on G real GPUs).
+int rl_router::submit_local(uint32_t k) {
+  const uint32_t G = cfg.n_shards;
+  const double t0 = t_pack0;
+  for (uint32_t s = 0; s < G; ++s) {
+    ShardStep& t = sh[s].st[k];
+    hipError_t he = hipMemcpyAsync(t.h_x, t.d_x, 8 * G, hipMemcpyDeviceToHost, sh[s].os);
+    if (he == hipSuccess) he = hipStreamSynchronize(sh[s].os);
+    if (he != hipSuccess && !t.rc_pack) {
+      t.rc_pack = RL_EHIP;
+      t.msg = std::string("counts: ") + hipGetErrorString(he);
+      t.phase = "pack";
+    }
+    if (!t.rc_pack && t.h_x[1]) {
+      t.rc_pack = t.h_x[1];
+      t.msg = t.rc_pack == RL_EDEVICE ? "route pack: the device's look-back spin limit expired (device fault)"
+                                      : "route pack: batch references an unknown rule id or request index, malformed "
+                                        "prefix offsets, or a time outside [0, 0xFFFD0000]";
+      t.phase = "pack";
+    }
+    slot[k].status[s] = t.rc_pack;
   }
-  const double t3 = now_us();
-  st.decide_us = st.decide_max_us = t3 - t2;
-  for (uint32_t j = 0; j < G; ++j) hs[j] = rc_dec;
-  he = hipMemcpyAsync(d_x, hs, 4 * G, hipMemcpyHostToDevice, rs);
-  if (int rc = hip(he, "status upload")) return rc;
-  // replies go back with the reverse splits; the status words ride in the same group
+  st.pack_us = now_us() - t0;
+  bool any = false;
+  for (uint32_t s = 0; s < G; ++s) any |= sh[s].st[k].rc_pack != 0;
+  if (any) {
+    slot[k].counts_failed = true;
+    return 0;
+  }
+  for (uint32_t s = 0; s < G; ++s) {
+    ShardStep& t = sh[s].st[k];
+    for (uint32_t j = 0; j < G; ++j) t.cnt[j] = (uint32_t)t.h_x[2 * j];
+    note_combine(s, k);
+  }
+  for (uint32_t j = 0; j < G; ++j) st.sent[j] = sh[0].st[k].cnt[j];
+  const size_t D = cfg.max_desc;
+  hipError_t he = hipSuccess;
+  for (uint32_t j = 0; j < G; ++j) {  // owner j: origin 0's section j, then origin 1's, ...
+    uint64_t o = 0;
+    for (uint32_t i = 0; i < G; ++i) {
+      const uint32_t c = sh[i].st[k].cnt[j];
+      sh[j].st[k].rcv[i] = c;
+      if (c && he == hipSuccess)
+        he = hipMemcpyAsync(sh[j].st[k].recv + o, sh[i].st[k].pb.send + j * D, (size_t)c * REC,
+                            hipMemcpyDeviceToDevice, rs);
+      o += c;
+    }
+    sh[j].st[k].n_in = (uint32_t)o;
+    st.recv[j] = (uint32_t)o;
+  }
+  if (he == hipSuccess) he = hipStreamSynchronize(rs);
+  const double t1 = now_us();
+  st.exchange_us = t1 - t0 - st.pack_us;
+  st.decide_max_us = 0;
   for (uint32_t j = 0; j < G; ++j) {
-    sc[j] = (size_t)(uint32_t)hr[2 * j] * REP;  // to origin j: the replies to its records
-    rc_[j] = (size_t)s.cnt[j] * REP;
+    ShardStep& t = sh[j].st[k];
+    if (he != hipSuccess || fault(PH_RECORDS, j)) {
+      t.rc_local = RL_EHIP;
+      t.msg = he != hipSuccess ? std::string("record exchange: ") + hipGetErrorString(he) : "injected fault (records)";
+      t.phase = "records";
+      continue;
+    }
+    const double a = now_us();
+    if (t.n_in) {
+      t.rc_dec = rl_submit_routed_async(sh[j].e, t.recv, t.n_in, t.reply, RL_ROUTED_RAW, nullptr);
+      if (!t.rc_dec) t.rc_dec = rl_wait(sh[j].e);
+      if (t.rc_dec) {
+        t.msg = rl_last_error(sh[j].e);
+        t.phase = "decide";
+      }
+    }
+    st.decide_max_us = std::max(st.decide_max_us, now_us() - a);
   }
-  so = 0;
+  st.decide_us = now_us() - t1;
+  return 0;
+}
+
+int rl_router::submit(const rl_batch* batches, rl_status* const* out, uint32_t* const* thr, bool host) {
+  if (broken) return fail(RL_ECOMM, "the router's communicator was aborted after a transport failure");
+  const uint32_t k = (uint32_t)(seq % NSLOT);
+  if (slot[k].busy) return fail(RL_ESTATE, "two routed steps in flight: call rl_router_wait");
+  if (host && !(cfg.flags & RL_ROUTER_HOST)) return fail(RL_EINVAL, "router created without RL_ROUTER_HOST");
+  const uint32_t G = cfg.n_shards, nl = n_local();
+  if (!rccl)  // the local transport refuses a bad batch before anything moves (RCCL: in the counts exchange)
+    for (uint32_t s = 0; s < G; ++s)
+      if (batches[s].n_desc > cfg.max_desc)
+        return fail(RL_ECAPACITY, "shard %u: batch of %u descriptors exceeds the router's max_desc %u", s,
+                    batches[s].n_desc, cfg.max_desc);
+  for (uint32_t j = 0; j < MAXS; ++j) st.recv[j] = 0, st.sent[j] = 0, slot[k].status[j] = 0;
+  slot[k].t0 = now_us();
+  t_pack0 = slot[k].t0;
+  slot[k].host = host;
+  slot[k].counts_failed = false;
+  if (seq % ROUTE_HOT_EVERY == 0) {
+    refresh_hot();
+    if (broken) return RL_ECOMM;
+  }
+  for (uint32_t s = 0; s < nl; ++s) {
+    Shard& S = sh[s];
+    ShardStep& t = S.st[k];
+    t.rc_pack = t.rc_dec = t.rc_local = 0;
+    t.msg.clear();
+    t.phase = "";
+    t.submitted = false;
+    t.n_in = 0;
+    t.rc_pack = validate(batches[s]);
+    if (t.rc_pack) {
+      t.msg = "bad origin batch (capacity, reserved, request count or null arrays)";
+      t.phase = "pack";
+    }
+    if (host) {
+      t.out = t.hs.d_out;
+      t.thr = t.hs.d_thr;
+      if (!t.rc_pack) {
+        t.rc_pack = stage_host(s, k, batches[s], t.b);
+        if (t.rc_pack) {
+          t.msg = "host staging (capacity)";
+          t.phase = "pack";
+        }
+      }
+      if (t.rc_pack) t.b = rl_batch{};
+    } else {
+      t.b = batches[s];
+      t.out = out[s];
+      t.thr = thr[s];
+      if (t.rc_pack) t.b = rl_batch{};
+    }
+    const int rc = rlx_engine_view(S.e, &S.v);  // (rules may have been appended since)
+    if (rc && !t.rc_pack) {
+      t.rc_pack = rc;
+      t.msg = rl_last_error(S.e);
+      t.phase = "pack";
+    }
+    pack(s, k);
+    // local transport (logical shards on one device): one origin's pack at a time, so
+    // pack_us / G is one origin's pack (as on G GPUs)
+    if (!rccl) (void)hipStreamSynchronize(S.os);
+  }
+  slot[k].busy = true;
+  ++seq;
+  return rccl ? submit_rccl(k) : submit_local(k);
+}
+
+// The step's outcome from each shard's status: the first failing shard's code on that shard
+// (local transport: returned), RL_EPEER on the others.
+int rl_router::step_result(uint32_t k) {
+  const uint32_t G = cfg.n_shards;
+  for (uint32_t j = 0; j < MAXS; ++j) st.status[j] = j < G ? slot[k].status[j] : 0;
+  int bad = -1;
+  for (uint32_t j = 0; j < G && bad < 0; ++j)
+    if (st.status[j]) bad = (int)j;
+  if (bad < 0) return 0;
+  const int code = st.status[bad];
+  for (uint32_t j = 0; j < G; ++j)
+    if (st.status[j] == 0) st.status[j] = RL_EPEER;
+  if (rccl && (uint32_t)bad != cfg.rank) {
+    const int32_t own = st.status[cfg.rank];
+    const ShardStep& t = sh[0].st[k];
+    if (own != RL_EPEER) return fail(own, "shard %u (%s): %s", cfg.rank, t.phase, t.msg.c_str());
+    return fail(RL_EPEER, "shard %d failed this step with %d (see rl_router_stats.status)", bad, code);
+  }
+  const ShardStep& t = sh[rccl ? 0 : bad].st[k];
+  return fail(code, "shard %d (%s): %s", bad, t.phase, t.msg.c_str());
+}
+
+void rl_router::wait_rccl(uint32_t k) {
+  const uint32_t G = cfg.n_shards;
+  Shard& S = sh[0];
+  ShardStep& t = S.st[k];
+  const double t0 = now_us();
+  if (t.submitted) {
+    const int rc = rl_wait(S.e);
+    if (rc) {
+      t.rc_dec = rc;
+      t.msg = rl_last_error(S.e);
+      t.phase = "decide";
+    }
+    t.submitted = false;
+  }
+  if (!t.rc_dec && !t.rc_local && fault(PH_DECIDE, 0)) {
+    t.rc_dec = RL_EHIP;
+    t.msg = "injected fault (decide)";
+    t.phase = "decide";
+  }
+  st.decide_us = st.decide_max_us = now_us() - t0;
+  const double t1 = now_us();
+  int32_t* hs = t.h_x + 4 * G;  // statuses sent | received
+  int32_t mine = t.rc_dec ? t.rc_dec : t.rc_local;
+  if (!mine && fault(PH_REPLIES, 0)) {
+    mine = t.rc_local = RL_EHIP;
+    t.msg = "injected fault (replies)";
+    t.phase = "replies";
+  }
+  for (uint32_t j = 0; j < G; ++j) hs[j] = mine;
+  hipError_t he = hipMemcpyAsync(t.d_x + 4 * G, hs, 4 * G, hipMemcpyHostToDevice, rs);
+  // replies: to origin j the replies to its records (compact), into its back buffer at my section
+  const size_t D = cfg.max_desc;
+  std::vector<size_t> sc(G), sd(G), rc(G), rd(G);
+  uint64_t so = 0;
   for (uint32_t j = 0; j < G; ++j) {
+    sc[j] = (size_t)t.rcv[j] * RAWB;
     sd[j] = so;
     so += sc[j];
-    rd[j] = j * D * REP;  // perm[i] = owner * D + position
+    rc[j] = (size_t)t.cnt[j] * RAWB;
+    rd[j] = j * D * RAWB;  // perm = owner * D + position
   }
   ncclResult_t nr = ncclGroupStart();
-  if (nr == ncclSuccess) nr = ncclAllToAll(d_x, d_x + 2 * G, 1, ncclInt32, comm, rs);
+  if (nr == ncclSuccess) nr = ncclAllToAll(t.d_x + 4 * G, t.d_x + 5 * G, 1, ncclInt32, comm, rs);
   if (nr == ncclSuccess)
-    nr = ncclAllToAllv(s.reply, sc.data(), sd.data(), s.back, rc_.data(), rd.data(), ncclUint8, comm, rs);
+    nr = ncclAllToAllv(t.reply, sc.data(), sd.data(), t.back, rc.data(), rd.data(), ncclUint8, comm, rs);
   const ncclResult_t ne = ncclGroupEnd();
-  if (int rc = nccl(nr != ncclSuccess ? nr : ne, "ncclAllToAll(replies)")) return rc;
-  int32_t* hst = h_x + 4 * G;  // the owners' statuses (own pinned words: hs is still being uploaded)
-  he = hipMemcpyAsync(hst, d_x + 2 * G, 4 * G, hipMemcpyDeviceToHost, rs);
-  if (he == hipSuccess) he = hipEventRecord(ev, rs);
-  if (he == hipSuccess) he = hipStreamWaitEvent(es, ev, 0);
-  if (int rc = hip(he, "reply exchange")) return rc;
-  int rc = rl_route_unpack(s.e, b, s.perm, s.back, out, thr);
-  if (rc) {
-    (void)hipStreamSynchronize(rs);  // the exchange is complete before the error returns
-    return fail(rc, "shard %u (unpack): %s", me, rl_last_error(s.e));
+  if (nr != ncclSuccess || ne != ncclSuccess) {
+    nccl_fail(nr != ncclSuccess ? nr : ne, "ncclAllToAll(replies)");
+    return;
   }
-  if ((rc = hip(hipStreamSynchronize(es), "reply exchange and unpack"))) return rc;
-  st.reply_us = now_us() - t3;
-  st.unpack_us = 0;  // inside reply_us
+  if (he == hipSuccess) he = hipMemcpyAsync(t.h_x + 5 * G, t.d_x + 5 * G, 4 * G, hipMemcpyDeviceToHost, rs);
+  if (he == hipSuccess) he = hipEventRecord(ev_rs, rs);
+  if (he == hipSuccess) he = hipStreamWaitEvent(S.os, ev_rs, 0);
+  st.reply_us = now_us() - t1;
+  const double t2 = now_us();
+  if (he == hipSuccess && t.b.n_req) he = hipMemsetAsync(t.thr, 0, (size_t)t.b.n_req * 4, S.os);
+  if (he == hipSuccess) {
+    launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.out, t.thr);
+    he = hipGetLastError();
+  }
+  if (he == hipSuccess && slot[k].host) {
+    if (t.b.n_desc)
+      he = hipMemcpyAsync(t.hs.h_out, t.out, (size_t)t.b.n_desc * sizeof(rl_status), hipMemcpyDeviceToHost, S.os);
+    if (he == hipSuccess && t.b.n_req) he = hipMemcpyAsync(t.hs.h_thr, t.thr, (size_t)t.b.n_req * 4, hipMemcpyDeviceToHost, S.os);
+  }
+  const hipError_t h2 = hipStreamSynchronize(rs);
+  if (he == hipSuccess) he = h2;
+  if (he == hipSuccess) he = hipStreamSynchronize(S.os);
+  if (he == hipSuccess && fault(PH_UNPACK, 0)) he = hipErrorUnknown;
+  st.unpack_us = now_us() - t2;
+  for (uint32_t j = 0; j < G; ++j) slot[k].status[j] = h2 == hipSuccess ? t.h_x[5 * G + j] : RL_EHIP;
+  if (he != hipSuccess) {  // after the last collective: only this shard's results are lost
+    slot[k].status[cfg.rank] = RL_EHIP;
+    t.msg = std::string("reply exchange / unpack: ") +
+            (he == hipErrorUnknown ? "injected fault (unpack)" : hipGetErrorString(he));
+    t.phase = "unpack";
+  }
+}
+
+void rl_router::wait_local(uint32_t k) {
+  const uint32_t G = cfg.n_shards;
+  const size_t D = cfg.max_desc;
+  const double t0 = now_us();
   for (uint32_t j = 0; j < G; ++j) {
-    st.status[j] = hst[j];
-    if (hst[j] && !first_err) first_err = j == me ? hst[j] : RL_EPEER;
+    ShardStep& t = sh[j].st[k];
+    if (!t.rc_dec && !t.rc_local && fault(PH_DECIDE, j)) {
+      t.rc_dec = RL_EHIP;
+      t.msg = "injected fault (decide)";
+      t.phase = "decide";
+    }
+    if (!t.rc_dec && !t.rc_local && fault(PH_REPLIES, j)) {
+      t.rc_local = RL_EHIP;
+      t.msg = "injected fault (replies)";
+      t.phase = "replies";
+    }
+    slot[k].status[j] = t.rc_dec ? t.rc_dec : t.rc_local;
   }
-  if (first_err) {
-    if (rc_dec) return fail(rc_dec, "shard %u (decide): %s", me, dec_msg.c_str());
-    return fail(RL_EPEER, "a peer shard failed to decide its records (see rl_router_stats.status)");
+  hipError_t he = hipSuccess;
+  for (uint32_t j = 0; j < G; ++j) {  // owner j's replies, origin-major, into each origin's section j
+    uint64_t o = 0;
+    for (uint32_t i = 0; i < G; ++i) {
+      const uint32_t c = sh[j].st[k].rcv[i];
+      if (c && he == hipSuccess)
+        he = hipMemcpyAsync(sh[i].st[k].back + j * D, sh[j].st[k].reply + o, (size_t)c * RAWB, hipMemcpyDeviceToDevice,
+                            rs);
+      o += c;
+    }
   }
-  return 0;
+  if (he == hipSuccess) he = hipStreamSynchronize(rs);
+  st.reply_us = now_us() - t0;
+  const double t1 = now_us();
+  for (uint32_t i = 0; i < G; ++i) {
+    Shard& S = sh[i];
+    ShardStep& t = S.st[k];
+    hipError_t hu = he;
+    if (hu == hipSuccess && t.b.n_req) hu = hipMemsetAsync(t.thr, 0, (size_t)t.b.n_req * 4, S.os);
+    if (hu == hipSuccess) {
+      launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.out, t.thr);
+      hu = hipGetLastError();
+    }
+    if (hu == hipSuccess && slot[k].host) {
+      if (t.b.n_desc)
+        hu = hipMemcpyAsync(t.hs.h_out, t.out, (size_t)t.b.n_desc * sizeof(rl_status), hipMemcpyDeviceToHost, S.os);
+      if (hu == hipSuccess && t.b.n_req)
+        hu = hipMemcpyAsync(t.hs.h_thr, t.thr, (size_t)t.b.n_req * 4, hipMemcpyDeviceToHost, S.os);
+    }
+    if (hu == hipSuccess) hu = hipStreamSynchronize(S.os);
+    if (hu == hipSuccess && fault(PH_UNPACK, i)) hu = hipErrorUnknown;
+    if (hu != hipSuccess && !slot[k].status[i]) {
+      slot[k].status[i] = RL_EHIP;
+      t.msg = std::string("reply exchange / unpack: ") +
+              (hu == hipErrorUnknown ? "injected fault (unpack)" : hipGetErrorString(hu));
+      t.phase = "unpack";
+    }
+  }
+  st.unpack_us = now_us() - t1;
+}
+
+int rl_router::wait(rl_status* const* out, uint32_t* const* thr, bool into) {
+  if (broken) return fail(RL_ECOMM, "the router's communicator was aborted after a transport failure");
+  const uint32_t k = (uint32_t)(done % NSLOT);
+  if (!slot[k].busy) return fail(RL_ESTATE, "rl_router_wait without a routed step in flight");
+  if (!slot[k].counts_failed) {
+    if (rccl) wait_rccl(k);
+    else wait_local(k);
+  }
+  slot[k].busy = false;
+  ++done;
+  if (broken) return RL_ECOMM;
+  const int rc = step_result(k);
+  const ShardStep& t0s = sh[0].st[k];
+  st.hot_groups = (uint32_t)sh[0].hot.size();
+  st.combined = 0;
+  if (t0s.combined)
+    for (uint32_t i = 0; i < HOT_MAX; ++i) st.combined += t0s.h_x[HX_HOT + i] != 0 ? 1u : 0u;
+  if (into && !rc && slot[k].host)
+    for (uint32_t s = 0; s < n_local(); ++s) {
+      const ShardStep& t = sh[s].st[k];
+      if (out && out[s] && t.b.n_desc) memcpy(out[s], t.hs.h_out, (size_t)t.b.n_desc * sizeof(rl_status));
+      if (thr && thr[s] && t.b.n_req) memcpy(thr[s], t.hs.h_thr, (size_t)t.b.n_req * 4);
+    }
+  st.step_us = now_us() - slot[k].t0;
+  ++st.steps;
+  return rc;
 }
 
 extern "C" {
@@ -330,9 +850,11 @@ int rl_router_unique_id(uint8_t* id_out) {
 
 int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_router** out) {
   if (!cfg || !engines || !out) return RL_EINVAL;
+  *out = nullptr;
   if (cfg->struct_size != sizeof(rl_router_config)) return RL_EINVAL;
   const uint32_t G = cfg->n_shards;
   if (G == 0 || G > MAXS || cfg->max_desc == 0 || cfg->max_desc > (1u << 27)) return RL_EINVAL;
+  if (cfg->flags & ~(uint32_t)(RL_ROUTER_NO_COMBINE | RL_ROUTER_HOST)) return RL_EINVAL;
   const bool rccl = cfg->rccl_id != nullptr;
   if (rccl && cfg->rank >= G) return RL_EINVAL;
   const uint32_t n_eng = rccl ? 1u : G;
@@ -343,57 +865,99 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
   r->cfg.rccl_id = nullptr;
   r->rccl = rccl;
   r->st.n_shards = G;
-  auto bail = [&](hipError_t he) {
+  {
+    const size_t N = cfg->max_desc, B = cfg->max_blob_bytes ? cfg->max_blob_bytes : (size_t)cfg->max_desc * 64;
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    r->o_off = al(B + RL_BLOB_SLACK);
+    r->o_rule = r->o_off + al((N + 1) * 4);
+    r->o_req = r->o_rule + al(N * 4);
+    r->o_now = r->o_req + al(N * 4);
+    r->o_hits = r->o_now + al(N * 8);
+    r->in_bytes = r->o_hits + al(N * 4);
+  }
+  if (const char* f = getenv("RL_ROUTER_FAULT")) {  // tests: "phase:shard"
+    static const char* const names[] = {"", "pack", "records", "decide", "replies", "unpack"};
+    char ph[32] = {0};
+    unsigned s = 0;
+    if (sscanf(f, "%31[a-z]:%u", ph, &s) == 2)
+      for (int p = 1; p <= PH_UNPACK; ++p)
+        if (!strcmp(ph, names[p])) {
+          r->fault_phase = p;
+          r->fault_shard = rccl ? (s == cfg->rank ? 0u : 0xFFFFFFFFu) : s;
+        }
+  }
+  auto bail = [&](int code) {
     r->free_all();
     delete r;
-    return he == hipSuccess ? RL_ECOMM : RL_EHIP;
+    return code;
   };
-  hipError_t he = hipStreamCreateWithFlags(&r->rs, hipStreamNonBlocking);
-  if (he != hipSuccess) return bail(he);
-  const size_t D = cfg->max_desc;
+  if (hipStreamCreateWithFlags(&r->rs, hipStreamNonBlocking) != hipSuccess) return bail(RL_EHIP);
+  if (hipEventCreateWithFlags(&r->ev_rs, hipEventDisableTiming) != hipSuccess) return bail(RL_EHIP);
   r->sh.resize(n_eng);
-  for (uint32_t s = 0; s < n_eng && he == hipSuccess; ++s) {
-    ShardBufs& b = r->sh[s];
-    b.e = engines[s];
-    // RCCL transport: owner-strided send / back buffers (rl_route_pack_strided); local: compact
-    he = hipMalloc(&b.send, D * (rccl ? G : 1) * REC);
-    if (he == hipSuccess) he = hipMalloc(&b.d_cnt, MAXS * 4);
-    if (he == hipSuccess) he = hipMalloc(&b.perm, D * 4);
-    if (he == hipSuccess) he = hipMalloc(&b.recv, D * G * REC);
-    if (he == hipSuccess) he = hipMalloc(&b.reply, D * G * REP);
-    if (he == hipSuccess) he = hipMalloc(&b.back, D * (rccl ? G : 1) * REP);
+  for (uint32_t s = 0; s < n_eng; ++s) {
+    r->sh[s].e = engines[s];
+    if (rlx_engine_view(engines[s], &r->sh[s].v)) return bail(RL_EINVAL);
+    if (r->alloc_shard(r->sh[s])) return bail(RL_EHIP);
   }
-  if (he == hipSuccess && rccl) {
-    he = hipMalloc(&r->d_x, 4 * G * 4);
-    if (he == hipSuccess) he = hipHostMalloc(&r->h_x, 5 * G * 4, hipHostMallocDefault);
-    if (he == hipSuccess) he = hipEventCreateWithFlags(&r->ev, hipEventDisableTiming);
-  }
-  if (he != hipSuccess) return bail(he);
   if (rccl) {
+    if (hipMalloc(&r->d_ag, sizeof(AgEntry) * HOT_MAX * (G + 1)) != hipSuccess ||
+        hipHostMalloc(&r->h_ag, sizeof(AgEntry) * HOT_MAX * (G + 1), hipHostMallocDefault) != hipSuccess)
+      return bail(RL_EHIP);
     ncclUniqueId id;
     memcpy(&id, cfg->rccl_id, RL_ROUTER_ID_BYTES);
     if (ncclCommInitRank(&r->comm, (int)G, id, (int)cfg->rank) != ncclSuccess) {
       r->comm = nullptr;
-      return bail(hipSuccess);
+      return bail(RL_ECOMM);
     }
   }
   *out = r;
   return 0;
 }
 
-int rl_router_step(rl_router* r, const rl_batch* batches, rl_status* const* d_out, uint32_t* const* d_thr) {
+int rl_router_submit(rl_router* r, const rl_batch* batches, rl_status* const* d_out, uint32_t* const* d_thr) {
   if (!r || !batches || !d_out || !d_thr) return RL_EINVAL;
-  if (!r->rccl)  // (the RCCL transport reports an oversized batch through the counts exchange)
-    for (uint32_t s = 0; s < r->cfg.n_shards; ++s)
-      if (batches[s].n_desc > r->cfg.max_desc)
-        return r->fail(RL_ECAPACITY, "shard %u: batch of %u descriptors exceeds the router's max_desc %u", s,
-                       batches[s].n_desc, r->cfg.max_desc);
-  for (uint32_t j = 0; j < MAXS; ++j) r->st.status[j] = 0, r->st.recv[j] = 0, r->st.sent[j] = 0;
-  const double t0 = now_us();
-  const int rc = r->rccl ? r->step_rccl(batches, d_out[0], d_thr[0]) : r->step_local(batches, d_out, d_thr);
-  r->st.step_us = now_us() - t0;
-  ++r->st.steps;
-  return rc;
+  return r->submit(batches, d_out, d_thr, false);
+}
+
+int rl_router_wait(rl_router* r) {
+  if (!r) return RL_EINVAL;
+  return r->wait(nullptr, nullptr, false);
+}
+
+int rl_router_step(rl_router* r, const rl_batch* batches, rl_status* const* d_out, uint32_t* const* d_thr) {
+  const int rc = rl_router_submit(r, batches, d_out, d_thr);
+  if (rc) return rc;
+  return rl_router_wait(r);
+}
+
+int rl_router_host_acquire(rl_router* r, uint32_t shard, rl_host_batch* out) {
+  if (!r || !out) return RL_EINVAL;
+  if (!(r->cfg.flags & RL_ROUTER_HOST)) return r->fail(RL_EINVAL, "router created without RL_ROUTER_HOST");
+  if (shard >= r->n_local()) return r->fail(RL_EINVAL, "shard %u out of range", shard);
+  const uint32_t k = (uint32_t)(r->seq % NSLOT);
+  if (r->slot[k].busy) return r->fail(RL_ESTATE, "two routed steps in flight: call rl_router_wait_into");
+  uint8_t* h = r->sh[shard].st[k].hs.h_in;
+  out->prefix_blob = h;
+  out->prefix_off = reinterpret_cast<uint32_t*>(h + r->o_off);
+  out->rule_id = reinterpret_cast<uint32_t*>(h + r->o_rule);
+  out->req_of = reinterpret_cast<uint32_t*>(h + r->o_req);
+  out->now = reinterpret_cast<int64_t*>(h + r->o_now);
+  out->hits_addend = reinterpret_cast<uint32_t*>(h + r->o_hits);
+  out->max_desc = r->cfg.max_desc;
+  out->max_req = r->cfg.max_desc;
+  out->max_blob = (uint32_t)(r->o_off - RL_BLOB_SLACK);
+  out->reserved = 0;
+  return 0;
+}
+
+int rl_router_submit_host(rl_router* r, const rl_batch* host_batches) {
+  if (!r || !host_batches) return RL_EINVAL;
+  return r->submit(host_batches, nullptr, nullptr, true);
+}
+
+int rl_router_wait_into(rl_router* r, rl_status* const* out, uint32_t* const* thr) {
+  if (!r) return RL_EINVAL;
+  return r->wait(out, thr, true);
 }
 
 int rl_router_get_stats(const rl_router* r, rl_router_stats* out) {
@@ -406,6 +970,10 @@ const char* rl_router_last_error(const rl_router* r) { return r ? r->err.c_str()
 
 void rl_router_destroy(rl_router* r) {
   if (!r) return;
+  // steps still in flight: complete them (every rank issued their collectives)
+  while (!r->broken && r->done < r->seq) (void)r->wait(nullptr, nullptr, false);
+  for (Shard& s : r->sh) (void)hipStreamSynchronize(s.os);
+  if (r->rs) (void)hipStreamSynchronize(r->rs);
   r->free_all();
   delete r;
 }

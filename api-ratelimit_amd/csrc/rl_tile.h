@@ -367,7 +367,8 @@ RL_DEV rl_status local_hit_status(uint32_t h, uint32_t reset, uint32_t shadow) {
 }
 
 // Decision of a descriptor whose INCRBY post-value is base + P (decide_one in rl_decide.h).
-// routed: a routed record's ThrottleMillis slot is its own position (idx), not its request.
+// routed (OUT_*): a routed record's ThrottleMillis slot is its own position (idx), not its
+// request; OUT_RAW writes the raw reply instead.
 RL_DEV void decide_at(uint32_t idx, uint32_t req, uint32_t rule, uint32_t h, uint32_t now_mod, uint64_t base,
                       uint64_t P, uint32_t freeze, const DevRule* __restrict__ rules, rl_status* __restrict__ out,
                       uint32_t* __restrict__ req_thr, int routed) {
@@ -383,7 +384,16 @@ RL_DEV void decide_at(uint32_t idx, uint32_t req, uint32_t rule, uint32_t h, uin
   si.base = base;
   si.freeze = freeze;
   si.pad = 0;
-  decide_one(o, si, rules[rule], out, req_thr, routed ? idx : req);
+  decide_one(o, si, rules[rule], out, req_thr, routed ? idx : req, routed);
+}
+
+// A local-cache hit (base_limiter.go:76-81), as a status or a raw reply (mode OUT_*).
+RL_DEV void emit_local_hit(rl_status* __restrict__ out, uint32_t i, uint32_t h, uint32_t reset, uint32_t shadow,
+                           int mode) {
+  if (mode == OUT_RAW)
+    emit_raw(out, i, 0u, RAW_LOCAL_HIT);
+  else
+    out[i] = local_hit_status(h, reset, shadow);
 }
 
 }  // namespace tile

@@ -40,7 +40,7 @@ STATUS_DTYPE = np.dtype([("code_flags", "<u4"), ("limit_remaining", "<u4"), ("re
 
 
 PIPELINE_FLAGS = {"v4": 0, "lsd": 1}  # rl_config.flags (RL_CFG_LSD_ONLY)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class RlConfig(C.Structure):
@@ -95,14 +95,18 @@ class RlHostBatch(C.Structure):
 # (name, argtypes, restype) of every symbol include/rl_hip.h declares
 class RlRouterConfig(C.Structure):
     _fields_ = [("struct_size", C.c_uint32), ("n_shards", C.c_uint32), ("rank", C.c_uint32), ("max_desc", C.c_uint32),
-                ("rccl_id", C.c_void_p)]
+                ("rccl_id", C.c_void_p), ("flags", C.c_uint32), ("max_blob_bytes", C.c_uint32)]
+
+
+ROUTER_NO_COMBINE, ROUTER_HOST = 1, 2  # rl_router_config.flags
 
 
 class RlRouterStats(C.Structure):
     _fields_ = [("steps", C.c_uint64), ("n_shards", C.c_uint32), ("status", C.c_int32 * 16), ("recv", C.c_uint32 * 16),
                 ("sent", C.c_uint32 * 16), ("pack_us", C.c_double), ("exchange_us", C.c_double),
                 ("decide_us", C.c_double), ("decide_max_us", C.c_double), ("reply_us", C.c_double),
-                ("unpack_us", C.c_double), ("step_us", C.c_double)]
+                ("unpack_us", C.c_double), ("step_us", C.c_double), ("hot_groups", C.c_uint32), ("combined", C.c_uint32),
+                ("repacks", C.c_uint64), ("combined_steps", C.c_uint64)]
 
 
 ROUTER_ID_BYTES = 128
@@ -136,6 +140,7 @@ ABI = [
     ("rl_route_pack_strided", [C.c_void_p, C.POINTER(RlBatch), C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p,
                                C.c_void_p, C.c_void_p], C.c_int),
     ("rl_submit_routed", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p], C.c_int),
+    ("rl_submit_routed_async", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p], C.c_int),
     ("rl_route_unpack", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     ("rl_load_tree", [C.c_void_p, C.POINTER(RlTreeNode), C.c_uint32, C.c_void_p, C.c_uint32], C.c_int),
     ("rl_resolve", [C.c_void_p, C.POINTER(RlResolveBatch), C.c_void_p], C.c_int),
@@ -143,6 +148,11 @@ ABI = [
     ("rl_router_unique_id", [C.c_void_p], C.c_int),
     ("rl_router_create", [C.POINTER(RlRouterConfig), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
     ("rl_router_step", [C.c_void_p, C.POINTER(RlBatch), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
+    ("rl_router_submit", [C.c_void_p, C.POINTER(RlBatch), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
+    ("rl_router_wait", [C.c_void_p], C.c_int),
+    ("rl_router_host_acquire", [C.c_void_p, C.c_uint32, C.POINTER(RlHostBatch)], C.c_int),
+    ("rl_router_submit_host", [C.c_void_p, C.POINTER(RlBatch)], C.c_int),
+    ("rl_router_wait_into", [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
     ("rl_router_get_stats", [C.c_void_p, C.POINTER(RlRouterStats)], C.c_int),
     ("rl_router_last_error", [C.c_void_p], C.c_char_p),
     ("rl_router_destroy", [C.c_void_p], None),
@@ -483,10 +493,12 @@ class Engine:
 class Router:
     """The routed step owned by the C ABI (rl_router_*): G engines in this process (local
     transport) or this rank's engine over an RCCL communicator (rccl_id from
-    router_unique_id() on one rank, shared out of band)."""
+    router_unique_id() on one rank, shared out of band). combine: hot-prefix combining
+    (DESIGN.md §5); host: pinned host staging for submit_host / wait_into."""
 
     def __init__(self, engines, max_desc: int, n_shards: Optional[int] = None, rank: int = 0,
-                 rccl_id: Optional[bytes] = None):
+                 rccl_id: Optional[bytes] = None, combine: bool = True, host: bool = False,
+                 max_blob_bytes: int = 0):
         self.lib = engines[0].lib
         self.engines = list(engines)
         cfg = RlRouterConfig()
@@ -494,6 +506,8 @@ class Router:
         cfg.n_shards = n_shards if n_shards is not None else len(engines)
         cfg.rank = rank
         cfg.max_desc = max_desc
+        cfg.flags = (0 if combine else ROUTER_NO_COMBINE) | (ROUTER_HOST if host else 0)
+        cfg.max_blob_bytes = max_blob_bytes
         self._id = None
         if rccl_id is not None:
             self._id = C.create_string_buffer(bytes(rccl_id), ROUTER_ID_BYTES)
@@ -504,6 +518,7 @@ class Router:
         if rc:
             raise RedisError(f"rl_router_create failed: {RL_ERRORS.get(rc, rc)}")
         self.n = len(engines)
+        self._keep = []  # ctypes arrays of steps in flight
 
     @staticmethod
     def unique_id(lib=None) -> bytes:
@@ -514,15 +529,71 @@ class Router:
             raise RedisError(f"rl_router_unique_id: {RL_ERRORS.get(rc, rc)}")
         return buf.raw
 
+    def _check(self, rc, what):
+        if rc:
+            raise RedisError(f"{what}: {RL_ERRORS.get(rc, rc)}: {self.lib.rl_router_last_error(self.h).decode()}", rc)
+
     def step(self, batches, out_ptrs, thr_ptrs):
         """batches: RlBatch per engine (device pointers); outputs: device pointers per engine."""
         arr = (RlBatch * self.n)(*batches)
         o = (C.c_void_p * self.n)(*out_ptrs)
         t = (C.c_void_p * self.n)(*thr_ptrs)
-        rc = self.lib.rl_router_step(self.h, arr, o, t)
-        if rc:
-            raise RedisError(f"rl_router_step: {RL_ERRORS.get(rc, rc)}: {self.lib.rl_router_last_error(self.h).decode()}",
-                             rc)
+        self._check(self.lib.rl_router_step(self.h, arr, o, t), "rl_router_step")
+
+    def submit(self, batches, out_ptrs, thr_ptrs):
+        """rl_router_submit: a step handed over, up to two in flight (wait() completes the oldest)."""
+        arr = (RlBatch * self.n)(*batches)
+        o = (C.c_void_p * self.n)(*out_ptrs)
+        t = (C.c_void_p * self.n)(*thr_ptrs)
+        self._keep.append((arr, o, t))
+        self._check(self.lib.rl_router_submit(self.h, arr, o, t), "rl_router_submit")
+
+    def wait(self):
+        try:
+            self._check(self.lib.rl_router_wait(self.h), "rl_router_wait")
+        finally:
+            if self._keep:
+                self._keep.pop(0)
+
+    def host_acquire(self, shard: int = 0) -> dict:
+        """rl_router_host_acquire: numpy views of the next step's pinned staging slot of a shard."""
+        hb = RlHostBatch()
+        self._check(self.lib.rl_router_host_acquire(self.h, shard, C.byref(hb)), "rl_router_host_acquire")
+
+        def view(ptr, n, dt):
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(n,))
+        return dict(blob=view(hb.prefix_blob, hb.max_blob, np.uint8), off=view(hb.prefix_off, hb.max_desc + 1, np.uint32),
+                    rule=view(hb.rule_id, hb.max_desc, np.uint32), req_of=view(hb.req_of, hb.max_desc, np.uint32),
+                    now=view(hb.now, hb.max_req, np.int64), hits=view(hb.hits_addend, hb.max_req, np.uint32))
+
+    def submit_host(self, batches):
+        """rl_router_submit_host: host Batch objects (or dicts from host_acquire with n_desc/n_req/blob_bytes)."""
+        structs = []
+        for b in batches:
+            if isinstance(b, dict):
+                s = RlBatch()
+                s.n_desc, s.n_req, s.blob_bytes, s.reserved = b["n_desc"], b["n_req"], b["blob_bytes"], 0
+                s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = (
+                    b[k].ctypes.data for k in ("blob", "off", "rule", "req_of", "now", "hits"))
+                structs.append(s)
+            else:
+                structs.append(_batch_struct(b))
+        arr = (RlBatch * self.n)(*structs)
+        self._keep.append((arr, batches))
+        self._check(self.lib.rl_router_submit_host(self.h, arr), "rl_router_submit_host")
+
+    def wait_into(self, sizes):
+        """rl_router_wait_into: sizes = [(n_desc, n_req)] per shard -> [(status array, throttle array)]."""
+        outs = [np.zeros(max(1, nd), STATUS_DTYPE) for nd, _ in sizes]
+        thrs = [np.zeros(max(1, nr), np.uint32) for _, nr in sizes]
+        o = (C.c_void_p * self.n)(*[x.ctypes.data for x in outs])
+        t = (C.c_void_p * self.n)(*[x.ctypes.data for x in thrs])
+        try:
+            self._check(self.lib.rl_router_wait_into(self.h, o, t), "rl_router_wait_into")
+        finally:
+            if self._keep:
+                self._keep.pop(0)
+        return [(outs[i][:nd], thrs[i][:nr]) for i, (nd, nr) in enumerate(sizes)]
 
     def stats(self) -> dict:
         s = RlRouterStats()

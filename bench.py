@@ -69,7 +69,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=[2, 3])
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3],
+                    help="BASELINE config: 3 (headline), 2, or 1 (examples/ratelimit rules, 10k keys: the CPU row)")
     ap.add_argument("--desc", type=int, default=1_000_000, help="descriptors per batch")
     ap.add_argument("--batches-per-second", type=int, default=8000,
                     help="batches per SECOND window (now advances once every K batches); 1 = round-1 mode")
@@ -96,6 +97,11 @@ def parse():
     ap.add_argument("--lib", type=str, default="", help=argparse.SUPPRESS)  # diagnostics: a variant library
     # tests: the routed (RCCL all-to-all) step on one rank, so the multi-GPU path runs on a 1-GPU box
     ap.add_argument("--force-routed", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--router-depth", type=int, default=2, help="routed steps in flight (rl_router_submit / _wait)")
+    ap.add_argument("--no-combine", action="store_true", help="routed steps without hot-prefix combining")
+    ap.add_argument("--xgmi-gbps", type=float, default=400.0,
+                    help="--logical-shards estimate: all-to-all bandwidth per GPU and direction over xGMI (GB/s); "
+                         "7 links x ~153 GB/s = 1.07 TB/s raw, RCCL all-to-all assumed to reach ~37%% of it")
     ap.add_argument("--torch-router", action="store_true",
                     help="routed steps through router.ShardRouter (torch.distributed over RCCL) instead of the "
                          "C-ABI router rl_router_step (the Go host's path, the default)")
@@ -135,6 +141,11 @@ class DeviceGen:
                                   t.empty(d, dtype=t.int64, device=dev), t.ones(d, dtype=t.int32, device=dev),
                                   d * 17)
 
+    def make(self, b: int):
+        db = self.alloc()
+        self.fill(b, db)
+        return db
+
     def fill(self, b: int, db):
         """Batch b (counter stream b): now = T0 + b // K."""
         t = self.torch
@@ -146,6 +157,17 @@ class DeviceGen:
         db.now.fill_(T0 + b // self.K)
         if rc:
             raise RuntimeError("workload generator launch failed")
+
+
+class HostGen:
+    """Config-1 batches (examples/ratelimit rules, 10k keys, workload.config1_batch) made on the
+    host and copied to the device once, before timing."""
+
+    def __init__(self, d: int, seed: int, dev):
+        self.d, self.seed, self.dev = d, seed, dev
+
+    def make(self, b: int):
+        return router.DeviceBatch.from_host(workload.config1_batch(b, d=self.d, seed=self.seed, t0=T0), self.dev)
 
 
 def random_access_roofline(eng, alg_bytes, U, pipe_ms, step_ms):
@@ -196,7 +218,11 @@ def cpu_baseline(args, rules, d, seed, K, b0):
     import oracle as orc
 
     n_thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-    gen = workload.config3_batch if args.config == 3 else workload.config2_batch
+    if args.config == 1:
+        def gen(b, d, seed, batches_per_s, t0):
+            return workload.config1_batch(b, d=d, seed=seed, t0=t0)
+    else:
+        gen = workload.config3_batch if args.config == 3 else workload.config2_batch
     hbs, legs = [], {}
     for threads in (1, n_thr):
         o = orc.Oracle()
@@ -205,6 +231,8 @@ def cpu_baseline(args, rules, d, seed, K, b0):
         while t_cpu < args.cpu_seconds and nb < 64:
             if nb == len(hbs):
                 hbs.append(gen(b0 + nb, d=d, seed=seed, batches_per_s=K, t0=T0))
+            if threads > 1 and nb == 0:  # one warm-up submit: the thread pool and the map start cold
+                o.submit(hbs[nb], threads=threads)
             t1 = time.perf_counter()
             o.submit(hbs[nb], threads=threads)
             t_cpu += time.perf_counter() - t1
@@ -223,8 +251,9 @@ def cpu_baseline(args, rules, d, seed, K, b0):
 def logical_shards_main(args):
     """G logical shards on one GPU (SURVEY.md §8e readiness without a multi-GPU box): every
     origin draws its batch from the same Zipf key distribution, so each hot key lands on one
-    owner from every origin. Reports records per owner (max / mean) and the router's step
-    breakdown; decide_max_us is the owners' critical path when each owner has its own GPU."""
+    owner from every origin. Reports records per owner (max / mean), the router's step
+    breakdown (each origin's pack and unpack and each owner's decide timed alone), the bytes
+    each GPU would move over xGMI, and the G-GPU step estimate from them."""
     import torch
 
     G, d, K = args.logical_shards, args.desc, max(1, args.batches_per_second)
@@ -239,7 +268,7 @@ def logical_shards_main(args):
                          lib_path=(ROOT / args.lib) if args.lib else None)
         e.load_rules(rules)
         engines.append(e)
-    r = hiprl.Router(engines, max_desc=d)
+    r = hiprl.Router(engines, max_desc=d, combine=not args.no_combine)
     gens = [DeviceGen(args.config, d, (3 if args.config == 3 else 2) + 7919 * g, K, dev) for g in range(G)]
     bufs = [[gen.alloc() for gen in gens] for _ in range(2)]
     outs = [torch.empty(d * 20, dtype=torch.uint8, device=dev) for _ in range(G)]
@@ -262,19 +291,40 @@ def logical_shards_main(args):
     mean_owner = rec.mean(axis=1)
     keys = ["pack_us", "exchange_us", "decide_us", "decide_max_us", "reply_us", "unpack_us", "step_us"]
     br = {k: round(float(np.mean([x[k] for x in rows])), 1) for k in keys}
-    # G real GPUs: packs, decides and unpacks run side by side; the exchanges are the same bytes
-    est = br["pack_us"] / G + br["exchange_us"] + br["decide_max_us"] + br["reply_us"] + br["unpack_us"] / G
+    # G real GPUs, one origin and one owner each: an origin packs and unpacks its own batch
+    # (pack_us / G, unpack_us / G: the origins were timed one at a time), the hottest owner
+    # decides its records (decide_max_us), and each GPU sends and receives over xGMI about
+    # (G-1)/G of its records (32 B) and replies (8 B): max over owners of what it receives.
+    xg = args.xgmi_gbps * 1e3  # bytes per us
+    rmax = float(rec.max(axis=1).mean())
+    xch_rec_us = (G - 1) / G * max(float(mean_owner.mean()), rmax) * hiprl.ROUTE_RECORD_BYTES / xg
+    xch_rep_us = (G - 1) / G * max(float(mean_owner.mean()), rmax) * 8 / xg
+    compute_us = br["pack_us"] / G + br["decide_max_us"] + br["unpack_us"] / G
+    serial_us = compute_us + xch_rec_us + xch_rep_us
+    # two steps in flight (rl_router_submit / _wait): exchanges overlap the other step's compute
+    piped_us = max(compute_us, xch_rec_us + xch_rep_us)
     line = {"mode": "logical_shards", "n_shards": G, "descriptors_per_origin_batch": d, "steps": args.steps,
             "prefill_steps": prefill, "config": args.config, "log2_slots_per_shard": lg,
+            "combining": not args.no_combine, "combined_steps": int(rows[-1]["combined_steps"]),
+            "repacks": int(rows[-1]["repacks"]), "hot_groups_origin0": int(rows[-1]["hot_groups"]),
             "records_per_owner_mean": round(float(mean_owner.mean()), 1),
             "records_per_owner_max": int(rec.max()),
+            "records_per_origin_batch": d,
             "owner_imbalance_max_over_mean": round(float((rec.max(axis=1) / mean_owner).mean()), 3),
             "records_per_owner_last_step": [int(x) for x in rows[-1]["recv"]],
             "step_breakdown_us": br,
-            "estimated_step_us_on_G_gpus": round(est, 1),
-            "estimated_desc_per_s_on_G_gpus": round(G * d / (est * 1e-6), 1),
-            "note": "one GPU, G engines (local transport: exchanges are device copies); estimate = pack/G + "
-                    "exchange + max owner decide + reply + unpack/G"}
+            "xgmi_assumed_GBps_per_direction": args.xgmi_gbps,
+            "estimate_us": {"pack_per_origin": round(br["pack_us"] / G, 1), "decide_hottest_owner": br["decide_max_us"],
+                            "unpack_per_origin": round(br["unpack_us"] / G, 1),
+                            "records_xgmi": round(xch_rec_us, 1), "replies_xgmi": round(xch_rep_us, 1),
+                            "serial_step": round(serial_us, 1), "pipelined_step": round(piped_us, 1)},
+            "estimated_step_us_on_G_gpus": round(piped_us, 1),
+            "estimated_desc_per_s_on_G_gpus": round(G * d / (piped_us * 1e-6), 1),
+            "estimated_desc_per_s_on_G_gpus_serial": round(G * d / (serial_us * 1e-6), 1),
+            "note": "one GPU, G engines (local transport: exchanges are device copies, each origin's pack / unpack and "
+                    "each owner's decide timed alone); estimate on G GPUs = max(pack/G + hottest decide + unpack/G, "
+                    "xGMI time of the hottest owner's records + replies at the assumed bandwidth), two steps in "
+                    "flight; serial = their sum"}
     print(json.dumps(line), flush=True)
     if args.json_out:
         Path(args.json_out).write_text(json.dumps(line) + "\n")
@@ -310,35 +360,45 @@ def main():
     if args.config == 3:
         rules, log2 = workload.CONFIG3_RULES, (lg, lg, lg, 12)
         wl = "config3: 1e8 keys Zipf s=1.1, SECOND/MINUTE/HOUR by rank%3, 1 descriptor/request"
-    else:
+    elif args.config == 2:
         rules, log2 = workload.CONFIG2_RULES, (lg, 12, 12, 12)
         wl = "config2: 1e6 uniform keys, SECOND L=5, 1 descriptor/request"
+    else:
+        if d == 1_000_000:  # (the default): config 1 is 10k keys, one batch of 10k requests per second
+            d = 10_000
+        K = 1
+        rules, log2 = workload.CONFIG1_RULES, (20, 12, 12, 12)
+        wl = ("config1: examples/ratelimit rules (rl.foo.baz SECOND 1, mongo_cps SECOND 500), 10k keys, "
+              "1 descriptor/request, now +1 s per batch")
     prefill = args.prefill if args.prefill >= 0 else (K + K // 2 if K > 1 else 0)
-    seed = (3 if args.config == 3 else 2) + 7919 * rank  # each rank its own stream
+    seed = {1: 1, 2: 2, 3: 3}[args.config] + 7919 * rank  # each rank its own stream
     routed = (world > 1 or args.force_routed) and not args.independent
     # an owner may receive up to every origin's batch (hot keys concentrate on their owner)
     cap = d * world if routed else d
     eng = hiprl.Engine(device=local, log2_slots=log2, max_batch_desc=cap, max_batch_req=cap,
-                       max_blob_bytes=cap * 17 + 64, sort_bits=48, pipeline=args.pipeline,
+                       max_blob_bytes=cap * 32 + 64, sort_bits=48, pipeline=args.pipeline,
                        lib_path=(ROOT / args.lib) if args.lib else None)
     eng.load_rules(rules)
-    gen = DeviceGen(args.config, d, seed, K, dev)
+    gen = HostGen(d, seed, dev) if args.config == 1 else DeviceGen(args.config, d, seed, K, dev)
     rtr = nrt = None
     if routed and args.native_router:
         ids = [hiprl.Router.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(ids, src=0)
-        nrt = hiprl.Router([eng], max_desc=d, n_shards=world, rank=rank, rccl_id=ids[0])
+        nrt = hiprl.Router([eng], max_desc=d, n_shards=world, rank=rank, rccl_id=ids[0], combine=not args.no_combine)
     elif routed:
         rtr = router.ShardRouter(router.EngineShard(eng, rank, world, dev, d))
     pipelined = not routed and not args.serial
     DEPTH = min(args.depth, hiprl.MAX_IN_FLIGHT) if pipelined else 1
+    RDEPTH = max(1, min(2, args.router_depth)) if nrt is not None else 1
     outs = [torch.empty(d * 20, dtype=torch.uint8, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
     thrs = [torch.empty(d, dtype=torch.int32, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
 
-    def run(dbs, first=0):
+    def run(dbs, first=0, depth=None):
         """One step per batch. Pipelined: batch k+1 is submitted before batch k is waited for (the
-        micro-batcher's double buffering); every batch is complete on return."""
+        micro-batcher's double buffering; routed: rl_router_submit / rl_router_wait, two steps in
+        flight); every batch is complete on return."""
         pend = 0
+        rdepth = RDEPTH if depth is None else depth
         for j, db in enumerate(dbs):
             if rtr is not None:
                 rtr.step(db)
@@ -346,7 +406,11 @@ def main():
             sb = hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs())
             o, t = outs[(first + j) % len(outs)].data_ptr(), thrs[(first + j) % len(thrs)].data_ptr()
             if nrt is not None:
-                nrt.step([sb], [o], [t])
+                nrt.submit([sb], [o], [t])
+                pend += 1
+                if pend == rdepth:
+                    nrt.wait()
+                    pend -= 1
                 continue
             if pipelined:
                 eng.submit_pipelined_batch(sb, o, t)
@@ -358,12 +422,15 @@ def main():
                 eng.submit_device_async(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), o, t)
                 eng.wait()
         for _ in range(pend):
-            eng.wait()
+            if nrt is not None:
+                nrt.wait()
+            else:
+                eng.wait()
 
     # Prefill (untimed): one batch generated at a time into a ring of buffers, the engine two
     # batches behind (a buffer is refilled only after the batch that used it completed).
     t_fill = time.time()
-    ring = [gen.alloc() for _ in range(4)]
+    ring = [gen.alloc() for _ in range(4)] if prefill else []
     pend = 0
     for b in range(prefill):
         db = ring[b % len(ring)]
@@ -373,26 +440,23 @@ def main():
             rtr.step(db)
             continue
         sb = hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs())
+        o, t = outs[b % len(outs)].data_ptr(), thrs[b % len(thrs)].data_ptr()
         if nrt is not None:
-            nrt.step([sb], [outs[b % len(outs)].data_ptr()], [thrs[b % len(thrs)].data_ptr()])
-            continue
-        eng.submit_pipelined_batch(sb, outs[b % len(outs)].data_ptr(), thrs[b % len(thrs)].data_ptr())
+            nrt.submit([sb], [o], [t])
+        else:
+            eng.submit_pipelined_batch(sb, o, t)
         pend += 1
         if pend == 2:
-            eng.wait()
+            nrt.wait() if nrt is not None else eng.wait()
             pend -= 1
     for _ in range(pend):
-        eng.wait()
+        nrt.wait() if nrt is not None else eng.wait()
     t_fill = time.time() - t_fill
     fallbacks_prefill = eng.stats()["lsd_fallbacks"]
     # Timed batches (and warmup and kernel-timing batches) resident before timing.
     n_kt = 0 if args.no_kernel_times else args.steps
     b0 = prefill
-    dbs = []
-    for j in range(args.warmup + args.steps + n_kt):
-        db = gen.alloc()
-        gen.fill(b0 + j, db)
-        dbs.append(db)
+    dbs = [gen.make(b0 + j) for j in range(args.warmup + args.steps + n_kt)]
     torch.cuda.synchronize()
     run(dbs[:args.warmup])
     if dist:
@@ -406,6 +470,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     fb_timed = eng.stats()["lsd_fallbacks"] - fb0
+    rstats = nrt.stats() if nrt is not None else None
     if dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if args.native_router else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -434,10 +499,16 @@ def main():
     stats = eng.stats()
     occ = eng.occupancy()
 
-    # Host (PCIe) path: the timed batches from host memory through rl_submit, staged by the
-    # submitter in the engine's pinned slots (rl_host_acquire, as a Go micro-batcher builds
-    # batches in C memory), three in flight (H2D, kernels and D2H of different batches
-    # overlap), outputs copied out by rl_wait_into — what the Go side sees end to end.
+    # Host (PCIe) path (what a Go service sees, rl_submit of host batches, three in flight):
+    #  - pcie: H2D / D2H / both-directions copy bandwidth of this box (pinned, 64 MB);
+    #  - staged: batches built in place in the engine's pinned slots (rl_host_acquire), as a Go
+    #    batcher writes its requests straight into C memory: only H2D, kernels and D2H are timed
+    #    (each slot holds its batch from an untimed first pass; the batches repeat, which changes
+    #    counters, not the cost); results copied out by rl_wait_into;
+    #  - with_copy: the same with a numpy copy of every array into the slot per batch (the
+    #    round-2 line, a caller whose batches live elsewhere in host memory);
+    #  - the bound: max(H2D bytes / H2D rate, D2H bytes / D2H rate) per batch, the directions
+    #    concurrent, against the measured per-batch time.
     host = None
     if not args.no_host_path and not routed:
         hbatches = []
@@ -449,18 +520,50 @@ def main():
         out_h = np.empty(d, hiprl.STATUS_DTYPE)
         thr_h = np.empty(d, np.uint32)
 
-        def host_round(bs):
+        def pcie_rates():
+            nbytes = 64 << 20
+            hsrc = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+            hdst = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
+            dbuf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            dbuf2 = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+            def timed(fn, reps=10):
+                fn()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for _ in range(reps):
+                    fn()
+                torch.cuda.synchronize()
+                return (time.perf_counter() - t1) / reps
+
+            h2d = nbytes / timed(lambda: dbuf.copy_(hsrc, non_blocking=True)) / 1e9
+            d2h = nbytes / timed(lambda: hdst.copy_(dbuf2, non_blocking=True)) / 1e9
+
+            def both():
+                with torch.cuda.stream(s1):
+                    dbuf.copy_(hsrc, non_blocking=True)
+                with torch.cuda.stream(s2):
+                    hdst.copy_(dbuf2, non_blocking=True)
+            bi = 2 * nbytes / timed(both) / 1e9
+            return h2d, d2h, bi
+
+        def fill(sl, b):
+            n = int(b.blob.shape[0])
+            sl["blob"][:n] = b.blob
+            sl["off"][:b.n_desc + 1] = b.off
+            sl["rule"][:b.n_desc] = b.rule
+            sl["req_of"][:b.n_desc] = b.req_of
+            sl["now"][:b.n_req] = b.now
+            sl["hits"][:b.n_req] = b.hits
+
+        def host_round(bs, copy):
             pend = 0
-            for b in bs:
+            for k, b in enumerate(bs):
                 sl = eng.host_acquire()
-                n = int(b.blob.shape[0])
-                sl["blob"][:n] = b.blob
-                sl["off"][:b.n_desc + 1] = b.off
-                sl["rule"][:b.n_desc] = b.rule
-                sl["req_of"][:b.n_desc] = b.req_of
-                sl["now"][:b.n_req] = b.now
-                sl["hits"][:b.n_req] = b.hits
-                eng.submit_staged(b.n_desc, b.n_req, n, sl)
+                if copy:
+                    fill(sl, b)
+                eng.submit_staged(b.n_desc, b.n_req, int(b.blob.shape[0]), sl)
                 pend += 1
                 if pend == hiprl.MAX_IN_FLIGHT:
                     eng._check(eng.lib.rl_wait_into(eng.h, out_h.ctypes.data, thr_h.ctypes.data), "rl_wait_into")
@@ -468,17 +571,42 @@ def main():
             for _ in range(pend):
                 eng._check(eng.lib.rl_wait_into(eng.h, out_h.ctypes.data, thr_h.ctypes.data), "rl_wait_into")
 
-        host_round(hbatches[:2])
+        h2d_gbs, d2h_gbs, bi_gbs = pcie_rates()
+        nb3 = hiprl.MAX_IN_FLIGHT
+        # slot k % 3 holds batch k % 3 from the untimed first pass; the staged rounds reuse them
+        host_round(hbatches[:nb3], True)
+        rep = [hbatches[k % nb3] for k in range(len(hbatches))]
+        host_round(rep[:2], False)
         th = time.perf_counter()
-        host_round(hbatches)
-        t_host = time.perf_counter() - th
-        pcie = sum(int(b.blob.shape[0]) + 4 * (b.n_desc + 1) + 8 * b.n_desc + 12 * b.n_req + 20 * b.n_desc + 4 * b.n_req
-                   for b in hbatches)
-        host = {"value": round(len(hbatches) * d / t_host, 1), "unit": "descriptor decisions/s",
-                "ms_per_batch": round(t_host / len(hbatches) * 1e3, 4),
-                "pcie_GBps": round(pcie / t_host / 1e9, 2), "pcie_bytes_per_batch": pcie // len(hbatches),
-                "note": "same batches from host memory: staged into the engine's pinned slots (numpy copy, included), "
-                        "3 in flight, results copied out by rl_wait_into"}
+        host_round(rep, False)
+        t_staged = (time.perf_counter() - th) / len(rep)
+        # the copy into a slot alone (a caller that builds elsewhere)
+        sl = eng.host_acquire()
+        tc = time.perf_counter()
+        for b in hbatches[:4]:
+            fill(sl, b)
+        t_copy = (time.perf_counter() - tc) / 4
+        th = time.perf_counter()
+        host_round(hbatches, True)
+        t_with_copy = (time.perf_counter() - th) / len(hbatches)
+        h2d_b = sum(int(b.blob.shape[0]) + 32 + 4 * (b.n_desc + 1) + 8 * b.n_desc + 12 * b.n_req for b in rep) / len(rep)
+        d2h_b = sum(20 * b.n_desc + 4 * b.n_req for b in rep) / len(rep)
+        bound_s = max(h2d_b / (h2d_gbs * 1e9), d2h_b / (d2h_gbs * 1e9))
+        host = {"value": round(d / t_staged, 1), "unit": "descriptor decisions/s",
+                "ms_per_batch": round(t_staged * 1e3, 4),
+                "pcie_measured_GBps": {"h2d": round(h2d_gbs, 1), "d2h": round(d2h_gbs, 1),
+                                       "both_directions": round(bi_gbs, 1)},
+                "bytes_per_batch": {"h2d": int(h2d_b), "d2h": int(d2h_b)},
+                "pcie_bound_ms_per_batch": round(bound_s * 1e3, 4),
+                "frac_of_pcie_bound": round(bound_s / t_staged, 3),
+                "achieved_GBps": {"h2d": round(h2d_b / t_staged / 1e9, 1), "d2h": round(d2h_b / t_staged / 1e9, 1)},
+                "device_kernels_ms_per_batch": round(step_ms, 4),
+                "staging_copy_ms_per_batch": round(t_copy * 1e3, 4),
+                "with_copy": {"value": round(d / t_with_copy, 1), "ms_per_batch": round(t_with_copy * 1e3, 4)},
+                "note": "staged: batches built in place in the engine's pinned slots (rl_host_acquire), 3 in flight, "
+                        "H2D + kernels + D2H timed, results copied out by rl_wait_into; with_copy adds a numpy copy of "
+                        "every array into the slot per batch; bound = max(H2D bytes / H2D rate, D2H bytes / D2H "
+                        "rate), both directions concurrent"}
 
     if rank != 0:
         if dist:
@@ -526,7 +654,7 @@ def main():
     live_frac = [round(occ["live"][r] / occ["slots"][r], 4) for r in range(8)]
     line = {
         "metric": "descriptor decisions/sec, 100M keys Zipf, 1-8 GPUs; % of HBM peak" if args.config == 3
-        else "descriptor decisions/sec (config 2)",
+        else f"descriptor decisions/sec (config {args.config})",
         "value": round(value, 1),
         "unit": "descriptor decisions/s",
         "n_gpus": world,
@@ -544,11 +672,15 @@ def main():
                                    + (", C-ABI router (rl_router_step)" if nrt is not None else "")
                                    if routed else "single shard" if world == 1
                                    else f"x{world} independent replicas (no collective)"),
-                   "pipeline": args.pipeline, "batches_in_flight": DEPTH,
+                   "pipeline": args.pipeline, "batches_in_flight": RDEPTH if nrt is not None else DEPTH,
+                   "combining": (not args.no_combine) if nrt is not None else None,
                    "unique_keys_per_batch": int(U)},
         "roofline": roofline,
         "cpu_baseline": cpu,
         "host_path": host,
+        "router": ({k: rstats[k] for k in ("recv", "sent", "combined", "combined_steps", "repacks", "hot_groups",
+                                           "pack_us", "exchange_us", "decide_us", "reply_us", "unpack_us", "step_us")}
+                   if rstats else None),
         "table": {"live_keys": stats["live_keys"], "region_live_fraction": live_frac, "region_slots": occ["slots"],
                   "bytes": int(sum(occ["slots"])) * 32},
         "engine": {"resorts": stats["resorts"], "lsd_fallbacks_prefill": fallbacks_prefill,

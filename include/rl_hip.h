@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 2u
+#define RL_ABI_VERSION 3u
 
 /* rule id of a descriptor whose limit is nil ("don't check", src/limiter/cache.go:19-22) */
 #define RL_NIL_RULE 0xFFFFFFFFu
@@ -158,7 +158,12 @@ void rl_destroy(rl_engine* e);
 const char* rl_last_error(const rl_engine* e);
 uint32_t rl_abi_version(void);
 
-/* Load (replace) the rule table. Rule ids index it. Must not be called while a batch is in flight. */
+/* Load the rule table; rule ids index it. While batches are in flight the new table must keep
+ * every loaded rule at its id and may only append (RL_ESTATE otherwise): in-flight batches read
+ * rules by id, and the appended entries are written to slots none of them reads. A micro-batcher
+ * whose rule registry only grows (new (L, unit) pairs from a config reload or a descriptor.Limit
+ * override, src/config/config_impl.go:281-289) can therefore load at any time. Replacing or
+ * dropping rules needs nothing in flight. */
 int rl_load_rules(rl_engine* e, const rl_rule* rules, uint32_t n);
 
 /* Batches that may be in flight at once (rl_submit, rl_submit_pipelined). */
@@ -265,6 +270,22 @@ int rl_route_pack_strided(rl_engine* e, const rl_batch* device_batch, uint32_t o
  * Asynchronous like rl_submit_device; rl_wait() completes it. */
 int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_reply);
 
+/* Owner side, asynchronous and pipelined: like rl_submit_routed, but with RL_ROUTED_RAW the
+ * owner writes one raw reply per record (rl_raw_reply, 8 B: the INCRBY post-value the record
+ * saw, or a local-cache hit) and the origin makes the decisions (rl_route_unpack_raw); the call
+ * may be made while up to RL_MAX_IN_FLIGHT - 1 batches are in flight (distinct reply buffers),
+ * and the pipeline waits on the device for ready_event (a hipEvent_t recorded after the records
+ * arrived, e.g. on the stream of the exchange; NULL: ordered on the engine stream). flags = 0 is
+ * rl_submit_routed (ready_event must be NULL). rl_wait completes the oldest batch. */
+#define RL_ROUTED_RAW 1u
+typedef struct rl_raw_reply {
+  uint32_t after; /* INCRBY post-value (uint32, as fixed_cache_impl.go:51 decodes it); 0 for a hit */
+  uint32_t flags; /* RL_RAW_LOCAL_HIT: the key was in the local over-limit cache, no INCRBY */
+} rl_raw_reply;
+#define RL_RAW_LOCAL_HIT 1u
+int rl_submit_routed_async(rl_engine* e, const void* d_records, uint32_t n, void* d_reply, uint32_t flags,
+                           void* ready_event);
+
 /* Origin side: replies (in d_send order) -> d_out[n_desc] and d_req_throttle_ms[n_req].
  * Ordered on the engine stream; no host synchronisation. */
 int rl_route_unpack(rl_engine* e, const rl_batch* device_batch, const uint32_t* d_perm, const void* d_reply,
@@ -279,41 +300,79 @@ int rl_route_unpack(rl_engine* e, const rl_batch* device_batch, const uint32_t* 
  *                   id with rl_router_unique_id and hands it to the others out of band.
  *   local transport (rccl_id == NULL): n_shards engines in this process (logical shards, one
  *                   device or several); the exchanges are device-to-device copies.
+ * One step: each origin packs its batch by owner into a strided send buffer —
+ * one record per descriptor, except that descriptors of a hot prefix (the router's route hot
+ * set) are combined into one record carrying their sum of hits_addend (exact: one request time,
+ * one rule, local cache off; otherwise the batch is packed without combining); counts, then
+ * records move by all-to-all; each owner decides its records in origin order and answers each
+ * with its raw INCRBY post-value (rl_raw_reply); the replies return by the reverse all-to-all
+ * and the origin makes every descriptor's decision.
  * Every shard finishes every exchange of a step even when one fails, then all of them return
  * the failure: the failing shard its own code, the others RL_EPEER. The counts exchange
- * carries each origin's pack status, the reply exchange each owner's decide status, so a bad
- * batch on one GPU cannot leave its peers blocked in a collective. A refused owner batch
- * (RL_ENOSPC, RL_ECAPACITY) leaves that owner's table unchanged; other owners of the step
- * have applied theirs (per-shard atomicity, as a Redis cluster pipeline gives per-node). */
+ * carries each origin's pack status, the reply exchange each owner's decide status (and any
+ * local HIP failure after the counts), so a bad batch or a fault on one GPU cannot leave its
+ * peers blocked in a collective. An RCCL failure aborts the communicator (ncclCommAbort) and
+ * every later call returns RL_ECOMM. A refused owner batch (RL_ENOSPC, RL_ECAPACITY) leaves that
+ * owner's table unchanged; other owners of the step have applied theirs (per-shard atomicity,
+ * as a Redis cluster pipeline gives per-node); rl_router_stats.status says which. */
 #define RL_ROUTER_ID_BYTES 128u
 typedef struct rl_router rl_router;
 
 typedef struct rl_router_config {
-  uint32_t struct_size; /* sizeof(rl_router_config) */
-  uint32_t n_shards;    /* 1..RL_ROUTE_MAX_SHARDS */
-  uint32_t rank;        /* RCCL transport: this process's shard; local transport: 0 */
-  uint32_t max_desc;    /* descriptors per origin batch (an owner can receive n_shards x this) */
+  uint32_t struct_size;   /* sizeof(rl_router_config) */
+  uint32_t n_shards;      /* 1..RL_ROUTE_MAX_SHARDS */
+  uint32_t rank;          /* RCCL transport: this process's shard; local transport: 0 */
+  uint32_t max_desc;      /* descriptors per origin batch (an owner can receive n_shards x this) */
   const uint8_t* rccl_id; /* RL_ROUTER_ID_BYTES from rl_router_unique_id, or NULL: local transport */
+  uint32_t flags;         /* RL_ROUTER_* */
+  uint32_t max_blob_bytes; /* host staging (RL_ROUTER_HOST): key-prefix bytes per origin batch (0 = 64 x max_desc) */
 } rl_router_config;
+enum {
+  RL_ROUTER_NO_COMBINE = 1u, /* one record per descriptor (no hot-prefix combining) */
+  RL_ROUTER_HOST = 2u        /* allocate pinned host staging: rl_router_host_acquire / _submit_host / _wait_into */
+};
 
 typedef struct rl_router_stats {
   uint64_t steps;
   uint32_t n_shards;
-  int32_t status[RL_ROUTE_MAX_SHARDS]; /* last step: each shard's pack / decide status (0 = ok) */
+  int32_t status[RL_ROUTE_MAX_SHARDS]; /* last step: each shard's status (0 = ok, RL_EPEER = a peer failed) */
   uint32_t recv[RL_ROUTE_MAX_SHARDS];  /* last step: records each owner decided (RCCL: this rank's only) */
   uint32_t sent[RL_ROUTE_MAX_SHARDS];  /* last step: records origin 0 (RCCL: this rank) sent each owner */
   double pack_us, exchange_us, decide_us, decide_max_us, reply_us, unpack_us, step_us; /* last step, host clock */
+  uint32_t hot_groups;     /* last step: route hot set size of origin 0 (RCCL: this rank) */
+  uint32_t combined;       /* last step: combined records origin 0 (RCCL: this rank) sent (one per hot group) */
+  uint64_t repacks;        /* steps packed again without combining (a hot group not one key string) */
+  uint64_t combined_steps; /* steps whose origin 0 combined */
 } rl_router_stats;
 
 /* A fresh RCCL unique id (ncclGetUniqueId), RL_ROUTER_ID_BYTES bytes. */
 int rl_router_unique_id(uint8_t* id_out);
 /* engines: n_shards engines (local transport) or 1 (RCCL transport). The router does not own
- * them; they must outlive it and be used by nothing else while a step runs. */
+ * them; they must outlive it and be used by nothing else while a step runs. All engines share
+ * hash_seed and the rule table. */
 int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_router** out);
-/* One routed step, synchronous. batches / d_out / d_req_throttle_ms: one per engine passed at
- * create (device pointers; the same layouts as rl_submit_device). Decisions equal one engine
- * deciding the origins' batches one after another in shard order (include above). */
+/* One routed step, synchronous: rl_router_submit + rl_router_wait. batches / d_out /
+ * d_req_throttle_ms: one per engine passed at create (device pointers; the same layouts as
+ * rl_submit_device). Decisions equal one engine deciding the origins' batches one after
+ * another in shard order. */
 int rl_router_step(rl_router* r, const rl_batch* batches, rl_status* const* d_out, uint32_t* const* d_req_throttle_ms);
+/* Pipelined steps: up to two in flight. rl_router_submit packs, exchanges counts and records and
+ * hands the owner its records (returns once they are queued); rl_router_wait completes the
+ * oldest step (owner decisions, replies, the origin's decisions) and returns its status. With
+ * two in flight, step k+1's pack and exchange overlap step k's decide on the device. Every
+ * shard must make the same sequence of submit / wait calls (the collectives follow it). Inputs
+ * and outputs of a step stay untouched by the caller until its wait returns. */
+int rl_router_submit(rl_router* r, const rl_batch* batches, rl_status* const* d_out, uint32_t* const* d_req_throttle_ms);
+int rl_router_wait(rl_router* r);
+/* Host-memory steps (RL_ROUTER_HOST): a Go service on a multi-GPU node stages its batch in the
+ * router's pinned memory — rl_router_host_acquire hands out the next step's slot of a shard
+ * (RCCL: shard 0), C memory a cgo caller fills through unsafe slices — or passes any host
+ * arrays (copied before rl_router_submit_host returns). rl_router_wait_into completes the oldest
+ * step and copies each shard's statuses / ThrottleMillis into host memory during the call
+ * (NULL entries discard). No caller memory is retained. */
+int rl_router_host_acquire(rl_router* r, uint32_t shard, rl_host_batch* out);
+int rl_router_submit_host(rl_router* r, const rl_batch* host_batches);
+int rl_router_wait_into(rl_router* r, rl_status* const* out, uint32_t* const* req_throttle_ms);
 int rl_router_get_stats(const rl_router* r, rl_router_stats* out);
 const char* rl_router_last_error(const rl_router* r);
 void rl_router_destroy(rl_router* r);

@@ -149,3 +149,59 @@ def test_shadow_rule_through_cpp_mirror():
     assert s["shadow_mode"] == 3 and e["shadow_mode"] == 0
     assert {k: v for k, v in s.items() if k != "shadow_mode"} == {k: v for k, v in e.items() if k != "shadow_mode"}
     m.close()
+
+
+def test_rules_arrive_mid_stream_two_in_flight():
+    """The pipelined batcher (two batches in flight, rl_host_acquire slots, 2-s / slot-fit cuts)
+    under 8 concurrent callers whose requests keep introducing new (L, unit) limits — as a
+    config reload or a descriptor.Limit override does (config_impl.go:281-289) — so new rules
+    are appended to the device table while earlier batches are still in flight (rl_load_rules,
+    append-only). Each caller's statuses, throttles and stats equal a serial oracle of its own
+    requests (callers use disjoint keys), and some rule loads did happen with a batch in flight."""
+    T, n = 8, 220
+    units = [hiprl.SECOND, hiprl.MINUTE, hiprl.HOUR]
+    all_rules = [(3 + 2 * k, units[k % 3]) for k in range(40)]  # 40 distinct (L, unit) limits
+    m = Mirror(False, window_us=150)
+    m.lib.rlc_batcher_stats.argtypes = [C.c_void_p, C.c_void_p]
+    ids = [m.add_rule(L, u, f"rule{k}") for k, (L, u) in enumerate(all_rules)]
+    now = 1_700_000_123
+    m.lib.rlc_set_time(m.h, now)
+    rng = np.random.default_rng(23)
+    per = []
+    for t in range(T):
+        reqs = []
+        for q in range(n):
+            avail = min(len(all_rules), 1 + q // 6 + t)  # limits appear progressively, staggered per caller
+            nd = 1 + int(rng.integers(0, 3))
+            descs = [[("k", str(int(rng.integers(0, 5))))] for _ in range(nd)]
+            rr = [int(rng.integers(0, avail)) if rng.random() < 0.9 else None for _ in range(nd)]
+            reqs.append((f"mid{t}", descs, rr, int(rng.integers(0, 3)), now))
+        per.append(reqs)
+    res = [None] * T
+
+    def run(t):
+        res[t] = [m.do_limit(d, de, [None if x is None else ids[x] for x in ru], h) for d, de, ru, h, _ in per[t]]
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    m.lib.rlc_flush(m.h)
+    for t in range(T):
+        o = oracle.Oracle()
+        o.load_rules(all_rules)
+        for q, ((got, gthr), (d, de, ru, h, tq)) in enumerate(zip(res[t], per[t])):
+            b = hiprl.build_batch([(d, de, [hiprl.NIL_RULE if x is None else x for x in ru], h, tq)])
+            st, thr = o.submit(b)
+            for k, g in enumerate(got):
+                code, rem, has_limit, reset = g
+                want = (int(st["code_flags"][k]) & 0xFF, int(st["limit_remaining"][k]), ru[k] is not None,
+                        int(st["reset_s"][k]) if ru[k] is not None else 0)
+                assert (code, rem, bool(has_limit), reset if ru[k] is not None else 0) == want, (t, q, k)
+            assert gthr == int(thr[0]), (t, q)
+    bs = (C.c_uint64 * 3)()
+    m.lib.rlc_batcher_stats(m.h, bs)
+    assert bs[1] >= 10, list(bs)  # new limits kept arriving
+    assert bs[2] >= 1, list(bs)   # and at least one load happened behind a batch in flight
+    m.close()

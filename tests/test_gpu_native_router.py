@@ -129,7 +129,7 @@ def test_owner_over_capacity_fails_every_shard():
     r = hiprl.Router(es, max_desc=per)
     with pytest.raises(hiprl.RedisError, match="shard 1 \\(decide\\)") as ex:
         _step(r, batches)
-    assert ex.value.code == -4 and r.stats()["status"] == [0, -4], r.stats()
+    assert ex.value.code == -4 and r.stats()["status"] == [-7, -4], r.stats()  # the other shard: RL_EPEER
 
 
 def test_rccl_transport_one_rank_errors(monkeypatch):
