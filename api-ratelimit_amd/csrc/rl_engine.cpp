@@ -50,6 +50,7 @@ void launch_route_pack_strided(hipStream_t, const rl_batch&, const DevRule*, uin
 void launch_route_pack(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint32_t, uint32_t, RRec*,
                        uint8_t*, uint32_t*, RRec*, uint32_t*, uint32_t*, EngineCtl*, uint32_t*);
 void launch_route_reply(hipStream_t, uint32_t, const rl_status*, const uint32_t*, RReply*);
+int route_set_spin_limit(uint32_t v);
 void launch_route_unpack(hipStream_t, uint32_t, const uint32_t*, const uint32_t*, const RReply*, rl_status*,
                          uint32_t*);
 uint32_t v4_tiles(uint32_t n);
@@ -949,6 +950,12 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     e->done_ev[k] = e->ev_done[k];
   }
   if (he == hipSuccess) chk(hipMemset(e->zero_block, 0, e->zero_cap));
+  // the route packs' look-back bound: the default, or a diagnostic value (tests of the
+  // RL_EDEVICE path set it tiny)
+  if (he == hipSuccess) {
+    const char* sl = getenv("RL_DIAG_LB_SPIN_LIMIT");
+    if (route_set_spin_limit(sl ? (uint32_t)strtoul(sl, nullptr, 10) : (1u << 22))) he = hipErrorUnknown;
+  }
   if (he == hipSuccess) chk(hipDeviceSynchronize());
   if (he != hipSuccess) {
     rl_destroy(e);

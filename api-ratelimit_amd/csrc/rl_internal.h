@@ -77,8 +77,11 @@ void launch_route_pack2(hipStream_t st, const rl_batch& b, const DevRule* rules,
                         uint32_t origin, uint32_t n_shards, uint32_t stride, const HotEntry* hot,
                         const RoutePackBufs& o);
 // Origin: raw replies (back, strided like send) -> statuses and ThrottleMillis (the decisions).
+// owner_status: per owner its decide status (device; nonzero: that owner applied nothing and its
+// descriptors come out RL_CODE_UNKNOWN); stride: the owners' section size in back.
 void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* rules, const RoutePackBufs& o,
-                             const RawReply* back, rl_status* out, uint32_t* thr);
+                             const RawReply* back, const int32_t* owner_status, uint32_t stride, rl_status* out,
+                             uint32_t* thr);
 constexpr uint32_t ROUTE2_BLOCK = 1024;  // descriptors per pack block
 constexpr uint32_t PERM_HOT = 0x80000000u;
 constexpr int PERM_HOT_PRE_BITS = 22;

@@ -211,6 +211,8 @@ __global__ __launch_bounds__(NT) void k_route_scatter(uint32_t n, const RRec* __
 // back one block at a time took 2 ms per 10^6 descriptors.
 constexpr uint32_t LB_A = 1u << 30, LB_P = 2u << 30, LB_V = (1u << 30) - 1u;
 constexpr uint32_t LB_SPIN_LIMIT = 1u << 22;
+// The look-back's bound (tests lower it: RL_DIAG_LB_SPIN_LIMIT, read by rl_create).
+__device__ uint32_t g_lb_spin_limit = LB_SPIN_LIMIT;
 constexpr int LB_U = 1;  // look-back words per lane per read (4: 52 us, every extra word a line)
 __global__ __launch_bounds__(NT) void k_route_pack1(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
                                                      uint64_t seed, uint32_t origin, uint32_t n_shards, uint32_t stride,
@@ -306,7 +308,7 @@ __global__ __launch_bounds__(NT) void k_route_pack1(DevBatch in, const DevRule* 
         // waiting: an unpublished word nearer than the first P
         const bool wait = lane < lp ? un < LB_U : lane == lp ? un < up : false;
         if (__ballot(wait)) {
-          if (++spun > LB_SPIN_LIMIT) {
+          if (++spun > g_lb_spin_limit) {
             if (lane == 0) {
               atomicOr(gerr, (uint32_t)ERR_SPIN);
               __threadfence();  // the flag is visible before the (wrong) prefix below is published
@@ -464,7 +466,7 @@ RL_DEV uint32_t lookback_owner(uint32_t* lb, uint32_t* gerr, uint32_t bi, uint32
       const uint32_t lp = pm ? (uint32_t)__ffsll((unsigned long long)pm) - 1u : 64u;
       const bool wait = lane <= lp && lane < 64u && (v >> 30) == 0u;
       if (__ballot(wait)) {
-        if (++spun > LB_SPIN_LIMIT) {
+        if (++spun > g_lb_spin_limit) {
           if (lane == 0) {
             atomicOr(gerr, (uint32_t)ERR_SPIN);
             __threadfence();
@@ -824,12 +826,15 @@ __global__ __launch_bounds__(HS_NT) void k_route_hot_scan(uint32_t nb, uint32_t 
 }
 
 // Origin: every descriptor's decision from its owner's raw reply.
+// owner_status[j] != 0: owner j refused its records (nothing applied for them): their
+// descriptors get code RL_CODE_UNKNOWN, so a caller can answer every other descriptor.
 __global__ __launch_bounds__(NT) void k_route_unpack_raw(DevBatch in, const DevRule* __restrict__ rules,
                                                           const uint32_t* __restrict__ perm,
                                                           const RawReply* __restrict__ back,
                                                           const uint32_t* __restrict__ boff,
                                                           const uint32_t* __restrict__ hot_pos,
                                                           const uint32_t* __restrict__ hot_tot,
+                                                          const int32_t* __restrict__ owner_status, uint32_t stride,
                                                           rl_status* __restrict__ out, uint32_t* __restrict__ req_thr) {
   const uint32_t i = blockIdx.x * NT + threadIdx.x;
   if (i >= in.n_desc) return;
@@ -850,6 +855,17 @@ __global__ __launch_bounds__(NT) void k_route_unpack_raw(DevBatch in, const DevR
   const uint32_t ha = in.hits[q];
   const uint32_t h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
   const DevRule R = rules[rule];
+  const uint32_t pos = (p & PERM_HOT) ? hot_pos[(p >> PERM_HOT_PRE_BITS) & (uint32_t)(HOT_MAX - 1)] : p;
+  if (owner_status[pos / stride] != 0) {  // refused by its owner: undecided
+    rl_status st;
+    st.code_flags = RL_CODE_UNKNOWN;
+    st.limit_remaining = 0;
+    st.reset_s = 0;
+    st.over_limit_delta = 0;
+    st.near_limit_delta = 0;
+    out[i] = st;
+    return;
+  }
   uint32_t after, fl;
   if (p & PERM_HOT) {
     // post-value of this descriptor's INCRBY inside its combined group: the group's reply minus
@@ -925,10 +941,15 @@ void launch_route_pack2(hipStream_t st, const rl_batch& b, const DevRule* rules,
 }
 
 void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* rules, const RoutePackBufs& o,
-                             const RawReply* back, rl_status* out, uint32_t* thr) {
+                             const RawReply* back, const int32_t* owner_status, uint32_t stride, rl_status* out,
+                             uint32_t* thr) {
   if (!b.n_desc) return;
   hipLaunchKernelGGL(route::k_route_unpack_raw, dim3(route_blocks(b.n_desc)), dim3(route::NT), 0, st, make_dev_batch(b),
-                     rules, o.perm, back, o.bhs, o.hot_pos, o.hot_tot, out, thr);
+                     rules, o.perm, back, o.bhs, o.hot_pos, o.hot_tot, owner_status, stride, out, thr);
+}
+
+int route_set_spin_limit(uint32_t v) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(route::g_lb_spin_limit), &v, sizeof v) == hipSuccess ? 0 : -1;
 }
 
 void launch_route_reply(hipStream_t st, uint32_t n, const rl_status* out, const uint32_t* thr, RReply* reply) {

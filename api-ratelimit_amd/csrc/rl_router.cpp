@@ -728,8 +728,8 @@ void rl_router::wait_rccl(uint32_t k) {
   st.reply_us = now_us() - t1;
   const double t2 = now_us();
   if (he == hipSuccess && t.b.n_req) he = hipMemsetAsync(t.thr, 0, (size_t)t.b.n_req * 4, S.os);
-  if (he == hipSuccess) {
-    launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.out, t.thr);
+  if (he == hipSuccess) {  // (the owners' statuses arrived with the replies, d_x[5G, 6G))
+    launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 5 * G, cfg.max_desc, t.out, t.thr);
     he = hipGetLastError();
   }
   if (he == hipSuccess && slot[k].host) {
@@ -787,9 +787,13 @@ void rl_router::wait_local(uint32_t k) {
     Shard& S = sh[i];
     ShardStep& t = S.st[k];
     hipError_t hu = he;
+    // every owner's decide status into this origin's device words (as the RCCL reply exchange
+    // delivers them)
+    for (uint32_t j = 0; j < G; ++j) t.h_x[5 * G + j] = slot[k].status[j];
+    if (hu == hipSuccess) hu = hipMemcpyAsync(t.d_x + 5 * G, t.h_x + 5 * G, 4 * G, hipMemcpyHostToDevice, S.os);
     if (hu == hipSuccess && t.b.n_req) hu = hipMemsetAsync(t.thr, 0, (size_t)t.b.n_req * 4, S.os);
     if (hu == hipSuccess) {
-      launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.out, t.thr);
+      launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 5 * G, cfg.max_desc, t.out, t.thr);
       hu = hipGetLastError();
     }
     if (hu == hipSuccess && slot[k].host) {

@@ -314,7 +314,11 @@ int rl_route_unpack(rl_engine* e, const rl_batch* device_batch, const uint32_t* 
  * peers blocked in a collective. An RCCL failure aborts the communicator (ncclCommAbort) and
  * every later call returns RL_ECOMM. A refused owner batch (RL_ENOSPC, RL_ECAPACITY) leaves that
  * owner's table unchanged; other owners of the step have applied theirs (per-shard atomicity,
- * as a Redis cluster pipeline gives per-node); rl_router_stats.status says which. */
+ * as a Redis cluster pipeline gives per-node): rl_router_stats.status says which, and after a
+ * failure at an owner (decide or later) the outputs still hold every decision the healthy
+ * owners made, the descriptors of a failed owner coming out with code RL_CODE_UNKNOWN (not
+ * known to be applied) — the caller can answer those requests and fail only the others. After
+ * a pack failure (any origin) nothing was applied anywhere and the outputs are untouched. */
 #define RL_ROUTER_ID_BYTES 128u
 typedef struct rl_router rl_router;
 

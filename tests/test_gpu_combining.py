@@ -421,3 +421,85 @@ def test_config5_stream_routed(transport, monkeypatch):
     run_steps(r, steps, o, "pipelined", f"config5 {transport}")
     assert r.stats()["combined_steps"] > 0
     r.close()
+
+
+def test_lookback_spin_expiry_reports_edevice_everywhere(monkeypatch):
+    """The packs' decoupled look-back with its spin bound at 0 (RL_DIAG_LB_SPIN_LIMIT, read by
+    rl_create): blocks that find a predecessor unpublished give up at once. Every owner's
+    (count, status) pair must then carry RL_EDEVICE — one status per origin, so every rank
+    leaves the step at the counts exchange — and the router step fails with RL_EDEVICE
+    ("device fault"), for the one-kernel pack (k_route_pack1, 256 descriptors per block) and the
+    combining router's pack (1024 per block), on grids far larger than what is resident."""
+    n = 2_000_000
+    b = workload.config3_batch(9, d=n)
+    monkeypatch.setenv("RL_DIAG_LB_SPIN_LIMIT", "0")
+    e = engines(1, n, rules=workload.CONFIG3_RULES, log2_slots=(22, 22, 22, 12), blob=int(b.blob.shape[0]) + 64)[0]
+    monkeypatch.delenv("RL_DIAG_LB_SPIN_LIMIT")
+    db = router.DeviceBatch.from_host(b, DEV)
+    G = 4
+    send = torch.zeros(G * n * 32, dtype=torch.uint8, device=DEV)
+    perm = torch.zeros(n, dtype=torch.int32, device=DEV)
+    x = torch.zeros(2 * G, dtype=torch.int32, device=DEV)
+    torch.cuda.synchronize()
+    e.route_pack_strided(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), 0, G, n, send.data_ptr(), x.data_ptr(),
+                         perm.data_ptr())
+    torch.cuda.synchronize()
+    st = x.cpu().numpy()[1::2]
+    assert len(set(st.tolist())) == 1, st  # one status for every owner
+    assert st[0] == -6, st
+    r = hiprl.Router([e], max_desc=n)
+    bf = Bufs([b])
+    torch.cuda.synchronize()
+    with pytest.raises(hiprl.RedisError, match="device fault") as ex:
+        r.step(*bf.args())
+    assert ex.value.code == -6
+    r.close()
+    # a fresh engine restores the bound: the same batch packs cleanly
+    e2 = engines(1, n, rules=workload.CONFIG3_RULES, log2_slots=(22, 22, 22, 12), blob=int(b.blob.shape[0]) + 64)[0]
+    x.zero_()
+    e2.route_pack_strided(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), 0, G, n, send.data_ptr(), x.data_ptr(),
+                          perm.data_ptr())
+    torch.cuda.synchronize()
+    xs = x.cpu().numpy()
+    assert list(xs[1::2]) == [0] * G and int(xs[0::2].sum()) == n
+
+
+@pytest.mark.parametrize("combine", [True, False])
+def test_refused_owner_leaves_the_others_decided(combine):
+    """Owner 1 cannot take its records (engine capacity 1000): the step fails with its
+    RL_ECAPACITY on shard 1 and RL_EPEER on shard 0, but every descriptor owner 0 decided has
+    its decision in the outputs (equal to an oracle that applies only owner 0's keys) and owner
+    1's descriptors come out RL_CODE_UNKNOWN; the next steps see only what was applied."""
+    G, per = 2, 1500
+    steps = skew_batches(G, 12, per, seed=61)
+    es = engines(1, 3 * per * G) + engines(1, 3 * per * G)
+    r = hiprl.Router(es, max_desc=3 * per, combine=combine)
+    o = new_oracle()
+    run_steps(r, steps[:10], o, "sync", "before")
+    small = hiprl.Engine(max_batch_desc=1000, max_batch_req=1000)
+    small.load_rules(RULES)
+    # owner 1's engine replaced by one too small: a router over (engine 0, small engine) that
+    # shares engine 0's table; owner 1's table is empty, so only owner 0's decisions are checked
+    r2 = hiprl.Router([es[0], small], max_desc=3 * per, combine=combine)
+    bf = Bufs(steps[10])
+    torch.cuda.synchronize()
+    with pytest.raises(hiprl.RedisError, match="shard 1 \\(decide\\)") as ex:
+        r2.step(*bf.args())
+    assert ex.value.code == -4 and r2.stats()["status"] == [-7, -4], r2.stats()
+    got = bf.results()
+    part = []
+    for b in steps[10]:
+        own = routing.owners_of(b, RULES, G, SEED)
+        part.append(hiprl.Batch(b.blob, b.off, np.where(own == 1, hiprl.NIL_RULE, b.rule).astype(np.uint32), b.req_of,
+                                b.now, b.hits))
+    est, ethr = o.submit(routing.concat_batches(part))
+    d0 = r0 = 0
+    for g, (b, (st, thr)) in enumerate(zip(steps[10], got)):
+        own = routing.owners_of(b, RULES, G, SEED)
+        e_st = est[d0:d0 + b.n_desc].copy()
+        e_st[own == 1] = (0, 0, 0, 0, 0)  # RL_CODE_UNKNOWN
+        streams.assert_same(e_st, ethr[r0:r0 + b.n_req], st, thr, f"partial step origin={g}")
+        d0 += b.n_desc
+        r0 += b.n_req
+    r2.close()
+    r.close()

@@ -1,0 +1,36 @@
+#!/bin/bash
+# One GPU call of measurements: smoke, the N=1 bench line, the routed step on a one-rank RCCL
+# communicator (torchrun, two steps in flight), G logical shards (records per owner, step
+# breakdown, G-GPU estimate), the config-1 row. Each step under its own limit; a crash, abort
+# or timeout (rc >= 124) stops the call there.
+# usage (on the GPU box, from the repo root): tools/gpu_bench_round.sh <tag> [steps...]
+set -u
+TAG=$1
+shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/$TAG
+mkdir -p "$OUT"
+run() {  # name limit cmd...
+  local name=$1 lim=$2
+  shift 2
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.json" 2> "$OUT/$name.err"
+  local rc=$?
+  echo "$name rc=$rc" | tee -a "$OUT/steps.txt"
+  tail -c 1500 "$OUT/$name.json"
+  echo
+  if [ "$rc" -ge 124 ] || [ "$rc" -lt 0 ]; then echo "stopping after $name (rc=$rc)"; exit "$rc"; fi
+}
+for s in "${@:-smoke bench routed1 ls8 ls2 config1}"; do
+  for step in $s; do
+    case $step in
+      smoke) run smoke 240 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
+      bench) run bench 600 python -u bench.py ;;
+      routed1) run routed1 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
+                 --master-port 29533 bench.py --gpus 1 --force-routed --steps 30 --warmup 10 --cpu-seconds 0 \
+                 --no-host-path --no-roofline-probe ;;
+      ls8) run ls8 600 python -u bench.py --logical-shards 8 --steps 10 --warmup 3 --prefill 40 ;;
+      ls2) run ls2 600 python -u bench.py --logical-shards 2 --steps 10 --warmup 3 --prefill 40 ;;
+      config1) run config1 400 python -u bench.py --config 1 --steps 200 --warmup 20 --cpu-seconds 6 --no-roofline-probe ;;
+    esac
+  done
+done
