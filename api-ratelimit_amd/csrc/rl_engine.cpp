@@ -50,7 +50,7 @@ void launch_route_pack_strided(hipStream_t, const rl_batch&, const DevRule*, uin
 void launch_route_pack(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint32_t, uint32_t, RRec*,
                        uint8_t*, uint32_t*, RRec*, uint32_t*, uint32_t*, EngineCtl*, uint32_t*);
 void launch_route_reply(hipStream_t, uint32_t, const rl_status*, const uint32_t*, RReply*);
-int route_set_spin_limit(uint32_t v);
+hipError_t route_set_spin_limit(uint32_t v);
 void launch_route_unpack(hipStream_t, uint32_t, const uint32_t*, const uint32_t*, const RReply*, rl_status*,
                          uint32_t*);
 uint32_t v4_tiles(uint32_t n);
@@ -815,7 +815,10 @@ extern "C" {
 
 uint32_t rl_abi_version(void) { return RL_ABI_VERSION; }
 
-const char* rl_last_error(const rl_engine* e) { return e ? e->err.c_str() : "null engine"; }
+// rl_create's failures have no engine to hold their message: rl_last_error(NULL) returns the
+// calling thread's last one.
+static thread_local std::string t_create_err = "no rl_create failure on this thread";
+const char* rl_last_error(const rl_engine* e) { return e ? e->err.c_str() : t_create_err.c_str(); }
 
 int rl_create(const rl_config* cfg_in, rl_engine** out) {
   if (!cfg_in || !out) return RL_EINVAL;
@@ -842,8 +845,16 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   e->npasses = (int)c.sort_bits / 8;
   e->lo_bit = 64 - (int)c.sort_bits;
   hipError_t he = hipSetDevice(c.device);
-  if (he != hipSuccess) { delete e; return RL_EHIP; }
-  auto chk = [&](hipError_t x) { if (x != hipSuccess && he == hipSuccess) he = x; };
+  if (he != hipSuccess) {
+    t_create_err = std::string("rl_create: hipSetDevice: ") + hipGetErrorString(he);
+    delete e;
+    return RL_EHIP;
+  }
+  const char* where = "";
+  auto chk_at = [&](hipError_t x, const char* what) {
+    if (x != hipSuccess && he == hipSuccess) he = x, where = what;
+  };
+#define chk(x) chk_at((x), #x)
   chk(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking));
   chk(hipStreamCreateWithFlags(&e->front, hipStreamNonBlocking));
   chk(hipStreamCreateWithFlags(&e->xin, hipStreamNonBlocking));
@@ -954,10 +965,12 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   // RL_EDEVICE path set it tiny)
   if (he == hipSuccess) {
     const char* sl = getenv("RL_DIAG_LB_SPIN_LIMIT");
-    if (route_set_spin_limit(sl ? (uint32_t)strtoul(sl, nullptr, 10) : (1u << 22))) he = hipErrorUnknown;
+    chk(route_set_spin_limit(sl ? (uint32_t)strtoul(sl, nullptr, 10) : (1u << 22)));
   }
   if (he == hipSuccess) chk(hipDeviceSynchronize());
+#undef chk
   if (he != hipSuccess) {
+    t_create_err = std::string("rl_create: ") + where + ": " + hipGetErrorString(he);
     rl_destroy(e);
     return RL_EHIP;
   }

@@ -948,8 +948,8 @@ void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* r
                      rules, o.perm, back, o.bhs, o.hot_pos, o.hot_tot, owner_status, stride, out, thr);
 }
 
-int route_set_spin_limit(uint32_t v) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(route::g_lb_spin_limit), &v, sizeof v) == hipSuccess ? 0 : -1;
+hipError_t route_set_spin_limit(uint32_t v) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(route::g_lb_spin_limit), &v, sizeof v);
 }
 
 void launch_route_reply(hipStream_t st, uint32_t n, const rl_status* out, const uint32_t* thr, RReply* reply) {

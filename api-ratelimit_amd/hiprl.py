@@ -306,7 +306,8 @@ class Engine:
         h = C.c_void_p()
         rc = self.lib.rl_create(C.byref(cfg), C.byref(h))
         if rc:
-            raise RedisError(f"rl_create failed: {RL_ERRORS.get(rc, rc)}")
+            raise RedisError(f"rl_create failed: {RL_ERRORS.get(rc, rc)}: "
+                             f"{self.lib.rl_last_error(None).decode(errors='replace')}")
         self.h = h
         self.near_limit_ratio = near_limit_ratio
 

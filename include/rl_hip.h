@@ -155,6 +155,8 @@ typedef struct rl_occupancy {
 
 int rl_create(const rl_config* cfg, rl_engine** out);
 void rl_destroy(rl_engine* e);
+/* The engine's last error message; with e == NULL, the calling thread's last rl_create
+ * failure (which HIP call failed and why). */
 const char* rl_last_error(const rl_engine* e);
 uint32_t rl_abi_version(void);
 

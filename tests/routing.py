@@ -29,7 +29,7 @@ def concat_batches(batches):
     blobs, offs, rules, reqs, nows, hits = [], [], [], [], [], []
     boff, roff = 0, 0
     for b in batches:
-        blobs.append(b.blob)
+        blobs.append(b.blob[:int(b.off[-1])])  # (a generated blob may carry slack past its last prefix)
         offs.append(b.off[:-1].astype(np.int64) + boff)
         rules.append(b.rule)
         reqs.append(b.req_of.astype(np.int64) + roff)
