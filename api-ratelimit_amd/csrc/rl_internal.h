@@ -65,13 +65,18 @@ struct RoutePackBufs {
   uint32_t* lb;        // look-back words + error word, two areas (pack, repack), zeroed by the caller
   uint32_t* bhs;       // [blocks][HOT_MAX] hot h sums per block -> exclusive prefixes over blocks
   uint32_t* bstat;     // [blocks][4] per block: ~min now, max now, flags of its hot descriptors
-  uint32_t* rctl;      // [16] step words: [0] repack (combining refused), [1] combined records, [2] done ctr
+  uint32_t* rctl;      // [16] step words: [0] repack (combining refused), [1] combined records, [2] done ctr;
+                       // then the hot scan's look-back words (route2_hot_lb_words), then its u64 sums
   uint32_t* hot_pos;   // [HOT_MAX] record position of each hot group's combined record
   uint32_t* hot_tot;   // [HOT_MAX] its sum of hits_addend
+  uint32_t* h_hot;     // pinned host [HOT_MAX + 2]: group sums, repack flag, applied flag (k_route_hot_scan)
+  uint32_t* thr;       // the origin's ThrottleMillis output: zeroed by the pack (nullable)
+  uint32_t zero_words; // lb / rctl words the unpack clears for the slot's next step (from lb)
 };
 uint32_t route2_blocks(uint32_t n);
 size_t route2_lb_words(uint32_t n);     // one area
 size_t route2_bhs_words(uint32_t n);
+size_t route2_hot_lb_words();          // the hot scan's look-back words (after rctl[16], zeroed with it)
 // hot == nullptr: no combining
 void launch_route_pack2(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
                         uint32_t origin, uint32_t n_shards, uint32_t stride, const HotEntry* hot,

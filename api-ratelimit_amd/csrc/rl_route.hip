@@ -493,7 +493,8 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
                                                      const HotEntry* __restrict__ hot, RRec* __restrict__ send,
                                                      uint32_t* __restrict__ perm, uint32_t* lb, uint32_t* gerr,
                                                      uint32_t* __restrict__ x, uint32_t* __restrict__ bhs,
-                                                     uint32_t* __restrict__ bstat, const uint32_t* __restrict__ rctl) {
+                                                     uint32_t* __restrict__ bstat, const uint32_t* __restrict__ rctl,
+                                                     uint32_t* __restrict__ req_thr) {
   __shared__ uint32_t s_wc[PR][PW][NS + 2];
   __shared__ uint32_t s_tot[NS], s_base[NS];
   __shared__ uint32_t s_err;
@@ -502,6 +503,8 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
   __shared__ uint32_t s_st[3];  // the block's hot descriptors: ~min now, max now, RF_* flags
   if (REPACK && rctl[0] == 0u) return;  // combining was accepted: nothing to redo
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6, bi = blockIdx.x;
+  if (!REPACK && req_thr)  // ThrottleMillis starts at 0 (k_route_unpack_raw takes the max per request)
+    for (uint32_t q = bi * NT + tid; q < in.n_req; q += gridDim.x * NT) req_thr[q] = 0u;
   for (uint32_t k = tid; k < PR * PW * (NS + 2); k += NT) (&s_wc[0][0][0])[k] = 0;
   if constexpr (COMBINE) {
     const uint32_t* tg = reinterpret_cast<const uint32_t*>(hot);
@@ -597,7 +600,25 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
     uint32_t mn = 0xFFFFFFFFu, mx = 0;
 #pragma unroll
     for (int r = 0; r < PR; ++r) {
-      uint64_t todo = __ballot(cat[r] == CAT_HOT);
+      const bool ht = cat[r] == CAT_HOT;
+      uint64_t todo = __ballot(ht);
+      if (todo && __ballot(ht && rec[r].h != 1u) == 0ull) {
+        // every hot h of the wave's round is 1 (hits_addend 0 or 1, the common case): a lane's
+        // exclusive prefix is the number of its group's lanes below it. The group's lanes by
+        // a match on the 8 group-index bits, no loop over the wave's groups.
+        uint64_t m = todo;
+#pragma unroll
+        for (int bt = 0; bt < 8; ++bt) {
+          const bool bit = (hix[r] >> bt) & 1u;
+          const uint64_t bal = __ballot(bit);
+          m &= bit ? bal : ~bal;
+        }
+        if (ht) {
+          hex[r] = (uint32_t)__popcll(m & lt);
+          if (lane == (uint32_t)__ffsll((unsigned long long)m) - 1u) s_hw[r * PW + w][hix[r]] = (uint32_t)__popcll(m);
+        }
+        todo = 0;
+      }
       while (todo) {  // one group of the wave per iteration (wave-uniform)
         const uint32_t ld = (uint32_t)__ffsll((unsigned long long)todo) - 1u;
         const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane((int)hix[r], (int)ld);
@@ -690,50 +711,110 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
   }
 }
 
-constexpr int HS_NT = 1024, HS_COLS = 16, HS_SLICES = HS_NT / HS_COLS, HS_Q = 16;
-static_assert(HOT_MAX % HS_COLS == 0, "hot scan columns");
+// Hot scan: the per-(block, group) sums of k_route_pack2 -> exclusive prefixes over blocks (in
+// place) and each group's total; then the last block's verdict and the combined records.
+// Grid: HS_CC column chunks of 64 groups (lane = group) x HS_RCH row chunks (the pack blocks,
+// split in 16); each wave loads up to HS_Q rows of its chunk into registers (one coalesced
+// 256-B row segment per load), the chunk's column sums go out through a decoupled look-back
+// over the row chunks before it (64-bit words, flag in bit 63), and the prefixes are written
+// from the registers. At 1024 threads x 16 columns the kernel spilled 76 VGPRs and took 32 us
+// per 10^6 descriptors; at 256 x 16 (two passes over the rows) 14.8 us.
+constexpr int HS_NT = 256, HS_W = HS_NT / 64, HS_CC = HOT_MAX / 64, HS_RCH = 16, HS_Q = 16;
+static_assert(HOT_MAX % 64 == 0 && HS_NT == HOT_MAX, "hot scan geometry: one last-block thread per group");
+constexpr unsigned long long HLB_FLAG = 1ull << 63;
+// h_out (pinned host words, written through): [0, HOT_MAX) each group's sum of h this step
+// (0 for a group without descriptors), [HOT_MAX] 1 = the batch needs the repack, [HOT_MAX + 1]
+// 1 = combining applied — read by the host after the step's counts, with no copy.
+// hlb: [HS_RCH][HOT_MAX] look-back words, zero before the launch.
 __global__ __launch_bounds__(HS_NT) void k_route_hot_scan(uint32_t nb, uint32_t n_shards, uint32_t origin,
                                                            uint32_t stride, const HotEntry* __restrict__ hot,
                                                            uint32_t* __restrict__ bhs, const uint32_t* bstat,
                                                            RRec* __restrict__ send, uint32_t* x, uint32_t* rctl,
                                                            uint32_t* __restrict__ hot_pos,
                                                            uint32_t* __restrict__ hot_tot,
-                                                           unsigned long long* tot64, const uint32_t* gerr) {
-  __shared__ unsigned long long s_sl[HS_SLICES][HS_COLS];
+                                                           unsigned long long* tot64, uint32_t* gerr,
+                                                           uint32_t* h_out, unsigned long long* hlb) {
+  __shared__ unsigned long long s_w[HS_W][64];
   __shared__ uint32_t s_last, s_mn, s_mx, s_fl, s_bad;
   __shared__ uint32_t s_oc[4][NS + 1];
-  const uint32_t tid = threadIdx.x, c = tid % HS_COLS, sl = tid / HS_COLS;
-  const uint32_t col = blockIdx.x * HS_COLS + c;
-  const uint32_t Q = (nb + HS_SLICES - 1) / HS_SLICES;
-  const uint32_t r0 = min(nb, sl * Q), r1 = min(nb, r0 + Q);
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t cc = blockIdx.x % HS_CC, rc = blockIdx.x / HS_CC;
+  const uint32_t col = cc * 64 + lane;
+  const uint32_t R = (nb + HS_RCH - 1) / HS_RCH;             // rows per chunk
+  const uint32_t RW = (R + HS_W - 1) / HS_W;                 // rows per wave
+  const uint32_t r0 = min(nb, rc * R + wv * RW), r1 = min(min(nb, rc * R + R), r0 + RW);
+  const bool in_regs = RW <= (uint32_t)HS_Q;                 // grid-uniform
+  uint32_t v[HS_Q];
   unsigned long long sum = 0;
-  for (uint32_t rr = r0; rr < r1; rr += HS_Q) {
-    uint32_t v[HS_Q];
+  if (in_regs) {
 #pragma unroll
-    for (int u = 0; u < HS_Q; ++u) v[u] = bhs[(size_t)min(rr + u, r1 - 1u) * HOT_MAX + col];
+    for (int u = 0; u < HS_Q; ++u) v[u] = r0 + u < r1 ? bhs[(size_t)(r0 + u) * HOT_MAX + col] : 0u;
 #pragma unroll
-    for (int u = 0; u < HS_Q; ++u) sum += rr + u < r1 ? v[u] : 0u;
+    for (int u = 0; u < HS_Q; ++u) sum += v[u];
+  } else {
+#pragma unroll 1
+    for (uint32_t rr = r0; rr < r1; rr += HS_Q) {
+#pragma unroll
+      for (int u = 0; u < HS_Q; ++u) v[u] = bhs[(size_t)min(rr + u, r1 - 1u) * HOT_MAX + col];
+#pragma unroll
+      for (int u = 0; u < HS_Q; ++u) sum += rr + u < r1 ? v[u] : 0u;
+    }
   }
-  s_sl[sl][c] = sum;
+  s_w[wv][lane] = sum;
   __syncthreads();
-  unsigned long long run = 0, tot = 0;
-  for (uint32_t k = 0; k < (uint32_t)HS_SLICES; ++k) {
-    const unsigned long long y = s_sl[k][c];
-    run += k < sl ? y : 0ull;
-    tot += y;
-  }
-  for (uint32_t rr = r0; rr < r1; rr += HS_Q) {  // the same rows again (L2): exclusive prefixes in place
-    uint32_t v[HS_Q];
+  if (wv == 0) {  // the chunk's column sums: publish, then look back over the chunks before it
+    unsigned long long agg = 0;
 #pragma unroll
-    for (int u = 0; u < HS_Q; ++u) v[u] = bhs[(size_t)min(rr + u, r1 - 1u) * HOT_MAX + col];
-#pragma unroll
-    for (int u = 0; u < HS_Q; ++u)
-      if (rr + u < r1) {
-        bhs[(size_t)(rr + u) * HOT_MAX + col] = (uint32_t)run;
-        run += v[u];
+    for (int k = 0; k < HS_W; ++k) agg += s_w[k][lane];
+    __hip_atomic_store(&hlb[(size_t)rc * HOT_MAX + col], HLB_FLAG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned long long ex = 0;
+    uint32_t spun = 0;
+    for (uint32_t k = 0; k < rc; ++k) {
+      unsigned long long w;
+      while (!((w = __hip_atomic_load(&hlb[(size_t)k * HOT_MAX + col], __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT)) & HLB_FLAG)) {
+        if (++spun > g_lb_spin_limit) break;
+        __builtin_amdgcn_s_sleep(1);
       }
+      ex += w & ~HLB_FLAG;
+    }
+    if (__ballot(spun > g_lb_spin_limit) && lane == 0) {
+      atomicOr(gerr, (uint32_t)ERR_SPIN);
+      __threadfence();
+    }
+    if (rc == HS_RCH - 1u) tot64[col] = ex + agg;
+    unsigned long long run = ex;  // (wave 0 alone reads and rewrites s_w; the others wait below)
+#pragma unroll
+    for (int k = 0; k < HS_W; ++k) {  // each wave's first row: the chunks before + the waves before
+      const unsigned long long y = s_w[k][lane];
+      s_w[k][lane] = run;
+      run += y;
+    }
   }
-  if (sl == 0) tot64[col] = tot;
+  __syncthreads();
+  {
+    unsigned long long run = s_w[wv][lane];
+    if (in_regs) {
+#pragma unroll
+      for (int u = 0; u < HS_Q; ++u)
+        if (r0 + u < r1) {
+          bhs[(size_t)(r0 + u) * HOT_MAX + col] = (uint32_t)run;
+          run += v[u];
+        }
+    } else {
+#pragma unroll 1
+      for (uint32_t rr = r0; rr < r1; rr += HS_Q) {  // the same rows again (L2)
+#pragma unroll
+        for (int u = 0; u < HS_Q; ++u) v[u] = bhs[(size_t)min(rr + u, r1 - 1u) * HOT_MAX + col];
+#pragma unroll
+        for (int u = 0; u < HS_Q; ++u)
+          if (rr + u < r1) {
+            bhs[(size_t)(rr + u) * HOT_MAX + col] = (uint32_t)run;
+            run += v[u];
+          }
+      }
+    }
+  }
   // hand-off to the last block (MI355X_MICROARCH.md, inter-workgroup visibility): every storing
   // wave drains, barrier, one lane's release + counter; the last arriver's lane acquires
   drain_vmem();
@@ -779,14 +860,23 @@ __global__ __launch_bounds__(HS_NT) void k_route_hot_scan(uint32_t nb, uint32_t 
   }
   __syncthreads();
   const uint32_t fl = s_fl, now_min = ~s_mn, now_max = s_mx;
-  if (*gerr) return;  // the batch is refused (its status is in x): nothing to add
+  const uint32_t ge = __hip_atomic_load(gerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool refused = ge != 0u;  // the batch is refused: nothing to add
+  if (refused && tid < n_shards)  // (the pack's status, or this kernel's look-back spin expiry)
+    x[2 * tid + 1] = ge & ERR_SPIN ? (uint32_t)RL_EDEVICE : (uint32_t)RL_EINVAL;
   const bool ok = !s_bad && !(fl & (RF_MISMATCH | RF_OVERFLOW)) && (!(fl & RF_HOT) || now_min == now_max);
-  if (!ok) {
-    if (tid == 0) rctl[0] = 1u;  // k_route_pack2<repack> redoes the batch without combining
+  h_out[tid] = ok && !refused ? (uint32_t)t : 0u;
+  if (tid == 0) {
+    h_out[HOT_MAX] = !refused && !ok ? 1u : 0u;
+    h_out[HOT_MAX + 1] = !refused && ok ? 1u : 0u;
+  }
+  if (refused || !ok) {
+    if (tid == 0 && !refused) rctl[0] = 1u;  // k_route_pack2<repack> redoes the batch without combining
+    __threadfence_system();
     return;
   }
   // rank of each non-empty group among its owner's groups (index order), per wave then over waves
-  const uint32_t lane = tid & 63, w = tid >> 6;
+  const uint32_t w = wv;
   const bool act = tid < (uint32_t)HOT_MAX && t > 0;
   const uint32_t o = act ? route_owner(e.a, e.b, n_shards) : (uint32_t)NS;
   uint32_t rank = 0;
@@ -823,6 +913,7 @@ __global__ __launch_bounds__(HS_NT) void k_route_hot_scan(uint32_t nb, uint32_t 
   __syncthreads();  // every group read x[] above
   if (tid < n_shards) x[2 * tid] += cnt;
   if (tid == 0) rctl[1] = 1u;  // combining applied
+  __threadfence_system();
 }
 
 // Origin: every descriptor's decision from its owner's raw reply.
@@ -835,57 +926,67 @@ __global__ __launch_bounds__(NT) void k_route_unpack_raw(DevBatch in, const DevR
                                                           const uint32_t* __restrict__ hot_pos,
                                                           const uint32_t* __restrict__ hot_tot,
                                                           const int32_t* __restrict__ owner_status, uint32_t stride,
-                                                          rl_status* __restrict__ out, uint32_t* __restrict__ req_thr) {
+                                                          rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
+                                                          uint32_t* __restrict__ zero, uint32_t zero_words) {
   const uint32_t i = blockIdx.x * NT + threadIdx.x;
-  if (i >= in.n_desc) return;
-  const uint32_t p = perm[i];
-  if (p == RL_ROUTE_LOCAL) {
-    // GetResponseDescriptorStatus("" key) -> {OK, nil limit, 0}  base_limiter.go:72-75
+  // the slot's look-back words and step words, cleared for its next step (the pack of step
+  // k + 2 runs behind this kernel on the same stream): no memset between steps
+  for (uint32_t k = i; k < zero_words; k += gridDim.x * NT) zero[k] = 0u;
+  const bool valid = i < in.n_desc;
+  uint32_t thr = 0, q = 0xFFFFFFFFu;
+  if (valid) {
     rl_status st;
-    st.code_flags = RL_CODE_OK;
     st.limit_remaining = 0;
     st.reset_s = 0;
     st.over_limit_delta = 0;
     st.near_limit_delta = 0;
+    const uint32_t p = perm[i];
+    q = in.req_of[i];
+    if (p == RL_ROUTE_LOCAL) {
+      st.code_flags = RL_CODE_OK;  // GetResponseDescriptorStatus("" key) -> {OK, nil limit, 0}  base_limiter.go:72-75
+    } else {
+      const uint32_t rule = in.rule[i];
+      const int64_t now = in.now[q];
+      const uint32_t ha = in.hits[q];
+      const uint32_t h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
+      const DevRule R = rules[rule];
+      const uint32_t hl = (p >> PERM_HOT_PRE_BITS) & (uint32_t)(HOT_MAX - 1);
+      const uint32_t pos = (p & PERM_HOT) ? hot_pos[hl] : p;
+      if (owner_status[pos / stride] != 0) {  // refused by its owner: undecided
+        st.code_flags = RL_CODE_UNKNOWN;
+      } else {
+        const RawReply rr = back[pos];
+        uint32_t after = rr.after;
+        if (p & PERM_HOT) {
+          // post-value of this descriptor's INCRBY inside its combined group: the group's reply
+          // minus the group's sum plus the inclusive prefix of h up to this descriptor (arrival order)
+          const uint32_t P = boff[(size_t)(i / PBLK) * HOT_MAX + hl] + (p & HOT_PRE_MAX) + h;
+          after = after - hot_tot[hl] + P;
+        }
+        const uint32_t now_mod = (uint32_t)now % R.div;  // now - (now / div) * div
+        thr = decide_status(after, (rr.flags & RAW_LOCAL_HIT) != 0u, h, now_mod, R, st);
+      }
+    }
     out[i] = st;
-    return;
   }
-  const uint32_t rule = in.rule[i], q = in.req_of[i];
-  const int64_t now = in.now[q];
-  const uint32_t ha = in.hits[q];
-  const uint32_t h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
-  const DevRule R = rules[rule];
-  const uint32_t pos = (p & PERM_HOT) ? hot_pos[(p >> PERM_HOT_PRE_BITS) & (uint32_t)(HOT_MAX - 1)] : p;
-  if (owner_status[pos / stride] != 0) {  // refused by its owner: undecided
-    rl_status st;
-    st.code_flags = RL_CODE_UNKNOWN;
-    st.limit_remaining = 0;
-    st.reset_s = 0;
-    st.over_limit_delta = 0;
-    st.near_limit_delta = 0;
-    out[i] = st;
-    return;
+  // DoLimitResponse.ThrottleMillis = max over the request's descriptors  base_limiter.go:163-165.
+  // A request's descriptors are consecutive (req_of nondecreasing, checked by the pack): a
+  // segmented max over the wave, then one store per request — a plain store when the request
+  // lies inside the wave, an atomicMax on the pack's zero when it crosses the wave's edge.
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t qo = (uint32_t)__shfl_up((int)q, d, 64);
+    const uint32_t to = (uint32_t)__shfl_up((int)thr, d, 64);
+    if (lane >= (uint32_t)d && qo == q) thr = max(thr, to);
   }
-  uint32_t after, fl;
-  if (p & PERM_HOT) {
-    // post-value of this descriptor's INCRBY inside its combined group: the group's reply minus
-    // the group's sum plus the inclusive prefix of h up to this descriptor (arrival order)
-    const uint32_t hl = (p >> PERM_HOT_PRE_BITS) & (uint32_t)(HOT_MAX - 1);
-    const uint32_t P = boff[(size_t)(i / PBLK) * HOT_MAX + hl] + (p & HOT_PRE_MAX) + h;
-    const RawReply rr = back[hot_pos[hl]];
-    after = rr.after - hot_tot[hl] + P;
-    fl = rr.flags;
-  } else {
-    const RawReply rr = back[p];
-    after = rr.after;
-    fl = rr.flags;
+  const uint32_t qn = (uint32_t)__shfl_down((int)q, 1, 64);
+  const uint32_t q0 = (uint32_t)__shfl((int)q, 0, 64);
+  const bool seg_end = lane == 63u || qn != q;
+  if (valid && seg_end && thr) {
+    if (lane < 63u && q != q0) req_thr[q] = thr;  // every descriptor of the request is in this wave
+    else atomicMax(&req_thr[q], thr);
   }
-  const uint32_t now_mod = (uint32_t)now % R.div;  // now - (now / div) * div
-  rl_status st;
-  const uint32_t thr = decide_status(after, (fl & RAW_LOCAL_HIT) != 0u, h, now_mod, R, st);
-  out[i] = st;
-  // DoLimitResponse.ThrottleMillis = max over the request's descriptors  base_limiter.go:163-165
-  if (thr) atomicMax(&req_thr[q], thr);
 }
 
 }  // namespace route
@@ -914,6 +1015,7 @@ void launch_route_pack_strided(hipStream_t st, const rl_batch& b, const DevRule*
 }
 
 uint32_t route2_blocks(uint32_t n) { return n ? (n + ROUTE2_BLOCK - 1) / ROUTE2_BLOCK : 1; }
+size_t route2_hot_lb_words() { return (size_t)route::HS_RCH * HOT_MAX * 2; }
 size_t route2_lb_words(uint32_t n) { return ((size_t)route2_blocks(n) * route::NS + 1 + 63) / 64 * 64; }
 size_t route2_bhs_words(uint32_t n) { return (size_t)route2_blocks(n) * HOT_MAX; }
 
@@ -928,16 +1030,17 @@ void launch_route_pack2(hipStream_t st, const rl_batch& b, const DevRule* rules,
   const size_t gw = (size_t)nb * route::NS;  // the error word follows the look-back words
   if (!hot) {
     hipLaunchKernelGGL((route::k_route_pack2<false, false>), dim3(nb), dim3(route::NT), 0, st, in, rules, n_rules, seed,
-                       origin, n_shards, stride, hot, o.send, o.perm, lb1, lb1 + gw, o.x, o.bhs, o.bstat, o.rctl);
+                       origin, n_shards, stride, hot, o.send, o.perm, lb1, lb1 + gw, o.x, o.bhs, o.bstat, o.rctl, o.thr);
     return;
   }
   hipLaunchKernelGGL((route::k_route_pack2<true, false>), dim3(nb), dim3(route::NT), 0, st, in, rules, n_rules, seed,
-                     origin, n_shards, stride, hot, o.send, o.perm, lb1, lb1 + gw, o.x, o.bhs, o.bstat, o.rctl);
-  hipLaunchKernelGGL(route::k_route_hot_scan, dim3(HOT_MAX / route::HS_COLS), dim3(route::HS_NT), 0, st, nb, n_shards,
-                     origin, stride, hot, o.bhs, o.bstat, o.send, o.x, o.rctl, o.hot_pos, o.hot_tot,
-                     reinterpret_cast<unsigned long long*>(o.rctl + 16), lb1 + gw);
+                     origin, n_shards, stride, hot, o.send, o.perm, lb1, lb1 + gw, o.x, o.bhs, o.bstat, o.rctl, o.thr);
+  unsigned long long* hlb = reinterpret_cast<unsigned long long*>(o.rctl + 16);  // zeroed with the look-back areas
+  hipLaunchKernelGGL(route::k_route_hot_scan, dim3(route::HS_CC * route::HS_RCH), dim3(route::HS_NT), 0, st, nb,
+                     n_shards, origin, stride, hot, o.bhs, o.bstat, o.send, o.x, o.rctl, o.hot_pos, o.hot_tot,
+                     hlb + (size_t)route::HS_RCH * HOT_MAX, lb1 + gw, o.h_hot, hlb);
   hipLaunchKernelGGL((route::k_route_pack2<false, true>), dim3(nb), dim3(route::NT), 0, st, in, rules, n_rules, seed,
-                     origin, n_shards, stride, hot, o.send, o.perm, lb2, lb2 + gw, o.x, o.bhs, o.bstat, o.rctl);
+                     origin, n_shards, stride, hot, o.send, o.perm, lb2, lb2 + gw, o.x, o.bhs, o.bstat, o.rctl, nullptr);
 }
 
 void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* rules, const RoutePackBufs& o,
@@ -945,7 +1048,8 @@ void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* r
                              uint32_t* thr) {
   if (!b.n_desc) return;
   hipLaunchKernelGGL(route::k_route_unpack_raw, dim3(route_blocks(b.n_desc)), dim3(route::NT), 0, st, make_dev_batch(b),
-                     rules, o.perm, back, o.bhs, o.hot_pos, o.hot_tot, owner_status, stride, out, thr);
+                     rules, o.perm, back, o.bhs, o.hot_pos, o.hot_tot, owner_status, stride, out, thr, o.lb,
+                     o.zero_words);
 }
 
 hipError_t route_set_spin_limit(uint32_t v) {

@@ -81,8 +81,9 @@ struct HostStage {
 // One shard's part of one step in flight.
 struct ShardStep {
   RoutePackBufs pb{};
-  uint8_t* zero = nullptr;    // look-back areas + control words, zeroed per step
+  uint8_t* zero = nullptr;    // look-back areas + control words: clear before every pack
   size_t zero_bytes = 0;
+  bool zeroed = true;         // the unpack cleared them (else the next pack memsets first)
   RRec* recv = nullptr;       // owner: records from every origin
   RawReply* reply = nullptr;  // owner: one raw reply per received record
   RawReply* back = nullptr;   // origin: replies to its records, strided like send
@@ -235,16 +236,20 @@ int rl_router::alloc_shard(Shard& s) {
     chk(hipMalloc(&t.pb.hot_pos, (size_t)HOT_MAX * 8));  // hot_pos | hot_tot
     t.pb.hot_tot = t.pb.hot_pos + HOT_MAX;
     // zeroed per step: two look-back areas and the control words; the hot scan's u64 sums follow
-    t.zero_bytes = (2 * lbw + 16) * 4;
+    t.zero_bytes = (2 * lbw + 16 + route2_hot_lb_words()) * 4;
     chk(hipMalloc(&t.zero, t.zero_bytes + (size_t)HOT_MAX * 8 + 64));
     t.pb.lb = reinterpret_cast<uint32_t*>(t.zero);
     t.pb.rctl = t.pb.lb + 2 * lbw;
+    t.pb.zero_words = (uint32_t)(t.zero_bytes / 4);
+    if (he == hipSuccess) chk(hipMemset(t.zero, 0, t.zero_bytes));
+    t.zeroed = true;
     chk(hipMalloc(&t.recv, D * G * REC));
     chk(hipMalloc(&t.reply, D * G * RAWB));
     chk(hipMalloc(&t.back, D * G * RAWB));
     chk(hipMalloc(&t.d_x, 8 * MAXS * 4));
     chk(hipHostMalloc(&t.h_x, (HX_HOT + HOT_MAX + 16) * 4, hipHostMallocDefault));
     t.pb.x = reinterpret_cast<uint32_t*>(t.d_x);
+    t.pb.h_hot = reinterpret_cast<uint32_t*>(t.h_x + HX_HOT);
     if (cfg.flags & RL_ROUTER_HOST) {
       chk(hipMalloc(&t.hs.d_in, in_bytes));
       chk(hipHostMalloc(&t.hs.h_in, in_bytes, hipHostMallocDefault));
@@ -309,18 +314,18 @@ void rl_router::pack(uint32_t s, uint32_t k) {
     (void)hipMemcpyAsync(t.d_x, t.h_x, 8 * G, hipMemcpyHostToDevice, S.os);
   };
   if (t.rc_pack || !t.b.n_desc) {
+    if (!t.rc_pack && t.b.n_req && t.thr) (void)hipMemsetAsync(t.thr, 0, (size_t)t.b.n_req * 4, S.os);
     send_status(t.rc_pack);
     return;
   }
   const bool combine = !(cfg.flags & RL_ROUTER_NO_COMBINE) && !S.v.local_cache && !S.hot.empty();
-  (void)hipMemsetAsync(t.zero, 0, t.zero_bytes, S.os);
+  if (!t.zeroed) (void)hipMemsetAsync(t.zero, 0, t.zero_bytes, S.os);  // (the slot's last step had no unpack)
+  t.pb.thr = t.thr;  // zeroed by the pack
+  // the hot scan writes the group sums and its verdict straight into the pinned mirror
   launch_route_pack2(S.os, t.b, S.v.rules, S.v.n_rules, S.v.seed, shard_id(s), G, cfg.max_desc,
                      combine ? S.d_hot : nullptr, t.pb);
+  t.zeroed = false;
   t.combined = combine;
-  if (combine) {
-    (void)hipMemcpyAsync(t.h_x + HX_HOT, t.pb.hot_tot, HOT_MAX * 4, hipMemcpyDeviceToHost, S.os);
-    (void)hipMemcpyAsync(t.h_x + HX_HOT + HOT_MAX, t.pb.rctl, 4 * 4, hipMemcpyDeviceToHost, S.os);
-  }
   const hipError_t he = hipGetLastError();
   if (he != hipSuccess || fault(PH_PACK, s)) {  // the pack cannot be trusted: fail the step everywhere
     t.rc_pack = RL_EHIP;
@@ -336,8 +341,8 @@ void rl_router::pack(uint32_t s, uint32_t k) {
 void rl_router::note_combine(uint32_t s, uint32_t k) {
   ShardStep& t = sh[s].st[k];
   if (!t.combined) return;
-  const uint32_t* ctl = reinterpret_cast<const uint32_t*>(t.h_x + HX_HOT + HOT_MAX);
-  if (ctl[0]) {
+  const uint32_t* ctl = reinterpret_cast<const uint32_t*>(t.h_x + HX_HOT + HOT_MAX);  // k_route_hot_scan
+  if (ctl[0] || !ctl[1]) {
     if (s == 0) ++st.repacks;
     sh[s].repacked = true;
     t.combined = false;
@@ -727,10 +732,10 @@ void rl_router::wait_rccl(uint32_t k) {
   if (he == hipSuccess) he = hipStreamWaitEvent(S.os, ev_rs, 0);
   st.reply_us = now_us() - t1;
   const double t2 = now_us();
-  if (he == hipSuccess && t.b.n_req) he = hipMemsetAsync(t.thr, 0, (size_t)t.b.n_req * 4, S.os);
-  if (he == hipSuccess) {  // (the owners' statuses arrived with the replies, d_x[5G, 6G))
+  if (he == hipSuccess) {  // (the owners' statuses arrived with the replies, d_x[5G, 6G); thr zeroed by the pack)
     launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 5 * G, cfg.max_desc, t.out, t.thr);
     he = hipGetLastError();
+    t.zeroed = he == hipSuccess && t.b.n_desc;
   }
   if (he == hipSuccess && slot[k].host) {
     if (t.b.n_desc)
@@ -791,10 +796,10 @@ void rl_router::wait_local(uint32_t k) {
     // delivers them)
     for (uint32_t j = 0; j < G; ++j) t.h_x[5 * G + j] = slot[k].status[j];
     if (hu == hipSuccess) hu = hipMemcpyAsync(t.d_x + 5 * G, t.h_x + 5 * G, 4 * G, hipMemcpyHostToDevice, S.os);
-    if (hu == hipSuccess && t.b.n_req) hu = hipMemsetAsync(t.thr, 0, (size_t)t.b.n_req * 4, S.os);
-    if (hu == hipSuccess) {
+    if (hu == hipSuccess) {  // (thr zeroed by the pack)
       launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 5 * G, cfg.max_desc, t.out, t.thr);
       hu = hipGetLastError();
+      t.zeroed = hu == hipSuccess && t.b.n_desc;
     }
     if (hu == hipSuccess && slot[k].host) {
       if (t.b.n_desc)
