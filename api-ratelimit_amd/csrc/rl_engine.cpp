@@ -1154,6 +1154,22 @@ int rl_wait_into(rl_engine* e, rl_status* out, uint32_t* req_throttle_ms) {
   return e->finish(out, req_throttle_ms, true);
 }
 
+int rl_wait_view(rl_engine* e, const rl_status** out, const uint32_t** req_throttle_ms) {
+  if (!e || !out || !req_throttle_ms) return RL_EINVAL;
+  *out = nullptr;
+  *req_throttle_ms = nullptr;
+  if (!e->n_fl) return e->fail(RL_ESTATE, "rl_wait_view without a batch in flight");
+  const rl_engine::Flight& f = e->fl[0];
+  if (!f.host || f.user_out || f.user_thr)
+    return e->fail(RL_ESTATE, "rl_wait_view: the oldest batch is not a host batch submitted without output pointers");
+  const uint32_t s = f.slot;
+  int rc = e->finish(nullptr, nullptr, true);  // (into, with no targets: no copy)
+  if (rc) return rc;
+  *out = e->stage[s].h_out;
+  *req_throttle_ms = e->stage[s].h_thr;
+  return 0;
+}
+
 int rl_submit_device(rl_engine* e, const rl_batch* b, rl_status* d_out, uint32_t* d_req_throttle_ms) {
   if (!e || !b) return RL_EINVAL;
   if (e->n_fl) return e->fail(RL_ESTATE, "rl_submit_device while a batch is in flight (call rl_wait)");

@@ -121,6 +121,7 @@ ABI = [
     ("rl_submit", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
     ("rl_wait", [C.c_void_p], C.c_int),
     ("rl_wait_into", [C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
+    ("rl_wait_view", [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
     ("rl_submit_device", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
     ("rl_submit_pipelined", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
     ("rl_stream", [C.c_void_p], C.c_void_p),
@@ -352,6 +353,16 @@ class Engine:
         thr = np.zeros(n_req, np.uint32)
         self._check(self.lib.rl_wait_into(self.h, _ptr(out) or None, _ptr(thr) or None), "rl_wait_into")
         return out, thr
+
+    def wait_view(self, n_desc: int, n_req: int):
+        """rl_wait_view: complete the oldest batch (a host batch submitted without output
+        pointers) and return numpy views of its results in the slot's pinned memory (valid until
+        the next submit)."""
+        po, pt = C.c_void_p(), C.c_void_p()
+        self._check(self.lib.rl_wait_view(self.h, C.byref(po), C.byref(pt)), "rl_wait_view")
+        out = np.ctypeslib.as_array(C.cast(po, C.POINTER(C.c_uint8)), shape=(n_desc * STATUS_DTYPE.itemsize,))
+        thr = np.ctypeslib.as_array(C.cast(pt, C.POINTER(C.c_uint32)), shape=(n_req,))
+        return out.view(STATUS_DTYPE), thr
 
     def host_acquire(self) -> dict:
         """rl_host_acquire: numpy views of the next free pinned staging slot (zero-copy submit)."""

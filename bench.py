@@ -564,7 +564,15 @@ def main():
 
         held = {}  # pinned slot (blob address) -> the batch built in it
 
-        def host_round(bs, copy):
+        pv, pt = C.c_void_p(), C.c_void_p()
+
+        def collect(view):
+            if view:  # results read where they landed (rl_wait_view: the slot's pinned arrays)
+                eng._check(eng.lib.rl_wait_view(eng.h, C.byref(pv), C.byref(pt)), "rl_wait_view")
+            else:  # copied out into caller memory (rl_wait_into)
+                eng._check(eng.lib.rl_wait_into(eng.h, out_h.ctypes.data, thr_h.ctypes.data), "rl_wait_into")
+
+        def host_round(bs, copy, view=True):
             pend = 0
             for k, b in enumerate(bs):
                 sl = eng.host_acquire()
@@ -577,10 +585,10 @@ def main():
                 eng.submit_staged(b.n_desc, b.n_req, int(b.blob.shape[0]), sl)
                 pend += 1
                 if pend == hiprl.MAX_IN_FLIGHT:
-                    eng._check(eng.lib.rl_wait_into(eng.h, out_h.ctypes.data, thr_h.ctypes.data), "rl_wait_into")
+                    collect(view)
                     pend -= 1
             for _ in range(pend):
-                eng._check(eng.lib.rl_wait_into(eng.h, out_h.ctypes.data, thr_h.ctypes.data), "rl_wait_into")
+                collect(view)
 
         h2d_gbs, d2h_gbs, bi_gbs = pcie_rates()
         nb3 = hiprl.MAX_IN_FLIGHT
@@ -591,6 +599,9 @@ def main():
         th = time.perf_counter()
         host_round(rep, False)
         t_staged = (time.perf_counter() - th) / len(rep)
+        th = time.perf_counter()
+        host_round(rep, False, view=False)
+        t_into = (time.perf_counter() - th) / len(rep)
         # the copy into a slot alone (a caller that builds elsewhere)
         sl = eng.host_acquire()
         tc = time.perf_counter()
@@ -598,7 +609,7 @@ def main():
             fill(sl, b)
         t_copy = (time.perf_counter() - tc) / 4
         th = time.perf_counter()
-        host_round(hbatches, True)
+        host_round(hbatches, True, view=False)
         t_with_copy = (time.perf_counter() - th) / len(hbatches)
         h2d_b = sum(int(b.blob.shape[0]) + 32 + 4 * (b.n_desc + 1) + 8 * b.n_desc + 12 * b.n_req for b in rep) / len(rep)
         d2h_b = sum(20 * b.n_desc + 4 * b.n_req for b in rep) / len(rep)
@@ -613,9 +624,11 @@ def main():
                 "achieved_GBps": {"h2d": round(h2d_b / t_staged / 1e9, 1), "d2h": round(d2h_b / t_staged / 1e9, 1)},
                 "device_kernels_ms_per_batch": round(step_ms, 4),
                 "staging_copy_ms_per_batch": round(t_copy * 1e3, 4),
+                "copy_out": {"value": round(d / t_into, 1), "ms_per_batch": round(t_into * 1e3, 4)},
                 "with_copy": {"value": round(d / t_with_copy, 1), "ms_per_batch": round(t_with_copy * 1e3, 4)},
                 "note": "staged: batches built in place in the engine's pinned slots (rl_host_acquire), 3 in flight, "
-                        "H2D + kernels + D2H timed, results copied out by rl_wait_into; with_copy adds a numpy copy of "
+                        "H2D + kernels + D2H timed, results read in the slot (rl_wait_view); copy_out: the same with "
+                        "results copied into caller memory (rl_wait_into); with_copy: copy_out plus a numpy copy of "
                         "every array into the slot per batch; bound = max(H2D bytes / H2D rate, D2H bytes / D2H "
                         "rate), both directions concurrent"}
 

@@ -157,10 +157,47 @@ def test_host_path_three_in_flight_and_staged(local_cache):
             e.submit_host_async(b)
         pend.append(b)
         if len(pend) == hiprl.MAX_IN_FLIGHT:
-            got.append(e.wait_into(pend[0].n_desc, pend[0].n_req))
+            got.append(_collect(e, pend[0], k))
             pend.pop(0)
-    for b in pend:
-        got.append(e.wait_into(b.n_desc, b.n_req))
+    for j, b in enumerate(pend):
+        got.append(_collect(e, b, j))
     want = _oracle(hbs, streams.RULES, local_cache)
     streams.assert_same(*want, np.concatenate([g[0] for g in got]), np.concatenate([g[1] for g in got]), "host path")
     assert e.stats()["host_batches"] == len(hbs)
+
+
+def _collect(e, b, k):
+    """Every other batch through rl_wait_view (results read in the pinned slot, copied here
+    before the next submit reuses it), the others through rl_wait_into."""
+    if k % 2:
+        st, thr = e.wait_view(b.n_desc, b.n_req)
+        return st.copy(), thr.copy()
+    return e.wait_into(b.n_desc, b.n_req)
+
+
+def test_wait_view_refuses_device_batches():
+    """rl_wait_view only hands out a host batch's slot: on a device batch it gives RL_ESTATE,
+    completes nothing, and rl_wait still completes that batch."""
+    import router
+
+    dev = torch.device("cuda", 0)
+    reqs = [("wv", [[("k", str(i % 11))]], [0], 1, 1_700_000_000) for i in range(200)]
+    hb = hiprl.build_batch(reqs)
+    db = router.DeviceBatch.from_host(hb, dev)
+    out = torch.zeros(200 * 20, dtype=torch.uint8, device=dev)
+    thr = torch.zeros(200, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    e = hiprl.Engine(max_batch_desc=1 << 10)
+    e.load_rules(streams.RULES)
+    e.submit_device_async(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), out.data_ptr(), thr.data_ptr())
+    with pytest.raises(hiprl.RedisError):
+        e.wait_view(hb.n_desc, hb.n_req)
+    e.wait()
+    # a host batch submitted with nothing in flight: its view equals the oracle's answer
+    e.submit_host_async(hb)
+    st, th = e.wait_view(hb.n_desc, hb.n_req)
+    o = oracle.Oracle()
+    o.load_rules(streams.RULES)
+    o.submit(hb)  # the device batch above decided the same requests first
+    ost, oth = o.submit(hb)
+    streams.assert_same(ost, oth, st.copy(), th.copy(), "wait_view")
