@@ -767,16 +767,26 @@ __global__ __launch_bounds__(HS_NT) void k_route_hot_scan(uint32_t nb, uint32_t 
 #pragma unroll
     for (int k = 0; k < HS_W; ++k) agg += s_w[k][lane];
     __hip_atomic_store(&hlb[(size_t)rc * HOT_MAX + col], HLB_FLAG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every earlier chunk's word loaded at once (one memory round trip per poll, not one per
+    // chunk: the chunks publish their sums right away, so the first poll usually finds them all)
     unsigned long long ex = 0;
     uint32_t spun = 0;
-    for (uint32_t k = 0; k < rc; ++k) {
-      unsigned long long w;
-      while (!((w = __hip_atomic_load(&hlb[(size_t)k * HOT_MAX + col], __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT)) & HLB_FLAG)) {
-        if (++spun > g_lb_spin_limit) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-      ex += w & ~HLB_FLAG;
+    uint32_t pending = (1u << rc) - 1u;  // rc < HS_RCH <= 16
+    while (pending) {
+      unsigned long long wv[HS_RCH];
+#pragma unroll
+      for (int k = 0; k < HS_RCH; ++k)
+        wv[k] = __hip_atomic_load(&hlb[(size_t)min((uint32_t)k, rc) * HOT_MAX + col], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int k = 0; k < HS_RCH; ++k)
+        if (((pending >> k) & 1u) && (wv[k] & HLB_FLAG)) {
+          ex += wv[k] & ~HLB_FLAG;
+          pending &= ~(1u << k);
+        }
+      if (__ballot(pending != 0u) == 0ull) break;
+      if (++spun > g_lb_spin_limit) break;
+      __builtin_amdgcn_s_sleep(1);
     }
     if (__ballot(spun > g_lb_spin_limit) && lane == 0) {
       atomicOr(gerr, (uint32_t)ERR_SPIN);

@@ -53,6 +53,16 @@ constexpr uint32_t ROUTE_HOT_KEEP = 64;    // a group stays while its origin sen
 static_assert(REC == RL_ROUTE_RECORD_BYTES && RAWB == sizeof(rl_raw_reply), "record layouts");
 constexpr uint32_t HX_HOT = 8 * MAXS;      // pinned mirror: hot sums, then the control words
 
+// Host wait for an event by polling: a blocking stream synchronize sleeps and wakes 10-20 us
+// after the GPU is done, on the routed step's critical path between exchanges.
+hipError_t poll_event(hipEvent_t ev) {
+  for (int k = 0; k < (1 << 20); ++k) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e;
+  }
+  return hipEventSynchronize(ev);
+}
+
 double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -135,6 +145,8 @@ struct rl_router {
   ncclComm_t comm = nullptr;
   hipStream_t rs = nullptr;  // exchanges
   hipEvent_t ev_rs = nullptr;
+  hipEvent_t ev_cnt = nullptr;  // the counts' host copy
+  hipEvent_t ev_end = nullptr;  // the reply exchange (rs) and the unpack (os) of the step
   std::vector<Shard> sh;
   StepSlot slot[NSLOT];
   uint64_t seq = 0, done = 0;
@@ -207,12 +219,13 @@ void rl_router::free_all() {
   if (d_ag) (void)hipFree(d_ag);
   if (h_ag) (void)hipHostFree(h_ag);
   if (comm) (void)ncclCommDestroy(comm);
-  if (ev_rs) (void)hipEventDestroy(ev_rs);
+  for (hipEvent_t e : {ev_rs, ev_cnt, ev_end})
+    if (e) (void)hipEventDestroy(e);
   if (rs) (void)hipStreamDestroy(rs);
   d_ag = nullptr;
   h_ag = nullptr;
   comm = nullptr;
-  ev_rs = nullptr;
+  ev_rs = ev_cnt = ev_end = nullptr;
   rs = nullptr;
 }
 
@@ -434,7 +447,8 @@ int rl_router::submit_rccl(uint32_t k) {
   ncclResult_t nr = ncclAllToAll(t.d_x, t.d_x + 2 * G, 2, ncclInt32, comm, rs);
   if (nr != ncclSuccess) return nccl_fail(nr, "ncclAllToAll(counts)");
   if (he == hipSuccess) he = hipMemcpyAsync(t.h_x, t.d_x, 16 * G, hipMemcpyDeviceToHost, rs);
-  if (he == hipSuccess) he = hipStreamSynchronize(rs);
+  if (he == hipSuccess) he = hipEventRecord(ev_cnt, rs);
+  if (he == hipSuccess) he = poll_event(ev_cnt);
   if (he != hipSuccess) {  // the counts are unknown: nobody can take part in the record exchange
     broken = true;
     if (comm) (void)ncclCommAbort(comm);
@@ -742,9 +756,17 @@ void rl_router::wait_rccl(uint32_t k) {
       he = hipMemcpyAsync(t.hs.h_out, t.out, (size_t)t.b.n_desc * sizeof(rl_status), hipMemcpyDeviceToHost, S.os);
     if (he == hipSuccess && t.b.n_req) he = hipMemcpyAsync(t.hs.h_thr, t.thr, (size_t)t.b.n_req * 4, hipMemcpyDeviceToHost, S.os);
   }
-  const hipError_t h2 = hipStreamSynchronize(rs);
-  if (he == hipSuccess) he = h2;
-  if (he == hipSuccess) he = hipStreamSynchronize(S.os);
+  // the unpack waited for the reply exchange (ev_rs), so one event on os covers both streams;
+  // after a failure to enqueue, drain both streams
+  hipError_t h2;
+  if (he == hipSuccess && hipEventRecord(ev_end, S.os) == hipSuccess) {
+    h2 = poll_event(ev_end);
+    he = h2;
+  } else {
+    h2 = hipStreamSynchronize(rs);
+    if (he == hipSuccess) he = h2;
+    if (he == hipSuccess) he = hipStreamSynchronize(S.os);
+  }
   if (he == hipSuccess && fault(PH_UNPACK, 0)) he = hipErrorUnknown;
   st.unpack_us = now_us() - t2;
   for (uint32_t j = 0; j < G; ++j) slot[k].status[j] = h2 == hipSuccess ? t.h_x[5 * G + j] : RL_EHIP;
@@ -901,7 +923,10 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
     return code;
   };
   if (hipStreamCreateWithFlags(&r->rs, hipStreamNonBlocking) != hipSuccess) return bail(RL_EHIP);
-  if (hipEventCreateWithFlags(&r->ev_rs, hipEventDisableTiming) != hipSuccess) return bail(RL_EHIP);
+  if (hipEventCreateWithFlags(&r->ev_rs, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&r->ev_cnt, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&r->ev_end, hipEventDisableTiming) != hipSuccess)
+    return bail(RL_EHIP);
   r->sh.resize(n_eng);
   for (uint32_t s = 0; s < n_eng; ++s) {
     r->sh[s].e = engines[s];
