@@ -505,15 +505,15 @@ def main():
     occ = eng.occupancy()
 
     # Host (PCIe) path (what a Go service sees, rl_submit of host batches, three in flight):
-    #  - pcie: H2D / D2H / both-directions copy bandwidth of this box (pinned, 64 MB);
+    #  - the link bound: one batch's exact copies (six H2D arrays, two D2H arrays) moved by the
+    #    link alone, H2D and D2H on two streams (tools/pcie_probe.py's shapes);
     #  - staged: batches built in place in the engine's pinned slots (rl_host_acquire), as a Go
     #    batcher writes its requests straight into C memory: only H2D, kernels and D2H are timed
     #    (each slot holds its batch from an untimed first pass; the batches repeat, which changes
     #    counters, not the cost); results copied out by rl_wait_into;
     #  - with_copy: the same with a numpy copy of every array into the slot per batch (the
     #    round-2 line, a caller whose batches live elsewhere in host memory);
-    #  - the bound: max(H2D bytes / H2D rate, D2H bytes / D2H rate) per batch, the directions
-    #    concurrent, against the measured per-batch time.
+    #  - frac_of_pcie_bound = that bound / the measured per-batch time.
     host = None
     if not args.no_host_path and not routed:
         hbatches = []
@@ -525,33 +525,36 @@ def main():
         out_h = np.empty(d, hiprl.STATUS_DTYPE)
         thr_h = np.empty(d, np.uint32)
 
-        def pcie_rates():
-            nbytes = 64 << 20
-            hsrc = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
-            hdst = torch.empty(nbytes, dtype=torch.uint8).pin_memory()
-            dbuf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-            dbuf2 = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        def link_probe(sz_in, sz_out, n=20):
+            """ms per batch for the link to move one batch's exact copies (the engine's six H2D
+            arrays on one stream, its two D2H arrays on another; pinned host buffers): H2D alone,
+            D2H alone, and both directions concurrently (the host path's bound)."""
+            hin = [torch.empty(x, dtype=torch.uint8).pin_memory() for x in sz_in]
+            din = [torch.empty(x, dtype=torch.uint8, device=dev) for x in sz_in]
+            hout = [torch.empty(x, dtype=torch.uint8).pin_memory() for x in sz_out]
+            dout = [torch.empty(x, dtype=torch.uint8, device=dev) for x in sz_out]
             s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
 
-            def timed(fn, reps=10):
-                fn()
+            def run(k, do_in, do_out):
+                for _ in range(k):
+                    if do_in:
+                        with torch.cuda.stream(s1):
+                            for h, dd in zip(hin, din):
+                                dd.copy_(h, non_blocking=True)
+                    if do_out:
+                        with torch.cuda.stream(s2):
+                            for h, dd in zip(hout, dout):
+                                h.copy_(dd, non_blocking=True)
+
+            res = []
+            for do_in, do_out in ((True, False), (False, True), (True, True)):
+                run(2, do_in, do_out)
                 torch.cuda.synchronize()
                 t1 = time.perf_counter()
-                for _ in range(reps):
-                    fn()
+                run(n, do_in, do_out)
                 torch.cuda.synchronize()
-                return (time.perf_counter() - t1) / reps
-
-            h2d = nbytes / timed(lambda: dbuf.copy_(hsrc, non_blocking=True)) / 1e9
-            d2h = nbytes / timed(lambda: hdst.copy_(dbuf2, non_blocking=True)) / 1e9
-
-            def both():
-                with torch.cuda.stream(s1):
-                    dbuf.copy_(hsrc, non_blocking=True)
-                with torch.cuda.stream(s2):
-                    hdst.copy_(dbuf2, non_blocking=True)
-            bi = 2 * nbytes / timed(both) / 1e9
-            return h2d, d2h, bi
+                res.append((time.perf_counter() - t1) / n)
+            return res
 
         def fill(sl, b):
             n = int(b.blob.shape[0])
@@ -590,11 +593,10 @@ def main():
             for _ in range(pend):
                 collect(view)
 
-        h2d_gbs, d2h_gbs, bi_gbs = pcie_rates()
         nb3 = hiprl.MAX_IN_FLIGHT
         # the untimed first pass builds a batch in every slot; the staged rounds reuse them
         host_round(hbatches[:nb3], True)
-        rep = [hbatches[k % nb3] for k in range(len(hbatches))]  # (sizes for the byte counts)
+        rep = [hbatches[k % nb3] for k in range(max(3 * len(hbatches), 30))]  # (sizes for the byte counts)
         host_round(rep[:2], False)
         th = time.perf_counter()
         host_round(rep, False)
@@ -602,6 +604,10 @@ def main():
         th = time.perf_counter()
         host_round(rep, False, view=False)
         t_into = (time.perf_counter() - th) / len(rep)
+        ab = hbatches[0]
+        t_h2d, t_d2h, t_link = link_probe(
+            [int(ab.blob.shape[0]) + 32, 4 * (ab.n_desc + 1), 4 * ab.n_desc, 4 * ab.n_desc, 8 * ab.n_req, 4 * ab.n_req],
+            [20 * ab.n_desc, 4 * ab.n_req])
         # the copy into a slot alone (a caller that builds elsewhere)
         sl = eng.host_acquire()
         tc = time.perf_counter()
@@ -613,11 +619,13 @@ def main():
         t_with_copy = (time.perf_counter() - th) / len(hbatches)
         h2d_b = sum(int(b.blob.shape[0]) + 32 + 4 * (b.n_desc + 1) + 8 * b.n_desc + 12 * b.n_req for b in rep) / len(rep)
         d2h_b = sum(20 * b.n_desc + 4 * b.n_req for b in rep) / len(rep)
-        bound_s = max(h2d_b / (h2d_gbs * 1e9), d2h_b / (d2h_gbs * 1e9))
+        bound_s = t_link
         host = {"value": round(d / t_staged, 1), "unit": "descriptor decisions/s",
                 "ms_per_batch": round(t_staged * 1e3, 4),
-                "pcie_measured_GBps": {"h2d": round(h2d_gbs, 1), "d2h": round(d2h_gbs, 1),
-                                       "both_directions": round(bi_gbs, 1)},
+                "pcie_measured_GBps": {"h2d": round(h2d_b / t_h2d / 1e9, 1), "d2h": round(d2h_b / t_d2h / 1e9, 1),
+                                       "both_directions": round((h2d_b + d2h_b) / t_link / 1e9, 1)},
+                "link_ms_per_batch": {"h2d": round(t_h2d * 1e3, 4), "d2h": round(t_d2h * 1e3, 4),
+                                      "both": round(t_link * 1e3, 4)},
                 "bytes_per_batch": {"h2d": int(h2d_b), "d2h": int(d2h_b)},
                 "pcie_bound_ms_per_batch": round(bound_s * 1e3, 4),
                 "frac_of_pcie_bound": round(bound_s / t_staged, 3),
@@ -629,8 +637,9 @@ def main():
                 "note": "staged: batches built in place in the engine's pinned slots (rl_host_acquire), 3 in flight, "
                         "H2D + kernels + D2H timed, results read in the slot (rl_wait_view); copy_out: the same with "
                         "results copied into caller memory (rl_wait_into); with_copy: copy_out plus a numpy copy of "
-                        "every array into the slot per batch; bound = max(H2D bytes / H2D rate, D2H bytes / D2H "
-                        "rate), both directions concurrent"}
+                        "every array into the slot per batch; bound = the link moving one batch's exact copies (six H2D "
+                        "arrays on one stream, two D2H arrays on another, pinned buffers, nothing else running), "
+                        "both directions concurrent (link_ms_per_batch.both)"}
 
     if rank != 0:
         if dist:
