@@ -219,7 +219,7 @@ void HipRateLimitCache::submit(Staged& st) {
     b.req_of = st.hb.req_of;
     b.now = st.hb.now;
     b.hits_addend = st.hb.hits_addend;
-    rc = rl_submit(eng_, &b, nullptr, nullptr);  // results stay in the engine until rl_wait_into
+    rc = rl_submit(eng_, &b, nullptr, nullptr);  // results stay in the slot until rl_wait_view
     if (!rc) n_batches_ += 1;
   }
   if (rc) {
@@ -228,12 +228,13 @@ void HipRateLimitCache::submit(Staged& st) {
   }
 }
 
-// Collect the oldest batch in flight: rl_wait_into copies its results out during the call.
+// Collect the oldest batch in flight: rl_wait_view hands out its results in the slot's pinned
+// memory (no copy), read here before the next submit reuses the slot.
 void HipRateLimitCache::finish(Staged& st) {
   if (st.failed) return;
-  std::vector<rl_status> out(st.nd);
-  std::vector<uint32_t> thr(st.nr);
-  if (rl_wait_into(eng_, out.data(), thr.data())) {
+  const rl_status* out = nullptr;
+  const uint32_t* thr = nullptr;
+  if (rl_wait_view(eng_, &out, &thr)) {
     fail(st.calls);
     return;
   }

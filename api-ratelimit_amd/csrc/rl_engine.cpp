@@ -883,9 +883,10 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   const size_t N = c.max_batch_desc, R = c.max_batch_req, B = c.max_blob_bytes;
   // host staging: blob | off | rule | req | now | hits (same layout on host and device)
   e->o_off = align_up(B + RL_BLOB_SLACK, 256);
+  // prefix_off, rule_id and req_of at one pitch: their H2D copies go as one 2-D copy
   e->o_rule = e->o_off + align_up((N + 1) * 4, 256);
-  e->o_req = e->o_rule + align_up(N * 4, 256);
-  e->o_now = e->o_req + align_up(N * 4, 256);
+  e->o_req = e->o_rule + align_up((N + 1) * 4, 256);
+  e->o_now = e->o_req + align_up((N + 1) * 4, 256);
   e->o_hits = e->o_now + align_up(R * 8, 256);
   e->in_bytes = e->o_hits + align_up(R * 4, 256);
   for (auto& g : e->stage) {
@@ -1125,9 +1126,15 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
   e->acquired = -1;
   hipError_t he = hipSuccess;
   // Copy only the used extents of each array, on the copy-in stream: the previous batch's
-  // kernels keep running meanwhile.
+  // kernels keep running meanwhile. prefix_off / rule_id / req_of (one pitch apart) move as one
+  // 2-D copy: four copies per batch instead of six (each costs 10-20 us of copy-engine gap).
   const size_t ext[] = {(size_t)b->blob_bytes + RL_BLOB_SLACK, arrs[1].n, arrs[2].n, arrs[3].n, arrs[4].n, arrs[5].n};
-  for (int k = 0; k < 6 && he == hipSuccess; ++k)
+  if (ext[0]) he = hipMemcpyAsync(g.d_in, h, ext[0], hipMemcpyHostToDevice, e->xin);
+  if (he == hipSuccess && b->n_desc) {
+    const size_t pitch = e->o_rule - e->o_off;
+    he = hipMemcpy2DAsync(g.d_in + e->o_off, pitch, h + e->o_off, pitch, ext[1], 3, hipMemcpyHostToDevice, e->xin);
+  }
+  for (int k = 4; k < 6 && he == hipSuccess; ++k)
     if (ext[k]) he = hipMemcpyAsync(g.d_in + arrs[k].o, h + arrs[k].o, ext[k], hipMemcpyHostToDevice, e->xin);
   if (he == hipSuccess) he = hipEventRecord(e->ev_in[s], e->xin);
   if (he != hipSuccess) return e->hip_fail(he, "hipMemcpyAsync(H2D)");

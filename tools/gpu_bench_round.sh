@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU call of measurements: smoke, the N=1 bench line, the routed step on a one-rank RCCL
 # communicator (torchrun, two steps in flight), G logical shards (records per owner, step
-# breakdown, G-GPU estimate), the config-1 row. Each step under its own limit; a crash, abort
+# breakdown, G-GPU estimate), the config-1 row; on request the PCIe probe and rocprofv3
+# timelines (rtrace: routed steps; htrace: host path kernels + copies; strace: single GPU). Each step under its own limit; a crash, abort
 # or timeout (rc >= 124) stops the call there.
 # usage (on the GPU box, from the repo root): tools/gpu_bench_round.sh <tag> [steps...]
 set -u
@@ -35,6 +36,20 @@ for s in "${@:-smoke bench routed1 ls8 ls2 config1}"; do
                  --output-format csv -- python3 -u bench.py --force-routed --steps 30 --warmup 10 --cpu-seconds 0 \
                  --no-host-path --no-roofline-probe && cp /tmp/rprof_$TAG/run_kernel_stats.csv "$OUT/routed_kernel_stats.csv" ;;
       config1) run config1 400 python -u bench.py --config 1 --steps 200 --warmup 20 --cpu-seconds 6 --no-roofline-probe ;;
+      pcie) run pcie 120 python -u tools/pcie_probe.py 20 ;;
+      rtrace) mkdir -p /tmp/rt_$TAG && run rtrace 600 rocprofv3 --kernel-trace --stats -d /tmp/rt_$TAG -o run \
+                 --output-format csv -- python3 -u bench.py --force-routed --steps 30 --warmup 10 --cpu-seconds 0 \
+                 --no-host-path --no-roofline-probe --no-kernel-times --prefill 2000 \
+                 && python3 tools/trace_tail.py /tmp/rt_$TAG/run_kernel_trace.csv 80 > "$OUT/routed_timeline.txt" ;;
+      htrace) mkdir -p /tmp/ht_$TAG && run htrace 600 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/ht_$TAG -o run \
+                 --output-format csv -- python3 -u bench.py --cpu-seconds 0 --no-roofline-probe --no-kernel-times \
+                 --steps 20 --prefill 200 \
+                 && python3 tools/copy_timeline.py /tmp/ht_$TAG/run_kernel_trace.csv /tmp/ht_$TAG/run_memory_copy_trace.csv \
+                    200 500 > "$OUT/host_copy_timeline.txt" ;;
+      strace) mkdir -p /tmp/st_$TAG && run strace 600 rocprofv3 --kernel-trace --stats -d /tmp/st_$TAG -o run \
+                 --output-format csv -- python3 -u bench.py --steps 30 --warmup 5 --cpu-seconds 0 --no-host-path \
+                 --no-roofline-probe --no-kernel-times \
+                 && python3 tools/timeline.py /tmp/st_$TAG/run_kernel_trace.csv 24 > "$OUT/timeline.txt" ;;
     esac
   done
 done
