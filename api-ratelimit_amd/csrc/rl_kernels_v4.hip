@@ -157,13 +157,21 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
                                               uint32_t* __restrict__ req_thr, uint32_t* __restrict__ fpart,
                                               uint16_t* __restrict__ tstart, unsigned long long* __restrict__ thsum,
                                               MRec* __restrict__ srec, rl_status* __restrict__ out, EngineCtl* ctl) {
-  __shared__ HotEntry sh_hot[HOT_SLOTS + HOT_MAX];  // tag words, then the entries (rl_common.h)
+  // sh_hot (the hot table: tag words, then the entries, rl_common.h) and s_res (hot in-tile
+  // prefixes) share one pool: once every thread holds its descriptors' prefixes, the pool
+  // stages half a tile of records at a time for coalesced, whole-line stores.
+  constexpr size_t HOT_LDS = sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX);
+  __shared__ __attribute__((aligned(32))) uint8_t s_pool[HOT_LDS + sizeof(unsigned long long) * T];
+  HotEntry* const sh_hot = reinterpret_cast<HotEntry*>(s_pool);
+  unsigned long long* const s_res = reinterpret_cast<unsigned long long*>(s_pool + HOT_LDS);
+  MRec* const s_stage = reinterpret_cast<MRec*>(s_pool);
+  constexpr uint32_t STAGE = (uint32_t)(sizeof(s_pool) / sizeof(MRec));  // records per staging pass
+  static_assert(HOT_LDS % 16 == 0 && STAGE >= (uint32_t)T / 2 && T % STAGE == 0, "record staging");
   __shared__ uint16_t sh_cnt[ROW];
   __shared__ unsigned long long sh_hs[HOT_BUCKETS];
   __shared__ uint16_t s_d[T];
   __shared__ uint16_t s_pa[T], s_pb[T];
   __shared__ uint32_t s_h[T];
-  __shared__ unsigned long long s_res[T];
   __shared__ uint32_t s_cnt[W][64];
   __shared__ uint32_t sh_w[W];
   __shared__ SegEl s_agg[W];
@@ -327,37 +335,60 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   }
   STH(6);
   // Records in bucket order. A hot record carries its in-tile INCRBY prefix and its bucket;
-  // an MSD record its sort key and fp_lo; a nil-limit descriptor is decided here.
+  // an MSD record its sort key and fp_lo; a nil-limit descriptor is decided here. Each record
+  // goes to its sorted position in the LDS stage (half a tile per pass), and the stage leaves
+  // in 16-B stores, consecutive across the block: whole 128-B lines, where scattered 32-B
+  // stores left partly written lines for the L2 to evict (≈14 MB of extra writes per batch).
+  uint32_t spos[R];
+  unsigned long long sres[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint32_t o = r * NT + tid;
-    const uint32_t i = t0 + o;
-    const D3& x = d[r];
-    if (x.bucket == BKT_NONE) continue;
-    if (x.bucket == NIL_BUCKET) {
-      if (ROUTED && !req_thr) {  // raw replies (a routed batch never carries a nil limit)
-        emit_raw(out, i, 0u, RAW_NIL);
+    spos[r] = s_pb[o];
+    sres[r] = d[r].bucket < (uint32_t)HOT_BUCKETS ? s_res[o] : 0ull;
+  }
+  const uint32_t nvalid = min((uint32_t)T, in.n_desc > t0 ? in.n_desc - t0 : 0u);  // the tile's records
+  for (uint32_t h0 = 0; h0 < (uint32_t)T; h0 += STAGE) {
+    __syncthreads();  // (h0 = 0: every thread has read s_res; else: the previous pass's copy is done)
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const uint32_t o = r * NT + tid;
+      const uint32_t i = t0 + o;
+      const D3& x = d[r];
+      if (x.bucket == BKT_NONE || spos[r] - h0 >= STAGE) continue;
+      if (x.bucket == NIL_BUCKET) {
+        if (ROUTED && !req_thr) {  // raw replies (a routed batch never carries a nil limit)
+          emit_raw(out, i, 0u, RAW_NIL);
+          continue;
+        }
+        // GetResponseDescriptorStatus("" key) -> {OK, nil limit, 0}  base_limiter.go:72-75
+        rl_status st;
+        st.code_flags = RL_CODE_OK;
+        st.limit_remaining = 0;
+        st.reset_s = 0;
+        st.over_limit_delta = 0;
+        st.near_limit_delta = 0;
+        out[i] = st;
         continue;
       }
-      // GetResponseDescriptorStatus("" key) -> {OK, nil limit, 0}  base_limiter.go:72-75
-      rl_status st;
-      st.code_flags = RL_CODE_OK;
-      st.limit_remaining = 0;
-      st.reset_s = 0;
-      st.over_limit_delta = 0;
-      st.near_limit_delta = 0;
-      out[i] = st;
-      continue;
+      const bool hotb = x.bucket < (uint32_t)HOT_BUCKETS;
+      MRec m;
+      m.key = hotb ? (uint64_t)sres[r] : x.key;
+      m.fp_lo = hotb ? (uint64_t)x.bucket : x.lo;
+      m.idx = i;
+      m.req = x.req;
+      m.h = x.h;
+      m.rn = rule_of(x.rule) | (x.now_mod << V4_RULE_BITS);
+      s_stage[spos[r] - h0] = m;
     }
-    const bool hotb = x.bucket < (uint32_t)HOT_BUCKETS;
-    MRec m;
-    m.key = hotb ? (uint64_t)s_res[o] : x.key;
-    m.fp_lo = hotb ? (uint64_t)x.bucket : x.lo;
-    m.idx = i;
-    m.req = x.req;
-    m.h = x.h;
-    m.rn = rule_of(x.rule) | (x.now_mod << V4_RULE_BITS);
-    srec[t0 + s_pb[o]] = m;
+    __syncthreads();
+    // the pass's records (positions past the tile's valid ones hold nil / past-the-end
+    // descriptors: never read, and not stored past the batch)
+    const uint32_t np = nvalid > h0 ? min(STAGE, nvalid - h0) : 0u;
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));  // 16-B aligned: one dwordx4 each
+    const v4u* sv = reinterpret_cast<const v4u*>(s_stage);
+    v4u* dv = reinterpret_cast<v4u*>(srec + t0 + h0);
+    for (uint32_t c = tid; c < np * (uint32_t)(sizeof(MRec) / 16); c += NT) dv[c] = sv[c];
   }
   __syncthreads();
   uint32_t* trow = reinterpret_cast<uint32_t*>(tstart + (size_t)tile * ROW);
