@@ -16,11 +16,12 @@ traffic is 8000 distinct 1e6-descriptor batches.
 
 Multi-GPU (torchrun, one rank per GPU): the key space is hash-sharded one
 shard per GPU. Every rank ingests its own 1e6-descriptor batch per step, routes each
-descriptor to the GPU owning its key with an RCCL all-to-all (32-B records), the owners
-decide, and the 24-B replies return with the reverse all-to-all — weak scaling. The step
-runs through the C-ABI router (rl_router_step, csrc/rl_router.cpp: the Go host's entry point,
-its own RCCL communicator); --torch-router runs it through api-ratelimit_amd/router.py
-(torch.distributed) instead. value = descriptors decided for all ranks / max-over-ranks time.
+descriptor to the GPU owning its key with an RCCL all-to-all (32-B records; one combined
+record per hot key per origin), the owners decide, and 8-B raw replies return with the reverse
+all-to-all; the origins decide from them — weak scaling, two steps in flight. The step runs
+through the C-ABI router (rl_router_submit / rl_router_wait, csrc/rl_router.cpp: the Go
+host's entry point, its own RCCL communicator); --torch-router runs the round-2 step through
+api-ratelimit_amd/router.py (torch.distributed) instead. value = descriptors decided for all ranks / max-over-ranks time.
 --independent runs N unrouted replicas instead (each rank its own key space).
 
 Also reported (rank 0): per-kernel HIP-event times over an extra K steps, the roofline of the
@@ -686,6 +687,14 @@ def main():
         cpu = cpu_baseline(args, rules, d, seed, K, b0)
 
     live_frac = [round(occ["live"][r] / occ["slots"][r], 4) for r in range(8)]
+    if routed and nrt is not None:
+        parallelism = (f"key-sharded x{world}, RCCL all-to-all routing through the C-ABI router (32-B records out, one "
+                       f"per hot key per origin with combining; 8-B raw replies back; {RDEPTH} steps in flight)")
+    elif routed:
+        parallelism = (f"key-sharded x{world}, RCCL all-to-all routing through router.ShardRouter (32-B records out, "
+                       f"24-B replies back)")
+    else:
+        parallelism = "single shard" if world == 1 else f"x{world} independent replicas (no collective)"
     line = {
         "metric": "descriptor decisions/sec, 100M keys Zipf, 1-8 GPUs; % of HBM peak" if args.config == 3
         else f"descriptor decisions/sec (config {args.config})",
@@ -702,10 +711,7 @@ def main():
         "data": "synthetic (seeded splitmix64 / bounded Zipf stream, generated on the device, resident in HBM)",
         "config": {"workload": wl, "descriptors_per_batch": d, "requests_per_batch": d,
                    "batches_per_second_window": K, "prefill_batches": prefill,
-                   "parallelism": (f"key-sharded x{world}, RCCL all-to-all routing (32-B records out, 24-B replies back)"
-                                   + (", C-ABI router (rl_router_step)" if nrt is not None else "")
-                                   if routed else "single shard" if world == 1
-                                   else f"x{world} independent replicas (no collective)"),
+                   "parallelism": parallelism,
                    "pipeline": args.pipeline, "batches_in_flight": RDEPTH if nrt is not None else DEPTH,
                    "combining": (not args.no_combine) if nrt is not None else None,
                    "unique_keys_per_batch": int(U)},
