@@ -365,15 +365,23 @@ class Engine:
         return out.view(STATUS_DTYPE), thr
 
     def host_acquire(self) -> dict:
-        """rl_host_acquire: numpy views of the next free pinned staging slot (zero-copy submit)."""
+        """rl_host_acquire: numpy views of the next free pinned staging slot (zero-copy submit).
+        The views of a slot are built once and reused (the slots rotate; a batcher's loop should
+        not pay for six ctypes casts per batch)."""
         hb = RlHostBatch()
         self._check(self.lib.rl_host_acquire(self.h, C.byref(hb)), "rl_host_acquire")
+        cache = self.__dict__.setdefault("_slot_views", {})
+        got = cache.get(hb.prefix_blob)
+        if got is not None:
+            return got
 
         def view(ptr, n, dt):
             return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(n,))
-        return dict(blob=view(hb.prefix_blob, hb.max_blob, np.uint8), off=view(hb.prefix_off, hb.max_desc + 1, np.uint32),
-                    rule=view(hb.rule_id, hb.max_desc, np.uint32), req_of=view(hb.req_of, hb.max_desc, np.uint32),
-                    now=view(hb.now, hb.max_req, np.int64), hits=view(hb.hits_addend, hb.max_req, np.uint32))
+        got = dict(blob=view(hb.prefix_blob, hb.max_blob, np.uint8), off=view(hb.prefix_off, hb.max_desc + 1, np.uint32),
+                   rule=view(hb.rule_id, hb.max_desc, np.uint32), req_of=view(hb.req_of, hb.max_desc, np.uint32),
+                   now=view(hb.now, hb.max_req, np.int64), hits=view(hb.hits_addend, hb.max_req, np.uint32))
+        cache[hb.prefix_blob] = got
+        return got
 
     def submit_staged(self, n_desc: int, n_req: int, blob_bytes: int, staged: dict):
         """rl_submit of a batch built in place in an acquired staging slot (no host copy)."""
