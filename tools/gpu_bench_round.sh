@@ -32,6 +32,7 @@ for s in "${@:-smoke bench routed1 ls8 ls2 config1}"; do
                  --no-host-path --no-roofline-probe ;;
       ls8) run ls8 600 python -u bench.py --logical-shards 8 --steps 10 --warmup 3 --prefill 40 ;;
       ls2) run ls2 600 python -u bench.py --logical-shards 2 --steps 10 --warmup 3 --prefill 40 ;;
+      ls4) run ls4 600 python -u bench.py --logical-shards 4 --steps 10 --warmup 3 --prefill 40 ;;
       rprof) mkdir -p /tmp/rprof_$TAG && run rprof 600 rocprofv3 --kernel-trace --stats -d /tmp/rprof_$TAG -o run \
                  --output-format csv -- python3 -u bench.py --force-routed --steps 30 --warmup 10 --cpu-seconds 0 \
                  --no-host-path --no-roofline-probe && cp /tmp/rprof_$TAG/run_kernel_stats.csv "$OUT/routed_kernel_stats.csv" ;;
