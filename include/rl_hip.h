@@ -201,10 +201,13 @@ int rl_wait(rl_engine* e);
  * req_throttle_ms[n_req] (a host batch's, or NULL to discard). */
 int rl_wait_into(rl_engine* e, rl_status* out, uint32_t* req_throttle_ms);
 /* Complete the oldest batch in flight, a host batch (rl_submit) whose outputs were NULL, and
- * hand out its results where they landed: the slot's pinned arrays (C memory; a cgo caller
- * reads them through unsafe slices, no copy). *out holds n_desc statuses and *req_throttle_ms
- * n_req words; both stay valid until the next submit call (which reuses the slot). A device
- * batch, or a host batch submitted with output pointers, gives RL_ESTATE (nothing completed).
+ * hand out its results where they landed: its staging slot's pinned arrays (C memory; a cgo
+ * caller reads them through unsafe slices, no copy). *out holds n_desc statuses and
+ * *req_throttle_ms n_req words. They stay valid until the slot is reused: until the batch
+ * submitted RL_MAX_IN_FLIGHT places after this one is submitted (a caller that keeps two
+ * batches in flight and collects one after each submit may read them until its next submit
+ * after this call returns). A device batch, or a host batch submitted with output pointers,
+ * gives RL_ESTATE (nothing completed).
  * Replaces the copy of rl_wait_into for a batcher that answers its callers straight from the
  * slot (DoLimit's []*DescriptorStatus, src/redis/fixed_cache_impl.go:108-123). */
 int rl_wait_view(rl_engine* e, const rl_status** out, const uint32_t** req_throttle_ms);
