@@ -1,6 +1,7 @@
 // rl_cache.cpp — HipRateLimitCache: the reference's RateLimitCache contract on the HIP engine.
 #include "rl_cache.hpp"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 
@@ -196,35 +197,51 @@ void HipRateLimitCache::done_calls(size_t n) {
 
 // Hand the slot's batch to the engine. New (L, unit) rules are appended to the device table
 // first: that is allowed while the previous batch is in flight (rule ids keep their meaning,
-// rl_hip.h rl_load_rules), and a refusal fails this batch's calls, keeping the table dirty.
-void HipRateLimitCache::submit(Staged& st) {
-  int rc = 0;
-  if (rules_dirty_) {
-    rc = rl_load_rules(eng_, rules_.data(), (uint32_t)rules_.size());
-    if (!rc) {
-      rules_dirty_ = false;
-      n_loads_ += 1;
-      if (n_inflight_batches_) n_loads_inflight_ += 1;
+// rl_hip.h rl_load_rules). Two things need nothing in flight (RL_ESTATE otherwise): a rule
+// table that crosses V4_MAX_RULES or outgrows its allocation, and a second batch in flight once
+// the engine runs the LSD pipeline (more than 32768 rules). Then the batches in flight are
+// completed first (their callers answered) and the load / submit is made again; any other
+// refusal fails this batch's calls, keeping the table dirty.
+void HipRateLimitCache::submit(Staged& st, std::deque<Staged>& inflight) {
+  for (int attempt = 0;; ++attempt) {
+    int rc = 0;
+    if (rules_dirty_) {
+      rc = rl_load_rules(eng_, rules_.data(), (uint32_t)rules_.size());
+      if (!rc) {
+        rules_dirty_ = false;
+        n_loads_ += 1;
+        if (!inflight.empty()) n_loads_inflight_ += 1;
+      }
     }
-  }
-  if (!rc) {
-    rl_batch b;
-    memset(&b, 0, sizeof b);
-    b.n_desc = st.nd;
-    b.n_req = st.nr;
-    b.blob_bytes = st.nb;
-    b.prefix_blob = st.hb.prefix_blob;  // the slot's own arrays: rl_submit does not copy them
-    b.prefix_off = st.hb.prefix_off;
-    b.rule_id = st.hb.rule_id;
-    b.req_of = st.hb.req_of;
-    b.now = st.hb.now;
-    b.hits_addend = st.hb.hits_addend;
-    rc = rl_submit(eng_, &b, nullptr, nullptr);  // results stay in the slot until rl_wait_view
-    if (!rc) n_batches_ += 1;
-  }
-  if (rc) {
-    fail(st.calls);
-    st.failed = true;
+    if (!rc) {
+      rl_batch b;
+      memset(&b, 0, sizeof b);
+      b.n_desc = st.nd;
+      b.n_req = st.nr;
+      b.blob_bytes = st.nb;
+      b.prefix_blob = st.hb.prefix_blob;  // the slot's own arrays: rl_submit does not copy them
+      b.prefix_off = st.hb.prefix_off;
+      b.rule_id = st.hb.rule_id;
+      b.req_of = st.hb.req_of;
+      b.now = st.hb.now;
+      b.hits_addend = st.hb.hits_addend;
+      rc = rl_submit(eng_, &b, nullptr, nullptr);  // results stay in the slot until rl_wait_view
+      if (!rc) n_batches_ += 1;
+    }
+    if (rc == RL_ESTATE && attempt == 0 && !inflight.empty()) {
+      // the slot acquired for this batch stays this batch's: completing the others submits nothing
+      while (!inflight.empty()) {
+        finish(inflight.front());
+        inflight.pop_front();
+      }
+      n_drains_ += 1;
+      continue;
+    }
+    if (rc) {
+      fail(st.calls);
+      st.failed = true;
+    }
+    return;
   }
 }
 
@@ -284,7 +301,6 @@ void HipRateLimitCache::submitter() {
         g.unlock();
         finish(inflight.front());
         inflight.pop_front();
-        n_inflight_batches_ = inflight.size();
         continue;
       }
       cv_.wait(g, [&] { return stop_ || !q_.empty(); });
@@ -318,19 +334,33 @@ void HipRateLimitCache::submitter() {
           add(st, c);
         }
         if (stop_ || st.nd >= s_.batch_limit) break;
-        if (cv_.wait_until(g, deadline) == std::cv_status::timeout && q_.empty()) break;
+        if (!inflight.empty()) {
+          // while gathering, answer the batch in flight as soon as the device is done with it
+          // (rl_query), not when this window closes: under light load a caller's latency is then
+          // its batch's own, not that plus the next batch's window
+          g.unlock();
+          const int qr = rl_query(eng_);
+          if (qr == 1) {
+            finish(inflight.front());
+            inflight.pop_front();
+          }
+          g.lock();
+          if (qr == 1) continue;
+          const auto slice = std::min(deadline, std::chrono::steady_clock::now() + std::chrono::microseconds(10));
+          cv_.wait_until(g, slice);
+        } else if (cv_.wait_until(g, deadline) == std::cv_status::timeout && q_.empty()) {
+          break;
+        }
         if (std::chrono::steady_clock::now() >= deadline) break;
       }
     full:;
     }
-    submit(st);
+    submit(st, inflight);
     inflight.push_back(std::move(st));
-    n_inflight_batches_ = inflight.size();
     if (inflight.size() == 2) {
       finish(inflight.front());
       inflight.pop_front();
     }
-    n_inflight_batches_ = inflight.size();
   }
   for (auto& st : inflight) finish(st);
 }

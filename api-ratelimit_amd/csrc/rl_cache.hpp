@@ -163,10 +163,14 @@ class HipRateLimitCache : public RateLimitCache {
 
   // Batcher counters (tests): batches submitted, rule-table loads, and loads made while an
   // earlier batch was still in flight (append-only rule table, rl_hip.h rl_load_rules).
+  // drains: times the batches in flight were completed early so that a rule-table load or a
+  // submit the engine refused with them in flight (RL_ESTATE) could be made.
   struct BatcherStats {
-    uint64_t batches, rule_loads, rule_loads_in_flight;
+    uint64_t batches, rule_loads, rule_loads_in_flight, drains;
   };
-  BatcherStats batcher_stats() const { return {n_batches_.load(), n_loads_.load(), n_loads_inflight_.load()}; }
+  BatcherStats batcher_stats() const {
+    return {n_batches_.load(), n_loads_.load(), n_loads_inflight_.load(), n_drains_.load()};
+  }
 
  private:
   struct Call;
@@ -175,7 +179,7 @@ class HipRateLimitCache : public RateLimitCache {
   uint32_t rule_id(const RateLimitLimit& l, bool shadow);
   bool fits(const Staged& st, const Call& c) const;
   void add(Staged& st, const std::shared_ptr<Call>& c);
-  void submit(Staged& st);
+  void submit(Staged& st, std::deque<Staged>& inflight);
   void finish(Staged& st);
   void fail(std::vector<std::shared_ptr<Call>>& calls);
   void done_calls(size_t n);
@@ -194,8 +198,7 @@ class HipRateLimitCache : public RateLimitCache {
   std::map<std::pair<uint32_t, uint32_t>, uint32_t> rule_ids_;
   std::vector<rl_rule> rules_;
   bool rules_dirty_ = false;
-  size_t n_inflight_batches_ = 0;  // submitter thread only
-  std::atomic<uint64_t> n_batches_{0}, n_loads_{0}, n_loads_inflight_{0};
+  std::atomic<uint64_t> n_batches_{0}, n_loads_{0}, n_loads_inflight_{0}, n_drains_{0};
 };
 
 }  // namespace ratelimit

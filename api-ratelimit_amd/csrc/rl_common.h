@@ -209,8 +209,41 @@ struct RegionOcc {
   uint32_t gen;    // window generation the count belongs to
   uint32_t live;   // slots claimed for that generation
   uint32_t limit;  // load limit (slots)
-  uint32_t pad;
+  uint32_t prev;   // SECOND-home regions: slots of the region's previous generation (gen - 2), still live
 };
+
+// Slot reuse (window expiry). A slot of an older window generation is free for a key of
+// generation G. In the two SECOND-home regions (a key string lives one second there) the
+// region's previous generation stays live too — a slot is free only when its generation g
+// satisfies g + 2 < G — so a request may come up to 3 s behind the newest time the table has
+// seen (requests of several origins in rank order, a multi-GPU step whose origins' clocks
+// or batch cuts differ) and still find its key string. MINUTE/HOUR/DAY strings
+// live a minute or more per generation: there the previous generation is already that far back.
+__host__ __device__ __forceinline__ bool lazy_region(uint32_t region) { return region < 2u; }
+__host__ __device__ __forceinline__ bool slot_free_for(uint32_t g, uint32_t G, uint32_t region) {
+  return lazy_region(region) ? (g == 0u || g + 2u < G) : g < G;
+}
+// Slots of region r that a key of generation `gen` cannot take (capacity check).
+__host__ __device__ __forceinline__ uint32_t region_live(const RegionOcc& o, uint32_t r, uint32_t gen) {
+  if (!lazy_region(r)) return o.gen < gen ? 0u : o.live;
+  uint32_t v = 0;
+  if (o.gen + 2u >= gen) v += o.live;  // generation o.gen >= gen - 2
+  if (o.gen >= gen) v += o.prev;       // generation o.gen - 2 >= gen - 2
+  return v;
+}
+// After a batch: its new slots `ins` of generation gm in region r (gm = 0: untouched).
+__host__ __device__ __forceinline__ void occ_advance(RegionOcc& o, uint32_t r, uint32_t gm, uint32_t ins) {
+  if (!gm) return;
+  if (o.gen < gm) {
+    o.prev = (lazy_region(r) && o.gen + 2u == gm) ? o.live : 0u;
+    o.gen = gm;
+    o.live = ins;
+  } else if (lazy_region(r) && o.gen == gm + 2u) {
+    o.prev += ins;  // a batch behind the region's newest generation (its slots are generation gm)
+  } else {
+    o.live += ins;
+  }
+}
 
 // Hot-key set entry: a key prefix seen with many descriptors per batch. (a, b) is the
 // fingerprint lane state after the prefix bytes (length folded in), i.e. a 128-bit hash of

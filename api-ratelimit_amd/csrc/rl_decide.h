@@ -65,7 +65,7 @@ RL_DEV void slot_reset(Slot* s, uint64_t key) {
 }
 
 // Find the slot of (key, fp_lo) for window generation G in its region, or claim an empty one
-// (a slot whose generation is older than G is empty for this window: window expiry). The
+// (a slot of an older generation is empty for this window: window expiry, slot_free_for). The
 // capacity check (RegionOcc, before any table write) keeps every region below its load
 // limit, so a free slot always exists within the region: the probe is bounded by its size.
 // A claimed slot is reset by the caller (slot_reset) before anything reads it: a key's slot
@@ -98,7 +98,7 @@ RL_DEV bool table_claim_pre(const TableDesc& tab, uint64_t key, uint64_t fp_lo, 
       st_out = cur.st;
       return true;
     }
-    if (g < G) {  // empty for this window generation: claim it
+    if (slot_free_for(g, G, key_region(key))) {  // empty for this window generation: claim it
       const unsigned long long want = ((unsigned long long)tag << 32) | G;
       const unsigned long long old = atomicCAS((unsigned long long*)&s->ctrl, (unsigned long long)cur.ctrl, want);
       if (old == cur.ctrl) {
@@ -197,12 +197,11 @@ RL_DEV void exotic_sequence(KeyState& s, const TableDesc& tab, const DevRule* __
 // slot. Counts are per window generation: a newer generation finds the region empty (its
 // older slots are free for it). gmax / cnt: the batch's generation and descriptor count per
 // region (0 = untouched).
-RL_DEV uint32_t region_live(const RegionOcc& o, uint32_t gen) { return (o.gen < gen) ? 0u : o.live; }
 RL_DEV bool capacity_ok(const RegionOcc (&o)[8], const uint32_t* gmax, const uint32_t* cnt) {
   bool ok = true;
 #pragma unroll
   for (int r = 0; r < 8; ++r)
-    ok &= !cnt[r] || (uint64_t)region_live(o[r], gmax[r]) + cnt[r] <= (uint64_t)o[r].limit;
+    ok &= !cnt[r] || (uint64_t)region_live(o[r], (uint32_t)r, gmax[r]) + cnt[r] <= (uint64_t)o[r].limit;
   return ok;
 }
 RL_DEV bool capacity_ok(const RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* cnt) {
@@ -216,12 +215,7 @@ RL_DEV void occ_update(RegionOcc* __restrict__ occ, const uint32_t* gmax, const 
   for (int r = 0; r < 8; ++r) {
     if (!gmax[r]) continue;  // region untouched
     RegionOcc o = occ[r];
-    if (o.gen < gmax[r]) {
-      o.gen = gmax[r];
-      o.live = ins[r];
-    } else {
-      o.live += ins[r];
-    }
+    occ_advance(o, (uint32_t)r, gmax[r], ins[r]);
     occ[r] = o;
   }
 }

@@ -308,15 +308,7 @@ struct rl_engine {
   int submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, RReply* reply, hipEvent_t in_ev,
                     bool inputs_ready, bool host, rl_status* user_out, uint32_t* user_thr);
   void occ_host_update(const EngineCtl* c) {
-    for (int r = 0; r < 8; ++r) {
-      if (!c->gen_max[r]) continue;
-      if (occ[r].gen < c->gen_max[r]) {
-        occ[r].gen = c->gen_max[r];
-        occ[r].live = c->ins[r];
-      } else {
-        occ[r].live += c->ins[r];
-      }
-    }
+    for (int r = 0; r < 8; ++r) occ_advance(occ[r], (uint32_t)r, c->gen_max[r], c->ins[r]);
   }
   uint64_t live_total() const {
     uint64_t s = 0;
@@ -327,6 +319,7 @@ struct rl_engine {
     for (int r = 0; r < 8; ++r) {
       occ[r].gen = 0;
       occ[r].live = 0;
+      occ[r].prev = 0;
     }
     hipError_t e = hipMemcpy(d_occ, occ, sizeof occ, hipMemcpyHostToDevice);
     return e == hipSuccess ? 0 : hip_fail(e, "reset occupancy");
@@ -869,7 +862,7 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     e->occ[r].gen = 0;
     e->occ[r].live = 0;
     e->occ[r].limit = (uint32_t)(((uint64_t)1 << lg) * c.max_load_permille / 1000);
-    e->occ[r].pad = 0;
+    e->occ[r].prev = 0;
     off += (size_t)1 << lg;
   }
   e->tab.split = c.per_second_split ? 1u : 0u;
@@ -1153,6 +1146,17 @@ int rl_wait(rl_engine* e) {
   if (!e) return RL_EINVAL;
   if (!e->n_fl) return e->fail(RL_ESTATE, "rl_wait without a batch in flight");
   return e->finish(nullptr, nullptr, false);
+}
+
+int rl_query(rl_engine* e) {
+  if (!e) return RL_EINVAL;
+  if (!e->n_fl) return e->fail(RL_ESTATE, "rl_query without a batch in flight");
+  const rl_engine::Flight& f = e->fl[0];
+  if (f.settled) return 1;
+  const hipError_t q = hipEventQuery(e->done_ev[f.slot]);
+  if (q == hipSuccess) return 1;
+  if (q == hipErrorNotReady) return 0;
+  return e->hip_fail(q, "hipEventQuery");
 }
 
 int rl_wait_into(rl_engine* e, rl_status* out, uint32_t* req_throttle_ms) {

@@ -61,7 +61,7 @@ void rlx_engine_hot(rl_engine* e, std::vector<HotKey>& out);
 struct RoutePackBufs {
   RRec* send;          // n_shards * stride records
   uint32_t* perm;      // per descriptor: record position | PERM_HOT group code | RL_ROUTE_LOCAL
-  uint32_t* x;         // [2 * n_shards]: (count, status) per owner
+  uint32_t* x;         // [xs * n_shards]: (count, status[, tmin, tmax]) per owner
   uint32_t* lb;        // look-back words + error word, two areas (pack, repack), zeroed by the caller
   uint32_t* bhs;       // [blocks][HOT_MAX] hot h sums per block -> exclusive prefixes over blocks
   uint32_t* bstat;     // [blocks][4] per block: ~min now, max now, flags of its hot descriptors
@@ -72,6 +72,8 @@ struct RoutePackBufs {
   uint32_t* h_hot;     // pinned host [HOT_MAX + 2]: group sums, repack flag, applied flag (k_route_hot_scan)
   uint32_t* thr;       // the origin's ThrottleMillis output: zeroed by the pack (nullable)
   uint32_t zero_words; // lb / rctl words the unpack clears for the slot's next step (from lb)
+  uint32_t xs;         // words per owner in x: 2 = (count, status); 4 = (count, status, tmin, tmax)
+  uint32_t* tr;        // [8][64] zeroed: the pack blocks' request-time range words (xs = 4)
 };
 uint32_t route2_blocks(uint32_t n);
 size_t route2_lb_words(uint32_t n);     // one area

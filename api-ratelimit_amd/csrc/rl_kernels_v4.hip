@@ -1659,12 +1659,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
     const uint32_t r = tid;
     ctl->ins[r] = s_ins[r];
     if (gm) {
-      if (ro.gen < gm) {
-        ro.gen = gm;
-        ro.live = s_ins[r];
-      } else {
-        ro.live += s_ins[r];
-      }
+      occ_advance(ro, r, gm, s_ins[r]);
       occ[r] = ro;
     }
   }

@@ -494,13 +494,14 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
                                                      uint32_t* __restrict__ perm, uint32_t* lb, uint32_t* gerr,
                                                      uint32_t* __restrict__ x, uint32_t* __restrict__ bhs,
                                                      uint32_t* __restrict__ bstat, const uint32_t* __restrict__ rctl,
-                                                     uint32_t* __restrict__ req_thr) {
+                                                     uint32_t* __restrict__ req_thr, uint32_t xs, uint32_t* tr) {
   __shared__ uint32_t s_wc[PR][PW][NS + 2];
   __shared__ uint32_t s_tot[NS], s_base[NS];
   __shared__ uint32_t s_err;
   __shared__ uint32_t s_tags[COMBINE ? HOT_TAGS : 1];
   __shared__ uint32_t s_hw[COMBINE ? PV : 1][COMBINE ? HOT_MAX : 1];
   __shared__ uint32_t s_st[3];  // the block's hot descriptors: ~min now, max now, RF_* flags
+  __shared__ uint32_t s_tr[2];  // the block's routed descriptors: ~min now, max now + 1 (0: none)
   if (REPACK && rctl[0] == 0u) return;  // combining was accepted: nothing to redo
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6, bi = blockIdx.x;
   if (!REPACK && req_thr)  // ThrottleMillis starts at 0 (k_route_unpack_raw takes the max per request)
@@ -513,6 +514,7 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
   }
   if (tid == 0) s_err = 0;
   if (tid < 3) s_st[tid] = 0;
+  if (tid < 2) s_tr[tid] = 0;
   __syncthreads();
   const uint32_t i0 = bi * PBLK, last = in.n_desc - 1u;  // n_desc >= 1, n_req >= 1 (host-checked)
   // two levels of loads, each issued together at clamped indices (k_route_pack1)
@@ -647,6 +649,21 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
     if (stf) atomicOr(&s_st[2], stf);
   }
   if (err) atomicOr(&s_err, err);
+  if (!REPACK) {  // the batch's request-time range (every owner learns it in the counts exchange)
+    uint32_t tmn = 0xFFFFFFFFu, tmx = 0;
+#pragma unroll
+    for (int r = 0; r < PR; ++r)
+      if (cat[r] != CAT_LOCAL) {
+        tmn = min(tmn, rec[r].now);
+        tmx = max(tmx, rec[r].now);
+      }
+    tmn = wave_min_u32(tmn);
+    tmx = wave_max_u32(tmx);
+    if (lane == 0 && tmn <= tmx) {
+      atomicMax(&s_tr[0], ~tmn);
+      atomicMax(&s_tr[1], tmx + 1u);
+    }
+  }
   __syncthreads();
   if (tid < NS) {  // per owner: exclusive offsets of the (round, wave) runs, block total
     uint32_t run = 0;
@@ -674,13 +691,31 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
     atomicOr(gerr, s_err);
     __threadfence();
   }
+  if (!REPACK && tid == 0 && s_tr[0]) {
+    // into one of 8 lines (fewer same-line atomics in a row); returning atomics, their values
+    // consumed: performed before this thread publishes owner 0's look-back word below, so the
+    // last block, whose look-back transitively saw every block's word, reads every block's range
+    uint32_t* tw = tr + (size_t)(bi & 7u) * 64u;
+    const uint32_t pa = __hip_atomic_fetch_max(&tw[0], s_tr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t pb = __hip_atomic_fetch_max(&tw[1], s_tr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" ::"v"(pa), "v"(pb));
+  }
+  if (!REPACK && tid == 0 && s_tr[0]) {
+    // into one of 8 lines (fewer same-line atomics in a row); returning atomics, their values
+    // consumed: performed before this thread publishes owner 0's look-back word below, so the
+    // last block, whose look-back transitively saw every block's word, reads every block's range
+    uint32_t* tw = tr + (size_t)(bi & 7u) * 64u;
+    const uint32_t pa = __hip_atomic_fetch_max(&tw[0], s_tr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t pb = __hip_atomic_fetch_max(&tw[1], s_tr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("" ::"v"(pa), "v"(pb));
+  }
   if (COMBINE && tid < 3) bstat[(size_t)bi * 4 + tid] = s_st[tid];
   __syncthreads();
   for (uint32_t j = w; j < n_shards; j += PW) {  // wave-uniform
     const uint32_t excl = lookback_owner(lb, gerr, bi, j, s_tot[j]);
     if (lane == 0) {
       s_base[j] = excl;
-      if (bi == gridDim.x - 1u) x[2 * j] = excl + s_tot[j];  // the last block: every owner's cold total
+      if (bi == gridDim.x - 1u) x[xs * j] = excl + s_tot[j];  // the last block: every owner's cold total
     }
   }
   __syncthreads();
@@ -689,7 +724,18 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
     const uint32_t e = __hip_atomic_load(gerr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t status = e & ERR_SPIN ? (uint32_t)RL_EDEVICE
                             : e & (ERR_BAD_INPUT | ERR_BAD_TIME) ? (uint32_t)RL_EINVAL : 0u;
-    for (uint32_t j = 0; j < n_shards; ++j) x[2 * j + 1] = status;
+    for (uint32_t j = 0; j < n_shards; ++j) x[xs * j + 1] = status;
+    if (!REPACK && xs >= 4u) {  // (tmin, tmax) of the batch's routed descriptors to every owner
+      uint32_t mn = 0, mx = 0;
+      for (uint32_t l = 0; l < 8u; ++l) {
+        mn = max(mn, __hip_atomic_fetch_or(&tr[l * 64u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        mx = max(mx, __hip_atomic_fetch_or(&tr[l * 64u + 1u], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+      for (uint32_t j = 0; j < n_shards; ++j) {
+        x[xs * j + 2] = mn ? ~mn : 0xFFFFFFFFu;
+        x[xs * j + 3] = mx ? mx - 1u : 0u;
+      }
+    }
   }
 #pragma unroll
   for (int r = 0; r < PR; ++r) {
@@ -733,7 +779,7 @@ __global__ __launch_bounds__(HS_NT) void k_route_hot_scan(uint32_t nb, uint32_t 
                                                            uint32_t* __restrict__ hot_pos,
                                                            uint32_t* __restrict__ hot_tot,
                                                            unsigned long long* tot64, uint32_t* gerr,
-                                                           uint32_t* h_out, unsigned long long* hlb) {
+                                                           uint32_t* h_out, unsigned long long* hlb, uint32_t xs) {
   __shared__ unsigned long long s_w[HS_W][64];
   __shared__ uint32_t s_last, s_mn, s_mx, s_fl, s_bad;
   __shared__ uint32_t s_oc[4][NS + 1];
@@ -873,7 +919,7 @@ __global__ __launch_bounds__(HS_NT) void k_route_hot_scan(uint32_t nb, uint32_t 
   const uint32_t ge = __hip_atomic_load(gerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const bool refused = ge != 0u;  // the batch is refused: nothing to add
   if (refused && tid < n_shards)  // (the pack's status, or this kernel's look-back spin expiry)
-    x[2 * tid + 1] = ge & ERR_SPIN ? (uint32_t)RL_EDEVICE : (uint32_t)RL_EINVAL;
+    x[xs * tid + 1] = ge & ERR_SPIN ? (uint32_t)RL_EDEVICE : (uint32_t)RL_EINVAL;
   const bool ok = !s_bad && !(fl & (RF_MISMATCH | RF_OVERFLOW)) && (!(fl & RF_HOT) || now_min == now_max);
   h_out[tid] = ok && !refused ? (uint32_t)t : 0u;
   if (tid == 0) {
@@ -905,7 +951,7 @@ __global__ __launch_bounds__(HS_NT) void k_route_hot_scan(uint32_t nb, uint32_t 
   uint32_t before = 0, cnt = 0;
   if (act) {
     for (uint32_t k = 0; k < 4; ++k) before += k < w ? s_oc[k][o] : 0u;
-    const uint32_t pos = o * stride + x[2 * o] + before + rank;
+    const uint32_t pos = o * stride + x[xs * o] + before + rank;
     RRec r;
     r.a = e.a;
     r.b = e.b;
@@ -921,7 +967,7 @@ __global__ __launch_bounds__(HS_NT) void k_route_hot_scan(uint32_t nb, uint32_t 
     for (uint32_t k = 0; k < 4; ++k) cnt += s_oc[k][tid];
   }
   __syncthreads();  // every group read x[] above
-  if (tid < n_shards) x[2 * tid] += cnt;
+  if (tid < n_shards) x[xs * tid] += cnt;
   if (tid == 0) rctl[1] = 1u;  // combining applied
   __threadfence_system();
 }
@@ -1040,17 +1086,20 @@ void launch_route_pack2(hipStream_t st, const rl_batch& b, const DevRule* rules,
   const size_t gw = (size_t)nb * route::NS;  // the error word follows the look-back words
   if (!hot) {
     hipLaunchKernelGGL((route::k_route_pack2<false, false>), dim3(nb), dim3(route::NT), 0, st, in, rules, n_rules, seed,
-                       origin, n_shards, stride, hot, o.send, o.perm, lb1, lb1 + gw, o.x, o.bhs, o.bstat, o.rctl, o.thr);
+                       origin, n_shards, stride, hot, o.send, o.perm, lb1, lb1 + gw, o.x, o.bhs, o.bstat, o.rctl, o.thr,
+                       o.xs, o.tr);
     return;
   }
   hipLaunchKernelGGL((route::k_route_pack2<true, false>), dim3(nb), dim3(route::NT), 0, st, in, rules, n_rules, seed,
-                     origin, n_shards, stride, hot, o.send, o.perm, lb1, lb1 + gw, o.x, o.bhs, o.bstat, o.rctl, o.thr);
+                     origin, n_shards, stride, hot, o.send, o.perm, lb1, lb1 + gw, o.x, o.bhs, o.bstat, o.rctl, o.thr,
+                     o.xs, o.tr);
   unsigned long long* hlb = reinterpret_cast<unsigned long long*>(o.rctl + 16);  // zeroed with the look-back areas
   hipLaunchKernelGGL(route::k_route_hot_scan, dim3(route::HS_CC * route::HS_RCH), dim3(route::HS_NT), 0, st, nb,
                      n_shards, origin, stride, hot, o.bhs, o.bstat, o.send, o.x, o.rctl, o.hot_pos, o.hot_tot,
-                     hlb + (size_t)route::HS_RCH * HOT_MAX, lb1 + gw, o.h_hot, hlb);
+                     hlb + (size_t)route::HS_RCH * HOT_MAX, lb1 + gw, o.h_hot, hlb, o.xs);
   hipLaunchKernelGGL((route::k_route_pack2<false, true>), dim3(nb), dim3(route::NT), 0, st, in, rules, n_rules, seed,
-                     origin, n_shards, stride, hot, o.send, o.perm, lb2, lb2 + gw, o.x, o.bhs, o.bstat, o.rctl, nullptr);
+                     origin, n_shards, stride, hot, o.send, o.perm, lb2, lb2 + gw, o.x, o.bhs, o.bstat, o.rctl, nullptr,
+                     o.xs, o.tr);
 }
 
 void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* rules, const RoutePackBufs& o,

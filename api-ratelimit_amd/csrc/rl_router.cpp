@@ -14,11 +14,21 @@
 //   origin   every descriptor's post-value from its record's reply (and, inside a combined
 //            record, its prefix of hits_addend), then its decision (k_route_unpack_raw)
 //
-// Transports: RCCL (one process per GPU, ncclAllToAll / ncclAllToAllv / ncclAllGather on a
-// stream the router owns) or local (n_shards engines in one process, device copies). Status
-// words ride in the counts exchange (pack) and the reply exchange (decide, and any local HIP
-// failure after the counts), so every shard completes every collective of a step and all of
-// them fail together.
+// Transports: collective (one rank per GPU: RCCL's ncclAllToAll / ncclAllToAllv / ncclAllGather
+// on a stream the router owns, or the same code path over an in-process emulation of those three
+// collectives for G ranks driven by G threads of one process — device copies driven by the very
+// count and displacement vectors RCCL would get, every rank's counts checked against its peers',
+// so the N > 1 exchange runs and is tested on one GPU) or local (n_shards engines in one process,
+// device copies). Status words ride in the counts exchange (pack) and the reply exchange
+// (decide, and any local HIP failure after the counts), so every shard completes every
+// collective of a step and all of them fail together.
+//
+// Time: each origin's (count, status) word pair to an owner carries its batch's
+// request-time range. An owner decides its records origin by origin in runs whose times span at
+// most one second (the engine's window rule), so origins whose clocks or batch cuts differ by
+// seconds never make a step fail; the table keeps a SECOND key string findable for a request up
+// to 3 s behind the newest time it has seen (rl_common.h slot_free_for), and a step with an
+// origin further behind the node's step clock is refused everywhere with RL_EINVAL.
 //
 // Two steps may be in flight (rl_router_submit / rl_router_wait): step k+1's pack, counts and
 // record exchange run on the origin and exchange streams while step k's owner batch is decided
@@ -28,10 +38,13 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_set>
 #include <vector>
@@ -51,7 +64,12 @@ constexpr int NSLOT = 2;                   // steps in flight
 constexpr uint64_t ROUTE_HOT_EVERY = 8;    // route hot set refresh period (steps)
 constexpr uint32_t ROUTE_HOT_KEEP = 64;    // a group stays while its origin sends it >= this sum of hits per step
 static_assert(REC == RL_ROUTE_RECORD_BYTES && RAWB == sizeof(rl_raw_reply), "record layouts");
-constexpr uint32_t HX_HOT = 8 * MAXS;      // pinned mirror: hot sums, then the control words
+// d_x / h_x words per step: [XS G] (count, status, tmin, tmax) sent to each owner | [XS G] received
+// from each origin | [G] decide statuses sent | [G] received; the pinned mirror then holds the hot
+// scan's group sums and control words at HX_HOT
+constexpr uint32_t XS = 4;
+constexpr uint32_t HX_HOT = (2 * XS + 2) * MAXS;
+constexpr uint32_t MAX_LAG_S = 3;          // a request may come this many seconds behind the step clock
 
 // Host wait for an event by polling: a blocking stream synchronize sleeps and wakes 10-20 us
 // after the GPU is done, on the routed step's critical path between exchanges.
@@ -69,7 +87,207 @@ double now_us() {
 
 // Fault injection for the tests (RL_ROUTER_FAULT="phase:shard", read at create, fires once):
 // the shard behaves as if a HIP call of that phase failed.
-enum Phase { PH_NONE = 0, PH_PACK, PH_RECORDS, PH_DECIDE, PH_REPLIES, PH_UNPACK };
+enum Phase { PH_NONE = 0, PH_PACK, PH_RECORDS, PH_DECIDE, PH_REPLIES, PH_UNPACK, PH_STATUS };
+const char* const kPhaseNames[] = {"", "pack", "records", "decide", "replies", "unpack", "status"};
+
+// ---- collective transports ----------------------------------------------------------------
+// The three collectives a routed step uses, in bytes, on the router's exchange stream.
+struct Xport {
+  virtual ~Xport() = default;
+  virtual ncclResult_t a2av(const void* s, const size_t* sc, const size_t* sd, void* r, const size_t* rc,
+                            const size_t* rd, hipStream_t st) = 0;
+  virtual ncclResult_t a2a(const void* s, void* r, size_t n, hipStream_t st) = 0;
+  virtual ncclResult_t allgather(const void* s, void* r, size_t n, hipStream_t st) = 0;
+  virtual ncclResult_t group_start() { return ncclSuccess; }
+  virtual ncclResult_t group_end() { return ncclSuccess; }
+  virtual void abort() = 0;
+  virtual std::string why(ncclResult_t r) { return ncclGetErrorString(r); }
+};
+
+struct RcclXport : Xport {
+  ncclComm_t comm = nullptr;
+  ~RcclXport() override {
+    if (comm) (void)ncclCommDestroy(comm);
+  }
+  ncclResult_t a2av(const void* s, const size_t* sc, const size_t* sd, void* r, const size_t* rc, const size_t* rd,
+                    hipStream_t st) override {
+    return ncclAllToAllv(s, sc, sd, r, rc, rd, ncclUint8, comm, st);
+  }
+  ncclResult_t a2a(const void* s, void* r, size_t n, hipStream_t st) override {
+    return ncclAllToAll(s, r, n, ncclUint8, comm, st);
+  }
+  ncclResult_t allgather(const void* s, void* r, size_t n, hipStream_t st) override {
+    return ncclAllGather(s, r, n, ncclUint8, comm, st);
+  }
+  ncclResult_t group_start() override { return ncclGroupStart(); }
+  ncclResult_t group_end() override { return ncclGroupEnd(); }
+  void abort() override {
+    if (comm) (void)ncclCommAbort(comm);
+    comm = nullptr;
+  }
+};
+
+// In-process emulation of the collectives for G ranks (one thread each, one or more devices of
+// this process): every rank posts its buffers, count and displacement vectors and an event
+// recorded on its exchange stream; after a host barrier each rank copies what its peers send it
+// (device-to-device on its own stream, behind their events), checking that each peer's send
+// count equals its own receive count (RCCL would silently corrupt: here the world aborts with
+// the mismatch); a second barrier orders every peer's copies before a rank's stream moves on
+// (its send buffer may be rewritten then), as the completion of an RCCL collective does.
+struct EmuWorld {
+  uint32_t G = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  uint32_t arrived = 0;
+  uint64_t gen = 0;
+  bool aborted = false;
+  int refs = 0;
+  std::string why;
+  struct Post {
+    const uint8_t* s;
+    uint8_t* r;
+    size_t sc[MAXS], sd[MAXS];
+    hipEvent_t ev;
+  };
+  Post post[MAXS];
+  hipEvent_t done[MAXS];
+  // all G ranks arrive, or the world aborts (a rank failed, or one never came: 120 s)
+  bool barrier() {
+    std::unique_lock<std::mutex> l(mu);
+    if (aborted) return false;
+    const uint64_t g = gen;
+    if (++arrived == G) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return true;
+    }
+    const bool ok = cv.wait_for(l, std::chrono::seconds(120), [&] { return gen != g || aborted; });
+    if (aborted) return false;
+    if (!ok) {
+      aborted = true;
+      why = "a rank did not arrive at a collective within 120 s";
+      cv.notify_all();
+      return false;
+    }
+    return true;
+  }
+  void abort(const std::string& w) {
+    std::lock_guard<std::mutex> l(mu);
+    if (!aborted && why.empty()) why = w;
+    aborted = true;
+    cv.notify_all();
+  }
+};
+constexpr uint64_t EMU_MAGIC = 0x444c524f57554d45ull;  // "EMUWORLD"
+
+struct EmuXport : Xport {
+  EmuWorld* w = nullptr;
+  uint32_t me = 0;
+  hipEvent_t ev_pre = nullptr, ev_post = nullptr;
+  ~EmuXport() override {
+    for (hipEvent_t e : {ev_pre, ev_post})
+      if (e) (void)hipEventDestroy(e);
+    if (w) {
+      bool last;
+      {
+        std::lock_guard<std::mutex> l(w->mu);
+        last = --w->refs == 0;
+      }
+      if (last) delete w;
+    }
+  }
+  ncclResult_t a2av(const void* s, const size_t* sc, const size_t* sd, void* r, const size_t* rc, const size_t* rd,
+                    hipStream_t st) override {
+    const uint32_t G = w->G;
+    if (hipEventRecord(ev_pre, st) != hipSuccess) {
+      w->abort("rank " + std::to_string(me) + ": hipEventRecord");
+      return ncclUnhandledCudaError;
+    }
+    {
+      std::lock_guard<std::mutex> l(w->mu);
+      EmuWorld::Post& p = w->post[me];
+      p.s = static_cast<const uint8_t*>(s);
+      p.r = static_cast<uint8_t*>(r);
+      for (uint32_t j = 0; j < G; ++j) p.sc[j] = sc[j], p.sd[j] = sd[j];
+      p.ev = ev_pre;
+    }
+    if (!w->barrier()) return ncclRemoteError;
+    hipError_t he = hipSuccess;
+    for (uint32_t i = 0; i < G; ++i) {
+      const EmuWorld::Post& p = w->post[i];
+      if (p.sc[me] != rc[i]) {
+        w->abort("rank " + std::to_string(me) + " expects " + std::to_string(rc[i]) + " bytes from rank " +
+                 std::to_string(i) + ", which sends " + std::to_string(p.sc[me]));
+        return ncclInvalidUsage;
+      }
+      if (he == hipSuccess) he = hipStreamWaitEvent(st, p.ev, 0);
+      if (he == hipSuccess && rc[i])
+        he = hipMemcpyAsync(static_cast<uint8_t*>(r) + rd[i], p.s + p.sd[me], rc[i], hipMemcpyDeviceToDevice, st);
+    }
+    if (he == hipSuccess) he = hipEventRecord(ev_post, st);
+    if (he != hipSuccess) {
+      w->abort("rank " + std::to_string(me) + ": " + hipGetErrorString(he));
+      return ncclUnhandledCudaError;
+    }
+    {
+      std::lock_guard<std::mutex> l(w->mu);
+      w->done[me] = ev_post;
+    }
+    if (!w->barrier()) return ncclRemoteError;
+    for (uint32_t i = 0; i < G; ++i)
+      if (hipStreamWaitEvent(st, w->done[i], 0) != hipSuccess) {
+        w->abort("rank " + std::to_string(me) + ": hipStreamWaitEvent");
+        return ncclUnhandledCudaError;
+      }
+    return ncclSuccess;
+  }
+  ncclResult_t a2a(const void* s, void* r, size_t n, hipStream_t st) override {
+    size_t c[MAXS], d[MAXS];
+    for (uint32_t j = 0; j < w->G; ++j) c[j] = n, d[j] = j * n;
+    return a2av(s, c, d, r, c, d, st);
+  }
+  ncclResult_t allgather(const void* s, void* r, size_t n, hipStream_t st) override {
+    size_t c[MAXS], z[MAXS], d[MAXS];
+    for (uint32_t j = 0; j < w->G; ++j) c[j] = n, z[j] = 0, d[j] = j * n;
+    return a2av(s, c, z, r, c, d, st);
+  }
+  void abort() override { w->abort("rank " + std::to_string(me) + " aborted the communicator"); }
+  std::string why(ncclResult_t r) override {
+    std::lock_guard<std::mutex> l(w->mu);
+    return std::string(ncclGetErrorString(r)) + (w->why.empty() ? "" : " (" + w->why + ")");
+  }
+};
+
+// One owner run: consecutive origins' records (compact by origin) whose times fit one engine batch.
+struct Run {
+  uint32_t off, n;
+};
+// Split an owner's records at origin boundaries into runs whose request times span at most one
+// second (rl_submit's window rule: a batch may straddle one window boundary of a unit). rcv[i]:
+// records from origin i; [tmin[i], tmax[i]]: its batch's times.
+void owner_runs(const uint32_t* rcv, const uint32_t* tmin, const uint32_t* tmax, uint32_t G, std::vector<Run>& runs) {
+  runs.clear();
+  uint32_t off = 0, lo = 0, hi = 0;
+  bool open = false;
+  Run cur{0, 0};
+  for (uint32_t i = 0; i < G; off += rcv[i], ++i) {
+    if (!rcv[i]) continue;
+    const uint32_t a = std::min(tmin[i], tmax[i]), b = tmax[i];
+    if (open && std::max(hi, b) - std::min(lo, a) <= 1u) {
+      cur.n += rcv[i];
+      lo = std::min(lo, a);
+      hi = std::max(hi, b);
+      continue;
+    }
+    if (open) runs.push_back(cur);
+    cur = Run{off, rcv[i]};
+    lo = a;
+    hi = b;
+    open = true;
+  }
+  if (open) runs.push_back(cur);
+}
 
 // One hot-set entry as exchanged between ranks (32 B): an owner's hot prefix.
 struct AgEntry {
@@ -97,7 +315,7 @@ struct ShardStep {
   RRec* recv = nullptr;       // owner: records from every origin
   RawReply* reply = nullptr;  // owner: one raw reply per received record
   RawReply* back = nullptr;   // origin: replies to its records, strided like send
-  int32_t* d_x = nullptr;     // [2G] pairs sent | [2G] received | [G] statuses sent | [G] received
+  int32_t* d_x = nullptr;     // step words (XS layout above)
   int32_t* h_x = nullptr;     // pinned mirror; at HX_HOT the hot sums, then the control words
   HostStage hs;
   rl_batch b{};               // the origin batch (device pointers)
@@ -105,11 +323,13 @@ struct ShardStep {
   uint32_t* thr = nullptr;
   uint32_t cnt[MAXS] = {};    // records this origin sends each owner
   uint32_t rcv[MAXS] = {};    // records this owner receives from each origin
+  uint32_t tmin[MAXS] = {}, tmax[MAXS] = {};  // each origin's request-time range
   uint32_t n_in = 0;
+  uint32_t n_sub = 0;         // owner batches (runs) handed to the engine and not yet completed
+  uint32_t n_runs = 0;        // owner batches of the step
   int rc_pack = 0, rc_dec = 0, rc_local = 0;
   std::string msg;
-  const char* phase = "";     // where msg comes from: pack, records, decide, replies, unpack
-  bool submitted = false;     // owner batch handed to the engine (rl_wait pending)
+  const char* phase = "";     // where msg comes from: pack, records, decide, replies, unpack, status
   bool combined = false;
 };
 
@@ -134,15 +354,23 @@ struct StepSlot {
   bool host = false;
   bool counts_failed = false;  // every shard left after the counts exchange
   double t0 = 0;
-  int32_t status[MAXS] = {};   // per shard (RCCL: as received from every origin / owner)
+  int32_t status[MAXS] = {};   // per shard (collective: as received from every origin / owner)
 };
+
+// A routed step's configuration words, compared across ranks at create (the owners' combining
+// and local-cache semantics must agree, rl_hip.h "Router object").
+struct CfgWord {
+  uint64_t magic, seed;
+  uint32_t local_cache, n_shards, max_desc, flags;
+};
+static_assert(sizeof(CfgWord) == 32, "config word");
 
 }  // namespace
 
 struct rl_router {
   rl_router_config cfg{};
-  bool rccl = false, broken = false;
-  ncclComm_t comm = nullptr;
+  bool coll = false, broken = false;  // coll: RCCL or emulated collectives (one rank per router)
+  std::unique_ptr<Xport> xp;
   hipStream_t rs = nullptr;  // exchanges
   hipEvent_t ev_rs = nullptr;
   hipEvent_t ev_cnt = nullptr;  // the counts' host copy
@@ -150,9 +378,10 @@ struct rl_router {
   std::vector<Shard> sh;
   StepSlot slot[NSLOT];
   uint64_t seq = 0, done = 0;
+  uint32_t tclock = 0;       // the step clock: the newest request time of every step applied so far
   double t_pack0 = 0;        // start of the current submit's packs (host clock)
   size_t in_bytes = 0, o_off = 0, o_rule = 0, o_req = 0, o_now = 0, o_hits = 0;  // host staging layout
-  AgEntry* d_ag = nullptr;   // RCCL hot-set allgather: [HOT_MAX] send | [G * HOT_MAX] receive
+  AgEntry* d_ag = nullptr;   // collective hot-set allgather: [HOT_MAX] send | [G * HOT_MAX] receive
   AgEntry* h_ag = nullptr;
   int fault_phase = PH_NONE;
   uint32_t fault_shard = 0;
@@ -168,12 +397,12 @@ struct rl_router {
     err = buf;
     return code;
   }
-  // RCCL failure: abort the communicator (its peers' collectives return), every later call fails
+  // collective failure: abort the communicator (its peers' collectives return), every later call fails
   int nccl_fail(ncclResult_t nr, const char* what) {
-    if (comm) (void)ncclCommAbort(comm);
-    comm = nullptr;
+    const std::string w = xp ? xp->why(nr) : ncclGetErrorString(nr);
+    if (xp) xp->abort();
     broken = true;
-    return fail(RL_ECOMM, "%s: %s (communicator aborted)", what, ncclGetErrorString(nr));
+    return fail(RL_ECOMM, "%s: %s (communicator aborted)", what, w.c_str());
   }
   bool fault(int phase, uint32_t s) {
     if (fault_phase != phase || fault_shard != s) return false;
@@ -181,7 +410,7 @@ struct rl_router {
     return true;
   }
   uint32_t n_local() const { return (uint32_t)sh.size(); }
-  uint32_t shard_id(uint32_t s) const { return rccl ? cfg.rank : s; }
+  uint32_t shard_id(uint32_t s) const { return coll ? cfg.rank : s; }
 
   int alloc_shard(Shard& s);
   void free_all();
@@ -190,11 +419,15 @@ struct rl_router {
   void pack(uint32_t s, uint32_t k);
   void note_combine(uint32_t s, uint32_t k);
   void refresh_hot();
+  int check_config();
+  bool step_clock(uint32_t k, const uint32_t* tmin, const uint32_t* tmax, uint32_t* late);
+  int submit_owner(uint32_t s, uint32_t k, const Run& u, void* ready);
+  void drain(Shard& S, ShardStep& x);
   int submit(const rl_batch* batches, rl_status* const* out, uint32_t* const* thr, bool host);
   int wait(rl_status* const* out, uint32_t* const* thr, bool into);
-  int submit_rccl(uint32_t k);
+  int submit_coll(uint32_t k);
   int submit_local(uint32_t k);
-  void wait_rccl(uint32_t k);
+  void wait_coll(uint32_t k);
   void wait_local(uint32_t k);
   int step_result(uint32_t k);
 };
@@ -218,13 +451,12 @@ void rl_router::free_all() {
   sh.clear();
   if (d_ag) (void)hipFree(d_ag);
   if (h_ag) (void)hipHostFree(h_ag);
-  if (comm) (void)ncclCommDestroy(comm);
+  xp.reset();
   for (hipEvent_t e : {ev_rs, ev_cnt, ev_end})
     if (e) (void)hipEventDestroy(e);
   if (rs) (void)hipStreamDestroy(rs);
   d_ag = nullptr;
   h_ag = nullptr;
-  comm = nullptr;
   ev_rs = ev_cnt = ev_end = nullptr;
   rs = nullptr;
 }
@@ -241,6 +473,9 @@ int rl_router::alloc_shard(Shard& s) {
   chk(hipHostMalloc(&s.h_hot, sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX), hipHostMallocDefault));
   if (he == hipSuccess) chk(hipEventRecord(s.ev_hot, s.os));
   const size_t lbw = route2_lb_words((uint32_t)D);
+  // words after rctl: [16] step words, the hot scan's look-back words, its u64 sums, then (on a
+  // 256-B line) the pack's 8 x 64 time-range words
+  const size_t tr_off = (16 + route2_hot_lb_words() + 2 * (size_t)HOT_MAX + 63) / 64 * 64;
   for (ShardStep& t : s.st) {
     chk(hipMalloc(&t.pb.send, D * G * REC));
     chk(hipMalloc(&t.pb.perm, D * 4 + 64));
@@ -248,18 +483,20 @@ int rl_router::alloc_shard(Shard& s) {
     chk(hipMalloc(&t.pb.bstat, (size_t)route2_blocks((uint32_t)D) * 16 + 64));
     chk(hipMalloc(&t.pb.hot_pos, (size_t)HOT_MAX * 8));  // hot_pos | hot_tot
     t.pb.hot_tot = t.pb.hot_pos + HOT_MAX;
-    // zeroed per step: two look-back areas and the control words; the hot scan's u64 sums follow
-    t.zero_bytes = (2 * lbw + 16 + route2_hot_lb_words()) * 4;
-    chk(hipMalloc(&t.zero, t.zero_bytes + (size_t)HOT_MAX * 8 + 64));
+    // zeroed per step: two look-back areas, the control words, the hot scan's words, the time words
+    t.zero_bytes = (2 * lbw + tr_off + 8 * 64) * 4;
+    chk(hipMalloc(&t.zero, t.zero_bytes + 64));
     t.pb.lb = reinterpret_cast<uint32_t*>(t.zero);
     t.pb.rctl = t.pb.lb + 2 * lbw;
+    t.pb.tr = t.pb.rctl + tr_off;
+    t.pb.xs = XS;
     t.pb.zero_words = (uint32_t)(t.zero_bytes / 4);
     if (he == hipSuccess) chk(hipMemset(t.zero, 0, t.zero_bytes));
     t.zeroed = true;
     chk(hipMalloc(&t.recv, D * G * REC));
     chk(hipMalloc(&t.reply, D * G * RAWB));
     chk(hipMalloc(&t.back, D * G * RAWB));
-    chk(hipMalloc(&t.d_x, 8 * MAXS * 4));
+    chk(hipMalloc(&t.d_x, HX_HOT * 4));
     chk(hipHostMalloc(&t.h_x, (HX_HOT + HOT_MAX + 16) * 4, hipHostMallocDefault));
     t.pb.x = reinterpret_cast<uint32_t*>(t.d_x);
     t.pb.h_hot = reinterpret_cast<uint32_t*>(t.h_x + HX_HOT);
@@ -312,19 +549,22 @@ int rl_router::stage_host(uint32_t s, uint32_t k, const rl_batch& b, rl_batch& d
   return 0;
 }
 
-// Origin pack of shard s for slot k on its origin stream: the (count, status) pairs land in
-// d_x[0, 2G) and, with combining, the groups' sums and the control words in the pinned mirror.
+// Origin pack of shard s for slot k on its origin stream: the (count, status, tmin, tmax) words
+// land in d_x[0, XS G) and, with combining, the groups' sums and the control words in the
+// pinned mirror.
 void rl_router::pack(uint32_t s, uint32_t k) {
   Shard& S = sh[s];
   ShardStep& t = S.st[k];
   const uint32_t G = cfg.n_shards;
   t.combined = false;
-  auto send_status = [&](int32_t rc) {  // pairs (0, rc) to every owner
+  auto send_status = [&](int32_t rc) {  // (0, rc, no times) to every owner
     for (uint32_t j = 0; j < G; ++j) {
-      t.h_x[2 * j] = 0;
-      t.h_x[2 * j + 1] = rc;
+      t.h_x[XS * j] = 0;
+      t.h_x[XS * j + 1] = rc;
+      t.h_x[XS * j + 2] = (int32_t)0xFFFFFFFFu;
+      t.h_x[XS * j + 3] = 0;
     }
-    (void)hipMemcpyAsync(t.d_x, t.h_x, 8 * G, hipMemcpyHostToDevice, S.os);
+    (void)hipMemcpyAsync(t.d_x, t.h_x, 4 * XS * G, hipMemcpyHostToDevice, S.os);
   };
   if (t.rc_pack || !t.b.n_desc) {
     if (!t.rc_pack && t.b.n_req && t.thr) (void)hipMemsetAsync(t.thr, 0, (size_t)t.b.n_req * 4, S.os);
@@ -368,11 +608,12 @@ void rl_router::note_combine(uint32_t s, uint32_t k) {
 
 // Route hot set refresh (every ROUTE_HOT_EVERY steps, at the same step on every shard): keep the
 // groups this origin still sends with >= ROUTE_HOT_KEEP hits per step, add the owners' hot keys
-// (each engine's own hot set: prefixes that reach it with many records per batch; over RCCL
-// gathered from every rank), up to HOT_MAX. A shard that had to repack starts over.
+// (each engine's own hot set: prefixes that reach it with many records per batch; over the
+// collective transport gathered from every rank), up to HOT_MAX. A shard that had to repack
+// starts over.
 void rl_router::refresh_hot() {
   std::vector<HotKey> cand;
-  if (rccl) {
+  if (coll) {
     std::vector<HotKey> mine;
     rlx_engine_hot(sh[0].e, mine);
     for (uint32_t i = 0; i < HOT_MAX; ++i) {
@@ -382,9 +623,9 @@ void rl_router::refresh_hot() {
     }
     const size_t n = HOT_MAX * sizeof(AgEntry);
     hipError_t he = hipMemcpyAsync(d_ag, h_ag, n, hipMemcpyHostToDevice, rs);
-    const ncclResult_t nr = ncclAllGather(d_ag, d_ag + HOT_MAX, n, ncclUint8, comm, rs);
+    const ncclResult_t nr = xp->allgather(d_ag, d_ag + HOT_MAX, n, rs);
     if (nr != ncclSuccess) {
-      nccl_fail(nr, "ncclAllGather(hot sets)");
+      nccl_fail(nr, "allgather(hot sets)");
       return;
     }
     if (he == hipSuccess) he = hipMemcpyAsync(h_ag + HOT_MAX, d_ag + HOT_MAX, n * cfg.n_shards, hipMemcpyDeviceToHost, rs);
@@ -436,28 +677,114 @@ void rl_router::refresh_hot() {
   }
 }
 
-// RCCL: counts (+ pack statuses), then records; the owner batch is handed to the engine.
-int rl_router::submit_rccl(uint32_t k) {
+// At create: every rank's configuration words (collective transports) or every engine's (local)
+// must agree — one hash seed (owners), one local-cache setting (combining is exact only when no
+// owner freezes a key inside a combined group). A mismatch fails create on every rank alike.
+int rl_router::check_config() {
+  auto word = [&](const EngineView& v) {
+    return CfgWord{0x52544346474f5752ull, v.seed, (uint32_t)v.local_cache, cfg.n_shards, cfg.max_desc,
+                   cfg.flags & (RL_ROUTER_NO_COMBINE | RL_ROUTER_HOST)};
+  };
+  std::vector<CfgWord> all;
+  if (coll) {
+    CfgWord* hw = reinterpret_cast<CfgWord*>(h_ag);
+    CfgWord* dw = reinterpret_cast<CfgWord*>(d_ag);
+    hw[0] = word(sh[0].v);
+    hipError_t he = hipMemcpyAsync(dw, hw, sizeof(CfgWord), hipMemcpyHostToDevice, rs);
+    const ncclResult_t nr = xp->allgather(dw, dw + 1, sizeof(CfgWord), rs);
+    if (nr != ncclSuccess) return nccl_fail(nr, "allgather(router configuration)");
+    if (he == hipSuccess)
+      he = hipMemcpyAsync(hw + 1, dw + 1, sizeof(CfgWord) * cfg.n_shards, hipMemcpyDeviceToHost, rs);
+    if (he == hipSuccess) he = hipStreamSynchronize(rs);
+    if (he != hipSuccess) return fail(RL_EHIP, "router configuration exchange: %s", hipGetErrorString(he));
+    all.assign(hw + 1, hw + 1 + cfg.n_shards);
+  } else {
+    for (Shard& s : sh) all.push_back(word(s.v));
+  }
+  for (uint32_t j = 1; j < all.size(); ++j)
+    if (memcmp(&all[j], &all[0], sizeof(CfgWord)) != 0)
+      return fail(RL_EINVAL, "shard %u's configuration differs from shard 0's (hash_seed, local_cache, n_shards, "
+                             "max_desc and flags must agree on every shard)", j);
+  return 0;
+}
+
+// The step clock after the counts: origin i's batch may start at most MAX_LAG_S seconds behind
+// the newest request time of everything before it in rank order (earlier steps included) — the
+// table keeps a SECOND key string findable that far back. Every rank computes the same verdict
+// from the same exchanged ranges; late[i] = 1 for an origin behind it. Commits the clock only
+// when the step goes ahead.
+bool rl_router::step_clock(uint32_t k, const uint32_t* tmin, const uint32_t* tmax, uint32_t* late) {
+  (void)k;
+  uint32_t c = tclock;
+  bool any = false;
+  for (uint32_t i = 0; i < cfg.n_shards; ++i) {
+    late[i] = 0;
+    if (tmin[i] > tmax[i]) continue;  // no routed descriptors
+    if (c > tmin[i] + MAX_LAG_S) {
+      late[i] = 1;
+      any = true;
+    }
+    c = std::max(c, tmax[i]);
+  }
+  if (!any) tclock = c;
+  return any;
+}
+
+// Complete the oldest owner batch of the engine: x's (the older step's first, FIFO).
+void rl_router::drain(Shard& S, ShardStep& x) {
+  const int rp = rl_wait(S.e);
+  if (rp && !x.rc_dec) {
+    x.rc_dec = rp;
+    x.msg = rl_last_error(S.e);
+    x.phase = "decide";
+  }
+  --x.n_sub;
+}
+
+// One owner run to the engine; an engine that cannot take another batch now (in flight at its
+// limit, or an LSD engine that cannot pipeline) completes its oldest ones first.
+int rl_router::submit_owner(uint32_t s, uint32_t k, const Run& u, void* ready) {
+  Shard& S = sh[s];
+  ShardStep& t = S.st[k];
+  ShardStep& prev = S.st[k ^ 1u];
+  for (;;) {
+    const int rc = rl_submit_routed_async(S.e, t.recv + u.off, u.n, t.reply + u.off, RL_ROUTED_RAW, ready);
+    if (rc != RL_ESTATE) {
+      if (!rc) ++t.n_sub;
+      return rc;
+    }
+    if (prev.n_sub) drain(S, prev);
+    else if (t.n_sub) drain(S, t);
+    else return rc;
+  }
+}
+
+// Collective transport: counts (+ pack statuses and time ranges), then records; the owner's runs
+// are handed to the engine.
+int rl_router::submit_coll(uint32_t k) {
   const uint32_t G = cfg.n_shards, me = cfg.rank;
   Shard& S = sh[0];
   ShardStep& t = S.st[k];
   const double t0 = t_pack0;
   hipError_t he = hipEventRecord(S.ev, S.os);
   if (he == hipSuccess) he = hipStreamWaitEvent(rs, S.ev, 0);
-  ncclResult_t nr = ncclAllToAll(t.d_x, t.d_x + 2 * G, 2, ncclInt32, comm, rs);
-  if (nr != ncclSuccess) return nccl_fail(nr, "ncclAllToAll(counts)");
-  if (he == hipSuccess) he = hipMemcpyAsync(t.h_x, t.d_x, 16 * G, hipMemcpyDeviceToHost, rs);
+  // the decide statuses this rank sends in the reply exchange start as a failure word: only a
+  // successful upload of its real status replaces it (wait_coll), so a failed upload cannot hand
+  // peers a stale status from an earlier step
+  if (he == hipSuccess) he = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(t.d_x + 2 * XS * G), RL_EHIP, G, rs);
+  ncclResult_t nr = xp->a2a(t.d_x, t.d_x + XS * G, 4 * XS, rs);
+  if (nr != ncclSuccess) return nccl_fail(nr, "all-to-all(counts)");
+  if (he == hipSuccess) he = hipMemcpyAsync(t.h_x, t.d_x, 8 * XS * G, hipMemcpyDeviceToHost, rs);
   if (he == hipSuccess) he = hipEventRecord(ev_cnt, rs);
   if (he == hipSuccess) he = poll_event(ev_cnt);
   if (he != hipSuccess) {  // the counts are unknown: nobody can take part in the record exchange
     broken = true;
-    if (comm) (void)ncclCommAbort(comm);
-    comm = nullptr;
+    if (xp) xp->abort();
     return fail(RL_ECOMM, "counts exchange: %s (communicator aborted)", hipGetErrorString(he));
   }
   const int32_t* hs = t.h_x;
-  const int32_t* hr = t.h_x + 2 * G;
-  if (!t.rc_pack && hs[1]) {  // the device refused the pack (one status in every owner's pair)
+  const int32_t* hr = t.h_x + XS * G;
+  if (!t.rc_pack && hs[1]) {  // the device refused the pack (one status in every owner's words)
     t.rc_pack = hs[1];
     t.msg = t.rc_pack == RL_EDEVICE ? "route pack: the device's look-back spin limit expired (device fault)"
                                     : "route pack: batch references an unknown rule id or request index, malformed "
@@ -467,10 +794,26 @@ int rl_router::submit_rccl(uint32_t k) {
   st.pack_us = now_us() - t0;
   bool any = false;
   for (uint32_t j = 0; j < G; ++j) {
-    t.cnt[j] = t.rc_pack ? 0u : (uint32_t)hs[2 * j];
-    t.rcv[j] = (uint32_t)hr[2 * j];
-    slot[k].status[j] = hr[2 * j + 1];
-    any |= hr[2 * j + 1] != 0;
+    t.cnt[j] = t.rc_pack ? 0u : (uint32_t)hs[XS * j];
+    t.rcv[j] = (uint32_t)hr[XS * j];
+    t.tmin[j] = (uint32_t)hr[XS * j + 2];
+    t.tmax[j] = (uint32_t)hr[XS * j + 3];
+    slot[k].status[j] = hr[XS * j + 1];
+    any |= hr[XS * j + 1] != 0;
+  }
+  if (!any) {  // every rank sees the same ranges: the same verdict everywhere
+    uint32_t late[MAXS];
+    if (step_clock(k, t.tmin, t.tmax, late)) {
+      for (uint32_t j = 0; j < G; ++j)
+        if (late[j]) slot[k].status[j] = RL_EINVAL;
+      if (late[me]) {
+        t.rc_pack = RL_EINVAL;
+        t.msg = "the batch's request times start more than 3 s behind the step clock (the newest time of the "
+                "origins before it); the table cannot keep SECOND keys that long";
+        t.phase = "pack";
+      }
+      any = true;
+    }
   }
   if (any) {  // every rank saw the same status words: all leave after this exchange
     slot[k].counts_failed = true;
@@ -479,7 +822,7 @@ int rl_router::submit_rccl(uint32_t k) {
   note_combine(0, k);
   // records: to owner j this origin's section j (stride D); from origin j its count, compact
   const size_t D = cfg.max_desc;
-  std::vector<size_t> sc(G), sd(G), rc(G), rd(G);
+  size_t sc[MAXS], sd[MAXS], rc[MAXS], rd[MAXS];
   uint64_t ro = 0;
   for (uint32_t j = 0; j < G; ++j) {
     sc[j] = (size_t)t.cnt[j] * REC;
@@ -491,8 +834,8 @@ int rl_router::submit_rccl(uint32_t k) {
   }
   t.n_in = (uint32_t)(ro / REC);
   for (uint32_t j = 0; j < G; ++j) st.recv[j] = j == me ? t.n_in : 0;
-  nr = ncclAllToAllv(t.pb.send, sc.data(), sd.data(), t.recv, rc.data(), rd.data(), ncclUint8, comm, rs);
-  if (nr != ncclSuccess) return nccl_fail(nr, "ncclAllToAllv(records)");
+  nr = xp->a2av(t.pb.send, sc, sd, t.recv, rc, rd, rs);
+  if (nr != ncclSuccess) return nccl_fail(nr, "all-to-all-v(records)");
   const double t1 = now_us();
   he = hipEventRecord(ev_rs, rs);
   if (fault(PH_RECORDS, 0)) he = hipErrorUnknown;
@@ -501,24 +844,20 @@ int rl_router::submit_rccl(uint32_t k) {
     t.msg = std::string("record exchange: ") + (he == hipErrorUnknown ? "injected fault (records)" : hipGetErrorString(he));
     t.phase = "records";
   } else if (t.n_in) {
-    ShardStep& prev = S.st[k ^ 1u];
-    t.rc_dec = rl_submit_routed_async(S.e, t.recv, t.n_in, t.reply, RL_ROUTED_RAW, ev_rs);
-    if (t.rc_dec == RL_ESTATE && prev.submitted) {
-      // an engine that cannot pipeline (LSD only): finish the previous owner batch first
-      const int rp = rl_wait(S.e);
-      if (rp) {
-        prev.rc_dec = rp;
-        prev.msg = rl_last_error(S.e);
-        prev.phase = "decide";
+    std::vector<Run> runs;
+    owner_runs(t.rcv, t.tmin, t.tmax, G, runs);
+    t.n_runs = (uint32_t)runs.size();
+    for (const Run& u : runs) {
+      const int rc2 = submit_owner(0, k, u, ev_rs);
+      if (rc2) {
+        if (!t.rc_dec) {
+          t.rc_dec = rc2;
+          t.msg = rl_last_error(S.e);
+          t.phase = "decide";
+        }
+        break;  // (runs after a refused one are not applied, like the rest of a refused batch)
       }
-      prev.submitted = false;
-      t.rc_dec = rl_submit_routed_async(S.e, t.recv, t.n_in, t.reply, RL_ROUTED_RAW, ev_rs);
     }
-    if (t.rc_dec) {
-      t.msg = rl_last_error(S.e);
-      t.phase = "decide";
-    }
-    t.submitted = t.rc_dec == 0;
   }
   st.exchange_us = now_us() - t1;
   return 0;
@@ -530,9 +869,10 @@ int rl_router::submit_rccl(uint32_t k) {
 int rl_router::submit_local(uint32_t k) {
   const uint32_t G = cfg.n_shards;
   const double t0 = t_pack0;
+  uint32_t tmin[MAXS], tmax[MAXS];
   for (uint32_t s = 0; s < G; ++s) {
     ShardStep& t = sh[s].st[k];
-    hipError_t he = hipMemcpyAsync(t.h_x, t.d_x, 8 * G, hipMemcpyDeviceToHost, sh[s].os);
+    hipError_t he = hipMemcpyAsync(t.h_x, t.d_x, 4 * XS * G, hipMemcpyDeviceToHost, sh[s].os);
     if (he == hipSuccess) he = hipStreamSynchronize(sh[s].os);
     if (he != hipSuccess && !t.rc_pack) {
       t.rc_pack = RL_EHIP;
@@ -547,17 +887,33 @@ int rl_router::submit_local(uint32_t k) {
       t.phase = "pack";
     }
     slot[k].status[s] = t.rc_pack;
+    tmin[s] = t.rc_pack ? 0xFFFFFFFFu : (uint32_t)t.h_x[2];
+    tmax[s] = t.rc_pack ? 0u : (uint32_t)t.h_x[3];
   }
   st.pack_us = now_us() - t0;
   bool any = false;
   for (uint32_t s = 0; s < G; ++s) any |= sh[s].st[k].rc_pack != 0;
+  if (!any) {
+    uint32_t late[MAXS];
+    if (step_clock(k, tmin, tmax, late)) {
+      for (uint32_t s = 0; s < G; ++s)
+        if (late[s]) {
+          ShardStep& t = sh[s].st[k];
+          t.rc_pack = slot[k].status[s] = RL_EINVAL;
+          t.msg = "the batch's request times start more than 3 s behind the step clock (the newest time of the "
+                  "origins before it); the table cannot keep SECOND keys that long";
+          t.phase = "pack";
+        }
+      any = true;
+    }
+  }
   if (any) {
     slot[k].counts_failed = true;
     return 0;
   }
   for (uint32_t s = 0; s < G; ++s) {
     ShardStep& t = sh[s].st[k];
-    for (uint32_t j = 0; j < G; ++j) t.cnt[j] = (uint32_t)t.h_x[2 * j];
+    for (uint32_t j = 0; j < G; ++j) t.cnt[j] = (uint32_t)t.h_x[XS * j];
     note_combine(s, k);
   }
   for (uint32_t j = 0; j < G; ++j) st.sent[j] = sh[0].st[k].cnt[j];
@@ -567,10 +923,12 @@ int rl_router::submit_local(uint32_t k) {
     uint64_t o = 0;
     for (uint32_t i = 0; i < G; ++i) {
       const uint32_t c = sh[i].st[k].cnt[j];
-      sh[j].st[k].rcv[i] = c;
+      ShardStep& tj = sh[j].st[k];
+      tj.rcv[i] = c;
+      tj.tmin[i] = tmin[i];
+      tj.tmax[i] = tmax[i];
       if (c && he == hipSuccess)
-        he = hipMemcpyAsync(sh[j].st[k].recv + o, sh[i].st[k].pb.send + j * D, (size_t)c * REC,
-                            hipMemcpyDeviceToDevice, rs);
+        he = hipMemcpyAsync(tj.recv + o, sh[i].st[k].pb.send + j * D, (size_t)c * REC, hipMemcpyDeviceToDevice, rs);
       o += c;
     }
     sh[j].st[k].n_in = (uint32_t)o;
@@ -580,6 +938,7 @@ int rl_router::submit_local(uint32_t k) {
   const double t1 = now_us();
   st.exchange_us = t1 - t0 - st.pack_us;
   st.decide_max_us = 0;
+  std::vector<Run> runs;
   for (uint32_t j = 0; j < G; ++j) {
     ShardStep& t = sh[j].st[k];
     if (he != hipSuccess || fault(PH_RECORDS, j)) {
@@ -590,11 +949,17 @@ int rl_router::submit_local(uint32_t k) {
     }
     const double a = now_us();
     if (t.n_in) {
-      t.rc_dec = rl_submit_routed_async(sh[j].e, t.recv, t.n_in, t.reply, RL_ROUTED_RAW, nullptr);
-      if (!t.rc_dec) t.rc_dec = rl_wait(sh[j].e);
-      if (t.rc_dec) {
-        t.msg = rl_last_error(sh[j].e);
-        t.phase = "decide";
+      owner_runs(t.rcv, t.tmin, t.tmax, G, runs);
+      t.n_runs = (uint32_t)runs.size();
+      for (const Run& u : runs) {
+        int rc = rl_submit_routed_async(sh[j].e, t.recv + u.off, u.n, t.reply + u.off, RL_ROUTED_RAW, nullptr);
+        if (!rc) rc = rl_wait(sh[j].e);
+        if (rc) {
+          t.rc_dec = rc;
+          t.msg = rl_last_error(sh[j].e);
+          t.phase = "decide";
+          break;
+        }
       }
     }
     st.decide_max_us = std::max(st.decide_max_us, now_us() - a);
@@ -609,7 +974,7 @@ int rl_router::submit(const rl_batch* batches, rl_status* const* out, uint32_t* 
   if (slot[k].busy) return fail(RL_ESTATE, "two routed steps in flight: call rl_router_wait");
   if (host && !(cfg.flags & RL_ROUTER_HOST)) return fail(RL_EINVAL, "router created without RL_ROUTER_HOST");
   const uint32_t G = cfg.n_shards, nl = n_local();
-  if (!rccl)  // the local transport refuses a bad batch before anything moves (RCCL: in the counts exchange)
+  if (!coll)  // the local transport refuses a bad batch before anything moves (collective: in the counts exchange)
     for (uint32_t s = 0; s < G; ++s)
       if (batches[s].n_desc > cfg.max_desc)
         return fail(RL_ECAPACITY, "shard %u: batch of %u descriptors exceeds the router's max_desc %u", s,
@@ -629,7 +994,7 @@ int rl_router::submit(const rl_batch* batches, rl_status* const* out, uint32_t* 
     t.rc_pack = t.rc_dec = t.rc_local = 0;
     t.msg.clear();
     t.phase = "";
-    t.submitted = false;
+    t.n_sub = t.n_runs = 0;
     t.n_in = 0;
     t.rc_pack = validate(batches[s]);
     if (t.rc_pack) {
@@ -662,11 +1027,11 @@ int rl_router::submit(const rl_batch* batches, rl_status* const* out, uint32_t* 
     pack(s, k);
     // local transport (logical shards on one device): one origin's pack at a time, so
     // pack_us / G is one origin's pack (as on G GPUs)
-    if (!rccl) (void)hipStreamSynchronize(S.os);
+    if (!coll) (void)hipStreamSynchronize(S.os);
   }
   slot[k].busy = true;
   ++seq;
-  return rccl ? submit_rccl(k) : submit_local(k);
+  return coll ? submit_coll(k) : submit_local(k);
 }
 
 // The step's outcome from each shard's status: the first failing shard's code on that shard
@@ -681,30 +1046,22 @@ int rl_router::step_result(uint32_t k) {
   const int code = st.status[bad];
   for (uint32_t j = 0; j < G; ++j)
     if (st.status[j] == 0) st.status[j] = RL_EPEER;
-  if (rccl && (uint32_t)bad != cfg.rank) {
+  if (coll && (uint32_t)bad != cfg.rank) {
     const int32_t own = st.status[cfg.rank];
     const ShardStep& t = sh[0].st[k];
     if (own != RL_EPEER) return fail(own, "shard %u (%s): %s", cfg.rank, t.phase, t.msg.c_str());
     return fail(RL_EPEER, "shard %d failed this step with %d (see rl_router_stats.status)", bad, code);
   }
-  const ShardStep& t = sh[rccl ? 0 : bad].st[k];
+  const ShardStep& t = sh[coll ? 0 : bad].st[k];
   return fail(code, "shard %d (%s): %s", bad, t.phase, t.msg.c_str());
 }
 
-void rl_router::wait_rccl(uint32_t k) {
+void rl_router::wait_coll(uint32_t k) {
   const uint32_t G = cfg.n_shards;
   Shard& S = sh[0];
   ShardStep& t = S.st[k];
   const double t0 = now_us();
-  if (t.submitted) {
-    const int rc = rl_wait(S.e);
-    if (rc) {
-      t.rc_dec = rc;
-      t.msg = rl_last_error(S.e);
-      t.phase = "decide";
-    }
-    t.submitted = false;
-  }
+  while (t.n_sub) drain(S, t);
   if (!t.rc_dec && !t.rc_local && fault(PH_DECIDE, 0)) {
     t.rc_dec = RL_EHIP;
     t.msg = "injected fault (decide)";
@@ -712,7 +1069,7 @@ void rl_router::wait_rccl(uint32_t k) {
   }
   st.decide_us = st.decide_max_us = now_us() - t0;
   const double t1 = now_us();
-  int32_t* hs = t.h_x + 4 * G;  // statuses sent | received
+  int32_t* hs = t.h_x + 2 * XS * G;  // statuses sent | received
   int32_t mine = t.rc_dec ? t.rc_dec : t.rc_local;
   if (!mine && fault(PH_REPLIES, 0)) {
     mine = t.rc_local = RL_EHIP;
@@ -720,10 +1077,20 @@ void rl_router::wait_rccl(uint32_t k) {
     t.phase = "replies";
   }
   for (uint32_t j = 0; j < G; ++j) hs[j] = mine;
-  hipError_t he = hipMemcpyAsync(t.d_x + 4 * G, hs, 4 * G, hipMemcpyHostToDevice, rs);
+  // this rank's status words: a failed upload leaves the failure word submit_coll put there
+  hipError_t hu = fault(PH_STATUS, 0) ? hipErrorUnknown
+                                      : hipMemcpyAsync(t.d_x + 2 * XS * G, hs, 4 * G, hipMemcpyHostToDevice, rs);
+  if (hu != hipSuccess) {
+    if (!t.rc_dec && !t.rc_local) {
+      t.rc_local = RL_EHIP;
+      t.msg = std::string("decide status upload: ") +
+              (hu == hipErrorUnknown ? "injected fault (status)" : hipGetErrorString(hu));
+      t.phase = "status";
+    }
+  }
   // replies: to origin j the replies to its records (compact), into its back buffer at my section
   const size_t D = cfg.max_desc;
-  std::vector<size_t> sc(G), sd(G), rc(G), rd(G);
+  size_t sc[MAXS], sd[MAXS], rc[MAXS], rd[MAXS];
   uint64_t so = 0;
   for (uint32_t j = 0; j < G; ++j) {
     sc[j] = (size_t)t.rcv[j] * RAWB;
@@ -732,22 +1099,21 @@ void rl_router::wait_rccl(uint32_t k) {
     rc[j] = (size_t)t.cnt[j] * RAWB;
     rd[j] = j * D * RAWB;  // perm = owner * D + position
   }
-  ncclResult_t nr = ncclGroupStart();
-  if (nr == ncclSuccess) nr = ncclAllToAll(t.d_x + 4 * G, t.d_x + 5 * G, 1, ncclInt32, comm, rs);
-  if (nr == ncclSuccess)
-    nr = ncclAllToAllv(t.reply, sc.data(), sd.data(), t.back, rc.data(), rd.data(), ncclUint8, comm, rs);
-  const ncclResult_t ne = ncclGroupEnd();
+  ncclResult_t nr = xp->group_start();
+  if (nr == ncclSuccess) nr = xp->a2a(t.d_x + 2 * XS * G, t.d_x + 2 * XS * G + G, 4, rs);
+  if (nr == ncclSuccess) nr = xp->a2av(t.reply, sc, sd, t.back, rc, rd, rs);
+  const ncclResult_t ne = xp->group_end();
   if (nr != ncclSuccess || ne != ncclSuccess) {
-    nccl_fail(nr != ncclSuccess ? nr : ne, "ncclAllToAll(replies)");
+    nccl_fail(nr != ncclSuccess ? nr : ne, "all-to-all(replies)");
     return;
   }
-  if (he == hipSuccess) he = hipMemcpyAsync(t.h_x + 5 * G, t.d_x + 5 * G, 4 * G, hipMemcpyDeviceToHost, rs);
+  hipError_t he = hipMemcpyAsync(t.h_x + 2 * XS * G + G, t.d_x + 2 * XS * G + G, 4 * G, hipMemcpyDeviceToHost, rs);
   if (he == hipSuccess) he = hipEventRecord(ev_rs, rs);
   if (he == hipSuccess) he = hipStreamWaitEvent(S.os, ev_rs, 0);
   st.reply_us = now_us() - t1;
   const double t2 = now_us();
-  if (he == hipSuccess) {  // (the owners' statuses arrived with the replies, d_x[5G, 6G); thr zeroed by the pack)
-    launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 5 * G, cfg.max_desc, t.out, t.thr);
+  if (he == hipSuccess) {  // (the owners' statuses arrived with the replies; thr zeroed by the pack)
+    launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 2 * XS * G + G, cfg.max_desc, t.out, t.thr);
     he = hipGetLastError();
     t.zeroed = he == hipSuccess && t.b.n_desc;
   }
@@ -769,7 +1135,7 @@ void rl_router::wait_rccl(uint32_t k) {
   }
   if (he == hipSuccess && fault(PH_UNPACK, 0)) he = hipErrorUnknown;
   st.unpack_us = now_us() - t2;
-  for (uint32_t j = 0; j < G; ++j) slot[k].status[j] = h2 == hipSuccess ? t.h_x[5 * G + j] : RL_EHIP;
+  for (uint32_t j = 0; j < G; ++j) slot[k].status[j] = h2 == hipSuccess ? t.h_x[2 * XS * G + G + j] : RL_EHIP;
   if (he != hipSuccess) {  // after the last collective: only this shard's results are lost
     slot[k].status[cfg.rank] = RL_EHIP;
     t.msg = std::string("reply exchange / unpack: ") +
@@ -789,7 +1155,7 @@ void rl_router::wait_local(uint32_t k) {
       t.msg = "injected fault (decide)";
       t.phase = "decide";
     }
-    if (!t.rc_dec && !t.rc_local && fault(PH_REPLIES, j)) {
+    if (!t.rc_dec && !t.rc_local && (fault(PH_REPLIES, j) || fault(PH_STATUS, j))) {
       t.rc_local = RL_EHIP;
       t.msg = "injected fault (replies)";
       t.phase = "replies";
@@ -814,12 +1180,13 @@ void rl_router::wait_local(uint32_t k) {
     Shard& S = sh[i];
     ShardStep& t = S.st[k];
     hipError_t hu = he;
-    // every owner's decide status into this origin's device words (as the RCCL reply exchange
-    // delivers them)
-    for (uint32_t j = 0; j < G; ++j) t.h_x[5 * G + j] = slot[k].status[j];
-    if (hu == hipSuccess) hu = hipMemcpyAsync(t.d_x + 5 * G, t.h_x + 5 * G, 4 * G, hipMemcpyHostToDevice, S.os);
+    // every owner's decide status into this origin's device words (as the collective reply
+    // exchange delivers them)
+    int32_t* srecv = t.h_x + 2 * XS * G + G;
+    for (uint32_t j = 0; j < G; ++j) srecv[j] = slot[k].status[j];
+    if (hu == hipSuccess) hu = hipMemcpyAsync(t.d_x + 2 * XS * G + G, srecv, 4 * G, hipMemcpyHostToDevice, S.os);
     if (hu == hipSuccess) {  // (thr zeroed by the pack)
-      launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 5 * G, cfg.max_desc, t.out, t.thr);
+      launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 2 * XS * G + G, cfg.max_desc, t.out, t.thr);
       hu = hipGetLastError();
       t.zeroed = hu == hipSuccess && t.b.n_desc;
     }
@@ -846,7 +1213,7 @@ int rl_router::wait(rl_status* const* out, uint32_t* const* thr, bool into) {
   const uint32_t k = (uint32_t)(done % NSLOT);
   if (!slot[k].busy) return fail(RL_ESTATE, "rl_router_wait without a routed step in flight");
   if (!slot[k].counts_failed) {
-    if (rccl) wait_rccl(k);
+    if (coll) wait_coll(k);
     else wait_local(k);
   }
   slot[k].busy = false;
@@ -856,6 +1223,8 @@ int rl_router::wait(rl_status* const* out, uint32_t* const* thr, bool into) {
   const ShardStep& t0s = sh[0].st[k];
   st.hot_groups = (uint32_t)sh[0].hot.size();
   st.combined = 0;
+  st.owner_batches = t0s.n_runs;
+  st.step_clock = tclock;
   if (t0s.combined)
     for (uint32_t i = 0; i < HOT_MAX; ++i) st.combined += t0s.h_x[HX_HOT + i] != 0 ? 1u : 0u;
   if (into && !rc && slot[k].host)
@@ -879,23 +1248,49 @@ int rl_router_unique_id(uint8_t* id_out) {
   return 0;
 }
 
+int rl_router_emu_world(uint32_t n_ranks, uint8_t* id_out) {
+  if (!id_out || n_ranks == 0 || n_ranks > MAXS) return RL_EINVAL;
+  EmuWorld* w = new EmuWorld();
+  w->G = n_ranks;
+  w->refs = (int)n_ranks;
+  memset(id_out, 0, RL_ROUTER_ID_BYTES);
+  const uint64_t words[3] = {EMU_MAGIC, (uint64_t)(uintptr_t)w, n_ranks};
+  memcpy(id_out, words, sizeof words);
+  return 0;
+}
+
 int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_router** out) {
   if (!cfg || !engines || !out) return RL_EINVAL;
   *out = nullptr;
   if (cfg->struct_size != sizeof(rl_router_config)) return RL_EINVAL;
   const uint32_t G = cfg->n_shards;
   if (G == 0 || G > MAXS || cfg->max_desc == 0 || cfg->max_desc > (1u << 27)) return RL_EINVAL;
-  if (cfg->flags & ~(uint32_t)(RL_ROUTER_NO_COMBINE | RL_ROUTER_HOST)) return RL_EINVAL;
-  const bool rccl = cfg->rccl_id != nullptr;
-  if (rccl && cfg->rank >= G) return RL_EINVAL;
-  const uint32_t n_eng = rccl ? 1u : G;
+  if (cfg->flags & ~(uint32_t)(RL_ROUTER_NO_COMBINE | RL_ROUTER_HOST | RL_ROUTER_EMULATED)) return RL_EINVAL;
+  const bool emu = (cfg->flags & RL_ROUTER_EMULATED) != 0;
+  const bool coll = cfg->rccl_id != nullptr;
+  if (emu && !coll) return RL_EINVAL;
+  if (coll && cfg->rank >= G) return RL_EINVAL;
+  EmuWorld* world = nullptr;
+  if (emu) {
+    uint64_t words[3];
+    memcpy(words, cfg->rccl_id, sizeof words);
+    world = reinterpret_cast<EmuWorld*>((uintptr_t)words[1]);
+    if (words[0] != EMU_MAGIC || !world || words[2] != G) return RL_EINVAL;
+  }
+  const uint32_t n_eng = coll ? 1u : G;
   for (uint32_t s = 0; s < n_eng; ++s)
     if (!engines[s]) return RL_EINVAL;
   rl_router* r = new rl_router();
   r->cfg = *cfg;
   r->cfg.rccl_id = nullptr;
-  r->rccl = rccl;
+  r->coll = coll;
   r->st.n_shards = G;
+  if (emu) {  // attached now: the world lives until every rank's router is destroyed
+    auto* ex = new EmuXport();
+    ex->w = world;
+    ex->me = cfg->rank;
+    r->xp.reset(ex);
+  }
   {
     const size_t N = cfg->max_desc, B = cfg->max_blob_bytes ? cfg->max_blob_bytes : (size_t)cfg->max_desc * 64;
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
@@ -907,17 +1302,17 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
     r->in_bytes = r->o_hits + al(N * 4);
   }
   if (const char* f = getenv("RL_ROUTER_FAULT")) {  // tests: "phase:shard"
-    static const char* const names[] = {"", "pack", "records", "decide", "replies", "unpack"};
     char ph[32] = {0};
     unsigned s = 0;
     if (sscanf(f, "%31[a-z]:%u", ph, &s) == 2)
-      for (int p = 1; p <= PH_UNPACK; ++p)
-        if (!strcmp(ph, names[p])) {
+      for (int p = 1; p <= PH_STATUS; ++p)
+        if (!strcmp(ph, kPhaseNames[p])) {
           r->fault_phase = p;
-          r->fault_shard = rccl ? (s == cfg->rank ? 0u : 0xFFFFFFFFu) : s;
+          r->fault_shard = coll ? (s == cfg->rank ? 0u : 0xFFFFFFFFu) : s;
         }
   }
   auto bail = [&](int code) {
+    if (emu && r->xp) r->xp->abort();  // peers blocked in create's exchange return
     r->free_all();
     delete r;
     return code;
@@ -927,23 +1322,34 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
       hipEventCreateWithFlags(&r->ev_cnt, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&r->ev_end, hipEventDisableTiming) != hipSuccess)
     return bail(RL_EHIP);
+  if (emu) {
+    auto* ex = static_cast<EmuXport*>(r->xp.get());
+    if (hipEventCreateWithFlags(&ex->ev_pre, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ex->ev_post, hipEventDisableTiming) != hipSuccess)
+      return bail(RL_EHIP);
+  }
   r->sh.resize(n_eng);
   for (uint32_t s = 0; s < n_eng; ++s) {
     r->sh[s].e = engines[s];
     if (rlx_engine_view(engines[s], &r->sh[s].v)) return bail(RL_EINVAL);
     if (r->alloc_shard(r->sh[s])) return bail(RL_EHIP);
   }
-  if (rccl) {
+  if (coll) {
     if (hipMalloc(&r->d_ag, sizeof(AgEntry) * HOT_MAX * (G + 1)) != hipSuccess ||
         hipHostMalloc(&r->h_ag, sizeof(AgEntry) * HOT_MAX * (G + 1), hipHostMallocDefault) != hipSuccess)
       return bail(RL_EHIP);
-    ncclUniqueId id;
-    memcpy(&id, cfg->rccl_id, RL_ROUTER_ID_BYTES);
-    if (ncclCommInitRank(&r->comm, (int)G, id, (int)cfg->rank) != ncclSuccess) {
-      r->comm = nullptr;
-      return bail(RL_ECOMM);
+    if (!emu) {
+      auto* rx = new RcclXport();
+      r->xp.reset(rx);
+      ncclUniqueId id;
+      memcpy(&id, cfg->rccl_id, RL_ROUTER_ID_BYTES);
+      if (ncclCommInitRank(&rx->comm, (int)G, id, (int)cfg->rank) != ncclSuccess) {
+        rx->comm = nullptr;
+        return bail(RL_ECOMM);
+      }
     }
   }
+  if (int rc = r->check_config()) return bail(rc);
   *out = r;
   return 0;
 }
@@ -1006,7 +1412,11 @@ void rl_router_destroy(rl_router* r) {
   if (!r) return;
   // steps still in flight: complete them (every rank issued their collectives)
   while (!r->broken && r->done < r->seq) (void)r->wait(nullptr, nullptr, false);
-  for (Shard& s : r->sh) (void)hipStreamSynchronize(s.os);
+  for (Shard& s : r->sh) {
+    while (s.st[0].n_sub) r->drain(s, s.st[0]);
+    while (s.st[1].n_sub) r->drain(s, s.st[1]);
+    (void)hipStreamSynchronize(s.os);
+  }
   if (r->rs) (void)hipStreamSynchronize(r->rs);
   r->free_all();
   delete r;

@@ -40,7 +40,7 @@ STATUS_DTYPE = np.dtype([("code_flags", "<u4"), ("limit_remaining", "<u4"), ("re
 
 
 PIPELINE_FLAGS = {"v4": 0, "lsd": 1}  # rl_config.flags (RL_CFG_LSD_ONLY)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class RlConfig(C.Structure):
@@ -98,7 +98,7 @@ class RlRouterConfig(C.Structure):
                 ("rccl_id", C.c_void_p), ("flags", C.c_uint32), ("max_blob_bytes", C.c_uint32)]
 
 
-ROUTER_NO_COMBINE, ROUTER_HOST = 1, 2  # rl_router_config.flags
+ROUTER_NO_COMBINE, ROUTER_HOST, ROUTER_EMULATED = 1, 2, 4  # rl_router_config.flags
 
 
 class RlRouterStats(C.Structure):
@@ -106,7 +106,8 @@ class RlRouterStats(C.Structure):
                 ("sent", C.c_uint32 * 16), ("pack_us", C.c_double), ("exchange_us", C.c_double),
                 ("decide_us", C.c_double), ("decide_max_us", C.c_double), ("reply_us", C.c_double),
                 ("unpack_us", C.c_double), ("step_us", C.c_double), ("hot_groups", C.c_uint32), ("combined", C.c_uint32),
-                ("repacks", C.c_uint64), ("combined_steps", C.c_uint64)]
+                ("repacks", C.c_uint64), ("combined_steps", C.c_uint64), ("owner_batches", C.c_uint32),
+                ("step_clock", C.c_uint32)]
 
 
 ROUTER_ID_BYTES = 128
@@ -120,6 +121,7 @@ ABI = [
     ("rl_host_acquire", [C.c_void_p, C.POINTER(RlHostBatch)], C.c_int),
     ("rl_submit", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
     ("rl_wait", [C.c_void_p], C.c_int),
+    ("rl_query", [C.c_void_p], C.c_int),
     ("rl_wait_into", [C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     ("rl_wait_view", [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
     ("rl_submit_device", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
@@ -147,6 +149,7 @@ ABI = [
     ("rl_resolve", [C.c_void_p, C.POINTER(RlResolveBatch), C.c_void_p], C.c_int),
     ("rl_resolve_device", [C.c_void_p, C.POINTER(RlResolveBatch), C.c_void_p], C.c_int),
     ("rl_router_unique_id", [C.c_void_p], C.c_int),
+    ("rl_router_emu_world", [C.c_uint32, C.c_void_p], C.c_int),
     ("rl_router_create", [C.POINTER(RlRouterConfig), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
     ("rl_router_step", [C.c_void_p, C.POINTER(RlBatch), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
     ("rl_router_submit", [C.c_void_p, C.POINTER(RlBatch), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
@@ -422,6 +425,13 @@ class Engine:
     def wait(self):
         self._check(self.lib.rl_wait(self.h), "rl_wait")
 
+    def query(self) -> bool:
+        """rl_query: True when the oldest batch in flight is done on the device."""
+        rc = self.lib.rl_query(self.h)
+        if rc < 0:
+            self._check(rc, "rl_query")
+        return rc == 1
+
     def load_tree(self, nodes: np.ndarray, names: bytes):
         """nodes: uint32 [n, 4] (parent, name_off, name_len, rule); names: the tree's map keys."""
         nodes = np.ascontiguousarray(nodes, dtype=np.uint32).reshape(-1, 4)
@@ -518,7 +528,9 @@ class Router:
 
     def __init__(self, engines, max_desc: int, n_shards: Optional[int] = None, rank: int = 0,
                  rccl_id: Optional[bytes] = None, combine: bool = True, host: bool = False,
-                 max_blob_bytes: int = 0):
+                 max_blob_bytes: int = 0, emulated: bool = False):
+        """emulated: rccl_id is an emu_world() id — the collective transport with in-process
+        collectives (one Router per rank, each driven by its own thread)."""
         self.lib = engines[0].lib
         self.engines = list(engines)
         cfg = RlRouterConfig()
@@ -526,7 +538,8 @@ class Router:
         cfg.n_shards = n_shards if n_shards is not None else len(engines)
         cfg.rank = rank
         cfg.max_desc = max_desc
-        cfg.flags = (0 if combine else ROUTER_NO_COMBINE) | (ROUTER_HOST if host else 0)
+        cfg.flags = ((0 if combine else ROUTER_NO_COMBINE) | (ROUTER_HOST if host else 0)
+                     | (ROUTER_EMULATED if emulated else 0))
         cfg.max_blob_bytes = max_blob_bytes
         self._id = None
         if rccl_id is not None:
@@ -536,7 +549,7 @@ class Router:
         self.h = C.c_void_p()
         rc = self.lib.rl_router_create(C.byref(cfg), arr, C.byref(self.h))
         if rc:
-            raise RedisError(f"rl_router_create failed: {RL_ERRORS.get(rc, rc)}")
+            raise RedisError(f"rl_router_create failed: {RL_ERRORS.get(rc, rc)}", rc)
         self.n = len(engines)
         self._keep = []  # ctypes arrays of steps in flight
 
@@ -547,6 +560,16 @@ class Router:
         rc = lib.rl_router_unique_id(buf)
         if rc:
             raise RedisError(f"rl_router_unique_id: {RL_ERRORS.get(rc, rc)}")
+        return buf.raw
+
+    @staticmethod
+    def emu_world(n_ranks: int, lib=None) -> bytes:
+        """rl_router_emu_world: the id of an in-process world of n_ranks emulated ranks."""
+        lib = lib or load_library()
+        buf = C.create_string_buffer(ROUTER_ID_BYTES)
+        rc = lib.rl_router_emu_world(n_ranks, buf)
+        if rc:
+            raise RedisError(f"rl_router_emu_world: {RL_ERRORS.get(rc, rc)}", rc)
         return buf.raw
 
     def _check(self, rc, what):

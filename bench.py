@@ -651,6 +651,17 @@ def main():
     U = float(np.mean(uniq))
     nbytes = int(dbs[-1].off[-1].item())
     alg_bytes = nbytes + 12 * d + 12 * d + 20 * d + 4 * d + 64 * int(U)  # workload.algorithmic_bytes, r = d
+    alg_def = ("achieved = algorithmic bytes of one batch (SURVEY §8d: prefixes + 12 B/desc + 16 B/req + 20 B/desc out "
+               "+ 64 B per unique key) / the dominant kernel's average launch time (HIP events on the engine stream, "
+               "kernels unoverlapped)")
+    if routed and rstats is not None:
+        # an owner's launch decides the records it received, not a whole batch: price it at those
+        # (32-B record in, 8-B raw reply out per record, 64 B per unique key of the owner batch)
+        n_rec = int(rstats["recv"][rank]) or d
+        alg_bytes = 40 * n_rec + 64 * int(U)
+        alg_def = ("routed: achieved = the owner batch's algorithmic bytes (its received records: 32-B record in + 8-B "
+                   "raw reply out each, + 64 B per unique key of the owner batch) / the dominant kernel's average "
+                   "launch time on that batch (HIP events, unoverlapped); not a whole-batch figure")
     roofline = None
     if kernel:
         per_batch_ms = {k: v["total_ms"] / args.steps for k, v in kernel.items()}
@@ -661,7 +672,8 @@ def main():
         # figure x the descriptors one launch processes): every kernel of a batch handles all of
         # its descriptors, so each launch is held to the whole batch's bytes.
         achieved = alg_bytes / (dom_us * 1e-6) / 1e9
-        traffic, tsrc, traffic_batch = pmc_traffic(dom)
+        # (the PMC summary profiles the unrouted step: no counter figure for an owner batch)
+        traffic, tsrc, traffic_batch = pmc_traffic(dom) if not routed else (None, None, None)
         roofline = {
             "bound": "hbm", "kernel": dom,
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -673,9 +685,7 @@ def main():
             "pipeline_us_per_batch": round(pipe_ms * 1e3, 2),
             "pipeline_achieved_GBps": round(alg_bytes / (pipe_ms * 1e-3) / 1e9, 1),
             "kernels_us_per_batch": {k: round(v * 1e3, 2) for k, v in per_batch_ms.items()},
-            "definition": "achieved = algorithmic bytes of one batch (SURVEY §8d: prefixes + 12 B/desc + 16 B/req "
-                          "+ 20 B/desc out + 64 B per unique key) / the dominant kernel's average launch time "
-                          "(HIP events on the engine stream, kernels unoverlapped)",
+            "definition": alg_def,
         }
         if not args.no_roofline_probe:
             ra = random_access_roofline(eng, alg_bytes, int(U), pipe_ms, step_ms)

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 3u
+#define RL_ABI_VERSION 4u
 
 /* rule id of a descriptor whose limit is nil ("don't check", src/limiter/cache.go:19-22) */
 #define RL_NIL_RULE 0xFFFFFFFFu
@@ -197,6 +197,12 @@ int rl_host_acquire(rl_engine* e, rl_host_batch* out);
 int rl_submit(rl_engine* e, const rl_batch* batch, rl_status* out, uint32_t* req_throttle_ms);
 /* Complete the oldest batch in flight (any submit form). */
 int rl_wait(rl_engine* e);
+/* Non-blocking: 1 if the oldest batch in flight is done on the device (rl_wait would not block on
+ * it, barring a rerun the device asked for), 0 if not yet, RL_ESTATE with nothing in flight. A
+ * batcher gathering its next batch polls it to answer the callers of the batch in flight as soon
+ * as they can be answered (no counterpart in the reference: radix's pipelining answers each
+ * command as its reply arrives, src/redis/driver_impl.go:84-89). */
+int rl_query(rl_engine* e);
 /* Complete the oldest batch in flight, copying its results into out[n_desc] and
  * req_throttle_ms[n_req] (a host batch's, or NULL to discard). */
 int rl_wait_into(rl_engine* e, rl_status* out, uint32_t* req_throttle_ms);
@@ -331,7 +337,13 @@ int rl_route_unpack(rl_engine* e, const rl_batch* device_batch, const uint32_t* 
  * failure at an owner (decide or later) the outputs still hold every decision the healthy
  * owners made, the descriptors of a failed owner coming out with code RL_CODE_UNKNOWN (not
  * known to be applied) — the caller can answer those requests and fail only the others. After
- * a pack failure (any origin) nothing was applied anywhere and the outputs are untouched. */
+ * a pack failure (any origin) nothing was applied anywhere and the statuses are untouched; the
+ * ThrottleMillis words of origins whose pack ran may have been zeroed (the pack starts them at 0).
+ * Request times: every origin's batch-time range travels with its counts. An owner decides its
+ * records origin by origin in engine batches whose times span at most one second, so origins
+ * whose clocks or batch cuts differ by seconds are exact; a step whose origin starts more than
+ * 3 s behind the newest request time before it (the step clock: earlier steps and the origins
+ * before it in rank order) fails on every shard with RL_EINVAL from that origin's shard. */
 #define RL_ROUTER_ID_BYTES 128u
 typedef struct rl_router rl_router;
 
@@ -346,7 +358,9 @@ typedef struct rl_router_config {
 } rl_router_config;
 enum {
   RL_ROUTER_NO_COMBINE = 1u, /* one record per descriptor (no hot-prefix combining) */
-  RL_ROUTER_HOST = 2u        /* allocate pinned host staging: rl_router_host_acquire / _submit_host / _wait_into */
+  RL_ROUTER_HOST = 2u,       /* allocate pinned host staging: rl_router_host_acquire / _submit_host / _wait_into */
+  RL_ROUTER_EMULATED = 4u    /* rccl_id is an rl_router_emu_world id: the collective transport's code path with
+                                the collectives emulated in process (one thread per rank; tests) */
 };
 
 typedef struct rl_router_stats {
@@ -360,10 +374,19 @@ typedef struct rl_router_stats {
   uint32_t combined;       /* last step: combined records origin 0 (RCCL: this rank) sent (one per hot group) */
   uint64_t repacks;        /* steps packed again without combining (a hot group not one key string) */
   uint64_t combined_steps; /* steps whose origin 0 combined */
+  uint32_t owner_batches;  /* last step: engine batches owner 0 (collective: this rank) decided its records in
+                              (origins whose request times differ by 2 s or more go to separate batches) */
+  uint32_t step_clock;     /* the newest request time of every step applied so far (unix seconds) */
 } rl_router_stats;
 
 /* A fresh RCCL unique id (ncclGetUniqueId), RL_ROUTER_ID_BYTES bytes. */
 int rl_router_unique_id(uint8_t* id_out);
+/* An in-process world of n_ranks emulated ranks (RL_ROUTER_EMULATED): the id to pass as
+ * rccl_id to each rank's rl_router_create, every rank driven by its own thread. The collective
+ * transport runs unchanged; ncclAllToAll / ncclAllToAllv / ncclAllGather become device copies
+ * driven by the same count and displacement vectors, each rank's receive counts checked against
+ * its peers' send counts. The world is freed when the last of its n_ranks routers is destroyed. */
+int rl_router_emu_world(uint32_t n_ranks, uint8_t* id_out);
 /* engines: n_shards engines (local transport) or 1 (RCCL transport). The router does not own
  * them; they must outlive it and be used by nothing else while a step runs. All engines share
  * hash_seed and the rule table. */

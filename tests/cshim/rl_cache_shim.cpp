@@ -107,12 +107,14 @@ const char* rlc_error(void* p) { return static_cast<Shim*>(p)->err.c_str(); }
 
 void rlc_flush(void* p) { static_cast<Shim*>(p)->cache->Flush(); }
 
-// Batcher counters: batches, rule loads, rule loads made while a batch was in flight.
+// Batcher counters: batches, rule loads, rule loads made while a batch was in flight, drains
+// (batches in flight completed early for a load / submit the engine refused with them in flight).
 void rlc_batcher_stats(void* p, uint64_t* out) {
   const auto s = static_cast<Shim*>(p)->cache->batcher_stats();
   out[0] = s.batches;
   out[1] = s.rule_loads;
   out[2] = s.rule_loads_in_flight;
+  out[3] = s.drains;
 }
 
 }  // extern "C"

@@ -205,3 +205,51 @@ def test_rules_arrive_mid_stream_two_in_flight():
     assert bs[1] >= 10, list(bs)  # new limits kept arriving
     assert bs[2] >= 1, list(bs)   # and at least one load happened behind a batch in flight
     m.close()
+
+
+def test_more_than_v4_max_rules_through_do_limit():
+    """33000 distinct (L, unit) limits registered through DoLimit by 8
+    concurrent callers, so the rule table crosses V4_MAX_RULES (32768) while batches are in flight
+    and the engine then runs the LSD pipeline (one batch in flight). rl_load_rules / rl_submit
+    refuse those with RL_ESTATE; the batcher completes its batches in flight and retries (drains),
+    and no caller sees a RedisError. Every caller's results equal a serial oracle of its own
+    requests."""
+    T, per_req, n_rules = 8, 4, 33000
+    all_rules = [(k + 1, hiprl.SECOND) for k in range(n_rules)]
+    m = Mirror(False, window_us=100)
+    m.lib.rlc_batcher_stats.argtypes = [C.c_void_p, C.c_void_p]
+    ids = [m.add_rule(L, u, f"r{k}") for k, (L, u) in enumerate(all_rules)]
+    now = 1_700_000_321
+    m.lib.rlc_set_time(m.h, now)
+    per = []
+    for t in range(T):
+        mine = list(range(t, n_rules, T))  # each limit used by one caller, in increasing order
+        reqs = []
+        for q in range(0, len(mine), per_req):
+            rr = mine[q:q + per_req]
+            reqs.append((f"big{t}", [[("k", str((q // per_req + j) % 3))] for j in range(len(rr))], rr, 1, now))
+        per.append(reqs)
+    res = [None] * T
+
+    def run(t):
+        res[t] = [m.do_limit(d, de, [ids[x] for x in ru], h) for d, de, ru, h, _ in per[t]]
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    m.lib.rlc_flush(m.h)
+    for t in range(T):
+        o = oracle.Oracle()
+        o.load_rules(all_rules)
+        for q, ((got, gthr), (d, de, ru, h, tq)) in enumerate(zip(res[t], per[t])):
+            st, thr = o.submit(hiprl.build_batch([(d, de, ru, h, tq)]))
+            for k, g in enumerate(got):
+                assert (g[0], g[1], g[3]) == (int(st["code_flags"][k]) & 0xFF, int(st["limit_remaining"][k]),
+                                              int(st["reset_s"][k])), (t, q, k)
+            assert gthr == int(thr[0]), (t, q)
+    bs = (C.c_uint64 * 4)()
+    m.lib.rlc_batcher_stats(m.h, bs)
+    assert bs[3] >= 1, list(bs)  # the batcher drained at least once (the crossing / the LSD pipeline)
+    m.close()
