@@ -41,7 +41,7 @@ int64_t SystemTimeSource::UnixNow() {
       .count();
 }
 
-struct HipRateLimitCache::Call {
+struct PendingCall {
   const RateLimitRequest* req = nullptr;
   const std::vector<std::shared_ptr<RateLimit>>* limits = nullptr;
   int64_t now = 0;
@@ -51,6 +51,69 @@ struct HipRateLimitCache::Call {
   DoLimitResponse resp;
   std::promise<void> done;
 };
+
+namespace {
+
+// The caller's side of DoLimit, shared by both batchers: GenerateCacheKeys' prefix bytes per
+// descriptor with a limit (cache_key.go:57-65), one time per request (base_limiter.go:43), the
+// hits (fixed_cache_impl.go:39), Stats.TotalHits (base_limiter.go:49-51).
+std::shared_ptr<PendingCall> make_call(const RateLimitRequest& request,
+                                       const std::vector<std::shared_ptr<RateLimit>>& limits, TimeSource& ts) {
+  // assert.Assert(len(request.Descriptors) == len(limits))  base_limiter.go:41
+  if (request.Descriptors.size() != limits.size())
+    throw std::logic_error("assert: len(request.Descriptors) == len(limits)");
+  auto call = std::make_shared<PendingCall>();
+  call->req = &request;
+  call->limits = &limits;
+  call->now = ts.UnixNow();                                     // base_limiter.go:43
+  call->hits = request.HitsAddend > 1 ? request.HitsAddend : 1;  // fixed_cache_impl.go:39
+  call->prefix.resize(limits.size());
+  for (size_t i = 0; i < limits.size(); ++i) {
+    if (!limits[i]) continue;
+    // GenerateCacheKey prefix: domain '_' (key '_' value '_')*   cache_key.go:57-65
+    std::string& p = call->prefix[i];
+    p = request.Domain;
+    p += '_';
+    for (const auto& e : request.Descriptors[i].Entries) {
+      p += e.Key;
+      p += '_';
+      p += e.Value;
+      p += '_';
+    }
+    call->blob_bytes += p.size();
+    // Stats.TotalHits.Add(hitsAddend) for every non-nil limit  base_limiter.go:49-51
+    limits[i]->Stats->TotalHits.Add(call->hits);
+  }
+  return call;
+}
+
+// A call's DescriptorStatuses and stat adds from its statuses (GetResponseDescriptorStatus's
+// outputs, base_limiter.go:70-115,129-177), then the caller is released.
+void answer(PendingCall& c, const rl_status* out, uint32_t thr) {
+  c.resp.DescriptorStatuses.resize(c.prefix.size());
+  c.resp.ThrottleMillis = thr;
+  for (size_t i = 0; i < c.prefix.size(); ++i) {
+    const auto& lim = (*c.limits)[i];
+    const rl_status& s = out[i];
+    DescriptorStatus& o = c.resp.DescriptorStatuses[i];
+    o.code = (Code)(s.code_flags & 0xFF);
+    o.LimitRemaining = s.limit_remaining;
+    const uint32_t fl = s.code_flags >> 8;
+    if (lim && (fl & RL_FLAG_HAS_LIMIT)) {
+      o.CurrentLimit = &lim->Limit;
+      o.HasDurationUntilReset = true;
+      o.DurationUntilResetSeconds = s.reset_s;
+      // Stats adds of GetResponseDescriptorStatus (base_limiter.go:77-78,129-177)
+      if (s.over_limit_delta) lim->Stats->OverLimit.Add(s.over_limit_delta);
+      if (fl & RL_FLAG_LOCAL_CACHE_HIT) lim->Stats->OverLimitWithLocalCache.Add(s.over_limit_delta);
+      if (s.near_limit_delta) lim->Stats->NearLimit.Add(s.near_limit_delta);
+      if (fl & RL_FLAG_SHADOW) lim->Stats->ShadowMode.Add(1);
+    }
+  }
+  c.done.set_value();
+}
+
+}  // namespace
 
 HipRateLimitCache::HipRateLimitCache(const HipSettings& s, std::shared_ptr<TimeSource> ts)
     : s_(s), ts_(std::move(ts)) {
@@ -89,31 +152,7 @@ void HipRateLimitCache::Flush() {
 
 DoLimitResponse HipRateLimitCache::DoLimit(const RateLimitRequest& request,
                                            const std::vector<std::shared_ptr<RateLimit>>& limits) {
-  // assert.Assert(len(request.Descriptors) == len(limits))  base_limiter.go:41
-  if (request.Descriptors.size() != limits.size())
-    throw std::logic_error("assert: len(request.Descriptors) == len(limits)");
-  auto call = std::make_shared<Call>();
-  call->req = &request;
-  call->limits = &limits;
-  call->now = ts_->UnixNow();                                   // base_limiter.go:43
-  call->hits = request.HitsAddend > 1 ? request.HitsAddend : 1;  // fixed_cache_impl.go:39
-  call->prefix.resize(limits.size());
-  for (size_t i = 0; i < limits.size(); ++i) {
-    if (!limits[i]) continue;
-    // GenerateCacheKey prefix: domain '_' (key '_' value '_')*   cache_key.go:57-65
-    std::string& p = call->prefix[i];
-    p = request.Domain;
-    p += '_';
-    for (const auto& e : request.Descriptors[i].Entries) {
-      p += e.Key;
-      p += '_';
-      p += e.Value;
-      p += '_';
-    }
-    call->blob_bytes += p.size();
-    // Stats.TotalHits.Add(hitsAddend) for every non-nil limit  base_limiter.go:49-51
-    limits[i]->Stats->TotalHits.Add(call->hits);
-  }
+  auto call = make_call(request, limits, *ts_);
   std::future<void> f = call->done.get_future();
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -139,14 +178,14 @@ uint32_t HipRateLimitCache::rule_id(const RateLimitLimit& l, bool shadow) {
 // The batch being built in one of the engine's pinned staging slots (rl_host_acquire): calls
 // are written straight into C memory, the way the Go batcher does.
 struct HipRateLimitCache::Staged {
-  std::vector<std::shared_ptr<Call>> calls;
+  std::vector<std::shared_ptr<PendingCall>> calls;
   rl_host_batch hb{};
   uint32_t nd = 0, nr = 0, nb = 0;
   int64_t tmin = 0, tmax = 0;
   bool failed = false;  // refused at submit: its callers already have the error
 };
 
-bool HipRateLimitCache::fits(const Staged& st, const Call& c) const {
+bool HipRateLimitCache::fits(const Staged& st, const PendingCall& c) const {
   if (st.calls.empty()) return true;
   const int64_t lo = c.now < st.tmin ? c.now : st.tmin, hi = c.now > st.tmax ? c.now : st.tmax;
   // A batch may straddle at most one window boundary of a unit (rl_submit refuses a SECOND key
@@ -158,8 +197,8 @@ bool HipRateLimitCache::fits(const Staged& st, const Call& c) const {
 
 // One request into the slot: GenerateCacheKey's bytes before the timestamp per descriptor with
 // a limit (cache_key.go:57-65), the rule id, the request index; now and the raw HitsAddend.
-void HipRateLimitCache::add(Staged& st, const std::shared_ptr<Call>& cp) {
-  Call& c = *cp;
+void HipRateLimitCache::add(Staged& st, const std::shared_ptr<PendingCall>& cp) {
+  PendingCall& c = *cp;
   if (st.calls.empty()) st.tmin = st.tmax = c.now;
   st.tmin = c.now < st.tmin ? c.now : st.tmin;
   st.tmax = c.now > st.tmax ? c.now : st.tmax;
@@ -179,7 +218,7 @@ void HipRateLimitCache::add(Staged& st, const std::shared_ptr<Call>& cp) {
   st.calls.push_back(cp);
 }
 
-void HipRateLimitCache::fail(std::vector<std::shared_ptr<Call>>& calls) {
+void HipRateLimitCache::fail(std::vector<std::shared_ptr<PendingCall>>& calls) {
   // checkError -> panic(RedisError(...))  src/redis/driver_impl.go:50-54
   const std::string msg = std::string("hip backend: ") + rl_last_error(eng_);
   for (auto& c : calls) c->done.set_exception(std::make_exception_ptr(RedisError(msg)));
@@ -257,28 +296,9 @@ void HipRateLimitCache::finish(Staged& st) {
   }
   size_t d = 0;
   for (size_t r = 0; r < st.calls.size(); ++r) {
-    Call& c = *st.calls[r];
-    c.resp.DescriptorStatuses.resize(c.prefix.size());
-    c.resp.ThrottleMillis = thr[r];
-    for (size_t i = 0; i < c.prefix.size(); ++i, ++d) {
-      const auto& lim = (*c.limits)[i];
-      const rl_status& s = out[d];
-      DescriptorStatus& o = c.resp.DescriptorStatuses[i];
-      o.code = (Code)(s.code_flags & 0xFF);
-      o.LimitRemaining = s.limit_remaining;
-      const uint32_t fl = s.code_flags >> 8;
-      if (lim && (fl & RL_FLAG_HAS_LIMIT)) {
-        o.CurrentLimit = &lim->Limit;
-        o.HasDurationUntilReset = true;
-        o.DurationUntilResetSeconds = s.reset_s;
-        // Stats adds of GetResponseDescriptorStatus (base_limiter.go:77-78,129-177)
-        if (s.over_limit_delta) lim->Stats->OverLimit.Add(s.over_limit_delta);
-        if (fl & RL_FLAG_LOCAL_CACHE_HIT) lim->Stats->OverLimitWithLocalCache.Add(s.over_limit_delta);
-        if (s.near_limit_delta) lim->Stats->NearLimit.Add(s.near_limit_delta);
-        if (fl & RL_FLAG_SHADOW) lim->Stats->ShadowMode.Add(1);
-      }
-    }
-    c.done.set_value();
+    PendingCall& c = *st.calls[r];
+    answer(c, out + d, thr[r]);
+    d += c.prefix.size();
   }
   done_calls(st.calls.size());
 }
@@ -291,9 +311,9 @@ void HipRateLimitCache::finish(Staged& st) {
 // src/redis/driver_impl.go:84-89).
 void HipRateLimitCache::submitter() {
   std::deque<Staged> inflight;
-  std::shared_ptr<Call> carry;
+  std::shared_ptr<PendingCall> carry;
   for (;;) {
-    std::shared_ptr<Call> first = std::move(carry);
+    std::shared_ptr<PendingCall> first = std::move(carry);
     carry.reset();
     if (!first) {
       std::unique_lock<std::mutex> g(mu_);
@@ -310,7 +330,7 @@ void HipRateLimitCache::submitter() {
     }
     Staged st;
     if (rl_host_acquire(eng_, &st.hb)) {
-      std::vector<std::shared_ptr<Call>> one{first};
+      std::vector<std::shared_ptr<PendingCall>> one{first};
       fail(one);
       continue;
     }
@@ -325,7 +345,7 @@ void HipRateLimitCache::submitter() {
       const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(s_.batch_window_us);
       for (;;) {
         while (!q_.empty()) {
-          std::shared_ptr<Call> c = q_.front();
+          std::shared_ptr<PendingCall> c = q_.front();
           q_.pop_front();
           if (!fits(st, *c)) {
             carry = std::move(c);  // starts the next batch
@@ -363,6 +383,299 @@ void HipRateLimitCache::submitter() {
     }
   }
   for (auto& st : inflight) finish(st);
+}
+
+// ---- HipRoutedRateLimitCache ------------------------------------------------------------
+struct HipRoutedRateLimitCache::Step {
+  std::vector<std::shared_ptr<PendingCall>> calls;
+  uint32_t nd = 0, nr = 0, nb = 0;
+  int64_t tmin = 0, tmax = 0;
+};
+
+namespace {
+// One rank's words in a rule / stop agreement (rl_router_allgather_host, RL_ROUTER_AG_MAX bytes).
+constexpr uint32_t SYNC_RULES = (RL_ROUTER_AG_MAX - 8) / sizeof(rl_rule);
+struct SyncWords {
+  uint32_t stop, n;
+  rl_rule rules[SYNC_RULES];
+};
+static_assert(sizeof(SyncWords) <= RL_ROUTER_AG_MAX, "sync words");
+std::pair<uint32_t, uint32_t> limit_key(const RateLimit& r) {
+  return {r.Limit.RequestsPerUnit, (uint32_t)r.Limit.unit | (r.ShadowMode ? RL_RULE_SHADOW : 0u)};
+}
+}  // namespace
+
+HipRoutedRateLimitCache::HipRoutedRateLimitCache(const HipSettings& s, const HipRoutedSettings& r,
+                                                 std::shared_ptr<TimeSource> ts)
+    : s_(s), r_(r), ts_(std::move(ts)) {
+  if (r.id.size() != RL_ROUTER_ID_BYTES) throw RedisError("routed cache: id must hold RL_ROUTER_ID_BYTES bytes");
+  rl_config c;
+  memset(&c, 0, sizeof c);
+  c.struct_size = sizeof c;
+  c.device = s.device;
+  for (int u = 0; u < 4; ++u) c.log2_slots[u] = s.log2_slots[u];
+  c.near_limit_ratio = s.near_limit_ratio;
+  c.local_cache = s.local_cache ? 1 : 0;
+  c.per_second_split = s.per_second_split ? 1 : 0;
+  // an owner may receive every origin's whole batch (a key hot everywhere)
+  c.max_batch_desc = s.batch_limit * r.n_shards;
+  c.max_batch_req = s.batch_limit * r.n_shards;
+  c.max_blob_bytes = s.batch_limit * 128u;
+  c.hash_seed = s.hash_seed;
+  c.max_load_permille = s.max_load_permille;
+  int rc = rl_create(&c, &eng_);
+  if (rc) throw RedisError("rl_create failed: " + std::to_string(rc) + ": " + rl_last_error(nullptr));
+  rl_router_config rc2;
+  memset(&rc2, 0, sizeof rc2);
+  rc2.struct_size = sizeof rc2;
+  rc2.n_shards = r.n_shards;
+  rc2.rank = r.rank;
+  rc2.max_desc = s.batch_limit;
+  rc2.rccl_id = r.id.data();
+  rc2.flags = RL_ROUTER_HOST | (r.emulated ? RL_ROUTER_EMULATED : 0u);
+  rc2.max_blob_bytes = s.batch_limit * 128u;
+  rl_engine* es[1] = {eng_};
+  rc = rl_router_create(&rc2, es, &rt_);
+  if (rc) {
+    rl_destroy(eng_);
+    throw RedisError("rl_router_create failed: " + std::to_string(rc));
+  }
+  thr_ = std::thread([this] { submitter(); });
+}
+
+HipRoutedRateLimitCache::~HipRoutedRateLimitCache() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  thr_.join();
+  rl_router_destroy(rt_);
+  rl_destroy(eng_);
+}
+
+void HipRoutedRateLimitCache::Flush() {
+  std::unique_lock<std::mutex> g(mu_);
+  idle_cv_.wait(g, [&] { return inflight_ == 0; });
+}
+
+DoLimitResponse HipRoutedRateLimitCache::DoLimit(const RateLimitRequest& request,
+                                                 const std::vector<std::shared_ptr<RateLimit>>& limits) {
+  auto call = make_call(request, limits, *ts_);
+  std::future<void> f = call->done.get_future();
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (broken_) throw RedisError("hip backend: " + broken_msg_);
+    q_.push_back(call);
+    ++inflight_;
+  }
+  cv_.notify_one();
+  f.get();  // rethrows RedisError
+  return std::move(call->resp);
+}
+
+void HipRoutedRateLimitCache::done_calls(size_t n) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    inflight_ -= n;
+  }
+  idle_cv_.notify_all();
+}
+
+void HipRoutedRateLimitCache::fail(std::vector<std::shared_ptr<PendingCall>>& calls, const std::string& msg) {
+  for (auto& c : calls) c->done.set_exception(std::make_exception_ptr(RedisError("hip backend: " + msg)));
+  done_calls(calls.size());
+  calls.clear();
+}
+
+// Every limit of the call has an agreed id; otherwise its new limits are queued for the next sync.
+bool HipRoutedRateLimitCache::known(const PendingCall& c) {
+  bool ok = true;
+  for (const auto& lim : *c.limits) {
+    if (!lim) continue;
+    const auto k = limit_key(*lim);
+    if (ids_.count(k)) continue;
+    ok = false;
+    if (pending_set_.insert(k).second) pending_.push_back(rl_rule{k.first, k.second});
+  }
+  return ok;
+}
+
+// The rule / stop agreement (nothing in flight on any rank): every rank's new limits appended to
+// every rank's table in rank order (the first occurrence keeps its id), loaded into the engine.
+// Returns true when every rank asked to stop.
+bool HipRoutedRateLimitCache::sync(bool want_stop) {
+  SyncWords mine;
+  memset(&mine, 0, sizeof mine);
+  mine.stop = want_stop ? 1u : 0u;
+  mine.n = (uint32_t)std::min<size_t>(pending_.size(), SYNC_RULES);
+  std::copy(pending_.begin(), pending_.begin() + mine.n, mine.rules);
+  std::vector<SyncWords> all(r_.n_shards);
+  int rc = rl_router_allgather_host(rt_, &mine, sizeof mine, all.data());
+  if (rc) throw RedisError(std::string("rule agreement: ") + rl_router_last_error(rt_));
+  n_syncs_ += 1;
+  bool all_stop = true;
+  const size_t before = rules_.size();
+  for (const SyncWords& w : all) {
+    all_stop &= w.stop != 0;
+    for (uint32_t i = 0; i < w.n; ++i) {
+      const auto k = std::make_pair(w.rules[i].requests_per_unit, w.rules[i].unit);
+      if (ids_.emplace(k, (uint32_t)rules_.size()).second) rules_.push_back(w.rules[i]);
+    }
+  }
+  for (uint32_t i = 0; i < mine.n; ++i)
+    pending_set_.erase(std::make_pair(pending_[i].requests_per_unit, pending_[i].unit));
+  pending_.erase(pending_.begin(), pending_.begin() + mine.n);
+  if (rules_.size() != before) {
+    rc = rl_load_rules(eng_, rules_.data(), (uint32_t)rules_.size());
+    if (rc) throw RedisError(std::string("rl_load_rules: ") + rl_last_error(eng_));
+    n_rules_ = rules_.size();
+  }
+  return all_stop;
+}
+
+// The rank's step loop: rule / stop agreement every rule_sync_every steps (nothing in flight),
+// otherwise gather for one step period, submit (an empty batch when idle), two steps in flight.
+void HipRoutedRateLimitCache::submitter() {
+  std::deque<Step> fl;
+  std::deque<std::shared_ptr<PendingCall>> held;  // calls waiting for a rule agreement
+  std::vector<rl_status> out;
+  std::vector<uint32_t> thr;
+  uint64_t seq = 0;
+  auto finish_one = [&] {
+    Step st = std::move(fl.front());
+    fl.pop_front();
+    out.resize(std::max<size_t>(1, st.nd));
+    thr.resize(std::max<size_t>(1, st.nr));
+    rl_status* o[1] = {out.data()};
+    uint32_t* t[1] = {thr.data()};
+    const int rc = rl_router_wait_into(rt_, o, t);
+    if (rc) {
+      if (rc == RL_ECOMM) {
+        std::lock_guard<std::mutex> g(mu_);
+        broken_ = true;
+        broken_msg_ = rl_router_last_error(rt_);
+      }
+      fail(st.calls, rl_router_last_error(rt_));
+      return;
+    }
+    size_t d = 0;
+    for (size_t r = 0; r < st.calls.size(); ++r) {
+      PendingCall& c = *st.calls[r];
+      answer(c, out.data() + d, thr[r]);
+      d += c.prefix.size();
+    }
+    done_calls(st.calls.size());
+  };
+  auto fail_all = [&](const std::string& msg) {
+    while (!fl.empty()) {
+      fail(fl.front().calls, msg);
+      fl.pop_front();
+    }
+    std::vector<std::shared_ptr<PendingCall>> rest(held.begin(), held.end());
+    held.clear();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      broken_ = true;
+      broken_msg_ = msg;
+      rest.insert(rest.end(), q_.begin(), q_.end());
+      q_.clear();
+    }
+    fail(rest, msg);
+  };
+  try {
+    for (;;) {
+      if (broken_) break;
+      if (seq % r_.rule_sync_every == 0) {
+        while (!fl.empty()) finish_one();
+        bool want_stop;
+        {
+          std::lock_guard<std::mutex> g(mu_);
+          want_stop = stop_ && q_.empty() && held.empty();
+        }
+        if (sync(want_stop)) break;  // every rank stops here
+        if (!held.empty()) {  // calls whose limits are agreed now go back to the front, in order
+          std::lock_guard<std::mutex> g(mu_);
+          for (auto it = held.rbegin(); it != held.rend(); ++it) q_.push_front(*it);
+          held.clear();
+        }
+      }
+      Step st;
+      rl_host_batch hb;
+      if (rl_router_host_acquire(rt_, 0, &hb)) throw RedisError(rl_router_last_error(rt_));
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(r_.step_us);
+        for (;;) {
+          while (!q_.empty()) {
+            std::shared_ptr<PendingCall> cp = q_.front();
+            PendingCall& c = *cp;
+            if (!known(c)) {  // waits for the next agreement
+              held.push_back(cp);
+              q_.pop_front();
+              n_held_ += 1;
+              continue;
+            }
+            const int64_t lo = st.calls.empty() ? c.now : std::min(st.tmin, c.now);
+            const int64_t hi = st.calls.empty() ? c.now : std::max(st.tmax, c.now);
+            // one batch straddles at most one window boundary (hi - lo < 2), and fits the slot
+            if (hi - lo >= 2 || st.nd + c.prefix.size() > s_.batch_limit || st.nd + c.prefix.size() > hb.max_desc ||
+                st.nr + 1 > hb.max_req || st.nb + c.blob_bytes > hb.max_blob)
+              goto full;
+            q_.pop_front();
+            st.tmin = lo;
+            st.tmax = hi;
+            const uint32_t rq = st.nr++;
+            hb.now[rq] = c.now;
+            hb.hits_addend[rq] = c.req->HitsAddend;
+            hb.prefix_off[0] = 0;
+            for (size_t i = 0; i < c.prefix.size(); ++i) {
+              const auto& lim = (*c.limits)[i];
+              memcpy(hb.prefix_blob + st.nb, c.prefix[i].data(), c.prefix[i].size());
+              st.nb += (uint32_t)c.prefix[i].size();
+              hb.rule_id[st.nd] = lim ? ids_.at(limit_key(*lim)) : RL_NIL_RULE;
+              hb.req_of[st.nd] = rq;
+              ++st.nd;
+              hb.prefix_off[st.nd] = st.nb;
+            }
+            st.calls.push_back(cp);
+          }
+          if (st.nd >= s_.batch_limit) break;
+          if (cv_.wait_until(g, deadline) == std::cv_status::timeout) break;
+          if (std::chrono::steady_clock::now() >= deadline) break;
+        }
+      full:;
+      }
+      rl_batch b;
+      memset(&b, 0, sizeof b);
+      b.n_desc = st.nd;
+      b.n_req = st.nr;
+      b.blob_bytes = st.nb;
+      if (st.nd || st.nr) {
+        b.prefix_blob = hb.prefix_blob;  // the router's pinned slot: staged without a copy
+        b.prefix_off = hb.prefix_off;
+        b.rule_id = hb.rule_id;
+        b.req_of = hb.req_of;
+        b.now = hb.now;
+        b.hits_addend = hb.hits_addend;
+      } else {
+        n_empty_ += 1;  // an idle rank still takes part in the step's collectives
+      }
+      const int rc = rl_router_submit_host(rt_, &b);
+      ++seq;
+      n_steps_ += 1;
+      if (rc) {  // refused before its collectives (a broken communicator): this rank cannot step on
+        const std::string msg = rl_router_last_error(rt_);
+        fail(st.calls, msg);
+        throw RedisError(msg);
+      }
+      fl.push_back(std::move(st));
+      if (fl.size() == 2) finish_one();
+    }
+  } catch (const RedisError& e) {
+    fail_all(e.what());
+  }
+  while (!fl.empty()) finish_one();
 }
 
 }  // namespace ratelimit

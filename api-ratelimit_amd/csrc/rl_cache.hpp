@@ -21,6 +21,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -137,6 +138,9 @@ class RateLimitCache {
   virtual void Flush() = 0;
 };
 
+// One DoLimit call waiting in a micro-batcher (rl_cache.cpp).
+struct PendingCall;
+
 // HIP_* settings (BACKEND_TYPE=hip)
 struct HipSettings {
   int device = 0;                         // HIP_DEVICES
@@ -173,15 +177,14 @@ class HipRateLimitCache : public RateLimitCache {
   }
 
  private:
-  struct Call;
   struct Staged;
   void submitter();
   uint32_t rule_id(const RateLimitLimit& l, bool shadow);
-  bool fits(const Staged& st, const Call& c) const;
-  void add(Staged& st, const std::shared_ptr<Call>& c);
+  bool fits(const Staged& st, const PendingCall& c) const;
+  void add(Staged& st, const std::shared_ptr<PendingCall>& c);
   void submit(Staged& st, std::deque<Staged>& inflight);
   void finish(Staged& st);
-  void fail(std::vector<std::shared_ptr<Call>>& calls);
+  void fail(std::vector<std::shared_ptr<PendingCall>>& calls);
   void done_calls(size_t n);
 
   HipSettings s_;
@@ -189,7 +192,7 @@ class HipRateLimitCache : public RateLimitCache {
   rl_engine* eng_ = nullptr;
   std::mutex mu_;
   std::condition_variable cv_, idle_cv_;
-  std::deque<std::shared_ptr<Call>> q_;
+  std::deque<std::shared_ptr<PendingCall>> q_;
   size_t inflight_ = 0;  // calls enqueued and not yet answered
   bool stop_ = false;
   std::thread thr_;
@@ -199,6 +202,76 @@ class HipRateLimitCache : public RateLimitCache {
   std::vector<rl_rule> rules_;
   bool rules_dirty_ = false;
   std::atomic<uint64_t> n_batches_{0}, n_loads_{0}, n_loads_inflight_{0}, n_drains_{0};
+};
+
+// ---- Multi-GPU deployment ------------------------------------------------
+// One HipRoutedRateLimitCache per GPU: one process per GPU over RCCL (rl_router_unique_id made by
+// rank 0 and handed to the others out of band), or one thread per rank of this process over the
+// emulated collectives (rl_router_emu_world; tests). Each rank's DoLimit callers enqueue on its
+// own batcher; every rank steps on a fixed cadence (step_us) — gathering what its callers queued
+// during the step into the router's pinned slot, or an EMPTY batch when its queue is idle — so the
+// ranks' collectives always pair up (rl_hip.h: every rank makes the same sequence of router
+// calls). Two steps are in flight. Rule ids must mean one limit on every owner: a new (L, unit)
+// is agreed at the next rule-sync step (every rule_sync_every steps, with nothing in flight, by
+// rl_router_allgather_host: every rank appends every rank's new rules in rank order), and a call
+// that needs it waits for that step. A stop is agreed the same way: a rank leaves only when every
+// rank asked to stop with nothing queued. Serial order: each step, rank 0's batch, rank 1's, ...
+// The reference's equivalent is the radix cluster client sending each key's commands to the node
+// that owns it, pipelined (src/redis/driver_impl.go:84-110); DoLimit stays synchronous for its
+// caller (src/limiter/cache.go:15-33).
+struct HipRoutedSettings {
+  uint32_t n_shards = 1;
+  uint32_t rank = 0;
+  std::vector<uint8_t> id;        // RL_ROUTER_ID_BYTES: rl_router_unique_id, or rl_router_emu_world
+  bool emulated = false;          // id is an emulated world (one thread per rank in this process)
+  uint32_t step_us = 200;         // step cadence (HIP_STEP_US)
+  uint32_t rule_sync_every = 16;  // steps between rule / stop agreements
+};
+
+class HipRoutedRateLimitCache : public RateLimitCache {
+ public:
+  // Collective: every rank constructs at the same time (rl_router_create agrees configurations).
+  HipRoutedRateLimitCache(const HipSettings& s, const HipRoutedSettings& r, std::shared_ptr<TimeSource> time_source);
+  // Collective too: returns once every rank has asked to stop and nothing is queued anywhere.
+  ~HipRoutedRateLimitCache() override;
+  DoLimitResponse DoLimit(const RateLimitRequest& request,
+                          const std::vector<std::shared_ptr<RateLimit>>& limits) override;
+  void Flush() override;
+
+  struct RoutedStats {
+    uint64_t steps, empty_steps, rule_syncs, rules, held_calls;
+  };
+  RoutedStats routed_stats() const {
+    return {n_steps_.load(), n_empty_.load(), n_syncs_.load(), n_rules_.load(), n_held_.load()};
+  }
+
+ private:
+  struct Step;
+  void submitter();
+  bool known(const PendingCall& c);
+  bool sync(bool want_stop);
+  void fail(std::vector<std::shared_ptr<PendingCall>>& calls, const std::string& msg);
+  void done_calls(size_t n);
+
+  HipSettings s_;
+  HipRoutedSettings r_;
+  std::shared_ptr<TimeSource> ts_;
+  rl_engine* eng_ = nullptr;
+  rl_router* rt_ = nullptr;
+  std::mutex mu_;
+  std::condition_variable cv_, idle_cv_;
+  std::deque<std::shared_ptr<PendingCall>> q_;
+  size_t inflight_ = 0;
+  bool stop_ = false;
+  bool broken_ = false;  // the router's communicator is gone: every call fails
+  std::string broken_msg_;
+  std::thread thr_;
+  // agreed rule registry (submitter thread): identical on every rank after each sync
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> ids_;
+  std::vector<rl_rule> rules_;
+  std::vector<rl_rule> pending_;  // new limits seen here, not agreed yet
+  std::set<std::pair<uint32_t, uint32_t>> pending_set_;
+  std::atomic<uint64_t> n_steps_{0}, n_empty_{0}, n_syncs_{0}, n_rules_{0}, n_held_{0};
 };
 
 }  // namespace ratelimit

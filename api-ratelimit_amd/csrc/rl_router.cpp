@@ -1400,6 +1400,32 @@ int rl_router_wait_into(rl_router* r, rl_status* const* out, uint32_t* const* th
   return r->wait(out, thr, true);
 }
 
+int rl_router_allgather_host(rl_router* r, const void* in, uint32_t n_bytes, void* out) {
+  if (!r || (n_bytes && (!in || !out))) return RL_EINVAL;
+  if (!r->coll) return r->fail(RL_ESTATE, "rl_router_allgather_host needs the collective transport");
+  if (n_bytes > RL_ROUTER_AG_MAX) return r->fail(RL_EINVAL, "rl_router_allgather_host: %u bytes > %u", n_bytes,
+                                                 RL_ROUTER_AG_MAX);
+  if (r->broken) return r->fail(RL_ECOMM, "the router's communicator was aborted after a transport failure");
+  const uint32_t G = r->cfg.n_shards;
+  uint8_t* hs = reinterpret_cast<uint8_t*>(r->h_ag);
+  uint8_t* ds = reinterpret_cast<uint8_t*>(r->d_ag);
+  static_assert(RL_ROUTER_AG_MAX <= sizeof(AgEntry) * HOT_MAX, "allgather staging");
+  if (n_bytes) memcpy(hs, in, n_bytes);
+  hipError_t he = n_bytes ? hipMemcpyAsync(ds, hs, n_bytes, hipMemcpyHostToDevice, r->rs) : hipSuccess;
+  const ncclResult_t nr = r->xp->allgather(ds, ds + RL_ROUTER_AG_MAX, n_bytes, r->rs);
+  if (nr != ncclSuccess) return r->nccl_fail(nr, "allgather(host words)");
+  if (he == hipSuccess && n_bytes)
+    he = hipMemcpyAsync(hs + RL_ROUTER_AG_MAX, ds + RL_ROUTER_AG_MAX, (size_t)n_bytes * G, hipMemcpyDeviceToHost, r->rs);
+  if (he == hipSuccess) he = hipStreamSynchronize(r->rs);
+  if (he != hipSuccess) {  // the peers have their words; this rank cannot tell what it received
+    if (r->xp) r->xp->abort();
+    r->broken = true;
+    return r->fail(RL_ECOMM, "allgather(host words): %s (communicator aborted)", hipGetErrorString(he));
+  }
+  if (n_bytes) memcpy(out, hs + RL_ROUTER_AG_MAX, (size_t)n_bytes * G);
+  return 0;
+}
+
 int rl_router_get_stats(const rl_router* r, rl_router_stats* out) {
   if (!r || !out) return RL_EINVAL;
   *out = r->st;

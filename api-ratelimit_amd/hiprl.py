@@ -157,6 +157,7 @@ ABI = [
     ("rl_router_host_acquire", [C.c_void_p, C.c_uint32, C.POINTER(RlHostBatch)], C.c_int),
     ("rl_router_submit_host", [C.c_void_p, C.POINTER(RlBatch)], C.c_int),
     ("rl_router_wait_into", [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
+    ("rl_router_allgather_host", [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p], C.c_int),
     ("rl_router_get_stats", [C.c_void_p, C.POINTER(RlRouterStats)], C.c_int),
     ("rl_router_last_error", [C.c_void_p], C.c_char_p),
     ("rl_router_destroy", [C.c_void_p], None),

@@ -413,6 +413,14 @@ int rl_router_wait(rl_router* r);
 int rl_router_host_acquire(rl_router* r, uint32_t shard, rl_host_batch* out);
 int rl_router_submit_host(rl_router* r, const rl_batch* host_batches);
 int rl_router_wait_into(rl_router* r, rl_status* const* out, uint32_t* const* req_throttle_ms);
+/* A small collective over the router's transport (collective transports only): every rank
+ * contributes n_bytes (<= RL_ROUTER_AG_MAX, the same on every rank) of host memory `in`, and out
+ * receives n_shards * n_bytes in rank order. Synchronous. Every rank must make the same sequence
+ * of router calls (steps and these), e.g. with no step in flight at the same step number: a
+ * multi-GPU batcher uses it to agree new rules and a stop at the same step on every rank (rule
+ * ids must mean the same limit on every owner). */
+#define RL_ROUTER_AG_MAX 8192u
+int rl_router_allgather_host(rl_router* r, const void* in, uint32_t n_bytes, void* out);
 int rl_router_get_stats(const rl_router* r, rl_router_stats* out);
 const char* rl_router_last_error(const rl_router* r);
 void rl_router_destroy(rl_router* r);

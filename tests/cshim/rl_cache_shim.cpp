@@ -21,7 +21,9 @@ struct Shim {
   std::shared_ptr<FixedTime> ts = std::make_shared<FixedTime>();
   StatsStore store;
   std::vector<std::shared_ptr<RateLimit>> rules;
-  std::unique_ptr<HipRateLimitCache> cache;
+  std::unique_ptr<RateLimitCache> cache;
+  HipRateLimitCache* single = nullptr;
+  HipRoutedRateLimitCache* routed = nullptr;
   std::string err;
 };
 }  // namespace
@@ -37,12 +39,54 @@ void* rlc_create(int local_cache, float near_ratio, int per_second, uint32_t win
   hs.batch_window_us = window_us;
   hs.batch_limit = 1u << 14;
   try {
-    s->cache = std::make_unique<HipRateLimitCache>(hs, s->ts);
+    auto c = std::make_unique<HipRateLimitCache>(hs, s->ts);
+    s->single = c.get();
+    s->cache = std::move(c);
   } catch (const std::exception& e) {
     delete s;
     return nullptr;
   }
   return s;
+}
+
+// One rank of the multi-GPU batcher (HipRoutedRateLimitCache). id: RL_ROUTER_ID_BYTES from
+// rl_router_unique_id or rl_router_emu_world (emulated != 0). Collective: every rank's create runs
+// at the same time (one thread per rank). Destroy (rlc_destroy) is collective too.
+void* rlc_create_routed(uint32_t n_shards, uint32_t rank, const uint8_t* id, int emulated, int local_cache,
+                        uint32_t step_us, uint32_t rule_sync_every, uint32_t batch_limit) {
+  auto* s = new Shim();
+  HipSettings hs;
+  hs.local_cache = local_cache != 0;
+  hs.batch_limit = batch_limit;
+  hs.log2_slots[0] = hs.log2_slots[1] = hs.log2_slots[2] = 16;
+  hs.log2_slots[3] = 14;
+  HipRoutedSettings rs;
+  rs.n_shards = n_shards;
+  rs.rank = rank;
+  rs.id.assign(id, id + RL_ROUTER_ID_BYTES);
+  rs.emulated = emulated != 0;
+  rs.step_us = step_us;
+  rs.rule_sync_every = rule_sync_every;
+  try {
+    auto c = std::make_unique<HipRoutedRateLimitCache>(hs, rs, s->ts);
+    s->routed = c.get();
+    s->cache = std::move(c);
+  } catch (const std::exception& e) {
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+
+// Routed batcher counters: steps, empty steps, rule agreements, agreed rules, calls held for one.
+void rlc_routed_stats(void* p, uint64_t* out) {
+  const auto* r = static_cast<Shim*>(p)->routed;
+  const auto s = r ? r->routed_stats() : HipRoutedRateLimitCache::RoutedStats{0, 0, 0, 0, 0};
+  out[0] = s.steps;
+  out[1] = s.empty_steps;
+  out[2] = s.rule_syncs;
+  out[3] = s.rules;
+  out[4] = s.held_calls;
 }
 
 void rlc_destroy(void* p) { delete static_cast<Shim*>(p); }
@@ -110,7 +154,7 @@ void rlc_flush(void* p) { static_cast<Shim*>(p)->cache->Flush(); }
 // Batcher counters: batches, rule loads, rule loads made while a batch was in flight, drains
 // (batches in flight completed early for a load / submit the engine refused with them in flight).
 void rlc_batcher_stats(void* p, uint64_t* out) {
-  const auto s = static_cast<Shim*>(p)->cache->batcher_stats();
+  const auto s = static_cast<Shim*>(p)->single->batcher_stats();
   out[0] = s.batches;
   out[1] = s.rule_loads;
   out[2] = s.rule_loads_in_flight;

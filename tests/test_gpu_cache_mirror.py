@@ -253,3 +253,106 @@ def test_more_than_v4_max_rules_through_do_limit():
     m.lib.rlc_batcher_stats(m.h, bs)
     assert bs[3] >= 1, list(bs)  # the batcher drained at least once (the crossing / the LSD pipeline)
     m.close()
+
+
+class RoutedMirror(Mirror):
+    """One rank of the multi-GPU C++ batcher (HipRoutedRateLimitCache) through the shim."""
+
+    def __init__(self, lib, h):  # noqa: super-init not called: the handle is made collectively
+        self.lib, self.h = lib, h
+
+
+def _parallel(n, fn):
+    th = [threading.Thread(target=fn, args=(i,), daemon=True) for i in range(n)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(600)
+    assert not any(x.is_alive() for x in th), "a thread hung"
+
+
+def test_routed_batcher_g4_uneven_arrival_new_rules_mid_stream():
+    """the multi-GPU micro-batcher (one HipRoutedRateLimitCache per rank over the
+    router's collective transport, here 4 emulated ranks of one process, one thread each): a fixed
+    step cadence, an EMPTY step when a rank's queue is idle, the router's host entry, two steps in
+    flight, new (L, unit) limits agreed across ranks mid-stream. 8 concurrent callers per rank;
+    rank 2's callers start late and rank 3's pause for stretches, so ranks idle while others run;
+    limits appear progressively and differ per rank (a limit is registered by whichever rank sees
+    it first; every owner must read one rule table). Each caller's statuses, throttles and its
+    rank's stats equal a serial oracle of its own requests (callers use disjoint keys, which the
+    router sends to owners on every rank)."""
+    import time
+
+    G, T, n = 4, 8, 90
+    lib = _lib()
+    lib.rlc_create_routed.argtypes = [C.c_uint32, C.c_uint32, C.c_char_p, C.c_int, C.c_int, C.c_uint32,
+                                      C.c_uint32, C.c_uint32]
+    lib.rlc_create_routed.restype = C.c_void_p
+    lib.rlc_routed_stats.argtypes = [C.c_void_p, C.c_void_p]
+    wid = hiprl.Router.emu_world(G)
+    hs = [None] * G
+    _parallel(G, lambda r: hs.__setitem__(r, lib.rlc_create_routed(G, r, wid, 1, 0, 200, 8, 4096)))
+    assert all(hs), hs
+    ms = [RoutedMirror(lib, h) for h in hs]
+    units = [hiprl.SECOND, hiprl.MINUTE, hiprl.HOUR]
+    all_rules = [(4 + 3 * k, units[k % 3]) for k in range(48)]
+    ids = [[m.add_rule(L, u, f"rule{k}") for k, (L, u) in enumerate(all_rules)] for m in ms]
+    now = 1_700_000_457
+    for m in ms:
+        lib.rlc_set_time(m.h, now)
+    rng = np.random.default_rng(5)
+    per = {}
+    for r in range(G):
+        for t in range(T):
+            reqs = []
+            for q in range(n):
+                avail = min(len(all_rules), 1 + q // 4 + t + 6 * r)  # new limits keep appearing, per rank
+                nd = 1 + int(rng.integers(0, 3))
+                descs = [[("k", str(int(rng.integers(0, 4))))] for _ in range(nd)]
+                rr = [int(rng.integers(0, avail)) if rng.random() < 0.9 else None for _ in range(nd)]
+                reqs.append((f"rk{r}c{t}", descs, rr, int(rng.integers(0, 3)), now))
+            per[(r, t)] = reqs
+    res = {}
+
+    def caller(i):
+        r, t = divmod(i, T)
+        m = ms[r]
+        if r == 2:
+            time.sleep(0.15)  # rank 2 idle at first: its steps are empty
+        out = []
+        for q, (d, de, ru, h, _) in enumerate(per[(r, t)]):
+            if r == 3 and q % 30 == 29:
+                time.sleep(0.05)  # rank 3 idles for stretches
+            out.append(m.do_limit(d, de, [None if x is None else ids[r][x] for x in ru], h))
+        res[(r, t)] = out
+
+    _parallel(G * T, caller)
+    for m in ms:
+        lib.rlc_flush(m.h)
+    tot = [dict() for _ in range(G)]
+    for (r, t), reqs in per.items():
+        o = oracle.Oracle()
+        o.load_rules(all_rules)
+        for q, ((got, gthr), (d, de, ru, h, tq)) in enumerate(zip(res[(r, t)], reqs)):
+            st, thr = o.submit(hiprl.build_batch([(d, de, [hiprl.NIL_RULE if x is None else x for x in ru], h, tq)]))
+            for k, g in enumerate(got):
+                want = (int(st["code_flags"][k]) & 0xFF, int(st["limit_remaining"][k]), ru[k] is not None,
+                        int(st["reset_s"][k]) if ru[k] is not None else 0)
+                assert (g[0], g[1], bool(g[2]), g[3] if ru[k] is not None else 0) == want, (r, t, q, k)
+                if ru[k] is not None:
+                    tot[r][ru[k]] = tot[r].get(ru[k], 0) + max(1, h)
+            assert gthr == int(thr[0]), (r, t, q)
+    for r in range(G):
+        for k, v in tot[r].items():
+            assert ms[r].stats(ids[r][k])["total_hits"] == v, (r, k)
+    rstats = []
+    for m in ms:
+        o = (C.c_uint64 * 5)()
+        lib.rlc_routed_stats(m.h, o)
+        rstats.append(list(o))
+    assert len({s[0] for s in rstats}) == 1, rstats  # every rank made the same number of steps
+    assert max(s[1] for s in rstats) > 0, rstats      # some rank stepped with an empty batch
+    used = {x for reqs in per.values() for (_, _, ru, _, _) in reqs for x in ru if x is not None}
+    assert all(s[2] >= 2 and s[3] == len(used) for s in rstats), rstats  # one agreed table everywhere
+    assert sum(s[4] for s in rstats) > 0, rstats      # calls waited for a rule agreement
+    _parallel(G, lambda r: lib.rlc_destroy(hs[r]))  # collective: every rank agrees to stop
