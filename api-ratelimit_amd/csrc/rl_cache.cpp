@@ -175,24 +175,49 @@ uint32_t HipRateLimitCache::rule_id(const RateLimitLimit& l, bool shadow) {
   return id;
 }
 
-// The batch being built in one of the engine's pinned staging slots (rl_host_acquire): calls
-// are written straight into C memory, the way the Go batcher does.
+// The batch being built in one of the engine's pinned staging slots (rl_host_acquire_c, or
+// rl_host_acquire for the full format): calls are written straight into C memory, the way the Go
+// batcher does. The compact wire format (rl_batch_c) is the default; a batch
+// whose first call does not fit it goes as rl_batch.
 struct HipRateLimitCache::Staged {
   std::vector<std::shared_ptr<PendingCall>> calls;
-  rl_host_batch hb{};
+  bool compact = true;
+  rl_host_batch hb{};      // full format
+  rl_host_batch_c hc{};    // compact format
   uint32_t nd = 0, nr = 0, nb = 0;
+  uint32_t max_desc = 0, max_req = 0, max_blob = 0;
   int64_t tmin = 0, tmax = 0;
-  bool failed = false;  // refused at submit: its callers already have the error
+  bool one_per_req = true;  // compact: every request so far holds one descriptor (req_of implicit)
+  bool failed = false;      // refused at submit: its callers already have the error
 };
+
+static int64_t compact_base(int64_t first_now) { return first_now > 0 ? first_now - 1 : 0; }
+
+// A call the compact form can carry: prefixes of at most 65535 bytes, hits_addend below 2^24 and
+// rule ids (those it has and those it would be given) below 0xFFFF.
+bool HipRateLimitCache::compactable(const PendingCall& c) const {
+  if (c.req->HitsAddend > 0xFFFFFFu) return false;
+  size_t fresh = 0;
+  for (size_t i = 0; i < c.prefix.size(); ++i) {
+    if (c.prefix[i].size() > 0xFFFFu) return false;
+    const auto& lim = (*c.limits)[i];
+    if (!lim) continue;
+    auto it = rule_ids_.find({lim->Limit.RequestsPerUnit, (uint32_t)lim->Limit.unit | (lim->ShadowMode ? RL_RULE_SHADOW : 0u)});
+    if (it == rule_ids_.end()) ++fresh;
+    else if (it->second >= RL_NIL_RULE16) return false;
+  }
+  return rules_.size() + fresh < RL_NIL_RULE16;
+}
 
 bool HipRateLimitCache::fits(const Staged& st, const PendingCall& c) const {
   if (st.calls.empty()) return true;
+  if (st.compact && !compactable(c)) return false;  // starts a full-format batch
   const int64_t lo = c.now < st.tmin ? c.now : st.tmin, hi = c.now > st.tmax ? c.now : st.tmax;
   // A batch may straddle at most one window boundary of a unit (rl_submit refuses a SECOND key
   // spanning three windows), so it is cut before a request 2 s or more from the others; and
   // before one the slot cannot hold, or past HIP_BATCH_LIMIT descriptors.
-  return hi - lo < 2 && st.nd + c.prefix.size() <= s_.batch_limit && st.nd + c.prefix.size() <= st.hb.max_desc &&
-         st.nr + 1 <= st.hb.max_req && st.nb + c.blob_bytes <= st.hb.max_blob;
+  return hi - lo < 2 && st.nd + c.prefix.size() <= s_.batch_limit && st.nd + c.prefix.size() <= st.max_desc &&
+         st.nr + 1 <= st.max_req && st.nb + c.blob_bytes <= st.max_blob;
 }
 
 // One request into the slot: GenerateCacheKey's bytes before the timestamp per descriptor with
@@ -203,6 +228,24 @@ void HipRateLimitCache::add(Staged& st, const std::shared_ptr<PendingCall>& cp) 
   st.tmin = c.now < st.tmin ? c.now : st.tmin;
   st.tmax = c.now > st.tmax ? c.now : st.tmax;
   const uint32_t r = st.nr++;
+  if (st.compact) {
+    // one word per request: hits_addend | (now - now_base) << 24, now_base = the batch's first
+    // time minus one (the batch spans < 2 s, so the delta is 0..2)
+    const int64_t base = compact_base(st.calls.empty() ? c.now : st.calls[0]->now);
+    st.hc.req_word[r] = c.req->HitsAddend | (uint32_t)(c.now - base) << 24;
+    if (c.prefix.size() != 1) st.one_per_req = false;
+    for (size_t i = 0; i < c.prefix.size(); ++i) {
+      const auto& lim = (*c.limits)[i];
+      memcpy(st.hc.prefix_blob + st.nb, c.prefix[i].data(), c.prefix[i].size());
+      st.nb += (uint32_t)c.prefix[i].size();
+      const uint32_t rid = lim ? rule_id(lim->Limit, lim->ShadowMode) : RL_NIL_RULE16;
+      st.hc.desc_word[st.nd] = (uint32_t)c.prefix[i].size() | rid << 16;
+      st.hc.req_of[st.nd] = r;  // (sent only when some request holds several descriptors)
+      ++st.nd;
+    }
+    st.calls.push_back(cp);
+    return;
+  }
   st.hb.now[r] = c.now;
   st.hb.hits_addend[r] = c.req->HitsAddend;
   st.hb.prefix_off[0] = 0;
@@ -252,7 +295,21 @@ void HipRateLimitCache::submit(Staged& st, std::deque<Staged>& inflight) {
         if (!inflight.empty()) n_loads_inflight_ += 1;
       }
     }
-    if (!rc) {
+    if (!rc && st.compact) {
+      rl_batch_c b;
+      memset(&b, 0, sizeof b);
+      b.n_desc = st.nd;
+      b.n_req = st.nr;
+      b.blob_bytes = st.nb;
+      b.flags = st.one_per_req ? RL_BC_ONE_PER_REQ : 0u;
+      b.now_base = compact_base(st.calls[0]->now);
+      b.prefix_blob = st.hc.prefix_blob;  // the slot's own arrays: rl_submit_c does not copy them
+      b.desc_word = st.hc.desc_word;
+      b.req_word = st.hc.req_word;
+      b.req_of = st.one_per_req ? nullptr : st.hc.req_of;
+      rc = rl_submit_c(eng_, &b);  // raw replies stay in the slot until rl_wait_raw_view
+      if (!rc) n_batches_ += 1, n_compact_ += 1;
+    } else if (!rc) {
       rl_batch b;
       memset(&b, 0, sizeof b);
       b.n_desc = st.nd;
@@ -290,7 +347,30 @@ void HipRateLimitCache::finish(Staged& st) {
   if (st.failed) return;
   const rl_status* out = nullptr;
   const uint32_t* thr = nullptr;
-  if (rl_wait_view(eng_, &out, &thr)) {
+  if (st.compact) {
+    // raw replies (the INCRBY post-values, fixed_cache_impl.go:91-102) -> statuses on the host:
+    // GetResponseDescriptorStatus (base_limiter.go:70-195) by rl_decide_raw
+    const rl_raw_reply* raw = nullptr;
+    rl_batch_c b;
+    memset(&b, 0, sizeof b);
+    b.n_desc = st.nd;
+    b.n_req = st.nr;
+    b.blob_bytes = st.nb;
+    b.flags = st.one_per_req ? RL_BC_ONE_PER_REQ : 0u;
+    b.now_base = compact_base(st.calls[0]->now);
+    b.prefix_blob = st.hc.prefix_blob;
+    b.desc_word = st.hc.desc_word;  // the slot's inputs stay until it is acquired again
+    b.req_word = st.hc.req_word;
+    b.req_of = st.one_per_req ? nullptr : st.hc.req_of;
+    if (dec_out_.size() < st.nd) dec_out_.resize(st.nd);
+    if (dec_thr_.size() < st.nr) dec_thr_.resize(st.nr);
+    if (rl_wait_raw_view(eng_, &raw) || rl_decide_raw(eng_, &b, raw, 0, st.nd, dec_out_.data(), dec_thr_.data())) {
+      fail(st.calls);
+      return;
+    }
+    out = dec_out_.data();
+    thr = dec_thr_.data();
+  } else if (rl_wait_view(eng_, &out, &thr)) {
     fail(st.calls);
     return;
   }
@@ -329,12 +409,16 @@ void HipRateLimitCache::submitter() {
       q_.pop_front();
     }
     Staged st;
-    if (rl_host_acquire(eng_, &st.hb)) {
+    st.compact = compactable(*first);
+    if (st.compact ? rl_host_acquire_c(eng_, &st.hc) : rl_host_acquire(eng_, &st.hb)) {
       std::vector<std::shared_ptr<PendingCall>> one{first};
       fail(one);
       continue;
     }
-    if (first->prefix.size() > st.hb.max_desc || first->blob_bytes > st.hb.max_blob) {
+    st.max_desc = st.compact ? st.hc.max_desc : st.hb.max_desc;
+    st.max_req = st.compact ? st.hc.max_req : st.hb.max_req;
+    st.max_blob = st.compact ? st.hc.max_blob : st.hb.max_blob;
+    if (first->prefix.size() > st.max_desc || first->blob_bytes > st.max_blob) {
       first->done.set_exception(std::make_exception_ptr(RedisError("hip backend: request larger than a batch")));
       done_calls(1);
       continue;

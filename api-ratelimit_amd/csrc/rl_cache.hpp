@@ -169,11 +169,13 @@ class HipRateLimitCache : public RateLimitCache {
   // earlier batch was still in flight (append-only rule table, rl_hip.h rl_load_rules).
   // drains: times the batches in flight were completed early so that a rule-table load or a
   // submit the engine refused with them in flight (RL_ESTATE) could be made.
+  // compact_batches: batches sent in the compact wire format (rl_submit_c); the others went as
+  // rl_batch (a rule id past 0xFFFE, a prefix past 65535 bytes or hits_addend past 2^24 - 1).
   struct BatcherStats {
-    uint64_t batches, rule_loads, rule_loads_in_flight, drains;
+    uint64_t batches, rule_loads, rule_loads_in_flight, drains, compact_batches;
   };
   BatcherStats batcher_stats() const {
-    return {n_batches_.load(), n_loads_.load(), n_loads_inflight_.load(), n_drains_.load()};
+    return {n_batches_.load(), n_loads_.load(), n_loads_inflight_.load(), n_drains_.load(), n_compact_.load()};
   }
 
  private:
@@ -181,6 +183,7 @@ class HipRateLimitCache : public RateLimitCache {
   void submitter();
   uint32_t rule_id(const RateLimitLimit& l, bool shadow);
   bool fits(const Staged& st, const PendingCall& c) const;
+  bool compactable(const PendingCall& c) const;
   void add(Staged& st, const std::shared_ptr<PendingCall>& c);
   void submit(Staged& st, std::deque<Staged>& inflight);
   void finish(Staged& st);
@@ -201,7 +204,10 @@ class HipRateLimitCache : public RateLimitCache {
   std::map<std::pair<uint32_t, uint32_t>, uint32_t> rule_ids_;
   std::vector<rl_rule> rules_;
   bool rules_dirty_ = false;
-  std::atomic<uint64_t> n_batches_{0}, n_loads_{0}, n_loads_inflight_{0}, n_drains_{0};
+  std::atomic<uint64_t> n_batches_{0}, n_loads_{0}, n_loads_inflight_{0}, n_drains_{0}, n_compact_{0};
+  // statuses of a compact batch made on the host from its raw replies (rl_decide_raw)
+  std::vector<rl_status> dec_out_;
+  std::vector<uint32_t> dec_thr_;
 };
 
 // ---- Multi-GPU deployment ------------------------------------------------

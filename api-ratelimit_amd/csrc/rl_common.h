@@ -156,6 +156,48 @@ __host__ __device__ inline uint32_t shadow_code(uint32_t code_flags, uint32_t sh
              : code_flags;
 }
 
+// The decision from the INCRBY reply (after) or a local-cache hit: GetResponseDescriptorStatus
+// + checkOverLimitThreshold + checkNearLimitThreshold + CalculateReset (base_limiter.go:70-195,
+// utilities.go:34-38). Returns the ThrottleMillis contribution (0 = none). Host and device share
+// it: the device decides every status form, the host a compact batch's raw replies (rl_decide_raw).
+__host__ __device__ inline uint32_t decide_status(uint32_t after, bool local_hit, uint32_t h, uint32_t now_mod, const DevRule& R,
+                              rl_status& st) {
+  const uint32_t reset = R.div - now_mod;  // div - now % div
+  st.reset_s = reset;
+  st.over_limit_delta = 0;
+  st.near_limit_delta = 0;
+  uint32_t throttle = 0;
+  if (local_hit) {
+    st.code_flags = RL_CODE_OVER_LIMIT | ((RL_FLAG_HAS_LIMIT | RL_FLAG_LOCAL_CACHE_HIT) << 8);
+    st.limit_remaining = 0;
+    st.over_limit_delta = h;
+  } else {
+    const uint32_t before = after - h;
+    const uint32_t L = R.L, near = R.near;
+    if (after > L) {
+      st.code_flags = RL_CODE_OVER_LIMIT | (RL_FLAG_HAS_LIMIT << 8);
+      st.limit_remaining = 0;
+      if (before >= L) {
+        st.over_limit_delta = h;
+      } else {
+        st.over_limit_delta = after - L;
+        st.near_limit_delta = L - (near > before ? near : before);
+      }
+    } else {
+      st.code_flags = RL_CODE_OK | (RL_FLAG_HAS_LIMIT << 8);
+      st.limit_remaining = L - after;
+      if (after > near) {
+        const uint32_t millis = reset * 1000u;  // uint32(end - now) * 1000
+        const uint32_t calls = (L - after) > 1u ? (L - after) : 1u;
+        throttle = millis / calls;
+        st.near_limit_delta = before >= near ? h : after - near;
+      }
+    }
+  }
+  st.code_flags = shadow_code(st.code_flags, R.shadow);
+  return throttle;
+}
+
 // Device error flags (bitmask in EngineCtl.err).
 enum : uint32_t {
   ERR_TABLE_FULL = 1u,    // a region would pass its load limit: refused before any table write
@@ -332,7 +374,7 @@ constexpr uint8_t ROUTE_LOCAL = 0xFF;  // descriptor decided at the origin (nil 
 // rl_batch.reserved bit: prefix_blob holds RRec records (rl_submit_routed), n_req = n_desc and
 // every record has its own ThrottleMillis slot.
 constexpr uint32_t RL_BATCH_ROUTED = 1u;
-constexpr uint32_t RL_BATCH_RAW = 2u;  // with RL_BATCH_ROUTED: raw replies (RawReply) instead of statuses
+constexpr uint32_t RL_BATCH_RAW = 2u;  // raw replies (RawReply per descriptor / record) instead of statuses
 
 // MSD descriptor record (32 B): tile-sorted (k4_hist) and in bucket order (k4_place,
 // grouped by k4_group). A hot record carries its in-tile INCRBY prefix in `key` and its hot

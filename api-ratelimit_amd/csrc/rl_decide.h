@@ -358,46 +358,7 @@ RL_DEV void emit_raw(rl_status* __restrict__ out, uint32_t idx, uint32_t after, 
   reinterpret_cast<RawReply*>(out)[idx] = r;
 }
 
-// The decision from the INCRBY reply (after) or a local-cache hit: GetResponseDescriptorStatus
-// + checkOverLimitThreshold + checkNearLimitThreshold + CalculateReset (base_limiter.go:70-195,
-// utilities.go:34-38). Returns the ThrottleMillis contribution (0 = none).
-RL_DEV uint32_t decide_status(uint32_t after, bool local_hit, uint32_t h, uint32_t now_mod, const DevRule& R,
-                              rl_status& st) {
-  const uint32_t reset = R.div - now_mod;  // div - now % div
-  st.reset_s = reset;
-  st.over_limit_delta = 0;
-  st.near_limit_delta = 0;
-  uint32_t throttle = 0;
-  if (local_hit) {
-    st.code_flags = RL_CODE_OVER_LIMIT | ((RL_FLAG_HAS_LIMIT | RL_FLAG_LOCAL_CACHE_HIT) << 8);
-    st.limit_remaining = 0;
-    st.over_limit_delta = h;
-  } else {
-    const uint32_t before = after - h;
-    const uint32_t L = R.L, near = R.near;
-    if (after > L) {
-      st.code_flags = RL_CODE_OVER_LIMIT | (RL_FLAG_HAS_LIMIT << 8);
-      st.limit_remaining = 0;
-      if (before >= L) {
-        st.over_limit_delta = h;
-      } else {
-        st.over_limit_delta = after - L;
-        st.near_limit_delta = L - (near > before ? near : before);
-      }
-    } else {
-      st.code_flags = RL_CODE_OK | (RL_FLAG_HAS_LIMIT << 8);
-      st.limit_remaining = L - after;
-      if (after > near) {
-        const uint32_t millis = reset * 1000u;  // uint32(end - now) * 1000
-        const uint32_t calls = (L - after) > 1u ? (L - after) : 1u;
-        throttle = millis / calls;
-        st.near_limit_delta = before >= near ? h : after - near;
-      }
-    }
-  }
-  st.code_flags = shadow_code(st.code_flags, R.shadow);
-  return throttle;
-}
+// decide_status (rl_common.h): the decision from the INCRBY reply, on the device and the host.
 
 // One descriptor of a segment: its post-value from the segment's state, then the decision
 // (or the raw reply). thr_idx: the ThrottleMillis slot (the request; a routed record's own

@@ -33,7 +33,8 @@ constexpr uint32_t SPIN_LIMIT = 1u << 24;
 // k_fingerprint
 // ---------------------------------------------------------------------------
 struct DevBatch {
-  uint32_t n_desc, n_req, blob_bytes, pad;
+  uint32_t n_desc, n_req, blob_bytes;
+  uint32_t raw;  // 1: decisions leave as raw replies (RawReply per descriptor), no ThrottleMillis
   const uint8_t* blob;
   const uint32_t* off;
   const uint32_t* rule;
@@ -47,7 +48,7 @@ inline DevBatch make_dev_batch(const rl_batch& b) {
   d.n_desc = b.n_desc;
   d.n_req = b.n_req;
   d.blob_bytes = b.blob_bytes;
-  d.pad = 0;
+  d.raw = (b.reserved & RL_BATCH_RAW) ? 1u : 0u;
   d.blob = b.prefix_blob;
   d.off = b.prefix_off;
   d.rule = b.rule_id;

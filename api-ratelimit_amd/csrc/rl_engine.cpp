@@ -53,6 +53,9 @@ void launch_route_reply(hipStream_t, uint32_t, const rl_status*, const uint32_t*
 hipError_t route_set_spin_limit(uint32_t v);
 void launch_route_unpack(hipStream_t, uint32_t, const uint32_t*, const uint32_t*, const RReply*, rl_status*,
                          uint32_t*);
+uint32_t compact_chunks(uint32_t n);
+void launch_compact_expand(hipStream_t, uint32_t, uint32_t, int64_t, const uint32_t*, const uint32_t*, const uint32_t*,
+                           uint32_t*, uint32_t*, uint32_t*, uint32_t*, int64_t*, uint32_t*);
 uint32_t v4_tiles(uint32_t n);
 uint32_t v4_group_blocks(uint32_t n);
 uint32_t v4_scan_blocks();
@@ -142,9 +145,12 @@ struct rl_engine {
     uint32_t* d_thr = nullptr;
     rl_status* h_out = nullptr;
     uint32_t* h_thr = nullptr;
+    uint8_t* d_cin = nullptr;   // compact batches: device copies of the desc / req words and req_of
+    uint32_t* d_csum = nullptr; // compact batches: per-chunk prefix-length sums
   };
   Stage stage[HSLOTS];
   size_t in_bytes = 0, o_off = 0, o_rule = 0, o_req = 0, o_now = 0, o_hits = 0;
+  size_t c_pitch = 0;  // compact layout: rows desc_word | req_word | req_of at this pitch from o_off (host), 0 (device)
 
   // LSD pipeline scratch
   uint64_t *keys_orig = nullptr, *keys_a = nullptr, *keys_b = nullptr;
@@ -232,6 +238,7 @@ struct rl_engine {
     bool settled = false;          // reruns done
     bool fell_back = false;
     bool host = false;             // host batch: results D2H into the slot's pinned outputs
+    bool raw = false;              // raw replies (compact host batch): RawReply per descriptor, no ThrottleMillis
     uint32_t errs = 0;
     rl_status* user_out = nullptr; // host batch: rl_wait copies here (may be null)
     uint32_t* user_thr = nullptr;
@@ -306,7 +313,7 @@ struct rl_engine {
   int enqueue_d2h(const Flight& f, hipStream_t s);
   int check_batch(const rl_batch* b, bool host);
   int submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, RReply* reply, hipEvent_t in_ev,
-                    bool inputs_ready, bool host, rl_status* user_out, uint32_t* user_thr);
+                    bool inputs_ready, bool host, rl_status* user_out, uint32_t* user_thr, bool raw = false);
   void occ_host_update(const EngineCtl* c) {
     for (int r = 0; r < 8; ++r) occ_advance(occ[r], (uint32_t)r, c->gen_max[r], c->ins[r]);
   }
@@ -339,7 +346,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   uint64_t* lb_head = reinterpret_cast<uint64_t*>(zero_block + z.lb_head);
   const size_t lb_pass_stride = (size_t)sort_tiles(n > 0 ? n : 1) * RADIX;  // per-digit look-back words
   // how decisions are written (rl_common.h OUT_*): statuses, routed statuses, raw replies
-  const int routed = (b.reserved & RL_BATCH_ROUTED) ? ((b.reserved & RL_BATCH_RAW) ? OUT_RAW : OUT_ROUTED) : OUT_STATUS;
+  const int routed = (b.reserved & RL_BATCH_RAW) ? OUT_RAW : (b.reserved & RL_BATCH_ROUTED) ? OUT_ROUTED : OUT_STATUS;
   hipError_t e;
   if (mode == MODE_V4) {
     const uint32_t sl = (uint32_t)(sub_seq & 1u);
@@ -581,6 +588,11 @@ void rl_engine::update_hot(const HotCand* cand, uint32_t n_cand) {
 int rl_engine::enqueue_d2h(const Flight& f, hipStream_t s) {
   hipError_t e;
   const Stage& g = stage[f.slot];
+  if (f.raw) {  // 8-B raw replies, no ThrottleMillis
+    e = f.b.n_desc ? hipMemcpyAsync(g.h_out, f.out, (size_t)f.b.n_desc * sizeof(RawReply), hipMemcpyDeviceToHost, s)
+                   : hipSuccess;
+    return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpyAsync(D2H raw)");
+  }
   if (f.b.n_desc) {
     e = hipMemcpyAsync(g.h_out, f.out, (size_t)f.b.n_desc * sizeof(rl_status), hipMemcpyDeviceToHost, s);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(D2H out)");
@@ -708,7 +720,9 @@ int rl_engine::finish(rl_status* out_into, uint32_t* thr_into, bool into) {
   st.inserted_keys += h_ctl->n_inserted;
   st.live_keys = live_total();
   want_cand = hot.empty() || (st.batches & 7) == 0;
-  if (f.host) {
+  if (f.host && f.raw) {
+    if (into && out_into && f.b.n_desc) memcpy(out_into, stage[f.slot].h_out, (size_t)f.b.n_desc * sizeof(RawReply));
+  } else if (f.host) {
     rl_status* o = into ? out_into : f.user_out;
     uint32_t* t = into ? thr_into : f.user_thr;
     const Stage& g = stage[f.slot];
@@ -738,7 +752,7 @@ int rl_engine::check_batch(const rl_batch* b, bool host) {
 // Common tail of every submit form: run the pipeline behind what is in flight, record the
 // completion point, queue the flight.
 int rl_engine::submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, RReply* reply, hipEvent_t in_ev,
-                             bool inputs_ready, bool host, rl_status* user_out, uint32_t* user_thr) {
+                             bool inputs_ready, bool host, rl_status* user_out, uint32_t* user_thr, bool raw) {
   const uint32_t s = (uint32_t)(sub_seq % HSLOTS);
   h_ctl = h_ctl_s[s];
   h_cand = h_cand_s[s];
@@ -756,6 +770,7 @@ int rl_engine::submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, R
   f.host = host;
   f.user_out = user_out;
   f.user_thr = user_thr;
+  f.raw = raw;
   hipError_t e;
   if (host) {
     // outputs leave on the copy-out stream while the next batch's kernels run
@@ -882,7 +897,12 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   e->o_now = e->o_req + align_up((N + 1) * 4, 256);
   e->o_hits = e->o_now + align_up(R * 8, 256);
   e->in_bytes = e->o_hits + align_up(R * 4, 256);
+  // compact layout (rl_batch_c): blob, then three rows (desc words, req words, req_of)
+  e->c_pitch = align_up((std::max(N, R) + 1) * 4, 256);
+  e->in_bytes = std::max(e->in_bytes, e->o_off + 3 * e->c_pitch);
   for (auto& g : e->stage) {
+    chk(hipMalloc(&g.d_cin, 3 * e->c_pitch));
+    chk(hipMalloc(&g.d_csum, (size_t)compact_chunks((uint32_t)N) * 4 + 64));
     chk(hipMalloc(&g.d_in, e->in_bytes));
     chk(hipHostMalloc(&g.h_in, e->in_bytes, hipHostMallocDefault));
     chk(hipMalloc(&g.d_out, N * sizeof(rl_status) + 64));
@@ -987,6 +1007,8 @@ void rl_destroy(rl_engine* e) {
     hipHostFree(e->h_ctl_s[k]);
   }
   for (auto& g : e->stage) {
+    hipFree(g.d_cin);
+    hipFree(g.d_csum);
     hipFree(g.d_in);
     hipHostFree(g.h_in);
     hipFree(g.d_out);
@@ -1162,6 +1184,7 @@ int rl_query(rl_engine* e) {
 int rl_wait_into(rl_engine* e, rl_status* out, uint32_t* req_throttle_ms) {
   if (!e) return RL_EINVAL;
   if (!e->n_fl) return e->fail(RL_ESTATE, "rl_wait_into without a batch in flight");
+  if (e->fl[0].raw) return e->fail(RL_ESTATE, "rl_wait_into: the oldest batch is compact (rl_wait_raw_into)");
   return e->finish(out, req_throttle_ms, true);
 }
 
@@ -1171,13 +1194,177 @@ int rl_wait_view(rl_engine* e, const rl_status** out, const uint32_t** req_throt
   *req_throttle_ms = nullptr;
   if (!e->n_fl) return e->fail(RL_ESTATE, "rl_wait_view without a batch in flight");
   const rl_engine::Flight& f = e->fl[0];
-  if (!f.host || f.user_out || f.user_thr)
+  if (!f.host || f.raw || f.user_out || f.user_thr)
     return e->fail(RL_ESTATE, "rl_wait_view: the oldest batch is not a host batch submitted without output pointers");
   const uint32_t s = f.slot;
   int rc = e->finish(nullptr, nullptr, true);  // (into, with no targets: no copy)
   if (rc) return rc;
   *out = e->stage[s].h_out;
   *req_throttle_ms = e->stage[s].h_thr;
+  return 0;
+}
+
+// ---- compact host batches (rl_batch_c) ----------------------------------------------------
+
+int rl_host_acquire_c(rl_engine* e, rl_host_batch_c* out) {
+  if (!e || !out) return RL_EINVAL;
+  if (e->n_fl >= HSLOTS) return e->fail(RL_ESTATE, "rl_host_acquire_c with %d batches in flight (call rl_wait)", HSLOTS);
+  const int s = (int)(e->sub_seq % HSLOTS);
+  uint8_t* h = e->stage[s].h_in;
+  out->prefix_blob = h;
+  out->desc_word = reinterpret_cast<uint32_t*>(h + e->o_off);
+  out->req_word = reinterpret_cast<uint32_t*>(h + e->o_off + e->c_pitch);
+  out->req_of = reinterpret_cast<uint32_t*>(h + e->o_off + 2 * e->c_pitch);
+  out->max_desc = e->cfg.max_batch_desc;
+  out->max_req = e->cfg.max_batch_req;
+  out->max_blob = e->cfg.max_blob_bytes;
+  out->reserved = 0;
+  e->acquired = s;
+  return 0;
+}
+
+int rl_submit_c(rl_engine* e, const rl_batch_c* b) {
+  if (!e || !b) return RL_EINVAL;
+  if (e->n_fl >= HSLOTS) return e->fail(RL_ESTATE, "rl_submit_c with %d batches in flight (call rl_wait)", HSLOTS);
+  if (b->n_desc > e->cfg.max_batch_desc || b->n_req > e->cfg.max_batch_req || b->blob_bytes > e->cfg.max_blob_bytes)
+    return e->fail(RL_ECAPACITY, "batch exceeds engine capacity (%u desc, %u req, %u blob bytes)",
+                   e->cfg.max_batch_desc, e->cfg.max_batch_req, e->cfg.max_blob_bytes);
+  if (b->flags & ~(uint32_t)RL_BC_ONE_PER_REQ) return e->fail(RL_EINVAL, "unknown rl_batch_c flags 0x%x", b->flags);
+  const bool one = (b->flags & RL_BC_ONE_PER_REQ) != 0;
+  if (one && b->n_desc != b->n_req) return e->fail(RL_EINVAL, "RL_BC_ONE_PER_REQ needs n_desc == n_req");
+  if (b->n_desc && (!b->desc_word || (!one && !b->req_of))) return e->fail(RL_EINVAL, "null descriptor array");
+  if (b->n_req && !b->req_word) return e->fail(RL_EINVAL, "null request array");
+  if (b->n_desc && !b->n_req) return e->fail(RL_EINVAL, "descriptors without requests");
+  if (b->blob_bytes && !b->prefix_blob) return e->fail(RL_EINVAL, "null prefix_blob");
+  if (b->now_base < 0 || b->now_base > MAX_NOW) return e->fail(RL_EINVAL, "now_base outside [0, 0xFFFD0000]");
+  if (e->n_fl && e->default_mode() != MODE_V4)
+    return e->fail(RL_ESTATE, "a second batch in flight needs the v4 pipeline (call rl_wait)");
+  if (!e->d_rules) {
+    int rc = rl_load_rules(e, nullptr, 0);
+    if (rc) return rc;
+  }
+  const uint32_t s = (uint32_t)(e->sub_seq % HSLOTS);
+  rl_engine::Stage& g = e->stage[s];
+  uint8_t* h = g.h_in;
+  const size_t P = e->c_pitch;
+  struct Arr { const void* src; size_t o, n; } arrs[] = {
+      {b->prefix_blob, 0, b->blob_bytes}, {b->desc_word, e->o_off, (size_t)b->n_desc * 4},
+      {b->req_word, e->o_off + P, (size_t)b->n_req * 4}, {one ? nullptr : b->req_of, e->o_off + 2 * P, one ? 0 : (size_t)b->n_desc * 4}};
+  for (auto& a : arrs)
+    if (a.n && a.src != h + a.o) memcpy(h + a.o, a.src, a.n);
+  memset(h + b->blob_bytes, 0, RL_BLOB_SLACK);  // the device reads prefixes in 16-B words
+  e->acquired = -1;
+  // Two copies at one descriptor per request: the blob, and the desc and req words as one
+  // 2-D copy (rows P apart); req_of, when present, is a third.
+  hipError_t he = hipMemcpyAsync(g.d_in, h, (size_t)b->blob_bytes + RL_BLOB_SLACK, hipMemcpyHostToDevice, e->xin);
+  const size_t w = (size_t)std::max(b->n_desc, b->n_req) * 4;
+  if (he == hipSuccess && w) he = hipMemcpy2DAsync(g.d_cin, P, h + e->o_off, P, w, 2, hipMemcpyHostToDevice, e->xin);
+  if (he == hipSuccess && arrs[3].n)
+    he = hipMemcpyAsync(g.d_cin + 2 * P, h + e->o_off + 2 * P, arrs[3].n, hipMemcpyHostToDevice, e->xin);
+  if (he != hipSuccess) return e->hip_fail(he, "hipMemcpyAsync(H2D compact)");
+  // the rl_batch arrays, expanded on the device behind the copies
+  uint32_t* d_off = reinterpret_cast<uint32_t*>(g.d_in + e->o_off);
+  uint32_t* d_rule = reinterpret_cast<uint32_t*>(g.d_in + e->o_rule);
+  uint32_t* d_req = reinterpret_cast<uint32_t*>(g.d_in + e->o_req);
+  int64_t* d_now = reinterpret_cast<int64_t*>(g.d_in + e->o_now);
+  uint32_t* d_hits = reinterpret_cast<uint32_t*>(g.d_in + e->o_hits);
+  if (b->n_desc || b->n_req)
+    launch_compact_expand(e->xin, b->n_desc, b->n_req, b->now_base, reinterpret_cast<const uint32_t*>(g.d_cin),
+                          reinterpret_cast<const uint32_t*>(g.d_cin + P),
+                          one ? nullptr : reinterpret_cast<const uint32_t*>(g.d_cin + 2 * P), g.d_csum, d_off, d_rule,
+                          d_req, d_now, d_hits);
+  he = hipGetLastError();
+  if (he == hipSuccess) he = hipEventRecord(e->ev_in[s], e->xin);
+  if (he != hipSuccess) return e->hip_fail(he, "compact expand");
+  rl_batch d{};
+  d.n_desc = b->n_desc;
+  d.n_req = b->n_req;
+  d.blob_bytes = b->blob_bytes;
+  d.reserved = RL_BATCH_RAW;
+  d.prefix_blob = g.d_in;
+  d.prefix_off = d_off;
+  d.rule_id = d_rule;
+  d.req_of = d_req;
+  d.now = d_now;
+  d.hits_addend = d_hits;
+  e->st.host_batches += 1;
+  // raw replies land in the slot's device output array (8 B of its 20 per descriptor)
+  return e->submit_common(d, g.d_out, nullptr, nullptr, e->ev_in[s], false, true, nullptr, nullptr, true);
+}
+
+int rl_wait_raw_view(rl_engine* e, const rl_raw_reply** out) {
+  if (!e || !out) return RL_EINVAL;
+  *out = nullptr;
+  if (!e->n_fl) return e->fail(RL_ESTATE, "rl_wait_raw_view without a batch in flight");
+  if (!e->fl[0].raw) return e->fail(RL_ESTATE, "rl_wait_raw_view: the oldest batch is not a compact host batch");
+  const uint32_t s = e->fl[0].slot;
+  int rc = e->finish(nullptr, nullptr, true);
+  if (rc) return rc;
+  *out = reinterpret_cast<const rl_raw_reply*>(e->stage[s].h_out);
+  return 0;
+}
+
+int rl_wait_raw_into(rl_engine* e, rl_raw_reply* out) {
+  if (!e) return RL_EINVAL;
+  if (!e->n_fl) return e->fail(RL_ESTATE, "rl_wait_raw_into without a batch in flight");
+  if (!e->fl[0].raw) return e->fail(RL_ESTATE, "rl_wait_raw_into: the oldest batch is not a compact host batch");
+  return e->finish(reinterpret_cast<rl_status*>(out), nullptr, true);
+}
+
+// GetResponseDescriptorStatus per descriptor from its INCRBY reply (base_limiter.go:70-195),
+// with the rules the device decided with (their near thresholds computed as Go does) and the
+// decision code the device runs (decide_status, rl_common.h).
+int rl_decide_raw(rl_engine* e, const rl_batch_c* b, const rl_raw_reply* raw, uint32_t d0, uint32_t d1,
+                  rl_status* out, uint32_t* thr) {
+  if (!e || !b || d0 > d1 || d1 > b->n_desc) return RL_EINVAL;
+  if (d0 == d1) return 0;
+  if (!raw || !out || !thr || !b->desc_word || !b->req_word) return RL_EINVAL;
+  const bool one = (b->flags & RL_BC_ONE_PER_REQ) != 0;
+  if (!one && !b->req_of) return RL_EINVAL;
+  const DevRule* rules = e->h_rules.data();
+  const uint32_t n_rules = e->n_rules;
+  static_assert(sizeof(rl_raw_reply) == sizeof(RawReply), "raw reply layout");
+  // Requests are written once all their descriptors lie in [d0, d1): a request that begins
+  // before d0 or ends at or past d1 is left to the call that holds its other descriptors.
+  // Requests without descriptors get 0 (the device zeroes every request's ThrottleMillis).
+  auto req_at = [&](uint32_t i) { return one ? i : b->req_of[i]; };
+  const uint32_t r_first = req_at(d0), r_last = req_at(d1 - 1);
+  const bool first_whole = d0 == 0 || req_at(d0 - 1) != r_first;
+  const bool last_whole = d1 == b->n_desc || req_at(d1) != r_last;
+  if (d0 == 0)
+    for (uint32_t q = 0; q < r_first; ++q) thr[q] = 0;
+  if (d1 == b->n_desc)
+    for (uint32_t q = r_last + 1; q < b->n_req; ++q) thr[q] = 0;
+  uint32_t cur_req = r_first, cur_thr = 0;
+  auto flush = [&](uint32_t next) {
+    if ((cur_req != r_first || first_whole) && (cur_req != r_last || last_whole)) thr[cur_req] = cur_thr;
+    for (uint32_t q = cur_req + 1; q < next; ++q) thr[q] = 0;  // requests without descriptors
+  };
+  for (uint32_t i = d0; i < d1; ++i) {
+    const uint32_t r = req_at(i);
+    if (r != cur_req) {
+      flush(r);
+      cur_req = r;
+      cur_thr = 0;
+    }
+    const uint32_t rw = b->req_word[r];
+    const uint32_t rule = b->desc_word[i] >> 16;
+    rl_status& st = out[i];
+    if (rule == RL_NIL_RULE16 || (raw[i].flags & RL_RAW_NIL)) {  // base_limiter.go:72-75
+      st.code_flags = RL_CODE_OK;
+      st.limit_remaining = st.reset_s = st.over_limit_delta = st.near_limit_delta = 0;
+      continue;
+    }
+    if (rule >= n_rules) return e->fail(RL_EINVAL, "rl_decide_raw: descriptor %u has rule %u of %u", i, rule, n_rules);
+    const DevRule& R = rules[rule];
+    const uint64_t now = (uint64_t)(b->now_base + (int64_t)(rw >> 24));
+    const uint32_t hh = rw & 0xFFFFFFu;
+    const uint32_t h = hh > 1u ? hh : 1u;  // utils.Max(1, HitsAddend)  fixed_cache_impl.go:39
+    const uint32_t now_mod = (uint32_t)(now % R.div);
+    const uint32_t t = decide_status(raw[i].after, (raw[i].flags & RL_RAW_LOCAL_HIT) != 0u, h, now_mod, R, st);
+    cur_thr = t > cur_thr ? t : cur_thr;  // response.ThrottleMillis = max  base_limiter.go:163-165
+  }
+  flush(cur_req + 1);
   return 0;
 }
 

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
     const uint32_t ha = q_ok ? in.hits[q] : 1u;
     // Zero DoLimitResponse.ThrottleMillis of the requests this descriptor opens
     // (k_decide max-reduces into it); the last descriptor also zeroes trailing requests.
-    if (q_ok) {
+    if (q_ok && req_thr) {  // (raw replies: no ThrottleMillis slots)
       const uint32_t pq = i == 0 ? 0u : in.req_of[i - 1];
       const uint32_t first = i == 0 ? 0u : (pq < q ? pq + 1u : q + 1u);
       for (uint32_t rr = first; rr <= q; ++rr) req_thr[rr] = 0;
@@ -132,7 +132,9 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
     }
     recs[i] = rec;
     keys_orig[i] = key;
-    if (nil) {
+    if (nil && in.raw) {
+      emit_raw(out, i, 0u, RAW_NIL);
+    } else if (nil) {
       // GetResponseDescriptorStatus("" key) -> {OK, nil limit, 0}  base_limiter.go:72-75
       rl_status st;
       st.code_flags = RL_CODE_OK;

@@ -357,7 +357,7 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
       const D3& x = d[r];
       if (x.bucket == BKT_NONE || spos[r] - h0 >= STAGE) continue;
       if (x.bucket == NIL_BUCKET) {
-        if (ROUTED && !req_thr) {  // raw replies (a routed batch never carries a nil limit)
+        if (in.raw) {  // raw replies (a routed batch never carries a nil limit)
           emit_raw(out, i, 0u, RAW_NIL);
           continue;
         }
@@ -1236,7 +1236,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
     }
     __syncthreads();
   }
-  const uint32_t q0 = routed ? in.recs[t0].greq : in.req_of[t0];  // request of the tile's first descriptor
+  const uint32_t q0 = in.recs ? in.recs[t0].greq : in.req_of[t0];  // request of the tile's first descriptor
   for (uint32_t p = tid; p < nhot; p += NT) {
     const MRec a = src[p];
     const uint32_t b = (uint32_t)a.fp_lo;

@@ -40,7 +40,7 @@ STATUS_DTYPE = np.dtype([("code_flags", "<u4"), ("limit_remaining", "<u4"), ("re
 
 
 PIPELINE_FLAGS = {"v4": 0, "lsd": 1}  # rl_config.flags (RL_CFG_LSD_ONLY)
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class RlConfig(C.Structure):
@@ -92,6 +92,25 @@ class RlHostBatch(C.Structure):
                 ("max_desc", C.c_uint32), ("max_req", C.c_uint32), ("max_blob", C.c_uint32), ("reserved", C.c_uint32)]
 
 
+class RlBatchC(C.Structure):
+    """rl_batch_c: the compact host wire format (rl_hip.h)."""
+    _fields_ = [("n_desc", C.c_uint32), ("n_req", C.c_uint32), ("blob_bytes", C.c_uint32), ("flags", C.c_uint32),
+                ("now_base", C.c_int64), ("prefix_blob", C.c_void_p), ("desc_word", C.c_void_p),
+                ("req_word", C.c_void_p), ("req_of", C.c_void_p)]
+
+
+class RlHostBatchC(C.Structure):
+    _fields_ = [("prefix_blob", C.c_void_p), ("desc_word", C.c_void_p), ("req_word", C.c_void_p),
+                ("req_of", C.c_void_p), ("max_desc", C.c_uint32), ("max_req", C.c_uint32), ("max_blob", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+BC_ONE_PER_REQ = 1   # RL_BC_ONE_PER_REQ
+NIL_RULE16 = 0xFFFF  # RL_NIL_RULE16
+RAW_LOCAL_HIT, RAW_NIL = 1, 2  # rl_raw_reply.flags
+RAW_DTYPE = np.dtype([("after", "<u4"), ("flags", "<u4")])
+
+
 # (name, argtypes, restype) of every symbol include/rl_hip.h declares
 class RlRouterConfig(C.Structure):
     _fields_ = [("struct_size", C.c_uint32), ("n_shards", C.c_uint32), ("rank", C.c_uint32), ("max_desc", C.c_uint32),
@@ -124,6 +143,12 @@ ABI = [
     ("rl_query", [C.c_void_p], C.c_int),
     ("rl_wait_into", [C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     ("rl_wait_view", [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
+    ("rl_host_acquire_c", [C.c_void_p, C.POINTER(RlHostBatchC)], C.c_int),
+    ("rl_submit_c", [C.c_void_p, C.POINTER(RlBatchC)], C.c_int),
+    ("rl_wait_raw_view", [C.c_void_p, C.POINTER(C.c_void_p)], C.c_int),
+    ("rl_wait_raw_into", [C.c_void_p, C.c_void_p], C.c_int),
+    ("rl_decide_raw", [C.c_void_p, C.POINTER(RlBatchC), C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p],
+     C.c_int),
     ("rl_submit_device", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
     ("rl_submit_pipelined", [C.c_void_p, C.POINTER(RlBatch), C.c_void_p, C.c_void_p], C.c_int),
     ("rl_stream", [C.c_void_p], C.c_void_p),
@@ -265,6 +290,66 @@ def _ptr(a: np.ndarray) -> int:
     return a.ctypes.data if a.size else 0
 
 
+@dataclass
+class CompactBatch:
+    """A Batch in the compact host wire format (rl_batch_c): prefix bytes back to back, one word
+    per descriptor (prefix length | rule id << 16), one per request (hits_addend | (now -
+    now_base) << 24), req_of only when some request holds several descriptors."""
+    blob: np.ndarray       # uint8
+    desc_word: np.ndarray  # uint32 [n_desc]
+    req_word: np.ndarray   # uint32 [n_req]
+    req_of: Optional[np.ndarray]  # uint32 [n_desc] or None (one descriptor per request)
+    now_base: int
+
+    @property
+    def n_desc(self) -> int:
+        return int(self.desc_word.shape[0])
+
+    @property
+    def n_req(self) -> int:
+        return int(self.req_word.shape[0])
+
+    @property
+    def flags(self) -> int:
+        return BC_ONE_PER_REQ if self.req_of is None else 0
+
+    def struct(self) -> RlBatchC:
+        s = RlBatchC()
+        s.n_desc, s.n_req, s.blob_bytes, s.flags, s.now_base = (self.n_desc, self.n_req, int(self.blob.shape[0]),
+                                                                self.flags, self.now_base)
+        s.prefix_blob, s.desc_word, s.req_word = _ptr(self.blob), _ptr(self.desc_word), _ptr(self.req_word)
+        s.req_of = 0 if self.req_of is None else _ptr(self.req_of)
+        return s
+
+    def wire_bytes(self) -> int:
+        """Bytes this batch moves host -> device (rl_submit_c's copies, without the blob slack)."""
+        return int(self.blob.shape[0]) + 4 * self.n_desc + 4 * self.n_req + (0 if self.req_of is None else 4 * self.n_desc)
+
+
+def compact_batch(b: Batch) -> CompactBatch:
+    """Batch -> CompactBatch. Raises ValueError when the batch does not fit the compact form
+    (rule id >= 0xFFFF, a prefix over 65535 bytes, hits_addend >= 2^24, times spanning > 255 s)."""
+    lens = np.diff(b.off.astype(np.int64))
+    if b.n_desc and (lens.max() > 0xFFFF or lens.min() < 0):
+        raise ValueError("prefix length outside [0, 65535]")
+    nil = b.rule == NIL_RULE
+    if np.any(~nil & (b.rule >= NIL_RULE16)):
+        raise ValueError("rule id >= 0xFFFF")
+    # prefixes back to back: the compact form has no offsets, so the blob is rebuilt in order
+    if b.n_desc and not (b.off[0] == 0 and b.off[-1] == b.blob.shape[0]):
+        blob = np.concatenate([b.blob[b.off[i]:b.off[i + 1]] for i in range(b.n_desc)]).astype(np.uint8)
+    else:
+        blob = b.blob.copy()
+    dw = (lens.astype(np.uint32) | (np.where(nil, NIL_RULE16, b.rule).astype(np.uint32) << 16)).astype(np.uint32)
+    base = int(b.now.min()) if b.n_req else 0
+    delta = b.now - base
+    if b.n_req and (delta.max() > 255 or np.any(b.hits >= (1 << 24))):
+        raise ValueError("request times span more than 255 s or hits_addend >= 2^24")
+    rw = ((b.hits.astype(np.uint32) & 0xFFFFFF) | (delta.astype(np.uint32) << 24)).astype(np.uint32)
+    one = b.n_desc == b.n_req and np.array_equal(b.req_of, np.arange(b.n_desc, dtype=np.uint32))
+    return CompactBatch(blob, dw, rw, None if one else b.req_of.copy(), base)
+
+
 def _batch_struct(b: Batch, ptrs=None) -> RlBatch:
     s = RlBatch()
     s.n_desc, s.n_req, s.blob_bytes, s.reserved = b.n_desc, b.n_req, int(b.blob.shape[0]), 0
@@ -394,6 +479,71 @@ class Engine:
         s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = (
             staged[k].ctypes.data for k in ("blob", "off", "rule", "req_of", "now", "hits"))
         self._check(self.lib.rl_submit(self.h, C.byref(s), None, None), "rl_submit")
+
+    # ---- compact host batches (rl_batch_c, raw replies) ----
+    def submit_c(self, cb: CompactBatch):
+        """rl_submit_c of a compact host batch (copied into the staging slot)."""
+        s = cb.struct()
+        self._check(self.lib.rl_submit_c(self.h, C.byref(s)), "rl_submit_c")
+
+    def host_acquire_c(self) -> dict:
+        """rl_host_acquire_c: numpy views of the next free slot in the compact layout (built once
+        per slot)."""
+        hb = RlHostBatchC()
+        self._check(self.lib.rl_host_acquire_c(self.h, C.byref(hb)), "rl_host_acquire_c")
+        cache = self.__dict__.setdefault("_slot_views_c", {})
+        got = cache.get(hb.prefix_blob)
+        if got is not None:
+            return got
+
+        def view(ptr, n, dt):
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(n,))
+        got = dict(blob=view(hb.prefix_blob, hb.max_blob, np.uint8), desc_word=view(hb.desc_word, hb.max_desc, np.uint32),
+                   req_word=view(hb.req_word, hb.max_req, np.uint32), req_of=view(hb.req_of, hb.max_desc, np.uint32))
+        cache[hb.prefix_blob] = got
+        return got
+
+    def submit_c_staged(self, n_desc: int, n_req: int, blob_bytes: int, now_base: int, staged: dict,
+                        one_per_req: bool = True):
+        """rl_submit_c of a compact batch built in place in an acquired slot (no host copy)."""
+        s = RlBatchC()
+        s.n_desc, s.n_req, s.blob_bytes, s.now_base = n_desc, n_req, blob_bytes, now_base
+        s.flags = BC_ONE_PER_REQ if one_per_req else 0
+        s.prefix_blob, s.desc_word, s.req_word = (staged[k].ctypes.data for k in ("blob", "desc_word", "req_word"))
+        s.req_of = 0 if one_per_req else staged["req_of"].ctypes.data
+        self._check(self.lib.rl_submit_c(self.h, C.byref(s)), "rl_submit_c")
+
+    def wait_raw_view(self, n_desc: int) -> np.ndarray:
+        """rl_wait_raw_view: the oldest compact batch's raw replies in the slot (RAW_DTYPE view)."""
+        p = C.c_void_p()
+        self._check(self.lib.rl_wait_raw_view(self.h, C.byref(p)), "rl_wait_raw_view")
+        if not n_desc:
+            return np.zeros(0, RAW_DTYPE)
+        return np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), shape=(n_desc * 8,)).view(RAW_DTYPE)
+
+    def wait_raw_into(self, n_desc: int) -> np.ndarray:
+        out = np.zeros(n_desc, RAW_DTYPE)
+        self._check(self.lib.rl_wait_raw_into(self.h, _ptr(out) or None), "rl_wait_raw_into")
+        return out
+
+    def decide_raw(self, cb: CompactBatch, raw: np.ndarray, d0: int = 0, d1: Optional[int] = None,
+                   out: Optional[np.ndarray] = None, thr: Optional[np.ndarray] = None):
+        """rl_decide_raw: statuses and ThrottleMillis of descriptors [d0, d1) from raw replies."""
+        d1 = cb.n_desc if d1 is None else d1
+        out = np.zeros(cb.n_desc, STATUS_DTYPE) if out is None else out
+        thr = np.zeros(cb.n_req, np.uint32) if thr is None else thr
+        s = cb.struct()
+        self._check(self.lib.rl_decide_raw(self.h, C.byref(s), _ptr(raw), d0, d1, _ptr(out) or None,
+                                           _ptr(thr) or None), "rl_decide_raw")
+        return out, thr
+
+    def submit_compact(self, b: Batch):
+        """A host batch through the compact wire format: rl_submit_c, rl_wait_raw_into,
+        rl_decide_raw -> (statuses, throttles), equal to submit(b)."""
+        cb = compact_batch(b)
+        self.submit_c(cb)
+        raw = self.wait_raw_into(cb.n_desc)
+        return self.decide_raw(cb, raw)
 
     def occupancy(self) -> dict:
         o = RlOccupancy()

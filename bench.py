@@ -505,15 +505,19 @@ def main():
     stats = eng.stats()
     occ = eng.occupancy()
 
-    # Host (PCIe) path (what a Go service sees, rl_submit of host batches, three in flight):
-    #  - the link bound: one batch's exact copies (six H2D arrays, two D2H arrays) moved by the
-    #    link alone, H2D and D2H on two streams (tools/pcie_probe.py's shapes);
-    #  - staged: batches built in place in the engine's pinned slots (rl_host_acquire), as a Go
-    #    batcher writes its requests straight into C memory: only H2D, kernels and D2H are timed
-    #    (each slot holds its batch from an untimed first pass; the batches repeat, which changes
-    #    counters, not the cost); results copied out by rl_wait_into;
-    #  - with_copy: the same with a numpy copy of every array into the slot per batch (the
-    #    round-2 line, a caller whose batches live elsewhere in host memory);
+    # Host (PCIe) path (what a Go service sees: host batches, three in flight), in the compact
+    # wire format (rl_batch_c: prefix bytes + one word per descriptor + one per request in, 8-B
+    # raw replies out) and, for comparison, in the full rl_batch format (20-B statuses out):
+    #  - the link bound: one batch's exact copies moved by the link alone, H2D and D2H on two
+    #    streams (tools/pcie_probe.py's shapes);
+    #  - staged: batches built in place in the engine's pinned slots (rl_host_acquire_c /
+    #    rl_host_acquire), as a Go batcher writes its requests straight into C memory: only H2D,
+    #    kernels (+ the compact form's expansion) and D2H are timed (each slot holds its batch
+    #    from an untimed first pass; the batches repeat, which changes counters, not the cost);
+    #    results read in the slot (rl_wait_raw_view / rl_wait_view);
+    #  - host_decide: rl_decide_raw (GetResponseDescriptorStatus on the host, the work the
+    #    reference's Go BaseRateLimiter does per descriptor) over those replies, ns per
+    #    descriptor on 1 thread and desc/s on `threads` threads splitting each batch;
     #  - frac_of_pcie_bound = that bound / the measured per-batch time.
     host = None
     if not args.no_host_path and not routed:
@@ -523,13 +527,12 @@ def main():
             hbatches.append(hiprl.Batch(db.blob[:n].cpu().numpy(), db.off.cpu().numpy().view(np.uint32),
                                         db.rule.cpu().numpy().view(np.uint32), db.req_of.cpu().numpy().view(np.uint32),
                                         db.now.cpu().numpy(), db.hits.cpu().numpy().view(np.uint32)))
-        out_h = np.empty(d, hiprl.STATUS_DTYPE)
-        thr_h = np.empty(d, np.uint32)
+        cbatches = [hiprl.compact_batch(b) for b in hbatches]
 
         def link_probe(sz_in, sz_out, n=20):
-            """ms per batch for the link to move one batch's exact copies (the engine's six H2D
-            arrays on one stream, its two D2H arrays on another; pinned host buffers): H2D alone,
-            D2H alone, and both directions concurrently (the host path's bound)."""
+            """ms per batch for the link to move one batch's exact copies (H2D arrays on one
+            stream, D2H arrays on another; pinned host buffers): H2D alone, D2H alone, and both
+            directions concurrently."""
             hin = [torch.empty(x, dtype=torch.uint8).pin_memory() for x in sz_in]
             din = [torch.empty(x, dtype=torch.uint8, device=dev) for x in sz_in]
             hout = [torch.empty(x, dtype=torch.uint8).pin_memory() for x in sz_out]
@@ -566,82 +569,108 @@ def main():
             sl["now"][:b.n_req] = b.now
             sl["hits"][:b.n_req] = b.hits
 
-        held = {}  # pinned slot (blob address) -> the batch built in it
+        def fill_c(sl, cb):
+            n = int(cb.blob.shape[0])
+            sl["blob"][:n] = cb.blob
+            sl["desc_word"][:cb.n_desc] = cb.desc_word
+            sl["req_word"][:cb.n_req] = cb.req_word
 
+        held = {}  # pinned slot (blob address) -> the batch built in it
         pv, pt = C.c_void_p(), C.c_void_p()
 
-        def collect(view):
-            if view:  # results read where they landed (rl_wait_view: the slot's pinned arrays)
-                eng._check(eng.lib.rl_wait_view(eng.h, C.byref(pv), C.byref(pt)), "rl_wait_view")
-            else:  # copied out into caller memory (rl_wait_into)
-                eng._check(eng.lib.rl_wait_into(eng.h, out_h.ctypes.data, thr_h.ctypes.data), "rl_wait_into")
-
-        def host_round(bs, copy, view=True):
+        def host_round(bs, build, compact):
             pend = 0
-            for k, b in enumerate(bs):
-                sl = eng.host_acquire()
-                key = sl["blob"].ctypes.data
-                if copy:
-                    fill(sl, b)
+            for b in bs:
+                sl = eng.host_acquire_c() if compact else eng.host_acquire()
+                key = (compact, sl["blob"].ctypes.data)
+                if build:
+                    (fill_c if compact else fill)(sl, b)
                     held[key] = b
                 else:  # the batch this slot already holds (built in place once)
                     b = held[key]
-                eng.submit_staged(b.n_desc, b.n_req, int(b.blob.shape[0]), sl)
+                if compact:
+                    eng.submit_c_staged(b.n_desc, b.n_req, int(b.blob.shape[0]), b.now_base, sl)
+                else:
+                    eng.submit_staged(b.n_desc, b.n_req, int(b.blob.shape[0]), sl)
                 pend += 1
                 if pend == hiprl.MAX_IN_FLIGHT:
-                    collect(view)
+                    if compact:
+                        eng._check(eng.lib.rl_wait_raw_view(eng.h, C.byref(pv)), "rl_wait_raw_view")
+                    else:
+                        eng._check(eng.lib.rl_wait_view(eng.h, C.byref(pv), C.byref(pt)), "rl_wait_view")
                     pend -= 1
             for _ in range(pend):
-                collect(view)
+                if compact:
+                    eng._check(eng.lib.rl_wait_raw_view(eng.h, C.byref(pv)), "rl_wait_raw_view")
+                else:
+                    eng._check(eng.lib.rl_wait_view(eng.h, C.byref(pv), C.byref(pt)), "rl_wait_view")
 
         nb3 = hiprl.MAX_IN_FLIGHT
-        # the untimed first pass builds a batch in every slot; the staged rounds reuse them
-        host_round(hbatches[:nb3], True)
-        rep = [hbatches[k % nb3] for k in range(max(3 * len(hbatches), 30))]  # (sizes for the byte counts)
-        host_round(rep[:2], False)
-        th = time.perf_counter()
-        host_round(rep, False)
-        t_staged = (time.perf_counter() - th) / len(rep)
-        th = time.perf_counter()
-        host_round(rep, False, view=False)
-        t_into = (time.perf_counter() - th) / len(rep)
-        ab = hbatches[0]
-        t_h2d, t_d2h, t_link = link_probe(
-            [int(ab.blob.shape[0]) + 32, 4 * (ab.n_desc + 1), 4 * ab.n_desc, 4 * ab.n_desc, 8 * ab.n_req, 4 * ab.n_req],
-            [20 * ab.n_desc, 4 * ab.n_req])
-        # the copy into a slot alone (a caller that builds elsewhere)
-        sl = eng.host_acquire()
-        tc = time.perf_counter()
-        for b in hbatches[:4]:
-            fill(sl, b)
-        t_copy = (time.perf_counter() - tc) / 4
-        th = time.perf_counter()
-        host_round(hbatches, True, view=False)
-        t_with_copy = (time.perf_counter() - th) / len(hbatches)
-        h2d_b = sum(int(b.blob.shape[0]) + 32 + 4 * (b.n_desc + 1) + 8 * b.n_desc + 12 * b.n_req for b in rep) / len(rep)
-        d2h_b = sum(20 * b.n_desc + 4 * b.n_req for b in rep) / len(rep)
-        # the link cannot beat the slower direction alone; both-concurrent is reported beside it
-        bound_s = max(t_h2d, t_d2h)
-        host = {"value": round(d / t_staged, 1), "unit": "descriptor decisions/s",
-                "ms_per_batch": round(t_staged * 1e3, 4),
-                "pcie_measured_GBps": {"h2d": round(h2d_b / t_h2d / 1e9, 1), "d2h": round(d2h_b / t_d2h / 1e9, 1),
-                                       "both_directions": round((h2d_b + d2h_b) / t_link / 1e9, 1)},
-                "link_ms_per_batch": {"h2d": round(t_h2d * 1e3, 4), "d2h": round(t_d2h * 1e3, 4),
-                                      "both": round(t_link * 1e3, 4)},
-                "bytes_per_batch": {"h2d": int(h2d_b), "d2h": int(d2h_b)},
-                "pcie_bound_ms_per_batch": round(bound_s * 1e3, 4),
-                "frac_of_pcie_bound": round(bound_s / t_staged, 3),
-                "achieved_GBps": {"h2d": round(h2d_b / t_staged / 1e9, 1), "d2h": round(d2h_b / t_staged / 1e9, 1)},
+        reps = max(3 * len(hbatches), 30)
+        res = {}
+        for compact, src in ((True, cbatches), (False, hbatches)):
+            # the untimed first pass builds a batch in every slot; the timed rounds reuse them
+            host_round(src[:nb3], True, compact)
+            rep = [src[k % nb3] for k in range(reps)]
+            host_round(rep[:2], False, compact)
+            th = time.perf_counter()
+            host_round(rep, False, compact)
+            res[compact] = ((time.perf_counter() - th) / len(rep), rep)
+        t_c, rep_c = res[True]
+        t_f, rep_f = res[False]
+        h2d_c = sum(cb.wire_bytes() + 32 for cb in rep_c) / len(rep_c)
+        d2h_c = 8 * d
+        h2d_f = sum(int(b.blob.shape[0]) + 32 + 4 * (b.n_desc + 1) + 8 * b.n_desc + 12 * b.n_req for b in rep_f) / len(rep_f)
+        d2h_f = sum(20 * b.n_desc + 4 * b.n_req for b in rep_f) / len(rep_f)
+        cb0, ab = cbatches[0], hbatches[0]
+        lc = link_probe([int(cb0.blob.shape[0]) + 32, 8 * cb0.n_desc], [8 * cb0.n_desc])
+        lf = link_probe([int(ab.blob.shape[0]) + 32, 4 * (ab.n_desc + 1), 4 * ab.n_desc, 4 * ab.n_desc,
+                         8 * ab.n_req, 4 * ab.n_req], [20 * ab.n_desc, 4 * ab.n_req])
+        # host decisions from raw replies (rl_decide_raw), 1 and `threads` threads
+        import concurrent.futures as cf
+        eng.submit_c(cb0)
+        raw0 = eng.wait_raw_into(cb0.n_desc)
+        st0 = np.empty(cb0.n_desc, hiprl.STATUS_DTYPE)
+        th0 = np.empty(cb0.n_req, np.uint32)
+        tq = time.perf_counter()
+        for _ in range(3):
+            eng.decide_raw(cb0, raw0, 0, cb0.n_desc, st0, th0)
+        t_dec1 = (time.perf_counter() - tq) / 3
+        nthr = 8
+        cuts = [cb0.n_desc * k // nthr for k in range(nthr + 1)]  # one descriptor per request: any cut
+        with cf.ThreadPoolExecutor(nthr) as ex:
+            def dec_all():
+                list(ex.map(lambda k: eng.decide_raw(cb0, raw0, cuts[k], cuts[k + 1], st0, th0), range(nthr)))
+            dec_all()
+            tq = time.perf_counter()
+            for _ in range(5):
+                dec_all()
+            t_decn = (time.perf_counter() - tq) / 5
+        host = {"value": round(d / t_c, 1), "unit": "descriptor decisions/s",
+                "format": "compact (rl_submit_c / rl_wait_raw_view)",
+                "ms_per_batch": round(t_c * 1e3, 4),
+                "bytes_per_desc": {"h2d": round(h2d_c / d, 2), "d2h": round(d2h_c / d, 2)},
+                "bytes_per_batch": {"h2d": int(h2d_c), "d2h": int(d2h_c)},
+                "link_ms_per_batch": {"h2d": round(lc[0] * 1e3, 4), "d2h": round(lc[1] * 1e3, 4),
+                                      "both": round(lc[2] * 1e3, 4)},
+                "pcie_bound_ms_per_batch": round(max(lc[0], lc[1]) * 1e3, 4),
+                "frac_of_pcie_bound": round(max(lc[0], lc[1]) / t_c, 3),
+                "achieved_GBps": {"h2d": round(h2d_c / t_c / 1e9, 1), "d2h": round(d2h_c / t_c / 1e9, 1)},
                 "device_kernels_ms_per_batch": round(step_ms, 4),
-                "staging_copy_ms_per_batch": round(t_copy * 1e3, 4),
-                "copy_out": {"value": round(d / t_into, 1), "ms_per_batch": round(t_into * 1e3, 4)},
-                "with_copy": {"value": round(d / t_with_copy, 1), "ms_per_batch": round(t_with_copy * 1e3, 4)},
-                "note": "staged: batches built in place in the engine's pinned slots (rl_host_acquire), 3 in flight, "
-                        "H2D + kernels + D2H timed, results read in the slot (rl_wait_view); copy_out: the same with "
-                        "results copied into caller memory (rl_wait_into); with_copy: copy_out plus a numpy copy of "
-                        "every array into the slot per batch; bound = the link moving one batch's exact copies (six H2D "
-                        "arrays, two D2H arrays, pinned buffers, measured in this process): the slower direction "
-                        "alone, max(link_ms_per_batch.h2d, .d2h); .both = the two directions on two streams at once"}
+                "host_decide": {"ns_per_desc_1_thread": round(t_dec1 / cb0.n_desc * 1e9, 2), "threads": nthr,
+                                "value": round(cb0.n_desc / t_decn, 1), "unit": "descriptor statuses/s"},
+                "full_format": {"value": round(d / t_f, 1), "ms_per_batch": round(t_f * 1e3, 4),
+                                "bytes_per_desc": {"h2d": round(h2d_f / d, 2), "d2h": round(d2h_f / d, 2)},
+                                "link_ms_per_batch": {"h2d": round(lf[0] * 1e3, 4), "d2h": round(lf[1] * 1e3, 4),
+                                                      "both": round(lf[2] * 1e3, 4)},
+                                "frac_of_pcie_bound": round(max(lf[0], lf[1]) / t_f, 3)},
+                "note": "compact: prefix bytes + a 4-B word per descriptor (length | rule) + a 4-B word per request "
+                        "(hits | time delta) H2D, expanded on the device; 8-B raw replies (INCRBY post-value or "
+                        "local-cache hit) D2H; statuses made on the host by rl_decide_raw (host_decide, run by the "
+                        "caller's threads as the reference's Go BaseRateLimiter would). full_format: rl_batch in, "
+                        "20-B statuses + ThrottleMillis out. staged in the engine's pinned slots, 3 in flight, "
+                        "H2D + kernels + D2H timed; bound = the link moving one batch's exact copies, the slower "
+                        "direction alone"}
 
     if rank != 0:
         if dist:

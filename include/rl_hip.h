@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 4u
+#define RL_ABI_VERSION 5u
 
 /* rule id of a descriptor whose limit is nil ("don't check", src/limiter/cache.go:19-22) */
 #define RL_NIL_RULE 0xFFFFFFFFu
@@ -218,6 +218,65 @@ int rl_wait_into(rl_engine* e, rl_status* out, uint32_t* req_throttle_ms);
  * slot (DoLimit's []*DescriptorStatus, src/redis/fixed_cache_impl.go:108-123). */
 int rl_wait_view(rl_engine* e, const rl_status** out, const uint32_t** req_throttle_ms);
 
+/* ---- Compact host batches (the PCIe wire format of a Go batcher) ------------------------
+ * The same batch as rl_batch in fewer bytes: per descriptor the prefix bytes plus ONE word
+ *   desc_word[i] = prefix_len (bits 0-15) | rule_id (bits 16-31; RL_NIL_RULE16 = nil limit)
+ * (prefixes lie back to back in prefix_blob, so their offsets are implicit), per request ONE word
+ *   req_word[r]  = hits_addend (bits 0-23; 0 means 1) | (now - now_base) (bits 24-31)
+ * and the request index of each descriptor only when requests hold several descriptors
+ * (req_of; NULL with RL_BC_ONE_PER_REQ: descriptor i belongs to request i). At one descriptor
+ * per request that is len(prefix) + 8 bytes per descriptor against len(prefix) + 24 for
+ * rl_batch. A batch whose rule ids reach 0xFFFF, whose prefixes pass 65535 bytes, whose
+ * hits_addend pass 2^24 - 1 or whose request times span more than 255 s goes through rl_submit.
+ * The device expands the words into the rl_batch arrays (a kernel on the copy stream) and runs
+ * the pipeline unchanged.
+ * Results come back as raw replies, 8 B per descriptor: the INCRBY post-value each descriptor
+ * saw, or its local-cache hit, or nil — what Redis answers the reference's DoLimit
+ * (fixed_cache_impl.go:91-102) plus the local-cache verdict (base_limiter.go:57-66). The status
+ * is then made on the host by the unchanged BaseRateLimiter logic (GetResponseDescriptorStatus,
+ * base_limiter.go:70-195): rl_decide_raw in C, or the Go service's own BaseRateLimiter. */
+#define RL_NIL_RULE16 0xFFFFu
+#define RL_RAW_NIL 2u /* rl_raw_reply.flags: a nil-limit descriptor (no INCRBY) */
+enum { RL_BC_ONE_PER_REQ = 1u /* req_of is implicit: descriptor i belongs to request i (n_desc == n_req) */ };
+typedef struct rl_batch_c {
+  uint32_t n_desc;
+  uint32_t n_req;
+  uint32_t blob_bytes;          /* = sum of the prefix lengths */
+  uint32_t flags;               /* RL_BC_* */
+  int64_t now_base;             /* request r's time = now_base + (req_word[r] >> 24) */
+  const uint8_t* prefix_blob;
+  const uint32_t* desc_word;    /* n_desc */
+  const uint32_t* req_word;     /* n_req */
+  const uint32_t* req_of;       /* n_desc, or NULL with RL_BC_ONE_PER_REQ */
+} rl_batch_c;
+typedef struct rl_host_batch_c {
+  uint8_t* prefix_blob;
+  uint32_t* desc_word;
+  uint32_t* req_word;
+  uint32_t* req_of;
+  uint32_t max_desc, max_req, max_blob, reserved;
+} rl_host_batch_c;
+/* The next free staging slot, compact layout (the rl_host_acquire contract). */
+int rl_host_acquire_c(rl_engine* e, rl_host_batch_c* out);
+/* Submit a compact host batch (arrays in the acquired slot, or any host memory: copied before
+ * the call returns). Complete it with rl_wait_raw_view / rl_wait_raw_into. */
+int rl_submit_c(rl_engine* e, const rl_batch_c* batch);
+typedef struct rl_raw_reply rl_raw_reply;
+/* Complete the oldest batch in flight, a compact host batch, and hand out its n_desc raw replies
+ * in the slot's pinned memory (valid as rl_wait_view's results are). */
+int rl_wait_raw_view(rl_engine* e, const rl_raw_reply** out);
+/* The same, copying the replies into out[n_desc] (NULL discards). */
+int rl_wait_raw_into(rl_engine* e, rl_raw_reply* out);
+/* Host side of the compact form: GetResponseDescriptorStatus + the near/over checks + the
+ * ThrottleMillis max (base_limiter.go:70-195) for descriptors [d0, d1) of a compact batch from
+ * its raw replies (indexed like the batch), with the engine's loaded rules. out / req_throttle_ms
+ * are indexed by descriptor / request; a request's ThrottleMillis is written once every one of
+ * its descriptors is in [d0, d1) (so a caller may split the range over threads at request
+ * boundaries). Bit-exact with the statuses rl_submit returns. Thread-safe against itself; not
+ * against rl_load_rules. */
+int rl_decide_raw(rl_engine* e, const rl_batch_c* batch, const rl_raw_reply* raw, uint32_t d0, uint32_t d1,
+                  rl_status* out, uint32_t* req_throttle_ms);
+
 /* Device-memory batch (inputs already resident in HBM; outputs stay in HBM), with nothing
  * else in flight. Ordered on the engine's stream; rl_wait() completes it. Used by the
  * multi-GPU router and by the benchmark. */
@@ -297,10 +356,11 @@ int rl_submit_routed(rl_engine* e, const void* d_records, uint32_t n, void* d_re
  * arrived, e.g. on the stream of the exchange; NULL: ordered on the engine stream). flags = 0 is
  * rl_submit_routed (ready_event must be NULL). rl_wait completes the oldest batch. */
 #define RL_ROUTED_RAW 1u
-typedef struct rl_raw_reply {
+struct rl_raw_reply {
   uint32_t after; /* INCRBY post-value (uint32, as fixed_cache_impl.go:51 decodes it); 0 for a hit */
-  uint32_t flags; /* RL_RAW_LOCAL_HIT: the key was in the local over-limit cache, no INCRBY */
-} rl_raw_reply;
+  uint32_t flags; /* RL_RAW_LOCAL_HIT: the key was in the local over-limit cache, no INCRBY;
+                     RL_RAW_NIL: nil limit */
+};
 #define RL_RAW_LOCAL_HIT 1u
 int rl_submit_routed_async(rl_engine* e, const void* d_records, uint32_t n, void* d_reply, uint32_t flags,
                            void* ready_event);

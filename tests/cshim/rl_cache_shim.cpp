@@ -151,14 +151,16 @@ const char* rlc_error(void* p) { return static_cast<Shim*>(p)->err.c_str(); }
 
 void rlc_flush(void* p) { static_cast<Shim*>(p)->cache->Flush(); }
 
-// Batcher counters: batches, rule loads, rule loads made while a batch was in flight, drains
-// (batches in flight completed early for a load / submit the engine refused with them in flight).
+// Batcher counters (5 words): batches, rule loads, rule loads made while a batch was in flight,
+// drains (batches in flight completed early for a load / submit the engine refused with them in
+// flight), batches sent in the compact wire format.
 void rlc_batcher_stats(void* p, uint64_t* out) {
   const auto s = static_cast<Shim*>(p)->single->batcher_stats();
   out[0] = s.batches;
   out[1] = s.rule_loads;
   out[2] = s.rule_loads_in_flight;
   out[3] = s.drains;
+  out[4] = s.compact_batches;
 }
 
 }  // extern "C"

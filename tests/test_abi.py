@@ -25,7 +25,7 @@ def test_library_exports_all_declared_symbols():
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
     assert sorted(n for n, _, _ in hiprl.ABI) == names
-    assert lib.rl_abi_version() == hiprl.ABI_VERSION == 4
+    assert lib.rl_abi_version() == hiprl.ABI_VERSION == 5
 
 
 def test_struct_layouts_match_header(tmp_path):
@@ -35,14 +35,18 @@ def test_struct_layouts_match_header(tmp_path):
                    'sizeof(rl_config),sizeof(rl_rule),sizeof(rl_batch),sizeof(rl_status),sizeof(rl_engine_stats),'
                    'offsetof(rl_config,hash_seed),offsetof(rl_config,max_load_permille),sizeof(rl_occupancy),'
                    'sizeof(rl_host_batch),RL_BLOB_SLACK,RL_MAX_IN_FLIGHT,sizeof(rl_router_config),sizeof(rl_router_stats),'
-                   'offsetof(rl_router_stats,pack_us));return 0;}\n')
+                   'offsetof(rl_router_stats,pack_us));printf("%zu %zu %zu %zu %zu\\n",sizeof(rl_batch_c),'
+                   'offsetof(rl_batch_c,now_base),offsetof(rl_batch_c,req_of),sizeof(rl_host_batch_c),'
+                   'sizeof(struct rl_raw_reply));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", str(ROOT / "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [C.sizeof(hiprl.RlConfig), C.sizeof(hiprl.RlRule), C.sizeof(hiprl.RlBatch), hiprl.STATUS_DTYPE.itemsize,
             C.sizeof(hiprl.RlEngineStats), hiprl.RlConfig.hash_seed.offset, hiprl.RlConfig.max_load_permille.offset,
             C.sizeof(hiprl.RlOccupancy), C.sizeof(hiprl.RlHostBatch), hiprl.BLOB_SLACK, hiprl.MAX_IN_FLIGHT, C.sizeof(hiprl.RlRouterConfig),
-            C.sizeof(hiprl.RlRouterStats), hiprl.RlRouterStats.pack_us.offset]
+            C.sizeof(hiprl.RlRouterStats), hiprl.RlRouterStats.pack_us.offset,
+            C.sizeof(hiprl.RlBatchC), hiprl.RlBatchC.now_base.offset, hiprl.RlBatchC.req_of.offset,
+            C.sizeof(hiprl.RlHostBatchC), hiprl.RAW_DTYPE.itemsize]
     assert got == want
     assert hiprl.STATUS_DTYPE.itemsize == 20
 

@@ -200,10 +200,11 @@ def test_rules_arrive_mid_stream_two_in_flight():
                         int(st["reset_s"][k]) if ru[k] is not None else 0)
                 assert (code, rem, bool(has_limit), reset if ru[k] is not None else 0) == want, (t, q, k)
             assert gthr == int(thr[0]), (t, q)
-    bs = (C.c_uint64 * 3)()
+    bs = (C.c_uint64 * 5)()
     m.lib.rlc_batcher_stats(m.h, bs)
     assert bs[1] >= 10, list(bs)  # new limits kept arriving
     assert bs[2] >= 1, list(bs)   # and at least one load happened behind a batch in flight
+    assert bs[4] == bs[0], list(bs)  # every batch crossed PCIe in the compact wire format
     m.close()
 
 
@@ -249,9 +250,55 @@ def test_more_than_v4_max_rules_through_do_limit():
                 assert (g[0], g[1], g[3]) == (int(st["code_flags"][k]) & 0xFF, int(st["limit_remaining"][k]),
                                               int(st["reset_s"][k])), (t, q, k)
             assert gthr == int(thr[0]), (t, q)
-    bs = (C.c_uint64 * 4)()
+    bs = (C.c_uint64 * 5)()
     m.lib.rlc_batcher_stats(m.h, bs)
     assert bs[3] >= 1, list(bs)  # the batcher drained at least once (the crossing / the LSD pipeline)
+    assert bs[4] == bs[0], list(bs)  # rule ids < 0xFFFF: compact batches throughout
+    m.close()
+
+
+def test_batches_outside_the_compact_form_go_full_format():
+    """Requests whose hits_addend passes 2^24 - 1 cannot ride in a compact batch (rl_batch_c's
+    24-bit hits): the batcher cuts the batch there and sends one in the full rl_batch format;
+    three concurrent callers mixing them with ordinary requests get the serial oracle's answers."""
+    T, n = 3, 120
+    rules = [(50, hiprl.SECOND), (1 << 26, hiprl.MINUTE)]
+    m = Mirror(False, window_us=300)
+    m.lib.rlc_batcher_stats.argtypes = [C.c_void_p, C.c_void_p]
+    ids = [m.add_rule(L, u, f"rule{k}") for k, (L, u) in enumerate(rules)]
+    now = 1_700_000_050
+    m.lib.rlc_set_time(m.h, now)
+    rng = np.random.default_rng(29)
+    per = []
+    for t in range(T):
+        reqs = []
+        for q in range(n):
+            big = q % 17 == 5
+            reqs.append((f"fx{t}", [[("k", str(int(rng.integers(0, 4))))]], [1 if big else int(rng.integers(0, 2))],
+                         (1 << 24) + 3 if big else int(rng.integers(0, 3)), now))
+        per.append(reqs)
+    res = [None] * T
+
+    def run(t):
+        res[t] = [m.do_limit(d, de, [ids[x] for x in ru], h) for d, de, ru, h, _ in per[t]]
+
+    th = [threading.Thread(target=run, args=(t,)) for t in range(T)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    m.lib.rlc_flush(m.h)
+    for t in range(T):
+        o = oracle.Oracle()
+        o.load_rules(rules)
+        st, thr = streams.replay(o, per[t], [1] * n)
+        for q, (got, gthr) in enumerate(res[t]):
+            assert (got[0][0], got[0][1], got[0][3]) == (int(st["code_flags"][q]) & 0xFF, int(st["limit_remaining"][q]),
+                                                         int(st["reset_s"][q])), (t, q)
+            assert gthr == int(thr[q]), (t, q)
+    bs = (C.c_uint64 * 5)()
+    m.lib.rlc_batcher_stats(m.h, bs)
+    assert 1 <= bs[4] < bs[0], list(bs)
     m.close()
 
 
