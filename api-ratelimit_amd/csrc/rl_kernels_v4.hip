@@ -45,6 +45,10 @@ using tile::W;
 using tile::BKT_NONE;
 
 constexpr int ROW = V4_ROW16;  // u16 bucket starts per tile (entries [0, NBUCKETS] used)
+// k4_hist's per-(tile, hot bucket) word: h sum (<= 2048 x (2^32 - 1) < 2^52) | count << 52
+constexpr int HS_CNT_SHIFT = 52;
+constexpr unsigned long long HS_SUM_MASK = (1ull << HS_CNT_SHIFT) - 1ull;
+static_assert((unsigned long long)V4_TILE * 0xFFFFFFFFull <= HS_SUM_MASK && V4_TILE < (1 << 12), "hot word fields");
 static_assert(ROW >= NBUCKETS + 1, "row holds every bucket start and the end");
 #ifndef RL_G_CAP
 // 896 records (two average config-3 buckets) per LDS stage at 3 blocks per CU (50 KB LDS,
@@ -393,8 +397,11 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   __syncthreads();
   uint32_t* trow = reinterpret_cast<uint32_t*>(tstart + (size_t)tile * ROW);
   for (int b = tid; b < ROW / 2; b += NT) trow[b] = reinterpret_cast<const uint32_t*>(sh_cnt)[b];
+  // per hot bucket one word: its h sum in the tile | its descriptor count << HS_CNT_SHIFT (k4_scan
+  // reads one word per (tile, hot bucket), not two u16 row entries and the sum)
   unsigned long long* hrow = thsum + (size_t)tile * HOT_BUCKETS;
-  for (int b = tid; b < HOT_BUCKETS; b += NT) hrow[b] = sh_hs[b];
+  for (int b = tid; b < HOT_BUCKETS; b += NT)
+    hrow[b] = sh_hs[b] | ((unsigned long long)(sh_cnt[b + 1] - sh_cnt[b]) << HS_CNT_SHIFT);
   // word-major ([word][tile]): k4_scan's hot blocks read each word of every tile coalesced
   if (tid < FP_PART_WORDS) fpart[(size_t)tid * ntiles + tile] = sh_f[tid];
   if (tid == 0 && sh_err) atomicOr(&ctl->err, sh_err);
@@ -521,20 +528,16 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
   if (in_regs && hotb) {
     // every load at a clamped tile, so all of them are in flight together (a load behind a
     // per-lane condition waits for the one before it)
-    uint32_t r0[HOT_Q], r1[HOT_Q];
 #pragma unroll
     for (int u = 0; u < HOT_Q; ++u) {
       const uint32_t t = min(tb + u, ntiles - 1u);
-      const uint16_t* row = tstart + (size_t)t * ROW + b;
-      r0[u] = row[0];
-      r1[u] = row[1];
-      hq[u] = thsum[(size_t)t * HOT_BUCKETS + b];
+      hq[u] = thsum[(size_t)t * HOT_BUCKETS + b];  // h sum | count << HS_CNT_SHIFT
     }
 #pragma unroll
     for (int u = 0; u < HOT_Q; ++u) {
       const bool v = tb + u < te;
-      c += v ? r1[u] - r0[u] : 0u;
-      hq[u] = v ? hq[u] : 0ull;
+      c += v ? (uint32_t)(hq[u] >> HS_CNT_SHIFT) : 0u;
+      hq[u] = v ? hq[u] & HS_SUM_MASK : 0ull;
       hs += hq[u];
     }
   } else if (in_regs) {
@@ -546,8 +549,9 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
 #pragma unroll
       for (int u = 0; u < SCAN_U; ++u) {
         const uint16_t* row = tstart + (size_t)(t + u) * ROW + b;
-        cv[u] = t + u < te ? (uint32_t)row[1] - (uint32_t)row[0] : 0u;
-        hv[u] = (hotb && t + u < te) ? thsum[(size_t)(t + u) * HOT_BUCKETS + b] : 0ull;
+        const unsigned long long w = (hotb && t + u < te) ? thsum[(size_t)(t + u) * HOT_BUCKETS + b] : 0ull;
+        cv[u] = t + u >= te ? 0u : hotb ? (uint32_t)(w >> HS_CNT_SHIFT) : (uint32_t)row[1] - (uint32_t)row[0];
+        hv[u] = w & HS_SUM_MASK;
       }
 #pragma unroll
       for (int u = 0; u < SCAN_U; ++u) {
@@ -711,7 +715,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
   for (uint32_t t = in_regs ? te : tb; t < te; t += SCAN_U) {
     unsigned long long hv[SCAN_U];
 #pragma unroll
-    for (int u = 0; u < SCAN_U; ++u) hv[u] = t + u < te ? thsum[(size_t)(t + u) * HOT_BUCKETS + b] : 0ull;
+    for (int u = 0; u < SCAN_U; ++u) hv[u] = t + u < te ? thsum[(size_t)(t + u) * HOT_BUCKETS + b] & HS_SUM_MASK : 0ull;
 #pragma unroll
     for (int u = 0; u < SCAN_U; ++u) {
       if (t + u < te) hoff[(size_t)(t + u) * HOT_BUCKETS + b] = hrun;
@@ -1718,7 +1722,13 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
       hw[tid] = v;
     }
     if (tid == HEAD) hctl->tile_ctr[CAND_CTR][0] = nc;
+#ifdef RL_EPI_NOSYSFENCE
+    // (A/B variant) the pinned words are uncached host memory: waiting for the stores to complete
+    // makes them visible without the system-scope release's write-back of this XCD's L2
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
     __threadfence_system();
+#endif
   }
   uint32_t* z = reinterpret_cast<uint32_t*>(next_ctl);
   constexpr uint32_t words = sizeof(EngineCtl) / 4;
