@@ -161,7 +161,10 @@ def test_rules_arrive_mid_stream_two_in_flight():
     T, n = 8, 220
     units = [hiprl.SECOND, hiprl.MINUTE, hiprl.HOUR]
     all_rules = [(3 + 2 * k, units[k % 3]) for k in range(40)]  # 40 distinct (L, unit) limits
-    m = Mirror(False, window_us=150)
+    # a gather window shorter than a batch's device time, so batch k + 1 (and its rule load) is
+    # submitted while batch k is still in flight (with a longer window the batcher answers batch
+    # k first: it polls rl_query while gathering)
+    m = Mirror(False, window_us=20)
     m.lib.rlc_batcher_stats.argtypes = [C.c_void_p, C.c_void_p]
     ids = [m.add_rule(L, u, f"rule{k}") for k, (L, u) in enumerate(all_rules)]
     now = 1_700_000_123
