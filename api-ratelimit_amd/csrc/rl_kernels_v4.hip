@@ -161,16 +161,28 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
                                               uint32_t* __restrict__ req_thr, uint32_t* __restrict__ fpart,
                                               uint16_t* __restrict__ tstart, unsigned long long* __restrict__ thsum,
                                               MRec* __restrict__ srec, rl_status* __restrict__ out, EngineCtl* ctl) {
+#ifndef RL_HIST_GLOBAL_HOT
   // sh_hot (the hot table: tag words, then the entries, rl_common.h) and s_res (hot in-tile
   // prefixes) share one pool: once every thread holds its descriptors' prefixes, the pool
   // stages half a tile of records at a time for coalesced, whole-line stores.
   constexpr size_t HOT_LDS = sizeof(HotEntry) * (HOT_SLOTS + HOT_MAX);
   __shared__ __attribute__((aligned(32))) uint8_t s_pool[HOT_LDS + sizeof(unsigned long long) * T];
   HotEntry* const sh_hot = reinterpret_cast<HotEntry*>(s_pool);
+#else
+  // Measured and not kept (round 4, A/B on one box): the hot table read where it lies (16 KB,
+  // L1/L2-resident) instead of copied into LDS, so a block needs ≈48 KB of LDS instead of ≈64
+  // and the pool stages a quarter tile per pass. k4_hist alone 42 -> 45 µs and the pipelined
+  // step 106 -> 122 µs: more of the next batch's tiles then sit beside k4_group and both slow
+  // down (with the VGPR budget cut to 96 as well, so that one tile fits beside two k4_group
+  // blocks, no better).
+  constexpr size_t HOT_LDS = 0;
+  __shared__ __attribute__((aligned(32))) uint8_t s_pool[sizeof(unsigned long long) * T];
+  const HotEntry* const sh_hot = hot;
+#endif
   unsigned long long* const s_res = reinterpret_cast<unsigned long long*>(s_pool + HOT_LDS);
   MRec* const s_stage = reinterpret_cast<MRec*>(s_pool);
   constexpr uint32_t STAGE = (uint32_t)(sizeof(s_pool) / sizeof(MRec));  // records per staging pass
-  static_assert(HOT_LDS % 16 == 0 && STAGE >= (uint32_t)T / 2 && T % STAGE == 0, "record staging");
+  static_assert(HOT_LDS % 16 == 0 && STAGE >= (uint32_t)T / 4 && T % STAGE == 0, "record staging");
   __shared__ uint16_t sh_cnt[ROW];
   __shared__ unsigned long long sh_hs[HOT_BUCKETS];
   __shared__ uint16_t s_d[T];
@@ -185,7 +197,9 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
   const uint32_t tile = blockIdx.x, ntiles = gridDim.x;
   const uint32_t t0 = tile * T;
   STH(0);
+#ifndef RL_HIST_GLOBAL_HOT
   tile::load_hot_table(hot, sh_hot);
+#endif
   for (int b = tid; b < ROW / 2; b += NT) reinterpret_cast<uint32_t*>(sh_cnt)[b] = 0;
   for (int b = tid; b < HOT_BUCKETS; b += NT) sh_hs[b] = 0;
   if (tid < FP_PART_WORDS) sh_f[tid] = 0;
