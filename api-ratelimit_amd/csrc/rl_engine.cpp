@@ -264,6 +264,7 @@ struct rl_engine {
     hipEvent_t done = nullptr;  // the batch's completion event, recorded behind its k4_group
     uint32_t slot = 0;          // its host slot (Flight::slot)
   } pg;
+  bool defer_req = false;      // set by rl_submit_pipelined: its batch may defer its group
   bool defer_ok = false;       // set by submit_common: the batch being submitted may defer its group
   bool deferred_now = false;   // set by run_pipeline: it did
   int flush_group();
@@ -829,7 +830,7 @@ int rl_engine::submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, R
   h_ctl = h_ctl_s[s];
   h_cand = h_cand_s[s];
   const bool want = want_cand;
-  defer_ok = !host && !reply;
+  defer_ok = defer_req && !host && !reply;
   int rc = run_pipeline(d, out, thr, default_mode(), in_ev, inputs_ready);
   defer_ok = false;
   if (rc) return rc;
@@ -1478,7 +1479,10 @@ int rl_submit_pipelined(rl_engine* e, const rl_batch* b, rl_status* d_out, uint3
   for (int q = 0; q < e->n_fl; ++q)
     if (e->fl[q].out == d_out || e->fl[q].thr == d_req_throttle_ms)
       return e->fail(RL_EINVAL, "batches in flight together need distinct output buffers");
-  return e->submit_common(*b, d_out, d_req_throttle_ms, nullptr, nullptr, true, false, nullptr, nullptr);
+  e->defer_req = true;  // (RL_DEFER_GROUP) its k4_group may wait for the next batch's k4_hist
+  rc = e->submit_common(*b, d_out, d_req_throttle_ms, nullptr, nullptr, true, false, nullptr, nullptr);
+  e->defer_req = false;
+  return rc;
 }
 
 void* rl_stream(rl_engine* e) { return e ? (void*)e->stream : nullptr; }
