@@ -246,29 +246,6 @@ struct rl_engine {
   Flight fl[HSLOTS];
   int n_fl = 0;
 
-  // Deferred k4_group (RL_DEFER_GROUP): a pipelined device batch's k4_group is launched by the
-  // next submit, on the engine stream behind that batch's k4_hist event, so the next batch's
-  // k4_hist runs beside this batch's k4_scan / k4_place only, never beside k4_group; or by the
-  // wait / query of the batch when no submit comes first.
-  struct PendingGroup {
-    bool valid = false;
-    rl_batch b{};
-    rl_status* out = nullptr;
-    uint32_t* thr = nullptr;
-    int routed = 0;
-    bool cand = false;
-    EngineCtl *c4 = nullptr, *c4n = nullptr, *hctl = nullptr;
-    HotCand* hcand = nullptr;
-    MRec* srt = nullptr;
-    uint16_t* tcount = nullptr;
-    hipEvent_t done = nullptr;  // the batch's completion event, recorded behind its k4_group
-    uint32_t slot = 0;          // its host slot (Flight::slot)
-  } pg;
-  bool defer_req = false;      // set by rl_submit_pipelined: its batch may defer its group
-  bool defer_ok = false;       // set by submit_common: the batch being submitted may defer its group
-  bool deferred_now = false;   // set by run_pipeline: it did
-  int flush_group();
-
   // timing
   bool timing = false;
   struct Mark { int kid; hipEvent_t a, b; };
@@ -335,7 +312,6 @@ struct rl_engine {
     return MODE_V4;
   }
   int run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, int mode, hipEvent_t in_ev, bool inputs_ready);
-  void launch_group(const PendingGroup& g);
   int upload_hot(hipStream_t us);
   void update_hot(const HotCand* cand, uint32_t n_cand);
   int settle(Flight& f);
@@ -378,11 +354,6 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   // how decisions are written (rl_common.h OUT_*): statuses, routed statuses, raw replies
   const int routed = (b.reserved & RL_BATCH_RAW) ? OUT_RAW : (b.reserved & RL_BATCH_ROUTED) ? OUT_ROUTED : OUT_STATUS;
   hipError_t e;
-  deferred_now = false;
-  if (pg.valid && !(mode == MODE_V4 && split_hist())) {  // (a split v4 batch flushes behind its k4_hist)
-    int rc = flush_group();
-    if (rc) return rc;
-  }
   if (mode == MODE_V4) {
     const uint32_t sl = (uint32_t)(sub_seq & 1u);
     EngineCtl* c4 = v4_ctl[sub_seq % 3];
@@ -425,10 +396,6 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     if (split) {
       hipEventRecord(ev_front[sl], front);
       hipStreamWaitEvent(stream, ev_front[sl], 0);
-      if (pg.valid) {  // the previous batch's k4_group, now behind this batch's k4_hist
-        int rc = flush_group();
-        if (rc) return rc;
-      }
     }
     timed(KT_V4_SCAN, [&] {
       launch_v4_scan(stream, n, v4_tcount[sl], v4_thsum[sl], v4_hoff, v4_fpart[sl], hot_t + HOT_SLOTS, v4_hb, tab,
@@ -439,26 +406,11 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
       launch_v4_place(stream, b, srt, v4_tcount[sl], v4_scratch, d_rules, n_rules, v4_hoff, v4_hb, lc, out,
                       thr, v4_dfr, routed, d_poison, c4);
     });
-    PendingGroup g;
-    g.valid = true;
-    g.b = b;
-    g.out = out;
-    g.thr = thr;
-    g.routed = routed;
-    g.cand = want_cand;
-    g.c4 = c4;
-    g.c4n = c4n;
-    g.hctl = h_ctl;
-    g.hcand = want_cand ? h_cand : nullptr;
-    g.srt = srt;
-    g.tcount = v4_tcount[sl];
-    static const bool defer_env = getenv("RL_DEFER_GROUP") != nullptr;
-    if (defer_env && defer_ok && split && !timing) {
-      pg = g;  // launched by the next submit (behind its k4_hist) or by the wait
-      deferred_now = true;
-    } else {
-      timed(KT_V4_GROUP, [&] { launch_group(g); });
-    }
+    timed(KT_V4_GROUP, [&] {
+      launch_v4_group(stream, b, d_rules, n_rules, tab, out, thr, v4_hb, v4_dfr, d_cand, want_cand ? 1 : 0,
+                      cfg.hash_seed, v4_scratch, v4_heads, v4_ins, v4_heads + ng, v4_ins + (size_t)ng * 4, routed,
+                      d_occ, c4, c4n, h_ctl, want_cand ? h_cand : nullptr, srt, v4_tcount[sl]);
+    });
     // k4_group's last block writes the summary into h_ctl / h_cand (pinned host memory)
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
@@ -555,22 +507,6 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   if (e == hipSuccess) e = hipMemcpyAsync(h_cand, d_cand, sizeof(HotCand) * CAND_MAX, hipMemcpyDeviceToHost, stream);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync(ctl)");
   return 0;
-}
-
-void rl_engine::launch_group(const PendingGroup& g) {
-  const uint32_t ng = v4_group_blocks(g.b.n_desc);
-  launch_v4_group(stream, g.b, d_rules, n_rules, tab, g.out, g.thr, v4_hb, v4_dfr, d_cand, g.cand ? 1 : 0,
-                  cfg.hash_seed, v4_scratch, v4_heads, v4_ins, v4_heads + ng, v4_ins + (size_t)ng * 4, g.routed, d_occ,
-                  g.c4, g.c4n, g.hctl, g.hcand, g.srt, g.tcount);
-}
-
-int rl_engine::flush_group() {
-  if (!pg.valid) return 0;
-  pg.valid = false;
-  launch_group(pg);
-  hipError_t e = hipGetLastError();
-  if (e == hipSuccess) e = hipEventRecord(pg.done, stream);
-  return e == hipSuccess ? 0 : hip_fail(e, "deferred k4_group");
 }
 
 // Upload the hot-key set: open-addressed tag words (rl_common.h HOT_TAGS; home = hot_home(a),
@@ -678,10 +614,6 @@ int rl_engine::enqueue_d2h(const Flight& f, hipStream_t s) {
 // prefix run held two fingerprints. Reruns are synchronous, so they are on the table before
 // anything submitted later.
 int rl_engine::settle(Flight& f) {
-  if (pg.valid && pg.slot == f.slot) {  // its k4_group is still deferred: launch it now
-    int rc = flush_group();
-    if (rc) return rc;
-  }
   h_ctl = h_ctl_s[f.slot];
   h_cand = h_cand_s[f.slot];
   hipError_t e = timing ? hipStreamSynchronize(stream) : wait_event_polling(done_ev[f.slot]);
@@ -830,9 +762,7 @@ int rl_engine::submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, R
   h_ctl = h_ctl_s[s];
   h_cand = h_cand_s[s];
   const bool want = want_cand;
-  defer_ok = defer_req && !host && !reply;
   int rc = run_pipeline(d, out, thr, default_mode(), in_ev, inputs_ready);
-  defer_ok = false;
   if (rc) return rc;
   if (reply) launch_route_reply(stream, d.n_desc, out, thr, reply);
   Flight f;
@@ -860,13 +790,7 @@ int rl_engine::submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, R
     // release by k4_group (or copied by the LSD path's own D2H copy, ordered before this)
     const bool dev_only = default_mode() == MODE_V4 && !reply && d.n_desc;
     done_ev[s] = dev_only ? ev_dd[s] : ev_done[s];
-    if (deferred_now) {
-      pg.done = done_ev[s];  // recorded when the deferred k4_group is launched
-      pg.slot = s;
-      e = hipSuccess;
-    } else {
-      e = hipEventRecord(done_ev[s], stream);
-    }
+    e = hipEventRecord(done_ev[s], stream);
   }
   if (e != hipSuccess) return hip_fail(e, "hipEventRecord(done)");
   fl[n_fl++] = f;
@@ -1256,10 +1180,6 @@ int rl_query(rl_engine* e) {
   if (!e->n_fl) return e->fail(RL_ESTATE, "rl_query without a batch in flight");
   const rl_engine::Flight& f = e->fl[0];
   if (f.settled) return 1;
-  if (e->pg.valid && e->pg.slot == f.slot) {
-    int rc = e->flush_group();
-    if (rc) return rc;
-  }
   const hipError_t q = hipEventQuery(e->done_ev[f.slot]);
   if (q == hipSuccess) return 1;
   if (q == hipErrorNotReady) return 0;
@@ -1479,10 +1399,7 @@ int rl_submit_pipelined(rl_engine* e, const rl_batch* b, rl_status* d_out, uint3
   for (int q = 0; q < e->n_fl; ++q)
     if (e->fl[q].out == d_out || e->fl[q].thr == d_req_throttle_ms)
       return e->fail(RL_EINVAL, "batches in flight together need distinct output buffers");
-  e->defer_req = true;  // (RL_DEFER_GROUP) its k4_group may wait for the next batch's k4_hist
-  rc = e->submit_common(*b, d_out, d_req_throttle_ms, nullptr, nullptr, true, false, nullptr, nullptr);
-  e->defer_req = false;
-  return rc;
+  return e->submit_common(*b, d_out, d_req_throttle_ms, nullptr, nullptr, true, false, nullptr, nullptr);
 }
 
 void* rl_stream(rl_engine* e) { return e ? (void*)e->stream : nullptr; }

@@ -1736,13 +1736,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
       hw[tid] = v;
     }
     if (tid == HEAD) hctl->tile_ctr[CAND_CTR][0] = nc;
-#ifdef RL_EPI_NOSYSFENCE
-    // (A/B variant) the pinned words are uncached host memory: waiting for the stores to complete
-    // makes them visible without the system-scope release's write-back of this XCD's L2
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
     __threadfence_system();
-#endif
   }
   uint32_t* z = reinterpret_cast<uint32_t*>(next_ctl);
   constexpr uint32_t words = sizeof(EngineCtl) / 4;
