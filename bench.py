@@ -85,6 +85,8 @@ def parse():
     ap.add_argument("--no-kernel-times", action="store_true")
     ap.add_argument("--no-roofline-probe", action="store_true")
     ap.add_argument("--no-host-path", action="store_true")
+    ap.add_argument("--host-formats", default="compact,full", help=argparse.SUPPRESS)  # traces: one format only
+    ap.add_argument("--host-no-probe", action="store_true", help=argparse.SUPPRESS)  # traces: no link probes
     ap.add_argument("--pipeline", choices=["v4", "lsd"], default="v4",
                     help="decision pipeline (v4 default; lsd = radix-sort only)")
     ap.add_argument("--independent", action="store_true",
@@ -608,7 +610,11 @@ def main():
         nb3 = hiprl.MAX_IN_FLIGHT
         reps = max(3 * len(hbatches), 30)
         res = {}
+        fmts = args.host_formats.split(",")
         for compact, src in ((True, cbatches), (False, hbatches)):
+            if ("compact" if compact else "full") not in fmts:
+                res[compact] = (float("nan"), src[:1])
+                continue
             # the untimed first pass builds a batch in every slot; the timed rounds reuse them
             host_round(src[:nb3], True, compact)
             rep = [src[k % nb3] for k in range(reps)]
@@ -623,9 +629,11 @@ def main():
         h2d_f = sum(int(b.blob.shape[0]) + 32 + 4 * (b.n_desc + 1) + 8 * b.n_desc + 12 * b.n_req for b in rep_f) / len(rep_f)
         d2h_f = sum(20 * b.n_desc + 4 * b.n_req for b in rep_f) / len(rep_f)
         cb0, ab = cbatches[0], hbatches[0]
-        lc = link_probe([int(cb0.blob.shape[0]) + 32, 8 * cb0.n_desc], [8 * cb0.n_desc])
-        lf = link_probe([int(ab.blob.shape[0]) + 32, 4 * (ab.n_desc + 1), 4 * ab.n_desc, 4 * ab.n_desc,
-                         8 * ab.n_req, 4 * ab.n_req], [20 * ab.n_desc, 4 * ab.n_req])
+        nan3 = (float("nan"),) * 3
+        lc = nan3 if args.host_no_probe else link_probe([int(cb0.blob.shape[0]) + 32, 8 * cb0.n_desc], [8 * cb0.n_desc])
+        lf = nan3 if args.host_no_probe else link_probe(
+            [int(ab.blob.shape[0]) + 32, 4 * (ab.n_desc + 1), 4 * ab.n_desc, 4 * ab.n_desc, 8 * ab.n_req, 4 * ab.n_req],
+            [20 * ab.n_desc, 4 * ab.n_req])
         # host decisions from raw replies (rl_decide_raw), 1 and `threads` threads
         import concurrent.futures as cf
         eng.submit_c(cb0)

@@ -47,6 +47,11 @@ for s in "${@:-smoke bench routed1 ls8 ls2 config1}"; do
                  --steps 20 --prefill 200 \
                  && python3 tools/copy_timeline.py /tmp/ht_$TAG/run_kernel_trace.csv /tmp/ht_$TAG/run_memory_copy_trace.csv \
                     200 500 > "$OUT/host_copy_timeline.txt" ;;
+      hctrace) mkdir -p /tmp/hc_$TAG && run hctrace 600 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/hc_$TAG -o run \
+                 --output-format csv -- python3 -u bench.py --cpu-seconds 0 --no-roofline-probe --no-kernel-times \
+                 --steps 20 --prefill 200 --host-formats compact --host-no-probe \
+                 && python3 tools/copy_timeline.py /tmp/hc_$TAG/run_kernel_trace.csv /tmp/hc_$TAG/run_memory_copy_trace.csv \
+                    160 0 > "$OUT/host_compact_timeline.txt" ;;
       strace) mkdir -p /tmp/st_$TAG && run strace 600 rocprofv3 --kernel-trace --stats -d /tmp/st_$TAG -o run \
                  --output-format csv -- python3 -u bench.py --steps 30 --warmup 5 --cpu-seconds 0 --no-host-path \
                  --no-roofline-probe --no-kernel-times \
