@@ -887,79 +887,6 @@ RL_DEV bool g_insert(const GS& g, uint32_t k, const DevRule* __restrict__ rules)
   return v == G_EMPTY;  // this position claimed the hash slot: it leads the key
 }
 
-// The lanes of one 64-position chunk whose positions share this lane's hash slot (a match-any
-// by ballots over the slot bits).
-RL_DEV uint64_t slot_match(const GS& g, uint32_t s, bool valid) {
-  uint64_t mm = __ballot(valid);
-#pragma unroll
-  for (int b = 0; b < 16; ++b) {
-    if ((g.hs >> b) <= 1u) break;  // wave-uniform
-    const bool bit = (s >> b) & 1u;
-    const uint64_t bal = __ballot(bit);
-    mm &= bit ? bal : ~bal;
-  }
-  return mm;
-}
-
-// Positions [c0, c1) (chunks of 64) appended to their keys' lists in position order, from the
-// per-slot cursors cur[] (advanced).
-RL_DEV void g_layout_chunks(const GS& g, uint16_t* cur, uint32_t c0, uint32_t c1, uint32_t m) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t lt = lanemask_lt();
-  for (uint32_t c = c0; c < c1; c += 64) {
-    const uint32_t k = c + lane;
-    const bool valid = k < m;
-    const uint32_t s = valid ? g.grp[k] : 0u;
-    const uint64_t mm = slot_match(g, s, valid);
-    uint32_t before = 0;
-    if (valid) before = cur[s];
-    __builtin_amdgcn_wave_barrier();
-    if (valid) {
-      if (lane == (uint32_t)__ffsll((unsigned long long)mm) - 1u) cur[s] = (uint16_t)(before + (uint32_t)__popcll(mm));
-      g.list[before + (uint32_t)__popcll(mm & lt)] = (uint16_t)k;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// All G_W waves (LDS path): each key's list in position order. Wave w takes the w-th quarter of
-// the chunks; waves 0..2 first count their quarter's positions per slot (LDS u16 arrays in the
-// space of g.P, which the scan fills only afterwards), the counts become each wave's starting
-// cursor per slot (start + the counts of the quarters before), then every wave lays out its
-// quarter. g.end[s] enters as the list start and leaves as its end, as with one wave.
-static_assert(3 * G_HASH * 2 <= G_CAP * 8 && G_W == 4, "layout counters in the space of s_P");
-RL_DEV void g_layout4(const GS& g, uint32_t m) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint16_t* const A = reinterpret_cast<uint16_t*>(g.P);  // [3][G_HASH]
-  uint32_t* const A32 = reinterpret_cast<uint32_t*>(g.P);
-  for (uint32_t w = tid; w < 3u * G_HASH / 2u; w += G_NT) A32[w] = 0;
-  const uint32_t nch = (m + 63u) / 64u, q = (nch + 3u) / 4u;
-  const uint32_t c0 = min(wave * q, nch) * 64u, c1 = min((wave + 1u) * q, nch) * 64u;
-  gbar<true>();
-  if (wave < 3u) {  // per-slot counts of this quarter
-    uint16_t* const cnt = A + wave * G_HASH;
-    for (uint32_t c = c0; c < c1; c += 64) {
-      const uint32_t k = c + lane;
-      const bool valid = k < m;
-      const uint32_t s = valid ? g.grp[k] : 0u;
-      const uint64_t mm = slot_match(g, s, valid);
-      if (valid && lane == (uint32_t)__ffsll((unsigned long long)mm) - 1u) cnt[s] = (uint16_t)(cnt[s] + (uint32_t)__popcll(mm));
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-  gbar<true>();
-  for (uint32_t s = tid; s < (uint32_t)G_HASH; s += G_NT) {  // counts -> cursors of waves 1..3
-    const uint32_t e0 = g.end[s], a0 = e0 + A[s], a1 = a0 + A[G_HASH + s], a2 = a1 + A[2 * G_HASH + s];
-    A[s] = (uint16_t)a0;
-    A[G_HASH + s] = (uint16_t)a1;
-    A[2 * G_HASH + s] = (uint16_t)a2;
-  }
-  gbar<true>();
-  g_layout_chunks(g, wave == 0u ? g.end : A + (wave - 1u) * G_HASH, c0, c1, m);
-  gbar<true>();
-  for (uint32_t s = tid; s < (uint32_t)G_HASH; s += G_NT) g.end[s] = A[2 * G_HASH + s];  // list ends
-}
-
 // One wave: each key's list in position order (positions [0, m), 64 at a time).
 RL_DEV void g_layout(const GS& g, uint32_t m) {
   const uint32_t lane = threadIdx.x & 63;
@@ -1224,14 +1151,7 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
   }
   gbar<LDS>();
   ST4(6);
-#ifndef RL_LAYOUT_ONE_WAVE
-  if constexpr (LDS) {
-    g_layout4(g, m);
-  } else
-#endif
-  if (wave == 0) {
-    g_layout(g, m);
-  }
+  if (wave == 0) g_layout(g, m);
   gbar<LDS>();
   ST4(7);
   g_scan<LDS>(g, m, s_agg, s_carry);
