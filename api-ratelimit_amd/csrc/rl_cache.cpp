@@ -438,7 +438,7 @@ void HipRateLimitCache::submitter() {
           add(st, c);
         }
         if (stop_ || st.nd >= s_.batch_limit) break;
-        if (!inflight.empty()) {
+        if (!inflight.empty() && s_.answer_early) {
           // while gathering, answer the batch in flight as soon as the device is done with it
           // (rl_query), not when this window closes: under light load a caller's latency is then
           // its batch's own, not that plus the next batch's window

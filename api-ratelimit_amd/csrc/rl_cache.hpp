@@ -152,6 +152,8 @@ struct HipSettings {
   uint32_t batch_limit = 1u << 16;        // HIP_BATCH_LIMIT (descriptors)
   uint64_t hash_seed = 0x5ee7ab1e5eedull;  // HIP_HASH_SEED: the same in every process of a deployment
   uint32_t max_load_permille = 750;        // HIP_TABLE_MAX_LOAD: refuse a batch past this region load
+  bool answer_early = true;                // HIP_BATCH_ANSWER_EARLY: while gathering, answer the batch in
+                                           // flight as soon as the device is done with it (rl_query)
 };
 
 // The HIP backend. Equivalent of redis.NewFixedRateLimitCacheImpl + fixedRateLimitCacheImpl.

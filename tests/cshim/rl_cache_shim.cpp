@@ -30,12 +30,14 @@ struct Shim {
 
 extern "C" {
 
-void* rlc_create(int local_cache, float near_ratio, int per_second, uint32_t window_us) {
+// flags: bit 0 = per-second split (REDIS_PERSECOND), bit 1 = no early answers (HIP_BATCH_ANSWER_EARLY=false)
+void* rlc_create(int local_cache, float near_ratio, int flags, uint32_t window_us) {
   auto* s = new Shim();
   HipSettings hs;
   hs.local_cache = local_cache != 0;
   hs.near_limit_ratio = near_ratio;
-  hs.per_second_split = per_second != 0;
+  hs.per_second_split = (flags & 1) != 0;
+  hs.answer_early = (flags & 2) == 0;
   hs.batch_window_us = window_us;
   hs.batch_limit = 1u << 14;
   try {

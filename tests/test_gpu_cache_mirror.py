@@ -37,9 +37,9 @@ def _lib():
 
 
 class Mirror:
-    def __init__(self, local_cache, window_us=0, ratio=0.8):
+    def __init__(self, local_cache, window_us=0, ratio=0.8, answer_early=True):
         self.lib = _lib()
-        self.h = self.lib.rlc_create(int(local_cache), ratio, 0, window_us)
+        self.h = self.lib.rlc_create(int(local_cache), ratio, 0 if answer_early else 2, window_us)
         assert self.h, "HipRateLimitCache construction failed"
 
     def add_rule(self, rpu, unit, key):
@@ -161,10 +161,10 @@ def test_rules_arrive_mid_stream_two_in_flight():
     T, n = 8, 220
     units = [hiprl.SECOND, hiprl.MINUTE, hiprl.HOUR]
     all_rules = [(3 + 2 * k, units[k % 3]) for k in range(40)]  # 40 distinct (L, unit) limits
-    # a gather window shorter than a batch's device time, so batch k + 1 (and its rule load) is
-    # submitted while batch k is still in flight (with a longer window the batcher answers batch
-    # k first: it polls rl_query while gathering)
-    m = Mirror(False, window_us=20)
+    # without early answers (HIP_BATCH_ANSWER_EARLY=false) batch k + 1 (and its rule load) is
+    # submitted while batch k is still in flight; with them the batcher answers batch k as soon as
+    # the device is done, so whether a load lands behind a batch in flight depends on timing
+    m = Mirror(False, window_us=150, answer_early=False)
     m.lib.rlc_batcher_stats.argtypes = [C.c_void_p, C.c_void_p]
     ids = [m.add_rule(L, u, f"rule{k}") for k, (L, u) in enumerate(all_rules)]
     now = 1_700_000_123
@@ -220,7 +220,7 @@ def test_more_than_v4_max_rules_through_do_limit():
     requests."""
     T, per_req, n_rules = 8, 4, 33000
     all_rules = [(k + 1, hiprl.SECOND) for k in range(n_rules)]
-    m = Mirror(False, window_us=100)
+    m = Mirror(False, window_us=100, answer_early=False)  # (batches in flight at the crossing: see above)
     m.lib.rlc_batcher_stats.argtypes = [C.c_void_p, C.c_void_p]
     ids = [m.add_rule(L, u, f"r{k}") for k, (L, u) in enumerate(all_rules)]
     now = 1_700_000_321
