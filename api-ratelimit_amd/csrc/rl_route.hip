@@ -214,6 +214,9 @@ constexpr uint32_t LB_SPIN_LIMIT = 1u << 22;
 // The look-back's bound (tests lower it: RL_DIAG_LB_SPIN_LIMIT, read by rl_create).
 __device__ uint32_t g_lb_spin_limit = LB_SPIN_LIMIT;
 constexpr int LB_U = 1;  // look-back words per lane per read (4: 52 us, every extra word a line)
+// (Round 4: the words owner-major instead, lb[j * nb + k], so a read of 64 blocks is 256
+// contiguous bytes, read one or four windows at a time: k_route_pack2 +7 / +17 us per 10^6
+// descriptors — 32 blocks then publish into one line.)
 __global__ __launch_bounds__(NT) void k_route_pack1(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
                                                      uint64_t seed, uint32_t origin, uint32_t n_shards, uint32_t stride,
                                                      RRec* __restrict__ send, uint32_t* __restrict__ perm,
@@ -690,15 +693,6 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
   if (tid == 0 && s_err) {  // before any owner's word of this block is published
     atomicOr(gerr, s_err);
     __threadfence();
-  }
-  if (!REPACK && tid == 0 && s_tr[0]) {
-    // into one of 8 lines (fewer same-line atomics in a row); returning atomics, their values
-    // consumed: performed before this thread publishes owner 0's look-back word below, so the
-    // last block, whose look-back transitively saw every block's word, reads every block's range
-    uint32_t* tw = tr + (size_t)(bi & 7u) * 64u;
-    const uint32_t pa = __hip_atomic_fetch_max(&tw[0], s_tr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t pb = __hip_atomic_fetch_max(&tw[1], s_tr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("" ::"v"(pa), "v"(pb));
   }
   if (!REPACK && tid == 0 && s_tr[0]) {
     // into one of 8 lines (fewer same-line atomics in a row); returning atomics, their values

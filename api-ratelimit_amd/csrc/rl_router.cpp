@@ -60,7 +60,7 @@ namespace {
 constexpr uint32_t REC = sizeof(RRec);
 constexpr uint32_t RAWB = sizeof(RawReply);
 constexpr uint32_t MAXS = RL_ROUTE_MAX_SHARDS;
-constexpr int NSLOT = 2;                   // steps in flight
+constexpr int NSLOT = 3;                   // steps in flight
 constexpr uint64_t ROUTE_HOT_EVERY = 8;    // route hot set refresh period (steps)
 constexpr uint32_t ROUTE_HOT_KEEP = 64;    // a group stays while its origin sends it >= this sum of hits per step
 static_assert(REC == RL_ROUTE_RECORD_BYTES && RAWB == sizeof(rl_raw_reply), "record layouts");
@@ -353,6 +353,10 @@ struct StepSlot {
   bool busy = false;
   bool host = false;
   bool counts_failed = false;  // every shard left after the counts exchange
+  bool replied = false;        // collective: the reply exchange and the unpack are enqueued
+  bool end_rec = false;        // ... and ev_end recorded behind them
+  hipError_t rep_he = hipSuccess;
+  hipEvent_t ev_end = nullptr; // the reply exchange (rs) and the unpack (os) of the step
   double t0 = 0;
   int32_t status[MAXS] = {};   // per shard (collective: as received from every origin / owner)
 };
@@ -374,7 +378,6 @@ struct rl_router {
   hipStream_t rs = nullptr;  // exchanges
   hipEvent_t ev_rs = nullptr;
   hipEvent_t ev_cnt = nullptr;  // the counts' host copy
-  hipEvent_t ev_end = nullptr;  // the reply exchange (rs) and the unpack (os) of the step
   std::vector<Shard> sh;
   StepSlot slot[NSLOT];
   uint64_t seq = 0, done = 0;
@@ -427,6 +430,7 @@ struct rl_router {
   int wait(rl_status* const* out, uint32_t* const* thr, bool into);
   int submit_coll(uint32_t k);
   int submit_local(uint32_t k);
+  void reply_coll(uint32_t k);
   void wait_coll(uint32_t k);
   void wait_local(uint32_t k);
   int step_result(uint32_t k);
@@ -452,12 +456,16 @@ void rl_router::free_all() {
   if (d_ag) (void)hipFree(d_ag);
   if (h_ag) (void)hipHostFree(h_ag);
   xp.reset();
-  for (hipEvent_t e : {ev_rs, ev_cnt, ev_end})
+  for (StepSlot& q : slot) {
+    if (q.ev_end) (void)hipEventDestroy(q.ev_end);
+    q.ev_end = nullptr;
+  }
+  for (hipEvent_t e : {ev_rs, ev_cnt})
     if (e) (void)hipEventDestroy(e);
   if (rs) (void)hipStreamDestroy(rs);
   d_ag = nullptr;
   h_ag = nullptr;
-  ev_rs = ev_cnt = ev_end = nullptr;
+  ev_rs = ev_cnt = nullptr;
   rs = nullptr;
 }
 
@@ -746,16 +754,17 @@ void rl_router::drain(Shard& S, ShardStep& x) {
 int rl_router::submit_owner(uint32_t s, uint32_t k, const Run& u, void* ready) {
   Shard& S = sh[s];
   ShardStep& t = S.st[k];
-  ShardStep& prev = S.st[k ^ 1u];
   for (;;) {
     const int rc = rl_submit_routed_async(S.e, t.recv + u.off, u.n, t.reply + u.off, RL_ROUTED_RAW, ready);
     if (rc != RL_ESTATE) {
       if (!rc) ++t.n_sub;
       return rc;
     }
-    if (prev.n_sub) drain(S, prev);
-    else if (t.n_sub) drain(S, t);
-    else return rc;
+    ShardStep* old = nullptr;  // the oldest step in flight (this one included) with owner batches
+    for (uint64_t q = done; q < seq && !old; ++q)
+      if (S.st[q % NSLOT].n_sub) old = &S.st[q % NSLOT];
+    if (!old) return rc;
+    drain(S, *old);
   }
 }
 
@@ -820,6 +829,18 @@ int rl_router::submit_coll(uint32_t k) {
     return 0;
   }
   note_combine(0, k);
+  // The reply exchanges of the steps before this one go first: their decides were handed to the
+  // engine one submit earlier (behind this rank's pack, so done or nearly), the caller's wait for
+  // them then returns while this step's records and decide are on their way, and its next pack
+  // runs beside this decide. (Every rank submits and waits in the same order, so every rank
+  // issues these collectives in the same order.)
+  for (uint64_t q = done; q + 1 < seq; ++q) {
+    const uint32_t kq = (uint32_t)(q % NSLOT);
+    if (slot[kq].busy && !slot[kq].counts_failed && !slot[kq].replied) {
+      reply_coll(kq);
+      if (broken) return RL_ECOMM;
+    }
+  }
   // records: to owner j this origin's section j (stride D); from origin j its count, compact
   const size_t D = cfg.max_desc;
   size_t sc[MAXS], sd[MAXS], rc[MAXS], rd[MAXS];
@@ -971,7 +992,7 @@ int rl_router::submit_local(uint32_t k) {
 int rl_router::submit(const rl_batch* batches, rl_status* const* out, uint32_t* const* thr, bool host) {
   if (broken) return fail(RL_ECOMM, "the router's communicator was aborted after a transport failure");
   const uint32_t k = (uint32_t)(seq % NSLOT);
-  if (slot[k].busy) return fail(RL_ESTATE, "two routed steps in flight: call rl_router_wait");
+  if (slot[k].busy) return fail(RL_ESTATE, "%d routed steps in flight: call rl_router_wait", NSLOT);
   if (host && !(cfg.flags & RL_ROUTER_HOST)) return fail(RL_EINVAL, "router created without RL_ROUTER_HOST");
   const uint32_t G = cfg.n_shards, nl = n_local();
   if (!coll)  // the local transport refuses a bad batch before anything moves (collective: in the counts exchange)
@@ -984,6 +1005,7 @@ int rl_router::submit(const rl_batch* batches, rl_status* const* out, uint32_t* 
   t_pack0 = slot[k].t0;
   slot[k].host = host;
   slot[k].counts_failed = false;
+  slot[k].replied = slot[k].end_rec = false;
   if (seq % ROUTE_HOT_EVERY == 0) {
     refresh_hot();
     if (broken) return RL_ECOMM;
@@ -1056,10 +1078,13 @@ int rl_router::step_result(uint32_t k) {
   return fail(code, "shard %d (%s): %s", bad, t.phase, t.msg.c_str());
 }
 
-void rl_router::wait_coll(uint32_t k) {
+// The owner's decide of step k completed, its status and replies exchanged, the origin's unpack
+// (and the host copies) enqueued behind them; slot[k].ev_end marks their end.
+void rl_router::reply_coll(uint32_t k) {
   const uint32_t G = cfg.n_shards;
   Shard& S = sh[0];
   ShardStep& t = S.st[k];
+  slot[k].replied = true;
   const double t0 = now_us();
   while (t.n_sub) drain(S, t);
   if (!t.rc_dec && !t.rc_local && fault(PH_DECIDE, 0)) {
@@ -1122,11 +1147,26 @@ void rl_router::wait_coll(uint32_t k) {
       he = hipMemcpyAsync(t.hs.h_out, t.out, (size_t)t.b.n_desc * sizeof(rl_status), hipMemcpyDeviceToHost, S.os);
     if (he == hipSuccess && t.b.n_req) he = hipMemcpyAsync(t.hs.h_thr, t.thr, (size_t)t.b.n_req * 4, hipMemcpyDeviceToHost, S.os);
   }
-  // the unpack waited for the reply exchange (ev_rs), so one event on os covers both streams;
+  // the unpack waited for the reply exchange (ev_rs), so one event on os covers both streams
+  slot[k].rep_he = he;
+  slot[k].end_rec = he == hipSuccess && hipEventRecord(slot[k].ev_end, S.os) == hipSuccess;
+  st.unpack_us = now_us() - t2;
+}
+
+void rl_router::wait_coll(uint32_t k) {
+  const uint32_t G = cfg.n_shards;
+  Shard& S = sh[0];
+  ShardStep& t = S.st[k];
+  if (!slot[k].replied) {
+    reply_coll(k);
+    if (broken) return;
+  }
+  const double t2 = now_us();
+  hipError_t he = slot[k].rep_he;
   // after a failure to enqueue, drain both streams
   hipError_t h2;
-  if (he == hipSuccess && hipEventRecord(ev_end, S.os) == hipSuccess) {
-    h2 = poll_event(ev_end);
+  if (slot[k].end_rec) {
+    h2 = poll_event(slot[k].ev_end);
     he = h2;
   } else {
     h2 = hipStreamSynchronize(rs);
@@ -1134,7 +1174,7 @@ void rl_router::wait_coll(uint32_t k) {
     if (he == hipSuccess) he = hipStreamSynchronize(S.os);
   }
   if (he == hipSuccess && fault(PH_UNPACK, 0)) he = hipErrorUnknown;
-  st.unpack_us = now_us() - t2;
+  st.unpack_us += now_us() - t2;
   for (uint32_t j = 0; j < G; ++j) slot[k].status[j] = h2 == hipSuccess ? t.h_x[2 * XS * G + G + j] : RL_EHIP;
   if (he != hipSuccess) {  // after the last collective: only this shard's results are lost
     slot[k].status[cfg.rank] = RL_EHIP;
@@ -1320,7 +1360,9 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
   if (hipStreamCreateWithFlags(&r->rs, hipStreamNonBlocking) != hipSuccess) return bail(RL_EHIP);
   if (hipEventCreateWithFlags(&r->ev_rs, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&r->ev_cnt, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&r->ev_end, hipEventDisableTiming) != hipSuccess)
+      std::any_of(std::begin(r->slot), std::end(r->slot), [](StepSlot& q) {
+        return hipEventCreateWithFlags(&q.ev_end, hipEventDisableTiming) != hipSuccess;
+      }))
     return bail(RL_EHIP);
   if (emu) {
     auto* ex = static_cast<EmuXport*>(r->xp.get());
@@ -1375,7 +1417,7 @@ int rl_router_host_acquire(rl_router* r, uint32_t shard, rl_host_batch* out) {
   if (!(r->cfg.flags & RL_ROUTER_HOST)) return r->fail(RL_EINVAL, "router created without RL_ROUTER_HOST");
   if (shard >= r->n_local()) return r->fail(RL_EINVAL, "shard %u out of range", shard);
   const uint32_t k = (uint32_t)(r->seq % NSLOT);
-  if (r->slot[k].busy) return r->fail(RL_ESTATE, "two routed steps in flight: call rl_router_wait_into");
+  if (r->slot[k].busy) return r->fail(RL_ESTATE, "%d routed steps in flight: call rl_router_wait_into", NSLOT);
   uint8_t* h = r->sh[shard].st[k].hs.h_in;
   out->prefix_blob = h;
   out->prefix_off = reinterpret_cast<uint32_t*>(h + r->o_off);

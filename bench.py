@@ -397,7 +397,7 @@ def main():
         rtr = router.ShardRouter(router.EngineShard(eng, rank, world, dev, d))
     pipelined = not routed and not args.serial
     DEPTH = min(args.depth, hiprl.MAX_IN_FLIGHT) if pipelined else 1
-    RDEPTH = max(1, min(2, args.router_depth)) if nrt is not None else 1
+    RDEPTH = max(1, min(3, args.router_depth)) if nrt is not None else 1
     outs = [torch.empty(d * 20, dtype=torch.uint8, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
     thrs = [torch.empty(d, dtype=torch.int32, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
 
