@@ -719,6 +719,10 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
     const uint32_t status = e & ERR_SPIN ? (uint32_t)RL_EDEVICE
                             : e & (ERR_BAD_INPUT | ERR_BAD_TIME) ? (uint32_t)RL_EINVAL : 0u;
     for (uint32_t j = 0; j < n_shards; ++j) x[xs * j + 1] = status;
+    // the decide statuses this rank will send in the reply exchange start as a failure word
+    // (after the counts words sent and received: rl_router.cpp's step words)
+    if (!REPACK)
+      for (uint32_t j = 0; j < n_shards; ++j) x[2u * xs * n_shards + j] = (uint32_t)RL_EHIP;
     if (!REPACK && xs >= 4u) {  // (tmin, tmax) of the batch's routed descriptors to every owner
       uint32_t mn = 0, mx = 0;
       for (uint32_t l = 0; l < 8u; ++l) {

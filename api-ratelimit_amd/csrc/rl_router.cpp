@@ -353,7 +353,8 @@ struct StepSlot {
   bool busy = false;
   bool host = false;
   bool counts_failed = false;  // every shard left after the counts exchange
-  bool replied = false;        // collective: the reply exchange and the unpack are enqueued
+  bool replied = false;        // collective: the reply exchange is enqueued
+  bool unpacked = false;       // ... and the unpack behind it
   bool end_rec = false;        // ... and ev_end recorded behind them
   hipError_t rep_he = hipSuccess;
   hipEvent_t ev_end = nullptr; // the reply exchange (rs) and the unpack (os) of the step
@@ -375,7 +376,8 @@ struct rl_router {
   rl_router_config cfg{};
   bool coll = false, broken = false;  // coll: RCCL or emulated collectives (one rank per router)
   std::unique_ptr<Xport> xp;
-  hipStream_t rs = nullptr;  // exchanges
+  hipStream_t rs = nullptr;  // exchanges (collective transports: the origin stream itself)
+  bool rs_own = true;        // rs is the router's own stream (local transport)
   hipEvent_t ev_rs = nullptr;
   hipEvent_t ev_cnt = nullptr;  // the counts' host copy
   std::vector<Shard> sh;
@@ -431,6 +433,7 @@ struct rl_router {
   int submit_coll(uint32_t k);
   int submit_local(uint32_t k);
   void reply_coll(uint32_t k);
+  void unpack_coll(uint32_t k);
   void wait_coll(uint32_t k);
   void wait_local(uint32_t k);
   int step_result(uint32_t k);
@@ -462,7 +465,7 @@ void rl_router::free_all() {
   }
   for (hipEvent_t e : {ev_rs, ev_cnt})
     if (e) (void)hipEventDestroy(e);
-  if (rs) (void)hipStreamDestroy(rs);
+  if (rs && rs_own) (void)hipStreamDestroy(rs);
   d_ag = nullptr;
   h_ag = nullptr;
   ev_rs = ev_cnt = nullptr;
@@ -565,14 +568,16 @@ void rl_router::pack(uint32_t s, uint32_t k) {
   ShardStep& t = S.st[k];
   const uint32_t G = cfg.n_shards;
   t.combined = false;
-  auto send_status = [&](int32_t rc) {  // (0, rc, no times) to every owner
+  auto send_status = [&](int32_t rc) {  // (0, rc, no times) to every owner; the decide statuses' failure words
     for (uint32_t j = 0; j < G; ++j) {
       t.h_x[XS * j] = 0;
       t.h_x[XS * j + 1] = rc;
       t.h_x[XS * j + 2] = (int32_t)0xFFFFFFFFu;
       t.h_x[XS * j + 3] = 0;
+      t.h_x[2 * XS * G + j] = RL_EHIP;
     }
     (void)hipMemcpyAsync(t.d_x, t.h_x, 4 * XS * G, hipMemcpyHostToDevice, S.os);
+    (void)hipMemcpyAsync(t.d_x + 2 * XS * G, t.h_x + 2 * XS * G, 4 * G, hipMemcpyHostToDevice, S.os);
   };
   if (t.rc_pack || !t.b.n_desc) {
     if (!t.rc_pack && t.b.n_req && t.thr) (void)hipMemsetAsync(t.thr, 0, (size_t)t.b.n_req * 4, S.os);
@@ -775,12 +780,14 @@ int rl_router::submit_coll(uint32_t k) {
   Shard& S = sh[0];
   ShardStep& t = S.st[k];
   const double t0 = t_pack0;
-  hipError_t he = hipEventRecord(S.ev, S.os);
-  if (he == hipSuccess) he = hipStreamWaitEvent(rs, S.ev, 0);
-  // the decide statuses this rank sends in the reply exchange start as a failure word: only a
-  // successful upload of its real status replaces it (wait_coll), so a failed upload cannot hand
-  // peers a stale status from an earlier step
-  if (he == hipSuccess) he = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(t.d_x + 2 * XS * G), RL_EHIP, G, rs);
+  hipError_t he = hipSuccess;
+  if (rs != S.os) {
+    he = hipEventRecord(S.ev, S.os);
+    if (he == hipSuccess) he = hipStreamWaitEvent(rs, S.ev, 0);
+  }
+  // (the decide statuses this rank sends in the reply exchange start as a failure word, written
+  // by the pack or with the host's status words: only a successful upload of its real status
+  // replaces it (reply_coll), so a failed upload cannot hand peers a stale status of an earlier step)
   ncclResult_t nr = xp->a2a(t.d_x, t.d_x + XS * G, 4 * XS, rs);
   if (nr != ncclSuccess) return nccl_fail(nr, "all-to-all(counts)");
   if (he == hipSuccess) he = hipMemcpyAsync(t.h_x, t.d_x, 8 * XS * G, hipMemcpyDeviceToHost, rs);
@@ -834,11 +841,16 @@ int rl_router::submit_coll(uint32_t k) {
   // them then returns while this step's records and decide are on their way, and its next pack
   // runs beside this decide. (Every rank submits and waits in the same order, so every rank
   // issues these collectives in the same order.)
+  // Their unpacks follow this step's records on the origin stream, so the decide of this step
+  // starts as early as it can.
   for (uint64_t q = done; q + 1 < seq; ++q) {
     const uint32_t kq = (uint32_t)(q % NSLOT);
     if (slot[kq].busy && !slot[kq].counts_failed && !slot[kq].replied) {
       reply_coll(kq);
       if (broken) return RL_ECOMM;
+#ifdef RL_ROUTER_UNPACK_FIRST
+      unpack_coll(kq);
+#endif
     }
   }
   // records: to owner j this origin's section j (stride D); from origin j its count, compact
@@ -879,6 +891,10 @@ int rl_router::submit_coll(uint32_t k) {
         break;  // (runs after a refused one are not applied, like the rest of a refused batch)
       }
     }
+  }
+  for (uint64_t q = done; q + 1 < seq; ++q) {
+    const uint32_t kq = (uint32_t)(q % NSLOT);
+    if (slot[kq].replied && !slot[kq].unpacked) unpack_coll(kq);
   }
   st.exchange_us = now_us() - t1;
   return 0;
@@ -1005,7 +1021,7 @@ int rl_router::submit(const rl_batch* batches, rl_status* const* out, uint32_t* 
   t_pack0 = slot[k].t0;
   slot[k].host = host;
   slot[k].counts_failed = false;
-  slot[k].replied = slot[k].end_rec = false;
+  slot[k].replied = slot[k].unpacked = slot[k].end_rec = false;
   if (seq % ROUTE_HOT_EVERY == 0) {
     refresh_hot();
     if (broken) return RL_ECOMM;
@@ -1078,8 +1094,7 @@ int rl_router::step_result(uint32_t k) {
   return fail(code, "shard %d (%s): %s", bad, t.phase, t.msg.c_str());
 }
 
-// The owner's decide of step k completed, its status and replies exchanged, the origin's unpack
-// (and the host copies) enqueued behind them; slot[k].ev_end marks their end.
+// The owner's decide of step k completed, its status and replies exchanged.
 void rl_router::reply_coll(uint32_t k) {
   const uint32_t G = cfg.n_shards;
   Shard& S = sh[0];
@@ -1133,9 +1148,20 @@ void rl_router::reply_coll(uint32_t k) {
     return;
   }
   hipError_t he = hipMemcpyAsync(t.h_x + 2 * XS * G + G, t.d_x + 2 * XS * G + G, 4 * G, hipMemcpyDeviceToHost, rs);
-  if (he == hipSuccess) he = hipEventRecord(ev_rs, rs);
-  if (he == hipSuccess) he = hipStreamWaitEvent(S.os, ev_rs, 0);
+  if (he == hipSuccess && rs != S.os) he = hipEventRecord(ev_rs, rs);
+  if (he == hipSuccess && rs != S.os) he = hipStreamWaitEvent(S.os, ev_rs, 0);
+  slot[k].rep_he = he;
   st.reply_us = now_us() - t1;
+}
+
+// The origin's unpack of step k (and the host copies) behind its reply exchange; slot[k].ev_end
+// marks their end.
+void rl_router::unpack_coll(uint32_t k) {
+  const uint32_t G = cfg.n_shards;
+  Shard& S = sh[0];
+  ShardStep& t = S.st[k];
+  slot[k].unpacked = true;
+  hipError_t he = slot[k].rep_he;
   const double t2 = now_us();
   if (he == hipSuccess) {  // (the owners' statuses arrived with the replies; thr zeroed by the pack)
     launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 2 * XS * G + G, cfg.max_desc, t.out, t.thr);
@@ -1161,6 +1187,7 @@ void rl_router::wait_coll(uint32_t k) {
     reply_coll(k);
     if (broken) return;
   }
+  if (!slot[k].unpacked) unpack_coll(k);
   const double t2 = now_us();
   hipError_t he = slot[k].rep_he;
   // after a failure to enqueue, drain both streams
@@ -1376,6 +1403,16 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
     if (rlx_engine_view(engines[s], &r->sh[s].v)) return bail(RL_EINVAL);
     if (r->alloc_shard(r->sh[s])) return bail(RL_EHIP);
   }
+#ifndef RL_ROUTER_TWO_STREAMS
+  if (coll) {
+    // One rank, one origin: its pack, exchanges and unpack on one stream. They form one chain
+    // anyway, and every hand-over between two streams costs ~10-15 us on the critical path
+    // (pack -> counts, replies -> unpack), more than their overlap with each other can win.
+    (void)hipStreamDestroy(r->rs);
+    r->rs = r->sh[0].os;
+    r->rs_own = false;
+  }
+#endif
   if (coll) {
     if (hipMalloc(&r->d_ag, sizeof(AgEntry) * HOT_MAX * (G + 1)) != hipSuccess ||
         hipHostMalloc(&r->h_ag, sizeof(AgEntry) * HOT_MAX * (G + 1), hipHostMallocDefault) != hipSuccess)

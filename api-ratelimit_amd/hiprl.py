@@ -735,7 +735,7 @@ class Router:
         self._check(self.lib.rl_router_step(self.h, arr, o, t), "rl_router_step")
 
     def submit(self, batches, out_ptrs, thr_ptrs):
-        """rl_router_submit: a step handed over, up to two in flight (wait() completes the oldest)."""
+        """rl_router_submit: a step handed over, up to three in flight (wait() completes the oldest)."""
         arr = (RlBatch * self.n)(*batches)
         o = (C.c_void_p * self.n)(*out_ptrs)
         t = (C.c_void_p * self.n)(*thr_ptrs)

@@ -456,10 +456,11 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
  * rl_submit_device). Decisions equal one engine deciding the origins' batches one after
  * another in shard order. */
 int rl_router_step(rl_router* r, const rl_batch* batches, rl_status* const* d_out, uint32_t* const* d_req_throttle_ms);
-/* Pipelined steps: up to two in flight. rl_router_submit packs, exchanges counts and records and
- * hands the owner its records (returns once they are queued); rl_router_wait completes the
- * oldest step (owner decisions, replies, the origin's decisions) and returns its status. With
- * two in flight, step k+1's pack and exchange overlap step k's decide on the device. Every
+/* Pipelined steps: up to three in flight. rl_router_submit packs, exchanges counts, exchanges
+ * the replies of the older steps in flight, exchanges records and hands the owner its records
+ * (returns once they are queued); rl_router_wait completes the oldest step (its origin's
+ * decisions) and returns its status. With two in flight, step k+1's pack overlaps step k's
+ * decide on the device. Every
  * shard must make the same sequence of submit / wait calls (the collectives follow it). Inputs
  * and outputs of a step stay untouched by the caller until its wait returns. */
 int rl_router_submit(rl_router* r, const rl_batch* batches, rl_status* const* d_out, uint32_t* const* d_req_throttle_ms);
