@@ -85,10 +85,12 @@ void launch_route_pack2(hipStream_t st, const rl_batch& b, const DevRule* rules,
                         const RoutePackBufs& o);
 // Origin: raw replies (back, strided like send) -> statuses and ThrottleMillis (the decisions).
 // owner_status: per owner its decide status (device; nonzero: that owner applied nothing and its
-// descriptors come out RL_CODE_UNKNOWN); stride: the owners' section size in back.
+// descriptors come out RL_CODE_UNKNOWN); stride: the owners' section size in back. h_status
+// (pinned host words, may be null): the n_shards owner statuses copied there by the kernel.
+// Launches nothing for an empty batch.
 void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* rules, const RoutePackBufs& o,
                              const RawReply* back, const int32_t* owner_status, uint32_t stride, rl_status* out,
-                             uint32_t* thr);
+                             uint32_t* thr, int32_t* h_status = nullptr, uint32_t n_shards = 0);
 constexpr uint32_t ROUTE2_BLOCK = 1024;  // descriptors per pack block
 constexpr uint32_t PERM_HOT = 0x80000000u;
 constexpr int PERM_HOT_PRE_BITS = 22;

@@ -981,8 +981,13 @@ __global__ __launch_bounds__(NT) void k_route_unpack_raw(DevBatch in, const DevR
                                                           const uint32_t* __restrict__ hot_tot,
                                                           const int32_t* __restrict__ owner_status, uint32_t stride,
                                                           rl_status* __restrict__ out, uint32_t* __restrict__ req_thr,
-                                                          uint32_t* __restrict__ zero, uint32_t zero_words) {
+                                                          uint32_t* __restrict__ zero, uint32_t zero_words,
+                                                          int32_t* h_status, uint32_t n_shards) {
   const uint32_t i = blockIdx.x * NT + threadIdx.x;
+  if (h_status && i < n_shards) {  // every owner's decide status into the pinned step words (no copy)
+    h_status[i] = owner_status[i];
+    __threadfence_system();
+  }
   // the slot's look-back words and step words, cleared for its next step (the pack of step
   // k + 2 runs behind this kernel on the same stream): no memset between steps
   for (uint32_t k = i; k < zero_words; k += gridDim.x * NT) zero[k] = 0u;
@@ -1102,11 +1107,11 @@ void launch_route_pack2(hipStream_t st, const rl_batch& b, const DevRule* rules,
 
 void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* rules, const RoutePackBufs& o,
                              const RawReply* back, const int32_t* owner_status, uint32_t stride, rl_status* out,
-                             uint32_t* thr) {
+                             uint32_t* thr, int32_t* h_status, uint32_t n_shards) {
   if (!b.n_desc) return;
   hipLaunchKernelGGL(route::k_route_unpack_raw, dim3(route_blocks(b.n_desc)), dim3(route::NT), 0, st, make_dev_batch(b),
                      rules, o.perm, back, o.bhs, o.hot_pos, o.hot_tot, owner_status, stride, out, thr, o.lb,
-                     o.zero_words);
+                     o.zero_words, h_status, n_shards);
 }
 
 hipError_t route_set_spin_limit(uint32_t v) {

@@ -387,6 +387,7 @@ struct rl_router {
   double t_pack0 = 0;        // start of the current submit's packs (host clock)
   size_t in_bytes = 0, o_off = 0, o_rule = 0, o_req = 0, o_now = 0, o_hits = 0;  // host staging layout
   AgEntry* d_ag = nullptr;   // collective hot-set allgather: [HOT_MAX] send | [G * HOT_MAX] receive
+  int32_t* d_ok = nullptr;   // [MAXS] zero words: the decide status sent when the decide succeeded
   AgEntry* h_ag = nullptr;
   int fault_phase = PH_NONE;
   uint32_t fault_shard = 0;
@@ -457,6 +458,7 @@ void rl_router::free_all() {
   }
   sh.clear();
   if (d_ag) (void)hipFree(d_ag);
+  if (d_ok) (void)hipFree(d_ok);
   if (h_ag) (void)hipHostFree(h_ag);
   xp.reset();
   for (StepSlot& q : slot) {
@@ -467,6 +469,7 @@ void rl_router::free_all() {
     if (e) (void)hipEventDestroy(e);
   if (rs && rs_own) (void)hipStreamDestroy(rs);
   d_ag = nullptr;
+  d_ok = nullptr;
   h_ag = nullptr;
   ev_rs = ev_cnt = nullptr;
   rs = nullptr;
@@ -1117,9 +1120,14 @@ void rl_router::reply_coll(uint32_t k) {
     t.phase = "replies";
   }
   for (uint32_t j = 0; j < G; ++j) hs[j] = mine;
-  // this rank's status words: a failed upload leaves the failure word submit_coll put there
-  hipError_t hu = fault(PH_STATUS, 0) ? hipErrorUnknown
-                                      : hipMemcpyAsync(t.d_x + 2 * XS * G, hs, 4 * G, hipMemcpyHostToDevice, rs);
+  // this rank's status words: a success sends the constant zero words (no upload on the step's
+  // chain); a failure is uploaded over the failure words the pack wrote, and a failed upload
+  // leaves those (so it never hands peers a stale status of an earlier step)
+  const int32_t* sw = t.d_x + 2 * XS * G;
+  hipError_t hu = hipSuccess;
+  if (fault(PH_STATUS, 0)) hu = hipErrorUnknown;
+  else if (mine) hu = hipMemcpyAsync(t.d_x + 2 * XS * G, hs, 4 * G, hipMemcpyHostToDevice, rs);
+  else sw = d_ok;
   if (hu != hipSuccess) {
     if (!t.rc_dec && !t.rc_local) {
       t.rc_local = RL_EHIP;
@@ -1140,15 +1148,15 @@ void rl_router::reply_coll(uint32_t k) {
     rd[j] = j * D * RAWB;  // perm = owner * D + position
   }
   ncclResult_t nr = xp->group_start();
-  if (nr == ncclSuccess) nr = xp->a2a(t.d_x + 2 * XS * G, t.d_x + 2 * XS * G + G, 4, rs);
+  if (nr == ncclSuccess) nr = xp->a2a(sw, t.d_x + 2 * XS * G + G, 4, rs);
   if (nr == ncclSuccess) nr = xp->a2av(t.reply, sc, sd, t.back, rc, rd, rs);
   const ncclResult_t ne = xp->group_end();
   if (nr != ncclSuccess || ne != ncclSuccess) {
     nccl_fail(nr != ncclSuccess ? nr : ne, "all-to-all(replies)");
     return;
   }
-  hipError_t he = hipMemcpyAsync(t.h_x + 2 * XS * G + G, t.d_x + 2 * XS * G + G, 4 * G, hipMemcpyDeviceToHost, rs);
-  if (he == hipSuccess && rs != S.os) he = hipEventRecord(ev_rs, rs);
+  hipError_t he = hipSuccess;
+  if (rs != S.os) he = hipEventRecord(ev_rs, rs);
   if (he == hipSuccess && rs != S.os) he = hipStreamWaitEvent(S.os, ev_rs, 0);
   slot[k].rep_he = he;
   st.reply_us = now_us() - t1;
@@ -1163,10 +1171,19 @@ void rl_router::unpack_coll(uint32_t k) {
   slot[k].unpacked = true;
   hipError_t he = slot[k].rep_he;
   const double t2 = now_us();
-  if (he == hipSuccess) {  // (the owners' statuses arrived with the replies; thr zeroed by the pack)
-    launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 2 * XS * G + G, cfg.max_desc, t.out, t.thr);
+  // (the owners' statuses arrived with the replies; thr zeroed by the pack); the unpack copies
+  // the statuses into the pinned step words, else a copy does
+  int32_t* hst = t.h_x + 2 * XS * G + G;
+  bool copied = false;
+  if (he == hipSuccess && t.b.n_desc) {
+    launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 2 * XS * G + G, cfg.max_desc, t.out, t.thr,
+                            hst, G);
     he = hipGetLastError();
-    t.zeroed = he == hipSuccess && t.b.n_desc;
+    t.zeroed = copied = he == hipSuccess;
+  }
+  if (!copied) {
+    const hipError_t hc = hipMemcpyAsync(hst, t.d_x + 2 * XS * G + G, 4 * G, hipMemcpyDeviceToHost, S.os);
+    if (he == hipSuccess) he = hc;
   }
   if (he == hipSuccess && slot[k].host) {
     if (t.b.n_desc)
@@ -1415,7 +1432,8 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
 #endif
   if (coll) {
     if (hipMalloc(&r->d_ag, sizeof(AgEntry) * HOT_MAX * (G + 1)) != hipSuccess ||
-        hipHostMalloc(&r->h_ag, sizeof(AgEntry) * HOT_MAX * (G + 1), hipHostMallocDefault) != hipSuccess)
+        hipHostMalloc(&r->h_ag, sizeof(AgEntry) * HOT_MAX * (G + 1), hipHostMallocDefault) != hipSuccess ||
+        hipMalloc(&r->d_ok, 4 * MAXS) != hipSuccess || hipMemset(r->d_ok, 0, 4 * MAXS) != hipSuccess)
       return bail(RL_EHIP);
     if (!emu) {
       auto* rx = new RcclXport();

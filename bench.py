@@ -100,7 +100,7 @@ def parse():
     ap.add_argument("--lib", type=str, default="", help=argparse.SUPPRESS)  # diagnostics: a variant library
     # tests: the routed (RCCL all-to-all) step on one rank, so the multi-GPU path runs on a 1-GPU box
     ap.add_argument("--force-routed", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--router-depth", type=int, default=2, help="routed steps in flight (rl_router_submit / _wait)")
+    ap.add_argument("--router-depth", type=int, default=3, help="routed steps in flight (rl_router_submit / _wait)")
     ap.add_argument("--no-combine", action="store_true", help="routed steps without hot-prefix combining")
     ap.add_argument("--xgmi-gbps", type=float, default=400.0,
                     help="--logical-shards estimate: all-to-all bandwidth per GPU and direction over xGMI (GB/s); "
