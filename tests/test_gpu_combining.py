@@ -202,6 +202,26 @@ def test_repack_when_a_group_is_not_one_key_string():
     r.close()
 
 
+def test_repack_over_many_pack_blocks():
+    """A repack over many pack blocks: a batch of ~75k descriptors (74 pack blocks of 1024, the
+    repack's look-back over all of them) whose hot descriptors carry two request times, after the
+    hot set formed; then a big step that combines. Bit-exact against the oracle."""
+    G, per, big = 2, 2000, 60_000
+    steps = skew_batches(G, 12, per, seed=31)
+    tail = skew_batches(G, 2, big, seed=32, t0=1_700_000_012)
+    b = tail[0][0]
+    now = b.now.copy()
+    now[b.n_req // 2:] += 1
+    tail[0][0] = hiprl.Batch(b.blob, b.off, b.rule, b.req_of, now, b.hits)
+    cap = max(b.n_desc for row in tail for b in row)
+    assert cap > 64 * 1024, cap
+    r = hiprl.Router(engines(G, cap * G, log2_slots=(20, 20, 20, 20)), max_desc=cap)
+    run_steps(r, steps + tail, new_oracle(), "sync", "repack many blocks")
+    st = r.stats()
+    assert st["repacks"] >= 1 and st["combined_steps"] >= 3, st
+    r.close()
+
+
 def test_local_cache_never_combines():
     G, per = 2, 2000
     steps = skew_batches(G, 12, per, seed=31)
