@@ -100,8 +100,8 @@ def check(o, batches, got, ctx):
         r0 += b.n_req
 
 
-def run_steps(r, steps, o, mode="sync", ctx=""):
-    """Every step through the router (sync: step; pipelined: two in flight; host: submit_host /
+def run_steps(r, steps, o, mode="sync", ctx="", depth=2):
+    """Every step through the router (sync: step; pipelined: `depth` in flight; host: submit_host /
     wait_into), each checked against the oracle in order."""
     if mode == "host":
         for s, batches in enumerate(steps):
@@ -122,7 +122,7 @@ def run_steps(r, steps, o, mode="sync", ctx=""):
         torch.cuda.synchronize()
         r.submit(*bf.args())
         pend.append((s, bf))
-        if len(pend) == 2:
+        if len(pend) == depth:
             s0, b0 = pend.pop(0)
             r.wait()
             check(o, b0.batches, b0.results(), f"{ctx} step={s0}")
@@ -158,6 +158,19 @@ def test_combining_rccl_one_rank_two_in_flight(monkeypatch):
     steps = skew_batches(1, 20, per, seed=7)
     r = hiprl.Router(engines(1, 3 * per), max_desc=3 * per, n_shards=1, rank=0, rccl_id=hiprl.Router.unique_id())
     run_steps(r, steps, new_oracle(), "pipelined", "rccl")
+    st = r.stats()
+    assert st["combined_steps"] >= 6 and st["steps"] == 20, st
+    r.close()
+
+
+def test_combining_rccl_one_rank_three_in_flight(monkeypatch):
+    """Three steps in flight (bench.py's default): every submit exchanges the replies of the two
+    older steps after its counts, and their unpacks follow its records."""
+    monkeypatch.setenv("NCCL_SOCKET_IFNAME", "lo")
+    per = 3000
+    steps = skew_batches(1, 20, per, seed=9)
+    r = hiprl.Router(engines(1, 3 * per), max_desc=3 * per, n_shards=1, rank=0, rccl_id=hiprl.Router.unique_id())
+    run_steps(r, steps, new_oracle(), "pipelined", "rccl depth 3", depth=3)
     st = r.stats()
     assert st["combined_steps"] >= 6 and st["steps"] == 20, st
     r.close()

@@ -66,8 +66,8 @@ def parallel(G, fn, timeout=600):
     assert not any(t.is_alive() for t in ths), "an emulated rank hung"
 
 
-def drive(ranks, steps, mode="pipelined"):
-    """Every step through every rank's router (pipelined: two steps in flight). Returns the
+def drive(ranks, steps, mode="pipelined", depth=2):
+    """Every step through every rank's router (pipelined: `depth` steps in flight). Returns the
     per-step Bufs and per (rank, step) error codes (None = ok)."""
     G = ranks.G
     bufs = [Bufs(row) for row in steps]
@@ -88,7 +88,7 @@ def drive(ranks, steps, mode="pipelined"):
         for s, (bs, outs, thrs) in enumerate(args):
             R.submit([bs[r]], [outs[r]], [thrs[r]])
             pend.append(s)
-            if mode == "sync" or len(pend) == 2:
+            if mode == "sync" or len(pend) == depth:
                 wait_one()
         while pend:
             wait_one()
@@ -136,6 +136,20 @@ def test_emulated_collectives_time_skew(G, combine):
         assert st[0]["combined_steps"] == 0
     # every rank ran the same step clock; some steps needed more than one owner batch
     assert len({x["step_clock"] for x in st}) == 1
+    ranks.close()
+
+
+def test_emulated_three_in_flight_time_skew():
+    """G = 4, three steps in flight (every submit exchanges the two older steps' replies after its
+    counts), skewed origin times so steps hold several owner batches and the engine's in-flight
+    limit makes submits drain older steps' batches: bit-exact."""
+    G, per = 4, 1500
+    steps = skew_times(skew_batches(G, 16, per, seed=440), seed=44)
+    ranks = EmuRanks(G, per)
+    bufs, codes = drive(ranks, steps, "pipelined", depth=3)
+    check_steps(new_oracle(), steps, bufs, codes, "emulated G=4 depth 3")
+    st = [r.stats() for r in ranks.routers]
+    assert all(x["status"] == [0] * G and x["steps"] == 16 for x in st), st
     ranks.close()
 
 
