@@ -1,16 +1,16 @@
 #!/bin/bash
 # Round 4: the router with three steps in flight. Router GPU tests, then the one-rank RCCL routed
-# step (the previous commit's library and the in-tree one, depth 3), interleaved,
+# step (the pack at 2 / 4 (in-tree) / 8 descriptors per thread, depth 3), interleaved,
 # then a kernel timeline of the in-tree library.
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/$1; mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests/test_gpu_combining.py tests/test_gpu_native_router.py \
+[ -n "${SKIP_TESTS:-}" ] || timeout -k 10 600 python -u -m pytest tests/test_gpu_combining.py tests/test_gpu_native_router.py \
   tests/test_gpu_emulated_router.py tests/test_gpu_routed_bench.py tests/test_gpu_router.py -m gpu -x -q \
   --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
 [ $rc -ne 0 ] && exit $rc
 for rep in 1 2 3; do
-  for v in prev,3 -,3; do
+  for v in pr2,3 -,3 pr8,3; do
     IFS=, read -r lib dep <<< "$v"
     lp=""; [ "$lib" != "-" ] && lp="--lib tools/variants/lib_$lib.so"
     timeout -k 10 200 python bench.py --force-routed --router-depth $dep --steps 40 --warmup 10 --cpu-seconds 0 \
