@@ -91,10 +91,7 @@ void launch_route_pack2(hipStream_t st, const rl_batch& b, const DevRule* rules,
 void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* rules, const RoutePackBufs& o,
                              const RawReply* back, const int32_t* owner_status, uint32_t stride, rl_status* out,
                              uint32_t* thr, int32_t* h_status = nullptr, uint32_t n_shards = 0);
-#ifndef RL_ROUTE_PR
-#define RL_ROUTE_PR 4
-#endif
-constexpr uint32_t ROUTE2_BLOCK = 256 * RL_ROUTE_PR;  // descriptors per pack block (256 threads x RL_ROUTE_PR)
+constexpr uint32_t ROUTE2_BLOCK = 1024;  // descriptors per pack block
 constexpr uint32_t PERM_HOT = 0x80000000u;
 constexpr int PERM_HOT_PRE_BITS = 22;
 

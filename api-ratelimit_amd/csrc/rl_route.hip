@@ -421,7 +421,7 @@ __global__ __launch_bounds__(NT) void k_route_unpack(uint32_t n, const uint32_t*
 //   k_route_pack2<repack>  the pack again without combining, only when asked (else it returns)
 //   k_route_unpack_raw     origin: raw replies -> each descriptor's post-value -> decision
 // ---------------------------------------------------------------------------------------------
-constexpr int PR = RL_ROUTE_PR;         // descriptors per thread
+constexpr int PR = 4;                   // descriptors per thread
 constexpr int PBLK = NT * PR;           // per block
 constexpr int PW = NT / 64;             // waves per block
 constexpr int PV = PR * PW;             // virtual waves per block, (round, wave) in arrival order
