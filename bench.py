@@ -18,7 +18,7 @@ Multi-GPU (torchrun, one rank per GPU): the key space is hash-sh
 shard per GPU. Every rank ingests its own 1e6-descriptor batch per step, routes each
 descriptor to the GPU owning its key with an RCCL all-to-all (32-B records; one combined
 record per hot key per origin), the owners decide, and 8-B raw replies return with the reverse
-all-to-all; the origins decide from them — weak scaling, two steps in flight. The step runs
+all-to-all; the origins decide from them — weak scaling, three steps in flight (--router-depth). The step runs
 through the C-ABI router (rl_router_submit / rl_router_wait, csrc/rl_router.cpp: the Go
 host's entry point, its own RCCL communicator); --torch-router runs the round-2 step through
 api-ratelimit_amd/router.py (torch.distributed) instead. value = descriptors decided for all ranks / max-over-ranks time.
