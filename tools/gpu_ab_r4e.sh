@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4: the router with three steps in flight. Router GPU tests, then the one-rank RCCL routed
-# step (the previous commit and the in-tree library, depth 3), interleaved,
+# step (records before the older steps' replies, and the in-tree order, depth 3), interleaved,
 # then a kernel timeline of the in-tree library.
 set -u
 export TMPDIR=/tmp
@@ -10,7 +10,7 @@ OUT=gpurun_out/$1; mkdir -p $OUT
   --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
 [ $rc -ne 0 ] && exit $rc
 for rep in 1 2 3; do
-  for v in prev,3 -,3; do
+  for v in recfirst,3 -,3; do
     IFS=, read -r lib dep <<< "$v"
     lp=""; [ "$lib" != "-" ] && lp="--lib tools/variants/lib_$lib.so"
     timeout -k 10 200 python bench.py --force-routed --router-depth $dep --steps 40 --warmup 10 --cpu-seconds 0 \
