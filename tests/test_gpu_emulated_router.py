@@ -183,6 +183,36 @@ def test_local_transport_time_skew():
     r.close()
 
 
+def faulted_step_oracle(phase, G, row, codes0, bufs0):
+    """Rank 2 failed `phase` in this step: the codes every rank returned, the outputs its peers
+    got, and an oracle that applied what the phase allows (for the steps after it)."""
+    if phase == "unpack":
+        assert codes0 == [None, None, -2, None], codes0
+    else:
+        assert codes0 == [-7, -7, -2, -7], codes0
+    o = new_oracle()
+    if phase == "records":  # owner 2 never decided
+        part = []
+        for b in row:
+            own = routing.owners_of(b, RULES, G, SEED)
+            part.append(hiprl.Batch(b.blob, b.off, np.where(own == 2, hiprl.NIL_RULE, b.rule).astype(np.uint32),
+                                    b.req_of, b.now, b.hits))
+        o.submit(routing.concat_batches(part))
+    elif phase != "pack":
+        est, ethr = o.submit(routing.concat_batches(row))
+        if phase in ("status", "replies", "decide"):
+            # every owner applied its records; owner 2's descriptors come out undecided
+            res = bufs0.results()
+            d0 = 0
+            for g, (b, (st, _)) in enumerate(zip(row, res)):
+                own = routing.owners_of(b, RULES, G, SEED)
+                want = est[d0:d0 + b.n_desc].copy()
+                want[own == 2] = (0, 0, 0, 0, 0)
+                assert np.array_equal(st, want), (phase, g)
+                d0 += b.n_desc
+    return o
+
+
 @pytest.mark.parametrize("phase", ["pack", "records", "decide", "replies", "unpack", "status"])
 def test_emulated_fault_injection(phase, monkeypatch):
     """A failure injected on rank 2 of 4 at each phase: rank 2 returns RL_EHIP naming the
@@ -196,33 +226,26 @@ def test_emulated_fault_injection(phase, monkeypatch):
     ranks = EmuRanks(G, per)
     monkeypatch.delenv("RL_ROUTER_FAULT")
     bufs, codes = drive(ranks, steps[:1], "sync")
-    got = [codes[r][0] for r in range(G)]
-    if phase == "unpack":
-        assert got == [None, None, -2, None], got
-    else:
-        assert got == [-7, -7, -2, -7], got
-    o = new_oracle()
-    if phase == "records":  # owner 2 never decided
-        part = []
-        for b in steps[0]:
-            own = routing.owners_of(b, RULES, G, SEED)
-            part.append(hiprl.Batch(b.blob, b.off, np.where(own == 2, hiprl.NIL_RULE, b.rule).astype(np.uint32),
-                                    b.req_of, b.now, b.hits))
-        o.submit(routing.concat_batches(part))
-    elif phase != "pack":
-        est, ethr = o.submit(routing.concat_batches(steps[0]))
-        if phase in ("status", "replies", "decide"):
-            # every owner applied its records; owner 2's descriptors come out undecided
-            res = bufs[0].results()
-            d0 = 0
-            for g, (b, (st, _)) in enumerate(zip(steps[0], res)):
-                own = routing.owners_of(b, RULES, G, SEED)
-                want = est[d0:d0 + b.n_desc].copy()
-                want[own == 2] = (0, 0, 0, 0, 0)
-                assert np.array_equal(st, want), (phase, g)
-                d0 += b.n_desc
+    o = faulted_step_oracle(phase, G, steps[0], [codes[r][0] for r in range(G)], bufs[0])
     b2, c2 = drive(ranks, steps[1:], "sync")
     check_steps(o, steps[1:], b2, c2, f"after {phase} fault")
+    ranks.close()
+
+
+@pytest.mark.parametrize("phase", ["pack", "records", "decide", "replies", "unpack", "status"])
+def test_emulated_fault_injection_three_in_flight(phase, monkeypatch):
+    """The same faults with three steps in flight: step 0's decide status, replies and unpack
+    are issued from step 1's submit (between its counts and its records), so a failure there
+    must land on step 0 only — step 0 returns the codes of the synchronous case, every later
+    step succeeds and equals the oracle."""
+    G, per = 4, 1000
+    steps = skew_batches(G, 6, per, seed=531)
+    monkeypatch.setenv("RL_ROUTER_FAULT", f"{phase}:2")
+    ranks = EmuRanks(G, per)
+    monkeypatch.delenv("RL_ROUTER_FAULT")
+    bufs, codes = drive(ranks, steps, "pipelined", depth=3)
+    o = faulted_step_oracle(phase, G, steps[0], [codes[r][0] for r in range(G)], bufs[0])
+    check_steps(o, steps[1:], bufs[1:], [c[1:] for c in codes], f"after {phase} fault, three in flight")
     ranks.close()
 
 
