@@ -109,7 +109,73 @@ def parse():
                     help="routed steps through router.ShardRouter (torch.distributed over RCCL) instead of the "
                          "C-ABI router rl_router_step (the Go host's path, the default)")
     ap.add_argument("--dump-stamps", type=str, default="", help=argparse.SUPPRESS)  # -DRL_STAMPS variant: raw stamps
+    ap.add_argument("--master-port", type=int, default=0,
+                    help="--gpus N > 1 without a launcher: rendezvous port of the ranks bench.py starts (0: pick one)")
+    ap.add_argument("--dry-launch", action="store_true",
+                    help="launch check: every rank joins a gloo group, prints the world it sees and exits (no GPU)")
     return ap.parse_args()
+
+
+def launch_ranks(args) -> int | None:
+    """`--gpus N` is the number of ranks, one per GPU. Under a launcher
+    (torch.distributed.run sets WORLD_SIZE) every rank checks WORLD_SIZE == N and goes on.
+    Without one and N > 1, bench.py starts the N ranks itself — a fresh
+    `torch.distributed.run --nproc-per-node N` child, started BEFORE anything in this process
+    touches the GPU (only the device count is read, which does not initialise it) — and
+    returns the child's exit code. A box with fewer than N GPUs fails here, loudly, instead
+    of measuring one GPU and calling it N. Returns None when this process is a rank."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if args.logical_shards:
+        return None
+    if env_world is not None:
+        if int(env_world) != args.gpus and not (args.gpus == 1 and args.force_routed):
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+        return None
+    if args.gpus <= 1:
+        return None
+    if not args.dry_launch:
+        import torch  # device_count() reads the device list without initialising HIP on this image
+
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, this box has {have}")
+    port = args.master_port
+    if not port:
+        import socket
+
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_launch_main(args):
+    """Every rank joins the gloo group the routed bench uses for its barrier and time max,
+    all-gathers (rank, world) and rank 0 prints what every rank saw. No GPU is touched."""
+    import torch
+    import torch.distributed as dist
+
+    world, rank = int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0"))
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+    if world > 1:
+        dist.init_process_group("gloo")
+        seen = [None] * world
+        dist.all_gather_object(seen, {"rank": rank, "world": world, "local_rank": int(os.environ["LOCAL_RANK"])})
+        t = torch.tensor([float(rank)], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.destroy_process_group()
+    else:
+        seen, t = [{"rank": 0, "world": 1, "local_rank": 0}], torch.tensor([0.0])
+    if rank == 0:
+        print(json.dumps({"dry_launch": True, "n_gpus": args.gpus, "world": world, "ranks": seen,
+                          "max_over_ranks": float(t.item())}), flush=True)
 
 
 class DeviceGen:
@@ -336,9 +402,15 @@ def logical_shards_main(args):
 
 def main():
     args = parse()
+    rc = launch_ranks(args)
+    if rc is not None:
+        return rc
+    if args.dry_launch:
+        return dry_launch_main(args)
     if args.logical_shards:
         return logical_shards_main(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    assert world == args.gpus or (args.gpus == 1 and args.force_routed), (world, args.gpus)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
@@ -783,4 +855,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)
