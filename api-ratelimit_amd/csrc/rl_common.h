@@ -241,6 +241,7 @@ struct TableDesc {
   uint32_t region_log2[8];
   uint32_t split;           // REDIS_PERSECOND: SECOND rules count in the per-second store
   uint32_t local_cache;     // local over-limit cache on
+  uint32_t lag;             // SECOND-home regions keep the previous generation live (routers' engines)
 };
 __host__ __device__ __forceinline__ bool per_second_store(const TableDesc& t, uint32_t unit) {
   return t.split && unit == RL_UNIT_SECOND;
@@ -255,32 +256,35 @@ struct RegionOcc {
 };
 
 // Slot reuse (window expiry). A slot of an older window generation is free for a key of
-// generation G. In the two SECOND-home regions (a key string lives one second there) the
-// region's previous generation stays live too — a slot is free only when its generation g
-// satisfies g + 2 < G — so a request may come up to 3 s behind the newest time the table has
-// seen (requests of several origins in rank order, a multi-GPU step whose origins' clocks
-// or batch cuts differ) and still find its key string. MINUTE/HOUR/DAY strings
-// live a minute or more per generation: there the previous generation is already that far back.
-__host__ __device__ __forceinline__ bool lazy_region(uint32_t region) { return region < 2u; }
-__host__ __device__ __forceinline__ bool slot_free_for(uint32_t g, uint32_t G, uint32_t region) {
-  return lazy_region(region) ? (g == 0u || g + 2u < G) : g < G;
+// generation G. Engines driven by a router (rl_router_create sets TableDesc.lag) keep, in the
+// two SECOND-home regions (a key string lives one second there), the region's previous
+// generation live too — a slot is free only when its generation g satisfies g + 2 < G — so a
+// request may come up to 3 s behind the newest time the table has seen (requests of several
+// origins in rank order, a multi-GPU step whose origins' clocks or batch cuts differ,
+// DESIGN.md §5c) and still find its key string. That costs the SECOND-home regions up to twice
+// the live slots against the same load limit, so a lone engine (one batcher, times in enqueue
+// order) runs without it. MINUTE/HOUR/DAY strings live a minute or more per generation: there
+// the previous generation is already that far back.
+__host__ __device__ __forceinline__ bool lazy_region(uint32_t lag, uint32_t region) { return lag && region < 2u; }
+__host__ __device__ __forceinline__ bool slot_free_for(uint32_t g, uint32_t G, bool lazy) {
+  return lazy ? (g == 0u || g + 2u < G) : g < G;
 }
-// Slots of region r that a key of generation `gen` cannot take (capacity check).
-__host__ __device__ __forceinline__ uint32_t region_live(const RegionOcc& o, uint32_t r, uint32_t gen) {
-  if (!lazy_region(r)) return o.gen < gen ? 0u : o.live;
+// Slots of a region that a key of generation `gen` cannot take (capacity check).
+__host__ __device__ __forceinline__ uint32_t region_live(const RegionOcc& o, bool lazy, uint32_t gen) {
+  if (!lazy) return o.gen < gen ? 0u : o.live;
   uint32_t v = 0;
   if (o.gen + 2u >= gen) v += o.live;  // generation o.gen >= gen - 2
   if (o.gen >= gen) v += o.prev;       // generation o.gen - 2 >= gen - 2
   return v;
 }
-// After a batch: its new slots `ins` of generation gm in region r (gm = 0: untouched).
-__host__ __device__ __forceinline__ void occ_advance(RegionOcc& o, uint32_t r, uint32_t gm, uint32_t ins) {
+// After a batch: its new slots `ins` of generation gm in a region (gm = 0: untouched).
+__host__ __device__ __forceinline__ void occ_advance(RegionOcc& o, bool lazy, uint32_t gm, uint32_t ins) {
   if (!gm) return;
   if (o.gen < gm) {
-    o.prev = (lazy_region(r) && o.gen + 2u == gm) ? o.live : 0u;
+    o.prev = (lazy && o.gen + 2u == gm) ? o.live : 0u;
     o.gen = gm;
     o.live = ins;
-  } else if (lazy_region(r) && o.gen == gm + 2u) {
+  } else if (lazy && o.gen == gm + 2u) {
     o.prev += ins;  // a batch behind the region's newest generation (its slots are generation gm)
   } else {
     o.live += ins;

@@ -98,7 +98,7 @@ RL_DEV bool table_claim_pre(const TableDesc& tab, uint64_t key, uint64_t fp_lo, 
       st_out = cur.st;
       return true;
     }
-    if (slot_free_for(g, G, key_region(key))) {  // empty for this window generation: claim it
+    if (slot_free_for(g, G, lazy_region(tab.lag, key_region(key)))) {  // empty for this window generation: claim it
       const unsigned long long want = ((unsigned long long)tag << 32) | G;
       const unsigned long long old = atomicCAS((unsigned long long*)&s->ctrl, (unsigned long long)cur.ctrl, want);
       if (old == cur.ctrl) {
@@ -197,25 +197,25 @@ RL_DEV void exotic_sequence(KeyState& s, const TableDesc& tab, const DevRule* __
 // slot. Counts are per window generation: a newer generation finds the region empty (its
 // older slots are free for it). gmax / cnt: the batch's generation and descriptor count per
 // region (0 = untouched).
-RL_DEV bool capacity_ok(const RegionOcc (&o)[8], const uint32_t* gmax, const uint32_t* cnt) {
+RL_DEV bool capacity_ok(const RegionOcc (&o)[8], const uint32_t* gmax, const uint32_t* cnt, uint32_t lag) {
   bool ok = true;
 #pragma unroll
   for (int r = 0; r < 8; ++r)
-    ok &= !cnt[r] || (uint64_t)region_live(o[r], (uint32_t)r, gmax[r]) + cnt[r] <= (uint64_t)o[r].limit;
+    ok &= !cnt[r] || (uint64_t)region_live(o[r], lazy_region(lag, (uint32_t)r), gmax[r]) + cnt[r] <= (uint64_t)o[r].limit;
   return ok;
 }
-RL_DEV bool capacity_ok(const RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* cnt) {
+RL_DEV bool capacity_ok(const RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* cnt, uint32_t lag) {
   RegionOcc o[8];  // all eight loads in flight together (no load behind a branch)
 #pragma unroll
   for (int r = 0; r < 8; ++r) o[r] = occ[r];
-  return capacity_ok(o, gmax, cnt);
+  return capacity_ok(o, gmax, cnt, lag);
 }
 // After the batch: add its new slots (one thread).
-RL_DEV void occ_update(RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* ins) {
+RL_DEV void occ_update(RegionOcc* __restrict__ occ, const uint32_t* gmax, const uint32_t* ins, uint32_t lag) {
   for (int r = 0; r < 8; ++r) {
     if (!gmax[r]) continue;  // region untouched
     RegionOcc o = occ[r];
-    occ_advance(o, (uint32_t)r, gmax[r], ins[r]);
+    occ_advance(o, lazy_region(lag, (uint32_t)r), gmax[r], ins[r]);
     occ[r] = o;
   }
 }

@@ -27,7 +27,7 @@ void launch_fingerprint(hipStream_t, const rl_batch&, const DevRule*, uint32_t, 
                         rl_status*, uint32_t*, uint32_t*, EngineCtl*);
 void launch_histogram(hipStream_t, const uint64_t*, uint32_t, int, int, uint32_t*, const uint32_t*, uint32_t*);
 void launch_hist_scan(hipStream_t, const uint32_t*, uint32_t, uint32_t*, int, const uint32_t*, const RegionOcc*,
-                      EngineCtl*);
+                      EngineCtl*, uint32_t);
 uint32_t hist_blocks(uint32_t n);
 uint32_t hist_sub_words();
 void launch_fallback_lo_keys(hipStream_t, const ItemRec*, const uint64_t*, uint32_t, uint64_t*, uint32_t*);
@@ -42,7 +42,7 @@ void launch_leader(hipStream_t, const uint64_t*, SortedRec*, const ItemRec*, con
                    const TableDesc&, SegInfo*, const uint32_t*, uint32_t, HotCand*, EngineCtl*);
 void launch_decide(hipStream_t, const SortedRec*, const SegInfo*, const DevRule*, uint32_t, rl_status*, uint32_t*, int,
                    EngineCtl*);
-void launch_occ_update(hipStream_t, RegionOcc*, EngineCtl*);
+void launch_occ_update(hipStream_t, RegionOcc*, EngineCtl*, uint32_t);
 void launch_cand_state(hipStream_t, const rl_batch&, const DevRule*, uint64_t, HotCand*, EngineCtl*);
 uint32_t route_bcnt_words(uint32_t n);
 void launch_route_pack_strided(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint64_t, uint32_t, uint32_t,
@@ -321,7 +321,7 @@ struct rl_engine {
   int submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, RReply* reply, hipEvent_t in_ev,
                     bool inputs_ready, bool host, rl_status* user_out, uint32_t* user_thr, bool raw = false);
   void occ_host_update(const EngineCtl* c) {
-    for (int r = 0; r < 8; ++r) occ_advance(occ[r], (uint32_t)r, c->gen_max[r], c->ins[r]);
+    for (int r = 0; r < 8; ++r) occ_advance(occ[r], lazy_region(tab.lag, (uint32_t)r), c->gen_max[r], c->ins[r]);
   }
   uint64_t live_total() const {
     uint64_t s = 0;
@@ -433,7 +433,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
       launch_fingerprint(stream, b, d_rules, n_rules, cfg.hash_seed, keys_orig, recs, out, thr, fp_part, ctl);
     });
     timed(KT_HISTOGRAM, [&] { launch_histogram(stream, keys_orig, n, lo_bit, npasses, hist, fp_part, fp_part2); });
-    timed(KT_HIST_SCAN, [&] { launch_hist_scan(stream, hist, n, offs, npasses, fp_part2, d_occ, ctl); });
+    timed(KT_HIST_SCAN, [&] { launch_hist_scan(stream, hist, n, offs, npasses, fp_part2, d_occ, ctl, tab.lag); });
     const uint64_t* kin = keys_orig;
     const uint32_t* vin = nullptr;
     for (int p = 0; p < npasses; ++p) {
@@ -454,7 +454,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
       launch_fingerprint(stream, b, d_rules, n_rules, cfg.hash_seed, keys_orig, recs, out, thr, fp_part, ctl);
       launch_fallback_lo_keys(stream, recs, keys_orig, n, keys_a, vals_a);
       launch_histogram(stream, keys_a, n, 0, 8, hist, fp_part, fp_part2);
-      launch_hist_scan(stream, hist, n, offs, 8, fp_part2, d_occ, ctl);
+      launch_hist_scan(stream, hist, n, offs, 8, fp_part2, d_occ, ctl, tab.lag);
     });
     const uint64_t* kin = keys_a;
     const uint32_t* vin = vals_a;
@@ -472,7 +472,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     timed(KT_FALLBACK, [&] {
       launch_gather_keys(stream, keys_orig, vals_a, n, keys_b);
       launch_histogram(stream, keys_b, n, 0, 8, hist, nullptr, nullptr);
-      launch_hist_scan(stream, hist, n, offs + 8 * hist_sub_words(), 8, nullptr, nullptr, ctl);
+      launch_hist_scan(stream, hist, n, offs + 8 * hist_sub_words(), 8, nullptr, nullptr, ctl, tab.lag);
     });
     kin = keys_b;
     vin = vals_a;
@@ -498,7 +498,7 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
   });
   timed(KT_DECIDE, [&] {
     launch_decide(stream, srec, seg, d_rules, n, out, thr, routed, ctl);
-    launch_occ_update(stream, d_occ, ctl);
+    launch_occ_update(stream, d_occ, ctl, tab.lag);
   });
   timed(KT_CAND, [&] { launch_cand_state(stream, b, d_rules, cfg.hash_seed, d_cand, ctl); });
   e = hipGetLastError();
@@ -822,6 +822,10 @@ int rlx_engine_view(rl_engine* e, EngineView* v) {
   return 0;
 }
 void rlx_engine_hot(rl_engine* e, std::vector<HotKey>& out) { out = e->hot; }
+void rlx_engine_set_lag(rl_engine* e) {
+  e->tab.lag = 1u;
+  e->cfg.flags |= RL_CFG_LAG_WINDOW;
+}
 }  // namespace rlhip
 
 extern "C" {
@@ -887,6 +891,7 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   }
   e->tab.split = c.per_second_split ? 1u : 0u;
   e->tab.local_cache = c.local_cache ? 1u : 0u;
+  e->tab.lag = (c.flags & RL_CFG_LAG_WINDOW) ? 1u : 0u;
   e->table_slots = off;
   chk(hipMalloc(&e->table, off * sizeof(Slot)));
   if (he == hipSuccess) chk(hipMemset(e->table, 0, off * sizeof(Slot)));
@@ -1340,6 +1345,19 @@ int rl_decide_raw(rl_engine* e, const rl_batch_c* b, const rl_raw_reply* raw, ui
   // before d0 or ends at or past d1 is left to the call that holds its other descriptors.
   // Requests without descriptors get 0 (the device zeroes every request's ThrottleMillis).
   auto req_at = [&](uint32_t i) { return one ? i : b->req_of[i]; };
+  // The caller's arrays are sized by n_req: every request index of the range must fall inside
+  // it and never decrease (the device takes nil-limit descriptors without looking at theirs)
+  // before anything is written.
+  if (one ? d1 > b->n_req : false)
+    return e->fail(RL_EINVAL, "rl_decide_raw: %u descriptors, one per request, but %u requests", d1, b->n_req);
+  if (!one)
+    for (uint32_t i = d0, prev = 0; i < d1; ++i) {
+      const uint32_t r = b->req_of[i];
+      if (r >= b->n_req || (i > d0 && r < prev))
+        return e->fail(RL_EINVAL, "rl_decide_raw: descriptor %u has request index %u (n_req %u, previous %u)", i, r,
+                       b->n_req, prev);
+      prev = r;
+    }
   const uint32_t r_first = req_at(d0), r_last = req_at(d1 - 1);
   const bool first_whole = d0 == 0 || req_at(d0 - 1) != r_first;
   const bool last_whole = d1 == b->n_desc || req_at(d1) != r_last;

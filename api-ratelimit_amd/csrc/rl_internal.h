@@ -50,6 +50,9 @@ struct EngineView {
   uint32_t max_batch_desc;
 };
 int rlx_engine_view(rl_engine* e, EngineView* v);
+// A router's engine keeps SECOND key strings findable up to 3 s behind its newest time
+// (TableDesc.lag, rl_common.h slot_free_for). Set by rl_router_create before the router's first step.
+void rlx_engine_set_lag(rl_engine* e);
 // The engine's current hot set (keys it owns that arrive with many descriptors per batch).
 void rlx_engine_hot(rl_engine* e, std::vector<HotKey>& out);
 

@@ -207,7 +207,8 @@ __global__ __launch_bounds__(1024) void k_histogram(const uint64_t* __restrict__
 __global__ __launch_bounds__(256) void k_hist_scan(const uint32_t* __restrict__ part, uint32_t nblocks,
                                                    uint32_t* __restrict__ sub, int npasses,
                                                    const uint32_t* __restrict__ fpart2, uint32_t fp_blocks,
-                                                   uint32_t n_all, const RegionOcc* __restrict__ occ, EngineCtl* ctl) {
+                                                   uint32_t n_all, const RegionOcc* __restrict__ occ, EngineCtl* ctl,
+                                                   uint32_t lag) {
   const uint32_t tid = threadIdx.x;
   if ((int)blockIdx.x == npasses * HIST_SUB) {
     __shared__ uint32_t shm[FP_PART_WORDS][256];
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(256) void k_hist_scan(const uint32_t* __restrict__ 
         gmax[r] = shm[FP_GMAX + r][0];
         cnt[r] = shm[FP_CNT + r][0];
       }
-      if (!capacity_ok(occ, gmax, cnt)) atomicOr(&ctl->err, ERR_TABLE_FULL);
+      if (!capacity_ok(occ, gmax, cnt, lag)) atomicOr(&ctl->err, ERR_TABLE_FULL);
     }
     return;
   }
@@ -795,7 +796,7 @@ __global__ __launch_bounds__(256) void k_cand_state(DevBatch in, const DevRule* 
 
 // k_occ_update — one thread: the batch's new slots per region into the occupancy counts
 // (the LSD pipeline; v4's last k4_group block does the same).
-__global__ void k_occ_update(RegionOcc* __restrict__ occ, EngineCtl* ctl) {
+__global__ void k_occ_update(RegionOcc* __restrict__ occ, EngineCtl* ctl, uint32_t lag) {
   const uint32_t errs = ctl->err;
   if (errs & (ERR_NEED_RESORT | ERR_SPIN | ERR_BAD_TIME | ERR_BAD_INPUT | ERR_WINDOW_SPAN | ERR_FALLBACK |
               ERR_TABLE_FULL))
@@ -807,7 +808,7 @@ __global__ void k_occ_update(RegionOcc* __restrict__ occ, EngineCtl* ctl) {
     n += ins[r];
   }
   ctl->n_inserted = n;
-  occ_update(occ, ctl->gen_max, ins);
+  occ_update(occ, ctl->gen_max, ins, lag);
 }
 
 // ---------------------------------------------------------------------------
@@ -828,10 +829,10 @@ void launch_histogram(hipStream_t st, const uint64_t* keys, uint32_t n, int lo_b
                      fpart2);
 }
 void launch_hist_scan(hipStream_t st, const uint32_t* part, uint32_t n, uint32_t* sub, int npasses,
-                      const uint32_t* fpart2, const RegionOcc* occ, EngineCtl* ctl) {
+                      const uint32_t* fpart2, const RegionOcc* occ, EngineCtl* ctl, uint32_t lag) {
   const uint32_t fpb = fpart2 ? hist_blocks(n) : 0;
   hipLaunchKernelGGL(k_hist_scan, dim3(npasses * HIST_SUB + (fpb ? 1 : 0)), dim3(256), 0, st, part, hist_blocks(n),
-                     sub, npasses, fpart2, fpb, n, occ, ctl);
+                     sub, npasses, fpart2, fpb, n, occ, ctl, lag);
 }
 uint32_t hist_sub_words() { return HIST_SUB * RADIX; }
 void launch_fallback_lo_keys(hipStream_t st, const ItemRec* recs, const uint64_t* keys_orig, uint32_t n,
@@ -865,8 +866,8 @@ void launch_cand_state(hipStream_t st, const rl_batch& b, const DevRule* rules, 
                        EngineCtl* ctl) {
   hipLaunchKernelGGL(k_cand_state, dim3(CAND_MAX / 256), dim3(256), 0, st, make_dev_batch(b), rules, seed, cand, ctl);
 }
-void launch_occ_update(hipStream_t st, RegionOcc* occ, EngineCtl* ctl) {
-  hipLaunchKernelGGL(k_occ_update, dim3(1), dim3(1), 0, st, occ, ctl);
+void launch_occ_update(hipStream_t st, RegionOcc* occ, EngineCtl* ctl, uint32_t lag) {
+  hipLaunchKernelGGL(k_occ_update, dim3(1), dim3(1), 0, st, occ, ctl, lag);
 }
 void launch_decide(hipStream_t st, const SortedRec* srec, const SegInfo* seg, const DevRule* rules, uint32_t n,
                    rl_status* out, uint32_t* req_thr, int routed, EngineCtl* ctl) {

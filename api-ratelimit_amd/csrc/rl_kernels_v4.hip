@@ -609,7 +609,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     }
     // Capacity (before any table write): every hot block computes the same verdict and
     // claims nothing when it fails; block 0 refuses the batch.
-    cap_ok = capacity_ok(oc, &s_f[FP_GMAX], &s_f[FP_CNT]);
+    cap_ok = capacity_ok(oc, &s_f[FP_GMAX], &s_f[FP_CNT], tab.lag);
     if (blockIdx.x == 0) {
       if (tid < 8) ctl->gen_min[tid] = ~s_f[FP_GMIN + tid];
       else if (tid < 16) ctl->gen_max[tid - 8] = s_f[FP_GMAX + tid - 8];
@@ -1677,7 +1677,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
     const uint32_t r = tid;
     ctl->ins[r] = s_ins[r];
     if (gm) {
-      occ_advance(ro, r, gm, s_ins[r]);
+      occ_advance(ro, lazy_region(tab.lag, r), gm, s_ins[r]);
       occ[r] = ro;
     }
   }

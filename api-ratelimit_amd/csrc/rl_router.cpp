@@ -27,8 +27,9 @@
 // request-time range. An owner decides its records origin by origin in runs whose times span at
 // most one second (the engine's window rule), so origins whose clocks or batch cuts differ by
 // seconds never make a step fail; the table keeps a SECOND key string findable for a request up
-// to 3 s behind the newest time it has seen (rl_common.h slot_free_for), and a step with an
-// origin further behind the node's step clock is refused everywhere with RL_EINVAL.
+// to 3 s behind the newest time it has seen (rl_common.h slot_free_for, RL_CFG_LAG_WINDOW); an
+// origin further behind the node's step clock is left out of the step alone (RL_ELATE on its
+// shard; every other shard's step goes ahead).
 //
 // Two steps may be in flight (rl_router_submit / rl_router_wait): step k+1's pack, counts and
 // record exchange run on the origin and exchange streams while step k's owner batch is decided
@@ -87,8 +88,10 @@ double now_us() {
 
 // Fault injection for the tests (RL_ROUTER_FAULT="phase:shard", read at create, fires once):
 // the shard behaves as if a HIP call of that phase failed.
-enum Phase { PH_NONE = 0, PH_PACK, PH_RECORDS, PH_DECIDE, PH_REPLIES, PH_UNPACK, PH_STATUS };
-const char* const kPhaseNames[] = {"", "pack", "records", "decide", "replies", "unpack", "status"};
+// "comm": the shard's communicator fails at the counts exchange (the transport aborts; every rank
+// is broken from then on).
+enum Phase { PH_NONE = 0, PH_PACK, PH_RECORDS, PH_DECIDE, PH_REPLIES, PH_UNPACK, PH_STATUS, PH_COMM };
+const char* const kPhaseNames[] = {"", "pack", "records", "decide", "replies", "unpack", "status", "comm"};
 
 // ---- collective transports ----------------------------------------------------------------
 // The three collectives a routed step uses, in bytes, on the router's exchange stream.
@@ -331,6 +334,7 @@ struct ShardStep {
   std::string msg;
   const char* phase = "";     // where msg comes from: pack, records, decide, replies, unpack, status
   bool combined = false;
+  bool late = false;          // origin batch refused (RL_ELATE): nothing sent, nothing unpacked
 };
 
 struct Shard {
@@ -360,6 +364,7 @@ struct StepSlot {
   hipEvent_t ev_end = nullptr; // the reply exchange (rs) and the unpack (os) of the step
   double t0 = 0;
   int32_t status[MAXS] = {};   // per shard (collective: as received from every origin / owner)
+  bool late[MAXS] = {};        // per origin: refused for starting too far behind the step clock
 };
 
 // A routed step's configuration words, compared across ranks at create (the owners' combining
@@ -391,6 +396,7 @@ struct rl_router {
   AgEntry* h_ag = nullptr;
   int fault_phase = PH_NONE;
   uint32_t fault_shard = 0;
+  uint64_t fault_step = 0;   // fires in a submit of step >= fault_step (or a wait after it)
   rl_router_stats st{};
   std::string err;
 
@@ -411,7 +417,7 @@ struct rl_router {
     return fail(RL_ECOMM, "%s: %s (communicator aborted)", what, w.c_str());
   }
   bool fault(int phase, uint32_t s) {
-    if (fault_phase != phase || fault_shard != s) return false;
+    if (fault_phase != phase || fault_shard != s || (fault_step && seq <= fault_step)) return false;
     fault_phase = PH_NONE;
     return true;
   }
@@ -727,22 +733,26 @@ int rl_router::check_config() {
 // The step clock after the counts: origin i's batch may start at most MAX_LAG_S seconds behind
 // the newest request time of everything before it in rank order (earlier steps included) — the
 // table keeps a SECOND key string findable that far back. Every rank computes the same verdict
-// from the same exchanged ranges; late[i] = 1 for an origin behind it. Commits the clock only
-// when the step goes ahead.
+// from the same exchanged ranges; late[i] = 1 for an origin behind it. A late origin is left out
+// of the step (its records are neither sent nor decided) and does not move the clock; the rest of
+// the step goes ahead, so one slow host fails only its own callers (a Redis cluster would decide
+// its late INCRBYs on their own; this table cannot place them exactly any more).
 bool rl_router::step_clock(uint32_t k, const uint32_t* tmin, const uint32_t* tmax, uint32_t* late) {
-  (void)k;
   uint32_t c = tclock;
   bool any = false;
   for (uint32_t i = 0; i < cfg.n_shards; ++i) {
     late[i] = 0;
+    slot[k].late[i] = false;
     if (tmin[i] > tmax[i]) continue;  // no routed descriptors
     if (c > tmin[i] + MAX_LAG_S) {
       late[i] = 1;
+      slot[k].late[i] = true;
       any = true;
+      continue;
     }
     c = std::max(c, tmax[i]);
   }
-  if (!any) tclock = c;
+  tclock = c;
   return any;
 }
 
@@ -791,6 +801,7 @@ int rl_router::submit_coll(uint32_t k) {
   // (the decide statuses this rank sends in the reply exchange start as a failure word, written
   // by the pack or with the host's status words: only a successful upload of its real status
   // replaces it (reply_coll), so a failed upload cannot hand peers a stale status of an earlier step)
+  if (fault(PH_COMM, 0)) return nccl_fail(ncclInternalError, "all-to-all(counts): injected fault (comm)");
   ncclResult_t nr = xp->a2a(t.d_x, t.d_x + XS * G, 4 * XS, rs);
   if (nr != ncclSuccess) return nccl_fail(nr, "all-to-all(counts)");
   if (he == hipSuccess) he = hipMemcpyAsync(t.h_x, t.d_x, 8 * XS * G, hipMemcpyDeviceToHost, rs);
@@ -824,14 +835,15 @@ int rl_router::submit_coll(uint32_t k) {
     uint32_t late[MAXS];
     if (step_clock(k, t.tmin, t.tmax, late)) {
       for (uint32_t j = 0; j < G; ++j)
-        if (late[j]) slot[k].status[j] = RL_EINVAL;
+        if (late[j]) t.rcv[j] = 0;  // (every rank drops the same origins: the exchanges still pair up)
       if (late[me]) {
-        t.rc_pack = RL_EINVAL;
+        for (uint32_t j = 0; j < G; ++j) t.cnt[j] = 0;
+        t.late = true;
+        ++st.late_steps;
         t.msg = "the batch's request times start more than 3 s behind the step clock (the newest time of the "
                 "origins before it); the table cannot keep SECOND keys that long";
         t.phase = "pack";
       }
-      any = true;
     }
   }
   if (any) {  // every rank saw the same status words: all leave after this exchange
@@ -933,27 +945,25 @@ int rl_router::submit_local(uint32_t k) {
   st.pack_us = now_us() - t0;
   bool any = false;
   for (uint32_t s = 0; s < G; ++s) any |= sh[s].st[k].rc_pack != 0;
-  if (!any) {
-    uint32_t late[MAXS];
-    if (step_clock(k, tmin, tmax, late)) {
-      for (uint32_t s = 0; s < G; ++s)
-        if (late[s]) {
-          ShardStep& t = sh[s].st[k];
-          t.rc_pack = slot[k].status[s] = RL_EINVAL;
-          t.msg = "the batch's request times start more than 3 s behind the step clock (the newest time of the "
-                  "origins before it); the table cannot keep SECOND keys that long";
-          t.phase = "pack";
-        }
-      any = true;
-    }
-  }
   if (any) {
     slot[k].counts_failed = true;
     return 0;
   }
+  uint32_t late[MAXS];
+  if (step_clock(k, tmin, tmax, late)) {
+    ++st.late_steps;
+    for (uint32_t s = 0; s < G; ++s)
+      if (late[s]) {
+        ShardStep& t = sh[s].st[k];
+        t.late = true;
+        t.msg = "the batch's request times start more than 3 s behind the step clock (the newest time of the "
+                "origins before it); the table cannot keep SECOND keys that long";
+        t.phase = "pack";
+      }
+  }
   for (uint32_t s = 0; s < G; ++s) {
     ShardStep& t = sh[s].st[k];
-    for (uint32_t j = 0; j < G; ++j) t.cnt[j] = (uint32_t)t.h_x[XS * j];
+    for (uint32_t j = 0; j < G; ++j) t.cnt[j] = t.late ? 0u : (uint32_t)t.h_x[XS * j];
     note_combine(s, k);
   }
   for (uint32_t j = 0; j < G; ++j) st.sent[j] = sh[0].st[k].cnt[j];
@@ -1019,7 +1029,7 @@ int rl_router::submit(const rl_batch* batches, rl_status* const* out, uint32_t* 
       if (batches[s].n_desc > cfg.max_desc)
         return fail(RL_ECAPACITY, "shard %u: batch of %u descriptors exceeds the router's max_desc %u", s,
                     batches[s].n_desc, cfg.max_desc);
-  for (uint32_t j = 0; j < MAXS; ++j) st.recv[j] = 0, st.sent[j] = 0, slot[k].status[j] = 0;
+  for (uint32_t j = 0; j < MAXS; ++j) st.recv[j] = 0, st.sent[j] = 0, slot[k].status[j] = 0, slot[k].late[j] = false;
   slot[k].t0 = now_us();
   t_pack0 = slot[k].t0;
   slot[k].host = host;
@@ -1033,6 +1043,7 @@ int rl_router::submit(const rl_batch* batches, rl_status* const* out, uint32_t* 
     Shard& S = sh[s];
     ShardStep& t = S.st[k];
     t.rc_pack = t.rc_dec = t.rc_local = 0;
+    t.late = false;
     t.msg.clear();
     t.phase = "";
     t.n_sub = t.n_runs = 0;
@@ -1083,7 +1094,17 @@ int rl_router::step_result(uint32_t k) {
   int bad = -1;
   for (uint32_t j = 0; j < G && bad < 0; ++j)
     if (st.status[j]) bad = (int)j;
-  if (bad < 0) return 0;
+  if (bad < 0) {  // every owner decided: only late origins fail, each alone
+    int late = -1;
+    for (uint32_t j = 0; j < G; ++j)
+      if (slot[k].late[j]) {
+        st.status[j] = RL_ELATE;
+        if (late < 0 && (!coll || j == cfg.rank)) late = (int)j;
+      }
+    if (late < 0) return 0;
+    const ShardStep& t = sh[coll ? 0 : late].st[k];
+    return fail(RL_ELATE, "shard %d (%s): %s", late, t.phase, t.msg.c_str());
+  }
   const int code = st.status[bad];
   for (uint32_t j = 0; j < G; ++j)
     if (st.status[j] == 0) st.status[j] = RL_EPEER;
@@ -1175,7 +1196,7 @@ void rl_router::unpack_coll(uint32_t k) {
   // the statuses into the pinned step words, else a copy does
   int32_t* hst = t.h_x + 2 * XS * G + G;
   bool copied = false;
-  if (he == hipSuccess && t.b.n_desc) {
+  if (he == hipSuccess && t.b.n_desc && !t.late) {
     launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 2 * XS * G + G, cfg.max_desc, t.out, t.thr,
                             hst, G);
     he = hipGetLastError();
@@ -1185,7 +1206,7 @@ void rl_router::unpack_coll(uint32_t k) {
     const hipError_t hc = hipMemcpyAsync(hst, t.d_x + 2 * XS * G + G, 4 * G, hipMemcpyDeviceToHost, S.os);
     if (he == hipSuccess) he = hc;
   }
-  if (he == hipSuccess && slot[k].host) {
+  if (he == hipSuccess && slot[k].host && !t.late) {
     if (t.b.n_desc)
       he = hipMemcpyAsync(t.hs.h_out, t.out, (size_t)t.b.n_desc * sizeof(rl_status), hipMemcpyDeviceToHost, S.os);
     if (he == hipSuccess && t.b.n_req) he = hipMemcpyAsync(t.hs.h_thr, t.thr, (size_t)t.b.n_req * 4, hipMemcpyDeviceToHost, S.os);
@@ -1269,12 +1290,12 @@ void rl_router::wait_local(uint32_t k) {
     int32_t* srecv = t.h_x + 2 * XS * G + G;
     for (uint32_t j = 0; j < G; ++j) srecv[j] = slot[k].status[j];
     if (hu == hipSuccess) hu = hipMemcpyAsync(t.d_x + 2 * XS * G + G, srecv, 4 * G, hipMemcpyHostToDevice, S.os);
-    if (hu == hipSuccess) {  // (thr zeroed by the pack)
+    if (hu == hipSuccess && !t.late) {  // (thr zeroed by the pack)
       launch_route_unpack_raw(S.os, t.b, S.v.rules, t.pb, t.back, t.d_x + 2 * XS * G + G, cfg.max_desc, t.out, t.thr);
       hu = hipGetLastError();
       t.zeroed = hu == hipSuccess && t.b.n_desc;
     }
-    if (hu == hipSuccess && slot[k].host) {
+    if (hu == hipSuccess && slot[k].host && !t.late) {
       if (t.b.n_desc)
         hu = hipMemcpyAsync(t.hs.h_out, t.out, (size_t)t.b.n_desc * sizeof(rl_status), hipMemcpyDeviceToHost, S.os);
       if (hu == hipSuccess && t.b.n_req)
@@ -1385,15 +1406,17 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
     r->o_hits = r->o_now + al(N * 8);
     r->in_bytes = r->o_hits + al(N * 4);
   }
-  if (const char* f = getenv("RL_ROUTER_FAULT")) {  // tests: "phase:shard"
+  if (const char* f = getenv("RL_ROUTER_FAULT")) {  // tests: "phase:shard[:step]"
     char ph[32] = {0};
-    unsigned s = 0;
-    if (sscanf(f, "%31[a-z]:%u", ph, &s) == 2)
-      for (int p = 1; p <= PH_STATUS; ++p)
+    unsigned s = 0, k = 0;
+    if (sscanf(f, "%31[a-z]:%u:%u", ph, &s, &k) >= 2) {
+      r->fault_step = k;
+      for (int p = 1; p <= PH_COMM; ++p)
         if (!strcmp(ph, kPhaseNames[p])) {
           r->fault_phase = p;
           r->fault_shard = coll ? (s == cfg->rank ? 0u : 0xFFFFFFFFu) : s;
         }
+    }
   }
   auto bail = [&](int code) {
     if (emu && r->xp) r->xp->abort();  // peers blocked in create's exchange return
@@ -1418,6 +1441,7 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
   for (uint32_t s = 0; s < n_eng; ++s) {
     r->sh[s].e = engines[s];
     if (rlx_engine_view(engines[s], &r->sh[s].v)) return bail(RL_EINVAL);
+    rlx_engine_set_lag(engines[s]);
     if (r->alloc_shard(r->sh[s])) return bail(RL_EHIP);
   }
 #ifndef RL_ROUTER_TWO_STREAMS
@@ -1535,9 +1559,16 @@ void rl_router_destroy(rl_router* r) {
   if (!r) return;
   // steps still in flight: complete them (every rank issued their collectives)
   while (!r->broken && r->done < r->seq) (void)r->wait(nullptr, nullptr, false);
+  // A broken router leaves steps unwaited: their owner batches are still queued in the engine,
+  // which outlives the router, and read and write buffers free_all releases. Complete them
+  // oldest step first (the engine's FIFO order), every slot.
   for (Shard& s : r->sh) {
-    while (s.st[0].n_sub) r->drain(s, s.st[0]);
-    while (s.st[1].n_sub) r->drain(s, s.st[1]);
+    for (uint64_t q = r->done; q < r->seq; ++q) {
+      ShardStep& x = s.st[q % NSLOT];
+      while (x.n_sub) r->drain(s, x);
+    }
+    for (ShardStep& x : s.st)
+      while (x.n_sub) r->drain(s, x);
     (void)hipStreamSynchronize(s.os);
   }
   if (r->rs) (void)hipStreamSynchronize(r->rs);

@@ -33,14 +33,15 @@ FLAG_HAS_LIMIT, FLAG_LOCAL_CACHE_HIT, FLAG_SHADOW = 1, 2, 4
 RULE_SHADOW = 0x100  # RL_RULE_SHADOW: shadow-mode rule (extension; rl_hip.h)
 
 RL_ERRORS = {-1: "RL_EINVAL", -2: "RL_EHIP", -3: "RL_ENOSPC", -4: "RL_ECAPACITY", -5: "RL_ESTATE", -6: "RL_EDEVICE",
-             -7: "RL_EPEER", -8: "RL_ECOMM"}
+             -7: "RL_EPEER", -8: "RL_ECOMM", -9: "RL_ELATE"}
 
 STATUS_DTYPE = np.dtype([("code_flags", "<u4"), ("limit_remaining", "<u4"), ("reset_s", "<u4"),
                          ("over_limit_delta", "<u4"), ("near_limit_delta", "<u4")])
 
 
 PIPELINE_FLAGS = {"v4": 0, "lsd": 1}  # rl_config.flags (RL_CFG_LSD_ONLY)
-ABI_VERSION = 5
+CFG_LAG_WINDOW = 2  # RL_CFG_LAG_WINDOW: SECOND key strings findable 3 s behind (routers' engines)
+ABI_VERSION = 6
 
 
 class RlConfig(C.Structure):
@@ -126,7 +127,7 @@ class RlRouterStats(C.Structure):
                 ("decide_us", C.c_double), ("decide_max_us", C.c_double), ("reply_us", C.c_double),
                 ("unpack_us", C.c_double), ("step_us", C.c_double), ("hot_groups", C.c_uint32), ("combined", C.c_uint32),
                 ("repacks", C.c_uint64), ("combined_steps", C.c_uint64), ("owner_batches", C.c_uint32),
-                ("step_clock", C.c_uint32)]
+                ("step_clock", C.c_uint32), ("late_steps", C.c_uint64)]
 
 
 ROUTER_ID_BYTES = 128
@@ -367,7 +368,7 @@ class Engine:
                  local_cache: bool = False, per_second_split: bool = False, max_batch_desc: int = 1 << 16,
                  max_batch_req: Optional[int] = None, max_blob_bytes: Optional[int] = None, sort_bits: int = 48,
                  hash_seed: int = 0x5EE7AB1E5EED, lib_path: Optional[os.PathLike] = None, lsd_only: bool = False,
-                 pipeline: str = "v4", max_load_permille: int = 0):
+                 pipeline: str = "v4", max_load_permille: int = 0, lag_window: bool = False):
         """pipeline: "v4" (default: tile-sorted records, hot keys decided in place, MSD buckets
         gathered and grouped in LDS) or "lsd" (radix-sort pipeline, also v4's fallback).
         lsd_only=True is pipeline="lsd". log2_slots: table slots per window generation for the
@@ -389,7 +390,7 @@ class Engine:
         cfg.max_batch_req = max_batch_req or max_batch_desc
         cfg.max_blob_bytes = max_blob_bytes or max_batch_desc * 64
         cfg.sort_bits = sort_bits
-        cfg.flags = PIPELINE_FLAGS[pipeline]
+        cfg.flags = PIPELINE_FLAGS[pipeline] | (CFG_LAG_WINDOW if lag_window else 0)
         cfg.hash_seed = hash_seed
         cfg.max_load_permille = max_load_permille
         self.cfg = cfg

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 5u
+#define RL_ABI_VERSION 6u
 
 /* rule id of a descriptor whose limit is nil ("don't check", src/limiter/cache.go:19-22) */
 #define RL_NIL_RULE 0xFFFFFFFFu
@@ -54,7 +54,10 @@ enum {
   RL_ESTATE = -5,    /* call out of order (e.g. rl_wait without rl_submit) */
   RL_EDEVICE = -6,   /* device-side fault detected (bounded spin expired) */
   RL_EPEER = -7,     /* rl_router_step: another shard failed this step (its code in rl_router_stats) */
-  RL_ECOMM = -8      /* rl_router: RCCL error */
+  RL_ECOMM = -8,     /* rl_router: RCCL error */
+  RL_ELATE = -9      /* rl_router: this shard's origin batch starts more than 3 s behind the step clock; none of
+                        its descriptors was applied (the other shards' steps went ahead: a clock-skew signal,
+                        counted in rl_router_stats.late_steps) */
 };
 
 typedef struct rl_engine rl_engine;
@@ -83,7 +86,11 @@ typedef struct rl_config {
 
 /* rl_config.flags */
 enum {
-  RL_CFG_LSD_ONLY = 1u   /* always use the LSD radix-sort pipeline (default: v4 pipeline, LSD as fallback) */
+  RL_CFG_LSD_ONLY = 1u,  /* always use the LSD radix-sort pipeline (default: v4 pipeline, LSD as fallback) */
+  RL_CFG_LAG_WINDOW = 2u /* keep a SECOND key string findable for requests up to 3 s behind the newest time the
+                            table has seen, at up to twice the SECOND regions' live slots against the same load
+                            limit. rl_router_create turns it on for its engines (origins' clocks differ); a lone
+                            engine fed in enqueue order does not need it */
 };
 
 /* One rate-limit rule: config.RateLimit.Limit (src/config/config.go:26-32). */
@@ -401,9 +408,11 @@ int rl_route_unpack(rl_engine* e, const rl_batch* device_batch, const uint32_t* 
  * ThrottleMillis words of origins whose pack ran may have been zeroed (the pack starts them at 0).
  * Request times: every origin's batch-time range travels with its counts. An owner decides its
  * records origin by origin in engine batches whose times span at most one second, so origins
- * whose clocks or batch cuts differ by seconds are exact; a step whose origin starts more than
+ * whose clocks or batch cuts differ by seconds are exact. An origin whose batch starts more than
  * 3 s behind the newest request time before it (the step clock: earlier steps and the origins
- * before it in rank order) fails on every shard with RL_EINVAL from that origin's shard. */
+ * before it in rank order) is left out of the step alone: its shard returns RL_ELATE with none of
+ * its descriptors applied, every other shard's step goes ahead (the late shard still decides the
+ * records it owns), and the clock does not move for it. */
 #define RL_ROUTER_ID_BYTES 128u
 typedef struct rl_router rl_router;
 
@@ -437,6 +446,8 @@ typedef struct rl_router_stats {
   uint32_t owner_batches;  /* last step: engine batches owner 0 (collective: this rank) decided its records in
                               (origins whose request times differ by 2 s or more go to separate batches) */
   uint32_t step_clock;     /* the newest request time of every step applied so far (unix seconds) */
+  uint64_t late_steps;     /* steps in which this rank's origin batch (local transport: any shard's) was refused
+                              with RL_ELATE */
 } rl_router_stats;
 
 /* A fresh RCCL unique id (ncclGetUniqueId), RL_ROUTER_ID_BYTES bytes. */

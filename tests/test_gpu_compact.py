@@ -163,3 +163,34 @@ def test_compact_refusals():
     assert ei.value.code == -1
     with pytest.raises(ValueError):
         hiprl.compact_batch(hiprl.Batch(b.blob, b.off, b.rule, b.req_of, b.now, np.full(b.n_req, 1 << 24, np.uint32)))
+
+
+def test_decide_raw_refuses_request_index_out_of_range():
+    """a compact batch whose trailing nil-limit descriptors carry req_of >= n_req
+    passes the device (nil descriptors never look at their request), but rl_decide_raw must not
+    read req_word or write ThrottleMillis past the caller's arrays: RL_EINVAL, nothing written.
+    A decreasing request index is refused the same way."""
+    e = hiprl.Engine(max_batch_desc=1024)
+    e.load_rules([(5, hiprl.SECOND)])
+    reqs = [("oob", [[("k", str(i))]], [0], 1, 1_700_000_001) for i in range(8)]
+    cb = hiprl.compact_batch(hiprl.build_batch(reqs))
+    n = cb.n_desc
+    # two nil descriptors past the last request, claiming requests 8 and 9 of 8
+    dw = np.concatenate([cb.desc_word, np.array([hiprl.NIL_RULE16 << 16] * 2, np.uint32)])
+    req_of = np.concatenate([np.arange(n, dtype=np.uint32), np.array([8, 9], np.uint32)])
+    bad = hiprl.CompactBatch(cb.blob, dw, cb.req_word, req_of, cb.now_base)
+    raw = np.zeros(n + 2, hiprl.RAW_DTYPE)
+    raw["flags"][n:] = hiprl.RAW_NIL
+    st = np.zeros(n + 2, hiprl.STATUS_DTYPE)
+    thr = np.full(bad.n_req + 4, 0xABCD, np.uint32)  # guard words past n_req
+    with pytest.raises(hiprl.RedisError) as ei:
+        e.decide_raw(bad, raw, 0, n + 2, st, thr)
+    assert ei.value.code == -1
+    assert np.all(thr == 0xABCD) and not st.view(np.uint32).any()
+    dec = req_of.copy()
+    dec[3], dec[4] = 4, 3
+    with pytest.raises(hiprl.RedisError):
+        e.decide_raw(hiprl.CompactBatch(cb.blob, dw, cb.req_word, dec, cb.now_base), raw, 0, n + 2, st, thr)
+    # the in-range part of the same batch is fine
+    e.decide_raw(bad, raw, 0, n, st, thr)
+    assert np.all(thr[bad.n_req:] == 0xABCD)
