@@ -189,6 +189,7 @@ struct HipRateLimitCache::Staged {
   int64_t tmin = 0, tmax = 0;
   bool one_per_req = true;  // compact: every request so far holds one descriptor (req_of implicit)
   bool failed = false;      // refused at submit: its callers already have the error
+  uint64_t seq = 0;         // gathered (and submitted) in this order
 };
 
 static int64_t compact_base(int64_t first_now) { return first_now > 0 ? first_now - 1 : 0; }
@@ -228,6 +229,7 @@ void HipRateLimitCache::add(Staged& st, const std::shared_ptr<PendingCall>& cp) 
   st.tmin = c.now < st.tmin ? c.now : st.tmin;
   st.tmax = c.now > st.tmax ? c.now : st.tmax;
   const uint32_t r = st.nr++;
+  if (trace_) trace_(c.req, st.seq, r);
   if (st.compact) {
     // one word per request: hits_addend | (now - now_base) << 24, now_base = the batch's first
     // time minus one (the batch spans < 2 s, so the delta is 0..2)
@@ -409,6 +411,7 @@ void HipRateLimitCache::submitter() {
       q_.pop_front();
     }
     Staged st;
+    st.seq = staged_seq_++;
     st.compact = compactable(*first);
     if (st.compact ? rl_host_acquire_c(eng_, &st.hc) : rl_host_acquire(eng_, &st.hb)) {
       std::vector<std::shared_ptr<PendingCall>> one{first};
@@ -710,6 +713,7 @@ void HipRoutedRateLimitCache::submitter() {
             st.tmin = lo;
             st.tmax = hi;
             const uint32_t rq = st.nr++;
+            if (trace_) trace_(c.req, seq, rq);
             hb.now[rq] = c.now;
             hb.hits_addend[rq] = c.req->HitsAddend;
             hb.prefix_off[0] = 0;

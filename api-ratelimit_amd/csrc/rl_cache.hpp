@@ -17,6 +17,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <future>
 #include <map>
 #include <memory>
@@ -141,6 +142,11 @@ class RateLimitCache {
 // One DoLimit call waiting in a micro-batcher (rl_cache.cpp).
 struct PendingCall;
 
+// Test hook of both batchers: every call's place in the serial order as it is put in a batch —
+// (the batch's / step's sequence number, the call's request position in it). The serial order
+// of one engine is (batch, position); of a routed deployment (step, rank, position).
+using TraceFn = std::function<void(const RateLimitRequest* request, uint64_t seq, uint32_t pos)>;
+
 // HIP_* settings (BACKEND_TYPE=hip)
 struct HipSettings {
   int device = 0;                         // HIP_DEVICES
@@ -179,6 +185,8 @@ class HipRateLimitCache : public RateLimitCache {
   BatcherStats batcher_stats() const {
     return {n_batches_.load(), n_loads_.load(), n_loads_inflight_.load(), n_drains_.load(), n_compact_.load()};
   }
+  // (tests) set before the first DoLimit
+  void set_trace(TraceFn f) { trace_ = std::move(f); }
 
  private:
   struct Staged;
@@ -210,6 +218,8 @@ class HipRateLimitCache : public RateLimitCache {
   // statuses of a compact batch made on the host from its raw replies (rl_decide_raw)
   std::vector<rl_status> dec_out_;
   std::vector<uint32_t> dec_thr_;
+  TraceFn trace_;
+  uint64_t staged_seq_ = 0;  // batches gathered (= submitted, in order)
 };
 
 // ---- Multi-GPU deployment ------------------------------------------------
@@ -252,6 +262,8 @@ class HipRoutedRateLimitCache : public RateLimitCache {
   RoutedStats routed_stats() const {
     return {n_steps_.load(), n_empty_.load(), n_syncs_.load(), n_rules_.load(), n_held_.load()};
   }
+  // (tests) set before the first DoLimit
+  void set_trace(TraceFn f) { trace_ = std::move(f); }
 
  private:
   struct Step;
@@ -280,6 +292,7 @@ class HipRoutedRateLimitCache : public RateLimitCache {
   std::vector<rl_rule> pending_;  // new limits seen here, not agreed yet
   std::set<std::pair<uint32_t, uint32_t>> pending_set_;
   std::atomic<uint64_t> n_steps_{0}, n_empty_{0}, n_syncs_{0}, n_rules_{0}, n_held_{0};
+  TraceFn trace_;
 };
 
 }  // namespace ratelimit

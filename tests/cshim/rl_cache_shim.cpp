@@ -3,7 +3,9 @@
 // points are C++ classes that ctypes cannot reach. Test infrastructure only: tests/
 // test_gpu_cache_mirror.py drives it with the reference's integration streams.
 #include <atomic>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -25,6 +27,17 @@ struct Shim {
   HipRateLimitCache* single = nullptr;
   HipRoutedRateLimitCache* routed = nullptr;
   std::string err;
+  // serial-order trace (rlc_trace_on): tag of each request in flight, and (tag, seq, pos) per call
+  std::mutex tmu;
+  std::map<const RateLimitRequest*, uint64_t> tags;
+  std::vector<uint64_t> trace;
+  void on_trace(const RateLimitRequest* r, uint64_t seq, uint32_t pos) {
+    std::lock_guard<std::mutex> g(tmu);
+    auto it = tags.find(r);
+    trace.push_back(it == tags.end() ? ~0ull : it->second);
+    trace.push_back(seq);
+    trace.push_back(pos);
+  }
 };
 }  // namespace
 
@@ -108,10 +121,32 @@ int rlc_add_rule(void* p, uint32_t rpu, uint32_t unit, const char* key) {
 // limit rule[i] (an rlc_add_rule index, -1 = nil). out[4 * i ..]: code, LimitRemaining,
 // CurrentLimit != nil, DurationUntilReset seconds. Returns 0, or -1 with rlc_error set
 // (a RedisError from the backend).
+int rlc_do_limit_tagged(void* p, uint64_t tag, const char* domain, uint32_t n_desc, const uint32_t* n_entries,
+                        const char* const* keys, const char* const* values, const int32_t* rule, uint32_t hits,
+                        uint32_t* out, uint32_t* throttle);
 int rlc_do_limit(void* p, const char* domain, uint32_t n_desc, const uint32_t* n_entries, const char* const* keys,
                  const char* const* values, const int32_t* rule, uint32_t hits, uint32_t* out, uint32_t* throttle) {
+  return rlc_do_limit_tagged(p, ~0ull, domain, n_desc, n_entries, keys, values, rule, hits, out, throttle);
+}
+
+// rlc_do_limit with a caller's tag: the trace (rlc_trace_on) names the call by it.
+int rlc_do_limit_tagged(void* p, uint64_t tag, const char* domain, uint32_t n_desc, const uint32_t* n_entries,
+                        const char* const* keys, const char* const* values, const int32_t* rule, uint32_t hits,
+                        uint32_t* out, uint32_t* throttle) {
   auto* s = static_cast<Shim*>(p);
   RateLimitRequest req;
+  struct Tagged {
+    Shim* s;
+    const RateLimitRequest* r;
+    Tagged(Shim* s_, const RateLimitRequest* r_, uint64_t t) : s(s_), r(r_) {
+      std::lock_guard<std::mutex> g(s->tmu);
+      s->tags[r] = t;
+    }
+    ~Tagged() {
+      std::lock_guard<std::mutex> g(s->tmu);
+      s->tags.erase(r);
+    }
+  } tagged(s, &req, tag);
   req.Domain = domain;
   req.HitsAddend = hits;
   std::vector<std::shared_ptr<RateLimit>> limits(n_desc);
@@ -150,6 +185,24 @@ void rlc_stats(void* p, int rule, uint64_t* out) {
 }
 
 const char* rlc_error(void* p) { return static_cast<Shim*>(p)->err.c_str(); }
+
+// Record every call's place in the serial order (HipRateLimitCache / HipRoutedRateLimitCache
+// set_trace): before the first DoLimit.
+void rlc_trace_on(void* p) {
+  auto* s = static_cast<Shim*>(p);
+  TraceFn f = [s](const RateLimitRequest* r, uint64_t seq, uint32_t pos) { s->on_trace(r, seq, pos); };
+  if (s->single) s->single->set_trace(f);
+  if (s->routed) s->routed->set_trace(f);
+}
+// The trace so far: up to max (tag, seq, pos) triples into out; returns how many there are.
+uint32_t rlc_trace(void* p, uint64_t* out, uint32_t max) {
+  auto* s = static_cast<Shim*>(p);
+  std::lock_guard<std::mutex> g(s->tmu);
+  const uint32_t n = (uint32_t)(s->trace.size() / 3);
+  for (uint32_t i = 0; i < n && i < max; ++i)
+    for (int k = 0; k < 3; ++k) out[3 * i + k] = s->trace[3 * i + k];
+  return n;
+}
 
 void rlc_flush(void* p) { static_cast<Shim*>(p)->cache->Flush(); }
 

@@ -406,3 +406,152 @@ def test_routed_batcher_g4_uneven_arrival_new_rules_mid_stream():
     assert all(s[2] >= 2 and s[3] == len(used) for s in rstats), rstats  # one agreed table everywhere
     assert sum(s[4] for s in rstats) > 0, rstats      # calls waited for a rule agreement
     _parallel(G, lambda r: lib.rlc_destroy(hs[r]))  # collective: every rank agrees to stop
+
+
+# ---- shared keys, replayed in the batchers' own serial order (VERDICT r4 #2b) -----------------
+def _trace_lib(lib):
+    lib.rlc_do_limit_tagged.argtypes = [C.c_void_p, C.c_uint64, C.c_char_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+    lib.rlc_do_limit_tagged.restype = C.c_int
+    lib.rlc_trace_on.argtypes = [C.c_void_p]
+    lib.rlc_trace.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32]
+    lib.rlc_trace.restype = C.c_uint32
+    return lib
+
+
+def _do_tagged(m, tag, domain, descs, rules, hits):
+    n = len(descs)
+    ne = (C.c_uint32 * max(1, n))(*[len(d) for d in descs])
+    flat = [e for d in descs for e in d]
+    keys = (C.c_char_p * max(1, len(flat)))(*[k.encode() for k, _ in flat])
+    vals = (C.c_char_p * max(1, len(flat)))(*[v.encode() for _, v in flat])
+    rl = (C.c_int32 * max(1, n))(*[-1 if r is None else r for r in rules])
+    out = (C.c_uint32 * (4 * max(1, n)))()
+    thr = C.c_uint32()
+    rc = m.lib.rlc_do_limit_tagged(m.h, tag, domain.encode(), n, ne, keys, vals, rl, hits, out, C.byref(thr))
+    if rc:
+        raise hiprl.RedisError(m.lib.rlc_error(m.h).decode())
+    return [tuple(out[4 * i:4 * i + 4]) for i in range(n)], thr.value
+
+
+def _trace(m, n):
+    buf = (C.c_uint64 * (3 * n))()
+    got = m.lib.rlc_trace(m.h, buf, n)
+    assert got == n, (got, n)
+    return {int(buf[3 * i]): (int(buf[3 * i + 1]), int(buf[3 * i + 2])) for i in range(n)}
+
+
+def _shared_requests(rng, n_calls, n_rules, now, keys=6):
+    """Requests on a handful of keys shared by every caller (and rank): 1-3 descriptors, some
+    duplicated inside a request, a few nil limits, hits 0..3."""
+    out = []
+    for _ in range(n_calls):
+        nd = 1 + int(rng.integers(0, 3))
+        descs = [[("k", str(int(rng.integers(0, keys))))] for _ in range(nd)]
+        if nd > 1 and rng.random() < 0.3:
+            descs[-1] = descs[0]
+        rr = [int(rng.integers(0, n_rules)) if rng.random() < 0.92 else None for _ in range(nd)]
+        out.append(("shared", descs, rr, int(rng.integers(0, 4)), now))
+    return out
+
+
+def _replay(order, calls, res, rules, local_cache):
+    """One oracle over every call in the traced serial order: each call's statuses and
+    ThrottleMillis must be the oracle's for that call."""
+    o = oracle.Oracle(local_cache=local_cache)
+    o.load_rules(rules)
+    for tag in order:
+        d, de, ru, h, tq = calls[tag]
+        st, thr = o.submit(hiprl.build_batch([(d, de, [hiprl.NIL_RULE if x is None else x for x in ru], h, tq)]))
+        got, gthr = res[tag]
+        for k, g in enumerate(got):
+            want = (int(st["code_flags"][k]) & 0xFF, int(st["limit_remaining"][k]), ru[k] is not None,
+                    int(st["reset_s"][k]) if ru[k] is not None else 0)
+            assert (g[0], g[1], bool(g[2]), g[3] if ru[k] is not None else 0) == want, (tag, k, got, want)
+        assert gthr == int(thr[0]), tag
+
+
+@pytest.mark.parametrize("local_cache", [False, True])
+def test_batcher_shared_keys_traced_order(local_cache):
+    """The single-GPU batcher with 12 concurrent callers all hitting the same 6 keys (so the
+    order in which the batcher interleaves them decides every counter): each call's answer
+    equals one serial oracle replaying the calls in the batcher's own (batch, position) order."""
+    T, n = 12, 120
+    m = Mirror(local_cache, window_us=150)
+    _trace_lib(m.lib)
+    m.lib.rlc_trace_on(m.h)
+    rules = [(6, hiprl.SECOND), (40, hiprl.MINUTE), (500, hiprl.HOUR)]
+    ids = [m.add_rule(L, u, f"r{k}") for k, (L, u) in enumerate(rules)]
+    now = 1_700_000_311
+    m.lib.rlc_set_time(m.h, now)
+    rng = np.random.default_rng(11)
+    calls = {}
+    for t in range(T):
+        for q, c in enumerate(_shared_requests(rng, n, len(rules), now)):
+            calls[t * n + q] = c
+    res = {}
+
+    def caller(t):
+        for q in range(n):
+            d, de, ru, h, _ = calls[t * n + q]
+            res[t * n + q] = _do_tagged(m, t * n + q, d, de, [None if x is None else ids[x] for x in ru], h)
+
+    _parallel(T, caller)
+    m.lib.rlc_flush(m.h)
+    tr = _trace(m, T * n)
+    order = sorted(tr, key=lambda tag: tr[tag])
+    assert len({tr[t][0] for t in order}) > 4  # many batches, each mixing callers
+    _replay(order, calls, res, rules, local_cache)
+    m.close()
+
+
+@pytest.mark.parametrize("local_cache", [False, True])
+def test_routed_batcher_g4_shared_keys_traced_order(local_cache):
+    """the multi-GPU batcher with keys SHARED across callers and ranks (the
+    case where a batcher or router ordering bug shows): G = 4 emulated ranks, 6 callers each, all
+    on the same 6 keys. Each rank traces every call's (step, position); the serial order of the
+    deployment is (step, rank, position) and one oracle replaying every rank's calls in it must
+    give every call's answer."""
+    G, T, n = 4, 6, 60
+    lib = _trace_lib(_lib())
+    lib.rlc_create_routed.argtypes = [C.c_uint32, C.c_uint32, C.c_char_p, C.c_int, C.c_int, C.c_uint32,
+                                      C.c_uint32, C.c_uint32]
+    lib.rlc_create_routed.restype = C.c_void_p
+    wid = hiprl.Router.emu_world(G)
+    hs = [None] * G
+    _parallel(G, lambda r: hs.__setitem__(r, lib.rlc_create_routed(G, r, wid, 1, int(local_cache), 300, 8, 4096)))
+    assert all(hs), hs
+    ms = [RoutedMirror(lib, h) for h in hs]
+    rules = [(8, hiprl.SECOND), (60, hiprl.MINUTE), (700, hiprl.HOUR)]
+    ids = [[m.add_rule(L, u, f"r{k}") for k, (L, u) in enumerate(rules)] for m in ms]
+    now = 1_700_000_517
+    for m in ms:
+        lib.rlc_set_time(m.h, now)
+        lib.rlc_trace_on(m.h)
+    rng = np.random.default_rng(23)
+    calls = {}
+    for r in range(G):
+        for t in range(T):
+            for q, c in enumerate(_shared_requests(rng, n, len(rules), now)):
+                calls[(r * T + t) * n + q] = c
+    res = {}
+
+    def caller(i):
+        r, t = divmod(i, T)
+        for q in range(n):
+            tag = (r * T + t) * n + q
+            d, de, ru, h, _ = calls[tag]
+            res[tag] = _do_tagged(ms[r], tag, d, de, [None if x is None else ids[r][x] for x in ru], h)
+
+    _parallel(G * T, caller)
+    for m in ms:
+        lib.rlc_flush(m.h)
+    place = {}
+    for r, m in enumerate(ms):
+        for tag, (step, pos) in _trace(m, T * n).items():
+            assert tag // (T * n) == r
+            place[tag] = (step, r, pos)
+    order = sorted(place, key=lambda tag: place[tag])
+    assert len({place[t][0] for t in order}) > 3
+    _replay(order, calls, res, rules, local_cache)
+    _parallel(G, lambda r: lib.rlc_destroy(hs[r]))
