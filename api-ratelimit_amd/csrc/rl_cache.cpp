@@ -113,10 +113,34 @@ void answer(PendingCall& c, const rl_status* out, uint32_t thr) {
   c.done.set_value();
 }
 
+// EXPIRATION_JITTER_MAX_SECONDS: the settings' jitter source, or a seeded Int63n one (the
+// reference seeds its lockedSource with the start time, runner.go / utils.NewLockedSource).
+bool setup_jitter(HipSettings& s) {
+  if (s.expiration_jitter_max_seconds <= 0) return false;
+  if (s.expiration_jitter_max_seconds > 65536)
+    throw RedisError("EXPIRATION_JITTER_MAX_SECONDS above 65536 (rl_batch.ttl_jitter is 16-bit)");
+  if (!s.jitter_rand) {
+    auto state = std::make_shared<std::pair<std::mutex, uint64_t>>();
+    state->second = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    s.jitter_rand = [state](int64_t n) {
+      std::lock_guard<std::mutex> g(state->first);
+      uint64_t z = (state->second += 0x9E3779B97F4A7C15ull);  // splitmix64
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      z ^= z >> 31;
+      return (int64_t)(z % (uint64_t)n);
+    };
+  }
+  return true;
+}
+// One draw: expirationSeconds += JitterRand.Int63n(max)  fixed_cache_impl.go:69-72
+uint16_t draw_jitter(const HipSettings& s) { return (uint16_t)s.jitter_rand(s.expiration_jitter_max_seconds); }
+
 }  // namespace
 
 HipRateLimitCache::HipRateLimitCache(const HipSettings& s, std::shared_ptr<TimeSource> ts)
     : s_(s), ts_(std::move(ts)) {
+  jitter_ = setup_jitter(s_);
   rl_config c;
   memset(&c, 0, sizeof c);
   c.struct_size = sizeof c;
@@ -243,6 +267,7 @@ void HipRateLimitCache::add(Staged& st, const std::shared_ptr<PendingCall>& cp) 
       const uint32_t rid = lim ? rule_id(lim->Limit, lim->ShadowMode) : RL_NIL_RULE16;
       st.hc.desc_word[st.nd] = (uint32_t)c.prefix[i].size() | rid << 16;
       st.hc.req_of[st.nd] = r;  // (sent only when some request holds several descriptors)
+      if (jitter_) st.hc.ttl_jitter[st.nd] = lim ? draw_jitter(s_) : 0;
       ++st.nd;
     }
     st.calls.push_back(cp);
@@ -257,6 +282,7 @@ void HipRateLimitCache::add(Staged& st, const std::shared_ptr<PendingCall>& cp) 
     st.nb += (uint32_t)c.prefix[i].size();
     st.hb.rule_id[st.nd] = lim ? rule_id(lim->Limit, lim->ShadowMode) : RL_NIL_RULE;
     st.hb.req_of[st.nd] = r;
+    if (jitter_) st.hb.ttl_jitter[st.nd] = lim ? draw_jitter(s_) : 0;
     ++st.nd;
     st.hb.prefix_off[st.nd] = st.nb;
   }
@@ -309,6 +335,7 @@ void HipRateLimitCache::submit(Staged& st, std::deque<Staged>& inflight) {
       b.desc_word = st.hc.desc_word;
       b.req_word = st.hc.req_word;
       b.req_of = st.one_per_req ? nullptr : st.hc.req_of;
+      b.ttl_jitter = jitter_ ? st.hc.ttl_jitter : nullptr;
       rc = rl_submit_c(eng_, &b);  // raw replies stay in the slot until rl_wait_raw_view
       if (!rc) n_batches_ += 1, n_compact_ += 1;
     } else if (!rc) {
@@ -323,6 +350,7 @@ void HipRateLimitCache::submit(Staged& st, std::deque<Staged>& inflight) {
       b.req_of = st.hb.req_of;
       b.now = st.hb.now;
       b.hits_addend = st.hb.hits_addend;
+      b.ttl_jitter = jitter_ ? st.hb.ttl_jitter : nullptr;
       rc = rl_submit(eng_, &b, nullptr, nullptr);  // results stay in the slot until rl_wait_view
       if (!rc) n_batches_ += 1;
     }
@@ -495,6 +523,7 @@ std::pair<uint32_t, uint32_t> limit_key(const RateLimit& r) {
 HipRoutedRateLimitCache::HipRoutedRateLimitCache(const HipSettings& s, const HipRoutedSettings& r,
                                                  std::shared_ptr<TimeSource> ts)
     : s_(s), r_(r), ts_(std::move(ts)) {
+  jitter_ = setup_jitter(s_);
   if (r.id.size() != RL_ROUTER_ID_BYTES) throw RedisError("routed cache: id must hold RL_ROUTER_ID_BYTES bytes");
   rl_config c;
   memset(&c, 0, sizeof c);
@@ -723,6 +752,7 @@ void HipRoutedRateLimitCache::submitter() {
               st.nb += (uint32_t)c.prefix[i].size();
               hb.rule_id[st.nd] = lim ? ids_.at(limit_key(*lim)) : RL_NIL_RULE;
               hb.req_of[st.nd] = rq;
+              if (jitter_) hb.ttl_jitter[st.nd] = lim ? draw_jitter(s_) : 0;
               ++st.nd;
               hb.prefix_off[st.nd] = st.nb;
             }
@@ -746,6 +776,7 @@ void HipRoutedRateLimitCache::submitter() {
         b.req_of = hb.req_of;
         b.now = hb.now;
         b.hits_addend = hb.hits_addend;
+        b.ttl_jitter = jitter_ ? hb.ttl_jitter : nullptr;
       } else {
         n_empty_ += 1;  // an idle rank still takes part in the step's collectives
       }

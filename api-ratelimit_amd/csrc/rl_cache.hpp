@@ -160,6 +160,12 @@ struct HipSettings {
   uint32_t max_load_permille = 750;        // HIP_TABLE_MAX_LOAD: refuse a batch past this region load
   bool answer_early = true;                // HIP_BATCH_ANSWER_EARLY: while gathering, answer the batch in
                                            // flight as soon as the device is done with it (rl_query)
+  // EXPIRATION_JITTER_MAX_SECONDS (settings.go:43, default 300; at most 65536 here): every INCRBY's
+  // EXPIRE gets JitterRand.Int63n(max) more seconds (fixed_cache_impl.go:69-72). The batcher draws
+  // one value per descriptor with a limit, in enqueue order, from jitter_rand (a seeded Int63n
+  // source by default; the reference's NewFixedRateLimitCacheImpl takes its jitterRand too).
+  int64_t expiration_jitter_max_seconds = 0;
+  std::function<int64_t(int64_t)> jitter_rand;  // Int63n(n): uniform in [0, n)
 };
 
 // The HIP backend. Equivalent of redis.NewFixedRateLimitCacheImpl + fixedRateLimitCacheImpl.
@@ -219,6 +225,7 @@ class HipRateLimitCache : public RateLimitCache {
   std::vector<rl_status> dec_out_;
   std::vector<uint32_t> dec_thr_;
   TraceFn trace_;
+  bool jitter_ = false;
   uint64_t staged_seq_ = 0;  // batches gathered (= submitted, in order)
 };
 
@@ -293,6 +300,7 @@ class HipRoutedRateLimitCache : public RateLimitCache {
   std::set<std::pair<uint32_t, uint32_t>> pending_set_;
   std::atomic<uint64_t> n_steps_{0}, n_empty_{0}, n_syncs_{0}, n_rules_{0}, n_held_{0};
   TraceFn trace_;
+  bool jitter_ = false;
 };
 
 }  // namespace ratelimit

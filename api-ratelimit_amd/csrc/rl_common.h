@@ -95,7 +95,7 @@ struct __attribute__((aligned(16))) ItemRec {
   uint32_t h;        // max(1, hits_addend)
   int32_t now_mod;   // now - window_start (CalculateReset: div - now % div)
   uint32_t gen;      // home window index + 1 (0 = never-used slot)
-  uint32_t pad;
+  uint32_t jit;      // EXPIRE jitter, seconds (rl_batch.ttl_jitter / the routed record's)
 };
 
 // Per-descriptor record in sorted order written by the LSD scan kernel (32 B).
@@ -343,10 +343,13 @@ constexpr int DFR_CTR = 29;               // EngineCtl::tile_ctr[DFR_CTR][0] cou
 struct __attribute__((aligned(16))) RRec {
   uint64_t a, b;     // fingerprint lane state after the key-prefix bytes
   uint32_t now;      // request time, unix seconds (<= MAX_NOW, checked at the origin)
-  uint32_t rule;     // rule id (every shard loads the same rule table)
+  uint32_t rule;     // rule id (< 0xFFFF; every shard loads the same rule table) | EXPIRE jitter << 16
   uint32_t h;        // max(1, hits_addend)
   uint32_t greq;     // global request id
 };
+__host__ __device__ __forceinline__ uint32_t rrec_rule(uint32_t w) { return w == 0xFFFFFFFFu ? w : (w & 0xFFFFu); }
+__host__ __device__ __forceinline__ uint32_t rrec_jit(uint32_t w) { return w == 0xFFFFFFFFu ? 0u : (w >> 16); }
+constexpr uint32_t RREC_MAX_RULE = 0xFFFFu;  // routed rule ids stay below it (the jitter shares the word)
 // Owner shard of a key: a mix of the prefix lanes, so every window of a key (and every
 // origin) maps to the same GPU. Multiply-shift keeps it uniform for any shard count.
 __host__ __device__ __forceinline__ uint32_t route_owner(uint64_t a, uint64_t b, uint32_t n_shards) {
@@ -382,10 +385,11 @@ constexpr uint32_t RL_BATCH_RAW = 2u;  // raw replies (RawReply per descriptor /
 
 // MSD descriptor record (32 B): tile-sorted (k4_hist) and in bucket order (k4_place,
 // grouped by k4_group). A hot record carries its in-tile INCRBY prefix in `key` and its hot
-// bucket in `fp_lo`.
+// bucket in `fp_lo`. The high half of fp_lo carries the descriptor's EXPIRE jitter (MREC_JIT):
+// a key's identity is the sort key and the low 32 bits of fp_lo (the table's tag).
 struct __attribute__((aligned(16))) MRec {
   uint64_t key;      // sort key (region | fp.hi >> 3)
-  uint64_t fp_lo;
+  uint64_t fp_lo;    // tag (or hot bucket) | jitter << 32
   uint32_t idx;      // arrival index
   uint32_t req;      // request index
   uint32_t h;        // max(1, hits_addend)
@@ -414,8 +418,9 @@ constexpr uint32_t HB_PS = 2u;          // counts in the per-second store
 // A hot descriptor whose decision needs the freezing request of an earlier tile (k4_group).
 struct __attribute__((aligned(16))) Deferred {
   uint64_t P;        // INCRBY prefix of the key up to and including this descriptor
-  uint32_t idx, bucket, req, h, rule, now_mod;
+  uint32_t idx, bucket, req, h, rule, now_mod;  // bucket | EXPIRE jitter << 16
 };
+__host__ __device__ __forceinline__ uint32_t mrec_jit(uint64_t fp_lo) { return (uint32_t)(fp_lo >> 32); }
 
 constexpr int RADIX_BITS = 8;
 constexpr int RADIX = 1 << RADIX_BITS;

@@ -128,7 +128,7 @@ RL_DEV bool table_claim(const TableDesc& tab, uint64_t key, uint64_t fp_lo, uint
 // local cache holds the key for the whole batch. False when an expiry can fall among the
 // batch's touches (a string shared by units of different sizes): the key then
 // takes the exact sequential path (exotic_sequence).
-//   EXPIRE key div (fixed_cache_impl.go:69-72, jitter 0): alive while now < exp;
+//   EXPIRE key div + jitter (fixed_cache_impl.go:69-72): alive while now < exp;
 //   freecache Set(key, TTL = div) (base_limiter.go:102): hit while now < frz.
 RL_DEV bool fast_state(const KeyState& s, bool ps, bool local_cache, uint32_t ws, uint32_t div, uint64_t& base,
                        bool& frozen_pre) {
@@ -144,7 +144,7 @@ RL_DEV bool fast_state(const KeyState& s, bool ps, bool local_cache, uint32_t ws
 
 // One descriptor of a key's batch sequence, for the sequential path.
 struct SeqItem {
-  uint32_t req, t, h, rule;
+  uint32_t req, t, h, rule, jit;  // jit: EXPIRE jitter (seconds) of the descriptor's INCRBY
 };
 
 // Exact serial DoLimit of one key's descriptors (positions 0..n-1 in arrival order), for keys
@@ -178,7 +178,7 @@ RL_DEV void exotic_sequence(KeyState& s, const TableDesc& tab, const DevRule* __
       } else {
         if (d.t >= s.exp) s.count = 0;  // expired (or absent): INCRBY starts from 0
         s.count += d.h;
-        s.exp = d.t + R.div;
+        s.exp = d.t + R.div + d.jit;  // EXPIRE key div + JitterRand.Int63n(max)
         after = s.count;
       }
       put(f, (uint64_t)after);
@@ -288,7 +288,7 @@ RL_DEV void leader_segment(uint32_t hp, uint32_t j, const SortedRec& tail, bool 
         ks, tab, rules, j - hp + 1,
         [&](uint32_t q) {
           const SortedRec r = srec[hp + q];
-          return SeqItem{r.req, ws + (uint32_t)r.now_mod, r.h, r.rule};
+          return SeqItem{r.req, ws + (uint32_t)r.now_mod, r.h, r.rule, recs[r.idx].jit};
         },
         [&](uint32_t q, uint64_t v) { srec[hp + q].P = v; });
     write_state(slot, ks);
@@ -337,7 +337,7 @@ RL_DEV void leader_segment(uint32_t hp, uint32_t j, const SortedRec& tail, bool 
       ks.pcount = (uint32_t)final_count;
     } else {
       ks.count = (uint32_t)final_count;
-      ks.exp = t_last + R0.div;
+      ks.exp = t_last + R0.div + recs[srec[last].idx].jit;  // EXPIRE of the last INCRBY, with its jitter
     }
     if (freeze != SEG_NO_FREEZE) ks.frz = t_last + R0.div;
     write_state(slot, ks);

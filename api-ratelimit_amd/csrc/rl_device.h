@@ -42,6 +42,7 @@ struct DevBatch {
   const int64_t* now;
   const uint32_t* hits;
   const RRec* recs;  // routed batch (multi-GPU owner side): records instead of prefix bytes
+  const uint16_t* jit;  // rl_batch.ttl_jitter (NULL: none); a routed record carries its own (rrec_jit)
 };
 inline DevBatch make_dev_batch(const rl_batch& b) {
   DevBatch d;
@@ -56,8 +57,11 @@ inline DevBatch make_dev_batch(const rl_batch& b) {
   d.now = b.now;
   d.hits = b.hits_addend;
   d.recs = (b.reserved & RL_BATCH_ROUTED) ? reinterpret_cast<const RRec*>(b.prefix_blob) : nullptr;
+  d.jit = d.recs ? nullptr : b.ttl_jitter;
   return d;
 }
+// EXPIRE jitter of an unrouted descriptor (rl_batch.ttl_jitter, fixed_cache_impl.go:69-72).
+RL_DEV uint32_t desc_jit(const DevBatch& in, uint32_t i) { return in.jit ? (uint32_t)in.jit[i] : 0u; }
 
 // Unaligned little-endian 8-byte words of a byte string, read as aligned dwords and
 // funnel-shifted (v_alignbyte_b32). The blob has >= 16 bytes of slack past its end.

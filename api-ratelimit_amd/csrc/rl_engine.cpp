@@ -65,17 +65,17 @@ void launch_v4_hist(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint
 void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const unsigned long long* thsum,
                     unsigned long long* hoff, const uint32_t* fpart, const HotEntry* hot_list, HotBucket* hb,
                     const TableDesc& tab, HotCand* cand, uint32_t* heads_out, uint32_t* ins_out, void* scratch,
-                    const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl);
+                    const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl, unsigned long long* hexp);
 void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart,
                      void* scratch, const DevRule* rules, uint32_t n_rules, const unsigned long long* hoff, HotBucket* hb,
                      int local_cache, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
-                     uint32_t* poison, EngineCtl* ctl);
+                     uint32_t* poison, EngineCtl* ctl, unsigned long long* hexp);
 void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, const TableDesc& tab,
                      rl_status* out, uint32_t* req_thr, const HotBucket* hb, const Deferred* dfr, HotCand* cand,
                      int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads, uint32_t* wg_ins,
                      const uint32_t* scan_heads, const uint32_t* scan_ins, int routed, RegionOcc* occ, EngineCtl* ctl,
                      EngineCtl* next_ctl, EngineCtl* hctl, HotCand* hcand, const MRec* srec,
-                     const uint16_t* tstart);
+                     const uint16_t* tstart, unsigned long long* hexp);
 }  // namespace rlhip
 
 using namespace rlhip;
@@ -149,7 +149,7 @@ struct rl_engine {
     uint32_t* d_csum = nullptr; // compact batches: per-chunk prefix-length sums
   };
   Stage stage[HSLOTS];
-  size_t in_bytes = 0, o_off = 0, o_rule = 0, o_req = 0, o_now = 0, o_hits = 0;
+  size_t in_bytes = 0, o_off = 0, o_rule = 0, o_req = 0, o_now = 0, o_hits = 0, o_jit = 0;
   size_t c_pitch = 0;  // compact layout: rows desc_word | req_word | req_of at this pitch from o_off (host), 0 (device)
 
   // LSD pipeline scratch
@@ -188,6 +188,7 @@ struct rl_engine {
   unsigned long long* v4_hoff = nullptr;      // [tile][HOT_BUCKETS] exclusive h prefix over tiles
   Deferred* v4_dfr = nullptr;                 // deferred hot descriptors
   HotBucket* v4_hb = nullptr;                 // per hot bucket batch state
+  unsigned long long* v4_hexp = nullptr;      // per hot bucket: (index, jitter) of the freezing request's last INCRBY
   void* v4_scratch = nullptr;                 // k4_group global scratch + k4_scan ranges
   uint32_t* v4_heads = nullptr;               // per-block unique-key counts (k4_group, then k4_scan)
   uint32_t* v4_ins = nullptr;                 // per-block new slots per region, 16-bit pairs (k4_group, then k4_scan)
@@ -400,16 +401,16 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     timed(KT_V4_SCAN, [&] {
       launch_v4_scan(stream, n, v4_tcount[sl], v4_thsum[sl], v4_hoff, v4_fpart[sl], hot_t + HOT_SLOTS, v4_hb, tab,
                      want_cand ? d_cand : nullptr, v4_heads + ng, v4_ins + (size_t)ng * 4, v4_scratch, d_poison,
-                     d_occ, c4);
+                     d_occ, c4, v4_hexp);
     });
     timed(KT_V4_PLACE, [&] {
       launch_v4_place(stream, b, srt, v4_tcount[sl], v4_scratch, d_rules, n_rules, v4_hoff, v4_hb, lc, out,
-                      thr, v4_dfr, routed, d_poison, c4);
+                      thr, v4_dfr, routed, d_poison, c4, v4_hexp);
     });
     timed(KT_V4_GROUP, [&] {
       launch_v4_group(stream, b, d_rules, n_rules, tab, out, thr, v4_hb, v4_dfr, d_cand, want_cand ? 1 : 0,
                       cfg.hash_seed, v4_scratch, v4_heads, v4_ins, v4_heads + ng, v4_ins + (size_t)ng * 4, routed,
-                      d_occ, c4, c4n, h_ctl, want_cand ? h_cand : nullptr, srt, v4_tcount[sl]);
+                      d_occ, c4, c4n, h_ctl, want_cand ? h_cand : nullptr, srt, v4_tcount[sl], v4_hexp);
     });
     // k4_group's last block writes the summary into h_ctl / h_cand (pinned host memory)
     e = hipGetLastError();
@@ -910,6 +911,9 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   // compact layout (rl_batch_c): blob, then three rows (desc words, req words, req_of)
   e->c_pitch = align_up((std::max(N, R) + 1) * 4, 256);
   e->in_bytes = std::max(e->in_bytes, e->o_off + 3 * e->c_pitch);
+  // both layouts: the EXPIRE jitter per descriptor (rl_batch.ttl_jitter) after everything else
+  e->o_jit = align_up(e->in_bytes, 256);
+  e->in_bytes = e->o_jit + align_up(N * 2, 256);
   for (auto& g : e->stage) {
     chk(hipMalloc(&g.d_cin, 3 * e->c_pitch));
     chk(hipMalloc(&g.d_csum, (size_t)compact_chunks((uint32_t)N) * 4 + 64));
@@ -959,6 +963,7 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     chk(hipMalloc(&e->v4_hoff, T4 * HOT_BUCKETS * 8));
     chk(hipMalloc(&e->v4_dfr, N * sizeof(Deferred) + 64));
     chk(hipMalloc(&e->v4_hb, HOT_BUCKETS * sizeof(HotBucket)));
+    chk(hipMalloc(&e->v4_hexp, HOT_BUCKETS * 8));
     const size_t nb = (size_t)v4_group_blocks((uint32_t)N) + v4_scan_blocks();
     chk(hipMalloc(&e->v4_heads, nb * 4 + 64));
     chk(hipMalloc(&e->v4_ins, nb * 4 * 4 + 64));
@@ -1033,7 +1038,7 @@ void rl_destroy(rl_engine* e) {
     hipFree(e->v4_fpart[k]);
   }
   for (int k = 0; k < 3; ++k) hipFree(e->v4_ctl[k]);
-  for (void* p : {(void*)e->v4_hoff, (void*)e->v4_dfr, (void*)e->v4_hb,
+  for (void* p : {(void*)e->v4_hoff, (void*)e->v4_dfr, (void*)e->v4_hb, (void*)e->v4_hexp,
                   (void*)e->v4_heads, (void*)e->v4_ins, e->v4_scratch, (void*)e->d_poison, (void*)e->d_tree_nodes,
                   (void*)e->d_tree_slots, (void*)e->d_tree_names, (void*)e->d_res, (void*)e->table, (void*)e->d_occ,
                   (void*)e->d_rules, (void*)e->keys_orig, (void*)e->keys_a, (void*)e->keys_b, (void*)e->vals_a,
@@ -1120,6 +1125,7 @@ int rl_host_acquire(rl_engine* e, rl_host_batch* out) {
   out->req_of = reinterpret_cast<uint32_t*>(h + e->o_req);
   out->now = reinterpret_cast<int64_t*>(h + e->o_now);
   out->hits_addend = reinterpret_cast<uint32_t*>(h + e->o_hits);
+  out->ttl_jitter = reinterpret_cast<uint16_t*>(h + e->o_jit);
   out->max_desc = e->cfg.max_batch_desc;
   out->max_req = e->cfg.max_batch_req;
   out->max_blob = e->cfg.max_blob_bytes;
@@ -1144,7 +1150,8 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
   struct Arr { const void* src; size_t o, n; } arrs[] = {
       {b->prefix_blob, 0, b->blob_bytes}, {b->prefix_off, e->o_off, b->n_desc ? ((size_t)b->n_desc + 1) * 4 : 0},
       {b->rule_id, e->o_rule, (size_t)b->n_desc * 4}, {b->req_of, e->o_req, (size_t)b->n_desc * 4},
-      {b->now, e->o_now, (size_t)b->n_req * 8}, {b->hits_addend, e->o_hits, (size_t)b->n_req * 4}};
+      {b->now, e->o_now, (size_t)b->n_req * 8}, {b->hits_addend, e->o_hits, (size_t)b->n_req * 4},
+      {b->ttl_jitter, e->o_jit, b->ttl_jitter ? (size_t)b->n_desc * 2 : 0}};
   for (auto& a : arrs)
     if (a.n && a.src != h + a.o) memcpy(h + a.o, a.src, a.n);
   memset(h + b->blob_bytes, 0, RL_BLOB_SLACK);  // the device reads prefixes in 16-B words
@@ -1161,6 +1168,8 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
   }
   for (int k = 4; k < 6 && he == hipSuccess; ++k)
     if (ext[k]) he = hipMemcpyAsync(g.d_in + arrs[k].o, h + arrs[k].o, ext[k], hipMemcpyHostToDevice, e->xin);
+  if (he == hipSuccess && arrs[6].n)
+    he = hipMemcpyAsync(g.d_in + e->o_jit, h + e->o_jit, arrs[6].n, hipMemcpyHostToDevice, e->xin);
   if (he == hipSuccess) he = hipEventRecord(e->ev_in[s], e->xin);
   if (he != hipSuccess) return e->hip_fail(he, "hipMemcpyAsync(H2D)");
   rl_batch d = *b;
@@ -1170,6 +1179,7 @@ int rl_submit(rl_engine* e, const rl_batch* b, rl_status* out, uint32_t* req_thr
   d.req_of = reinterpret_cast<const uint32_t*>(g.d_in + e->o_req);
   d.now = reinterpret_cast<const int64_t*>(g.d_in + e->o_now);
   d.hits_addend = reinterpret_cast<const uint32_t*>(g.d_in + e->o_hits);
+  d.ttl_jitter = b->ttl_jitter ? reinterpret_cast<const uint16_t*>(g.d_in + e->o_jit) : nullptr;
   e->st.host_batches += 1;
   return e->submit_common(d, g.d_out, g.d_thr, nullptr, e->ev_in[s], false, true, out, req_throttle_ms);
 }
@@ -1225,6 +1235,7 @@ int rl_host_acquire_c(rl_engine* e, rl_host_batch_c* out) {
   out->desc_word = reinterpret_cast<uint32_t*>(h + e->o_off);
   out->req_word = reinterpret_cast<uint32_t*>(h + e->o_off + e->c_pitch);
   out->req_of = reinterpret_cast<uint32_t*>(h + e->o_off + 2 * e->c_pitch);
+  out->ttl_jitter = reinterpret_cast<uint16_t*>(h + e->o_jit);
   out->max_desc = e->cfg.max_batch_desc;
   out->max_req = e->cfg.max_batch_req;
   out->max_blob = e->cfg.max_blob_bytes;
@@ -1259,7 +1270,8 @@ int rl_submit_c(rl_engine* e, const rl_batch_c* b) {
   const size_t P = e->c_pitch;
   struct Arr { const void* src; size_t o, n; } arrs[] = {
       {b->prefix_blob, 0, b->blob_bytes}, {b->desc_word, e->o_off, (size_t)b->n_desc * 4},
-      {b->req_word, e->o_off + P, (size_t)b->n_req * 4}, {one ? nullptr : b->req_of, e->o_off + 2 * P, one ? 0 : (size_t)b->n_desc * 4}};
+      {b->req_word, e->o_off + P, (size_t)b->n_req * 4}, {one ? nullptr : b->req_of, e->o_off + 2 * P, one ? 0 : (size_t)b->n_desc * 4},
+      {b->ttl_jitter, e->o_jit, b->ttl_jitter ? (size_t)b->n_desc * 2 : 0}};
   for (auto& a : arrs)
     if (a.n && a.src != h + a.o) memcpy(h + a.o, a.src, a.n);
   memset(h + b->blob_bytes, 0, RL_BLOB_SLACK);  // the device reads prefixes in 16-B words
@@ -1271,6 +1283,8 @@ int rl_submit_c(rl_engine* e, const rl_batch_c* b) {
   if (he == hipSuccess && w) he = hipMemcpy2DAsync(g.d_cin, P, h + e->o_off, P, w, 2, hipMemcpyHostToDevice, e->xin);
   if (he == hipSuccess && arrs[3].n)
     he = hipMemcpyAsync(g.d_cin + 2 * P, h + e->o_off + 2 * P, arrs[3].n, hipMemcpyHostToDevice, e->xin);
+  if (he == hipSuccess && arrs[4].n)  // (used in place by the pipeline: no expansion)
+    he = hipMemcpyAsync(g.d_in + e->o_jit, h + e->o_jit, arrs[4].n, hipMemcpyHostToDevice, e->xin);
   if (he == hipSuccess) he = hipEventRecord(e->ev_in[s], e->xin);
   if (he != hipSuccess) return e->hip_fail(he, "hipMemcpyAsync(H2D compact)");
   // The rl_batch arrays, expanded on the device behind the copies, on the stream k4_hist runs on
@@ -1303,6 +1317,7 @@ int rl_submit_c(rl_engine* e, const rl_batch_c* b) {
   d.req_of = d_req;
   d.now = d_now;
   d.hits_addend = d_hits;
+  d.ttl_jitter = b->ttl_jitter ? reinterpret_cast<const uint16_t*>(g.d_in + e->o_jit) : nullptr;
   e->st.host_batches += 1;
   // raw replies land in the slot's device output array (8 B of its 20 per descriptor)
   // inputs_ready: the expansion is queued ahead of k4_hist on its stream

@@ -71,19 +71,19 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
     const RRec x = in.recs[i];
     if (req_thr) req_thr[i] = 0;  // one ThrottleMillis slot per record (none for raw replies)
     ItemRec rec;
-    rec.rule = x.rule;
+    rec.rule = rrec_rule(x.rule);
     rec.req = x.greq;
     rec.h = x.h;
     rec.fp_lo = 0;
     rec.now_mod = 0;
     rec.gen = 0;
-    rec.pad = 0;
-    if (x.rule >= n_rules) {
+    rec.jit = rrec_jit(x.rule);
+    if (rec.rule >= n_rules) {
       err |= ERR_BAD_INPUT;
     } else if ((int64_t)x.now > MAX_NOW) {
       err |= ERR_BAD_TIME;
     } else {
-      fp_place(FpState{x.a, x.b}, (int64_t)x.now, rules[x.rule], key, rec, region, uw);
+      fp_place(FpState{x.a, x.b}, (int64_t)x.now, rules[rec.rule], key, rec, region, uw);
       gen = rec.gen;
       nil = false;
     }
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void k_fingerprint(DevBatch in, const DevRule*
     rec.fp_lo = 0;
     rec.now_mod = 0;
     rec.gen = 0;
-    rec.pad = 0;
+    rec.jit = desc_jit(in, i);
     // batch layout checks (the device validates every submit form): prefix offsets in
     // order and inside the blob, request indices non-decreasing
     const uint32_t o0 = in.off[i], o1 = in.off[i + 1];

@@ -392,7 +392,7 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
       const bool hotb = x.bucket < (uint32_t)HOT_BUCKETS;
       MRec m;
       m.key = hotb ? (uint64_t)sres[r] : x.key;
-      m.fp_lo = hotb ? (uint64_t)x.bucket : x.lo;
+      m.fp_lo = (hotb ? (uint64_t)x.bucket : (uint64_t)(uint32_t)x.lo) | ((uint64_t)x.jit << 32);
       m.idx = i;
       m.req = x.req;
       m.h = x.h;
@@ -482,7 +482,8 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
                                                    uint32_t* __restrict__ heads_out, uint32_t* __restrict__ ins_out,
                                                    uint32_t* __restrict__ ranges,
                                                    const uint32_t* __restrict__ poison,
-                                                   const RegionOcc* __restrict__ occ, EngineCtl* ctl) {
+                                                   const RegionOcc* __restrict__ occ, EngineCtl* ctl,
+                                                   unsigned long long* __restrict__ hexp) {
   const uint32_t local_cache = tab.local_cache;
   __shared__ uint32_t s_f[FP_PART_WORDS];
   __shared__ uint32_t s_pc[SCAN_W][64];
@@ -813,7 +814,10 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
       const uint32_t hi_n = (uint32_t)__popcll(__ballot(ins_region == (uint32_t)(2 * x + 1)));
       if (lane == 0) ins_out[blockIdx.x * 4 + x] = lo_n | (hi_n << 16);
     }
-    if (lane < (uint32_t)HOT_PER_BLOCK) hb[b] = x;
+    if (lane < (uint32_t)HOT_PER_BLOCK) {
+      hb[b] = x;
+      if (local_cache) hexp[b] = 0;  // the freezing request's last INCRBY: (index, jitter), k4_place / k4_group
+    }
     heads = tile::wave_sum(heads);
     if (lane == 0) heads_out[blockIdx.x] = heads;
     ST5(4);
@@ -854,7 +858,9 @@ RL_DEV void gbar() {
 // parallel, instead of by a walk of the key's list).
 constexpr uint32_t CNT_MASK = 0xFFFFu, CNT_MIXED = 0x10000u, CNT_MIXED_UNIT = 0x20000u;
 RL_DEV bool g_insert(const GS& g, uint32_t k, const DevRule* __restrict__ rules) {
-  const uint64_t key = g.rec[k].key, lo = g.rec[k].fp_lo;
+  // identity: the sort key and the tag (fp_lo's low half; its high half is the record's jitter)
+  const uint64_t key = g.rec[k].key;
+  const uint32_t lo = (uint32_t)g.rec[k].fp_lo;
   const uint32_t hmask = g.hs - 1u;
   uint32_t s = (uint32_t)key & hmask;
   uint32_t v;
@@ -866,7 +872,7 @@ RL_DEV bool g_insert(const GS& g, uint32_t k, const DevRule* __restrict__ rules)
 #ifdef RL_PROBE_STATS
     ++probes;
 #endif
-    if (v == G_EMPTY || (g.rec[v].key == key && g.rec[v].fp_lo == lo)) break;
+    if (v == G_EMPTY || (g.rec[v].key == key && (uint32_t)g.rec[v].fp_lo == lo)) break;
     s = (s + 1) & hmask;
   }
 #ifdef RL_PROBE_STATS
@@ -997,7 +1003,7 @@ RL_DEV void g_lead_exotic(const GS& g, uint32_t k, const DevRule* __restrict__ r
       ks, tab, rules, n,
       [&](uint32_t q) {
         const MRec& m = g.rec[g.list[e0 + q]];
-        return SeqItem{m.req, ws + (m.rn >> V4_RULE_BITS), m.h, rule_of(m.rn)};
+        return SeqItem{m.req, ws + (m.rn >> V4_RULE_BITS), m.h, rule_of(m.rn), mrec_jit(m.fp_lo)};
       },
       [&](uint32_t q, uint64_t v) { g.P[g.list[e0 + q]] = v; });
   write_state(slot, ks);
@@ -1049,9 +1055,10 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
   uint64_t base = 0;
   bool frozen_pre = false;
   if (mixed_unit || !fast_state(ks, ps, tab.local_cache != 0, ws, R0.div, base, frozen_pre)) {
-    // exact sequential path, in a pass of its own after the leaders (g_lead_exotic)
+    // exact sequential path, in a pass of its own after the leaders (g_lead_exotic); the tail
+    // record keeps its jitter in fp_lo's high half
     g.rec[tail].key = (uint64_t)(uintptr_t)slot;
-    g.rec[tail].fp_lo = SEG_EXOTIC_PENDING;
+    g.rec[tail].fp_lo = (g.rec[tail].fp_lo & ~0xFFFFFFFFull) | SEG_EXOTIC_PENDING;
     return;
   }
   uint32_t freeze = SEG_NO_FREEZE;
@@ -1094,7 +1101,8 @@ RL_DEV void g_lead(const GS& g, uint32_t k, const DevRule* __restrict__ rules, c
       ks.pcount = (uint32_t)final_count;
     } else {
       ks.count = (uint32_t)final_count;
-      ks.exp = t_last + R0.div;  // EXPIRE key div of the last INCRBY (fixed_cache_impl.go:69-72)
+      // EXPIRE key div + jitter of the last INCRBY (fixed_cache_impl.go:69-72)
+      ks.exp = t_last + R0.div + mrec_jit(g.rec[last].fp_lo);
     }
     if (freeze != SEG_NO_FREEZE) ks.frz = t_last + R0.div;  // freecache TTL (base_limiter.go:102)
     write_state(slot, ks);
@@ -1171,7 +1179,7 @@ RL_DEV uint32_t group_range(const GS& g, uint32_t m, const DevRule* __restrict__
   __syncthreads();
   // exotic keys (rare): their leaders' sequential pass
   for (uint32_t k = tid; k < m; k += G_NT)
-    if (g.rec[k].fp_lo == SEG_EXOTIC_PENDING && g_tail(g, k) == k) g_lead_exotic(g, k, rules, tab, ctl);
+    if ((uint32_t)g.rec[k].fp_lo == SEG_EXOTIC_PENDING && g_tail(g, k) == k) g_lead_exotic(g, k, rules, tab, ctl);
   __threadfence_block();
   __syncthreads();
   ST4(4);
@@ -1201,7 +1209,8 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
                                                HotBucket* __restrict__ hb, int local_cache,
                                                rl_status* __restrict__ out,
                                                uint32_t* __restrict__ req_thr, Deferred* __restrict__ dfr, int routed,
-                                               uint32_t* __restrict__ poison, EngineCtl* ctl) {
+                                               uint32_t* __restrict__ poison, EngineCtl* ctl,
+                                               unsigned long long* __restrict__ hexp) {
   __shared__ __attribute__((aligned(16))) uint16_t s_row[HOT_BUCKETS + 8];
   __shared__ uint32_t s_rstar[HOT_BUCKETS];
   __shared__ uint32_t s_err;
@@ -1270,7 +1279,8 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
     const uint64_t after = hx.base + P;
     if (!local_cache || after <= rl.L) {
       tile::decide_at(i, a.req, rule, a.h, now_mod, hx.base, P, SEG_NO_FREEZE, rules, out, req_thr, routed);
-      if (P == hx.total) hb[b].t_all = hx.ws + now_mod;  // the key's last INCRBY (EXPIRE time)
+      // the key's last INCRBY: EXPIRE at its time + div + its jitter
+      if (P == hx.total) hb[b].t_all = hx.ws + now_mod + mrec_jit(a.fp_lo);
       continue;
     }
     const uint32_t rs = s_rstar[b];
@@ -1280,6 +1290,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
       } else {  // same request as the freezing descriptor: its INCRBY still happens
         tile::decide_at(i, a.req, rule, a.h, now_mod, hx.base, P, SEG_NO_FREEZE, rules, out, req_thr, routed);
         atomicMax(hot_counter(hx), (uint32_t)after);
+        atomicMax(&hexp[b], ((unsigned long long)i << 32) | mrec_jit(a.fp_lo));  // the last of them sets EXPIRE
       }
     } else if (a.req > q0) {  // froze in an earlier tile, in a request <= q0
       tile::emit_local_hit(out, i, a.h, rl.div - now_mod, rl.shadow, routed);
@@ -1288,7 +1299,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
       Deferred df;
       df.P = P;
       df.idx = i;
-      df.bucket = b;
+      df.bucket = b | (mrec_jit(a.fp_lo) << 16);
       df.req = a.req;
       df.h = a.h;
       df.rule = rule;
@@ -1392,7 +1403,8 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
                                                  RegionOcc* __restrict__ occ, EngineCtl* ctl, EngineCtl* next_ctl,
                                                  EngineCtl* hctl, HotCand* hcand,
                                                  const MRec* __restrict__ srec, const uint16_t* __restrict__ tstart,
-                                                 uint32_t ntiles, uint32_t n_rules) {
+                                                 uint32_t ntiles, uint32_t n_rules,
+                                                 unsigned long long* __restrict__ hexp) {
   __shared__ DevRule s_rules[LR ? LDS_RULES : 1];
   const DevRule* __restrict__ rules = LR ? s_rules : rules_g;
   __shared__ MRec s_rec[G_CAP];
@@ -1439,16 +1451,14 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   if (tid == 0 && j < 1024) for (int k = 0; k < 8; ++k) g_st4[3072 + j][k] = 0;  // this batch's facts only
 #endif
   if (s_err == 0 && j < (uint32_t)(HOT_BUCKETS / G_NT)) {
-    // Hot keys (decided by k4_place): EXPIRE and freecache TTLs from the time of the last
-    // INCRBY / of the freezing request (fixed_cache_impl.go:69-72, base_limiter.go:102). The
-    // deferred hot descriptors below only raise the counter word.
+    // Hot keys (decided by k4_place) that no request froze: EXPIRE from the time and jitter of
+    // the last INCRBY (fixed_cache_impl.go:69-72). A key frozen in this batch gets its EXPIRE and
+    // freecache TTLs in the last block, once the deferred hot descriptors below have recorded
+    // which INCRBY of the freezing request came last.
     const HotBucket x = hb[j * G_NT + tid];
-    if (x.slot && !(x.flags & HB_FROZEN_PRE)) {
+    if (x.slot && !(x.flags & (HB_FROZEN_PRE | HB_PS)) && x.rstar == 0xFFFFFFFFu) {
       Slot* sl = reinterpret_cast<Slot*>(x.slot);
-      const uint32_t div = rules[x.rule].div;
-      const bool frozen = x.rstar != 0xFFFFFFFFu;
-      if (!(x.flags & HB_PS)) sl->exp = (frozen ? x.t_rstar : x.t_all) + div;
-      if (frozen) sl->frz = x.t_rstar + div;
+      sl->exp = x.t_all + rules[x.rule].div;
     }
   }
   if (s_err == 0) {
@@ -1457,13 +1467,15 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
     const uint32_t nd = s_rq[5];
     for (uint32_t e = j * G_NT + tid; e < nd; e += gridDim.x * G_NT) {
       const Deferred df = dfr[e];
-      const HotBucket& x = hb[df.bucket];
+      const uint32_t bk = df.bucket & 0xFFFFu;
+      const HotBucket& x = hb[bk];
       if (df.req > x.rstar) {
         tile::emit_local_hit(out, df.idx, df.h, rules[df.rule].div - df.now_mod, rules[df.rule].shadow, routed);
       } else {
         tile::decide_at(df.idx, df.req, df.rule, df.h, df.now_mod, x.base, df.P, SEG_NO_FREEZE, rules, out, req_thr,
                       routed);
         atomicMax(hot_counter(x), (uint32_t)(x.base + df.P));
+        atomicMax(&hexp[bk], ((unsigned long long)df.idx << 32) | (df.bucket >> 16));
       }
     }
     const uint32_t nq = s_rq[0];  // ranges of group g
@@ -1687,6 +1699,20 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
     for (int r = 0; r < 8; ++r) n += s_ins[r];
     ctl->n_inserted = n;
   }
+  if (tab.local_cache && s_err == 0) {
+    // Hot keys a request froze in this batch (base_limiter.go:94-106): freecache TTL from the
+    // freezing request's time, EXPIRE from the time and jitter of that request's last INCRBY of
+    // the key (every block's k4_place / deferred atomicMax is done; read at the memory side)
+    for (uint32_t b = tid; b < (uint32_t)HOT_BUCKETS; b += G_NT) {
+      const HotBucket x = hb[b];
+      if (!x.slot || (x.flags & HB_FROZEN_PRE) || x.rstar == 0xFFFFFFFFu) continue;
+      Slot* sl = reinterpret_cast<Slot*>(x.slot);
+      const uint32_t div = rules[x.rule].div;
+      const unsigned long long w = atomicMax(&hexp[b], 0ull);
+      if (!(x.flags & HB_PS)) sl->exp = x.t_rstar + div + (uint32_t)w;
+      sl->frz = x.t_rstar + div;
+    }
+  }
   STL(1);
   if (any_cand && !in.recs) {
     u32x4 b0[CPT], b1[CPT];
@@ -1777,29 +1803,29 @@ void launch_v4_hist(hipStream_t st, const rl_batch& b, const DevRule* rules, uin
 void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const unsigned long long* thsum,
                     unsigned long long* hoff, const uint32_t* fpart, const HotEntry* hot_list, HotBucket* hb,
                     const TableDesc& tab, HotCand* cand, uint32_t* heads_out, uint32_t* ins_out, void* scratch,
-                    const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl) {
+                    const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl, unsigned long long* hexp) {
   hipLaunchKernelGGL(v4::k4_scan, dim3(v4_scan_blocks()), dim3(v4::SCAN_NT), 0, st, tstart, thsum, v4_tiles(n), n, hoff,
-                     fpart, hot_list, hb, tab, cand, heads_out, ins_out, v4_ranges(scratch), poison, occ, ctl);
+                     fpart, hot_list, hb, tab, cand, heads_out, ins_out, v4_ranges(scratch), poison, occ, ctl, hexp);
 }
 void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart,
                      void* scratch, const DevRule* rules, uint32_t n_rules, const unsigned long long* hoff,
                      HotBucket* hb, int local_cache, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
-                     uint32_t* poison, EngineCtl* ctl) {
+                     uint32_t* poison, EngineCtl* ctl, unsigned long long* hexp) {
   if (n_rules <= v4::LDS_RULES)
     hipLaunchKernelGGL(v4::k4_place<true>, dim3(v4_tiles(b.n_desc)), dim3(V4_THREADS), 0, st, make_dev_batch(b), srec,
                        tstart, v4_ranges(scratch), rules, n_rules, hoff, hb, local_cache, out, req_thr, dfr, routed,
-                       poison, ctl);
+                       poison, ctl, hexp);
   else
     hipLaunchKernelGGL(v4::k4_place<false>, dim3(v4_tiles(b.n_desc)), dim3(V4_THREADS), 0, st, make_dev_batch(b), srec,
                        tstart, v4_ranges(scratch), rules, n_rules, hoff, hb, local_cache, out, req_thr, dfr, routed,
-                       poison, ctl);
+                       poison, ctl, hexp);
 }
 void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, const TableDesc& tab,
                      rl_status* out, uint32_t* req_thr, const HotBucket* hb, const Deferred* dfr, HotCand* cand,
                      int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads, uint32_t* wg_ins,
                      const uint32_t* scan_heads, const uint32_t* scan_ins, int routed, RegionOcc* occ, EngineCtl* ctl,
                      EngineCtl* next_ctl, EngineCtl* hctl, HotCand* hcand, const MRec* srec,
-                     const uint16_t* tstart) {
+                     const uint16_t* tstart, unsigned long long* hexp) {
   using namespace v4;
   uint8_t* p = reinterpret_cast<uint8_t*>(scratch);
   GScratch4 gs;
@@ -1822,12 +1848,12 @@ void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, ui
     hipLaunchKernelGGL(k4_group<true>, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), rules, tab, out, req_thr,
                        hb, dfr, cand, cand_on, seed, gs, wg_heads, wg_ins, scan_heads, scan_ins,
                        (uint32_t)HOT_SCAN_BLOCKS, v4_ranges(scratch), routed, occ, ctl, next_ctl, hctl, hcand, srec,
-                       tstart, v4_tiles(b.n_desc), n_rules);
+                       tstart, v4_tiles(b.n_desc), n_rules, hexp);
   else
     hipLaunchKernelGGL(k4_group<false>, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), rules, tab, out, req_thr,
                        hb, dfr, cand, cand_on, seed, gs, wg_heads, wg_ins, scan_heads, scan_ins,
                        (uint32_t)HOT_SCAN_BLOCKS, v4_ranges(scratch), routed, occ, ctl, next_ctl, hctl, hcand, srec,
-                       tstart, v4_tiles(b.n_desc), n_rules);
+                       tstart, v4_tiles(b.n_desc), n_rules, hexp);
 }
 
 }  // namespace rlhip

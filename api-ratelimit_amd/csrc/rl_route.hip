@@ -45,7 +45,7 @@ __global__ __launch_bounds__(NT) void k_route_hash(DevBatch in, const DevRule* _
     uint32_t err = 0, o = ROUTE_LOCAL;
     if (o1 < o0 || o1 > in.blob_bytes || qp > q) err |= ERR_BAD_INPUT;
     const bool nil = rule == RL_NIL_RULE;
-    if (!nil && !err && (rule >= n_rules || q >= in.n_req)) err |= ERR_BAD_INPUT;
+    if (!nil && !err && (rule >= n_rules || rule >= RREC_MAX_RULE || q >= in.n_req)) err |= ERR_BAD_INPUT;
     const uint32_t qc = q < in.n_req ? q : 0u;
     const uint32_t oc = err ? 0u : o0;
     const int64_t now = in.now[qc];
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(NT) void k_route_hash(DevBatch in, const DevRule* _
         r.a = s.a;
         r.b = s.b;
         r.now = (uint32_t)now;
-        r.rule = rule;
+        r.rule = rule | (desc_jit(in, i) << 16);  // the EXPIRE jitter travels with the record
         r.h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
         r.greq = (origin << ROUTE_REQ_BITS) | q;
         tmp[i] = r;
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(NT) void k_route_pack1(DevBatch in, const DevRule* 
     const uint32_t o0 = in.off[i], o1 = in.off[i + 1];
     if (o1 < o0 || o1 > in.blob_bytes || qp > q) err |= ERR_BAD_INPUT;
     const bool nil = rule == RL_NIL_RULE;
-    if (!nil && !err && (rule >= n_rules || q >= in.n_req)) err |= ERR_BAD_INPUT;
+    if (!nil && !err && (rule >= n_rules || rule >= RREC_MAX_RULE || q >= in.n_req)) err |= ERR_BAD_INPUT;
     const uint32_t qc = q < in.n_req ? q : 0u;
     const uint32_t oc = err ? 0u : o0;
     const int64_t now = in.now[qc];
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(NT) void k_route_pack1(DevBatch in, const DevRule* 
         r.a = fs.a;
         r.b = fs.b;
         r.now = (uint32_t)now;
-        r.rule = rule;
+        r.rule = rule | (desc_jit(in, i) << 16);  // the EXPIRE jitter travels with the record
         r.h = ha > 1u ? ha : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
         r.greq = (origin << ROUTE_REQ_BITS) | q;
         o = route_owner(fs.a, fs.b, n_shards);
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
   __syncthreads();
   const uint32_t i0 = bi * PBLK, last = in.n_desc - 1u;  // n_desc >= 1, n_req >= 1 (host-checked)
   // two levels of loads, each issued together at clamped indices (k_route_pack1)
-  uint32_t rl[PR], q[PR], qp[PR], oa[PR], ob[PR];
+  uint32_t rl[PR], q[PR], qp[PR], oa[PR], ob[PR], jv[PR];
 #pragma unroll
   for (int r = 0; r < PR; ++r) {
     const uint32_t i = min(i0 + r * NT + tid, last);
@@ -530,6 +530,7 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
     qp[r] = in.req_of[i ? i - 1u : 0u];
     oa[r] = in.off[i];
     ob[r] = in.off[i + 1u];
+    jv[r] = desc_jit(in, i);  // (kernel-uniform test: no load without jitter; combining is off with it)
   }
   bool okv[PR];
   int64_t nowv[PR];
@@ -540,7 +541,8 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
   for (int r = 0; r < PR; ++r) {
     const bool v = i0 + r * NT + tid < in.n_desc;
     const bool lay = oa[r] <= ob[r] && ob[r] <= in.blob_bytes && qp[r] <= q[r];
-    const bool nil = rl[r] == RL_NIL_RULE, q_ok = q[r] < in.n_req, rule_ok = rl[r] < n_rules;
+    const bool nil = rl[r] == RL_NIL_RULE, q_ok = q[r] < in.n_req;
+    const bool rule_ok = rl[r] < n_rules && rl[r] < RREC_MAX_RULE;  // (the record's rule word carries the jitter)
     if (v && (!lay || (!nil && (!rule_ok || !q_ok)))) err |= ERR_BAD_INPUT;
     okv[r] = v && !nil && lay && rule_ok && q_ok;
     const uint32_t qc = q_ok ? q[r] : 0u;
@@ -567,7 +569,7 @@ __global__ __launch_bounds__(NT) void k_route_pack2(DevBatch in, const DevRule* 
     rec[r].a = fs.a;
     rec[r].b = fs.b;
     rec[r].now = (uint32_t)nowv[r];
-    rec[r].rule = rl[r];
+    rec[r].rule = rl[r] | (jv[r] << 16);
     rec[r].h = hav[r] > 1u ? hav[r] : 1u;  // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
     rec[r].greq = (origin << ROUTE_REQ_BITS) | q[r];
     cat[r] = route_owner(fs.a, fs.b, n_shards);

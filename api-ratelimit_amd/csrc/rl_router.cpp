@@ -390,7 +390,7 @@ struct rl_router {
   uint64_t seq = 0, done = 0;
   uint32_t tclock = 0;       // the step clock: the newest request time of every step applied so far
   double t_pack0 = 0;        // start of the current submit's packs (host clock)
-  size_t in_bytes = 0, o_off = 0, o_rule = 0, o_req = 0, o_now = 0, o_hits = 0;  // host staging layout
+  size_t in_bytes = 0, o_off = 0, o_rule = 0, o_req = 0, o_now = 0, o_hits = 0, o_jit = 0;  // host staging layout
   AgEntry* d_ag = nullptr;   // collective hot-set allgather: [HOT_MAX] send | [G * HOT_MAX] receive
   int32_t* d_ok = nullptr;   // [MAXS] zero words: the decide status sent when the decide succeeded
   AgEntry* h_ag = nullptr;
@@ -550,13 +550,15 @@ int rl_router::stage_host(uint32_t s, uint32_t k, const rl_batch& b, rl_batch& d
   struct Arr { const void* src; size_t o, n; } arrs[] = {
       {b.prefix_blob, 0, b.blob_bytes}, {b.prefix_off, o_off, b.n_desc ? ((size_t)b.n_desc + 1) * 4 : 0},
       {b.rule_id, o_rule, (size_t)b.n_desc * 4}, {b.req_of, o_req, (size_t)b.n_desc * 4},
-      {b.now, o_now, (size_t)b.n_req * 8}, {b.hits_addend, o_hits, (size_t)b.n_req * 4}};
+      {b.now, o_now, (size_t)b.n_req * 8}, {b.hits_addend, o_hits, (size_t)b.n_req * 4},
+      {b.ttl_jitter, o_jit, b.ttl_jitter ? (size_t)b.n_desc * 2 : 0}};
   for (auto& a : arrs)
     if (a.n && a.src != h + a.o) memcpy(h + a.o, a.src, a.n);
   memset(h + b.blob_bytes, 0, RL_BLOB_SLACK);  // the device reads prefixes in 16-B words
-  const size_t ext[] = {(size_t)b.blob_bytes + RL_BLOB_SLACK, arrs[1].n, arrs[2].n, arrs[3].n, arrs[4].n, arrs[5].n};
+  const size_t ext[] = {(size_t)b.blob_bytes + RL_BLOB_SLACK, arrs[1].n, arrs[2].n, arrs[3].n, arrs[4].n, arrs[5].n,
+                        arrs[6].n};
   hipError_t he = hipSuccess;
-  for (int q = 0; q < 6 && he == hipSuccess; ++q)
+  for (int q = 0; q < 7 && he == hipSuccess; ++q)
     if (ext[q]) he = hipMemcpyAsync(t.hs.d_in + arrs[q].o, h + arrs[q].o, ext[q], hipMemcpyHostToDevice, sh[s].os);
   if (he != hipSuccess) return RL_EHIP;
   d = b;
@@ -566,6 +568,7 @@ int rl_router::stage_host(uint32_t s, uint32_t k, const rl_batch& b, rl_batch& d
   d.req_of = reinterpret_cast<const uint32_t*>(t.hs.d_in + o_req);
   d.now = reinterpret_cast<const int64_t*>(t.hs.d_in + o_now);
   d.hits_addend = reinterpret_cast<const uint32_t*>(t.hs.d_in + o_hits);
+  d.ttl_jitter = b.ttl_jitter ? reinterpret_cast<const uint16_t*>(t.hs.d_in + o_jit) : nullptr;
   return 0;
 }
 
@@ -593,7 +596,9 @@ void rl_router::pack(uint32_t s, uint32_t k) {
     send_status(t.rc_pack);
     return;
   }
-  const bool combine = !(cfg.flags & RL_ROUTER_NO_COMBINE) && !S.v.local_cache && !S.hot.empty();
+  // (no combining with EXPIRE jitter: a combined record's EXPIRE would need the group's last
+  // descriptor's jitter)
+  const bool combine = !(cfg.flags & RL_ROUTER_NO_COMBINE) && !S.v.local_cache && !S.hot.empty() && !t.b.ttl_jitter;
   if (!t.zeroed) (void)hipMemsetAsync(t.zero, 0, t.zero_bytes, S.os);  // (the slot's last step had no unpack)
   t.pb.thr = t.thr;  // zeroed by the pack
   // the hot scan writes the group sums and its verdict straight into the pinned mirror
@@ -1404,7 +1409,8 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
     r->o_req = r->o_rule + al(N * 4);
     r->o_now = r->o_req + al(N * 4);
     r->o_hits = r->o_now + al(N * 8);
-    r->in_bytes = r->o_hits + al(N * 4);
+    r->o_jit = r->o_hits + al(N * 4);
+    r->in_bytes = r->o_jit + al(N * 2);
   }
   if (const char* f = getenv("RL_ROUTER_FAULT")) {  // tests: "phase:shard[:step]"
     char ph[32] = {0};
@@ -1504,6 +1510,7 @@ int rl_router_host_acquire(rl_router* r, uint32_t shard, rl_host_batch* out) {
   out->req_of = reinterpret_cast<uint32_t*>(h + r->o_req);
   out->now = reinterpret_cast<int64_t*>(h + r->o_now);
   out->hits_addend = reinterpret_cast<uint32_t*>(h + r->o_hits);
+  out->ttl_jitter = reinterpret_cast<uint16_t*>(h + r->o_jit);
   out->max_desc = r->cfg.max_desc;
   out->max_req = r->cfg.max_desc;
   out->max_blob = (uint32_t)(r->o_off - RL_BLOB_SLACK);

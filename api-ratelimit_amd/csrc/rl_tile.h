@@ -108,6 +108,7 @@ RL_DEV uint32_t block_excl_scan(uint32_t v, uint32_t* sh_w, uint32_t& total) {
 struct D3 {
   uint64_t key, lo;
   uint32_t req, rule, h, now_mod, bucket, gen;
+  uint32_t jit;  // EXPIRE jitter (seconds) of the descriptor's INCRBY
   uint32_t uw;   // unit window slot (unit - 1) * 2 + parity, 8 = none
   uint32_t uwv;  // unit window index + 1
 };
@@ -186,7 +187,7 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
   // and inside the blob's 32 readable bytes of slack (rl_hip.h, rl_batch.prefix_blob).
   const uint32_t tid = threadIdx.x;
   const uint32_t last = in.n_desc - 1u;
-  uint32_t rl[R], q[R], qp[R], oa[R], ob[R];
+  uint32_t rl[R], q[R], qp[R], oa[R], ob[R], jv[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint32_t i = min(t0 + r * NT + tid, last);
@@ -195,6 +196,7 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
     qp[r] = in.req_of[i ? i - 1u : 0u];
     oa[r] = in.off[i];
     ob[r] = in.off[i + 1u];
+    jv[r] = desc_jit(in, i);  // (kernel-uniform test: no load without jitter)
   }
   HSTF(2);
   uint32_t o0[R], len[R];
@@ -229,6 +231,7 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
     D3& x = d[r];
     x.req = i < in.n_desc ? q[r] : 0u;
     x.rule = i < in.n_desc ? rl[r] : RL_NIL_RULE;
+    x.jit = jv[r];
     // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
     x.h = i < in.n_desc && q[r] < in.n_req && ha[r] > 1u ? ha[r] : 1u;
     x.now_mod = 0;
@@ -269,15 +272,16 @@ RL_DEV void load_routed(const DevBatch& in, const DevRule* __restrict__ rules, u
   bool ok[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
-    ok[r] = rc[r].rule < n_rules;
-    if (ok[r]) rr[r] = rules[rc[r].rule];
+    ok[r] = rrec_rule(rc[r].rule) < n_rules;
+    if (ok[r]) rr[r] = rules[rrec_rule(rc[r].rule)];
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint32_t i = t0 + r * NT + tid;
     D3& x = d[r];
     x.req = rc[r].greq;
-    x.rule = rc[r].rule;
+    x.rule = rrec_rule(rc[r].rule);
+    x.jit = rrec_jit(rc[r].rule);
     x.h = rc[r].h > 1u ? rc[r].h : 1u;
     x.now_mod = 0;
     x.gen = 0;

@@ -59,7 +59,8 @@ class RlRule(C.Structure):
 class RlBatch(C.Structure):
     _fields_ = [("n_desc", C.c_uint32), ("n_req", C.c_uint32), ("blob_bytes", C.c_uint32), ("reserved", C.c_uint32),
                 ("prefix_blob", C.c_void_p), ("prefix_off", C.c_void_p), ("rule_id", C.c_void_p),
-                ("req_of", C.c_void_p), ("now", C.c_void_p), ("hits_addend", C.c_void_p)]
+                ("req_of", C.c_void_p), ("now", C.c_void_p), ("hits_addend", C.c_void_p),
+                ("ttl_jitter", C.c_void_p)]
 
 
 class RlTreeNode(C.Structure):
@@ -89,7 +90,7 @@ class RlOccupancy(C.Structure):
 
 class RlHostBatch(C.Structure):
     _fields_ = [("prefix_blob", C.c_void_p), ("prefix_off", C.c_void_p), ("rule_id", C.c_void_p),
-                ("req_of", C.c_void_p), ("now", C.c_void_p), ("hits_addend", C.c_void_p),
+                ("req_of", C.c_void_p), ("now", C.c_void_p), ("hits_addend", C.c_void_p), ("ttl_jitter", C.c_void_p),
                 ("max_desc", C.c_uint32), ("max_req", C.c_uint32), ("max_blob", C.c_uint32), ("reserved", C.c_uint32)]
 
 
@@ -97,13 +98,13 @@ class RlBatchC(C.Structure):
     """rl_batch_c: the compact host wire format (rl_hip.h)."""
     _fields_ = [("n_desc", C.c_uint32), ("n_req", C.c_uint32), ("blob_bytes", C.c_uint32), ("flags", C.c_uint32),
                 ("now_base", C.c_int64), ("prefix_blob", C.c_void_p), ("desc_word", C.c_void_p),
-                ("req_word", C.c_void_p), ("req_of", C.c_void_p)]
+                ("req_word", C.c_void_p), ("req_of", C.c_void_p), ("ttl_jitter", C.c_void_p)]
 
 
 class RlHostBatchC(C.Structure):
     _fields_ = [("prefix_blob", C.c_void_p), ("desc_word", C.c_void_p), ("req_word", C.c_void_p),
-                ("req_of", C.c_void_p), ("max_desc", C.c_uint32), ("max_req", C.c_uint32), ("max_blob", C.c_uint32),
-                ("reserved", C.c_uint32)]
+                ("req_of", C.c_void_p), ("ttl_jitter", C.c_void_p), ("max_desc", C.c_uint32), ("max_req", C.c_uint32),
+                ("max_blob", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 BC_ONE_PER_REQ = 1   # RL_BC_ONE_PER_REQ
@@ -236,6 +237,9 @@ class Batch:
     req_of: np.ndarray    # uint32 [n_desc]
     now: np.ndarray       # int64 [n_req]
     hits: np.ndarray      # uint32 [n_req]
+    # uint16 [n_desc] or None: EXPIRE jitter per descriptor, seconds (rl_batch.ttl_jitter;
+    # JitterRand.Int63n(EXPIRATION_JITTER_MAX_SECONDS) drawn in serial order, fixed_cache_impl.go:69-72)
+    jit: Optional[np.ndarray] = None
 
     @property
     def n_desc(self) -> int:
@@ -255,7 +259,8 @@ class Batch:
         b0, b1 = int(self.off[d0]), int(self.off[d1])
         return Batch(self.blob[b0:b1].copy(), (self.off[d0:d1 + 1] - b0).astype(np.uint32),
                      self.rule[d0:d1].copy(), (self.req_of[d0:d1] - r0).astype(np.uint32),
-                     self.now[r0:r1].copy(), self.hits[r0:r1].copy())
+                     self.now[r0:r1].copy(), self.hits[r0:r1].copy(),
+                     None if self.jit is None else self.jit[d0:d1].copy())
 
 
 def cache_key_prefix(domain: str, entries: Sequence[tuple]) -> bytes:
@@ -267,9 +272,10 @@ def cache_key_prefix(domain: str, entries: Sequence[tuple]) -> bytes:
     return bytes(out)
 
 
-def build_batch(requests: Sequence[tuple]) -> Batch:
+def build_batch(requests: Sequence[tuple], jit=None) -> Batch:
     """requests: [(domain, [entries | None...], [rule_id...], hits_addend, now)] where each
-    descriptor is a list of (key, value) and rule_id is NIL_RULE for a nil limit."""
+    descriptor is a list of (key, value) and rule_id is NIL_RULE for a nil limit. jit: the
+    EXPIRE jitter per descriptor (flat, serial order), or None."""
     blob = bytearray()
     off, rule, req_of, now, hits = [0], [], [], [], []
     for r, (domain, descs, rules, ha, t) in enumerate(requests):
@@ -284,7 +290,7 @@ def build_batch(requests: Sequence[tuple]) -> Batch:
         hits.append(ha)
     return Batch(np.frombuffer(bytes(blob), dtype=np.uint8).copy(), np.array(off, np.uint32),
                  np.array(rule, np.uint32), np.array(req_of, np.uint32), np.array(now, np.int64),
-                 np.array(hits, np.uint32))
+                 np.array(hits, np.uint32), None if jit is None else np.asarray(jit, np.uint16))
 
 
 def _ptr(a: np.ndarray) -> int:
@@ -301,6 +307,7 @@ class CompactBatch:
     req_word: np.ndarray   # uint32 [n_req]
     req_of: Optional[np.ndarray]  # uint32 [n_desc] or None (one descriptor per request)
     now_base: int
+    jit: Optional[np.ndarray] = None  # uint16 [n_desc] or None: EXPIRE jitter (rl_batch_c.ttl_jitter)
 
     @property
     def n_desc(self) -> int:
@@ -320,11 +327,13 @@ class CompactBatch:
                                                                 self.flags, self.now_base)
         s.prefix_blob, s.desc_word, s.req_word = _ptr(self.blob), _ptr(self.desc_word), _ptr(self.req_word)
         s.req_of = 0 if self.req_of is None else _ptr(self.req_of)
+        s.ttl_jitter = 0 if self.jit is None else _ptr(self.jit)
         return s
 
     def wire_bytes(self) -> int:
         """Bytes this batch moves host -> device (rl_submit_c's copies, without the blob slack)."""
-        return int(self.blob.shape[0]) + 4 * self.n_desc + 4 * self.n_req + (0 if self.req_of is None else 4 * self.n_desc)
+        return (int(self.blob.shape[0]) + 4 * self.n_desc + 4 * self.n_req + (0 if self.req_of is None else 4 * self.n_desc)
+                + (0 if self.jit is None else 2 * self.n_desc))
 
 
 def compact_batch(b: Batch) -> CompactBatch:
@@ -348,16 +357,24 @@ def compact_batch(b: Batch) -> CompactBatch:
         raise ValueError("request times span more than 255 s or hits_addend >= 2^24")
     rw = ((b.hits.astype(np.uint32) & 0xFFFFFF) | (delta.astype(np.uint32) << 24)).astype(np.uint32)
     one = b.n_desc == b.n_req and np.array_equal(b.req_of, np.arange(b.n_desc, dtype=np.uint32))
-    return CompactBatch(blob, dw, rw, None if one else b.req_of.copy(), base)
+    return CompactBatch(blob, dw, rw, None if one else b.req_of.copy(), base,
+                        None if b.jit is None else np.ascontiguousarray(b.jit, np.uint16))
 
 
 def _batch_struct(b: Batch, ptrs=None) -> RlBatch:
     s = RlBatch()
     s.n_desc, s.n_req, s.blob_bytes, s.reserved = b.n_desc, b.n_req, int(b.blob.shape[0]), 0
     if ptrs is None:
-        ptrs = [_ptr(b.blob), _ptr(b.off), _ptr(b.rule), _ptr(b.req_of), _ptr(b.now), _ptr(b.hits)]
-    s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        ptrs = [_ptr(b.blob), _ptr(b.off), _ptr(b.rule), _ptr(b.req_of), _ptr(b.now), _ptr(b.hits),
+                0 if b.jit is None else _ptr(b.jit)]
+    _set_ptrs(s, ptrs)
     return s
+
+
+def _set_ptrs(s: RlBatch, ptrs):
+    """blob, off, rule, req_of, now, hits[, ttl_jitter] into an rl_batch."""
+    s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs[:6]
+    s.ttl_jitter = ptrs[6] if len(ptrs) > 6 and ptrs[6] else 0
 
 
 # ---------------------------------------------------------------------------
@@ -469,16 +486,19 @@ class Engine:
             return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(n,))
         got = dict(blob=view(hb.prefix_blob, hb.max_blob, np.uint8), off=view(hb.prefix_off, hb.max_desc + 1, np.uint32),
                    rule=view(hb.rule_id, hb.max_desc, np.uint32), req_of=view(hb.req_of, hb.max_desc, np.uint32),
-                   now=view(hb.now, hb.max_req, np.int64), hits=view(hb.hits_addend, hb.max_req, np.uint32))
+                   now=view(hb.now, hb.max_req, np.int64), hits=view(hb.hits_addend, hb.max_req, np.uint32),
+                   jit=view(hb.ttl_jitter, hb.max_desc, np.uint16))
         cache[hb.prefix_blob] = got
         return got
 
-    def submit_staged(self, n_desc: int, n_req: int, blob_bytes: int, staged: dict):
-        """rl_submit of a batch built in place in an acquired staging slot (no host copy)."""
+    def submit_staged(self, n_desc: int, n_req: int, blob_bytes: int, staged: dict, jitter: bool = False):
+        """rl_submit of a batch built in place in an acquired staging slot (no host copy);
+        jitter: the slot's jitter array holds the batch's EXPIRE jitter."""
         s = RlBatch()
         s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
         s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = (
             staged[k].ctypes.data for k in ("blob", "off", "rule", "req_of", "now", "hits"))
+        s.ttl_jitter = staged["jit"].ctypes.data if jitter else 0
         self._check(self.lib.rl_submit(self.h, C.byref(s), None, None), "rl_submit")
 
     # ---- compact host batches (rl_batch_c, raw replies) ----
@@ -500,18 +520,20 @@ class Engine:
         def view(ptr, n, dt):
             return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(np.ctypeslib.as_ctypes_type(dt))), shape=(n,))
         got = dict(blob=view(hb.prefix_blob, hb.max_blob, np.uint8), desc_word=view(hb.desc_word, hb.max_desc, np.uint32),
-                   req_word=view(hb.req_word, hb.max_req, np.uint32), req_of=view(hb.req_of, hb.max_desc, np.uint32))
+                   req_word=view(hb.req_word, hb.max_req, np.uint32), req_of=view(hb.req_of, hb.max_desc, np.uint32),
+                   jit=view(hb.ttl_jitter, hb.max_desc, np.uint16))
         cache[hb.prefix_blob] = got
         return got
 
     def submit_c_staged(self, n_desc: int, n_req: int, blob_bytes: int, now_base: int, staged: dict,
-                        one_per_req: bool = True):
+                        one_per_req: bool = True, jitter: bool = False):
         """rl_submit_c of a compact batch built in place in an acquired slot (no host copy)."""
         s = RlBatchC()
         s.n_desc, s.n_req, s.blob_bytes, s.now_base = n_desc, n_req, blob_bytes, now_base
         s.flags = BC_ONE_PER_REQ if one_per_req else 0
         s.prefix_blob, s.desc_word, s.req_word = (staged[k].ctypes.data for k in ("blob", "desc_word", "req_word"))
         s.req_of = 0 if one_per_req else staged["req_of"].ctypes.data
+        s.ttl_jitter = staged["jit"].ctypes.data if jitter else 0
         self._check(self.lib.rl_submit_c(self.h, C.byref(s)), "rl_submit_c")
 
     def wait_raw_view(self, n_desc: int) -> np.ndarray:
@@ -554,15 +576,15 @@ class Engine:
     def submit_device_async(self, n_desc: int, n_req: int, blob_bytes: int, ptrs, out_ptr: int, thr_ptr: int):
         s = RlBatch()
         s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
-        s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        _set_ptrs(s, ptrs)
         self._check(self.lib.rl_submit_device(self.h, C.byref(s), out_ptr, thr_ptr), "rl_submit_device")
 
     @staticmethod
     def device_batch(n_desc: int, n_req: int, blob_bytes: int, ptrs) -> RlBatch:
-        """An rl_batch of device pointers (ptrs = blob, off, rule, req_of, now, hits)."""
+        """An rl_batch of device pointers (ptrs = blob, off, rule, req_of, now, hits[, ttl_jitter])."""
         s = RlBatch()
         s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
-        s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        _set_ptrs(s, ptrs)
         return s
 
     def submit_pipelined(self, n_desc: int, n_req: int, blob_bytes: int, ptrs, out_ptr: int, thr_ptr: int):
@@ -636,7 +658,7 @@ class Engine:
         """Device batch -> routed records grouped by owner; returns the per-owner counts."""
         s = RlBatch()
         s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
-        s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        _set_ptrs(s, ptrs)
         counts = (C.c_uint32 * n_shards)()
         self._check(self.lib.rl_route_pack(self.h, C.byref(s), origin, n_shards, send_ptr, send_counts_ptr, perm_ptr,
                                            counts), "rl_route_pack")
@@ -647,7 +669,7 @@ class Engine:
         """rl_route_pack without the host round trip: (count, status) per owner in x (device)."""
         s = RlBatch()
         s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
-        s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        _set_ptrs(s, ptrs)
         self._check(self.lib.rl_route_pack_async(self.h, C.byref(s), origin, n_shards, send_ptr, x_ptr, perm_ptr),
                     "rl_route_pack_async")
 
@@ -656,7 +678,7 @@ class Engine:
         """rl_route_pack_strided: one-kernel pack, owner j's records at send[j * stride ...]."""
         s = RlBatch()
         s.n_desc, s.n_req, s.blob_bytes, s.reserved = n_desc, n_req, blob_bytes, 0
-        s.prefix_blob, s.prefix_off, s.rule_id, s.req_of, s.now, s.hits_addend = ptrs
+        _set_ptrs(s, ptrs)
         self._check(self.lib.rl_route_pack_strided(self.h, C.byref(s), origin, n_shards, stride, send_ptr, x_ptr,
                                                    perm_ptr), "rl_route_pack_strided")
 

@@ -31,6 +31,7 @@ engine in rank order, so the multi-GPU result equals one serial DoLimit stream.
 from __future__ import annotations
 
 from dataclasses import dataclass
+from typing import Optional
 
 import torch
 import torch.distributed as dist
@@ -52,6 +53,7 @@ class DeviceBatch:
     now: torch.Tensor    # int64 [n_req]
     hits: torch.Tensor   # int32 [n_req]
     nbytes: int = -1     # prefix bytes used (off[-1]); -1 = read it from the device
+    jit: Optional[torch.Tensor] = None  # int16 [n_desc] (uint16 EXPIRE jitter) or None
 
     @property
     def n_desc(self) -> int:
@@ -69,12 +71,14 @@ class DeviceBatch:
         # the device reads prefix bytes as 16-B loads: the blob is readable RL_BLOB_SLACK bytes past its end
         blob = np.zeros(int(b.blob.shape[0]) + hiprl.BLOB_SLACK, np.uint8)
         blob[:b.blob.shape[0]] = b.blob
+        jit = getattr(b, "jit", None)
         return cls(t(blob), t(b.off.view(np.int32)), t(b.rule.view(np.int32)), t(b.req_of.view(np.int32)),
-                   t(b.now), t(b.hits.view(np.int32)), int(b.off[-1]))
+                   t(b.now), t(b.hits.view(np.int32)), int(b.off[-1]),
+                   None if jit is None else t(np.ascontiguousarray(jit, np.uint16).view(np.int16)))
 
     def ptrs(self):
         return [self.blob.data_ptr(), self.off.data_ptr(), self.rule.data_ptr(), self.req_of.data_ptr(),
-                self.now.data_ptr(), self.hits.data_ptr()]
+                self.now.data_ptr(), self.hits.data_ptr(), 0 if self.jit is None else self.jit.data_ptr()]
 
     def blob_bytes(self) -> int:
         if self.nbytes < 0:

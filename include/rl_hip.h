@@ -128,6 +128,10 @@ typedef struct rl_batch {
   const uint32_t* req_of;      /* n_desc */
   const int64_t* now;          /* n_req: unix seconds, one per request (TimeSource.UnixNow) */
   const uint32_t* hits_addend; /* n_req: RateLimitRequest.HitsAddend (0 means 1, fixed_cache_impl.go:39) */
+  const uint16_t* ttl_jitter;  /* n_desc or NULL (= all 0): seconds added to the EXPIRE of the descriptor's
+                                  INCRBY, JitterRand.Int63n(EXPIRATION_JITTER_MAX_SECONDS) drawn by the host in
+                                  serial order (fixed_cache_impl.go:69-72); the key lives until its last INCRBY's
+                                  now + divider + jitter. Ignored for nil limits and local-cache hits */
 } rl_batch;
 
 /* One DescriptorStatus plus its stat increments (20 B). */
@@ -198,6 +202,7 @@ typedef struct rl_host_batch {
   uint32_t* req_of;
   int64_t* now;
   uint32_t* hits_addend;
+  uint16_t* ttl_jitter;  /* the slot's jitter array: pass it as rl_batch.ttl_jitter to use it */
   uint32_t max_desc, max_req, max_blob, reserved;
 } rl_host_batch;
 int rl_host_acquire(rl_engine* e, rl_host_batch* out);
@@ -255,12 +260,14 @@ typedef struct rl_batch_c {
   const uint32_t* desc_word;    /* n_desc */
   const uint32_t* req_word;     /* n_req */
   const uint32_t* req_of;       /* n_desc, or NULL with RL_BC_ONE_PER_REQ */
+  const uint16_t* ttl_jitter;   /* n_desc or NULL: rl_batch.ttl_jitter */
 } rl_batch_c;
 typedef struct rl_host_batch_c {
   uint8_t* prefix_blob;
   uint32_t* desc_word;
   uint32_t* req_word;
   uint32_t* req_of;
+  uint16_t* ttl_jitter;
   uint32_t max_desc, max_req, max_blob, reserved;
 } rl_host_batch_c;
 /* The next free staging slot, compact layout (the rl_host_acquire contract). */

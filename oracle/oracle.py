@@ -40,7 +40,7 @@ def lib():
         L.rlo_destroy.argtypes = [vp]
         L.rlo_load_rules.argtypes = [vp, vp, u32]
         L.rlo_load_rules.restype = C.c_int
-        sub = [vp, u32, vp, vp, vp, vp, u32, vp, vp, vp, vp]
+        sub = [vp, u32, vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
         L.rlo_submit.argtypes = sub
         L.rlo_submit.restype = C.c_int
         L.rlo_submit_mt.argtypes = [vp, C.c_int] + sub[1:]
@@ -102,8 +102,11 @@ class Oracle:
     def submit(self, b, threads: int = 1):
         out = np.zeros(b.n_desc, STATUS_DTYPE)
         thr = np.zeros(b.n_req, np.uint32)
+        jit = getattr(b, "jit", None)  # EXPIRE jitter per descriptor (uint16), or None
+        if jit is not None:
+            jit = np.ascontiguousarray(jit, np.uint16)
         args = (b.n_desc, _p(b.blob), _p(b.off), _p(b.rule), _p(b.req_of), b.n_req, _p(b.now), _p(b.hits),
-                _p(out), _p(thr))
+                None if jit is None else _p(jit), _p(out), _p(thr))
         if threads > 1:
             rc = self.L.rlo_submit_mt(self.h, threads, *args)
         else:

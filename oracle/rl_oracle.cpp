@@ -6,8 +6,9 @@
 // INCRBY returns the post-increment int64 (Redis semantics; pinned by
 // test/redis/driver_impl_test.go:121-133, miniredis v2.11.4: INCRBY -> 1 then 2).
 // EXPIRE follows Redis: every INCRBY is followed by `EXPIRE key ttl` (fixed_cache_impl.go:
-// 26-29), ttl = UnitToDivider(unit) + jitter (:69-72; this restatement takes jitter 0 — with
-// jitter the reference itself is nondeterministic), the key is alive while now < expiry and
+// 26-29), ttl = UnitToDivider(unit) + jitter (:69-72: JitterRand.Int63n(jitterMax) per INCRBY;
+// the draws are an input here, one per descriptor, as the host batcher draws them — 0 when the
+// caller passes none), the key is alive while now < expiry and
 // an expired key reads as missing (INCRBY starts from 0). Keys are exact strings, so a
 // MINUTE key "p_3600" and an HOUR key "p_3600" are one Redis key (one store) and one
 // freecache entry, whose TTL is the unit divider of the Set (base_limiter.go:102).
@@ -230,7 +231,7 @@ void build_keys(const rlo_engine* e, uint32_t d0, uint32_t d1, const uint8_t* bl
 // descriptors of the request (all of them, or one key shard's). Returns the request's
 // ThrottleMillis contribution.
 uint32_t do_limit(rlo_engine* e, const std::vector<Desc>& keys, const uint32_t* rule_id, int64_t now,
-                  uint32_t hits_addend, rlo_status* out) {
+                  uint32_t hits_addend, const uint16_t* jitter, rlo_status* out) {
   // hitsAddend := utils.Max(1, request.HitsAddend)  :39
   const uint32_t h = umax(1u, hits_addend);
   // HOT LOOP 1 :55-86 — local-cache lookups for every descriptor precede any Set.
@@ -254,7 +255,8 @@ uint32_t do_limit(rlo_engine* e, const std::vector<Desc>& keys, const uint32_t* 
       RKey& c = e->redis[store][keys[k].key];  // a new key is {0, 0}: expired
       if (now >= c.exp) c.count = 0;
       c.count += (int64_t)h;
-      c.exp = now + unit_to_divider(e->rules[rule_id[keys[k].i]].unit);
+      // EXPIRE key UnitToDivider(unit) + JitterRand.Int63n(max)  fixed_cache_impl.go:69-72
+      c.exp = now + unit_to_divider(e->rules[rule_id[keys[k].i]].unit) + (jitter ? jitter[keys[k].i] : 0);
       results[k] = (uint32_t)c.count;
     }
   }
@@ -293,7 +295,7 @@ uint32_t do_limit(rlo_engine* e, const std::vector<Desc>& keys, const uint32_t* 
 
 int rlo_submit(rlo_engine* e, uint32_t n_desc, const uint8_t* prefix_blob, const uint32_t* prefix_off,
                const uint32_t* rule_id, const uint32_t* req_of, uint32_t n_req, const int64_t* now,
-               const uint32_t* hits_addend, rlo_status* out, uint32_t* req_throttle_ms) {
+               const uint32_t* hits_addend, const uint16_t* ttl_jitter, rlo_status* out, uint32_t* req_throttle_ms) {
   int rc = validate(e, n_desc, prefix_off, rule_id, req_of, n_req);
   if (rc) return rc;
   merge_shards(e);
@@ -304,7 +306,7 @@ int rlo_submit(rlo_engine* e, uint32_t n_desc, const uint8_t* prefix_blob, const
     while (d1 < n_desc && req_of[d1] == r) ++d1;
     keys.clear();
     build_keys(e, d, d1, prefix_blob, prefix_off, rule_id, now[r], keys);
-    req_throttle_ms[r] = do_limit(e, keys, rule_id, now[r], hits_addend[r], out);
+    req_throttle_ms[r] = do_limit(e, keys, rule_id, now[r], hits_addend[r], ttl_jitter, out);
     d = d1;
   }
   return 0;
@@ -317,9 +319,10 @@ int rlo_submit(rlo_engine* e, uint32_t n_desc, const uint8_t* prefix_blob, const
 // outputs equal rlo_submit's.
 int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* prefix_blob,
                   const uint32_t* prefix_off, const uint32_t* rule_id, const uint32_t* req_of, uint32_t n_req,
-                  const int64_t* now, const uint32_t* hits_addend, rlo_status* out, uint32_t* req_throttle_ms) {
+                  const int64_t* now, const uint32_t* hits_addend, const uint16_t* ttl_jitter, rlo_status* out,
+                  uint32_t* req_throttle_ms) {
   if (n_threads <= 1)
-    return rlo_submit(e, n_desc, prefix_blob, prefix_off, rule_id, req_of, n_req, now, hits_addend, out,
+    return rlo_submit(e, n_desc, prefix_blob, prefix_off, rule_id, req_of, n_req, now, hits_addend, ttl_jitter, out,
                       req_throttle_ms);
   int rc = validate(e, n_desc, prefix_off, rule_id, req_of, n_req);
   if (rc) return rc;
@@ -394,7 +397,7 @@ int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* 
           keys.clear();
           while (b < L.size() && L[b].req == L[a].req) keys.push_back(std::move(L[b++].d));
           const uint32_t r = L[a].req;
-          thr[o].emplace_back(r, do_limit(shard[o], keys, rule_id, now[r], hits_addend[r], out));
+          thr[o].emplace_back(r, do_limit(shard[o], keys, rule_id, now[r], hits_addend[r], ttl_jitter, out));
           a = b;
         }
       }

@@ -67,12 +67,13 @@ int rlo_load_rules(rlo_engine* e, const rlo_rule* rules, uint32_t n);
  * Returns 0, or a negative value on bad input. */
 int rlo_submit(rlo_engine* e, uint32_t n_desc, const uint8_t* prefix_blob, const uint32_t* prefix_off,
                const uint32_t* rule_id, const uint32_t* req_of, uint32_t n_req, const int64_t* now,
-               const uint32_t* hits_addend, rlo_status* out, uint32_t* req_throttle_ms);
+               const uint32_t* hits_addend, const uint16_t* ttl_jitter, rlo_status* out, uint32_t* req_throttle_ms);
 
 /* Same semantics, key-sharded over n_threads host threads (the "B2" CPU baseline). */
 int rlo_submit_mt(rlo_engine* e, int n_threads, uint32_t n_desc, const uint8_t* prefix_blob,
                   const uint32_t* prefix_off, const uint32_t* rule_id, const uint32_t* req_of, uint32_t n_req,
-                  const int64_t* now, const uint32_t* hits_addend, rlo_status* out, uint32_t* req_throttle_ms);
+                  const int64_t* now, const uint32_t* hits_addend, const uint16_t* ttl_jitter, rlo_status* out,
+                  uint32_t* req_throttle_ms);
 
 /* Unit-level restatement of GetResponseDescriptorStatus for one descriptor given the
  * LimitInfo (limitBeforeIncrease, limitAfterIncrease) (base_limiter.go:23-35,70-177).

@@ -39,14 +39,40 @@ struct Shim {
     trace.push_back(pos);
   }
 };
+
+// The tests' jitter source (EXPIRATION_JITTER_MAX_SECONDS): draw k = splitmix64(seed + k) mod n,
+// so a test can replay the k-th draw of a batcher (they are made in its enqueue order).
+uint64_t splitmix(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+int64_t g_jitter_max = 0;
+uint64_t g_jitter_seed = 0;
+void set_jitter(HipSettings& hs) {
+  hs.expiration_jitter_max_seconds = g_jitter_max;
+  if (g_jitter_max > 0) {
+    auto k = std::make_shared<std::atomic<uint64_t>>(0);
+    const uint64_t seed = g_jitter_seed;
+    hs.jitter_rand = [k, seed](int64_t n) { return (int64_t)(splitmix(seed + k->fetch_add(1)) % (uint64_t)n); };
+  }
+}
 }  // namespace
 
 extern "C" {
+
+// The jitter settings of the caches created next (0 = none).
+void rlc_next_jitter(int64_t max_seconds, uint64_t seed) {
+  g_jitter_max = max_seconds;
+  g_jitter_seed = seed;
+}
 
 // flags: bit 0 = per-second split (REDIS_PERSECOND), bit 1 = no early answers (HIP_BATCH_ANSWER_EARLY=false)
 void* rlc_create(int local_cache, float near_ratio, int flags, uint32_t window_us) {
   auto* s = new Shim();
   HipSettings hs;
+  set_jitter(hs);
   hs.local_cache = local_cache != 0;
   hs.near_limit_ratio = near_ratio;
   hs.per_second_split = (flags & 1) != 0;
@@ -71,6 +97,7 @@ void* rlc_create_routed(uint32_t n_shards, uint32_t rank, const uint8_t* id, int
                         uint32_t step_us, uint32_t rule_sync_every, uint32_t batch_limit) {
   auto* s = new Shim();
   HipSettings hs;
+  set_jitter(hs);
   hs.local_cache = local_cache != 0;
   hs.batch_limit = batch_limit;
   hs.log2_slots[0] = hs.log2_slots[1] = hs.log2_slots[2] = 16;

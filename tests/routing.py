@@ -38,9 +38,12 @@ def concat_batches(batches):
         boff += int(b.off[-1])
         roff += b.n_req
     off = np.concatenate(offs + [np.array([boff])]).astype(np.uint32)
+    jit = None
+    if any(getattr(b, "jit", None) is not None for b in batches):
+        jit = np.concatenate([b.jit if b.jit is not None else np.zeros(b.n_desc, np.uint16) for b in batches])
     return hiprl.Batch(np.concatenate(blobs).astype(np.uint8), off, np.concatenate(rules).astype(np.uint32),
                        np.concatenate(reqs).astype(np.uint32), np.concatenate(nows).astype(np.int64),
-                       np.concatenate(hits).astype(np.uint32))
+                       np.concatenate(hits).astype(np.uint32), None if jit is None else jit.astype(np.uint16))
 
 
 def owners_of(b, rules, n_shards, seed):

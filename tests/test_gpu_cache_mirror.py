@@ -555,3 +555,167 @@ def test_routed_batcher_g4_shared_keys_traced_order(local_cache):
     assert len({place[t][0] for t in order}) > 3
     _replay(order, calls, res, rules, local_cache)
     _parallel(G, lambda r: lib.rlc_destroy(hs[r]))
+
+
+def _splitmix(z):
+    z = (z + 0x9E3779B97F4A7C15) & (2 ** 64 - 1)
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2 ** 64 - 1)
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2 ** 64 - 1)
+    return z ^ (z >> 31)
+
+
+def _replay_jitter(order, calls, res, rules, draws_of):
+    """_replay with the EXPIRE jitter the batcher drew: draws_of(tag) -> the call's draws, one
+    per descriptor with a limit (0 for a nil one)."""
+    o = oracle.Oracle()
+    o.load_rules(rules)
+    for tag in order:
+        d, de, ru, h, tq = calls[tag]
+        b = hiprl.build_batch([(d, de, [hiprl.NIL_RULE if x is None else x for x in ru], h, tq)], jit=draws_of(tag))
+        st, thr = o.submit(b)
+        got, gthr = res[tag]
+        for k, g in enumerate(got):
+            want = (int(st["code_flags"][k]) & 0xFF, int(st["limit_remaining"][k]), ru[k] is not None,
+                    int(st["reset_s"][k]) if ru[k] is not None else 0)
+            assert (g[0], g[1], bool(g[2]), g[3] if ru[k] is not None else 0) == want, (tag, k, got, want)
+        assert gthr == int(thr[0]), tag
+
+
+def _jitter_draws(order_by_source, calls, jmax, seed):
+    """The k-th descriptor with a limit a batcher put in a batch got splitmix64(seed + k) % jmax
+    (the shim's jitter source): the draws of every call, from each batcher's own order."""
+    draws = {}
+    for order in order_by_source:
+        k = 0
+        for tag in order:
+            js = []
+            for r in calls[tag][2]:
+                if r is None:
+                    js.append(0)
+                else:
+                    js.append(_splitmix(seed + k) % jmax)
+                    k += 1
+            draws[tag] = js
+    return draws
+
+
+NKEYS = 12
+
+
+def _two_phase_calls(rng, n_calls, t0):
+    """Phase 0 at a minute-aligned second: SECOND and MINUTE limits on 12 shared keys (one key
+    string per key); phase 1 twenty seconds later: MINUTE only, continuing a string only if its
+    last EXPIRE's jitter kept it alive."""
+    out = []
+    for ph in range(2):
+        for _ in range(n_calls):
+            nd = 1 + int(rng.integers(0, 2))
+            descs = [[("k", str(int(rng.integers(0, NKEYS))))] for _ in range(nd)]
+            rr = [(int(rng.integers(0, 2)) if ph == 0 else 1) if rng.random() < 0.95 else None for _ in range(nd)]
+            out.append(("jit", descs, rr, 1, t0 + 20 * ph))
+    return out
+
+
+def test_batcher_expiration_jitter_traced_order():
+    """HipSettings.expiration_jitter_max_seconds: the single-GPU batcher draws one jitter per
+    descriptor with a limit, in enqueue order, and ships it in the compact batch; replaying the
+    calls in the batcher's traced order with those draws, one oracle gives every answer."""
+    T, n, jmax, seed = 8, 80, 40, 77
+    lib = _trace_lib(_lib())
+    lib.rlc_next_jitter.argtypes = [C.c_int64, C.c_uint64]
+    lib.rlc_next_jitter(jmax, seed)
+    m = Mirror(False, window_us=100)
+    lib.rlc_next_jitter(0, 0)
+    m.lib = lib  # (the handle's calls through the CDLL whose prototypes are declared)
+    m.lib.rlc_trace_on(m.h)
+    rules = [(1000, hiprl.SECOND), (1000, hiprl.MINUTE)]
+    ids = [m.add_rule(L, u, f"r{k}") for k, (L, u) in enumerate(rules)]
+    t0 = 1_699_920_000
+    rng = np.random.default_rng(4)
+    calls = {}
+    for t in range(T):
+        for q, c in enumerate(_two_phase_calls(rng, n, t0)):
+            calls[t * 2 * n + q] = c
+    # the seal: one SECOND request per key, last in phase 0, so every key's last EXPIRE before
+    # phase 1 is a SECOND one (alive 20 s later only with a jitter above 19)
+    seal0 = T * 2 * n
+    for k in range(NKEYS):
+        calls[seal0 + k] = ("jit", [[("k", str(k))]], [0], 1, t0)
+    res = {}
+    for ph in range(2):
+        m.lib.rlc_set_time(m.h, t0 + 20 * ph)
+
+        def caller(t):
+            for q in range(ph * n, (ph + 1) * n):
+                tag = t * 2 * n + q
+                d, de, ru, h, _ = calls[tag]
+                res[tag] = _do_tagged(m, tag, d, de, [None if x is None else ids[x] for x in ru], h)
+        _parallel(T, caller)
+        m.lib.rlc_flush(m.h)
+        if ph == 0:
+            for k in range(NKEYS):
+                d, de, ru, h, _ = calls[seal0 + k]
+                res[seal0 + k] = _do_tagged(m, seal0 + k, d, de, [ids[0]], h)
+            m.lib.rlc_flush(m.h)
+    tr = _trace(m, T * 2 * n + NKEYS)
+    order = sorted(tr, key=lambda tag: tr[tag])
+    draws = _jitter_draws([order], calls, jmax, seed)
+    _replay_jitter(order, calls, res, rules, lambda tag: draws[tag])
+    # the draws decided answers: without them the replay differs somewhere
+    with pytest.raises(AssertionError):
+        _replay_jitter(order, calls, res, rules, lambda tag: [0] * len(calls[tag][1]))
+    m.close()
+
+
+def test_routed_batcher_expiration_jitter_traced_order():
+    """The same through the multi-GPU batcher (G = 3 emulated ranks, each with its own jitter
+    source): every rank's draws follow its own gather order; the deployment's serial order is
+    (step, rank, position)."""
+    G, T, n, jmax, seed = 3, 4, 50, 40, 91
+    lib = _trace_lib(_lib())
+    lib.rlc_next_jitter.argtypes = [C.c_int64, C.c_uint64]
+    lib.rlc_create_routed.argtypes = [C.c_uint32, C.c_uint32, C.c_char_p, C.c_int, C.c_int, C.c_uint32,
+                                      C.c_uint32, C.c_uint32]
+    lib.rlc_create_routed.restype = C.c_void_p
+    lib.rlc_next_jitter(jmax, seed)
+    wid = hiprl.Router.emu_world(G)
+    hs = [None] * G
+    _parallel(G, lambda r: hs.__setitem__(r, lib.rlc_create_routed(G, r, wid, 1, 0, 300, 8, 4096)))
+    lib.rlc_next_jitter(0, 0)
+    assert all(hs), hs
+    ms = [RoutedMirror(lib, h) for h in hs]
+    rules = [(1000, hiprl.SECOND), (1000, hiprl.MINUTE)]
+    ids = [[m.add_rule(L, u, f"r{k}") for k, (L, u) in enumerate(rules)] for m in ms]
+    t0 = 1_699_920_000
+    for m in ms:
+        lib.rlc_trace_on(m.h)
+    rng = np.random.default_rng(6)
+    calls = {}
+    for r in range(G):
+        for t in range(T):
+            for q, c in enumerate(_two_phase_calls(rng, n, t0)):
+                calls[(r * T + t) * 2 * n + q] = c
+    res = {}
+    for ph in range(2):
+        for m in ms:
+            lib.rlc_set_time(m.h, t0 + 20 * ph)
+
+        def caller(i):
+            r, t = divmod(i, T)
+            for q in range(ph * n, (ph + 1) * n):
+                tag = (r * T + t) * 2 * n + q
+                d, de, ru, h, _ = calls[tag]
+                res[tag] = _do_tagged(ms[r], tag, d, de, [None if x is None else ids[r][x] for x in ru], h)
+        _parallel(G * T, caller)
+        for m in ms:
+            lib.rlc_flush(m.h)
+    place, per_rank = {}, []
+    for r, m in enumerate(ms):
+        tr = _trace(m, T * 2 * n)
+        per_rank.append(sorted(tr, key=lambda tag: tr[tag]))
+        for tag, (step, pos) in tr.items():
+            place[tag] = (step, r, pos)
+    order = sorted(place, key=lambda tag: place[tag])
+    draws = _jitter_draws(per_rank, calls, jmax, seed)
+    _replay_jitter(order, calls, res, rules, lambda tag: draws[tag])
+    _parallel(G, lambda r: lib.rlc_destroy(hs[r]))
