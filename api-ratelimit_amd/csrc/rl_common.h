@@ -414,6 +414,12 @@ struct __attribute__((aligned(16))) HotBucket {
 };
 constexpr uint32_t HB_FROZEN_PRE = 1u;  // the local cache holds the key for the whole batch
 constexpr uint32_t HB_PS = 2u;          // counts in the per-second store
+// Behind the HOT_BUCKETS buckets (one allocation): per bucket, index << 32 | jitter of the
+// freezing request's last INCRBY of the key (atomicMax; local cache only). Derived from the
+// bucket array rather than passed, since k4_group is at its scalar-register limit.
+__host__ __device__ __forceinline__ unsigned long long* hot_exp(const HotBucket* hb) {
+  return reinterpret_cast<unsigned long long*>(const_cast<HotBucket*>(hb) + HOT_BUCKETS);
+}
 
 // A hot descriptor whose decision needs the freezing request of an earlier tile (k4_group).
 struct __attribute__((aligned(16))) Deferred {

@@ -65,17 +65,17 @@ void launch_v4_hist(hipStream_t, const rl_batch&, const DevRule*, uint32_t, uint
 void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const unsigned long long* thsum,
                     unsigned long long* hoff, const uint32_t* fpart, const HotEntry* hot_list, HotBucket* hb,
                     const TableDesc& tab, HotCand* cand, uint32_t* heads_out, uint32_t* ins_out, void* scratch,
-                    const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl, unsigned long long* hexp);
+                    const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl);
 void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart,
                      void* scratch, const DevRule* rules, uint32_t n_rules, const unsigned long long* hoff, HotBucket* hb,
                      int local_cache, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
-                     uint32_t* poison, EngineCtl* ctl, unsigned long long* hexp);
+                     uint32_t* poison, EngineCtl* ctl);
 void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, const TableDesc& tab,
                      rl_status* out, uint32_t* req_thr, const HotBucket* hb, const Deferred* dfr, HotCand* cand,
                      int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads, uint32_t* wg_ins,
                      const uint32_t* scan_heads, const uint32_t* scan_ins, int routed, RegionOcc* occ, EngineCtl* ctl,
                      EngineCtl* next_ctl, EngineCtl* hctl, HotCand* hcand, const MRec* srec,
-                     const uint16_t* tstart, unsigned long long* hexp);
+                     const uint16_t* tstart);
 }  // namespace rlhip
 
 using namespace rlhip;
@@ -188,7 +188,6 @@ struct rl_engine {
   unsigned long long* v4_hoff = nullptr;      // [tile][HOT_BUCKETS] exclusive h prefix over tiles
   Deferred* v4_dfr = nullptr;                 // deferred hot descriptors
   HotBucket* v4_hb = nullptr;                 // per hot bucket batch state
-  unsigned long long* v4_hexp = nullptr;      // per hot bucket: (index, jitter) of the freezing request's last INCRBY
   void* v4_scratch = nullptr;                 // k4_group global scratch + k4_scan ranges
   uint32_t* v4_heads = nullptr;               // per-block unique-key counts (k4_group, then k4_scan)
   uint32_t* v4_ins = nullptr;                 // per-block new slots per region, 16-bit pairs (k4_group, then k4_scan)
@@ -206,6 +205,8 @@ struct rl_engine {
   hipEvent_t ev_kern[HSLOTS] = {};            // host path: the slot's kernels done (D2H may start)
   hipEvent_t ev_front[2] = {};                // k4_hist of the device slot done (on front)
   hipEvent_t ev_ready = nullptr;              // inputs of a non-pipelined submit ready (on stream)
+  hipEvent_t ev_resolve = nullptr;            // an rl_resolve_device launched on the front stream
+  bool resolve_pending = false;               // ... not yet ordered before a submit
   hipEvent_t ev_hot = nullptr;                // hot-set upload copy done (staging reusable)
   uint64_t sub_seq = 0;                       // batches submitted (host slot = seq % HSLOTS, device slot = seq & 1)
   int acquired = -1;                          // host slot handed out by rl_host_acquire
@@ -342,6 +343,10 @@ struct rl_engine {
 
 int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, int mode, hipEvent_t in_ev,
                             bool inputs_ready) {
+  if (resolve_pending) {  // rl_resolve_device ran on the front stream: a batch not starting there waits for it
+    if (!(mode == MODE_V4 && split_hist())) hipStreamWaitEvent(stream, ev_resolve, 0);
+    resolve_pending = false;
+  }
   const uint32_t n = b.n_desc;
   const bool full = mode == MODE_LSD_FULL;
   const int passes = full ? 16 : npasses;
@@ -401,16 +406,16 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     timed(KT_V4_SCAN, [&] {
       launch_v4_scan(stream, n, v4_tcount[sl], v4_thsum[sl], v4_hoff, v4_fpart[sl], hot_t + HOT_SLOTS, v4_hb, tab,
                      want_cand ? d_cand : nullptr, v4_heads + ng, v4_ins + (size_t)ng * 4, v4_scratch, d_poison,
-                     d_occ, c4, v4_hexp);
+                     d_occ, c4);
     });
     timed(KT_V4_PLACE, [&] {
       launch_v4_place(stream, b, srt, v4_tcount[sl], v4_scratch, d_rules, n_rules, v4_hoff, v4_hb, lc, out,
-                      thr, v4_dfr, routed, d_poison, c4, v4_hexp);
+                      thr, v4_dfr, routed, d_poison, c4);
     });
     timed(KT_V4_GROUP, [&] {
       launch_v4_group(stream, b, d_rules, n_rules, tab, out, thr, v4_hb, v4_dfr, d_cand, want_cand ? 1 : 0,
                       cfg.hash_seed, v4_scratch, v4_heads, v4_ins, v4_heads + ng, v4_ins + (size_t)ng * 4, routed,
-                      d_occ, c4, c4n, h_ctl, want_cand ? h_cand : nullptr, srt, v4_tcount[sl], v4_hexp);
+                      d_occ, c4, c4n, h_ctl, want_cand ? h_cand : nullptr, srt, v4_tcount[sl]);
     });
     // k4_group's last block writes the summary into h_ctl / h_cand (pinned host memory)
     e = hipGetLastError();
@@ -962,8 +967,8 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     }
     chk(hipMalloc(&e->v4_hoff, T4 * HOT_BUCKETS * 8));
     chk(hipMalloc(&e->v4_dfr, N * sizeof(Deferred) + 64));
-    chk(hipMalloc(&e->v4_hb, HOT_BUCKETS * sizeof(HotBucket)));
-    chk(hipMalloc(&e->v4_hexp, HOT_BUCKETS * 8));
+    // the buckets, then per bucket the freezing request's last INCRBY (index, jitter): hot_exp()
+    chk(hipMalloc(&e->v4_hb, HOT_BUCKETS * (sizeof(HotBucket) + 8)));
     const size_t nb = (size_t)v4_group_blocks((uint32_t)N) + v4_scan_blocks();
     chk(hipMalloc(&e->v4_heads, nb * 4 + 64));
     chk(hipMalloc(&e->v4_ins, nb * 4 * 4 + 64));
@@ -975,7 +980,7 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     chk(hipMalloc(&e->d_poison, 64));
     if (he == hipSuccess) chk(hipMemset(e->d_poison, 0, 64));
   }
-  std::vector<hipEvent_t*> evs = {&e->ev_front[0], &e->ev_front[1], &e->ev_ready, &e->ev_hot};
+  std::vector<hipEvent_t*> evs = {&e->ev_front[0], &e->ev_front[1], &e->ev_ready, &e->ev_hot, &e->ev_resolve};
   for (int k = 0; k < HSLOTS; ++k) {
     evs.push_back(&e->ev_done[k]);
     evs.push_back(&e->ev_in[k]);
@@ -1038,7 +1043,7 @@ void rl_destroy(rl_engine* e) {
     hipFree(e->v4_fpart[k]);
   }
   for (int k = 0; k < 3; ++k) hipFree(e->v4_ctl[k]);
-  for (void* p : {(void*)e->v4_hoff, (void*)e->v4_dfr, (void*)e->v4_hb, (void*)e->v4_hexp,
+  for (void* p : {(void*)e->v4_hoff, (void*)e->v4_dfr, (void*)e->v4_hb,
                   (void*)e->v4_heads, (void*)e->v4_ins, e->v4_scratch, (void*)e->d_poison, (void*)e->d_tree_nodes,
                   (void*)e->d_tree_slots, (void*)e->d_tree_names, (void*)e->d_res, (void*)e->table, (void*)e->d_occ,
                   (void*)e->d_rules, (void*)e->keys_orig, (void*)e->keys_a, (void*)e->keys_b, (void*)e->vals_a,
@@ -1708,8 +1713,17 @@ int rl_resolve_device(rl_engine* e, const rl_resolve_batch* b, uint32_t* d_rule_
   if (!b->n_desc) return 0;
   if (!b->domain || !b->entry_first || !d_rule_out || (b->n_entries && (!b->entry || !b->bytes)))
     return e->fail(RL_EINVAL, "null resolve array");
-  launch_resolve(e->stream, resolve_in(b), e->tree, d_rule_out);
+  // On the stream the next submit's first kernel runs on: the front stream while batches are in
+  // flight (k4_hist of the next batch runs there, beside the decisions of the one before), else
+  // the engine stream — so resolving the next batch never waits for the batch in flight.
+  const bool front = e->default_mode() == MODE_V4 && e->split_hist();
+  launch_resolve(front ? e->front : e->stream, resolve_in(b), e->tree, d_rule_out);
   hipError_t he = hipGetLastError();
+  if (he == hipSuccess && front) {
+    // a next submit that does not start on the front stream waits for it (run_pipeline)
+    he = hipEventRecord(e->ev_resolve, e->front);
+    e->resolve_pending = he == hipSuccess;
+  }
   return he == hipSuccess ? 0 : e->hip_fail(he, "k_resolve launch");
 }
 

@@ -392,7 +392,11 @@ __global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __rest
       const bool hotb = x.bucket < (uint32_t)HOT_BUCKETS;
       MRec m;
       m.key = hotb ? (uint64_t)sres[r] : x.key;
-      m.fp_lo = (hotb ? (uint64_t)x.bucket : (uint64_t)(uint32_t)x.lo) | ((uint64_t)x.jit << 32);
+      // EXPIRE jitter: a routed record's rides in x.lo's high half (load_routed); an unrouted
+      // descriptor's is read here (kernel-uniform test: no load without jitter), not carried
+      // through the tile
+      const uint32_t jt = in.recs ? (uint32_t)(x.lo >> 32) : desc_jit(in, i);
+      m.fp_lo = (hotb ? (uint64_t)x.bucket : (uint64_t)(uint32_t)x.lo) | ((uint64_t)jt << 32);
       m.idx = i;
       m.req = x.req;
       m.h = x.h;
@@ -482,8 +486,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
                                                    uint32_t* __restrict__ heads_out, uint32_t* __restrict__ ins_out,
                                                    uint32_t* __restrict__ ranges,
                                                    const uint32_t* __restrict__ poison,
-                                                   const RegionOcc* __restrict__ occ, EngineCtl* ctl,
-                                                   unsigned long long* __restrict__ hexp) {
+                                                   const RegionOcc* __restrict__ occ, EngineCtl* ctl) {
   const uint32_t local_cache = tab.local_cache;
   __shared__ uint32_t s_f[FP_PART_WORDS];
   __shared__ uint32_t s_pc[SCAN_W][64];
@@ -816,7 +819,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
     }
     if (lane < (uint32_t)HOT_PER_BLOCK) {
       hb[b] = x;
-      if (local_cache) hexp[b] = 0;  // the freezing request's last INCRBY: (index, jitter), k4_place / k4_group
+      if (local_cache) hot_exp(hb)[b] = 0;  // the freezing request's last INCRBY: (index, jitter), k4_place / k4_group
     }
     heads = tile::wave_sum(heads);
     if (lane == 0) heads_out[blockIdx.x] = heads;
@@ -1209,8 +1212,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
                                                HotBucket* __restrict__ hb, int local_cache,
                                                rl_status* __restrict__ out,
                                                uint32_t* __restrict__ req_thr, Deferred* __restrict__ dfr, int routed,
-                                               uint32_t* __restrict__ poison, EngineCtl* ctl,
-                                               unsigned long long* __restrict__ hexp) {
+                                               uint32_t* __restrict__ poison, EngineCtl* ctl) {
   __shared__ __attribute__((aligned(16))) uint16_t s_row[HOT_BUCKETS + 8];
   __shared__ uint32_t s_rstar[HOT_BUCKETS];
   __shared__ uint32_t s_err;
@@ -1290,7 +1292,7 @@ __global__ __launch_bounds__(NT) void k4_place(DevBatch in, const MRec* __restri
       } else {  // same request as the freezing descriptor: its INCRBY still happens
         tile::decide_at(i, a.req, rule, a.h, now_mod, hx.base, P, SEG_NO_FREEZE, rules, out, req_thr, routed);
         atomicMax(hot_counter(hx), (uint32_t)after);
-        atomicMax(&hexp[b], ((unsigned long long)i << 32) | mrec_jit(a.fp_lo));  // the last of them sets EXPIRE
+        atomicMax(&hot_exp(hb)[b], ((unsigned long long)i << 32) | mrec_jit(a.fp_lo));  // the last of them sets EXPIRE
       }
     } else if (a.req > q0) {  // froze in an earlier tile, in a request <= q0
       tile::emit_local_hit(out, i, a.h, rl.div - now_mod, rl.shadow, routed);
@@ -1403,8 +1405,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
                                                  RegionOcc* __restrict__ occ, EngineCtl* ctl, EngineCtl* next_ctl,
                                                  EngineCtl* hctl, HotCand* hcand,
                                                  const MRec* __restrict__ srec, const uint16_t* __restrict__ tstart,
-                                                 uint32_t ntiles, uint32_t n_rules,
-                                                 unsigned long long* __restrict__ hexp) {
+                                                 uint32_t ntiles, uint32_t n_rules) {
   __shared__ DevRule s_rules[LR ? LDS_RULES : 1];
   const DevRule* __restrict__ rules = LR ? s_rules : rules_g;
   __shared__ MRec s_rec[G_CAP];
@@ -1475,7 +1476,7 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
         tile::decide_at(df.idx, df.req, df.rule, df.h, df.now_mod, x.base, df.P, SEG_NO_FREEZE, rules, out, req_thr,
                       routed);
         atomicMax(hot_counter(x), (uint32_t)(x.base + df.P));
-        atomicMax(&hexp[bk], ((unsigned long long)df.idx << 32) | (df.bucket >> 16));
+        atomicMax(&hot_exp(hb)[bk], ((unsigned long long)df.idx << 32) | (df.bucket >> 16));
       }
     }
     const uint32_t nq = s_rq[0];  // ranges of group g
@@ -1699,20 +1700,6 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
     for (int r = 0; r < 8; ++r) n += s_ins[r];
     ctl->n_inserted = n;
   }
-  if (tab.local_cache && s_err == 0) {
-    // Hot keys a request froze in this batch (base_limiter.go:94-106): freecache TTL from the
-    // freezing request's time, EXPIRE from the time and jitter of that request's last INCRBY of
-    // the key (every block's k4_place / deferred atomicMax is done; read at the memory side)
-    for (uint32_t b = tid; b < (uint32_t)HOT_BUCKETS; b += G_NT) {
-      const HotBucket x = hb[b];
-      if (!x.slot || (x.flags & HB_FROZEN_PRE) || x.rstar == 0xFFFFFFFFu) continue;
-      Slot* sl = reinterpret_cast<Slot*>(x.slot);
-      const uint32_t div = rules[x.rule].div;
-      const unsigned long long w = atomicMax(&hexp[b], 0ull);
-      if (!(x.flags & HB_PS)) sl->exp = x.t_rstar + div + (uint32_t)w;
-      sl->frz = x.t_rstar + div;
-    }
-  }
   STL(1);
   if (any_cand && !in.recs) {
     u32x4 b0[CPT], b1[CPT];
@@ -1764,6 +1751,23 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
     if (tid == HEAD) hctl->tile_ctr[CAND_CTR][0] = nc;
     __threadfence_system();
   }
+  // (here, where the epilogue's candidate registers are dead)
+  if (tab.local_cache && s_err == 0) {
+    // Hot keys a request froze in this batch (base_limiter.go:94-106): freecache TTL from the
+    // freezing request's time, EXPIRE from the time and jitter of that request's last INCRBY of
+    // the key (every block's k4_place / deferred atomicMax is done; read at the memory side)
+    for (uint32_t b = tid; b < (uint32_t)HOT_BUCKETS; b += G_NT) {
+      // field loads, not a copy of the 64-B bucket (which leaves a private-segment frame)
+      const uint64_t slot = hb[b].slot;
+      const uint32_t flags = hb[b].flags, rstar = hb[b].rstar;
+      if (!slot || (flags & HB_FROZEN_PRE) || rstar == 0xFFFFFFFFu) continue;
+      Slot* sl = reinterpret_cast<Slot*>(slot);
+      const uint32_t t = hb[b].t_rstar + rules[hb[b].rule].div;
+      const unsigned long long w = __hip_atomic_load(&hot_exp(hb)[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (!(flags & HB_PS)) sl->exp = t + (uint32_t)w;
+      sl->frz = t;
+    }
+  }
   uint32_t* z = reinterpret_cast<uint32_t*>(next_ctl);
   constexpr uint32_t words = sizeof(EngineCtl) / 4;
   STL(2);
@@ -1803,29 +1807,29 @@ void launch_v4_hist(hipStream_t st, const rl_batch& b, const DevRule* rules, uin
 void launch_v4_scan(hipStream_t st, uint32_t n, const uint16_t* tstart, const unsigned long long* thsum,
                     unsigned long long* hoff, const uint32_t* fpart, const HotEntry* hot_list, HotBucket* hb,
                     const TableDesc& tab, HotCand* cand, uint32_t* heads_out, uint32_t* ins_out, void* scratch,
-                    const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl, unsigned long long* hexp) {
+                    const uint32_t* poison, const RegionOcc* occ, EngineCtl* ctl) {
   hipLaunchKernelGGL(v4::k4_scan, dim3(v4_scan_blocks()), dim3(v4::SCAN_NT), 0, st, tstart, thsum, v4_tiles(n), n, hoff,
-                     fpart, hot_list, hb, tab, cand, heads_out, ins_out, v4_ranges(scratch), poison, occ, ctl, hexp);
+                     fpart, hot_list, hb, tab, cand, heads_out, ins_out, v4_ranges(scratch), poison, occ, ctl);
 }
 void launch_v4_place(hipStream_t st, const rl_batch& b, const MRec* srec, const uint16_t* tstart,
                      void* scratch, const DevRule* rules, uint32_t n_rules, const unsigned long long* hoff,
                      HotBucket* hb, int local_cache, rl_status* out, uint32_t* req_thr, Deferred* dfr, int routed,
-                     uint32_t* poison, EngineCtl* ctl, unsigned long long* hexp) {
+                     uint32_t* poison, EngineCtl* ctl) {
   if (n_rules <= v4::LDS_RULES)
     hipLaunchKernelGGL(v4::k4_place<true>, dim3(v4_tiles(b.n_desc)), dim3(V4_THREADS), 0, st, make_dev_batch(b), srec,
                        tstart, v4_ranges(scratch), rules, n_rules, hoff, hb, local_cache, out, req_thr, dfr, routed,
-                       poison, ctl, hexp);
+                       poison, ctl);
   else
     hipLaunchKernelGGL(v4::k4_place<false>, dim3(v4_tiles(b.n_desc)), dim3(V4_THREADS), 0, st, make_dev_batch(b), srec,
                        tstart, v4_ranges(scratch), rules, n_rules, hoff, hb, local_cache, out, req_thr, dfr, routed,
-                       poison, ctl, hexp);
+                       poison, ctl);
 }
 void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, const TableDesc& tab,
                      rl_status* out, uint32_t* req_thr, const HotBucket* hb, const Deferred* dfr, HotCand* cand,
                      int cand_on, uint64_t seed, void* scratch, uint32_t* wg_heads, uint32_t* wg_ins,
                      const uint32_t* scan_heads, const uint32_t* scan_ins, int routed, RegionOcc* occ, EngineCtl* ctl,
                      EngineCtl* next_ctl, EngineCtl* hctl, HotCand* hcand, const MRec* srec,
-                     const uint16_t* tstart, unsigned long long* hexp) {
+                     const uint16_t* tstart) {
   using namespace v4;
   uint8_t* p = reinterpret_cast<uint8_t*>(scratch);
   GScratch4 gs;
@@ -1848,12 +1852,12 @@ void launch_v4_group(hipStream_t st, const rl_batch& b, const DevRule* rules, ui
     hipLaunchKernelGGL(k4_group<true>, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), rules, tab, out, req_thr,
                        hb, dfr, cand, cand_on, seed, gs, wg_heads, wg_ins, scan_heads, scan_ins,
                        (uint32_t)HOT_SCAN_BLOCKS, v4_ranges(scratch), routed, occ, ctl, next_ctl, hctl, hcand, srec,
-                       tstart, v4_tiles(b.n_desc), n_rules, hexp);
+                       tstart, v4_tiles(b.n_desc), n_rules);
   else
     hipLaunchKernelGGL(k4_group<false>, dim3(GBLOCKS), dim3(G_NT), 0, st, make_dev_batch(b), rules, tab, out, req_thr,
                        hb, dfr, cand, cand_on, seed, gs, wg_heads, wg_ins, scan_heads, scan_ins,
                        (uint32_t)HOT_SCAN_BLOCKS, v4_ranges(scratch), routed, occ, ctl, next_ctl, hctl, hcand, srec,
-                       tstart, v4_tiles(b.n_desc), n_rules, hexp);
+                       tstart, v4_tiles(b.n_desc), n_rules);
 }
 
 }  // namespace rlhip

@@ -108,7 +108,6 @@ RL_DEV uint32_t block_excl_scan(uint32_t v, uint32_t* sh_w, uint32_t& total) {
 struct D3 {
   uint64_t key, lo;
   uint32_t req, rule, h, now_mod, bucket, gen;
-  uint32_t jit;  // EXPIRE jitter (seconds) of the descriptor's INCRBY
   uint32_t uw;   // unit window slot (unit - 1) * 2 + parity, 8 = none
   uint32_t uwv;  // unit window index + 1
 };
@@ -187,7 +186,7 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
   // and inside the blob's 32 readable bytes of slack (rl_hip.h, rl_batch.prefix_blob).
   const uint32_t tid = threadIdx.x;
   const uint32_t last = in.n_desc - 1u;
-  uint32_t rl[R], q[R], qp[R], oa[R], ob[R], jv[R];
+  uint32_t rl[R], q[R], qp[R], oa[R], ob[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     const uint32_t i = min(t0 + r * NT + tid, last);
@@ -196,7 +195,6 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
     qp[r] = in.req_of[i ? i - 1u : 0u];
     oa[r] = in.off[i];
     ob[r] = in.off[i + 1u];
-    jv[r] = desc_jit(in, i);  // (kernel-uniform test: no load without jitter)
   }
   HSTF(2);
   uint32_t o0[R], len[R];
@@ -231,7 +229,6 @@ RL_DEV void load_descs(const DevBatch& in, const DevRule* __restrict__ rules, ui
     D3& x = d[r];
     x.req = i < in.n_desc ? q[r] : 0u;
     x.rule = i < in.n_desc ? rl[r] : RL_NIL_RULE;
-    x.jit = jv[r];
     // utils.Max(1, request.HitsAddend)  fixed_cache_impl.go:39
     x.h = i < in.n_desc && q[r] < in.n_req && ha[r] > 1u ? ha[r] : 1u;
     x.now_mod = 0;
@@ -281,7 +278,6 @@ RL_DEV void load_routed(const DevBatch& in, const DevRule* __restrict__ rules, u
     D3& x = d[r];
     x.req = rc[r].greq;
     x.rule = rrec_rule(rc[r].rule);
-    x.jit = rrec_jit(rc[r].rule);
     x.h = rc[r].h > 1u ? rc[r].h : 1u;
     x.now_mod = 0;
     x.gen = 0;
@@ -299,6 +295,10 @@ RL_DEV void load_routed(const DevBatch& in, const DevRule* __restrict__ rules, u
       continue;
     }
     key_of(x, FpState{rc[r].a, rc[r].b}, (int64_t)rc[r].now, rr[r], sh_hot, err);
+    // the record's EXPIRE jitter rides in lo's high half (the key's identity uses the low half):
+    // no register of its own across the tile (k4_hist's VGPR count decides what of k4_group can
+    // run beside it)
+    x.lo = (uint32_t)x.lo | ((uint64_t)rrec_jit(rc[r].rule) << 32);
   }
 }
 

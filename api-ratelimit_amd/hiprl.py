@@ -613,6 +613,11 @@ class Engine:
         self._check(self.lib.rl_load_tree(self.h, nodes.ctypes.data_as(C.POINTER(RlTreeNode)), nodes.shape[0],
                                           nb.ctypes.data, len(names)), "rl_load_tree")
 
+    def resolve_device(self, s: "RlResolveBatch", d_rule_out: int):
+        """rl_resolve_device: an rl_resolve_batch of device pointers -> rule ids in device memory,
+        ordered before the next submit."""
+        self._check(self.lib.rl_resolve_device(self.h, C.byref(s), d_rule_out), "rl_resolve_device")
+
     def resolve(self, rb) -> np.ndarray:
         """GetLimit for every descriptor of an rl_config.ResolveBatch -> rule id per descriptor."""
         out = np.zeros(max(1, rb.n_desc), np.uint32)

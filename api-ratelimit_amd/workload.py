@@ -253,6 +253,73 @@ def config4_descriptors(seed: int, n: int, fan: int = 6, values: int = 1000, dom
     return out
 
 
+CONFIG4_N = 1_000_000_000
+
+
+class Resolve4:
+    """The rl_resolve_batch of a config-4 batch: domain "bench4" and the four entries of each
+    descriptor are ranges of its own prefix bytes ("bench4_a_<v>_b_<v>_c_<v>_d_<v>_")."""
+
+    def __init__(self, blob: np.ndarray, off: np.ndarray):
+        n = int(off.shape[0]) - 1
+        o = off[:-1].astype(np.int64)
+        nd = (off[1:].astype(np.int64) - o - 22)
+        self.bytes, self.bytes_len, self.n_desc, self.n_entries = blob, int(off[-1]), n, 4 * n
+        self.domain = np.stack([o, np.full(n, 6)], 1).astype(np.uint32).ravel()
+        self.entry_first = (4 * np.arange(n + 1)).astype(np.uint32)
+        ent = np.zeros((n, 4, 4), np.int64)
+        for e in range(4):
+            ent[:, e, 0] = o + 7 + 4 * e
+            ent[:, e, 1] = 1
+            ent[:, e, 2] = o + 9 + 4 * e
+            ent[:, e, 3] = 1 if e < 3 else nd
+        self.entry = ent.astype(np.uint32).ravel()
+
+    def struct(self):
+        import hiprl
+        s = hiprl.RlResolveBatch()
+        s.n_desc, s.n_entries, s.bytes_len, s.reserved = self.n_desc, self.n_entries, self.bytes_len, 0
+        p = lambda a: a.ctypes.data if a.size else None
+        s.bytes, s.domain, s.entry_first, s.entry = p(self.bytes), p(self.domain), p(self.entry_first), p(self.entry)
+        s.override_rule = None
+        return s
+
+    def descriptors(self):
+        """[(domain, [(key, value)...])] for config_oracle.Config.get_limit."""
+        out = []
+        for i in range(self.n_desc):
+            ents = []
+            for e in range(4):
+                ko, kl, vo, vl = (int(x) for x in self.entry[16 * i + 4 * e:16 * i + 4 * e + 4])
+                ents.append((bytes(self.bytes[ko:ko + kl]).decode(), bytes(self.bytes[vo:vo + vl]).decode()))
+            do, dl = int(self.domain[2 * i]), int(self.domain[2 * i + 1])
+            out.append((bytes(self.bytes[do:do + dl]).decode(), ents))
+        return out
+
+
+def config4_batch(b: int, d: int = 1_000_000, N: int = CONFIG4_N, s: float = 1.1, seed: int = 4,
+                  t0: int = 1_700_000_000, batches_per_s: int = 1, hits_max: int = 1):
+    """Config 4 (1e9 keys, nested 4-entry descriptors resolved by the config4_yaml tree): Zipf(s)
+    ranks through the permutation; key k's entries are a = k % 10, b = k / 10 % 10,
+    c = k / 100 % 10, d = k / 1000, so the tree's key/value nodes (values 0..5) and its key-only
+    defaults are both taken. Returns (Batch with the rule ids still to resolve, its Resolve4);
+    the same layout as tools/gen/workload_gen.hip's mode 3."""
+    from hiprl import NIL_RULE
+    rank = Zipf(N, s).sample(seed, b, d) - 1
+    kv = permute(rank, N)
+    ten = np.uint64(10)
+    blob, off = prefix_blob([b"bench4_a_", kv % ten, b"_b_", kv // ten % ten, b"_c_", kv // np.uint64(100) % ten,
+                             b"_d_", kv // np.uint64(1000), b"_"])
+    if hits_max > 1:
+        h = (splitmix64(np.uint64(seed) * np.uint64(1 << 40) + np.uint64(b) * np.uint64(1 << 24)
+                        + np.arange(d, dtype=np.uint64)) % np.uint64(hits_max) + np.uint64(1)).astype(np.uint32)
+    else:
+        h = np.ones(d, np.uint32)
+    batch = Batch(blob, off, np.full(d, NIL_RULE, np.uint32), np.arange(d, dtype=np.uint32),
+                  np.full(d, t0 + b // batches_per_s, np.int64), h)
+    return batch, Resolve4(blob, off)
+
+
 # ---------------------------------------------------------------------------------------
 # Config 5: a sustained stream over simulated seconds (window rollover / expiry, variable
 # hits_addend h ~ U{1..8}, near-limit ratio 0.8), mixed SECOND / MINUTE / HOUR rules.

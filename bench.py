@@ -70,11 +70,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3],
-                    help="BASELINE config: 3 (headline), 2, or 1 (examples/ratelimit rules, 10k keys: the CPU row)")
+    ap.add_argument("--config", type=int, default=3, choices=[1, 2, 3, 4, 5],
+                    help="BASELINE config: 3 (headline), 2, 1 (examples/ratelimit rules, 10k keys: the CPU row), 4 "
+                         "(1e9 keys, 4-entry descriptors resolved on the device each step, local cache, shadow rules) "
+                         "or 5 (60 simulated seconds, hits_addend U{1..8})")
     ap.add_argument("--desc", type=int, default=1_000_000, help="descriptors per batch")
-    ap.add_argument("--batches-per-second", type=int, default=8000,
-                    help="batches per SECOND window (now advances once every K batches); 1 = round-1 mode")
+    ap.add_argument("--batches-per-second", type=int, default=0,
+                    help="batches per SECOND window (now advances once every K batches; 0: 8000, config 5: 16); "
+                         "1 = round-1 mode")
     ap.add_argument("--prefill", type=int, default=-1,
                     help="untimed batches that fill the table before warmup (-1: 1.5 windows of K batches)")
     ap.add_argument("--log2-slots", type=int, default=27,
@@ -179,23 +182,32 @@ def dry_launch_main(args):
 
 
 class DeviceGen:
-    """Config-2/3 batches made on the device (tools/gen/libworkload_gen.so) into DeviceBatch buffers."""
+    """Config-2/3/4/5 batches made on the device (tools/gen/libworkload_gen.so) into DeviceBatch
+    buffers (config 4: with the batch's rl_resolve_batch arrays, the strings being the batch's own
+    prefix bytes; its rule ids are resolved by the engine inside the step)."""
+
+    PREFIX = {2: b"bench_k_", 3: b"bench_k_", 5: b"c5_k_"}
 
     def __init__(self, config: int, d: int, seed: int, K: int, dev):
         import torch
 
-        self.torch, self.d, self.seed, self.K, self.dev = torch, d, seed, K, dev
+        self.torch, self.d, self.seed, self.K, self.dev, self.config = torch, d, seed, K, dev, config
         lib = C.CDLL(str(ROOT / "tools" / "gen" / "libworkload_gen.so"))
         vp, u32, u64, dbl = C.c_void_p, C.c_uint32, C.c_uint64, C.c_double
-        lib.rlw_keys.argtypes = [C.c_int, u64, dbl, dbl, dbl, dbl, u64, u64, u64, u32, vp, vp, vp, vp]
-        lib.rlw_bytes.argtypes = [u32, vp, vp, vp, vp, vp]
+        lib.rlw_keys2.argtypes = [C.c_int, u64, dbl, dbl, dbl, dbl, u64, u64, u64, u32, vp, vp, vp, vp, u32, vp]
+        lib.rlw_bytes2.argtypes = [u32, vp, vp, vp, vp, C.c_char_p, u32, vp]
+        lib.rlw_bytes4.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, vp]
         self.lib = lib
-        if config == 3:
-            self.N, s, self.mode = 100_000_000, 1.1, 0
+        if config in (3, 4, 5):
+            self.N = workload.CONFIG4_N if config == 4 else 100_000_000
+            s = 1.1
+            self.mode = {3: 0, 4: 3, 5: 2}[config]
             z = workload.Zipf(self.N, s)
             self.z = (s, float(z.hx1), float(z.hN), float(z.sq))
         else:
             self.N, self.mode, self.z = 1_000_000, 1, (0.0, 0.0, 0.0, 0.0)
+        self.plen = len(self.PREFIX.get(config, b""))
+        self.max_len = 28 if config == 4 else self.plen + 10  # bytes per prefix at most
         a = 2654435761
         while math.gcd(a, self.N) != 1:
             a += 2
@@ -205,10 +217,14 @@ class DeviceGen:
 
     def alloc(self):
         t, d, dev = self.torch, self.d, self.dev
-        return router.DeviceBatch(t.empty(d * 17 + 64, dtype=t.uint8, device=dev), t.zeros(d + 1, dtype=t.int32, device=dev),
-                                  t.empty(d, dtype=t.int32, device=dev), t.empty(d, dtype=t.int32, device=dev),
-                                  t.empty(d, dtype=t.int64, device=dev), t.ones(d, dtype=t.int32, device=dev),
-                                  d * 17)
+        db = router.DeviceBatch(t.empty(d * self.max_len + 64, dtype=t.uint8, device=dev),
+                                t.zeros(d + 1, dtype=t.int32, device=dev), t.empty(d, dtype=t.int32, device=dev),
+                                t.empty(d, dtype=t.int32, device=dev), t.empty(d, dtype=t.int64, device=dev),
+                                t.ones(d, dtype=t.int32, device=dev), d * self.max_len)
+        if self.config == 4:  # the rl_resolve_batch arrays (device)
+            db.res = (t.empty(2 * d, dtype=t.int32, device=dev), t.empty(d + 1, dtype=t.int32, device=dev),
+                      t.empty(16 * d, dtype=t.int32, device=dev))
+        return db
 
     def make(self, b: int):
         db = self.alloc()
@@ -219,13 +235,29 @@ class DeviceGen:
         """Batch b (counter stream b): now = T0 + b // K."""
         t = self.torch
         st = t.cuda.current_stream(self.dev).cuda_stream
-        rc = self.lib.rlw_keys(self.mode, self.N, *self.z, self.seed, b, self.mult, self.d, self.key.data_ptr(),
-                               db.rule.data_ptr(), self.len.data_ptr(), st)
+        hits = db.hits.data_ptr() if self.config == 5 else None
+        rc = self.lib.rlw_keys2(self.mode, self.N, *self.z, self.seed, b, self.mult, self.d, self.key.data_ptr(),
+                                db.rule.data_ptr(), self.len.data_ptr(), hits, self.plen, st)
         t.cumsum(self.len, 0, dtype=t.int32, out=db.off[1:])
-        rc |= self.lib.rlw_bytes(self.d, self.key.data_ptr(), db.off.data_ptr(), db.blob.data_ptr(), db.req_of.data_ptr(), st)
+        if self.config == 4:
+            dom, first, ent = db.res
+            rc |= self.lib.rlw_bytes4(self.d, self.key.data_ptr(), db.off.data_ptr(), db.blob.data_ptr(),
+                                      db.req_of.data_ptr(), dom.data_ptr(), first.data_ptr(), ent.data_ptr(), st)
+        else:
+            rc |= self.lib.rlw_bytes2(self.d, self.key.data_ptr(), db.off.data_ptr(), db.blob.data_ptr(),
+                                      db.req_of.data_ptr(), self.PREFIX[self.config], self.plen, st)
         db.now.fill_(T0 + b // self.K)
         if rc:
             raise RuntimeError("workload generator launch failed")
+
+    def resolve_struct(self, db):
+        """Config 4: the batch's rl_resolve_batch (device pointers; strings = its prefix bytes)."""
+        dom, first, ent = db.res
+        s = hiprl.RlResolveBatch()
+        s.n_desc, s.n_entries, s.bytes_len, s.reserved = self.d, 4 * self.d, db.blob_bytes(), 0
+        s.bytes, s.domain, s.entry_first, s.entry = db.blob.data_ptr(), dom.data_ptr(), first.data_ptr(), ent.data_ptr()
+        s.override_rule = None
+        return s
 
 
 class HostGen:
@@ -280,9 +312,11 @@ def pmc_traffic(dom: str):
             pm.get("hbm_bytes_per_batch"))
 
 
-def cpu_baseline(args, rules, d, seed, K, b0):
+def cpu_baseline(args, rules, d, seed, K, b0, eng=None):
     """The C++ oracle (serial DoLimit restatement) on host batches of the same stream (numpy
-    generator, batch indices from b0): 1 thread, then N key-sharded threads on the same batches."""
+    generator, batch indices from b0): 1 thread, then N key-sharded threads on the same batches.
+    Config 4: the sample's rule ids are resolved beforehand (untimed, the engine's host
+    rl_resolve): the CPU leg times DoLimit only."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle as orc
 
@@ -290,11 +324,19 @@ def cpu_baseline(args, rules, d, seed, K, b0):
     if args.config == 1:
         def gen(b, d, seed, batches_per_s, t0):
             return workload.config1_batch(b, d=d, seed=seed, t0=t0)
+    elif args.config == 4:
+        def gen(b, d, seed, batches_per_s, t0):
+            hb, r4 = workload.config4_batch(b, d=d, seed=seed, t0=t0, batches_per_s=batches_per_s)
+            hb.rule = eng.resolve(r4)[:d].astype(np.uint32)
+            return hb
+    elif args.config == 5:
+        def gen(b, d, seed, batches_per_s, t0):
+            return workload.config5_batch(b, d=d, N=100_000_000, seed=seed, t0=t0, batches_per_s=batches_per_s)
     else:
         gen = workload.config3_batch if args.config == 3 else workload.config2_batch
     hbs, legs = [], {}
     for threads in (1, n_thr):
-        o = orc.Oracle()
+        o = orc.Oracle(local_cache=args.config == 4)
         o.load_rules(rules)
         n_done, t_cpu, nb = 0, 0.0, 0
         while t_cpu < args.cpu_seconds and nb < 64:
@@ -433,11 +475,27 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    d, K = args.desc, max(1, args.batches_per_second)
+    d, K = args.desc, max(1, args.batches_per_second or (16 if args.config == 5 else 8000))
     lg = args.log2_slots
+    tree = None
     if args.config == 3:
         rules, log2 = workload.CONFIG3_RULES, (lg, lg, lg, 12)
         wl = "config3: 1e8 keys Zipf s=1.1, SECOND/MINUTE/HOUR by rank%3, 1 descriptor/request"
+    elif args.config == 4:
+        import rl_config
+        # 1e9 keys: a larger live set than config 3's; 2^28 slots per region (51.5 GB)
+        lg = 28 if args.log2_slots == 27 else lg
+        log2 = (lg, lg, lg, 12)
+        tree = rl_config.RateLimitConfig([("config4.yaml", workload.config4_yaml(4))])
+        rules = [(r[0], r[1], k % 2 == 0) for k, r in enumerate(tree.rule_table())]  # every other rule shadow
+        wl = ("config4: 1e9 keys Zipf s=1.1, 4-entry descriptors (a, b, c, d) resolved on the device in every step "
+              "(rl_resolve_device) by a 4-level descriptor tree (workload.config4_yaml(4)), local over-limit cache on, "
+              "every other rule in shadow mode, 1 descriptor/request")
+    elif args.config == 5:
+        rules, log2 = workload.CONFIG5_RULES, (lg, lg, lg, 12)
+        wl = (f"config5: 60 simulated seconds ({K} batches per second, 59 s of prefill), 1e8 keys Zipf s=1.1, "
+              "SECOND 20 / MINUTE 400 / HOUR 9000 by rank%3, hits_addend U{1..8}, near-limit ratio 0.8, "
+              "1 descriptor/request")
     elif args.config == 2:
         rules, log2 = workload.CONFIG2_RULES, (lg, 12, 12, 12)
         wl = "config2: 1e6 uniform keys, SECOND L=5, 1 descriptor/request"
@@ -450,15 +508,19 @@ def main():
         rules, log2 = workload.CONFIG1_RULES, (20, 16, 16, 16)
         wl = ("config1: examples/ratelimit rules (rl.foo.baz SECOND 1, mongo_cps SECOND 500), 10k keys, "
               "1 descriptor/request, now +1 s per batch")
-    prefill = args.prefill if args.prefill >= 0 else (K + K // 2 if K > 1 else 0)
-    seed = {1: 1, 2: 2, 3: 3}[args.config] + 7919 * rank  # each rank its own stream
+    prefill = args.prefill if args.prefill >= 0 else (59 * K if args.config == 5 else K + K // 2 if K > 1 else 0)
+    seed = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5}[args.config] + 7919 * rank  # each rank its own stream
     routed = (world > 1 or args.force_routed) and not args.independent
     # an owner may receive up to every origin's batch (hot keys concentrate on their owner)
     cap = d * world if routed else d
     eng = hiprl.Engine(device=local, log2_slots=log2, max_batch_desc=cap, max_batch_req=cap,
                        max_blob_bytes=cap * 32 + 64, sort_bits=48, pipeline=args.pipeline,
-                       lib_path=(ROOT / args.lib) if args.lib else None)
+                       lib_path=(ROOT / args.lib) if args.lib else None, local_cache=args.config == 4)
+    if tree is not None:
+        tree.install(eng)  # the descriptor tree and its rule table (rl_load_tree, rl_load_rules)
     eng.load_rules(rules)
+    # config 4: rule ids resolved on the device in every step (before the batch's submit; routed:
+    # before timing, since the router's pack runs on the router's own stream)
     gen = HostGen(d, seed, dev) if args.config == 1 else DeviceGen(args.config, d, seed, K, dev)
     rtr = nrt = None
     if routed and args.native_router:
@@ -483,6 +545,8 @@ def main():
             if rtr is not None:
                 rtr.step(db)
                 continue
+            if args.config == 4 and nrt is None:
+                eng.resolve_device(gen.resolve_struct(db), db.rule.data_ptr())
             sb = hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs())
             o, t = outs[(first + j) % len(outs)].data_ptr(), thrs[(first + j) % len(thrs)].data_ptr()
             if nrt is not None:
@@ -516,6 +580,10 @@ def main():
         db = ring[b % len(ring)]
         gen.fill(b, db)
         torch.cuda.current_stream(dev).synchronize()
+        if args.config == 4:
+            eng.resolve_device(gen.resolve_struct(db), db.rule.data_ptr())
+            if nrt is not None or rtr is not None:
+                torch.cuda.synchronize()  # (the router's pack runs on its own stream)
         if rtr is not None:
             rtr.step(db)
             continue
@@ -538,6 +606,10 @@ def main():
     b0 = prefill
     dbs = [gen.make(b0 + j) for j in range(args.warmup + args.steps + n_kt)]
     torch.cuda.synchronize()
+    if args.config == 4 and (nrt is not None or rtr is not None):
+        for db in dbs:  # routed: rule ids resolved before timing (the N = 1 line resolves inside the step)
+            eng.resolve_device(gen.resolve_struct(db), db.rule.data_ptr())
+        torch.cuda.synchronize()
     run(dbs[:args.warmup])
     if dist:
         dist.barrier()
@@ -763,6 +835,11 @@ def main():
     alg_def = ("achieved = algorithmic bytes of one batch (SURVEY §8d: prefixes + 12 B/desc + 16 B/req + 20 B/desc out "
                "+ 64 B per unique key) / the dominant kernel's average launch time (HIP events on the engine stream, "
                "kernels unoverlapped)")
+    if args.config == 4 and not routed:
+        # + the resolve step's inputs and output (the reference's descriptor entries): domain (off, len)
+        # 8 B, entry_first 4 B, 4 entries x 16 B, the rule id written 4 B per descriptor
+        alg_bytes += 80 * d
+        alg_def += "; config 4: + 80 B/desc of rl_resolve_batch inputs and rule-id output (resolved in the step)"
     if routed and rstats is not None:
         # an owner's launch decides the records it received, not a whole batch: price it at those
         # (32-B record in, 8-B raw reply out per record, 64 B per unique key of the owner batch)
@@ -803,7 +880,7 @@ def main():
 
     cpu = None
     if world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(args, rules, d, seed, K, b0)
+        cpu = cpu_baseline(args, rules, d, seed, K, b0, eng)
 
     live_frac = [round(occ["live"][r] / occ["slots"][r], 4) for r in range(8)]
     if routed and nrt is not None:

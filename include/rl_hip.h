@@ -561,8 +561,9 @@ typedef struct rl_resolve_batch {
 
 /* Host memory in and out; synchronous. rule_out[n_desc]. */
 int rl_resolve(rl_engine* e, const rl_resolve_batch* batch, uint32_t* rule_out);
-/* Device memory in and out; ordered on the engine's stream (before an rl_submit_device of
- * the same batch), asynchronous. */
+/* Device memory in and out, asynchronous: ordered before the engine's next submit (run on the
+ * stream that submit's first kernel uses, so with batches in flight it runs beside their
+ * decisions, as the next batch's fingerprint pass does). */
 int rl_resolve_device(rl_engine* e, const rl_resolve_batch* device_batch, uint32_t* d_rule_out);
 
 #ifdef __cplusplus

@@ -1,4 +1,4 @@
-// workload_gen.hip — device-side generator of BASELINE config-2/3 batches for bench.py
+// workload_gen.hip — device-side generator of BASELINE config-2/3/4/5 batches for bench.py
 // (measurement tooling, not product; SURVEY.md §8d workload definitions).
 //
 // The same construction as api-ratelimit_amd/workload.py — bounded Zipf(s) ranks by
@@ -45,9 +45,13 @@ __device__ __forceinline__ uint32_t ndigits(uint64_t v) {
   return d;
 }
 
-// mode 0: Zipf ranks (config 3: rule = rank % 3); mode 1: uniform ranks (config 2: rule 0).
+// mode 0: Zipf ranks (config 3: rule = rank % 3); mode 1: uniform ranks (config 2: rule 0);
+// mode 2: Zipf ranks, rule = rank % 3, and hits_addend ~ U{1..8} per request (config 5); mode 3:
+// Zipf ranks of config 4's 4-entry descriptors (no rule: the device resolves it). plen: the
+// prefix's length before the key's decimal digits.
 __global__ void k_keys(ZipfC z, int mode, uint64_t ctr0, uint64_t mult, uint32_t n, uint64_t* __restrict__ key,
-                       uint32_t* __restrict__ rule, uint32_t* __restrict__ len) {
+                       uint32_t* __restrict__ rule, uint32_t* __restrict__ len, uint32_t* __restrict__ hits,
+                       uint32_t plen) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint64_t rank = 0;
@@ -68,24 +72,77 @@ __global__ void k_keys(ZipfC z, int mode, uint64_t ctr0, uint64_t mult, uint32_t
   }
   const uint64_t kv = (rank * mult + 0x2545F491ull) % z.N;  // rank, mult < 2^32: no overflow
   key[i] = kv;
+  if (mode == 3) {  // "bench4_a_<d0>_b_<d1>_c_<d2>_d_<kv / 1000>_"
+    len[i] = 22u + ndigits(kv / 1000u);
+    return;
+  }
   rule[i] = mode == 1 ? 0u : (uint32_t)(rank % 3);
-  len[i] = 8u + ndigits(kv) + 1u;  // "bench_k_" + decimal + "_"
+  len[i] = plen + ndigits(kv) + 1u;  // prefix + decimal + "_"
+  if (mode == 2 && hits) hits[i] = (uint32_t)(splitmix64(ctr0 ^ 0x5A5A5A5A00000000ull ^ i) % 8u) + 1u;
+}
+
+struct Prefix {
+  char p[16];
+  uint32_t n;
+};
+// Config 4 (BASELINE: 1e9 keys, nested 4-entry descriptors resolved by the tree): the key's
+// digits pick the entries' values, so the tree's key/value nodes (values 0..5) and its
+// key-only defaults are both taken; the prefix bytes double as the resolve batch's strings:
+// domain "bench4" and each entry's key and value are ranges of the prefix.
+__global__ void k_bytes4(uint32_t n, const uint64_t* __restrict__ key, const uint32_t* __restrict__ off,
+                         uint8_t* __restrict__ blob, uint32_t* __restrict__ req_of, uint32_t* __restrict__ domain,
+                         uint32_t* __restrict__ entry_first, uint32_t* __restrict__ entry) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n) return;
+  entry_first[i] = 4u * i;
+  if (i == n) return;
+  const uint32_t o = off[i];
+  uint8_t* p = blob + o;
+  const char pre[7] = {'b', 'e', 'n', 'c', 'h', '4', '_'};
+  for (int k = 0; k < 7; ++k) p[k] = (uint8_t)pre[k];
+  const uint64_t kv = key[i];
+  const uint32_t dg[3] = {(uint32_t)(kv % 10u), (uint32_t)(kv / 10u % 10u), (uint32_t)(kv / 100u % 10u)};
+  const char names[4] = {'a', 'b', 'c', 'd'};
+  for (int e = 0; e < 3; ++e) {
+    p[7 + 4 * e] = (uint8_t)names[e];
+    p[8 + 4 * e] = '_';
+    p[9 + 4 * e] = (uint8_t)('0' + dg[e]);
+    p[10 + 4 * e] = '_';
+  }
+  p[19] = 'd';
+  p[20] = '_';
+  uint64_t v = kv / 1000u;
+  const uint32_t nd = off[i + 1] - o - 22u;
+  for (int k = (int)nd - 1; k >= 0; --k) {
+    p[21 + k] = (uint8_t)('0' + v % 10);
+    v /= 10;
+  }
+  p[21 + nd] = '_';
+  req_of[i] = i;
+  domain[2 * i] = o;
+  domain[2 * i + 1] = 6u;
+  for (int e = 0; e < 4; ++e) {
+    uint32_t* x = entry + 16u * i + 4u * e;
+    x[0] = o + 7u + 4u * e;  // key
+    x[1] = 1u;
+    x[2] = o + 9u + 4u * e;  // value
+    x[3] = e < 3 ? 1u : nd;
+  }
 }
 
 __global__ void k_bytes(uint32_t n, const uint64_t* __restrict__ key, const uint32_t* __restrict__ off,
-                        uint8_t* __restrict__ blob, uint32_t* __restrict__ req_of) {
+                        uint8_t* __restrict__ blob, uint32_t* __restrict__ req_of, Prefix pre) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint8_t* p = blob + off[i];
-  const char pre[8] = {'b', 'e', 'n', 'c', 'h', '_', 'k', '_'};
-  for (int k = 0; k < 8; ++k) p[k] = (uint8_t)pre[k];
+  for (uint32_t k = 0; k < pre.n; ++k) p[k] = (uint8_t)pre.p[k];
   uint64_t v = key[i];
-  const uint32_t nd = off[i + 1] - off[i] - 9u;
+  const uint32_t nd = off[i + 1] - off[i] - pre.n - 1u;
   for (int k = (int)nd - 1; k >= 0; --k) {
-    p[8 + k] = (uint8_t)('0' + v % 10);
+    p[pre.n + k] = (uint8_t)('0' + v % 10);
     v /= 10;
   }
-  p[8 + nd] = '_';
+  p[pre.n + nd] = '_';
   req_of[i] = i;
 }
 
@@ -99,14 +156,43 @@ int rlw_keys(int mode, uint64_t N, double s, double hx1, double hN, double sq, u
   ZipfC z{s, hx1, hN, sq, N};
   const uint64_t ctr0 = ((seed * 1000003ull + stream) & 0xFFFFFFull) << 40;
   hipLaunchKernelGGL(k_keys, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)hip_stream, z, mode, ctr0, mult, n, key,
-                     rule, len);
+                     rule, len, (uint32_t*)nullptr, 8u);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// The same with the per-request hits (mode 2) and the prefix length before the digits.
+int rlw_keys2(int mode, uint64_t N, double s, double hx1, double hN, double sq, uint64_t seed, uint64_t stream,
+              uint64_t mult, uint32_t n, uint64_t* key, uint32_t* rule, uint32_t* len, uint32_t* hits,
+              uint32_t plen, void* hip_stream) {
+  ZipfC z{s, hx1, hN, sq, N};
+  const uint64_t ctr0 = ((seed * 1000003ull + stream) & 0xFFFFFFull) << 40;
+  hipLaunchKernelGGL(k_keys, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)hip_stream, z, mode, ctr0, mult, n, key,
+                     rule, len, hits, plen);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // Prefix bytes at the given offsets (off[n + 1], exclusive scan of the lengths) and req_of = i.
 int rlw_bytes(uint32_t n, const uint64_t* key, const uint32_t* off, uint8_t* blob, uint32_t* req_of,
               void* hip_stream) {
-  hipLaunchKernelGGL(k_bytes, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)hip_stream, n, key, off, blob, req_of);
+  Prefix pre{{'b', 'e', 'n', 'c', 'h', '_', 'k', '_'}, 8u};
+  hipLaunchKernelGGL(k_bytes, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)hip_stream, n, key, off, blob, req_of,
+                     pre);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+int rlw_bytes2(uint32_t n, const uint64_t* key, const uint32_t* off, uint8_t* blob, uint32_t* req_of,
+               const char* prefix, uint32_t plen, void* hip_stream) {
+  Prefix pre{};
+  if (plen > sizeof pre.p) return -1;
+  for (uint32_t k = 0; k < plen; ++k) pre.p[k] = prefix[k];
+  pre.n = plen;
+  hipLaunchKernelGGL(k_bytes, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)hip_stream, n, key, off, blob, req_of,
+                     pre);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+// Config 4: prefix bytes, req_of, and the resolve batch's domain / entry_first / entry arrays.
+int rlw_bytes4(uint32_t n, const uint64_t* key, const uint32_t* off, uint8_t* blob, uint32_t* req_of,
+               uint32_t* domain, uint32_t* entry_first, uint32_t* entry, void* hip_stream) {
+  hipLaunchKernelGGL(k_bytes4, dim3((n + 256) / 256), dim3(256), 0, (hipStream_t)hip_stream, n, key, off, blob, req_of,
+                     domain, entry_first, entry);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
