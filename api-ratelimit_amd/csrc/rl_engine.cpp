@@ -84,11 +84,12 @@ namespace {
 
 enum KernelId {
   KT_FINGERPRINT, KT_HISTOGRAM, KT_HIST_SCAN, KT_SORT_PASS, KT_SCAN, KT_LEADER, KT_DECIDE, KT_FALLBACK, KT_MEMSET,
-  KT_CAND, KT_V4_HIST, KT_V4_SCAN, KT_V4_PLACE, KT_V4_GROUP, KT_COUNT
+  KT_CAND, KT_V4_HIST, KT_V4_SCAN, KT_V4_PLACE, KT_V4_GROUP, KT_RESOLVE, KT_COUNT
 };
 const char* const kKernelNames[KT_COUNT] = {"k_fingerprint", "k_histogram", "k_hist_scan", "k_sort_pass", "k_scan",
                                             "k_leader",      "k_decide",    "fallback",    "memset",      "k_cand_state",
-                                            "k4_hist",       "k4_scan",     "k4_place",    "k4_group"};
+                                            "k4_hist",       "k4_scan",     "k4_place",    "k4_group",
+                                            "k_resolve"};
 
 enum Mode { MODE_LSD = 1, MODE_LSD_FULL = 2, MODE_V4 = 4 };
 
@@ -213,7 +214,7 @@ struct rl_engine {
 
   // descriptor tree (rl_load_tree / rl_resolve)
   TreeNodeDev* d_tree_nodes = nullptr;
-  uint32_t* d_tree_slots = nullptr;
+  uint64_t* d_tree_slots = nullptr;
   uint8_t* d_tree_names = nullptr;
   TreeDesc2 tree{};
   bool has_tree = false;
@@ -1672,9 +1673,10 @@ int rl_load_tree(rl_engine* e, const rl_tree_node* nodes, uint32_t n_nodes, cons
   if (e->n_fl) return e->fail(RL_ESTATE, "rl_load_tree while a batch is in flight");
   if ((n_nodes && !nodes) || (names_len && !names)) return e->fail(RL_EINVAL, "null tree array");
   std::vector<TreeNodeDev> hn;
-  std::vector<uint32_t> hs;
+  std::vector<uint64_t> hs;
   std::string err;
-  int rc = build_tree(nodes, n_nodes, names, names_len, hn, hs, err);
+  uint32_t mask = 0;
+  int rc = build_tree(nodes, n_nodes, names, names_len, hn, hs, mask, err);
   if (rc) return e->fail(rc, "%s", err.c_str());
   hipError_t he = hipStreamSynchronize(e->stream);  // resolutions queued on the old tree finish first
   hipFree(e->d_tree_nodes);
@@ -1685,17 +1687,17 @@ int rl_load_tree(rl_engine* e, const rl_tree_node* nodes, uint32_t n_nodes, cons
   e->d_tree_names = nullptr;
   e->has_tree = false;
   if (he == hipSuccess) he = hipMalloc(&e->d_tree_nodes, std::max<size_t>(1, hn.size()) * sizeof(TreeNodeDev));
-  if (he == hipSuccess) he = hipMalloc(&e->d_tree_slots, hs.size() * 4);
+  if (he == hipSuccess) he = hipMalloc(&e->d_tree_slots, hs.size() * 8);
   if (he == hipSuccess) he = hipMalloc(&e->d_tree_names, std::max<size_t>(16, names_len));
   if (he == hipSuccess && !hn.empty())
     he = hipMemcpy(e->d_tree_nodes, hn.data(), hn.size() * sizeof(TreeNodeDev), hipMemcpyHostToDevice);
-  if (he == hipSuccess) he = hipMemcpy(e->d_tree_slots, hs.data(), hs.size() * 4, hipMemcpyHostToDevice);
+  if (he == hipSuccess) he = hipMemcpy(e->d_tree_slots, hs.data(), hs.size() * 8, hipMemcpyHostToDevice);
   if (he == hipSuccess && names_len) he = hipMemcpy(e->d_tree_names, names, names_len, hipMemcpyHostToDevice);
   if (he != hipSuccess) return e->hip_fail(he, "rl_load_tree");
   e->tree.nodes = e->d_tree_nodes;
   e->tree.slots = e->d_tree_slots;
   e->tree.names = e->d_tree_names;
-  e->tree.mask = (uint32_t)hs.size() - 1u;
+  e->tree.mask = mask;
   e->has_tree = true;
   return 0;
 }
@@ -1703,6 +1705,8 @@ int rl_load_tree(rl_engine* e, const rl_tree_node* nodes, uint32_t n_nodes, cons
 static ResolveIn resolve_in(const rl_resolve_batch* b) {
   ResolveIn in;
   in.n_desc = b->n_desc;
+  in.n_entries = b->n_entries;
+  in.bytes_len = b->bytes_len;
   in.bytes = b->bytes;
   in.domain = b->domain;
   in.entry_first = b->entry_first;
@@ -1722,7 +1726,8 @@ int rl_resolve_device(rl_engine* e, const rl_resolve_batch* b, uint32_t* d_rule_
   // flight (k4_hist of the next batch runs there, beside the decisions of the one before), else
   // the engine stream — so resolving the next batch never waits for the batch in flight.
   const bool front = e->default_mode() == MODE_V4 && e->split_hist();
-  launch_resolve(front ? e->front : e->stream, resolve_in(b), e->tree, d_rule_out);
+  // (kernel timing runs everything on the engine stream: split_hist() is off then)
+  e->timed(KT_RESOLVE, [&] { launch_resolve(front ? e->front : e->stream, resolve_in(b), e->tree, d_rule_out); });
   hipError_t he = hipGetLastError();
   if (he == hipSuccess && front) {
     // a next submit that does not start on the front stream waits for it (run_pipeline)

@@ -10,29 +10,35 @@
 
 namespace rlhip {
 
-constexpr uint32_t TREE_EMPTY = 0xFFFFFFFFu;  // empty edge-table slot
+constexpr uint32_t TREE_EMPTY = 0xFFFFFFFFu;  // empty edge-table slot (node id half)
 constexpr uint32_t TREE_NONE = 0xFFFFFFFFu;   // lookup miss
+constexpr int TREE_INLINE = 32;               // name bytes held in the node itself
+constexpr int TREE_PROBE = 4;                 // edge slots read per probe round (one round trip)
 
-struct TreeNodeDev {
+// 64 B: the header and the first TREE_INLINE name bytes arrive in one load pair, so a lookup
+// whose name fits compares it without a third round trip.
+struct __attribute__((aligned(64))) TreeNodeDev {
   uint32_t parent;      // node id or RL_TREE_ROOT (a domain)
-  uint32_t name_off;    // map key: domain name, or finalKey = key["_" value]
-  uint32_t name_len;
+  uint32_t name_len;    // map key: domain name, or finalKey = key["_" value]
   uint32_t rule;        // rule id of the node's limit, RL_NIL_RULE if none
   uint32_t n_children;  // len(descriptors) (config_impl.go:320)
-  uint32_t hash;        // tree_hash(parent, name)
+  uint32_t hash;        // tree_hash(parent, fold(name))
+  uint32_t name_off;    // the whole name in the names blob (bytes past TREE_INLINE)
   uint32_t pad[2];
+  uint32_t name[TREE_INLINE / 4];  // first bytes of the name, little-endian, zero-padded
 };
-static_assert(sizeof(TreeNodeDev) == 32, "tree node layout");
+static_assert(sizeof(TreeNodeDev) == 64, "tree node layout");
 
 struct TreeDesc2 {
   const TreeNodeDev* nodes;
-  const uint32_t* slots;  // (parent, name) edge table: node id or TREE_EMPTY
+  const uint64_t* slots;  // (parent, name) edge table: hash << 32 | node id, or ~0; mask + TREE_PROBE entries
+                          // (the first TREE_PROBE - 1 repeated at the end, so a probe round never wraps)
   const uint8_t* names;
-  uint32_t mask;          // slots - 1 (power of two)
+  uint32_t mask;          // power-of-two table size - 1 (load <= 1/4)
 };
 
 struct ResolveIn {
-  uint32_t n_desc;
+  uint32_t n_desc, n_entries, bytes_len;
   const uint8_t* bytes;
   const uint32_t* domain;         // [2 n_desc] (off, len)
   const uint32_t* entry_first;    // [n_desc + 1]
@@ -40,10 +46,13 @@ struct ResolveIn {
   const uint32_t* override_rule;  // [n_desc] or null
 };
 
-// FNV-1a over (parent, name bytes) with a final avalanche; host and device agree.
-__host__ __device__ inline uint32_t tree_hash_init(uint32_t parent) { return 2166136261u ^ (parent * 0x9E3779B1u); }
-__host__ __device__ inline uint32_t tree_hash_step(uint32_t h, uint32_t byte) { return (h ^ byte) * 16777619u; }
-__host__ __device__ inline uint32_t tree_hash_final(uint32_t h) {
+// FNV-1a fold over the name bytes, then the parent and an avalanche: a name's fold does not
+// depend on where in the tree it is looked up, so the device folds every string of a
+// descriptor before its first lookup. Host and device agree.
+constexpr uint32_t TREE_FOLD0 = 2166136261u;
+__host__ __device__ inline uint32_t tree_fold(uint32_t h, uint32_t byte) { return (h ^ byte) * 16777619u; }
+__host__ __device__ inline uint32_t tree_hash(uint32_t parent, uint32_t fold) {
+  uint32_t h = fold ^ (parent * 0x9E3779B1u + 0x7F4A7C15u);
   h ^= h >> 15;
   h *= 0x2C1B3C6Du;
   h ^= h >> 12;
@@ -53,7 +62,8 @@ __host__ __device__ inline uint32_t tree_hash_final(uint32_t h) {
 }
 
 int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint32_t names_len,
-               std::vector<TreeNodeDev>& out_nodes, std::vector<uint32_t>& out_slots, std::string& err);
+               std::vector<TreeNodeDev>& out_nodes, std::vector<uint64_t>& out_slots, uint32_t& mask, std::string& err);
 void launch_resolve(hipStream_t st, const ResolveIn& in, const TreeDesc2& t, uint32_t* rule_out);
+uint32_t resolve_one_host(const ResolveIn& in, const TreeDesc2& t, uint32_t i);
 
 }  // namespace rlhip

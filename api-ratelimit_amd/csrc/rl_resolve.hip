@@ -11,11 +11,16 @@
 //     counts only at the last entry (:311-318); descend while the node has children, else
 //     stop (:320-325).
 //
-// Device layout: the tree's nodes (32 B each: parent, name, rule, child count, name hash) and
-// an open-addressing table over (parent, name) edges (u32 node ids, load <= 1/2), both small
-// enough to stay in L2. Names are compared byte-exactly after the hash matches, so
-// ("a_b") and ("a", "b") resolve exactly as the reference's string maps do. One thread per
-// descriptor; the work is a few dependent L2 lookups per entry.
+// Device layout: the tree's nodes (64 B each: parent, name length, rule, child count, name
+// hash and the name's first 32 bytes) and an open-addressing table over (parent, name) edges
+// (hash << 32 | node id, load <= 1/4), both small enough to stay in L2. Names are compared
+// byte-exactly after the hash matches, so ("a_b") and ("a", "b") resolve exactly as the
+// reference's string maps do. One thread per descriptor. A level of the walk loads the key and
+// the value as whole dwords into registers (one round trip), folds them, reads both edges'
+// first probe rounds (key_value and key) together, then both first candidates' nodes, whose
+// inline names compare against the register strings: three round trips per level where the
+// first version (byte loads in data-dependent loops) needed one per byte. Names longer than
+// 32 bytes take that byte path.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -29,73 +34,272 @@ namespace rlhip {
 
 namespace {
 
-__device__ __forceinline__ uint32_t ld_byte(const uint8_t* p, uint32_t i) { return p[i]; }
+#define RL_HD __host__ __device__
+constexpr int RS_NT = 256;        // descriptors per block, one per thread
+constexpr int SW = 8;             // dwords of a string held in registers
+constexpr uint32_t SB = 4 * SW;   // bytes: names up to 32 bytes take the register path
 
-// name = A, or A "_" B (finalKey, config_impl.go:126-129 and :300)
-__device__ uint32_t lookup(const TreeDesc2& t, uint32_t parent, const uint8_t* bytes, uint32_t a_off, uint32_t a_len,
-                           bool with_b, uint32_t b_off, uint32_t b_len) {
-  uint32_t h = tree_hash_init(parent);
-  for (uint32_t k = 0; k < a_len; ++k) h = tree_hash_step(h, ld_byte(bytes, a_off + k));
-  uint32_t len = a_len;
-  if (with_b) {
-    h = tree_hash_step(h, '_');
-    for (uint32_t k = 0; k < b_len; ++k) h = tree_hash_step(h, ld_byte(bytes, b_off + k));
-    len += 1 + b_len;
+// ---- the byte path (long names, strings at the blob's edges, an unaligned blob) ----
+// A byte from the aligned dword that holds it (never past that byte's page). Plain byte loads
+// in these loops were merged by the compiler into 16-bit loads at odd addresses, which read
+// wrong bytes on the MI355X boxes (unaligned global access is not enabled there).
+RL_HD inline uint32_t ld_u8(const uint8_t* p) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  return (*reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) >> (8u * (uint32_t)(a & 3u))) & 0xFFu;
+}
+RL_HD uint32_t fold_bytes(const uint8_t* bytes, uint32_t h, uint32_t off, uint32_t len) {
+  for (uint32_t k = 0; k < len; ++k) h = tree_fold(h, ld_u8(bytes + off + k));
+  return h;
+}
+// The queried name: A (wb false), or A "_" B (finalKey, config_impl.go:126-129 and :300), of
+// total length len, against the node's name in the names blob.
+RL_HD bool name_eq_bytes(const uint8_t* names, uint32_t noff, uint32_t len, const uint8_t* bytes, uint32_t a,
+                         uint32_t al, uint32_t b) {
+  uint32_t diff = 0;
+  for (uint32_t k = 0; k < len; ++k) {
+    const uint32_t c = k < al ? ld_u8(bytes + a + k) : k == al ? (uint32_t)'_' : ld_u8(bytes + b + (k - al - 1u));
+    diff |= ld_u8(names + noff + k) ^ c;
   }
-  h = tree_hash_final(h);
-  for (uint32_t s = h & t.mask, probes = 0; probes <= t.mask; s = (s + 1) & t.mask, ++probes) {
-    const uint32_t id = t.slots[s];
-    if (id == TREE_EMPTY) return TREE_NONE;
-    const TreeNodeDev nd = t.nodes[id];
-    if (nd.hash != h || nd.parent != parent || nd.name_len != len) continue;
-    bool eq = true;
-    for (uint32_t k = 0; eq && k < a_len; ++k) eq = t.names[nd.name_off + k] == ld_byte(bytes, a_off + k);
-    if (with_b) {
-      eq = eq && t.names[nd.name_off + a_len] == '_';
-      for (uint32_t k = 0; eq && k < b_len; ++k) eq = t.names[nd.name_off + a_len + 1 + k] == ld_byte(bytes, b_off + k);
-    }
-    if (eq) return id;
+  return diff == 0;
+}
+
+// The byte path's probe: (parent, name A["_" B]) with hash h, names compared in the blob.
+RL_HD uint32_t find_bytes(const TreeDesc2& t, uint32_t parent, uint32_t h, const uint8_t* bytes, uint32_t a,
+                          uint32_t al, uint32_t b, uint32_t len, uint32_t& rule, uint32_t& nch) {
+  uint32_t s = h & t.mask;
+  for (uint32_t probes = 0; probes <= t.mask; ++probes, s = (s + 1) & t.mask) {
+    const uint64_t w = t.slots[s];
+    if ((uint32_t)w == TREE_EMPTY) break;
+    if ((uint32_t)(w >> 32) != h) continue;
+    const uint32_t id = (uint32_t)w;
+    const uint32_t np = t.nodes[id].parent, nl = t.nodes[id].name_len, no = t.nodes[id].name_off;
+    if (np != parent || nl != len || !name_eq_bytes(t.names, no, len, bytes, a, al, b)) continue;
+    rule = t.nodes[id].rule;
+    nch = t.nodes[id].n_children;
+    return id;
   }
   return TREE_NONE;
 }
 
-__global__ __launch_bounds__(256) void k_resolve(ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= in.n_desc) return;
-  uint32_t rule = RL_NIL_RULE;
-  const uint32_t dom = lookup(t, RL_TREE_ROOT, in.bytes, in.domain[2 * i], in.domain[2 * i + 1], false, 0, 0);
-  if (dom != TREE_NONE) {
-    const uint32_t ov = in.override_rule ? in.override_rule[i] : RL_NIL_RULE;
-    if (ov != RL_NIL_RULE) {
-      rule = ov;  // descriptor.GetLimit() != nil (config_impl.go:286-296)
-    } else {
-      const uint32_t e0 = in.entry_first[i], e1 = in.entry_first[i + 1];
-      uint32_t parent = dom;
-      for (uint32_t e = e0; e < e1; ++e) {
-        const uint32_t ko = in.entry[4 * e], kl = in.entry[4 * e + 1], vo = in.entry[4 * e + 2],
-                       vl = in.entry[4 * e + 3];
-        uint32_t nd = lookup(t, parent, in.bytes, ko, kl, true, vo, vl);  // key "_" value
-        if (nd == TREE_NONE) nd = lookup(t, parent, in.bytes, ko, kl, false, 0, 0);  // key (default)
-        if (nd == TREE_NONE) break;
-        const TreeNodeDev x = t.nodes[nd];
-        if (x.rule != RL_NIL_RULE && e == e1 - 1) rule = x.rule;
-        if (x.n_children == 0) break;
-        parent = nd;
-      }
-    }
+// ---- the register path ----
+// bytes sh.. of the pair hi:lo (v_alignbyte_b32)
+RL_HD inline uint32_t align_byte(uint32_t hi, uint32_t lo, uint32_t sh) {
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
+}
+// s[k] = bytes 4k..4k+3 of the string at bytes + off (little-endian), zero past len (<= SB).
+// The blob is 4-B aligned and the string's last dword lies inside it (checked by the caller):
+// whole-dword loads at clamped indices, all in flight together.
+RL_HD void load_str(const uint8_t* bytes, uint32_t off, uint32_t len, uint32_t (&s)[SW]) {
+  if (len == 0) {
+#pragma unroll
+    for (int k = 0; k < SW; ++k) s[k] = 0u;
+    return;
   }
-  rule_out[i] = rule;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(bytes) + (off >> 2);
+  const uint32_t sh = off & 3u, nd = (sh + len + 3u) >> 2;  // dwords that hold the string (>= 1 if len)
+  const uint32_t last = nd ? nd - 1u : 0u;
+  uint32_t d[SW + 1];
+#pragma unroll
+  for (int k = 0; k <= SW; ++k) d[k] = w[min((uint32_t)k, last)];
+#pragma unroll
+  for (int k = 0; k < SW; ++k) {
+    const uint32_t v = align_byte(d[k + 1], d[k], sh);
+    const uint32_t b0 = 4u * (uint32_t)k;
+    s[k] = b0 >= len ? 0u : b0 + 4u <= len ? v : v & ((1u << (8u * (len - b0))) - 1u);
+  }
+}
+RL_HD uint32_t fold_reg(uint32_t h, const uint32_t (&s)[SW], uint32_t len) {
+#pragma unroll
+  for (int j = 0; j < (int)SB; ++j)
+    if ((uint32_t)j < len) h = tree_fold(h, (s[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+  return h;
+}
+// r = x moved n bytes up (byte j of r = byte j - n of x; zero below n), n < SB.
+RL_HD void shl_bytes(const uint32_t (&x)[SW], uint32_t n, uint32_t (&r)[SW]) {
+  uint32_t a[SW];
+#pragma unroll
+  for (int k = 0; k < SW; ++k) a[k] = x[k];
+#pragma unroll
+  for (int st = 4; st >= 1; st >>= 1) {  // whole dwords: a log shifter on n >> 2
+    const bool on = ((n >> 2) & (uint32_t)st) != 0;
+#pragma unroll
+    for (int k = SW - 1; k >= 0; --k) a[k] = on ? (k >= st ? a[k - st] : 0u) : a[k];
+  }
+  const uint32_t b = n & 3u;
+#pragma unroll
+  for (int k = SW - 1; k >= 0; --k) {
+    const uint32_t lo = k ? a[k - 1] : 0u;
+    r[k] = b ? align_byte(a[k], lo, 4u - b) : a[k];
+  }
+}
+// A node's header and inline name as four 16-B loads (fields read from the words: no copy of
+// the 64-B aligned struct, whose byte-path form the compiler got wrong).
+struct NodeView {
+  uint32_t parent, len, rule, nch, name[SW];
+};
+RL_HD NodeView load_node(const TreeDesc2& t, uint32_t id) {
+  const uint4* p = reinterpret_cast<const uint4*>(t.nodes + id);
+  const uint4 h = p[0], n0 = p[2], n1 = p[3];
+  NodeView v;
+  v.parent = h.x;
+  v.len = h.y;
+  v.rule = h.z;
+  v.nch = h.w;
+  v.name[0] = n0.x; v.name[1] = n0.y; v.name[2] = n0.z; v.name[3] = n0.w;
+  v.name[4] = n1.x; v.name[5] = n1.y; v.name[6] = n1.z; v.name[7] = n1.w;
+  return v;
+}
+RL_HD bool same(const NodeView& nd, uint32_t parent, uint32_t len, const uint32_t (&q)[SW]) {
+  uint32_t diff = (nd.parent ^ parent) | (nd.len ^ len);
+#pragma unroll
+  for (int k = 0; k < SW; ++k) diff |= nd.name[k] ^ q[k];
+  return diff == 0;
+}
+// The register path's full probe (a hash collision in the first round, or a longer chain).
+RL_HD uint32_t find_reg(const TreeDesc2& t, uint32_t parent, uint32_t h, uint32_t len, const uint32_t (&q)[SW],
+                        uint32_t& rule, uint32_t& nch) {
+  uint32_t s = h & t.mask;
+  for (uint32_t probes = 0; probes <= t.mask; ++probes, s = (s + 1) & t.mask) {
+    const uint64_t w = t.slots[s];
+    if ((uint32_t)w == TREE_EMPTY) break;
+    if ((uint32_t)(w >> 32) != h) continue;
+    const NodeView v = load_node(t, (uint32_t)w);
+    if (!same(v, parent, len, q)) continue;
+    rule = v.rule;
+    nch = v.nch;
+    return (uint32_t)w;
+  }
+  return TREE_NONE;
+}
+// First slot of the probe round (4 words from h's home) whose hash is h: its node id, or
+// TREE_NONE; done = the round settles it (an empty slot before any match).
+RL_HD uint32_t first_match(const uint64_t (&w)[TREE_PROBE], uint32_t h, bool& done) {
+  done = false;
+#pragma unroll
+  for (int j = 0; j < TREE_PROBE; ++j) {
+    if ((uint32_t)w[j] == TREE_EMPTY) {
+      done = true;
+      return TREE_NONE;
+    }
+    if ((uint32_t)(w[j] >> 32) == h) return (uint32_t)w[j];
+  }
+  return TREE_NONE;
+}
+RL_HD void probe_round(const TreeDesc2& t, uint32_t h, uint64_t (&w)[TREE_PROBE]) {
+  const uint32_t base = h & t.mask;
+#pragma unroll
+  for (int j = 0; j < TREE_PROBE; ++j) w[j] = t.slots[base + j];
+}
+
+// rateLimitConfigImpl.GetLimit (config_impl.go:274-323) for one descriptor: unknown domain ->
+// nil (:279-284); a descriptor limit override -> its rule before any walk (:286-296); per
+// entry the node of key_value, else of key (:300-309); the node's limit counts only at the
+// last entry (:311-318); descend while the node has children (:320-325).
+RL_HD uint32_t resolve_one(const ResolveIn& in, const TreeDesc2& t, uint32_t i) {
+  const uint32_t doff = in.domain[2 * i], dlen = in.domain[2 * i + 1];
+  const uint32_t e0 = in.entry_first[i], e1 = in.entry_first[i + 1];
+  const uint32_t ov = in.override_rule ? in.override_rule[i] : RL_NIL_RULE;
+  const uint64_t blen = in.bytes_len;
+  // a string outside bytes, or entries outside the entry array: nil (rl_resolve, the host
+  // form, refuses such a batch)
+  auto inside = [&](uint32_t o, uint32_t l) { return (uint64_t)o + l <= blen; };
+  // the register path: a 4-B aligned blob, the string's last dword inside it, <= SB bytes
+  const bool aligned = (reinterpret_cast<uintptr_t>(in.bytes) & 3u) == 0;
+  const uint64_t bwords = blen & ~3ull;
+  auto reg_ok = [&](uint32_t o, uint32_t l) { return aligned && l <= SB && (((uint64_t)o + l + 3u) & ~3ull) <= bwords; };
+  uint32_t rule = RL_NIL_RULE;
+  if (!(e0 <= e1 && e1 <= in.n_entries) || !inside(doff, dlen)) return rule;
+  uint32_t xr = RL_NIL_RULE, xn = 0;
+  uint32_t dom;
+  if (reg_ok(doff, dlen)) {
+    uint32_t D[SW];
+    load_str(in.bytes, doff, dlen, D);
+    dom = find_reg(t, RL_TREE_ROOT, tree_hash(RL_TREE_ROOT, fold_reg(TREE_FOLD0, D, dlen)), dlen, D, xr, xn);
+  } else {
+    dom = find_bytes(t, RL_TREE_ROOT, tree_hash(RL_TREE_ROOT, fold_bytes(in.bytes, TREE_FOLD0, doff, dlen)), in.bytes,
+                     doff, dlen, 0, dlen, xr, xn);
+  }
+  if (dom == TREE_NONE) return rule;
+  if (ov != RL_NIL_RULE) return ov;  // descriptor.GetLimit() != nil (config_impl.go:286-296)
+  uint32_t parent = dom;
+  for (uint32_t e = e0; e < e1; ++e) {
+    const uint32_t ko = in.entry[4 * e], kl = in.entry[4 * e + 1], vo = in.entry[4 * e + 2], vl = in.entry[4 * e + 3];
+    if (!inside(ko, kl) || !inside(vo, vl)) {
+      rule = RL_NIL_RULE;
+      break;
+    }
+    const uint32_t lv = kl + 1u + vl;  // key "_" value
+    uint32_t nd = TREE_NONE;
+    if (reg_ok(ko, kl) && reg_ok(vo, vl) && lv <= SB) {
+      uint32_t K[SW], V[SW], Q[SW];
+      load_str(in.bytes, ko, kl, K);
+      load_str(in.bytes, vo, vl, V);
+      const uint32_t fk = fold_reg(TREE_FOLD0, K, kl);
+      const uint32_t hv = tree_hash(parent, fold_reg(tree_fold(fk, '_'), V, vl)), hk = tree_hash(parent, fk);
+      // both edges' first probe rounds, then both first candidates' nodes, in two round trips
+      uint64_t wv[TREE_PROBE], wk[TREE_PROBE];
+      probe_round(t, hv, wv);
+      probe_round(t, hk, wk);
+      shl_bytes(V, kl + 1u, Q);  // Q = K "_" V
+#pragma unroll
+      for (int k = 0; k < SW; ++k) {
+        const uint32_t us = (uint32_t)k == (kl >> 2) ? (uint32_t)'_' << (8u * (kl & 3u)) : 0u;
+        Q[k] |= K[k] | us;
+      }
+      bool dv, dk;
+      const uint32_t cv = first_match(wv, hv, dv), ck = first_match(wk, hk, dk);
+      NodeView nv{}, nk{};
+      if (cv != TREE_NONE) nv = load_node(t, cv);
+      if (ck != TREE_NONE) nk = load_node(t, ck);
+      if (cv != TREE_NONE && same(nv, parent, lv, Q)) {
+        nd = cv;
+        xr = nv.rule;
+        xn = nv.nch;
+      } else if (!dv) {  // a hash collision in the round, or a longer probe chain: the full probe
+        nd = find_reg(t, parent, hv, lv, Q, xr, xn);
+      }
+      if (nd == TREE_NONE) {
+        if (ck != TREE_NONE && same(nk, parent, kl, K)) {
+          nd = ck;
+          xr = nk.rule;
+          xn = nk.nch;
+        } else if (!dk) {
+          nd = find_reg(t, parent, hk, kl, K, xr, xn);
+        }
+      }
+    } else {
+      const uint32_t fk = fold_bytes(in.bytes, TREE_FOLD0, ko, kl);
+      nd = find_bytes(t, parent, tree_hash(parent, fold_bytes(in.bytes, tree_fold(fk, '_'), vo, vl)), in.bytes, ko, kl,
+                      vo, lv, xr, xn);
+      if (nd == TREE_NONE) nd = find_bytes(t, parent, tree_hash(parent, fk), in.bytes, ko, kl, 0, kl, xr, xn);
+    }
+    if (nd == TREE_NONE) break;
+    if (xr != RL_NIL_RULE && e == e1 - 1) rule = xr;
+    if (xn == 0) break;
+    parent = nd;
+  }
+  return rule;
+}
+
+__global__ __launch_bounds__(RS_NT) void k_resolve(ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out) {
+  const uint32_t i = blockIdx.x * RS_NT + threadIdx.x;
+  if (i < in.n_desc) rule_out[i] = resolve_one(in, t, i);
 }
 
 }  // namespace
 
+// The same walk on the host, over host copies of the tree and the batch (tests/cshim: the
+// device code path checked against the config oracle without a GPU).
+uint32_t resolve_one_host(const ResolveIn& in, const TreeDesc2& t, uint32_t i) { return resolve_one(in, t, i); }
+
 int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint32_t names_len,
-               std::vector<TreeNodeDev>& out_nodes, std::vector<uint32_t>& out_slots, std::string& err) {
+               std::vector<TreeNodeDev>& out_nodes, std::vector<uint64_t>& out_slots, uint32_t& mask,
+               std::string& err) {
   out_nodes.assign(n, TreeNodeDev{});
   uint32_t cap = 16;
-  while (cap < 2u * n) cap <<= 1;
-  out_slots.assign(cap, TREE_EMPTY);
-  const uint32_t mask = cap - 1;
+  while (cap < 4u * n) cap <<= 1;  // load <= 1/4: a miss ends inside its first probe round
+  out_slots.assign(cap + TREE_PROBE - 1, ~0ull);
+  mask = cap - 1;
   for (uint32_t i = 0; i < n; ++i) {
     const rl_tree_node& x = nodes[i];
     if (x.parent != RL_TREE_ROOT && x.parent >= i) {
@@ -112,15 +316,18 @@ int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint
     d.name_len = x.name_len;
     d.rule = x.rule;
     d.n_children = 0;
-    uint32_t h = tree_hash_init(x.parent);
-    for (uint32_t k = 0; k < x.name_len; ++k) h = tree_hash_step(h, names[x.name_off + k]);
-    d.hash = h = tree_hash_final(h);
+    uint32_t f = TREE_FOLD0;
+    for (uint32_t k = 0; k < x.name_len; ++k) {
+      f = tree_fold(f, names[x.name_off + k]);
+      if (k < (uint32_t)TREE_INLINE) d.name[k >> 2] |= (uint32_t)names[x.name_off + k] << (8 * (k & 3));
+    }
+    const uint32_t h = d.hash = tree_hash(x.parent, f);
     if (x.parent != RL_TREE_ROOT) out_nodes[x.parent].n_children += 1;
     uint32_t s = h & mask;
     for (;; s = (s + 1) & mask) {
-      const uint32_t o = out_slots[s];
-      if (o == TREE_EMPTY) break;
-      const TreeNodeDev& y = out_nodes[o];
+      const uint64_t o = out_slots[s];
+      if ((uint32_t)o == TREE_EMPTY) break;
+      const TreeNodeDev& y = out_nodes[(uint32_t)o];
       if (y.hash == h && y.parent == x.parent && y.name_len == x.name_len &&
           std::equal(names + y.name_off, names + y.name_off + y.name_len, names + x.name_off)) {
         // loadDescriptors (config_impl.go:131-135) / loadConfig (:239-242)
@@ -129,14 +336,15 @@ int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint
         return RL_EINVAL;
       }
     }
-    out_slots[s] = i;
+    out_slots[s] = (uint64_t)h << 32 | i;
   }
+  for (int j = 0; j < TREE_PROBE - 1; ++j) out_slots[cap + j] = out_slots[j];  // probe rounds never wrap
   return 0;
 }
 
 void launch_resolve(hipStream_t st, const ResolveIn& in, const TreeDesc2& t, uint32_t* rule_out) {
   if (!in.n_desc) return;
-  hipLaunchKernelGGL(k_resolve, dim3((in.n_desc + 255) / 256), dim3(256), 0, st, in, t, rule_out);
+  hipLaunchKernelGGL(k_resolve, dim3((in.n_desc + RS_NT - 1) / RS_NT), dim3(RS_NT), 0, st, in, t, rule_out);
 }
 
 }  // namespace rlhip

@@ -1,0 +1,141 @@
+"""The device GetLimit walk (rl_resolve.hip resolve_one, the code k_resolve runs per
+descriptor) executed on the host through tests/cshim/librl_resolve_shim.so, against the config
+oracle (oracle/config_oracle.py, GetLimit config_impl.go:274-323, pinned by
+tests/test_config_golden.py). CPU only: it covers the register path (strings up to 32 bytes in
+whole-dword loads), the byte path (long names, strings whose last dword passes the blob's end,
+a blob that is not 4-B aligned) and the bounds checks, on the same source the GPU runs."""
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import config_oracle
+import hiprl
+import rl_config
+import workload
+from test_config_golden import BASIC, files
+
+SHIM = Path(__file__).resolve().parent / "cshim" / "librl_resolve_shim.so"
+
+
+@pytest.fixture(scope="module")
+def shim():
+    if not SHIM.exists():
+        subprocess.run(["make", "-C", str(SHIM.parent), SHIM.name], check=True, capture_output=True)
+    lib = C.CDLL(str(SHIM))
+    lib.rls_resolve.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.POINTER(hiprl.RlResolveBatch),
+                                C.c_void_p]
+    lib.rls_resolve.restype = C.c_int
+    return lib
+
+
+def resolve(lib, cfg, rb, shift=0):
+    """Rule ids of a ResolveBatch; shift > 0 places the bytes that many bytes past a 16-B
+    boundary (offsets unchanged), so the walk sees a blob that is not 4-B aligned."""
+    nodes, names = cfg.tree_arrays()
+    nodes = np.ascontiguousarray(nodes, np.uint32)
+    nb = np.frombuffer(names or b"\0", np.uint8)
+    s = rb.struct()
+    if shift:
+        raw = np.zeros(rb.bytes.size + 32, np.uint8)
+        base = (-raw.ctypes.data) % 16 + shift
+        raw[base:base + rb.bytes.size] = rb.bytes
+        s.bytes = raw.ctypes.data + base
+        keep = raw  # noqa: F841 (alive during the call)
+    out = np.zeros(max(1, rb.n_desc), np.uint32)
+    rc = lib.rls_resolve(nodes.ctypes.data, nodes.shape[0], nb.ctypes.data, len(names), C.byref(s), out.ctypes.data)
+    assert rc == 0
+    return out[:rb.n_desc]
+
+
+def _rule_tuple(cfg, rid):
+    if rid == hiprl.NIL_RULE:
+        return None
+    r = cfg.rules[int(rid)]
+    return (r.full_key, r.requests_per_unit, r.unit)
+
+
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+def test_basic_config(shim, shift):
+    """TestBasicConfig's lookups (config_test.go:24-149); the batch's last string ends past the
+    blob's last whole dword (the byte path), and shifted blobs take the byte path throughout."""
+    cfg = rl_config.RateLimitConfig(files("basic_config.yaml"))
+    rb = rl_config.ResolveBatch([(d, e, None) for d, e, _ in BASIC])
+    got = resolve(shim, cfg, rb, shift)
+    assert [_rule_tuple(cfg, r) for r in got] == [w for _, _, w in BASIC]
+
+
+def test_override(shim):
+    cfg = rl_config.RateLimitConfig(files("basic_config.yaml"))
+    e1 = [("key1", "value1"), ("subkey1", "something")]
+    ov = cfg.override_rule("test-domain", e1, 10, 4)
+    got = resolve(shim, cfg, rl_config.ResolveBatch([("test-domain", e1, ov), ("foo_domain", [], ov),
+                                                       ("test-domain", e1, None)]))
+    assert int(got[0]) == ov and got[1] == hiprl.NIL_RULE
+    assert _rule_tuple(cfg, got[2]) == ("test-domain.key1_value1.subkey1", 5, 1)
+
+
+@pytest.mark.parametrize("seed", [4, 5, 6])
+def test_config4_tree_against_oracle(shim, seed):
+    """A config-4 tree (4 levels, key/value nodes and defaults) and 4000 descriptors that hit
+    values, fall back to defaults, use a foreign key or an unknown domain."""
+    y = workload.config4_yaml(seed)
+    cfg = rl_config.RateLimitConfig([("c4.yaml", y)])
+    orc = config_oracle.Config([("c4.yaml", y)])
+    descs = workload.config4_descriptors(seed, 4000)
+    got = resolve(shim, cfg, rl_config.ResolveBatch([(d, e, None) for d, e in descs]))
+    for (d, e), r in zip(descs, got):
+        w = orc.get_limit(d, e)
+        have = None if r == hiprl.NIL_RULE else (cfg.rules[int(r)].requests_per_unit, cfg.rules[int(r)].unit)
+        assert have == (None if w is None else (w.requests_per_unit, w.unit)), (d, e)
+
+
+def test_long_and_empty_names(shim):
+    """Names past the 32 bytes a node holds inline and key "_" value past 32 bytes (the byte
+    path), an empty value, and names that share a prefix with a longer one."""
+    long_k, long_v = "k" * 30, "v" * 40
+    y = (
+        "domain: dlong\n"
+        "descriptors:\n"
+        f"  - key: {long_k}\n"
+        f"    value: {long_v}\n"
+        "    rate_limit: {unit: second, requests_per_unit: 3}\n"
+        f"  - key: {long_k}\n"
+        "    rate_limit: {unit: minute, requests_per_unit: 4}\n"
+        "  - key: ab\n"
+        "    value: c\n"
+        "    rate_limit: {unit: hour, requests_per_unit: 5}\n"
+        "  - key: a\n"
+        "    value: b_c\n"
+        "    rate_limit: {unit: day, requests_per_unit: 6}\n"
+        "  - key: e\n"
+        "    rate_limit: {unit: day, requests_per_unit: 7}\n"
+    )
+    cfg = rl_config.RateLimitConfig([("l.yaml", y)])
+    orc = config_oracle.Config([("l.yaml", y)])
+    descs = [("dlong", [(long_k, long_v)]), ("dlong", [(long_k, "x")]), ("dlong", [("ab", "c")]),
+             ("dlong", [("a", "b_c")]), ("dlong", [("a", "b")]), ("dlong", [("e", "")]), ("dlong", [("e", "z" * 33)]),
+             ("dlong", [(long_k[:-1], long_v)]), ("dlon", [("e", "1")])]
+    got = resolve(shim, cfg, rl_config.ResolveBatch([(d, e, None) for d, e in descs]))
+    for (d, e), r in zip(descs, got):
+        w = orc.get_limit(d, e)
+        have = None if r == hiprl.NIL_RULE else (cfg.rules[int(r)].requests_per_unit, cfg.rules[int(r)].unit)
+        assert have == (None if w is None else (w.requests_per_unit, w.unit)), (d, e)
+
+
+def test_strings_outside_bytes_resolve_nil(shim):
+    """rl_resolve_device does not refuse a batch (the host form does): a descriptor whose
+    domain or entry string lies past bytes_len, or whose entry range passes n_entries,
+    resolves to nil and the walk reads nothing outside the arrays."""
+    cfg = rl_config.RateLimitConfig(files("basic_config.yaml"))
+    rb = rl_config.ResolveBatch([("test-domain", [("key3", "foo")], None)] * 3)
+    rb.domain = rb.domain.copy()
+    rb.entry = rb.entry.copy()
+    rb.entry_first = rb.entry_first.copy()
+    rb.domain[2 * 0 + 1] = rb.bytes_len + 1       # descriptor 0: domain past the end
+    rb.entry[4 * 1 + 2] = rb.bytes_len            # descriptor 1: value offset at the end, length 3
+    rb.entry_first[3] = rb.n_entries + 5          # descriptor 2: entries past n_entries
+    got = resolve(shim, cfg, rb)
+    assert list(got) == [hiprl.NIL_RULE] * 3

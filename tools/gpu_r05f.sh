@@ -16,4 +16,4 @@ for c in 3 4 5; do
   echo "routed c$c rc=$rc"; tail -c 400 $OUT/routed_c$c.json; [ $rc -ne 0 ] && { tail -5 $OUT/routed_c$c.err; exit $rc; }
 done
 
-bash tools/ab.sh 40 "- tools/variants/lib_evdev.so - tools/variants/lib_evdev.so"
+bash tools/ab.sh 40 "- tools/variants/lib_evdev.so tools/variants/lib_nt1024.so - tools/variants/lib_evdev.so tools/variants/lib_nt1024.so"
