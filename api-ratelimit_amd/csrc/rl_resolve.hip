@@ -47,8 +47,18 @@ RL_HD inline uint32_t ld_u8(const uint8_t* p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
   return (*reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) >> (8u * (uint32_t)(a & 3u))) & 0xFFu;
 }
-RL_HD uint32_t fold_bytes(const uint8_t* bytes, uint32_t h, uint32_t off, uint32_t len) {
-  for (uint32_t k = 0; k < len; ++k) h = tree_fold(h, ld_u8(bytes + off + k));
+// Fold of the query name A["_" B] of length len (byte loads; the register path folds words).
+RL_HD uint32_t fold_query_bytes(const uint8_t* bytes, uint32_t a, uint32_t al, uint32_t b, uint32_t len) {
+  uint32_t h = TREE_FOLD0;
+  for (uint32_t k = 0; k < len; k += 4) {
+    uint32_t w = 0;
+    for (uint32_t j = 0; j < 4 && k + j < len; ++j) {
+      const uint32_t q = k + j;
+      const uint32_t c = q < al ? ld_u8(bytes + a + q) : q == al ? (uint32_t)'_' : ld_u8(bytes + b + (q - al - 1u));
+      w |= c << (8u * j);
+    }
+    h = tree_fold_word(h, w);
+  }
   return h;
 }
 // The queried name: A (wb false), or A "_" B (finalKey, config_impl.go:126-129 and :300), of
@@ -108,10 +118,12 @@ RL_HD void load_str(const uint8_t* bytes, uint32_t off, uint32_t len, uint32_t (
     s[k] = b0 >= len ? 0u : b0 + 4u <= len ? v : v & ((1u << (8u * (len - b0))) - 1u);
   }
 }
-RL_HD uint32_t fold_reg(uint32_t h, const uint32_t (&s)[SW], uint32_t len) {
+RL_HD uint32_t fold_reg(const uint32_t (&s)[SW], uint32_t len) {
+  uint32_t h = TREE_FOLD0;
+  const uint32_t nw = (len + 3u) >> 2;
 #pragma unroll
-  for (int j = 0; j < (int)SB; ++j)
-    if ((uint32_t)j < len) h = tree_fold(h, (s[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+  for (int k = 0; k < SW; ++k)
+    if ((uint32_t)k < nw) h = tree_fold_word(h, s[k]);
   return h;
 }
 // r = x moved n bytes up (byte j of r = byte j - n of x; zero below n), n < SB.
@@ -214,16 +226,17 @@ RL_HD uint32_t resolve_one(const ResolveIn& in, const TreeDesc2& t, uint32_t i) 
   if (reg_ok(doff, dlen)) {
     uint32_t D[SW];
     load_str(in.bytes, doff, dlen, D);
-    dom = find_reg(t, RL_TREE_ROOT, tree_hash(RL_TREE_ROOT, fold_reg(TREE_FOLD0, D, dlen)), dlen, D, xr, xn);
+    dom = find_reg(t, RL_TREE_ROOT, tree_hash(RL_TREE_ROOT, fold_reg(D, dlen), dlen), dlen, D, xr, xn);
   } else {
-    dom = find_bytes(t, RL_TREE_ROOT, tree_hash(RL_TREE_ROOT, fold_bytes(in.bytes, TREE_FOLD0, doff, dlen)), in.bytes,
-                     doff, dlen, 0, dlen, xr, xn);
+    dom = find_bytes(t, RL_TREE_ROOT, tree_hash(RL_TREE_ROOT, fold_query_bytes(in.bytes, doff, dlen, 0, dlen), dlen),
+                     in.bytes, doff, dlen, 0, dlen, xr, xn);
   }
   if (dom == TREE_NONE) return rule;
   if (ov != RL_NIL_RULE) return ov;  // descriptor.GetLimit() != nil (config_impl.go:286-296)
   uint32_t parent = dom;
   for (uint32_t e = e0; e < e1; ++e) {
-    const uint32_t ko = in.entry[4 * e], kl = in.entry[4 * e + 1], vo = in.entry[4 * e + 2], vl = in.entry[4 * e + 3];
+    const uint4 E = make_uint4(in.entry[4 * e], in.entry[4 * e + 1], in.entry[4 * e + 2], in.entry[4 * e + 3]);
+    const uint32_t ko = E.x, kl = E.y, vo = E.z, vl = E.w;
     if (!inside(ko, kl) || !inside(vo, vl)) {
       rule = RL_NIL_RULE;
       break;
@@ -234,18 +247,17 @@ RL_HD uint32_t resolve_one(const ResolveIn& in, const TreeDesc2& t, uint32_t i) 
       uint32_t K[SW], V[SW], Q[SW];
       load_str(in.bytes, ko, kl, K);
       load_str(in.bytes, vo, vl, V);
-      const uint32_t fk = fold_reg(TREE_FOLD0, K, kl);
-      const uint32_t hv = tree_hash(parent, fold_reg(tree_fold(fk, '_'), V, vl)), hk = tree_hash(parent, fk);
-      // both edges' first probe rounds, then both first candidates' nodes, in two round trips
-      uint64_t wv[TREE_PROBE], wk[TREE_PROBE];
-      probe_round(t, hv, wv);
-      probe_round(t, hk, wk);
       shl_bytes(V, kl + 1u, Q);  // Q = K "_" V
 #pragma unroll
       for (int k = 0; k < SW; ++k) {
         const uint32_t us = (uint32_t)k == (kl >> 2) ? (uint32_t)'_' << (8u * (kl & 3u)) : 0u;
         Q[k] |= K[k] | us;
       }
+      const uint32_t hv = tree_hash(parent, fold_reg(Q, lv), lv), hk = tree_hash(parent, fold_reg(K, kl), kl);
+      // both edges' first probe rounds, then both first candidates' nodes, in two round trips
+      uint64_t wv[TREE_PROBE], wk[TREE_PROBE];
+      probe_round(t, hv, wv);
+      probe_round(t, hk, wk);
       bool dv, dk;
       const uint32_t cv = first_match(wv, hv, dv), ck = first_match(wk, hk, dk);
       NodeView nv{}, nk{};
@@ -268,10 +280,11 @@ RL_HD uint32_t resolve_one(const ResolveIn& in, const TreeDesc2& t, uint32_t i) 
         }
       }
     } else {
-      const uint32_t fk = fold_bytes(in.bytes, TREE_FOLD0, ko, kl);
-      nd = find_bytes(t, parent, tree_hash(parent, fold_bytes(in.bytes, tree_fold(fk, '_'), vo, vl)), in.bytes, ko, kl,
-                      vo, lv, xr, xn);
-      if (nd == TREE_NONE) nd = find_bytes(t, parent, tree_hash(parent, fk), in.bytes, ko, kl, 0, kl, xr, xn);
+      nd = find_bytes(t, parent, tree_hash(parent, fold_query_bytes(in.bytes, ko, kl, vo, lv), lv), in.bytes, ko, kl, vo,
+                      lv, xr, xn);
+      if (nd == TREE_NONE)
+        nd = find_bytes(t, parent, tree_hash(parent, fold_query_bytes(in.bytes, ko, kl, 0, kl), kl), in.bytes, ko, kl, 0,
+                        kl, xr, xn);
     }
     if (nd == TREE_NONE) break;
     if (xr != RL_NIL_RULE && e == e1 - 1) rule = xr;
@@ -316,12 +329,17 @@ int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint
     d.name_len = x.name_len;
     d.rule = x.rule;
     d.n_children = 0;
-    uint32_t f = TREE_FOLD0;
+    uint32_t f = TREE_FOLD0, w = 0;
     for (uint32_t k = 0; k < x.name_len; ++k) {
-      f = tree_fold(f, names[x.name_off + k]);
-      if (k < (uint32_t)TREE_INLINE) d.name[k >> 2] |= (uint32_t)names[x.name_off + k] << (8 * (k & 3));
+      const uint32_t c = names[x.name_off + k];
+      w |= c << (8 * (k & 3));
+      if ((k & 3) == 3 || k + 1 == x.name_len) {
+        f = tree_fold_word(f, w);
+        w = 0;
+      }
+      if (k < (uint32_t)TREE_INLINE) d.name[k >> 2] |= c << (8 * (k & 3));
     }
-    const uint32_t h = d.hash = tree_hash(x.parent, f);
+    const uint32_t h = d.hash = tree_hash(x.parent, f, x.name_len);
     if (x.parent != RL_TREE_ROOT) out_nodes[x.parent].n_children += 1;
     uint32_t s = h & mask;
     for (;; s = (s + 1) & mask) {
