@@ -52,7 +52,7 @@ import workload  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 T0 = 1_700_000_020      # not minute-aligned: SECOND / MINUTE / HOUR keys in their own home regions
-PMC_SUMMARY = ROOT / "profiles" / "r04_pmc_traffic.json"
+PMC_SUMMARY = ROOT / "profiles" / "r05_pmc_traffic.json"
 SOURCES = sorted((ROOT / "api-ratelimit_amd" / "csrc").glob("*.h*")) + sorted(
     (ROOT / "api-ratelimit_amd" / "csrc").glob("*.cpp")) + [ROOT / "include" / "rl_hip.h"]
 
