@@ -480,3 +480,36 @@ def test_broken_router_destroy_drains_every_slot(monkeypatch):
         gs, gt = e.submit(b)
         es, et = new_oracle().submit(b)
         streams.assert_same(es, et, gs, gt, f"engine {k} after a broken router")
+
+
+@pytest.mark.parametrize("depth", [2, 3])
+def test_emulated_repack(depth):
+    """The repack on the collective transport (the hot scan refuses combining, the repack packs
+    the batch again before the counts exchange): after the hot set forms, steps where one
+    origin's hot descriptors carry two request times, a hot prefix arrives under a second rule, or
+    a hits_addend passes the combining range, while the other origin combines in the same step.
+    Bit-exact against the oracle, and the routers count the repacks."""
+    G, per = 2, 2000
+    steps = skew_batches(G, 12, per, seed=23)
+    tail = skew_batches(G, 6, per, seed=24, t0=1_700_000_012)
+    b = tail[0][0]  # (a) two request times in origin 0's batch
+    now = b.now.copy()
+    now[b.n_req // 2:] += 1
+    tail[0][0] = hiprl.Batch(b.blob, b.off, b.rule, b.req_of, now, b.hits)
+    b = tail[2][1]  # (b) a hot prefix under a second rule in origin 1's batch
+    rule = b.rule.copy()
+    hot_i = [i for i in range(b.n_desc) if b.prefix(i).startswith(b"cmb_hot_")]
+    rule[hot_i[len(hot_i) // 2]] = (int(rule[hot_i[len(hot_i) // 2]]) + 1) % len(RULES)
+    tail[2][1] = hiprl.Batch(b.blob, b.off, rule, b.req_of, b.now, b.hits)
+    b = tail[4][0]  # (c) a hits_addend past the combining range
+    hits = b.hits.copy()
+    hits[int(b.req_of[[i for i in range(b.n_desc) if b.prefix(i).startswith(b"cmb_hot_")][0]])] = 100_000
+    tail[4][0] = hiprl.Batch(b.blob, b.off, b.rule, b.req_of, b.now, hits)
+    all_steps = steps + tail
+    ranks = EmuRanks(G, per)
+    bufs, codes = drive(ranks, all_steps, "pipelined", depth=depth)
+    check_steps(new_oracle(), all_steps, bufs, codes, f"emulated repack depth {depth}")
+    st = [r.stats() for r in ranks.routers]
+    assert all(x["status"] == [0] * G and x["steps"] == len(all_steps) for x in st), st
+    assert st[0]["repacks"] >= 1 and st[0]["combined_steps"] >= 3, st[0]
+    ranks.close()
