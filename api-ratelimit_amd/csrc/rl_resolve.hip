@@ -40,9 +40,13 @@ constexpr int SW = 8;             // dwords of a string held in registers
 constexpr uint32_t SB = 4 * SW;   // bytes: names up to 32 bytes take the register path
 
 // ---- the byte path (long names, strings at the blob's edges, an unaligned blob) ----
-// A byte from the aligned dword that holds it (never past that byte's page). Plain byte loads
-// in these loops were merged by the compiler into 16-bit loads at odd addresses, which read
-// wrong bytes on the MI355X boxes (unaligned global access is not enabled there).
+// A byte from the aligned dword that holds it (never past that byte's page; no sub-dword
+// loads that the compiler could merge into misaligned wider ones). The byte path is written
+// out explicitly (no lookup template taking a compare lambda, no struct copies): its first
+// forms were bit-exact on the host and at -O1 but returned wrong lookups at -O3 on the device;
+// this form is checked there by tests/test_gpu_resolve.py and tools/diag_resolve.py (blobs
+// shifted by 1-3 bytes send every lookup down this path). Out of line it is also right, but
+// the kernel then needs a stack and took 118 us instead of 94 on config 4.
 RL_HD inline uint32_t ld_u8(const uint8_t* p) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
   return (*reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3) >> (8u * (uint32_t)(a & 3u))) & 0xFFu;

@@ -4,4 +4,4 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r05g; mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_resolve.py tests/test_gpu_configs45_regime.py tests/test_gpu_configs.py > $OUT/pytest.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -5 $OUT/pytest.log; [ $rc -ne 0 ] && exit $rc
-bash tools/ab.sh 20 "- tools/variants/lib_nopre.so tools/variants/lib_resolve0.so - tools/variants/lib_nopre.so" --config 4
+bash tools/ab.sh 20 "- tools/variants/lib_res1.so - tools/variants/lib_res1.so" --config 4
