@@ -158,3 +158,47 @@ def test_config5_sustained_stream_gpu(local_cache):
         near = int(st["near_limit_delta"].sum())
         assert near >= 0
     assert codes[1] > 0 and codes[2] > 0  # both OK and OVER_LIMIT decisions occur
+
+
+def test_resolve_long_names_and_shifted_blob_gpu():
+    """Names past the 32 bytes the register path holds (the byte path), key "_" value past 32
+    bytes, an empty value, names that share a prefix with a longer one; the batch's bytes also
+    at 1-3 bytes past a 16-B boundary (rl_resolve_device on device arrays). Against GetLimit."""
+    import torch
+    long_k, long_v = "k" * 30, "v" * 40
+    y = ("domain: dlong\n"
+         "descriptors:\n"
+         f"  - key: {long_k}\n    value: {long_v}\n    rate_limit: {{unit: second, requests_per_unit: 3}}\n"
+         f"  - key: {long_k}\n    rate_limit: {{unit: minute, requests_per_unit: 4}}\n"
+         "  - key: ab\n    value: c\n    rate_limit: {unit: hour, requests_per_unit: 5}\n"
+         "  - key: a\n    value: b_c\n    rate_limit: {unit: day, requests_per_unit: 6}\n"
+         "  - key: e\n    rate_limit: {unit: day, requests_per_unit: 7}\n")
+    cfg = rl_config.RateLimitConfig([("l.yaml", y)])
+    orc = config_oracle.Config([("l.yaml", y)])
+    descs = [("dlong", [(long_k, long_v)]), ("dlong", [(long_k, "x")]), ("dlong", [("ab", "c")]),
+             ("dlong", [("a", "b_c")]), ("dlong", [("a", "b")]), ("dlong", [("e", "")]), ("dlong", [("e", "z" * 33)]),
+             ("dlong", [(long_k[:-1], long_v)]), ("dlon", [("e", "1")])] * 40
+    eng = hiprl.Engine()
+    cfg.install(eng)
+    rb = rl_config.ResolveBatch([(d, e, None) for d, e in descs])
+    want = []
+    for d, e in descs:
+        w = orc.get_limit(d, e)
+        want.append(None if w is None else (w.requests_per_unit, w.unit))
+    have = lambda r: None if r == hiprl.NIL_RULE else (cfg.rules[int(r)].requests_per_unit, cfg.rules[int(r)].unit)
+    assert [have(r) for r in eng.resolve(rb)] == want
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(dev)
+    for shift in (1, 2, 3):
+        raw = torch.zeros(rb.bytes.size + 64, dtype=torch.uint8, device=dev)
+        raw[16 + shift:16 + shift + rb.bytes.size] = torch.from_numpy(rb.bytes.copy()).to(dev)
+        keep = [t(rb.domain), t(rb.entry_first), t(rb.entry)]
+        s = hiprl.RlResolveBatch()
+        s.n_desc, s.n_entries, s.bytes_len, s.reserved = rb.n_desc, rb.n_entries, rb.bytes_len, 0
+        s.bytes, s.domain, s.entry_first, s.entry = raw.data_ptr() + 16 + shift, keep[0].data_ptr(), keep[1].data_ptr(), keep[2].data_ptr()
+        s.override_rule = None
+        out = torch.zeros(rb.n_desc, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        eng.resolve_device(s, out.data_ptr())
+        torch.cuda.synchronize()
+        assert [have(r) for r in out.cpu().numpy().view(np.uint32)] == want, shift
