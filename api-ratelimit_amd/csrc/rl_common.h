@@ -331,10 +331,7 @@ struct __attribute__((aligned(16))) HotCand {
 // v4 pipeline (rl_kernels_v4.hip)
 // ---------------------------------------------------------------------------
 constexpr int V4_TILE = 2048;             // k4_hist / k4_place arrival tile
-#ifndef RL_V4_THREADS
-#define RL_V4_THREADS 512
-#endif
-constexpr int V4_THREADS = RL_V4_THREADS;  // k4_hist / k4_place threads per tile
+constexpr int V4_THREADS = 512;  // k4_hist / k4_place threads per tile (1024 measured slower: DESIGN.md §6)
 constexpr int V4_ROW16 = (NBUCKETS + 7) / 8 * 8;  // tile row of u16 bucket starts
 constexpr int V4_RULE_BITS = 15;          // MRec.rn = rule | now_mod << 15 (now_mod < 86400 < 2^17)
 constexpr uint32_t V4_MAX_RULES = 1u << V4_RULE_BITS;

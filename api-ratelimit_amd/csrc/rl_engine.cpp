@@ -988,12 +988,7 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
     evs.push_back(&e->ev_kern[k]);
   }
   for (hipEvent_t* ev : evs) {
-#ifdef RL_EVFRONT_DEV  // A/B variant: the cross-stream k4_hist events release to device scope only
-    const bool dev_ev = ev == &e->ev_front[0] || ev == &e->ev_front[1];
-    chk(hipEventCreateWithFlags(ev, hipEventDisableTiming | (dev_ev ? hipEventReleaseToDevice : 0)));
-#else
     chk(hipEventCreateWithFlags(ev, hipEventDisableTiming));
-#endif
     if (he == hipSuccess) chk(hipEventRecord(*ev, e->stream));
   }
   for (int k = 0; k < HSLOTS; ++k) {

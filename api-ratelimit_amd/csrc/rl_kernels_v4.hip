@@ -156,10 +156,7 @@ constexpr int SHARD_CTR0 = 0;  // EngineCtl::tile_ctr[0..7][0]: k4_group blocks 
 // k4_hist
 // ---------------------------------------------------------------------------
 template <bool ROUTED>
-#ifndef RL_HIST_BLOCKS
-#define RL_HIST_BLOCKS 1
-#endif
-__global__ __launch_bounds__(NT, RL_HIST_BLOCKS) void k4_hist(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
+__global__ __launch_bounds__(NT) void k4_hist(DevBatch in, const DevRule* __restrict__ rules, uint32_t n_rules,
                                               uint64_t seed, const HotEntry* __restrict__ hot,
                                               uint32_t* __restrict__ req_thr, uint32_t* __restrict__ fpart,
                                               uint16_t* __restrict__ tstart, unsigned long long* __restrict__ thsum,
