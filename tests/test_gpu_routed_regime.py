@@ -96,3 +96,53 @@ def test_routed_config3_g8_full_regime_against_oracle(local_cache):
     occ = [e.occupancy() for e in ranks.engines]
     assert sum(sum(x["live"]) for x in occ) > 0
     ranks.close()
+
+
+def test_routed_config5_g4_rollover_against_oracle():
+    """BASELINE config 5 routed: G = 4 emulated ranks, Zipf(1.1) keys over 10⁸ with SECOND /
+    MINUTE / HOUR rules by rank % 3 and hits_addend ~ U{1..8}, 10⁵ descriptors per origin, one
+    step per simulated second for 24 s across a minute boundary (window rollover and expiry on
+    the owners), origins 0-2 s apart, combining on. Every status and ThrottleMillis against one
+    serial oracle over the rank-order concatenation."""
+    G, steps, per = 4, 24, 100_000
+    rng = np.random.default_rng(5)
+    t0 = 1_700_000_000 - 37
+    rows = []
+    for s in range(steps):
+        row = []
+        for g in range(G):
+            b = workload.config5_batch(s, d=per, N=100_000_000, batches_per_s=1, seed=5 + 7919 * g, t0=t0)
+            t = t0 + s + int(rng.integers(0, 3))
+            row.append(hiprl.Batch(b.blob, b.off, b.rule, b.req_of, np.full(b.n_req, t, np.int64), b.hits))
+        rows.append(row)
+    wid = hiprl.Router.emu_world(G)
+    engines = []
+    for _ in range(G):
+        e = hiprl.Engine(log2_slots=(22, 22, 22, 12), max_batch_desc=per * G, max_batch_req=per * G,
+                         max_blob_bytes=per * G * 24 + 64)
+        e.load_rules(workload.CONFIG5_RULES)
+        engines.append(e)
+    routers = [None] * G
+
+    def mk(r):
+        routers[r] = hiprl.Router([engines[r]], max_desc=per, n_shards=G, rank=r, rccl_id=wid, emulated=True)
+    parallel(G, mk)
+
+    class R:
+        pass
+    ranks = R()
+    ranks.G, ranks.routers = G, routers
+    bufs, codes = drive(ranks, rows, "pipelined", depth=3)
+    assert all(c is None for cr in codes for c in cr), codes
+    st = [r.stats() for r in routers]
+    assert all(x["status"] == [0] * G and x["steps"] == steps for x in st), st
+    o = oracle.Oracle(near_limit_ratio=0.8)
+    o.load_rules(workload.CONFIG5_RULES)
+    for s, (row, bf) in enumerate(zip(rows, bufs)):
+        est, ethr = o.submit(routing.concat_batches(row), threads=16)
+        d0 = r0 = 0
+        for g, (b, (gst, gthr)) in enumerate(zip(row, bf.results())):
+            streams.assert_same(est[d0:d0 + b.n_desc], ethr[r0:r0 + b.n_req], gst, gthr, f"step={s} origin={g}")
+            d0 += b.n_desc
+            r0 += b.n_req
+    parallel(G, lambda r: routers[r].close())
