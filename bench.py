@@ -811,6 +811,13 @@ def main():
                 "device_kernels_ms_per_batch": round(step_ms, 4),
                 "host_decide": {"ns_per_desc_1_thread": round(t_dec1 / cb0.n_desc * 1e9, 2), "threads": nthr,
                                 "value": round(cb0.n_desc / t_decn, 1), "unit": "descriptor statuses/s"},
+                # the compact form's statuses are made on the host (rl_decide_raw): a caller gets
+                # decisions at the slower of the two rates (the copy-in/out pipeline and the decide,
+                # running on separate host threads), which the full format avoids
+                "end_to_end": {"value": round(min(d / t_c, cb0.n_desc / t_decn), 1),
+                               "bound_by": "host decide (rl_decide_raw)" if cb0.n_desc / t_decn < d / t_c
+                               else "PCIe copies + kernels",
+                               "unit": "descriptor decisions/s"},
                 "full_format": {"value": round(d / t_f, 1), "ms_per_batch": round(t_f * 1e3, 4),
                                 "bytes_per_desc": {"h2d": round(h2d_f / d, 2), "d2h": round(d2h_f / d, 2)},
                                 "link_ms_per_batch": {"h2d": round(lf[0] * 1e3, 4), "d2h": round(lf[1] * 1e3, 4),
