@@ -112,6 +112,8 @@ def parse():
                     help="routed steps through router.ShardRouter (torch.distributed over RCCL) instead of the "
                          "C-ABI router rl_router_step (the Go host's path, the default)")
     ap.add_argument("--dump-stamps", type=str, default="", help=argparse.SUPPRESS)  # -DRL_STAMPS variant: raw stamps
+    ap.add_argument("--dump-host-times", type=str, default="", help=argparse.SUPPRESS)  # per-call submit / wait seconds
+    ap.add_argument("--host-delay-us", type=float, default=0.0, help=argparse.SUPPRESS)  # diagnostic: spin before submit
     ap.add_argument("--master-port", type=int, default=0,
                     help="--gpus N > 1 without a launcher: rendezvous port of the ranks bench.py starts (0: pick one)")
     ap.add_argument("--dry-launch", action="store_true",
@@ -535,11 +537,14 @@ def main():
     outs = [torch.empty(d * 20, dtype=torch.uint8, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
     thrs = [torch.empty(d, dtype=torch.int32, device=dev) for _ in range(hiprl.MAX_IN_FLIGHT)]
 
+    host_t = {"submit": [], "wait": [], "step": []}  # host seconds per engine call / per loop step (pipelined)
+
     def run(dbs, first=0, depth=None):
         """One step per batch. Pipelined: batch k+1 is submitted before batch k is waited for (the
         micro-batcher's double buffering; routed: rl_router_submit / rl_router_wait, two steps in
         flight); every batch is complete on return."""
         pend = 0
+        hprev = 0.0
         rdepth = RDEPTH if depth is None else depth
         for j, db in enumerate(dbs):
             if rtr is not None:
@@ -557,10 +562,21 @@ def main():
                     pend -= 1
                 continue
             if pipelined:
+                if args.host_delay_us:  # (diagnostic: how the next batch's k4_hist start moves the step)
+                    tq = time.perf_counter() + args.host_delay_us * 1e-6
+                    while time.perf_counter() < tq:
+                        pass
+                h0 = time.perf_counter()
+                if j:
+                    host_t["step"].append(h0 - hprev)
+                hprev = h0
                 eng.submit_pipelined_batch(sb, o, t)
+                h1 = time.perf_counter()
+                host_t["submit"].append(h1 - h0)
                 pend += 1
                 if pend == DEPTH:
                     eng.wait()
+                    host_t["wait"].append(time.perf_counter() - h1)
                     pend -= 1
             else:
                 eng.submit_device_async(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), o, t)
@@ -615,12 +631,20 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     fb0 = eng.stats()["lsd_fallbacks"]
+    for v in host_t.values():
+        v.clear()
     t0 = time.perf_counter()
     run(dbs[args.warmup:args.warmup + args.steps], args.warmup)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # (outside the timed region)
+    host_us = {k: {"mean": round(sum(v) / max(1, len(v)) * 1e6, 1),
+                   "p50": round(float(np.median(v)) * 1e6, 1) if v else None,
+                   "max": round(max(v) * 1e6, 1) if v else None} for k, v in host_t.items()}
+    if args.dump_host_times:
+        Path(args.dump_host_times).write_text(json.dumps({k: [round(x * 1e6, 2) for x in v] for k, v in host_t.items()}))
     fb_timed = eng.stats()["lsd_fallbacks"] - fb0
     rstats = nrt.stats() if nrt is not None else None
     if dist:
@@ -928,12 +952,18 @@ def main():
                   "bytes": int(sum(occ["slots"])) * 32},
         "engine": {"resorts": stats["resorts"], "lsd_fallbacks_prefill": fallbacks_prefill,
                    "lsd_fallbacks_timed": fb_timed, "hot_keys": stats["hot_keys"], "batches": stats["batches"],
-                   "prefill_s": round(t_fill, 1), "source_sha": source_sha()},
+                   "prefill_s": round(t_fill, 1), "source_sha": source_sha(),
+                   # host time per step inside rl_submit_pipelined / rl_wait (pipelined single-GPU path only):
+                   # submit is launch overhead the device may idle behind; wait is time the host blocks
+                   "host_us_per_step": host_us if pipelined else None},
     }
     s = json.dumps(line)
     print(s, flush=True)
     if args.json_out:
         Path(args.json_out).write_text(s + "\n")
+    if nrt is not None:
+        nrt.close()
+    eng.close()
     if dist:
         dist.destroy_process_group()
 
