@@ -1,6 +1,8 @@
 #!/bin/bash
 # When the next batch's k4_hist may start: now (host-timed, gate 0), after the batch in
 # flight's k4_scan (1) or k4_place (2), at two and three batches in flight; interleaved.
+# (RL_DIAG_HIST_GATE was an A/B switch in the engine, removed after this measurement:
+# profiles/r05_ab_hist_start.txt; rerunning needs it back.)
 set -e
 mkdir -p gpurun_out/gate
 for rep in 1 2; do
