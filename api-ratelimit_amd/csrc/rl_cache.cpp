@@ -1,6 +1,8 @@
 // rl_cache.cpp — HipRateLimitCache: the reference's RateLimitCache contract on the HIP engine.
 #include "rl_cache.hpp"
 
+#include "rl_common.h"  // decide_status (a local-cache hit's status, as the device makes it)
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -47,6 +49,10 @@ struct PendingCall {
   int64_t now = 0;
   uint32_t hits = 1;
   std::vector<std::string> prefix;  // per descriptor ("" = nil limit)
+  // HIP_LOCAL_CACHE=freecache: per descriptor, a hit of the lookup made at enqueue (no INCRBY)
+  // and the full cache key (GenerateCacheKey, cache_key.go:57-68) it was looked up / is Set by
+  std::vector<uint8_t> lhit;
+  std::vector<std::string> fkey;
   size_t blob_bytes = 0;
   DoLimitResponse resp;
   std::promise<void> done;
@@ -89,12 +95,27 @@ std::shared_ptr<PendingCall> make_call(const RateLimitRequest& request,
 
 // A call's DescriptorStatuses and stat adds from its statuses (GetResponseDescriptorStatus's
 // outputs, base_limiter.go:70-115,129-177), then the caller is released.
+uint32_t unit_divider(Unit u) {  // utils.UnitToDivider
+  return u == Unit::SECOND ? 1u : u == Unit::MINUTE ? 60u : u == Unit::HOUR ? 3600u : u == Unit::DAY ? 86400u : 0u;
+}
+
 void answer(PendingCall& c, const rl_status* out, uint32_t thr) {
   c.resp.DescriptorStatuses.resize(c.prefix.size());
   c.resp.ThrottleMillis = thr;
   for (size_t i = 0; i < c.prefix.size(); ++i) {
     const auto& lim = (*c.limits)[i];
-    const rl_status& s = out[i];
+    rl_status hit_st;
+    if (!c.lhit.empty() && c.lhit[i]) {
+      // IsOverLimitWithLocalCache: OVER_LIMIT, nothing remaining, OverLimit and
+      // OverLimitWithLocalCache += hits (base_limiter.go:76-81); no ThrottleMillis
+      rlhip::DevRule R{};
+      R.L = lim->Limit.RequestsPerUnit;
+      R.div = unit_divider(lim->Limit.unit);
+      R.unit = (uint32_t)lim->Limit.unit;
+      R.shadow = lim->ShadowMode ? 1u : 0u;
+      rlhip::decide_status(0, true, c.hits, (uint32_t)(c.now % R.div), R, hit_st);
+    }
+    const rl_status& s = (!c.lhit.empty() && c.lhit[i]) ? hit_st : out[i];
     DescriptorStatus& o = c.resp.DescriptorStatuses[i];
     o.code = (Code)(s.code_flags & 0xFF);
     o.LimitRemaining = s.limit_remaining;
@@ -147,7 +168,9 @@ HipRateLimitCache::HipRateLimitCache(const HipSettings& s, std::shared_ptr<TimeS
   c.device = s.device;
   for (int u = 0; u < 4; ++u) c.log2_slots[u] = s.log2_slots[u];
   c.near_limit_ratio = s.near_limit_ratio;
-  c.local_cache = s.local_cache ? 1 : 0;
+  // HIP_LOCAL_CACHE=freecache: the host's bounded model is the local cache, the device keeps none
+  if (s.local_cache && s.local_cache_freecache) fc_ = std::make_unique<FreeCacheModel>(s.local_cache_bytes);
+  c.local_cache = s.local_cache && !fc_ ? 1 : 0;
   c.per_second_split = s.per_second_split ? 1 : 0;
   c.max_batch_desc = s.batch_limit + 4096;
   c.max_batch_req = s.batch_limit + 4096;
@@ -177,6 +200,20 @@ void HipRateLimitCache::Flush() {
 DoLimitResponse HipRateLimitCache::DoLimit(const RateLimitRequest& request,
                                            const std::vector<std::shared_ptr<RateLimit>>& limits) {
   auto call = make_call(request, limits, *ts_);
+  if (fc_) {
+    // every lookup of the request before any of its INCRBYs (fixed_cache_impl.go:55-66)
+    PendingCall& c = *call;
+    c.lhit.assign(c.prefix.size(), 0);
+    c.fkey.resize(c.prefix.size());
+    std::lock_guard<std::mutex> g(fc_mu_);
+    for (size_t i = 0; i < c.prefix.size(); ++i) {
+      if (!limits[i]) continue;  // "" keys are skipped
+      const int64_t div = unit_divider(limits[i]->Limit.unit);
+      if (!div) continue;
+      c.fkey[i] = c.prefix[i] + std::to_string(c.now / div * div);
+      c.lhit[i] = fc_->Get(c.fkey[i], (uint32_t)c.now) ? 1 : 0;
+    }
+  }
   std::future<void> f = call->done.get_future();
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -264,10 +301,12 @@ void HipRateLimitCache::add(Staged& st, const std::shared_ptr<PendingCall>& cp) 
       const auto& lim = (*c.limits)[i];
       memcpy(st.hc.prefix_blob + st.nb, c.prefix[i].data(), c.prefix[i].size());
       st.nb += (uint32_t)c.prefix[i].size();
-      const uint32_t rid = lim ? rule_id(lim->Limit, lim->ShadowMode) : RL_NIL_RULE16;
+      // a local-cache hit goes as a nil descriptor: no INCRBY, and no jitter draw (:61-65)
+      const bool inc = lim && (c.lhit.empty() || !c.lhit[i]);
+      const uint32_t rid = inc ? rule_id(lim->Limit, lim->ShadowMode) : RL_NIL_RULE16;
       st.hc.desc_word[st.nd] = (uint32_t)c.prefix[i].size() | rid << 16;
       st.hc.req_of[st.nd] = r;  // (sent only when some request holds several descriptors)
-      if (jitter_) st.hc.ttl_jitter[st.nd] = lim ? draw_jitter(s_) : 0;
+      if (jitter_) st.hc.ttl_jitter[st.nd] = inc ? draw_jitter(s_) : 0;
       ++st.nd;
     }
     st.calls.push_back(cp);
@@ -280,9 +319,10 @@ void HipRateLimitCache::add(Staged& st, const std::shared_ptr<PendingCall>& cp) 
     const auto& lim = (*c.limits)[i];
     memcpy(st.hb.prefix_blob + st.nb, c.prefix[i].data(), c.prefix[i].size());
     st.nb += (uint32_t)c.prefix[i].size();
-    st.hb.rule_id[st.nd] = lim ? rule_id(lim->Limit, lim->ShadowMode) : RL_NIL_RULE;
+    const bool inc = lim && (c.lhit.empty() || !c.lhit[i]);
+    st.hb.rule_id[st.nd] = inc ? rule_id(lim->Limit, lim->ShadowMode) : RL_NIL_RULE;
     st.hb.req_of[st.nd] = r;
-    if (jitter_) st.hb.ttl_jitter[st.nd] = lim ? draw_jitter(s_) : 0;
+    if (jitter_) st.hb.ttl_jitter[st.nd] = inc ? draw_jitter(s_) : 0;
     ++st.nd;
     st.hb.prefix_off[st.nd] = st.nb;
   }
@@ -407,10 +447,28 @@ void HipRateLimitCache::finish(Staged& st) {
   size_t d = 0;
   for (size_t r = 0; r < st.calls.size(); ++r) {
     PendingCall& c = *st.calls[r];
+    if (fc_) {
+      // a reply past the limit Sets the key with TTL = the unit's divider (base_limiter.go:94-106),
+      // shadow rules included (the limiter does not know them), before the caller is released
+      std::lock_guard<std::mutex> g(fc_mu_);
+      for (size_t i = 0; i < c.prefix.size(); ++i) {
+        const auto& lim = (*c.limits)[i];
+        if (!lim || c.lhit[i]) continue;
+        const uint32_t cf = out[d + i].code_flags;
+        if ((cf & 0xFFu) == RL_CODE_OVER_LIMIT || ((cf >> 8) & RL_FLAG_SHADOW))
+          fc_->Set(c.fkey[i], unit_divider(lim->Limit.unit), (uint32_t)c.now);
+      }
+    }
     answer(c, out + d, thr[r]);
     d += c.prefix.size();
   }
   done_calls(st.calls.size());
+}
+
+void HipRateLimitCache::local_cache_stats(uint64_t* out) {
+  for (int k = 0; k < 6; ++k) out[k] = 0;
+  std::lock_guard<std::mutex> g(fc_mu_);
+  if (fc_) fc_->stats(out);
 }
 
 // The submitter thread owns the engine (rl_hip.h: one thread per engine) and keeps two batches
@@ -525,6 +583,8 @@ HipRoutedRateLimitCache::HipRoutedRateLimitCache(const HipSettings& s, const Hip
     : s_(s), r_(r), ts_(std::move(ts)) {
   jitter_ = setup_jitter(s_);
   if (r.id.size() != RL_ROUTER_ID_BYTES) throw RedisError("routed cache: id must hold RL_ROUTER_ID_BYTES bytes");
+  if (s.local_cache && s.local_cache_freecache)
+    throw RedisError("routed cache: HIP_LOCAL_CACHE=freecache is single-engine only (the device cache is the routed one)");
   rl_config c;
   memset(&c, 0, sizeof c);
   c.struct_size = sizeof c;

@@ -29,6 +29,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "rl_freecache.hpp"
 #include "rl_hip.h"
 
 namespace ratelimit {
@@ -153,6 +154,12 @@ struct HipSettings {
   uint32_t log2_slots[4] = {20, 20, 20, 18};  // HIP_TABLE_SLOTS per unit
   float near_limit_ratio = 0.8f;          // NEAR_LIMIT_RATIO
   bool local_cache = false;               // LOCAL_CACHE_SIZE_IN_BYTES > 0
+  // HIP_LOCAL_CACHE=freecache (single-engine batcher): the local cache is a host-side model of
+  // freecache holding LOCAL_CACHE_SIZE_IN_BYTES bytes (rl_freecache.hpp: it evicts, as the
+  // reference's does under a small size; parity-unpinned), looked up when a call is enqueued and
+  // Set when its batch is decided, instead of the device's cache (which never evicts)
+  bool local_cache_freecache = false;
+  int64_t local_cache_bytes = 0;
   bool per_second_split = false;          // REDIS_PERSECOND
   uint32_t batch_window_us = 75;          // HIP_BATCH_WINDOW
   uint32_t batch_limit = 1u << 16;        // HIP_BATCH_LIMIT (descriptors)
@@ -193,6 +200,8 @@ class HipRateLimitCache : public RateLimitCache {
   }
   // (tests) set before the first DoLimit
   void set_trace(TraceFn f) { trace_ = std::move(f); }
+  // HIP_LOCAL_CACHE=freecache: hits, misses, lookups, entries, evicted, expired (zeros otherwise)
+  void local_cache_stats(uint64_t* out);
 
  private:
   struct Staged;
@@ -227,6 +236,8 @@ class HipRateLimitCache : public RateLimitCache {
   TraceFn trace_;
   bool jitter_ = false;
   uint64_t staged_seq_ = 0;  // batches gathered (= submitted, in order)
+  std::unique_ptr<FreeCacheModel> fc_;  // HIP_LOCAL_CACHE=freecache
+  std::mutex fc_mu_;                    // (freecache's segment locks)
 };
 
 // ---- Multi-GPU deployment ------------------------------------------------

@@ -90,6 +90,33 @@ void* rlc_create(int local_cache, float near_ratio, int flags, uint32_t window_u
   return s;
 }
 
+// HIP_LOCAL_CACHE=freecache: the single-engine batcher with the host's bounded local cache of
+// `bytes` (LOCAL_CACHE_SIZE_IN_BYTES; freecache's 512-KiB floor applies).
+void* rlc_create_fc(int64_t bytes, float near_ratio, int flags, uint32_t window_us) {
+  auto* s = new Shim();
+  HipSettings hs;
+  set_jitter(hs);
+  hs.local_cache = true;
+  hs.local_cache_freecache = true;
+  hs.local_cache_bytes = bytes;
+  hs.near_limit_ratio = near_ratio;
+  hs.per_second_split = (flags & 1) != 0;
+  hs.answer_early = (flags & 2) == 0;
+  hs.batch_window_us = window_us;
+  hs.batch_limit = 1u << 14;
+  try {
+    auto c = std::make_unique<HipRateLimitCache>(hs, s->ts);
+    s->single = c.get();
+    s->cache = std::move(c);
+  } catch (const std::exception& e) {
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+// hits, misses, lookups, entries, evicted, expired of the batcher's freecache model
+void rlc_local_cache_stats(void* p, uint64_t* out) { static_cast<Shim*>(p)->single->local_cache_stats(out); }
+
 // One rank of the multi-GPU batcher (HipRoutedRateLimitCache). id: RL_ROUTER_ID_BYTES from
 // rl_router_unique_id or rl_router_emu_world (emulated != 0). Collective: every rank's create runs
 // at the same time (one thread per rank). Destroy (rlc_destroy) is collective too.
