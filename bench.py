@@ -298,9 +298,10 @@ def random_access_roofline(eng, alg_bytes, U, pipe_ms, step_ms):
                           "frac = t_roof / t"}
 
 
-def pmc_traffic(dom: str):
+def pmc_traffic(dom: str, config: int):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc summary,
-    only if it was measured on these exact kernel sources."""
+    only if it was measured on these exact kernel sources and this workload (tools/pmc_round.sh
+    profiles the default bench: config 3)."""
     if not PMC_SUMMARY.exists():
         return None, "no PMC summary committed", None
     try:
@@ -309,6 +310,8 @@ def pmc_traffic(dom: str):
         return None, f"unreadable PMC summary: {ex}", None
     if pm.get("source_sha") != source_sha():
         return None, f"PMC summary {PMC_SUMMARY.name} is for other kernel sources ({pm.get('source_sha')})", None
+    if config != pm.get("config", 3):
+        return None, f"PMC summary {PMC_SUMMARY.name} is of config {pm.get('config', 3)}", None
     k = pm.get("kernels", {}).get(dom)
     return ((k or {}).get("hbm_bytes_per_launch"), f"{PMC_SUMMARY.name} (source {pm['source_sha']})",
             pm.get("hbm_bytes_per_batch"))
@@ -890,7 +893,7 @@ def main():
         # its descriptors, so each launch is held to the whole batch's bytes.
         achieved = alg_bytes / (dom_us * 1e-6) / 1e9
         # (the PMC summary profiles the unrouted step: no counter figure for an owner batch)
-        traffic, tsrc, traffic_batch = pmc_traffic(dom) if not routed else (None, None, None)
+        traffic, tsrc, traffic_batch = pmc_traffic(dom, args.config) if not routed else (None, None, None)
         roofline = {
             "bound": "hbm", "kernel": dom,
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
