@@ -1,6 +1,8 @@
 #!/bin/bash
 # Batch structs prebuilt before the timed region (default) against built in the loop
 # (--no-prebuilt), interleaved; the driver's step count (20) and 100.
+# (--no-prebuilt was an A/B switch of bench.py, removed after this measurement:
+# profiles/r05_ab_hist_start.txt.)
 set -e
 mkdir -p gpurun_out/pre
 for steps in 20 100; do
