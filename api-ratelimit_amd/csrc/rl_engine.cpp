@@ -245,8 +245,25 @@ struct rl_engine {
     uint32_t errs = 0;
     rl_status* user_out = nullptr; // host batch: rl_wait copies here (may be null)
     uint32_t* user_thr = nullptr;
+    bool poll = false;             // completion = k4_group's done word behind h_ctl (no event)
   };
   Flight fl[HSLOTS];
+  // A device v4 batch completes on the word k4_group's last block writes behind the slot's pinned
+  // control block after everything else (rl_kernels_v4.hip), not on a completion event: the
+  // event's marker packet cost ≈5 µs between k4_group of batch k and k4_scan of k+1, and the
+  // host sees the word as soon as it lands (profiles/r05_ab_poll_done.txt).
+  volatile uint32_t* done_word(uint32_t slot) {
+    return reinterpret_cast<volatile uint32_t*>(h_ctl_s[slot] + 1);
+  }
+  hipError_t poll_done(const Flight& f) {
+    volatile uint32_t* w = done_word(f.slot);
+    for (uint64_t k = 0; k < (1ull << 28); ++k)  // (a bound: then wait for the stream)
+      if (*w) {
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        return hipSuccess;
+      }
+    return hipStreamSynchronize(stream);
+  }
   int n_fl = 0;
 
   // timing
@@ -371,6 +388,11 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
     hipStream_t fs = split ? front : stream;
     if (split) {
       // slot buffers and control block free: batch seq-2 done
+      if (n_fl >= 2 && fl[n_fl - 2].poll && !fl[n_fl - 2].settled) {
+        // three in flight: batch seq-2 has no event to wait for on the device; the host waits
+        hipError_t pe = poll_done(fl[n_fl - 2]);
+        if (pe != hipSuccess) return hip_fail(pe, "poll");
+      }
       hipStreamWaitEvent(front, done_ev[(sub_seq + HSLOTS - 2) % HSLOTS], 0);
       if (in_ev) {
         hipStreamWaitEvent(front, in_ev, 0);
@@ -623,7 +645,7 @@ int rl_engine::enqueue_d2h(const Flight& f, hipStream_t s) {
 int rl_engine::settle(Flight& f) {
   h_ctl = h_ctl_s[f.slot];
   h_cand = h_cand_s[f.slot];
-  hipError_t e = timing ? hipStreamSynchronize(stream) : wait_event_polling(done_ev[f.slot]);
+  hipError_t e = timing ? hipStreamSynchronize(stream) : f.poll ? poll_done(f) : wait_event_polling(done_ev[f.slot]);
   if (e == hipSuccess && timing && f.host) e = hipStreamSynchronize(xout);
   if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
   uint32_t errs = h_ctl->err;
@@ -768,6 +790,7 @@ int rl_engine::submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, R
   const uint32_t s = (uint32_t)(sub_seq % HSLOTS);
   h_ctl = h_ctl_s[s];
   h_cand = h_cand_s[s];
+  *done_word(s) = 0;  // (the slot's previous batch is complete)
   const bool want = want_cand;
   int rc = run_pipeline(d, out, thr, default_mode(), in_ev, inputs_ready);
   if (rc) return rc;
@@ -796,8 +819,13 @@ int rl_engine::submit_common(const rl_batch& d, rl_status* out, uint32_t* thr, R
     // outputs stay in device memory; the host summary was written with a system-scope
     // release by k4_group (or copied by the LSD path's own D2H copy, ordered before this)
     const bool dev_only = default_mode() == MODE_V4 && !reply && d.n_desc;
-    done_ev[s] = dev_only ? ev_dd[s] : ev_done[s];
-    e = hipEventRecord(done_ev[s], stream);
+    if (dev_only && !timing) {
+      f.poll = true;  // k4_group writes the done word (cleared at this submit's start)
+      e = hipSuccess;
+    } else {
+      done_ev[s] = dev_only ? ev_dd[s] : ev_done[s];
+      e = hipEventRecord(done_ev[s], stream);
+    }
   }
   if (e != hipSuccess) return hip_fail(e, "hipEventRecord(done)");
   fl[n_fl++] = f;
@@ -953,7 +981,7 @@ int rl_create(const rl_config* cfg_in, rl_engine** out) {
   chk(hipMalloc(&e->d_cand, sizeof(HotCand) * CAND_MAX));
   for (int k = 0; k < HSLOTS; ++k) {
     chk(hipHostMalloc(&e->h_cand_s[k], sizeof(HotCand) * CAND_MAX, hipHostMallocDefault));
-    chk(hipHostMalloc(&e->h_ctl_s[k], sizeof(EngineCtl), hipHostMallocDefault));
+    chk(hipHostMalloc(&e->h_ctl_s[k], sizeof(EngineCtl) + 64, hipHostMallocDefault));  // + k4_group's done word
   }
   e->h_cand = e->h_cand_s[0];
   e->h_ctl = e->h_ctl_s[0];
@@ -1201,6 +1229,7 @@ int rl_query(rl_engine* e) {
   if (!e->n_fl) return e->fail(RL_ESTATE, "rl_query without a batch in flight");
   const rl_engine::Flight& f = e->fl[0];
   if (f.settled) return 1;
+  if (f.poll) return *e->done_word(f.slot) ? 1 : 0;
   const hipError_t q = hipEventQuery(e->done_ev[f.slot]);
   if (q == hipSuccess) return 1;
   if (q == hipErrorNotReady) return 0;

@@ -1773,6 +1773,16 @@ __global__ __launch_bounds__(G_NT, RL_G_OCC) void k4_group(DevBatch in,
   STL(2);
   for (uint32_t w = tid; w < words; w += G_NT) z[w] = 0;
   STL(3);
+  if (hctl) {
+    // The batch is complete: the host's done word behind its pinned control block, which
+    // rl_wait polls in place of a completion event. Last, after the frozen keys and the clear
+    // of batch k+2's control block, which batch k+2's k4_hist (launched once the host sees this
+    // word) uses.
+    __threadfence();
+    __syncthreads();
+    if (tid == 0)
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(hctl + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 }  // namespace v4
