@@ -392,8 +392,11 @@ int rl_engine::run_pipeline(const rl_batch& b, rl_status* out, uint32_t* thr, in
         // three in flight: batch seq-2 has no event to wait for on the device; the host waits
         hipError_t pe = poll_done(fl[n_fl - 2]);
         if (pe != hipSuccess) return hip_fail(pe, "poll");
+      } else if (n_fl >= 2) {
+        hipStreamWaitEvent(front, done_ev[(sub_seq + HSLOTS - 2) % HSLOTS], 0);
       }
-      hipStreamWaitEvent(front, done_ev[(sub_seq + HSLOTS - 2) % HSLOTS], 0);
+      // (with one batch in flight, batch seq-2 has completed through rl_wait: nothing to wait
+      // for, and no API call between rl_wait and this k4_hist launch)
       if (in_ev) {
         hipStreamWaitEvent(front, in_ev, 0);
       } else if (!inputs_ready) {  // inputs come from work queued on the stream
