@@ -220,6 +220,8 @@ struct rl_engine {
   bool has_tree = false;
   uint8_t* d_res = nullptr;  // rl_resolve staging (grown on demand)
   size_t res_cap = 0;
+  uint32_t* d_res_flags = nullptr;  // k_resolve's per-block flags (grown on demand)
+  uint32_t res_flag_cap = 0;
 
   // multi-GPU router scratch (allocated on first use)
   RRec* r_tmp = nullptr;           // origin: routed records in descriptor order
@@ -255,14 +257,23 @@ struct rl_engine {
   volatile uint32_t* done_word(uint32_t slot) {
     return reinterpret_cast<volatile uint32_t*>(h_ctl_s[slot] + 1);
   }
+  // Now and then (every 2^14 reads, ~1 ms) the stream is asked too: a fault in a kernel before
+  // the word shows there (the word would stay 0), and a stream that drained without the word
+  // (which k4_group writes last) ends the spin as the old bound's stream synchronize did.
   hipError_t poll_done(const Flight& f) {
     volatile uint32_t* w = done_word(f.slot);
-    for (uint64_t k = 0; k < (1ull << 28); ++k)  // (a bound: then wait for the stream)
+    for (uint64_t k = 0;; ++k) {
       if (*w) {
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
         return hipSuccess;
       }
-    return hipStreamSynchronize(stream);
+      if ((k & 0x3FFFu) == 0x3FFFu) {
+        const hipError_t q = hipStreamQuery(stream);
+        if (q == hipErrorNotReady) continue;
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        return q;
+      }
+    }
   }
   int n_fl = 0;
 
@@ -1077,7 +1088,7 @@ void rl_destroy(rl_engine* e) {
   for (int k = 0; k < 3; ++k) hipFree(e->v4_ctl[k]);
   for (void* p : {(void*)e->v4_hoff, (void*)e->v4_dfr, (void*)e->v4_hb,
                   (void*)e->v4_heads, (void*)e->v4_ins, e->v4_scratch, (void*)e->d_poison, (void*)e->d_tree_nodes,
-                  (void*)e->d_tree_slots, (void*)e->d_tree_names, (void*)e->d_res, (void*)e->table, (void*)e->d_occ,
+                  (void*)e->d_tree_slots, (void*)e->d_tree_names, (void*)e->d_res, (void*)e->d_res_flags, (void*)e->table, (void*)e->d_occ,
                   (void*)e->d_rules, (void*)e->keys_orig, (void*)e->keys_a, (void*)e->keys_b, (void*)e->vals_a,
                   (void*)e->vals_b, (void*)e->recs, (void*)e->srec, (void*)e->seg, (void*)e->offs,
                   (void*)e->hist_part, (void*)e->fp_part, (void*)e->fp_part2, (void*)e->tile_heads,
@@ -1232,7 +1243,14 @@ int rl_query(rl_engine* e) {
   if (!e->n_fl) return e->fail(RL_ESTATE, "rl_query without a batch in flight");
   const rl_engine::Flight& f = e->fl[0];
   if (f.settled) return 1;
-  if (f.poll) return *e->done_word(f.slot) ? 1 : 0;
+  if (f.poll) {
+    if (*e->done_word(f.slot)) return 1;
+    // not done: a fault on the stream shows in its query (the word would never be written)
+    const hipError_t q = hipStreamQuery(e->stream);
+    if (q == hipSuccess) return 1;  // (the stream drained: the batch is complete)
+    if (q == hipErrorNotReady) return 0;
+    return e->hip_fail(q, "hipStreamQuery");
+  }
   const hipError_t q = hipEventQuery(e->done_ev[f.slot]);
   if (q == hipSuccess) return 1;
   if (q == hipErrorNotReady) return 0;
@@ -1754,7 +1772,22 @@ int rl_resolve_device(rl_engine* e, const rl_resolve_batch* b, uint32_t* d_rule_
   // the engine stream — so resolving the next batch never waits for the batch in flight.
   const bool front = e->default_mode() == MODE_V4 && e->split_hist();
   // (kernel timing runs everything on the engine stream: split_hist() is off then)
-  e->timed(KT_RESOLVE, [&] { launch_resolve(front ? e->front : e->stream, resolve_in(b), e->tree, d_rule_out); });
+  const uint32_t nf = resolve_flag_words(b->n_desc);
+  if (nf > e->res_flag_cap) {  // the first batch of a size (then sized for the engine's batches)
+    const uint32_t cap = std::max(nf, resolve_flag_words(e->cfg.max_batch_desc));
+    hipError_t fe = hipStreamSynchronize(front ? e->front : e->stream);  // an older resolve may still read them
+    if (fe == hipSuccess) {
+      hipFree(e->d_res_flags);
+      e->d_res_flags = nullptr;
+      e->res_flag_cap = 0;
+      fe = hipMalloc(&e->d_res_flags, (size_t)cap * 4);
+    }
+    if (fe != hipSuccess) return e->hip_fail(fe, "rl_resolve flags");
+    e->res_flag_cap = cap;
+  }
+  e->timed(KT_RESOLVE, [&] {
+    launch_resolve(front ? e->front : e->stream, resolve_in(b), e->tree, d_rule_out, e->d_res_flags);
+  });
   hipError_t he = hipGetLastError();
   if (he == hipSuccess && front) {
     // a next submit that does not start on the front stream waits for it (run_pipeline)

@@ -91,6 +91,9 @@ void launch_route_pack2(hipStream_t st, const rl_batch& b, const DevRule* rules,
 // descriptors come out RL_CODE_UNKNOWN); stride: the owners' section size in back. h_status
 // (pinned host words, may be null): the n_shards owner statuses copied there by the kernel.
 // Launches nothing for an empty batch.
+// Test fault (RL_ROUTER_FAULT=stall): holds the stream until *release becomes non-zero (pinned
+// host word) or 20 s pass.
+void launch_router_stall(hipStream_t st, const uint32_t* release);
 void launch_route_unpack_raw(hipStream_t st, const rl_batch& b, const DevRule* rules, const RoutePackBufs& o,
                              const RawReply* back, const int32_t* owner_status, uint32_t stride, rl_status* out,
                              uint32_t* thr, int32_t* h_status = nullptr, uint32_t n_shards = 0);

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -298,16 +299,237 @@ RL_HD uint32_t resolve_one(const ResolveIn& in, const TreeDesc2& t, uint32_t i) 
   return rule;
 }
 
-__global__ __launch_bounds__(RS_NT) void k_resolve(ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out) {
+// ---- the level-pipelined walk (k_resolve's first pass) ----
+// resolve_one spends about four dependent round trips per level: the entry's words, its two
+// strings, the edge probe rounds, the candidate nodes. None of the first two depend on the
+// walk, and the node is needed only to confirm a hash match (a node's rule matters only at the
+// last entry; its child count not at all, see below). So this pass loads each level's entry
+// words two levels ahead and its strings one level ahead, hashes both names from registers,
+// takes a probe round's first hash match unconfirmed and confirms it one level later, beside
+// the next level's probe rounds: one round trip per level, plus one for the last node.
+//   * A probe round without a hash match that reaches an empty slot settles a miss exactly
+//     (equal names hash equally). A match whose node turns out to carry another name, a probe
+//     chain longer than one round, and any string the register path cannot hold (over 32 bytes,
+//     an unaligned blob, a last dword past the blob) leave the descriptor to the exact walk.
+//   * No child count check: the reference stops at a node without children (config_impl.go
+//     :320-325); this walk goes on and looks the next entry up under that node, which no edge
+//     has as parent, so it misses and stops there with the same (nil) result.
+constexpr uint32_t RS_EXACT = 0xFFFFFFFEu;  // first pass: left to the exact walk
+#ifndef RL_RESOLVE_FW
+#define RL_RESOLVE_FW 4
+#endif
+// Names the first pass holds in registers: FW dwords (16 bytes; config 4's longest key "_" value
+// is 9). Longer ones go to the exact walk: every dword held here costs the pass occupancy.
+constexpr int FW = RL_RESOLVE_FW;
+constexpr uint32_t FB = 4 * FW;
+static_assert(FW >= 1 && FW <= SW, "first-pass name words");
+
+// true when some lane of the wave still needs the value (device); the thread's own test (host)
+RL_HD inline bool any_lane(bool p) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __ballot(p) != 0ull;
+#else
+  return p;
+#endif
+}
+// load_str for FW dwords, loading only the dwords some lane of the wave needs (config-4 keys
+// are one dword, values one to three): nd dwords at clamped indices, all in flight together.
+RL_HD void load_str_w(const uint8_t* bytes, uint32_t off, uint32_t len, uint32_t (&s)[FW]) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(bytes) + (off >> 2);
+  const uint32_t sh = off & 3u, nd = len ? (sh + len + 3u) >> 2 : 0u;
+  const uint32_t last = nd ? nd - 1u : 0u;
+  uint32_t d[FW + 1];
+#pragma unroll
+  for (int k = 0; k <= FW; ++k) d[k] = any_lane((uint32_t)k < nd) && nd ? w[min((uint32_t)k, last)] : 0u;
+#pragma unroll
+  for (int k = 0; k < FW; ++k) {
+    const uint32_t v = align_byte(d[k + 1], d[k], sh);
+    const uint32_t b0 = 4u * (uint32_t)k;
+    s[k] = b0 >= len ? 0u : b0 + 4u <= len ? v : v & ((1u << (8u * (len - b0))) - 1u);
+  }
+}
+RL_HD uint32_t fold_w(const uint32_t (&s)[FW], uint32_t len) {  // = fold_reg for len <= FB
+  uint32_t h = TREE_FOLD0;
+  const uint32_t nw = (len + 3u) >> 2;
+#pragma unroll
+  for (int k = 0; k < FW; ++k)
+    if ((uint32_t)k < nw) h = tree_fold_word(h, s[k]);
+  return h;
+}
+// r = K "_" V (finalKey, config_impl.go:300): V moved kl + 1 bytes up (kl + 1 <= FB), then K and
+// the underscore
+RL_HD void key_value_w(const uint32_t (&K)[FW], const uint32_t (&V)[FW], uint32_t kl, uint32_t (&r)[FW]) {
+  const uint32_t n = kl + 1u;
+  uint32_t a[FW];
+#pragma unroll
+  for (int k = 0; k < FW; ++k) a[k] = V[k];
+#pragma unroll
+  for (int st = 4; st >= 1; st >>= 1) {  // whole dwords: a log shifter on n >> 2
+    const bool on = ((n >> 2) & (uint32_t)st) != 0;
+#pragma unroll
+    for (int k = FW - 1; k >= 0; --k) a[k] = on ? (k >= st ? a[k - st] : 0u) : a[k];
+  }
+  const uint32_t b = n & 3u;
+#pragma unroll
+  for (int k = FW - 1; k >= 0; --k) {
+    const uint32_t lo = k ? a[k - 1] : 0u;
+    const uint32_t us = (uint32_t)k == (kl >> 2) ? (uint32_t)'_' << (8u * (kl & 3u)) : 0u;
+    r[k] = (b ? align_byte(a[k], lo, 4u - b) : a[k]) | K[k] | us;
+  }
+}
+// A node's header (parent, name length, rule) and first FW name dwords.
+struct NodeW {
+  uint32_t parent, len, rule, name[FW];
+};
+RL_HD NodeW load_node_w(const TreeDesc2& t, uint32_t id) {
+  const uint4* p = reinterpret_cast<const uint4*>(t.nodes + id);
+  const uint4 h = p[0];
+  NodeW v;
+  v.parent = h.x;
+  v.len = h.y;
+  v.rule = h.z;
+  const uint32_t* nm = reinterpret_cast<const uint32_t*>(p + 2);
+#pragma unroll
+  for (int k = 0; k < FW; ++k) v.name[k] = nm[k];
+  return v;
+}
+// the node against (parent, len, the first len bytes of q): q may hold more bytes past len (a
+// key checked against key "_" value), masked here; len <= FB
+RL_HD bool confirm(const NodeW& nd, uint32_t parent, uint32_t len, const uint32_t (&q)[FW]) {
+  uint32_t diff = (nd.parent ^ parent) | (nd.len ^ len);
+#pragma unroll
+  for (int k = 0; k < FW; ++k) {
+    const uint32_t b0 = 4u * (uint32_t)k;
+    const uint32_t m = b0 >= len ? 0u : b0 + 4u <= len ? 0xFFFFFFFFu : (1u << (8u * (len - b0))) - 1u;
+    diff |= nd.name[k] ^ (q[k] & m);
+  }
+  return diff == 0;
+}
+RL_HD uint4 load_entry(const ResolveIn& in, uint32_t e) {
+  return make_uint4(in.entry[4 * e], in.entry[4 * e + 1], in.entry[4 * e + 2], in.entry[4 * e + 3]);
+}
+
+// rule id of descriptor i (exact), or RS_EXACT: the exact walk (resolve_one) decides it.
+RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, uint32_t i) {
+  const uint32_t doff = in.domain[2 * i], dlen = in.domain[2 * i + 1];
+  const uint32_t e0 = in.entry_first[i], e1 = in.entry_first[i + 1];
+  const uint32_t ov = in.override_rule ? in.override_rule[i] : RL_NIL_RULE;
+  const uint64_t blen = in.bytes_len;
+  if (!(e0 <= e1 && e1 <= in.n_entries) || (uint64_t)doff + dlen > blen) return RL_NIL_RULE;  // as resolve_one
+  const bool aligned = (reinterpret_cast<uintptr_t>(in.bytes) & 3u) == 0;
+  const uint64_t bwords = blen & ~3ull;
+  auto reg_ok = [&](uint32_t o, uint32_t l) { return aligned && l <= FB && (((uint64_t)o + l + 3u) & ~3ull) <= bwords; };
+  auto inside = [&](uint32_t o, uint32_t l) { return (uint64_t)o + l <= blen; };
+  auto str_ok = [&](const uint4& x) { return reg_ok(x.x, x.y) && reg_ok(x.z, x.w) && x.y + 1u + x.w <= FB; };
+  auto str_in = [&](const uint4& x) { return inside(x.x, x.y) && inside(x.z, x.w); };
+  if (!reg_ok(doff, dlen)) return RS_EXACT;
+  const uint32_t n = e1 - e0;
+  // round trip 1: the domain's dwords and the first two entries' words
+  uint32_t Q[FW];  // the name to confirm: the domain, then key ["_" value] of a level
+  load_str_w(in.bytes, doff, dlen, Q);
+  uint4 E = n > 0 ? load_entry(in, e0) : make_uint4(0, 0, 0, 0);
+  uint4 En = n > 1 ? load_entry(in, e0 + 1) : make_uint4(0, 0, 0, 0);
+  const uint32_t hd = tree_hash(RL_TREE_ROOT, fold_w(Q, dlen), dlen);
+  // round trip 2: the domain's probe round and level 0's strings
+  uint64_t w[TREE_PROBE];
+  probe_round(t, hd, w);
+  uint32_t K[FW], V[FW];
+  {
+    const bool ld = n > 0 && str_ok(E);
+    load_str_w(in.bytes, ld ? E.x : 0u, ld ? E.y : 0u, K);
+    load_str_w(in.bytes, ld ? E.z : 0u, ld ? E.w : 0u, V);
+  }
+  bool dn;
+  uint32_t pend = first_match(w, hd, dn);  // the node to confirm (parent pp, name Q[0, pl))
+  if (pend == TREE_NONE) return dn ? RL_NIL_RULE : RS_EXACT;  // unknown domain (:279-284)
+  uint32_t pp = RL_TREE_ROOT, pl = dlen;
+  if (ov != RL_NIL_RULE || n == 0) {  // override (:286-296), or no entries: the domain alone decides
+    if (!confirm(load_node_w(t, pend), pp, pl, Q)) return RS_EXACT;
+    return ov;
+  }
+  uint32_t parent = pend;
+  for (uint32_t l = 0; l < n; ++l) {
+    // level l: K / V hold entry l's strings, E its words, En entry l+1's
+    if (!str_in(E)) return RL_NIL_RULE;  // as resolve_one: a string outside bytes ends the walk nil
+    if (!str_ok(E)) return RS_EXACT;
+    const uint32_t kl = E.y, lv = kl + 1u + E.w;
+    uint32_t Qn[FW];
+    key_value_w(K, V, kl, Qn);
+    const uint32_t hv = tree_hash(parent, fold_w(Qn, lv), lv), hk = tree_hash(parent, fold_w(K, kl), kl);
+    // one round trip: both probe rounds, the pending node, level l+1's strings, entry l+2's words
+    uint64_t wv[TREE_PROBE], wk[TREE_PROBE];
+    probe_round(t, hv, wv);
+    probe_round(t, hk, wk);
+    const NodeW pv = load_node_w(t, pend);
+    {
+      const bool ld = l + 1 < n && str_ok(En);
+      load_str_w(in.bytes, ld ? En.x : 0u, ld ? En.y : 0u, K);
+      load_str_w(in.bytes, ld ? En.z : 0u, ld ? En.w : 0u, V);
+    }
+    const uint4 Enn = l + 2 < n ? load_entry(in, e0 + l + 2) : make_uint4(0, 0, 0, 0);
+    if (!confirm(pv, pp, pl, Q)) return RS_EXACT;
+    bool dv, dk;
+    const uint32_t cv = first_match(wv, hv, dv);
+    uint32_t nd;
+    if (cv != TREE_NONE) {
+      nd = cv;
+      pl = lv;
+    } else if (!dv) {
+      return RS_EXACT;
+    } else {
+      const uint32_t ck = first_match(wk, hk, dk);
+      if (ck == TREE_NONE) return dk ? RL_NIL_RULE : RS_EXACT;  // neither edge: the walk stops (:309), nil
+      nd = ck;
+      pl = kl;
+    }
+#pragma unroll
+    for (int k = 0; k < FW; ++k) Q[k] = Qn[k];  // (confirm masks it to pl bytes)
+    pp = parent;
+    pend = nd;
+    parent = nd;
+    E = En;
+    En = Enn;
+  }
+  // the last entry's node: confirmed, and its limit (:311-318)
+  const NodeW v = load_node_w(t, pend);
+  if (!confirm(v, pp, pl, Q)) return RS_EXACT;
+  return v.rule;
+}
+
+// First pass: one thread per descriptor; a block with a descriptor left to the exact walk
+// raises its flag (every block writes its flag, so nothing needs clearing between batches).
+__global__ __launch_bounds__(RS_NT) void k_resolve(ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out,
+                                                  uint32_t* __restrict__ flags) {
   const uint32_t i = blockIdx.x * RS_NT + threadIdx.x;
-  if (i < in.n_desc) rule_out[i] = resolve_one(in, t, i);
+  const uint32_t r = i < in.n_desc ? resolve_fast(in, t, i) : 0u;
+  if (i < in.n_desc) rule_out[i] = r;
+  const int any = __syncthreads_or(r == RS_EXACT);
+  if (threadIdx.x == 0) flags[blockIdx.x] = (uint32_t)any;
+}
+// Second pass: blocks stride over the first pass's flags; a flagged block's descriptors left
+// to the exact walk take it.
+constexpr uint32_t RS_EXACT_BLOCKS = 256;
+__global__ __launch_bounds__(RS_NT) void k_resolve_exact(ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out,
+                                                        const uint32_t* __restrict__ flags, uint32_t nblk) {
+  for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    if (!flags[b]) continue;  // block-uniform
+    const uint32_t i = b * RS_NT + threadIdx.x;
+    if (i < in.n_desc && rule_out[i] == RS_EXACT) rule_out[i] = resolve_one(in, t, i);
+  }
 }
 
 }  // namespace
 
 // The same walk on the host, over host copies of the tree and the batch (tests/cshim: the
-// device code path checked against the config oracle without a GPU).
-uint32_t resolve_one_host(const ResolveIn& in, const TreeDesc2& t, uint32_t i) { return resolve_one(in, t, i); }
+// device code path checked against the config oracle without a GPU): the first pass, then the
+// exact walk for what it leaves. *exact (optional) tells which pass decided.
+uint32_t resolve_one_host(const ResolveIn& in, const TreeDesc2& t, uint32_t i, bool* exact) {
+  const uint32_t r = resolve_fast(in, t, i);
+  if (exact) *exact = r == RS_EXACT;
+  return r == RS_EXACT ? resolve_one(in, t, i) : r;
+}
+uint32_t resolve_exact_host(const ResolveIn& in, const TreeDesc2& t, uint32_t i) { return resolve_one(in, t, i); }
+uint32_t resolve_flag_words(uint32_t n_desc) { return (n_desc + RS_NT - 1) / RS_NT; }
 
 int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint32_t names_len,
                std::vector<TreeNodeDev>& out_nodes, std::vector<uint64_t>& out_slots, uint32_t& mask,
@@ -364,9 +586,12 @@ int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint
   return 0;
 }
 
-void launch_resolve(hipStream_t st, const ResolveIn& in, const TreeDesc2& t, uint32_t* rule_out) {
+void launch_resolve(hipStream_t st, const ResolveIn& in, const TreeDesc2& t, uint32_t* rule_out, uint32_t* flags) {
   if (!in.n_desc) return;
-  hipLaunchKernelGGL(k_resolve, dim3((in.n_desc + RS_NT - 1) / RS_NT), dim3(RS_NT), 0, st, in, t, rule_out);
+  const uint32_t nblk = resolve_flag_words(in.n_desc);
+  hipLaunchKernelGGL(k_resolve, dim3(nblk), dim3(RS_NT), 0, st, in, t, rule_out, flags);
+  hipLaunchKernelGGL(k_resolve_exact, dim3(std::min(nblk, RS_EXACT_BLOCKS)), dim3(RS_NT), 0, st, in, t, rule_out, flags,
+                     nblk);
 }
 
 }  // namespace rlhip

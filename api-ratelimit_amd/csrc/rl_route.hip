@@ -1055,6 +1055,18 @@ __global__ __launch_bounds__(NT) void k_route_unpack_raw(DevBatch in, const DevR
 static uint32_t route_blocks(uint32_t n) { return n ? (n + route::NT - 1) / route::NT : 1; }
 uint32_t route_bcnt_words(uint32_t n) { return route_blocks(n) * (route::NS + 1); }  // counts, then errors
 
+// RL_ROUTER_FAULT=stall (tests): one wave holds the stream until the router raises the release
+// word on abort, or 20 s of the 100-MHz real-time clock pass (every launch ends).
+__global__ __launch_bounds__(64) void k_router_stall(const uint32_t* release) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u &&
+         __builtin_amdgcn_s_memrealtime() - t0 < 2000000000ull)
+    __builtin_amdgcn_s_sleep(127);
+}
+void launch_router_stall(hipStream_t st, const uint32_t* release) {
+  hipLaunchKernelGGL(k_router_stall, dim3(1), dim3(64), 0, st, release);
+}
+
 void launch_route_pack(hipStream_t st, const rl_batch& b, const DevRule* rules, uint32_t n_rules, uint64_t seed,
                        uint32_t origin, uint32_t n_shards, RRec* tmp, uint8_t* own, uint32_t* bcnt, RRec* send,
                        uint32_t* send_counts, uint32_t* perm, EngineCtl* ctl, uint32_t* x) {

@@ -47,6 +47,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
@@ -72,16 +73,6 @@ constexpr uint32_t XS = 4;
 constexpr uint32_t HX_HOT = (2 * XS + 2) * MAXS;
 constexpr uint32_t MAX_LAG_S = 3;          // a request may come this many seconds behind the step clock
 
-// Host wait for an event by polling: a blocking stream synchronize sleeps and wakes 10-20 us
-// after the GPU is done, on the routed step's critical path between exchanges.
-hipError_t poll_event(hipEvent_t ev) {
-  for (int k = 0; k < (1 << 20); ++k) {
-    const hipError_t e = hipEventQuery(ev);
-    if (e != hipErrorNotReady) return e;
-  }
-  return hipEventSynchronize(ev);
-}
-
 double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -90,8 +81,10 @@ double now_us() {
 // the shard behaves as if a HIP call of that phase failed.
 // "comm": the shard's communicator fails at the counts exchange (the transport aborts; every rank
 // is broken from then on).
-enum Phase { PH_NONE = 0, PH_PACK, PH_RECORDS, PH_DECIDE, PH_REPLIES, PH_UNPACK, PH_STATUS, PH_COMM };
-const char* const kPhaseNames[] = {"", "pack", "records", "decide", "replies", "unpack", "status", "comm"};
+// "stall": the shard's exchange stream stalls before the counts exchange (a device kernel that
+// waits for the router's abort, at most 20 s), as if a peer never reached the collective.
+enum Phase { PH_NONE = 0, PH_PACK, PH_RECORDS, PH_DECIDE, PH_REPLIES, PH_UNPACK, PH_STATUS, PH_COMM, PH_STALL };
+const char* const kPhaseNames[] = {"", "pack", "records", "decide", "replies", "unpack", "status", "comm", "stall"};
 
 // ---- collective transports ----------------------------------------------------------------
 // The three collectives a routed step uses, in bytes, on the router's exchange stream.
@@ -104,6 +97,9 @@ struct Xport {
   virtual ncclResult_t group_start() { return ncclSuccess; }
   virtual ncclResult_t group_end() { return ncclSuccess; }
   virtual void abort() = 0;
+  // an asynchronous failure of the communicator (a peer's, or the network's), polled while the
+  // host waits for work behind a collective
+  virtual ncclResult_t async_error() = 0;
   virtual std::string why(ncclResult_t r) { return ncclGetErrorString(r); }
 };
 
@@ -127,6 +123,11 @@ struct RcclXport : Xport {
   void abort() override {
     if (comm) (void)ncclCommAbort(comm);
     comm = nullptr;
+  }
+  ncclResult_t async_error() override {
+    ncclResult_t r = ncclSuccess;
+    if (comm && ncclCommGetAsyncError(comm, &r) != ncclSuccess) return ncclSystemError;
+    return r;
   }
 };
 
@@ -154,7 +155,8 @@ struct EmuWorld {
   };
   Post post[MAXS];
   hipEvent_t done[MAXS];
-  // all G ranks arrive, or the world aborts (a rank failed, or one never came: 120 s)
+  int64_t timeout_ms = 120000;  // the routers' RL_ROUTER_TIMEOUT_MS
+  // all G ranks arrive, or the world aborts (a rank failed, or one never came within the timeout)
   bool barrier() {
     std::unique_lock<std::mutex> l(mu);
     if (aborted) return false;
@@ -165,11 +167,11 @@ struct EmuWorld {
       cv.notify_all();
       return true;
     }
-    const bool ok = cv.wait_for(l, std::chrono::seconds(120), [&] { return gen != g || aborted; });
+    const bool ok = cv.wait_for(l, std::chrono::milliseconds(timeout_ms), [&] { return gen != g || aborted; });
     if (aborted) return false;
     if (!ok) {
       aborted = true;
-      why = "a rank did not arrive at a collective within 120 s";
+      why = "a rank did not arrive at a collective within " + std::to_string(timeout_ms) + " ms";
       cv.notify_all();
       return false;
     }
@@ -256,6 +258,10 @@ struct EmuXport : Xport {
     return a2av(s, c, z, r, c, d, st);
   }
   void abort() override { w->abort("rank " + std::to_string(me) + " aborted the communicator"); }
+  ncclResult_t async_error() override {
+    std::lock_guard<std::mutex> l(w->mu);
+    return w->aborted ? ncclRemoteError : ncclSuccess;
+  }
   std::string why(ncclResult_t r) override {
     std::lock_guard<std::mutex> l(w->mu);
     return std::string(ncclGetErrorString(r)) + (w->why.empty() ? "" : " (" + w->why + ")");
@@ -362,6 +368,8 @@ struct StepSlot {
   bool end_rec = false;        // ... and ev_end recorded behind them
   hipError_t rep_he = hipSuccess;
   hipEvent_t ev_end = nullptr; // the reply exchange (rs) and the unpack (os) of the step
+  hipEvent_t ev_rec = nullptr; // collective: the step's record exchange (its owner batches wait for it)
+  bool rec_rec = false;        // ... recorded
   double t0 = 0;
   int32_t status[MAXS] = {};   // per shard (collective: as received from every origin / owner)
   bool late[MAXS] = {};        // per origin: refused for starting too far behind the step clock
@@ -397,6 +405,8 @@ struct rl_router {
   int fault_phase = PH_NONE;
   uint32_t fault_shard = 0;
   uint64_t fault_step = 0;   // fires in a submit of step >= fault_step (or a wait after it)
+  uint32_t* h_stall = nullptr;  // "stall" fault: the stalled kernel's release word (pinned)
+  int64_t timeout_ms = 60000;   // bound of every host wait behind a collective (RL_ROUTER_TIMEOUT_MS)
   rl_router_stats st{};
   std::string err;
 
@@ -412,9 +422,40 @@ struct rl_router {
   // collective failure: abort the communicator (its peers' collectives return), every later call fails
   int nccl_fail(ncclResult_t nr, const char* what) {
     const std::string w = xp ? xp->why(nr) : ncclGetErrorString(nr);
+    abort_comm();
+    return fail(RL_ECOMM, "%s: %s (communicator aborted)", what, w.c_str());
+  }
+  void abort_comm() {
     if (xp) xp->abort();
     broken = true;
-    return fail(RL_ECOMM, "%s: %s (communicator aborted)", what, w.c_str());
+    if (h_stall) __atomic_store_n(h_stall, 1u, __ATOMIC_RELEASE);  // (a stalled test kernel ends)
+  }
+  // Collective transports: the host's wait for work queued behind a collective (an event, or the
+  // stream when ev is null). A peer that never reaches the collective (a rank that diverged or
+  // stopped without its launcher ending the job) would hold that work, and so this rank, forever:
+  // the wait polls the communicator's asynchronous error and ends after timeout_ms, and either
+  // aborts the communicator (which ends its pending kernels, here and at every peer) and returns
+  // RL_ECOMM; every later call of the router fails with it. The reference's analog: a Redis
+  // failure becomes a RedisError panic, not a stall (src/redis/driver_impl.go:50-54). Returns 0
+  // with *he the wait's own HIP result otherwise.
+  int wait_bounded(hipEvent_t ev, hipStream_t q, const char* what, hipError_t* he) {
+    const double t_end = now_us() + 1e3 * (double)timeout_ms;
+    for (uint64_t k = 0;; ++k) {
+      const hipError_t r = ev ? hipEventQuery(ev) : hipStreamQuery(q);
+      if (r != hipErrorNotReady) {
+        if (he) *he = r;
+        return 0;
+      }
+      if ((k & 255u) != 255u) continue;
+      const ncclResult_t ar = xp ? xp->async_error() : ncclSuccess;
+      if (ar != ncclSuccess && ar != ncclInProgress) return nccl_fail(ar, what);
+      if (now_us() > t_end) {
+        abort_comm();
+        return fail(RL_ECOMM, "%s: no progress within %lld ms (RL_ROUTER_TIMEOUT_MS): a peer did not reach the "
+                              "collective (communicator aborted)", what, (long long)timeout_ms);
+      }
+      if (k > (1u << 16)) std::this_thread::sleep_for(std::chrono::microseconds(20));  // a long wait: yield the core
+    }
   }
   bool fault(int phase, uint32_t s) {
     if (fault_phase != phase || fault_shard != s || (fault_step && seq <= fault_step)) return false;
@@ -468,9 +509,12 @@ void rl_router::free_all() {
   if (h_ag) (void)hipHostFree(h_ag);
   xp.reset();
   for (StepSlot& q : slot) {
-    if (q.ev_end) (void)hipEventDestroy(q.ev_end);
-    q.ev_end = nullptr;
+    for (hipEvent_t e : {q.ev_end, q.ev_rec})
+      if (e) (void)hipEventDestroy(e);
+    q.ev_end = q.ev_rec = nullptr;
   }
+  if (h_stall) (void)hipHostFree(h_stall);
+  h_stall = nullptr;
   for (hipEvent_t e : {ev_rs, ev_cnt})
     if (e) (void)hipEventDestroy(e);
   if (rs && rs_own) (void)hipStreamDestroy(rs);
@@ -656,7 +700,7 @@ void rl_router::refresh_hot() {
       return;
     }
     if (he == hipSuccess) he = hipMemcpyAsync(h_ag + HOT_MAX, d_ag + HOT_MAX, n * cfg.n_shards, hipMemcpyDeviceToHost, rs);
-    if (he == hipSuccess) he = hipStreamSynchronize(rs);
+    if (he == hipSuccess && wait_bounded(nullptr, rs, "allgather(hot sets)", &he)) return;
     if (he != hipSuccess) return;  // keep the current sets (decisions do not depend on them)
     for (uint32_t i = 0; i < HOT_MAX * cfg.n_shards; ++i) {
       const AgEntry& a = h_ag[HOT_MAX + i];
@@ -694,7 +738,14 @@ void rl_router::refresh_hot() {
     std::vector<HotEntry> t;
     build_hot_table(next, t);
     // the staging's previous copy is done; the next pack is ordered behind this copy on os
-    if (hipEventSynchronize(s.ev_hot) != hipSuccess) continue;
+    // (collective transports: os carries the exchanges, so the wait is bounded)
+    hipError_t hw = hipSuccess;
+    if (coll) {
+      if (wait_bounded(s.ev_hot, nullptr, "hot set staging", &hw)) return;
+    } else {
+      hw = hipEventSynchronize(s.ev_hot);
+    }
+    if (hw != hipSuccess) continue;
     memcpy(s.h_hot, t.data(), sizeof(HotEntry) * t.size());
     if (hipMemcpyAsync(s.d_hot, s.h_hot, sizeof(HotEntry) * t.size(), hipMemcpyHostToDevice, s.os) != hipSuccess)
       continue;
@@ -722,7 +773,8 @@ int rl_router::check_config() {
     if (nr != ncclSuccess) return nccl_fail(nr, "allgather(router configuration)");
     if (he == hipSuccess)
       he = hipMemcpyAsync(hw + 1, dw + 1, sizeof(CfgWord) * cfg.n_shards, hipMemcpyDeviceToHost, rs);
-    if (he == hipSuccess) he = hipStreamSynchronize(rs);
+    if (he == hipSuccess)
+      if (int rc = wait_bounded(nullptr, rs, "allgather(router configuration)", &he)) return rc;
     if (he != hipSuccess) return fail(RL_EHIP, "router configuration exchange: %s", hipGetErrorString(he));
     all.assign(hw + 1, hw + 1 + cfg.n_shards);
   } else {
@@ -763,6 +815,12 @@ bool rl_router::step_clock(uint32_t k, const uint32_t* tmin, const uint32_t* tma
 
 // Complete the oldest owner batch of the engine: x's (the older step's first, FIFO).
 void rl_router::drain(Shard& S, ShardStep& x) {
+  if (coll && !broken) {
+    // the step's owner batches run behind its record exchange: a bounded wait for that first
+    // (on expiry the communicator is aborted, which ends the exchange, and the engine drains)
+    const StepSlot& q = slot[&x - S.st];
+    if (q.rec_rec) (void)wait_bounded(q.ev_rec, nullptr, "all-to-all-v(records)", nullptr);
+  }
   const int rp = rl_wait(S.e);
   if (rp && !x.rc_dec) {
     x.rc_dec = rp;
@@ -807,14 +865,15 @@ int rl_router::submit_coll(uint32_t k) {
   // by the pack or with the host's status words: only a successful upload of its real status
   // replaces it (reply_coll), so a failed upload cannot hand peers a stale status of an earlier step)
   if (fault(PH_COMM, 0)) return nccl_fail(ncclInternalError, "all-to-all(counts): injected fault (comm)");
+  if (h_stall && fault(PH_STALL, 0)) launch_router_stall(rs, h_stall);
   ncclResult_t nr = xp->a2a(t.d_x, t.d_x + XS * G, 4 * XS, rs);
   if (nr != ncclSuccess) return nccl_fail(nr, "all-to-all(counts)");
   if (he == hipSuccess) he = hipMemcpyAsync(t.h_x, t.d_x, 8 * XS * G, hipMemcpyDeviceToHost, rs);
   if (he == hipSuccess) he = hipEventRecord(ev_cnt, rs);
-  if (he == hipSuccess) he = poll_event(ev_cnt);
+  if (he == hipSuccess)
+    if (int rc = wait_bounded(ev_cnt, nullptr, "all-to-all(counts)", &he)) return rc;
   if (he != hipSuccess) {  // the counts are unknown: nobody can take part in the record exchange
-    broken = true;
-    if (xp) xp->abort();
+    abort_comm();
     return fail(RL_ECOMM, "counts exchange: %s (communicator aborted)", hipGetErrorString(he));
   }
   const int32_t* hs = t.h_x;
@@ -890,7 +949,8 @@ int rl_router::submit_coll(uint32_t k) {
   nr = xp->a2av(t.pb.send, sc, sd, t.recv, rc, rd, rs);
   if (nr != ncclSuccess) return nccl_fail(nr, "all-to-all-v(records)");
   const double t1 = now_us();
-  he = hipEventRecord(ev_rs, rs);
+  he = hipEventRecord(slot[k].ev_rec, rs);
+  slot[k].rec_rec = he == hipSuccess;
   if (fault(PH_RECORDS, 0)) he = hipErrorUnknown;
   if (he != hipSuccess) {  // keep going: the failure travels in the reply exchange
     t.rc_local = RL_EHIP;
@@ -901,7 +961,7 @@ int rl_router::submit_coll(uint32_t k) {
     owner_runs(t.rcv, t.tmin, t.tmax, G, runs);
     t.n_runs = (uint32_t)runs.size();
     for (const Run& u : runs) {
-      const int rc2 = submit_owner(0, k, u, ev_rs);
+      const int rc2 = submit_owner(0, k, u, slot[k].ev_rec);
       if (rc2) {
         if (!t.rc_dec) {
           t.rc_dec = rc2;
@@ -1131,6 +1191,7 @@ void rl_router::reply_coll(uint32_t k) {
   slot[k].replied = true;
   const double t0 = now_us();
   while (t.n_sub) drain(S, t);
+  if (broken) return;  // a record exchange that never completed (drain's bounded wait aborted)
   if (!t.rc_dec && !t.rc_local && fault(PH_DECIDE, 0)) {
     t.rc_dec = RL_EHIP;
     t.msg = "injected fault (decide)";
@@ -1234,14 +1295,14 @@ void rl_router::wait_coll(uint32_t k) {
   const double t2 = now_us();
   hipError_t he = slot[k].rep_he;
   // after a failure to enqueue, drain both streams
-  hipError_t h2;
+  hipError_t h2 = hipSuccess;
   if (slot[k].end_rec) {
-    h2 = poll_event(slot[k].ev_end);
+    if (wait_bounded(slot[k].ev_end, nullptr, "all-to-all(replies)", &h2)) return;
     he = h2;
   } else {
-    h2 = hipStreamSynchronize(rs);
+    if (wait_bounded(nullptr, rs, "all-to-all(replies)", &h2)) return;
     if (he == hipSuccess) he = h2;
-    if (he == hipSuccess) he = hipStreamSynchronize(S.os);
+    if (he == hipSuccess && wait_bounded(nullptr, S.os, "all-to-all(replies)", &he)) return;
   }
   if (he == hipSuccess && fault(PH_UNPACK, 0)) he = hipErrorUnknown;
   st.unpack_us += now_us() - t2;
@@ -1412,12 +1473,20 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
     r->o_jit = r->o_hits + al(N * 4);
     r->in_bytes = r->o_jit + al(N * 2);
   }
+  if (const char* t = getenv("RL_ROUTER_TIMEOUT_MS")) {
+    const long long v = atoll(t);
+    if (v > 0) r->timeout_ms = v;
+  }
+  if (emu) {
+    std::lock_guard<std::mutex> l(world->mu);
+    world->timeout_ms = r->timeout_ms;
+  }
   if (const char* f = getenv("RL_ROUTER_FAULT")) {  // tests: "phase:shard[:step]"
     char ph[32] = {0};
     unsigned s = 0, k = 0;
     if (sscanf(f, "%31[a-z]:%u:%u", ph, &s, &k) >= 2) {
       r->fault_step = k;
-      for (int p = 1; p <= PH_COMM; ++p)
+      for (int p = 1; p <= PH_STALL; ++p)
         if (!strcmp(ph, kPhaseNames[p])) {
           r->fault_phase = p;
           r->fault_shard = coll ? (s == cfg->rank ? 0u : 0xFFFFFFFFu) : s;
@@ -1434,9 +1503,14 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
   if (hipEventCreateWithFlags(&r->ev_rs, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&r->ev_cnt, hipEventDisableTiming) != hipSuccess ||
       std::any_of(std::begin(r->slot), std::end(r->slot), [](StepSlot& q) {
-        return hipEventCreateWithFlags(&q.ev_end, hipEventDisableTiming) != hipSuccess;
+        return hipEventCreateWithFlags(&q.ev_end, hipEventDisableTiming) != hipSuccess ||
+               hipEventCreateWithFlags(&q.ev_rec, hipEventDisableTiming) != hipSuccess;
       }))
     return bail(RL_EHIP);
+  if (r->fault_phase == PH_STALL) {
+    if (hipHostMalloc(&r->h_stall, 64, hipHostMallocDefault) != hipSuccess) return bail(RL_EHIP);
+    *r->h_stall = 0;
+  }
   if (emu) {
     auto* ex = static_cast<EmuXport*>(r->xp.get());
     if (hipEventCreateWithFlags(&ex->ev_pre, hipEventDisableTiming) != hipSuccess ||
@@ -1544,10 +1618,10 @@ int rl_router_allgather_host(rl_router* r, const void* in, uint32_t n_bytes, voi
   if (nr != ncclSuccess) return r->nccl_fail(nr, "allgather(host words)");
   if (he == hipSuccess && n_bytes)
     he = hipMemcpyAsync(hs + RL_ROUTER_AG_MAX, ds + RL_ROUTER_AG_MAX, (size_t)n_bytes * G, hipMemcpyDeviceToHost, r->rs);
-  if (he == hipSuccess) he = hipStreamSynchronize(r->rs);
+  if (he == hipSuccess)
+    if (int rc = r->wait_bounded(nullptr, r->rs, "allgather(host words)", &he)) return rc;
   if (he != hipSuccess) {  // the peers have their words; this rank cannot tell what it received
-    if (r->xp) r->xp->abort();
-    r->broken = true;
+    r->abort_comm();
     return r->fail(RL_ECOMM, "allgather(host words): %s (communicator aborted)", hipGetErrorString(he));
   }
   if (n_bytes) memcpy(out, hs + RL_ROUTER_AG_MAX, (size_t)n_bytes * G);

@@ -47,8 +47,16 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "api-ratelimit_amd"))
 
 import hiprl  # noqa: E402
-import router  # noqa: E402
 import workload  # noqa: E402
+
+# router.py imports torch, which maps the HIP runtime: imported where used, so the launcher
+# process of `--gpus N` (launch_ranks) starts its ranks without it
+
+
+def _router():
+    import router
+
+    return router
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 T0 = 1_700_000_020      # not minute-aligned: SECOND / MINUTE / HOUR keys in their own home regions
@@ -139,9 +147,7 @@ def launch_ranks(args) -> int | None:
     if args.gpus <= 1:
         return None
     if not args.dry_launch:
-        import torch  # device_count() reads the device list without initialising HIP on this image
-
-        have = torch.cuda.device_count()
+        have = gpu_count_sysfs()
         if have < args.gpus:
             raise SystemExit(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, this box has {have}")
     port = args.master_port
@@ -158,7 +164,52 @@ def launch_ranks(args) -> int | None:
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     env.setdefault("OMP_NUM_THREADS", "4")
+    print(f"bench.py launcher: {launcher_device_report()}", file=sys.stderr, flush=True)
     return subprocess.run(cmd, env=env).returncode
+
+
+def gpu_count_sysfs() -> int:
+    """GPUs in the KFD topology (nodes whose gfx_target_version is non-zero; CPU nodes have 0),
+    narrowed by a non-empty ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES.
+    Read from sysfs: the launcher neither opens /dev/kfd nor loads the HIP runtime
+    (torch.cuda.device_count() falls back to hipGetDeviceCount when amdsmi fails)."""
+    n = 0
+    try:
+        nodes = list(Path("/sys/class/kfd/kfd/topology/nodes").iterdir())
+    except OSError:
+        return 0
+    for node in nodes:
+        try:
+            for line in (node / "properties").read_text().splitlines():
+                key, _, val = line.partition(" ")
+                if key == "gfx_target_version" and int(val) != 0:
+                    n += 1
+        except (OSError, ValueError):
+            continue
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var, "").strip()
+        if v:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
+def launcher_device_report() -> str:
+    """What this (launcher) process holds of the GPU: an open /dev/kfd, the HIP runtime mapped."""
+    kfd = False
+    try:
+        for fd in os.listdir("/proc/self/fd"):
+            try:
+                kfd |= os.readlink(f"/proc/self/fd/{fd}") == "/dev/kfd"
+            except OSError:
+                pass
+    except OSError:
+        pass
+    try:
+        with open("/proc/self/maps") as f:
+            hip = "libamdhip64" in f.read()
+    except OSError:
+        hip = False
+    return f"/dev/kfd open: {'yes' if kfd else 'no'}; HIP runtime loaded: {'yes' if hip else 'no'}"
 
 
 def dry_launch_main(args):
@@ -219,7 +270,7 @@ class DeviceGen:
 
     def alloc(self):
         t, d, dev = self.torch, self.d, self.dev
-        db = router.DeviceBatch(t.empty(d * self.max_len + 64, dtype=t.uint8, device=dev),
+        db = _router().DeviceBatch(t.empty(d * self.max_len + 64, dtype=t.uint8, device=dev),
                                 t.zeros(d + 1, dtype=t.int32, device=dev), t.empty(d, dtype=t.int32, device=dev),
                                 t.empty(d, dtype=t.int32, device=dev), t.empty(d, dtype=t.int64, device=dev),
                                 t.ones(d, dtype=t.int32, device=dev), d * self.max_len)
@@ -270,7 +321,7 @@ class HostGen:
         self.d, self.seed, self.dev = d, seed, dev
 
     def make(self, b: int):
-        return router.DeviceBatch.from_host(workload.config1_batch(b, d=self.d, seed=self.seed, t0=T0), self.dev)
+        return _router().DeviceBatch.from_host(workload.config1_batch(b, d=self.d, seed=self.seed, t0=T0), self.dev)
 
 
 def random_access_roofline(eng, alg_bytes, U, pipe_ms, step_ms):
@@ -533,6 +584,7 @@ def main():
         dist.broadcast_object_list(ids, src=0)
         nrt = hiprl.Router([eng], max_desc=d, n_shards=world, rank=rank, rccl_id=ids[0], combine=not args.no_combine)
     elif routed:
+        router = _router()
         rtr = router.ShardRouter(router.EngineShard(eng, rank, world, dev, d))
     pipelined = not routed and not args.serial
     DEPTH = min(args.depth, hiprl.MAX_IN_FLIGHT) if pipelined else 1

@@ -70,3 +70,29 @@ def test_not_enough_gpus_fails_loudly():
     assert p.returncode != 0
     assert "needs 2 GPUs" in p.stderr
     assert '"n_gpus"' not in p.stdout
+
+
+def test_launcher_parent_stays_off_the_gpu():
+    """the parent that starts the ranks counts GPUs from the KFD topology in
+    sysfs, so it never opens /dev/kfd nor loads the HIP runtime before its ranks start (it
+    reports what it holds, from /proc/self)."""
+    p = _run(["--gpus", "2", "--dry-launch"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "bench.py launcher: /dev/kfd open: no; HIP runtime loaded: no" in p.stderr, p.stderr[-2000:]
+
+
+def test_gpu_count_from_sysfs():
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    n = bench.gpu_count_sysfs()
+    assert n >= 0
+    old = os.environ.get("HIP_VISIBLE_DEVICES")
+    os.environ["HIP_VISIBLE_DEVICES"] = "0"
+    try:
+        assert bench.gpu_count_sysfs() == min(n, 1)
+    finally:
+        if old is None:
+            del os.environ["HIP_VISIBLE_DEVICES"]
+        else:
+            os.environ["HIP_VISIBLE_DEVICES"] = old

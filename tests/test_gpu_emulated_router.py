@@ -513,3 +513,42 @@ def test_emulated_repack(depth):
     assert all(x["status"] == [0] * G and x["steps"] == len(all_steps) for x in st), st
     assert st[0]["repacks"] >= 1 and st[0]["combined_steps"] >= 3, st[0]
     ranks.close()
+
+
+def test_stalled_rank_fails_every_rank_within_the_timeout(monkeypatch):
+    """rank 2 of 4 never completes the counts exchange (RL_ROUTER_FAULT=stall:
+    a device kernel holds its exchange stream, as a peer that never arrives holds a collective).
+    With RL_ROUTER_TIMEOUT_MS=2000 every rank's step fails with RL_ECOMM within seconds instead of
+    hanging (the bounded host wait aborts the communicator; the others see the abort), destroy
+    completes, and the engines then take a fresh batch exactly."""
+    import time
+    G, per = 4, 800
+    steps = skew_batches(G, 1, per, seed=78)
+    monkeypatch.setenv("RL_ROUTER_FAULT", "stall:2")
+    monkeypatch.setenv("RL_ROUTER_TIMEOUT_MS", "2000")
+    ranks = EmuRanks(G, per)
+    monkeypatch.delenv("RL_ROUTER_FAULT")
+    monkeypatch.delenv("RL_ROUTER_TIMEOUT_MS")
+    bs, outs, thrs = Bufs(steps[0]).args()
+    torch.cuda.synchronize()
+    codes = [None] * G
+
+    def worker(r):
+        R = ranks.routers[r]
+        try:
+            R.submit([bs[r]], [outs[r]], [thrs[r]])
+            R.wait()
+        except hiprl.RedisError as e:
+            codes[r] = e.code
+    t0 = time.monotonic()
+    parallel(G, worker, timeout=60)
+    dt = time.monotonic() - t0
+    assert codes == [-8] * G, codes
+    assert dt < 30, dt
+    ranks.close()
+    for k, e in enumerate(ranks.engines):
+        reqs = [(f"after{k}", [[("k", str(i % 89))]], [i % len(RULES)], 1 + i % 3, 1_700_000_200) for i in range(1200)]
+        b = hiprl.build_batch(reqs)
+        gs, gt = e.submit(b)
+        es, et = new_oracle().submit(b)
+        streams.assert_same(es, et, gs, gt, f"engine {k} after a stalled rank")

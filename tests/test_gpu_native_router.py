@@ -160,3 +160,36 @@ def test_rccl_transport_one_rank_errors(monkeypatch):
     assert ex.value.code == -4
     _check(o, steps[2], _step(r, steps[2]), "after")
     r.close()
+
+
+def test_rccl_transport_stall_times_out(monkeypatch):
+    """VERDICT r5 next-3a on the RCCL transport itself (one-rank communicator): the exchange
+    stream held before the counts exchange (RL_ROUTER_FAULT=stall:0). The bounded host wait
+    polls ncclCommGetAsyncError, gives up after RL_ROUTER_TIMEOUT_MS, aborts the communicator
+    (ncclCommAbort) and returns RL_ECOMM; every later call fails the same way and destroy
+    completes (the stalled kernel is released by the abort)."""
+    import time
+    monkeypatch.setenv("NCCL_SOCKET_IFNAME", "lo")
+    monkeypatch.setenv("RL_ROUTER_FAULT", "stall:0")
+    monkeypatch.setenv("RL_ROUTER_TIMEOUT_MS", "1500")
+    per = 1000
+    e = hiprl.Engine(local_cache=True, max_batch_desc=4 * per)
+    e.load_rules(streams.RULES)
+    r = hiprl.Router([e], max_desc=4 * per, n_shards=1, rank=0, rccl_id=hiprl.Router.unique_id())
+    monkeypatch.delenv("RL_ROUTER_FAULT")
+    monkeypatch.delenv("RL_ROUTER_TIMEOUT_MS")
+    steps = stream_batches(1, 2, per, seed=33)
+    t0 = time.monotonic()
+    with pytest.raises(hiprl.RedisError, match="no progress within 1500 ms") as ex:
+        _step(r, steps[0])
+    assert ex.value.code == -8 and time.monotonic() - t0 < 15
+    with pytest.raises(hiprl.RedisError) as ex2:
+        _step(r, steps[1])
+    assert ex2.value.code == -8
+    r.close()
+    o = oracle.Oracle(local_cache=True)
+    o.load_rules(streams.RULES)
+    b = steps[1][0]
+    gs, gt = e.submit(b)
+    es_, et = o.submit(b)
+    streams.assert_same(es_, et, gs, gt, "engine after the stalled router")

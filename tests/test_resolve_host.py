@@ -139,3 +139,105 @@ def test_strings_outside_bytes_resolve_nil(shim):
     rb.entry_first[3] = rb.n_entries + 5          # descriptor 2: entries past n_entries
     got = resolve(shim, cfg, rb)
     assert list(got) == [hiprl.NIL_RULE] * 3
+
+
+# ---- k_resolve's two passes: the level-pipelined walk, then the exact walk for what it leaves ----
+def _resolve2(lib, cfg, rb, mode=0):
+    lib.rls_resolve2.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.POINTER(hiprl.RlResolveBatch),
+                                 C.c_void_p, C.c_void_p, C.c_int]
+    lib.rls_resolve2.restype = C.c_int
+    nodes, names = cfg.tree_arrays()
+    nodes = np.ascontiguousarray(nodes, np.uint32)
+    nb = np.frombuffer(names or b"\0", np.uint8)
+    s = rb.struct()
+    out = np.zeros(max(1, rb.n_desc), np.uint32)
+    ex = np.zeros(max(1, rb.n_desc), np.uint8)
+    rc = lib.rls_resolve2(nodes.ctypes.data, nodes.shape[0], nb.ctypes.data, len(names), C.byref(s), out.ctypes.data,
+                          ex.ctypes.data, mode)
+    assert rc == 0
+    return out[:rb.n_desc], ex[:rb.n_desc].astype(bool)
+
+
+def _colliding(lib, parent, make, count=400_000):
+    """Two distinct names make(i), make(j) with equal tree_hash under parent (a birthday search
+    over the device's 32-bit edge hash)."""
+    lib.rls_tree_hash.argtypes = [C.c_uint32, C.c_char_p, C.c_uint32]
+    lib.rls_tree_hash.restype = C.c_uint32
+    seen = {}
+    for i in range(count):
+        n = make(i).encode()
+        h = lib.rls_tree_hash(parent, n, len(n))
+        if h in seen:
+            return seen[h], i
+        seen[h] = i
+    raise AssertionError("no 32-bit collision found")
+
+
+def _mix(k):
+    """A name part whose every dword varies with k (the fold is a bijection of the last word, so
+    names differing only there never collide)."""
+    return format((k * 0x9E3779B97F4A7C15) % (1 << 64), "x")[:6] + str(k)
+
+
+@pytest.mark.parametrize("seed", [4, 7])
+def test_config4_first_pass_decides_and_agrees(shim, seed):
+    """On a config-4 tree the level-pipelined pass decides (nearly) every descriptor itself, and
+    both passes together give exactly the exact walk's and the oracle's answers."""
+    y = workload.config4_yaml(seed)
+    cfg = rl_config.RateLimitConfig([("c4.yaml", y)])
+    orc = config_oracle.Config([("c4.yaml", y)])
+    descs = workload.config4_descriptors(seed, 3000)
+    rb = rl_config.ResolveBatch([(d, e, None) for d, e in descs])
+    got, ex = _resolve2(shim, cfg, rb)
+    exact, _ = _resolve2(shim, cfg, rb, mode=1)
+    assert np.array_equal(got, exact)
+    assert ex.mean() < 0.01, ex.mean()  # (the batch's last strings end past the blob's last dword)
+    for (d, e), r in zip(descs, got):
+        w = orc.get_limit(d, e)
+        have = None if r == hiprl.NIL_RULE else (cfg.rules[int(r)].requests_per_unit, cfg.rules[int(r)].unit)
+        assert have == (None if w is None else (w.requests_per_unit, w.unit)), (d, e)
+
+
+def test_edge_hash_collisions_take_the_exact_walk(shim):
+    """Sibling names whose 32-bit edge hashes collide: the first pass takes a probe round's first
+    hash match unconfirmed, finds the other name when it confirms the node, and leaves the
+    descriptor to the exact walk; answers equal the oracle's (key/value nodes, key-only nodes, a
+    colliding name absent from the tree, a collision one level down)."""
+    probe = rl_config.RateLimitConfig([("p.yaml", "domain: dc\ndescriptors:\n  - key: a\n    value: x\n")])
+    nodes, _ = probe.tree_arrays()
+    dom = int(np.nonzero(nodes[:, 0] == 0xFFFFFFFF)[0][0])
+    ci, cj = _colliding(shim, dom, lambda k: f"a_{_mix(k)}")
+    cp, cq = _colliding(shim, dom, lambda k: f"k{_mix(k)}")
+    i, j, p, q = _mix(ci), _mix(cj), _mix(cp), _mix(cq)
+    y = (
+        "domain: dc\n"
+        "descriptors:\n"
+        f"  - key: a\n    value: \"{i}\"\n    rate_limit: {{unit: second, requests_per_unit: 3}}\n"
+        f"    descriptors:\n      - key: b\n        rate_limit: {{unit: day, requests_per_unit: 9}}\n"
+        f"  - key: a\n    value: \"{j}\"\n    rate_limit: {{unit: minute, requests_per_unit: 4}}\n"
+        "  - key: a\n    rate_limit: {unit: hour, requests_per_unit: 5}\n"
+        f"  - key: k{p}\n    rate_limit: {{unit: day, requests_per_unit: 6}}\n"
+        f"  - key: k{q}\n    rate_limit: {{unit: second, requests_per_unit: 7}}\n"
+    )
+    y2 = (
+        "domain: dd\n"
+        "descriptors:\n"
+        f"  - key: a\n    value: \"{i}\"\n    rate_limit: {{unit: second, requests_per_unit: 8}}\n"
+        "  - key: a\n    rate_limit: {unit: hour, requests_per_unit: 2}\n"
+    )
+    files_ = [("c.yaml", y), ("d.yaml", y2)]
+    cfg = rl_config.RateLimitConfig(files_)
+    orc = config_oracle.Config(files_)
+    nodes2, _ = cfg.tree_arrays()
+    assert int(np.nonzero(nodes2[:, 0] == 0xFFFFFFFF)[0][0]) == dom  # the hashes were searched under this parent
+    descs = [("dc", [("a", str(i))]), ("dc", [("a", str(j))]), ("dc", [("a", "nope")]), ("dc", [(f"k{p}", "v")]),
+             ("dc", [(f"k{q}", "v")]), ("dc", [("a", str(i)), ("b", "z")]), ("dc", [("a", str(j)), ("b", "z")]),
+             ("dd", [("a", str(j))]), ("dd", [("a", str(i))]), ("dc", [(f"k{q}", "v"), ("b", "z")])]
+    got, ex = _resolve2(shim, cfg, rl_config.ResolveBatch([(d, e, None) for d, e in descs]))
+    exact, _ = _resolve2(shim, cfg, rl_config.ResolveBatch([(d, e, None) for d, e in descs]), mode=1)
+    assert np.array_equal(got, exact)
+    assert ex.any()  # at least one colliding lookup confirmed the wrong node and went to the exact walk
+    for (d, e), r in zip(descs, got):
+        w = orc.get_limit(d, e)
+        have = None if r == hiprl.NIL_RULE else (cfg.rules[int(r)].requests_per_unit, cfg.rules[int(r)].unit)
+        assert have == (None if w is None else (w.requests_per_unit, w.unit)), (d, e)
