@@ -220,8 +220,13 @@ struct rl_engine {
   bool has_tree = false;
   uint8_t* d_res = nullptr;  // rl_resolve staging (grown on demand)
   size_t res_cap = 0;
-  uint32_t* d_res_flags = nullptr;  // k_resolve's per-block flags (grown on demand)
-  uint32_t res_flag_cap = 0;
+  // k_resolve's per-block flags (grown on demand): RES_FLAG_SLOTS sets, one per call in turn, so
+  // a resolve on the front stream never shares its flags with one still running on the engine
+  // stream (a call finds at most RL_MAX_IN_FLIGHT batches, with their resolves, ahead of it)
+  static constexpr uint32_t RES_FLAG_SLOTS = RL_MAX_IN_FLIGHT + 1;
+  uint32_t* d_res_flags = nullptr;
+  uint32_t res_flag_cap = 0;  // words per set
+  uint64_t res_seq = 0;
 
   // multi-GPU router scratch (allocated on first use)
   RRec* r_tmp = nullptr;           // origin: routed records in descriptor order
@@ -871,9 +876,17 @@ int rlx_engine_view(rl_engine* e, EngineView* v) {
   return 0;
 }
 void rlx_engine_hot(rl_engine* e, std::vector<HotKey>& out) { out = e->hot; }
-void rlx_engine_set_lag(rl_engine* e) {
-  e->tab.lag = 1u;
-  e->cfg.flags |= RL_CFG_LAG_WINDOW;
+int rlx_engine_set_lag(rl_engine* e, bool dry) {
+  if (e->tab.lag) return 0;
+  // An engine that already decided batches kept its SECOND regions' occupancy under the
+  // one-generation rule (RegionOcc.prev stays 0 there), so lag mode's capacity check would
+  // under-count live slots: such an engine needs RL_CFG_LAG_WINDOW from rl_create.
+  if (e->st.batches > 0 || e->n_fl) return RL_ESTATE;
+  if (!dry) {
+    e->tab.lag = 1u;
+    e->cfg.flags |= RL_CFG_LAG_WINDOW;
+  }
+  return 0;
 }
 }  // namespace rlhip
 
@@ -1775,18 +1788,19 @@ int rl_resolve_device(rl_engine* e, const rl_resolve_batch* b, uint32_t* d_rule_
   const uint32_t nf = resolve_flag_words(b->n_desc);
   if (nf > e->res_flag_cap) {  // the first batch of a size (then sized for the engine's batches)
     const uint32_t cap = std::max(nf, resolve_flag_words(e->cfg.max_batch_desc));
-    hipError_t fe = hipStreamSynchronize(front ? e->front : e->stream);  // an older resolve may still read them
+    hipError_t fe = hipDeviceSynchronize();  // older resolves may still read them
     if (fe == hipSuccess) {
       hipFree(e->d_res_flags);
       e->d_res_flags = nullptr;
       e->res_flag_cap = 0;
-      fe = hipMalloc(&e->d_res_flags, (size_t)cap * 4);
+      fe = hipMalloc(&e->d_res_flags, (size_t)cap * 4 * rl_engine::RES_FLAG_SLOTS);
     }
     if (fe != hipSuccess) return e->hip_fail(fe, "rl_resolve flags");
     e->res_flag_cap = cap;
   }
+  uint32_t* flags = e->d_res_flags + (size_t)(e->res_seq++ % rl_engine::RES_FLAG_SLOTS) * e->res_flag_cap;
   e->timed(KT_RESOLVE, [&] {
-    launch_resolve(front ? e->front : e->stream, resolve_in(b), e->tree, d_rule_out, e->d_res_flags);
+    launch_resolve(front ? e->front : e->stream, resolve_in(b), e->tree, d_rule_out, flags);
   });
   hipError_t he = hipGetLastError();
   if (he == hipSuccess && front) {

@@ -51,8 +51,9 @@ struct EngineView {
 };
 int rlx_engine_view(rl_engine* e, EngineView* v);
 // A router's engine keeps SECOND key strings findable up to 3 s behind its newest time
-// (TableDesc.lag, rl_common.h slot_free_for). Set by rl_router_create before the router's first step.
-void rlx_engine_set_lag(rl_engine* e);
+// (TableDesc.lag, rl_common.h slot_free_for). Set by rl_router_create once the router exists
+// (dry: only the check); RL_ESTATE for an engine that decided batches without it.
+int rlx_engine_set_lag(rl_engine* e, bool dry);
 // The engine's current hot set (keys it owns that arrive with many descriptors per batch).
 void rlx_engine_hot(rl_engine* e, std::vector<HotKey>& out);
 

@@ -426,9 +426,10 @@ struct rl_router {
     return fail(RL_ECOMM, "%s: %s (communicator aborted)", what, w.c_str());
   }
   void abort_comm() {
+    // (a stalled test kernel ends first: ncclCommAbort waits for the work queued behind it)
+    if (h_stall) __atomic_store_n(h_stall, 1u, __ATOMIC_RELEASE);
     if (xp) xp->abort();
     broken = true;
-    if (h_stall) __atomic_store_n(h_stall, 1u, __ATOMIC_RELEASE);  // (a stalled test kernel ends)
   }
   // Collective transports: the host's wait for work queued behind a collective (an event, or the
   // stream when ev is null). A peer that never reaches the collective (a rank that diverged or
@@ -1521,7 +1522,10 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
   for (uint32_t s = 0; s < n_eng; ++s) {
     r->sh[s].e = engines[s];
     if (rlx_engine_view(engines[s], &r->sh[s].v)) return bail(RL_EINVAL);
-    rlx_engine_set_lag(engines[s]);
+    if (rlx_engine_set_lag(engines[s], true)) {
+      r->err = "an engine that already decided batches needs RL_CFG_LAG_WINDOW at rl_create to serve a router";
+      return bail(RL_ESTATE);
+    }
     if (r->alloc_shard(r->sh[s])) return bail(RL_EHIP);
   }
 #ifndef RL_ROUTER_TWO_STREAMS
@@ -1551,6 +1555,7 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
     }
   }
   if (int rc = r->check_config()) return bail(rc);
+  for (uint32_t s = 0; s < n_eng; ++s) (void)rlx_engine_set_lag(engines[s], false);  // (checked above)
   *out = r;
   return 0;
 }

@@ -131,7 +131,14 @@ typedef struct rl_batch {
   const uint16_t* ttl_jitter;  /* n_desc or NULL (= all 0): seconds added to the EXPIRE of the descriptor's
                                   INCRBY, JitterRand.Int63n(EXPIRATION_JITTER_MAX_SECONDS) drawn by the host in
                                   serial order (fixed_cache_impl.go:69-72); the key lives until its last INCRBY's
-                                  now + divider + jitter. Ignored for nil limits and local-cache hits */
+                                  now + divider + jitter. Ignored for nil limits and local-cache hits.
+                                  Draw order: the reference draws no jitter for a local-cache hit
+                                  (fixed_cache_impl.go:60-72); the device cache's hits are known only
+                                  after the batch, so a host drawing one per descriptor with a limit
+                                  matches the reference's sequence of draws only with the local cache
+                                  off or with HIP_LOCAL_CACHE=freecache (its hits are found on the
+                                  host, before the draws). Each INCRBY's jitter is still one
+                                  independent draw (tests/test_jitter.py pins the current behaviour) */
 } rl_batch;
 
 /* One DescriptorStatus plus its stat increments (20 B). */
@@ -563,7 +570,10 @@ typedef struct rl_resolve_batch {
 int rl_resolve(rl_engine* e, const rl_resolve_batch* batch, uint32_t* rule_out);
 /* Device memory in and out, asynchronous: ordered before the engine's next submit (run on the
  * stream that submit's first kernel uses, so with batches in flight it runs beside their
- * decisions, as the next batch's fingerprint pass does). */
+ * decisions, as the next batch's fingerprint pass does). It is NOT ordered after batches
+ * already in flight: d_rule_out must not be the rule_id array of a batch still in flight
+ * (give each batch in flight its own, as rl_batch inputs are). Two kernels: a level-pipelined
+ * walk, then the exact walk for the descriptors it leaves (rl_resolve.hip). */
 int rl_resolve_device(rl_engine* e, const rl_resolve_batch* device_batch, uint32_t* d_rule_out);
 
 #ifdef __cplusplus

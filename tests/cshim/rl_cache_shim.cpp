@@ -68,7 +68,9 @@ void rlc_next_jitter(int64_t max_seconds, uint64_t seed) {
   g_jitter_seed = seed;
 }
 
-// flags: bit 0 = per-second split (REDIS_PERSECOND), bit 1 = no early answers (HIP_BATCH_ANSWER_EARLY=false)
+// flags: bit 0 = per-second split (REDIS_PERSECOND), bit 1 = no early answers (HIP_BATCH_ANSWER_EARLY=false),
+// bit 2 = batches of at most 4 descriptors (HIP_BATCH_LIMIT=4: with several callers queued, every
+// batch is formed and submitted while the one before it is still in flight)
 void* rlc_create(int local_cache, float near_ratio, int flags, uint32_t window_us) {
   auto* s = new Shim();
   HipSettings hs;
@@ -78,7 +80,7 @@ void* rlc_create(int local_cache, float near_ratio, int flags, uint32_t window_u
   hs.per_second_split = (flags & 1) != 0;
   hs.answer_early = (flags & 2) == 0;
   hs.batch_window_us = window_us;
-  hs.batch_limit = 1u << 14;
+  hs.batch_limit = (flags & 4) ? 4u : 1u << 14;
   try {
     auto c = std::make_unique<HipRateLimitCache>(hs, s->ts);
     s->single = c.get();

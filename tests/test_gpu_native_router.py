@@ -193,3 +193,29 @@ def test_rccl_transport_stall_times_out(monkeypatch):
     gs, gt = e.submit(b)
     es_, et = o.submit(b)
     streams.assert_same(es_, et, gs, gt, "engine after the stalled router")
+
+
+def test_router_refuses_an_engine_that_decided_batches_without_the_lag_window():
+    """a router's engines keep the previous SECOND generation live (lag window); an
+    engine that already decided batches under the one-generation rule would under-count its
+    live slots in lag mode, so rl_router_create refuses it (RL_ESTATE) and leaves it as it was;
+    the same engine created with RL_CFG_LAG_WINDOW serves a router after deciding batches."""
+    for lag in (False, True):
+        e = hiprl.Engine(local_cache=False, max_batch_desc=4000, lag_window=lag)
+        e.load_rules(streams.RULES)
+        b = stream_batches(1, 1, 800, seed=41)[0][0]
+        e.submit(b)
+        if lag:
+            r = hiprl.Router([e], max_desc=4000)
+            r.close()
+            continue
+        with pytest.raises(hiprl.RedisError) as ex:
+            hiprl.Router([e], max_desc=4000)
+        assert ex.value.code == -5  # RL_ESTATE
+        o = oracle.Oracle()
+        o.load_rules(streams.RULES)
+        o.submit(b)
+        b2 = stream_batches(1, 1, 800, seed=42)[0][0]
+        gs, gt = e.submit(b2)
+        es, et = o.submit(b2)
+        streams.assert_same(es, et, gs, gt, "engine after the refused router")

@@ -135,3 +135,30 @@ def test_gpu_mirror_shadow_stats():
     assert sh.Stats.OverLimit.Value() == en.Stats.OverLimit.Value() == 3
     assert sh.Stats.OverLimitWithLocalCache.Value() == en.Stats.OverLimitWithLocalCache.Value() == 2
     assert sh.Stats.NearLimit.Value() == en.Stats.NearLimit.Value()
+
+
+@pytest.mark.gpu
+def test_gpu_mirror_shadow_stats_hits_addend():
+    """Stats.ShadowMode with hits_addend 4. It counts shadowed DECISIONS (+1
+    each, as upstream envoyproxy/ratelimit's GetResponseDescriptorStatus does with
+    `limitInfo.limit.Stats.ShadowMode.Inc()` — upstream is not in /root/reference, so this is
+    parity unpinned), while the over / near / local-cache stats grow by hits as for an enforced
+    rule. L = 10/SECOND, ratio 0.8 (near 8): posts 4, 8 OK; post 12 over (checkOverLimitThreshold,
+    base_limiter.go:129-145: OverLimit += 12 - 10, NearLimit += 10 - max(8, 8)), then a
+    local-cache hit (OverLimit += 4, OverLimitWithLocalCache += 4): ShadowMode 2."""
+    now = [T0]
+    cache = hiprl.HipRateLimitCache(lambda: now[0], local_cache=True)
+    scope = hiprl.StatsStore()
+    sh = hiprl.NewRateLimit(10, hiprl.SECOND, "key_shadow4", scope, shadow_mode=True)
+    en = hiprl.NewRateLimit(10, hiprl.SECOND, "key_enforced4", scope)
+    req = hiprl.NewRateLimitRequest("domain", [[("a", "b")], [("c", "d")]], 4)
+    codes = []
+    for _ in range(4):
+        r = cache.DoLimit(req, [sh, en])
+        codes.append([s.Code for s in r.DescriptorStatuses])
+    assert codes == [[OK, OK]] * 2 + [[OK, OVER]] * 2
+    assert sh.Stats.ShadowMode.Value() == 2 and en.Stats.ShadowMode.Value() == 0
+    assert sh.Stats.OverLimit.Value() == en.Stats.OverLimit.Value() == 2 + 4
+    assert sh.Stats.OverLimitWithLocalCache.Value() == en.Stats.OverLimitWithLocalCache.Value() == 4
+    assert sh.Stats.NearLimit.Value() == en.Stats.NearLimit.Value()
+    assert sh.Stats.TotalHits.Value() == en.Stats.TotalHits.Value() == 16

@@ -1,0 +1,4 @@
+bash tools/gpu_steps.sh r6b \
+ "300:python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_resolve.py tests/test_gpu_configs45_regime.py -k 'config4 or resolve'" \
+ "600:bash tools/ab.sh 30 '- tools/variants/lib_r5.so tools/variants/lib_fw6.so - tools/variants/lib_r5.so tools/variants/lib_fw6.so' --config 4" \
+ "90:python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 tools/rccl_probe.py"
