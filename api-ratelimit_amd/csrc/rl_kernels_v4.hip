@@ -72,7 +72,10 @@ constexpr int R_GTOT = R_BPRE + MSD_BUCKETS;
 constexpr int R_BTOT = R_GTOT + MSD_GROUPS;  // per MSD bucket its batch total (k4_scan block pair hand-off)
 constexpr int RANGE_WORDS = R_BTOT + MSD_BUCKETS;
 constexpr int DONE_CTR = 27;               // EngineCtl::tile_ctr[DONE_CTR][0]: k4_group blocks done
-constexpr int G_NT = 256;
+#ifndef RL_G_NT
+#define RL_G_NT 256
+#endif
+constexpr int G_NT = RL_G_NT;
 constexpr int G_W = G_NT / 64;
 constexpr int G_CAP = RL_G_CAP;    // records grouped in LDS (a larger pair runs bucket by bucket)
 constexpr int G_HASH = RL_G_HASH;  // LDS hash slots (power of two > G_CAP)
@@ -443,7 +446,11 @@ constexpr int SCAN_Q = 32;  // MSD column entries per lane kept in registers (16
 // Hot blocks take 16 buckets each over 64 tile slices (lane = slice % 4 * 16 + bucket, wave =
 // slice / 4): 32 blocks instead of 8, so the hot columns (u16 starts + u64 h sums of every
 // tile) are pulled by 32 CUs, 8 tiles per lane at config 3.
-constexpr int HOT_PER_BLOCK = 16;
+#ifndef RL_HOT_PER_BLOCK
+#define RL_HOT_PER_BLOCK 16
+#endif
+constexpr int HOT_PER_BLOCK = RL_HOT_PER_BLOCK;
+static_assert(HOT_PER_BLOCK >= 4 && HOT_PER_BLOCK <= 16 && (HOT_PER_BLOCK & (HOT_PER_BLOCK - 1)) == 0, "hot buckets per block");
 constexpr int HOT_SCAN_BLOCKS = HOT_BUCKETS / HOT_PER_BLOCK;
 constexpr int HOT_Q = 16;   // hot column entries per lane kept in registers
 static_assert(HOT_BUCKETS % 64 == 0 && MSD_BUCKETS % 64 == 0, "bucket blocks");
@@ -501,7 +508,7 @@ __global__ __launch_bounds__(SCAN_NT) void k4_scan(const uint16_t* __restrict__ 
   ST5(0);
   const bool hotb = blockIdx.x < (uint32_t)HOT_SCAN_BLOCKS;  // block-uniform
   const uint32_t errs = ctl->err;
-  const HotEntry he = hot_list[((blockIdx.x % (uint32_t)HOT_SCAN_BLOCKS) * HOT_PER_BLOCK + (lane & 15u)) >> 1];
+  const HotEntry he = hot_list[((blockIdx.x % (uint32_t)HOT_SCAN_BLOCKS) * HOT_PER_BLOCK + (lane & (HOT_PER_BLOCK - 1u))) >> 1];
   RegionOcc oc[8];
 #pragma unroll
   for (int r = 0; r < 8; ++r) oc[r] = occ[r];

@@ -34,7 +34,7 @@ struct TreeDesc2 {
   const uint64_t* slots;  // (parent, name) edge table: hash << 32 | node id, or ~0; mask + TREE_PROBE entries
                           // (the first TREE_PROBE - 1 repeated at the end, so a probe round never wraps)
   const uint8_t* names;
-  uint32_t mask;          // power-of-two table size - 1 (load <= 1/4)
+  uint32_t mask;          // power-of-two table size - 1 (load <= 1/8)
 };
 
 struct ResolveIn {

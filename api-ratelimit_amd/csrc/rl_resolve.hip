@@ -13,7 +13,7 @@
 //
 // Device layout: the tree's nodes (64 B each: parent, name length, rule, child count, name
 // hash and the name's first 32 bytes) and an open-addressing table over (parent, name) edges
-// (hash << 32 | node id, load <= 1/4), both small enough to stay in L2. Names are compared
+// (hash << 32 | node id, load <= 1/8), both small enough to stay in L2. Names are compared
 // byte-exactly after the hash matches, so ("a_b") and ("a", "b") resolve exactly as the
 // reference's string maps do. One thread per descriptor. A level of the walk loads the key and
 // the value as whole dwords into registers (one round trip), folds them, reads both edges'
@@ -307,10 +307,11 @@ RL_HD uint32_t resolve_one(const ResolveIn& in, const TreeDesc2& t, uint32_t i) 
 // words two levels ahead and its strings one level ahead, hashes both names from registers,
 // takes a probe round's first hash match unconfirmed and confirms it one level later, beside
 // the next level's probe rounds: one round trip per level, plus one for the last node.
-//   * A probe round without a hash match that reaches an empty slot settles a miss exactly
-//     (equal names hash equally). A match whose node turns out to carry another name, a probe
-//     chain longer than one round, and any string the register path cannot hold (over 32 bytes,
-//     an unaligned blob, a last dword past the blob) leave the descriptor to the exact walk.
+//   * A probe chain without a hash match settles a miss exactly (equal names hash equally); a
+//     chain longer than the first round is read on slot by slot (rare at load <= 1/8). A match
+//     whose node turns out to carry another name, and any string the register path cannot hold
+//     (over 16 bytes, an unaligned blob, a load window past the blob's end) leave the descriptor
+//     to the exact walk (k_resolve_exact).
 //   * No child count check: the reference stops at a node without children (config_impl.go
 //     :320-325); this walk goes on and looks the next entry up under that node, which no edge
 //     has as parent, so it misses and stops there with the same (nil) result.
@@ -324,28 +325,25 @@ constexpr int FW = RL_RESOLVE_FW;
 constexpr uint32_t FB = 4 * FW;
 static_assert(FW >= 1 && FW <= SW, "first-pass name words");
 
-// true when some lane of the wave still needs the value (device); the thread's own test (host)
-RL_HD inline bool any_lane(bool p) {
-#ifdef __HIP_DEVICE_COMPILE__
-  return __ballot(p) != 0ull;
-#else
-  return p;
-#endif
-}
-// load_str for FW dwords, loading only the dwords some lane of the wave needs (config-4 keys
-// are one dword, values one to three): nd dwords at clamped indices, all in flight together.
+// load_str for FW dwords: the FW + 1 dwords from the string's first, unconditional and not
+// clamped, all in flight together. The caller checks they lie inside the blob (FWB bytes from
+// the string's aligned start). A load behind a condition — even a wave-uniform one, or a
+// clamped index the compiler turns into one — made it wait for every load before it: 141 us
+// for this pass at config 4 against 96 for the old walk.
+constexpr uint32_t FWB = 4 * (FW + 1);
 RL_HD void load_str_w(const uint8_t* bytes, uint32_t off, uint32_t len, uint32_t (&s)[FW]) {
+  const uint32_t sh = off & 3u;
   const uint32_t* w = reinterpret_cast<const uint32_t*>(bytes) + (off >> 2);
-  const uint32_t sh = off & 3u, nd = len ? (sh + len + 3u) >> 2 : 0u;
-  const uint32_t last = nd ? nd - 1u : 0u;
   uint32_t d[FW + 1];
 #pragma unroll
-  for (int k = 0; k <= FW; ++k) d[k] = any_lane((uint32_t)k < nd) && nd ? w[min((uint32_t)k, last)] : 0u;
+  for (int k = 0; k <= FW; ++k) d[k] = w[k];
+  // branch-free from the loads on (a use behind a condition lets the compiler sink its load
+  // into the branch, and the branch then waits for every load before it)
 #pragma unroll
   for (int k = 0; k < FW; ++k) {
-    const uint32_t v = align_byte(d[k + 1], d[k], sh);
-    const uint32_t b0 = 4u * (uint32_t)k;
-    s[k] = b0 >= len ? 0u : b0 + 4u <= len ? v : v & ((1u << (8u * (len - b0))) - 1u);
+    const int32_t rem = (int32_t)len - 4 * k;
+    const uint32_t nb = rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem;
+    s[k] = align_byte(d[k + 1], d[k], sh) & (uint32_t)((1ull << (8u * nb)) - 1ull);
   }
 }
 RL_HD uint32_t fold_w(const uint32_t (&s)[FW], uint32_t len) {  // = fold_reg for len <= FB
@@ -382,15 +380,23 @@ struct NodeW {
   uint32_t parent, len, rule, name[FW];
 };
 RL_HD NodeW load_node_w(const TreeDesc2& t, uint32_t id) {
+  static_assert(FW % 4 == 0, "whole 16-B name loads");
   const uint4* p = reinterpret_cast<const uint4*>(t.nodes + id);
   const uint4 h = p[0];
+  uint4 nm[FW / 4];
+#pragma unroll
+  for (int k = 0; k < FW / 4; ++k) nm[k] = p[2 + k];
   NodeW v;
   v.parent = h.x;
   v.len = h.y;
   v.rule = h.z;
-  const uint32_t* nm = reinterpret_cast<const uint32_t*>(p + 2);
 #pragma unroll
-  for (int k = 0; k < FW; ++k) v.name[k] = nm[k];
+  for (int k = 0; k < FW / 4; ++k) {
+    v.name[4 * k] = nm[k].x;
+    v.name[4 * k + 1] = nm[k].y;
+    v.name[4 * k + 2] = nm[k].z;
+    v.name[4 * k + 3] = nm[k].w;
+  }
   return v;
 }
 // the node against (parent, len, the first len bytes of q): q may hold more bytes past len (a
@@ -405,11 +411,28 @@ RL_HD bool confirm(const NodeW& nd, uint32_t parent, uint32_t len, const uint32_
   }
   return diff == 0;
 }
+// first_match, and when the round neither matches nor ends (a probe chain longer than one round:
+// rare at load <= 1/8), the rest of the chain slot by slot: a miss is then settled exactly here
+// instead of sending the descriptor to the exact walk.
+RL_HD uint32_t match_chain(const TreeDesc2& t, uint32_t h, const uint64_t (&w)[TREE_PROBE]) {
+  bool done;
+  const uint32_t c = first_match(w, h, done);
+  if (c != TREE_NONE || done) return c;
+  uint32_t s = (h + TREE_PROBE) & t.mask;
+  for (uint32_t probes = TREE_PROBE; probes <= t.mask; ++probes, s = (s + 1) & t.mask) {
+    const uint64_t x = t.slots[s];
+    if ((uint32_t)x == TREE_EMPTY) break;
+    if ((uint32_t)(x >> 32) == h) return (uint32_t)x;
+  }
+  return TREE_NONE;
+}
 RL_HD uint4 load_entry(const ResolveIn& in, uint32_t e) {
   return make_uint4(in.entry[4 * e], in.entry[4 * e + 1], in.entry[4 * e + 2], in.entry[4 * e + 3]);
 }
 
 // rule id of descriptor i (exact), or RS_EXACT: the exact walk (resolve_one) decides it.
+// Every load is unconditional (entries at clamped indices; ENT: the batch has entries at all).
+template <bool ENT>
 RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, uint32_t i) {
   const uint32_t doff = in.domain[2 * i], dlen = in.domain[2 * i + 1];
   const uint32_t e0 = in.entry_first[i], e1 = in.entry_first[i + 1];
@@ -418,17 +441,22 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, uint32_t i)
   if (!(e0 <= e1 && e1 <= in.n_entries) || (uint64_t)doff + dlen > blen) return RL_NIL_RULE;  // as resolve_one
   const bool aligned = (reinterpret_cast<uintptr_t>(in.bytes) & 3u) == 0;
   const uint64_t bwords = blen & ~3ull;
-  auto reg_ok = [&](uint32_t o, uint32_t l) { return aligned && l <= FB && (((uint64_t)o + l + 3u) & ~3ull) <= bwords; };
+  // the register path: a 4-B aligned blob, <= FB bytes, the FWB bytes load_str_w reads inside it
+  auto reg_ok = [&](uint32_t o, uint32_t l) { return aligned && l <= FB && (uint64_t)(o & ~3u) + FWB <= blen; };
   auto inside = [&](uint32_t o, uint32_t l) { return (uint64_t)o + l <= blen; };
   auto str_ok = [&](const uint4& x) { return reg_ok(x.x, x.y) && reg_ok(x.z, x.w) && x.y + 1u + x.w <= FB; };
   auto str_in = [&](const uint4& x) { return inside(x.x, x.y) && inside(x.z, x.w); };
-  if (!reg_ok(doff, dlen)) return RS_EXACT;
+  if (!reg_ok(doff, dlen) || blen < FWB) return RS_EXACT;  // (so a skipped string may read offset 0)
   const uint32_t n = e1 - e0;
+  const uint32_t elast = ENT ? in.n_entries - 1u : 0u;
+  auto entry_at = [&](uint32_t e) {  // entry e (clamped: read always, used only when e < e1)
+    return ENT ? load_entry(in, min(e, elast)) : make_uint4(0, 0, 0, 0);
+  };
   // round trip 1: the domain's dwords and the first two entries' words
   uint32_t Q[FW];  // the name to confirm: the domain, then key ["_" value] of a level
   load_str_w(in.bytes, doff, dlen, Q);
-  uint4 E = n > 0 ? load_entry(in, e0) : make_uint4(0, 0, 0, 0);
-  uint4 En = n > 1 ? load_entry(in, e0 + 1) : make_uint4(0, 0, 0, 0);
+  uint4 E = entry_at(e0);
+  uint4 En = entry_at(e0 + 1);
   const uint32_t hd = tree_hash(RL_TREE_ROOT, fold_w(Q, dlen), dlen);
   // round trip 2: the domain's probe round and level 0's strings
   uint64_t w[TREE_PROBE];
@@ -439,9 +467,8 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, uint32_t i)
     load_str_w(in.bytes, ld ? E.x : 0u, ld ? E.y : 0u, K);
     load_str_w(in.bytes, ld ? E.z : 0u, ld ? E.w : 0u, V);
   }
-  bool dn;
-  uint32_t pend = first_match(w, hd, dn);  // the node to confirm (parent pp, name Q[0, pl))
-  if (pend == TREE_NONE) return dn ? RL_NIL_RULE : RS_EXACT;  // unknown domain (:279-284)
+  uint32_t pend = match_chain(t, hd, w);  // the node to confirm (parent pp, name Q[0, pl))
+  if (pend == TREE_NONE) return RL_NIL_RULE;  // unknown domain (:279-284)
   uint32_t pp = RL_TREE_ROOT, pl = dlen;
   if (ov != RL_NIL_RULE || n == 0) {  // override (:286-296), or no entries: the domain alone decides
     if (!confirm(load_node_w(t, pend), pp, pl, Q)) return RS_EXACT;
@@ -466,19 +493,16 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, uint32_t i)
       load_str_w(in.bytes, ld ? En.x : 0u, ld ? En.y : 0u, K);
       load_str_w(in.bytes, ld ? En.z : 0u, ld ? En.w : 0u, V);
     }
-    const uint4 Enn = l + 2 < n ? load_entry(in, e0 + l + 2) : make_uint4(0, 0, 0, 0);
+    const uint4 Enn = entry_at(e0 + l + 2);
     if (!confirm(pv, pp, pl, Q)) return RS_EXACT;
-    bool dv, dk;
-    const uint32_t cv = first_match(wv, hv, dv);
+    const uint32_t cv = match_chain(t, hv, wv);
     uint32_t nd;
     if (cv != TREE_NONE) {
       nd = cv;
       pl = lv;
-    } else if (!dv) {
-      return RS_EXACT;
     } else {
-      const uint32_t ck = first_match(wk, hk, dk);
-      if (ck == TREE_NONE) return dk ? RL_NIL_RULE : RS_EXACT;  // neither edge: the walk stops (:309), nil
+      const uint32_t ck = match_chain(t, hk, wk);
+      if (ck == TREE_NONE) return RL_NIL_RULE;  // neither edge: the walk stops (:309), nil
       nd = ck;
       pl = kl;
     }
@@ -501,14 +525,14 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, uint32_t i)
 __global__ __launch_bounds__(RS_NT) void k_resolve(ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out,
                                                   uint32_t* __restrict__ flags) {
   const uint32_t i = blockIdx.x * RS_NT + threadIdx.x;
-  const uint32_t r = i < in.n_desc ? resolve_fast(in, t, i) : 0u;
+  const uint32_t r = i >= in.n_desc ? 0u : in.n_entries ? resolve_fast<true>(in, t, i) : resolve_fast<false>(in, t, i);
   if (i < in.n_desc) rule_out[i] = r;
   const int any = __syncthreads_or(r == RS_EXACT);
   if (threadIdx.x == 0) flags[blockIdx.x] = (uint32_t)any;
 }
 // Second pass: blocks stride over the first pass's flags; a flagged block's descriptors left
 // to the exact walk take it.
-constexpr uint32_t RS_EXACT_BLOCKS = 256;
+constexpr uint32_t RS_EXACT_BLOCKS = 2048;  // (a tree of long names leaves every descriptor here)
 __global__ __launch_bounds__(RS_NT) void k_resolve_exact(ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out,
                                                         const uint32_t* __restrict__ flags, uint32_t nblk) {
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
@@ -524,7 +548,7 @@ __global__ __launch_bounds__(RS_NT) void k_resolve_exact(ResolveIn in, TreeDesc2
 // device code path checked against the config oracle without a GPU): the first pass, then the
 // exact walk for what it leaves. *exact (optional) tells which pass decided.
 uint32_t resolve_one_host(const ResolveIn& in, const TreeDesc2& t, uint32_t i, bool* exact) {
-  const uint32_t r = resolve_fast(in, t, i);
+  const uint32_t r = in.n_entries ? resolve_fast<true>(in, t, i) : resolve_fast<false>(in, t, i);
   if (exact) *exact = r == RS_EXACT;
   return r == RS_EXACT ? resolve_one(in, t, i) : r;
 }
@@ -536,7 +560,7 @@ int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint
                std::string& err) {
   out_nodes.assign(n, TreeNodeDev{});
   uint32_t cap = 16;
-  while (cap < 4u * n) cap <<= 1;  // load <= 1/4: a miss ends inside its first probe round
+  while (cap < 8u * n) cap <<= 1;  // load <= 1/8: a probe chain rarely passes its first round
   out_slots.assign(cap + TREE_PROBE - 1, ~0ull);
   mask = cap - 1;
   for (uint32_t i = 0; i < n; ++i) {

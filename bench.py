@@ -60,7 +60,8 @@ def _router():
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 T0 = 1_700_000_020      # not minute-aligned: SECOND / MINUTE / HOUR keys in their own home regions
-PMC_SUMMARY = ROOT / "profiles" / "r05_pmc_traffic.json"
+PMC_SUMMARIES = {3: ROOT / "profiles" / "r06_pmc_traffic.json", 4: ROOT / "profiles" / "r06_pmc_traffic_config4.json",
+                 5: ROOT / "profiles" / "r06_pmc_traffic_config5.json"}
 SOURCES = sorted((ROOT / "api-ratelimit_amd" / "csrc").glob("*.h*")) + sorted(
     (ROOT / "api-ratelimit_amd" / "csrc").glob("*.cpp")) + [ROOT / "include" / "rl_hip.h"]
 
@@ -350,10 +351,11 @@ def random_access_roofline(eng, alg_bytes, U, pipe_ms, step_ms):
 
 
 def pmc_traffic(dom: str, config: int):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc summary,
-    only if it was measured on these exact kernel sources and this workload (tools/pmc_round.sh
-    profiles the default bench: config 3)."""
-    if not PMC_SUMMARY.exists():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 --pmc summary of
+    this workload (tools/pmc_round.sh <tag> <steps> "" <config>), only if it was measured on these
+    exact kernel sources."""
+    PMC_SUMMARY = PMC_SUMMARIES.get(config)
+    if PMC_SUMMARY is None or not PMC_SUMMARY.exists():
         return None, "no PMC summary committed", None
     try:
         pm = json.loads(PMC_SUMMARY.read_text())
@@ -921,11 +923,18 @@ def main():
     alg_def = ("achieved = algorithmic bytes of one batch (SURVEY §8d: prefixes + 12 B/desc + 16 B/req + 20 B/desc out "
                "+ 64 B per unique key) / the dominant kernel's average launch time (HIP events on the engine stream, "
                "kernels unoverlapped)")
+    kernel_alg = {}  # a kernel whose work is not the whole §8d batch: its own algorithmic bytes
     if args.config == 4 and not routed:
         # + the resolve step's inputs and output (the reference's descriptor entries): domain (off, len)
         # 8 B, entry_first 4 B, 4 entries x 16 B, the rule id written 4 B per descriptor
         alg_bytes += 80 * d
         alg_def += "; config 4: + 80 B/desc of rl_resolve_batch inputs and rule-id output (resolved in the step)"
+        # k_resolve reads the strings (the descriptors' prefix bytes) and the 80 B/desc above, nothing
+        # of the decision's bytes (priced at its own work, config_impl.go:274-323)
+        for kname in ("k_resolve", "k_resolve_exact"):
+            kernel_alg[kname] = nbytes + 80 * d
+        alg_def += ("; a dominant k_resolve is priced at its own bytes: the prefix bytes it walks + 80 B/desc, "
+                    "the k4_* kernels at the batch's §8d bytes without the resolve's 80 B/desc")
     if routed and rstats is not None:
         # an owner's launch decides the records it received, not a whole batch: price it at those
         # (32-B record in, 8-B raw reply out per record, 64 B per unique key of the owner batch)
@@ -941,9 +950,11 @@ def main():
         dom = max((k for k in per_batch_ms if k != "memset"), key=lambda k: per_batch_ms[k])
         dom_us = kernel[dom]["total_ms"] * 1e3 / kernel[dom]["launches"]
         # The dominant kernel priced at the batch's algorithmic bytes (SURVEY §8d's per-descriptor
-        # figure x the descriptors one launch processes): every kernel of a batch handles all of
-        # its descriptors, so each launch is held to the whole batch's bytes.
-        achieved = alg_bytes / (dom_us * 1e-6) / 1e9
+        # figure x the descriptors one launch processes): every decision kernel of a batch handles
+        # all of its descriptors, so each launch is held to the whole batch's bytes (config 4:
+        # without the resolve's; k_resolve at its own, kernel_alg).
+        dom_bytes = kernel_alg.get(dom, alg_bytes - (80 * d if kernel_alg else 0))
+        achieved = dom_bytes / (dom_us * 1e-6) / 1e9
         # (the PMC summary profiles the unrouted step: no counter figure for an owner batch)
         traffic, tsrc, traffic_batch = pmc_traffic(dom, args.config) if not routed else (None, None, None)
         roofline = {
@@ -953,6 +964,7 @@ def main():
             "traffic_per_batch": traffic_batch,
             "traffic_over_algorithmic": round(traffic_batch / alg_bytes, 3) if traffic_batch else None,
             "algorithmic_bytes_per_batch": alg_bytes, "unique_keys_per_batch": int(U),
+            "dominant_kernel_algorithmic_bytes": dom_bytes,
             "dominant_kernel_avg_us": round(dom_us, 2),
             "pipeline_us_per_batch": round(pipe_ms * 1e3, 2),
             "pipeline_achieved_GBps": round(alg_bytes / (pipe_ms * 1e-3) / 1e9, 1),

@@ -191,7 +191,9 @@ def test_config4_first_pass_decides_and_agrees(shim, seed):
     got, ex = _resolve2(shim, cfg, rb)
     exact, _ = _resolve2(shim, cfg, rb, mode=1)
     assert np.array_equal(got, exact)
-    assert ex.mean() < 0.01, ex.mean()  # (the batch's last strings end past the blob's last dword)
+    # (strings whose 20-B load window passes the blob end take the exact walk: this batch dedupes its
+    # strings into a small blob, so a few percent of lookups sit there)
+    assert ex.mean() < 0.05, ex.mean()
     for (d, e), r in zip(descs, got):
         w = orc.get_limit(d, e)
         have = None if r == hiprl.NIL_RULE else (cfg.rules[int(r)].requests_per_unit, cfg.rules[int(r)].unit)

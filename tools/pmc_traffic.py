@@ -1,6 +1,6 @@
 """Per-kernel HBM traffic from rocprofv3 --pmc passes (tools/pmc_round.sh output).
 
-usage: pmc_traffic.py <pmc dir> <out.json> <timed steps> [tag]
+usage: pmc_traffic.py <pmc dir> <out.json> <timed steps> [tag] [bench config]
 
 Only the last <timed steps> dispatches of each kernel are used: the bench's timed region
 (prefill and warmup dispatches run at other table fills and are skipped). FETCH_SIZE and
@@ -20,6 +20,7 @@ import sys
 
 root, out, steps = sys.argv[1], sys.argv[2], int(sys.argv[3])
 tag = sys.argv[4] if len(sys.argv) > 4 else ""
+config = int(sys.argv[5]) if len(sys.argv) > 5 else 3
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from bench import source_sha  # noqa: E402
 
@@ -66,7 +67,7 @@ for k, c in cal_rows.items():
     cal[k] = {"fetch_size_bytes_per_op": round(f / U, 2), "write_size_bytes_per_op": round(w / U, 2)}
 cal["note"] = ("k_probe_read: one random 16-B load per op inside a 32-B slot; k_rmw: random 32-B slot "
                "load + store per op (two 16-B lanes); U = 230000 ops per launch on 2^28 slots")
-res = {"tag": tag, "source_sha": source_sha(), "timed_steps": steps,
+res = {"tag": tag, "source_sha": source_sha(), "config": config, "timed_steps": steps,
        "hbm_bytes_per_batch": sum(v["hbm_bytes_per_launch"] for v in kernels.values() if v["dispatches_seen"] >= steps),
        "definition": "hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (MI355X_MICROARCH.md gfx950 FETCH_SIZE "
                      "correction), mean over the last timed_steps dispatches of each kernel",
