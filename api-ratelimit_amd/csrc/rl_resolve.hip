@@ -522,7 +522,9 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, uint32_t i)
 
 // First pass: one thread per descriptor; a block with a descriptor left to the exact walk
 // raises its flag (every block writes its flag, so nothing needs clearing between batches).
-__global__ __launch_bounds__(RS_NT) void k_resolve(ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out,
+// 6 waves per SIMD: 79 VGPRs and no spill (5 waves at the compiler's own 84); 7 or 8 spill
+__global__ __launch_bounds__(RS_NT) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_resolve(
+    ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out,
                                                   uint32_t* __restrict__ flags) {
   const uint32_t i = blockIdx.x * RS_NT + threadIdx.x;
   const uint32_t r = i >= in.n_desc ? 0u : in.n_entries ? resolve_fast<true>(in, t, i) : resolve_fast<false>(in, t, i);

@@ -952,6 +952,16 @@ int rl_router::submit_coll(uint32_t k) {
   const double t1 = now_us();
   he = hipEventRecord(slot[k].ev_rec, rs);
   slot[k].rec_rec = he == hipSuccess;
+#ifndef RL_ROUTER_OWNER_FIRST
+  // The older steps' unpacks go out before this step's owner batch: they follow the records on
+  // the origin stream, which carries the step's critical chain (pack, exchanges, unpack), while
+  // the owner's kernels wait for the records on the engine's streams anyway; launching the owner
+  // batch first held the unpack back by its launch calls (~10 us of host time).
+  for (uint64_t q = done; q + 1 < seq; ++q) {
+    const uint32_t kq = (uint32_t)(q % NSLOT);
+    if (slot[kq].replied && !slot[kq].unpacked) unpack_coll(kq);
+  }
+#endif
   if (fault(PH_RECORDS, 0)) he = hipErrorUnknown;
   if (he != hipSuccess) {  // keep going: the failure travels in the reply exchange
     t.rc_local = RL_EHIP;
@@ -973,10 +983,12 @@ int rl_router::submit_coll(uint32_t k) {
       }
     }
   }
+#ifdef RL_ROUTER_OWNER_FIRST
   for (uint64_t q = done; q + 1 < seq; ++q) {
     const uint32_t kq = (uint32_t)(q % NSLOT);
     if (slot[kq].replied && !slot[kq].unpacked) unpack_coll(kq);
   }
+#endif
   st.exchange_us = now_us() - t1;
   return 0;
 }
