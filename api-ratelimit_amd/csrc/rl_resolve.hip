@@ -99,8 +99,14 @@ RL_HD uint32_t find_bytes(const TreeDesc2& t, uint32_t parent, uint32_t h, const
 // ---- the register path ----
 // bytes sh.. of the pair hi:lo (v_alignbyte_b32)
 RL_HD inline uint32_t align_byte(uint32_t hi, uint32_t lo, uint32_t sh) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);  // one VALU op (the host form below is the same value)
+#else
   return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
+#endif
 }
+// the low n bytes of a word (n <= 4): one shift and a select
+RL_HD inline uint32_t low_bytes_mask(uint32_t n) { return n ? 0xFFFFFFFFu >> (32u - 8u * n) : 0u; }
 // s[k] = bytes 4k..4k+3 of the string at bytes + off (little-endian), zero past len (<= SB).
 // The blob is 4-B aligned and the string's last dword lies inside it (checked by the caller):
 // whole-dword loads at clamped indices, all in flight together.
@@ -343,7 +349,7 @@ RL_HD void load_str_w(const uint8_t* bytes, uint32_t off, uint32_t len, uint32_t
   for (int k = 0; k < FW; ++k) {
     const int32_t rem = (int32_t)len - 4 * k;
     const uint32_t nb = rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem;
-    s[k] = align_byte(d[k + 1], d[k], sh) & (uint32_t)((1ull << (8u * nb)) - 1ull);
+    s[k] = align_byte(d[k + 1], d[k], sh) & low_bytes_mask(nb);
   }
 }
 RL_HD uint32_t fold_w(const uint32_t (&s)[FW], uint32_t len) {  // = fold_reg for len <= FB
@@ -405,9 +411,9 @@ RL_HD bool confirm(const NodeW& nd, uint32_t parent, uint32_t len, const uint32_
   uint32_t diff = (nd.parent ^ parent) | (nd.len ^ len);
 #pragma unroll
   for (int k = 0; k < FW; ++k) {
-    const uint32_t b0 = 4u * (uint32_t)k;
-    const uint32_t m = b0 >= len ? 0u : b0 + 4u <= len ? 0xFFFFFFFFu : (1u << (8u * (len - b0))) - 1u;
-    diff |= nd.name[k] ^ (q[k] & m);
+    const int32_t rem = (int32_t)len - 4 * k;
+    const uint32_t nb = rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem;
+    diff |= nd.name[k] ^ (q[k] & low_bytes_mask(nb));
   }
   return diff == 0;
 }
@@ -520,12 +526,14 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, uint32_t i)
   return v.rule;
 }
 
-// First pass: one thread per descriptor; a block with a descriptor left to the exact walk
-// raises its flag (every block writes its flag, so nothing needs clearing between batches).
-// 6 waves per SIMD: 79 VGPRs and no spill (5 waves at the compiler's own 84); 7 or 8 spill
+// First pass: one thread per descriptor; a block with a descriptor left to the exact walk raises
+// its flag (every block writes its flag, so nothing needs clearing between batches). 6 waves per
+// SIMD: 79 VGPRs and no spill (5 waves at the compiler's own 84; 7 or 8 spill). Measured and not
+// kept (config 4, one box): a persistent grid of 1024 / 512 blocks striding over the chunks, so
+// the pass leaves CUs to the engine stream's kernels: k_resolve 90 -> 95 / 113 us, the step
+// slower; the engine stream at a higher priority than the front stream: no change.
 __global__ __launch_bounds__(RS_NT) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_resolve(
-    ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out,
-                                                  uint32_t* __restrict__ flags) {
+    ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out, uint32_t* __restrict__ flags) {
   const uint32_t i = blockIdx.x * RS_NT + threadIdx.x;
   const uint32_t r = i >= in.n_desc ? 0u : in.n_entries ? resolve_fast<true>(in, t, i) : resolve_fast<false>(in, t, i);
   if (i < in.n_desc) rule_out[i] = r;

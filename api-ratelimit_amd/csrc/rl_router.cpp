@@ -186,6 +186,59 @@ struct EmuWorld {
 };
 constexpr uint64_t EMU_MAGIC = 0x444c524f57554d45ull;  // "EMUWORLD"
 
+// Host exchange (RL_ROUTER_HOST_XCHG, tests): each collective drains the stream, copies the send
+// sections to host memory (compact), calls the caller's all-to-all-v of host bytes, and copies
+// the received sections to their device displacements. The collective transport's code runs
+// unchanged with one process per rank.
+struct HostXchgXport : Xport {
+  rl_host_xchg_fn fn = nullptr;
+  void* ctx = nullptr;
+  uint32_t G = 0;
+  bool failed = false;
+  std::vector<uint8_t> hs, hr;
+  ncclResult_t a2av(const void* s, const size_t* sc, const size_t* sd, void* r, const size_t* rc, const size_t* rd,
+                    hipStream_t st) override {
+    if (failed) return ncclRemoteError;
+    size_t cs[MAXS], ds[MAXS], cr[MAXS], dr[MAXS], ns = 0, nr = 0;
+    for (uint32_t j = 0; j < G; ++j) {
+      cs[j] = sc[j], ds[j] = ns, ns += sc[j];
+      cr[j] = rc[j], dr[j] = nr, nr += rc[j];
+    }
+    hs.resize(std::max<size_t>(ns, 1));
+    hr.resize(std::max<size_t>(nr, 1));
+    hipError_t he = hipStreamSynchronize(st);
+    for (uint32_t j = 0; j < G && he == hipSuccess; ++j)
+      if (cs[j]) he = hipMemcpy(hs.data() + ds[j], static_cast<const uint8_t*>(s) + sd[j], cs[j], hipMemcpyDeviceToHost);
+    if (he != hipSuccess || fn(ctx, hs.data(), cs, ds, hr.data(), cr, dr) != 0) {
+      failed = true;
+      return he != hipSuccess ? ncclUnhandledCudaError : ncclRemoteError;
+    }
+    for (uint32_t j = 0; j < G && he == hipSuccess; ++j)
+      if (cr[j]) he = hipMemcpyAsync(static_cast<uint8_t*>(r) + rd[j], hr.data() + dr[j], cr[j], hipMemcpyHostToDevice, st);
+    if (he == hipSuccess) he = hipStreamSynchronize(st);  // (hr is reused by the next collective)
+    if (he != hipSuccess) {
+      failed = true;
+      return ncclUnhandledCudaError;
+    }
+    return ncclSuccess;
+  }
+  ncclResult_t a2a(const void* s, void* r, size_t n, hipStream_t st) override {
+    size_t c[MAXS], d[MAXS];
+    for (uint32_t j = 0; j < G; ++j) c[j] = n, d[j] = j * n;
+    return a2av(s, c, d, r, c, d, st);
+  }
+  ncclResult_t allgather(const void* s, void* r, size_t n, hipStream_t st) override {
+    size_t c[MAXS], z[MAXS], d[MAXS];
+    for (uint32_t j = 0; j < G; ++j) c[j] = n, z[j] = 0, d[j] = j * n;
+    return a2av(s, c, z, r, c, d, st);
+  }
+  void abort() override { failed = true; }
+  ncclResult_t async_error() override { return failed ? ncclRemoteError : ncclSuccess; }
+  std::string why(ncclResult_t r) override { return std::string("host exchange: ") + ncclGetErrorString(r); }
+};
+thread_local rl_host_xchg_fn t_xchg_fn = nullptr;
+thread_local void* t_xchg_ctx = nullptr;
+
 struct EmuXport : Xport {
   EmuWorld* w = nullptr;
   uint32_t me = 0;
@@ -1443,16 +1496,25 @@ int rl_router_emu_world(uint32_t n_ranks, uint8_t* id_out) {
   return 0;
 }
 
+int rl_router_use_host_xchg(rl_host_xchg_fn fn, void* ctx) {
+  t_xchg_fn = fn;
+  t_xchg_ctx = ctx;
+  return 0;
+}
+
 int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_router** out) {
   if (!cfg || !engines || !out) return RL_EINVAL;
   *out = nullptr;
   if (cfg->struct_size != sizeof(rl_router_config)) return RL_EINVAL;
   const uint32_t G = cfg->n_shards;
   if (G == 0 || G > MAXS || cfg->max_desc == 0 || cfg->max_desc > (1u << 27)) return RL_EINVAL;
-  if (cfg->flags & ~(uint32_t)(RL_ROUTER_NO_COMBINE | RL_ROUTER_HOST | RL_ROUTER_EMULATED)) return RL_EINVAL;
+  if (cfg->flags & ~(uint32_t)(RL_ROUTER_NO_COMBINE | RL_ROUTER_HOST | RL_ROUTER_EMULATED | RL_ROUTER_HOST_XCHG))
+    return RL_EINVAL;
   const bool emu = (cfg->flags & RL_ROUTER_EMULATED) != 0;
-  const bool coll = cfg->rccl_id != nullptr;
-  if (emu && !coll) return RL_EINVAL;
+  const bool hx = (cfg->flags & RL_ROUTER_HOST_XCHG) != 0;
+  const bool coll = cfg->rccl_id != nullptr || hx;
+  if (emu && (!cfg->rccl_id || hx)) return RL_EINVAL;
+  if (hx && !t_xchg_fn) return RL_EINVAL;
   if (coll && cfg->rank >= G) return RL_EINVAL;
   EmuWorld* world = nullptr;
   if (emu) {
@@ -1555,7 +1617,13 @@ int rl_router_create(const rl_router_config* cfg, rl_engine* const* engines, rl_
         hipHostMalloc(&r->h_ag, sizeof(AgEntry) * HOT_MAX * (G + 1), hipHostMallocDefault) != hipSuccess ||
         hipMalloc(&r->d_ok, 4 * MAXS) != hipSuccess || hipMemset(r->d_ok, 0, 4 * MAXS) != hipSuccess)
       return bail(RL_EHIP);
-    if (!emu) {
+    if (hx) {
+      auto* xx = new HostXchgXport();
+      xx->fn = t_xchg_fn;
+      xx->ctx = t_xchg_ctx;
+      xx->G = G;
+      r->xp.reset(xx);
+    } else if (!emu) {
       auto* rx = new RcclXport();
       r->xp.reset(rx);
       ncclUniqueId id;

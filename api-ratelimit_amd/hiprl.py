@@ -41,7 +41,7 @@ STATUS_DTYPE = np.dtype([("code_flags", "<u4"), ("limit_remaining", "<u4"), ("re
 
 PIPELINE_FLAGS = {"v4": 0, "lsd": 1}  # rl_config.flags (RL_CFG_LSD_ONLY)
 CFG_LAG_WINDOW = 2  # RL_CFG_LAG_WINDOW: SECOND key strings findable 3 s behind (routers' engines)
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class RlConfig(C.Structure):
@@ -119,7 +119,10 @@ class RlRouterConfig(C.Structure):
                 ("rccl_id", C.c_void_p), ("flags", C.c_uint32), ("max_blob_bytes", C.c_uint32)]
 
 
-ROUTER_NO_COMBINE, ROUTER_HOST, ROUTER_EMULATED = 1, 2, 4  # rl_router_config.flags
+ROUTER_NO_COMBINE, ROUTER_HOST, ROUTER_EMULATED, ROUTER_HOST_XCHG = 1, 2, 4, 8  # rl_router_config.flags
+# rl_host_xchg_fn: (ctx, send, send_counts, send_displs, recv, recv_counts, recv_displs) -> 0 | error
+HOST_XCHG_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.c_void_p,
+                           C.POINTER(C.c_size_t), C.POINTER(C.c_size_t))
 
 
 class RlRouterStats(C.Structure):
@@ -177,6 +180,7 @@ ABI = [
     ("rl_resolve_device", [C.c_void_p, C.POINTER(RlResolveBatch), C.c_void_p], C.c_int),
     ("rl_router_unique_id", [C.c_void_p], C.c_int),
     ("rl_router_emu_world", [C.c_uint32, C.c_void_p], C.c_int),
+    ("rl_router_use_host_xchg", [C.c_void_p, C.c_void_p], C.c_int),
     ("rl_router_create", [C.POINTER(RlRouterConfig), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
     ("rl_router_step", [C.c_void_p, C.POINTER(RlBatch), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
     ("rl_router_submit", [C.c_void_p, C.POINTER(RlBatch), C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)], C.c_int),
@@ -707,7 +711,7 @@ class Router:
 
     def __init__(self, engines, max_desc: int, n_shards: Optional[int] = None, rank: int = 0,
                  rccl_id: Optional[bytes] = None, combine: bool = True, host: bool = False,
-                 max_blob_bytes: int = 0, emulated: bool = False):
+                 max_blob_bytes: int = 0, emulated: bool = False, host_xchg=None):
         """emulated: rccl_id is an emu_world() id — the collective transport with in-process
         collectives (one Router per rank, each driven by its own thread)."""
         self.lib = engines[0].lib
@@ -718,7 +722,11 @@ class Router:
         cfg.rank = rank
         cfg.max_desc = max_desc
         cfg.flags = ((0 if combine else ROUTER_NO_COMBINE) | (ROUTER_HOST if host else 0)
-                     | (ROUTER_EMULATED if emulated else 0))
+                     | (ROUTER_EMULATED if emulated else 0) | (ROUTER_HOST_XCHG if host_xchg is not None else 0))
+        self._xchg = None
+        if host_xchg is not None:  # a HOST_XCHG_FN the caller keeps alive as long as the router
+            self._xchg = host_xchg
+            self.lib.rl_router_use_host_xchg(C.cast(host_xchg, C.c_void_p), None)
         cfg.max_blob_bytes = max_blob_bytes
         self._id = None
         if rccl_id is not None:
@@ -816,6 +824,15 @@ class Router:
             if self._keep:
                 self._keep.pop(0)
         return [(outs[i][:nd], thrs[i][:nr]) for i, (nd, nr) in enumerate(sizes)]
+
+    def allgather_host(self, data: bytes, n_ranks: int) -> list:
+        """rl_router_allgather_host: every rank's `data` (the same length everywhere), in rank
+        order (the batchers' rule and stop agreement)."""
+        buf = C.create_string_buffer(bytes(data), max(1, len(data)))
+        out = C.create_string_buffer(max(1, len(data) * n_ranks))
+        self._check(self.lib.rl_router_allgather_host(self.h, buf, len(data), out), "rl_router_allgather_host")
+        raw = out.raw
+        return [raw[i * len(data):(i + 1) * len(data)] for i in range(n_ranks)]
 
     def stats(self) -> dict:
         s = RlRouterStats()

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define RL_ABI_VERSION 6u
+#define RL_ABI_VERSION 7u
 
 /* rule id of a descriptor whose limit is nil ("don't check", src/limiter/cache.go:19-22) */
 #define RL_NIL_RULE 0xFFFFFFFFu
@@ -442,8 +442,10 @@ typedef struct rl_router_config {
 enum {
   RL_ROUTER_NO_COMBINE = 1u, /* one record per descriptor (no hot-prefix combining) */
   RL_ROUTER_HOST = 2u,       /* allocate pinned host staging: rl_router_host_acquire / _submit_host / _wait_into */
-  RL_ROUTER_EMULATED = 4u    /* rccl_id is an rl_router_emu_world id: the collective transport's code path with
+  RL_ROUTER_EMULATED = 4u,   /* rccl_id is an rl_router_emu_world id: the collective transport's code path with
                                 the collectives emulated in process (one thread per rank; tests) */
+  RL_ROUTER_HOST_XCHG = 8u   /* the collectives through the host exchange registered by rl_router_use_host_xchg
+                                (one process per rank where RCCL cannot run them; tests). rccl_id unused */
 };
 
 typedef struct rl_router_stats {
@@ -472,6 +474,16 @@ int rl_router_unique_id(uint8_t* id_out);
  * driven by the same count and displacement vectors, each rank's receive counts checked against
  * its peers' send counts. The world is freed when the last of its n_ranks routers is destroyed. */
 int rl_router_emu_world(uint32_t n_ranks, uint8_t* id_out);
+/* A host exchange (RL_ROUTER_HOST_XCHG; tests): an all-to-all-v of host bytes among the ranks of
+ * a process group the caller runs (e.g. torch.distributed over gloo). Rank j's bytes for this
+ * rank arrive at recv + recv_displs[j]; n_ranks counts and displacements each way. 0 = success.
+ * The collective transport then runs its code path unchanged with one process per rank on any
+ * number of GPUs — RCCL refuses two ranks on one device, so a one-GPU box cannot run it across
+ * processes otherwise. Every collective stages through host memory: not for performance. The
+ * registration holds for this thread's next rl_router_create with the flag. */
+typedef int (*rl_host_xchg_fn)(void* ctx, const void* send, const size_t* send_counts, const size_t* send_displs,
+                               void* recv, const size_t* recv_counts, const size_t* recv_displs);
+int rl_router_use_host_xchg(rl_host_xchg_fn fn, void* ctx);
 /* engines: n_shards engines (local transport) or 1 (RCCL transport). The router does not own
  * them; they must outlive it and be used by nothing else while a step runs. All engines share
  * hash_seed and the rule table. */

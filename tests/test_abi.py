@@ -25,7 +25,7 @@ def test_library_exports_all_declared_symbols():
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
     assert sorted(n for n, _, _ in hiprl.ABI) == names
-    assert lib.rl_abi_version() == hiprl.ABI_VERSION == 6
+    assert lib.rl_abi_version() == hiprl.ABI_VERSION == 7
 
 
 def test_struct_layouts_match_header(tmp_path):
