@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -262,22 +263,26 @@ struct rl_engine {
   volatile uint32_t* done_word(uint32_t slot) {
     return reinterpret_cast<volatile uint32_t*>(h_ctl_s[slot] + 1);
   }
-  // Now and then (every 2^14 reads, ~1 ms) the stream is asked too: a fault in a kernel before
-  // the word shows there (the word would stay 0), and a stream that drained without the word
-  // (which k4_group writes last) ends the spin as the old bound's stream synchronize did.
+  // A wait longer than 5 ms (a batch takes ~0.1 ms) asks the stream too, every 5 ms: a fault in
+  // a kernel before the word shows there (the word would stay 0), and a stream that drained
+  // without the word (k4_group writes it last) ends the spin as the old bound's stream
+  // synchronize did. Normal waits never call into the runtime: a hipStreamQuery every 2^14 reads
+  // fell inside ordinary waits and cost 8-18 % of the config-3 step.
   hipError_t poll_done(const Flight& f) {
     volatile uint32_t* w = done_word(f.slot);
+    auto next = std::chrono::steady_clock::now() + std::chrono::milliseconds(5);
     for (uint64_t k = 0;; ++k) {
       if (*w) {
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
         return hipSuccess;
       }
-      if ((k & 0x3FFFu) == 0x3FFFu) {
-        const hipError_t q = hipStreamQuery(stream);
-        if (q == hipErrorNotReady) continue;
+      if ((k & 0x3FFu) != 0x3FFu || std::chrono::steady_clock::now() < next) continue;
+      const hipError_t q = hipStreamQuery(stream);
+      if (q != hipErrorNotReady) {
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
         return q;
       }
+      next = std::chrono::steady_clock::now() + std::chrono::milliseconds(5);
     }
   }
   int n_fl = 0;

@@ -213,7 +213,11 @@ def load_library(path: Optional[os.PathLike] = None) -> C.CDLL:
         raise RuntimeError(f"HIP extension not built: {p} missing (run __graft_entry__.build())")
     lib = C.CDLL(str(p))
     for name, argt, rest in ABI:
-        f = getattr(lib, name)
+        # (a variant library given by path — an earlier round's build in a bench A/B — may lack
+        # entry points added since; the in-tree library must export them all)
+        f = getattr(lib, name) if path is None or hasattr(lib, name) else None
+        if f is None:
+            continue
         f.argtypes = argt
         f.restype = rest
     if path is None:
