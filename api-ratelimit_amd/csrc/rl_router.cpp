@@ -976,11 +976,25 @@ int rl_router::submit_coll(uint32_t k) {
   // issues these collectives in the same order.)
   // Their unpacks follow this step's records on the origin stream, so the decide of this step
   // starts as early as it can.
+  // The older steps' replies and this step's records form ONE collective group: one launch, and
+  // no host gap between the two exchanges on the origin stream (RL_ROUTER_SPLIT_GROUPS: two).
+#ifdef RL_ROUTER_SPLIT_GROUPS
+  constexpr bool fused = false;
+#else
+  constexpr bool fused = true;
+#endif
+  if (fused) {
+    const ncclResult_t gr = xp->group_start();
+    if (gr != ncclSuccess) return nccl_fail(gr, "group(replies, records)");
+  }
   for (uint64_t q = done; q + 1 < seq; ++q) {
     const uint32_t kq = (uint32_t)(q % NSLOT);
     if (slot[kq].busy && !slot[kq].counts_failed && !slot[kq].replied) {
       reply_coll(kq);
-      if (broken) return RL_ECOMM;
+      if (broken) {
+        if (fused) (void)xp->group_end();
+        return RL_ECOMM;
+      }
 #ifdef RL_ROUTER_UNPACK_FIRST
       unpack_coll(kq);
 #endif
@@ -1001,6 +1015,10 @@ int rl_router::submit_coll(uint32_t k) {
   t.n_in = (uint32_t)(ro / REC);
   for (uint32_t j = 0; j < G; ++j) st.recv[j] = j == me ? t.n_in : 0;
   nr = xp->a2av(t.pb.send, sc, sd, t.recv, rc, rd, rs);
+  if (fused) {
+    const ncclResult_t ge = xp->group_end();  // (ends the group on a failed a2av too)
+    if (nr == ncclSuccess) nr = ge;
+  }
   if (nr != ncclSuccess) return nccl_fail(nr, "all-to-all-v(records)");
   const double t1 = now_us();
   he = hipEventRecord(slot[k].ev_rec, rs);

@@ -27,6 +27,9 @@ for s in "${@:-smoke bench routed1 ls8 ls2 config1}"; do
     case $step in
       smoke) run smoke 240 python -u -c "import __graft_entry__ as g; g.smoke()" ;;
       bench) run bench 600 python -u bench.py ;;
+      bench_b) run bench_b 600 python -u bench.py ;;
+      bench4) run bench4 600 python -u bench.py --config 4 ;;
+      bench5) run bench5 600 python -u bench.py --config 5 ;;
       routed1) run routed1 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 \
                  --master-port 29533 bench.py --gpus 1 --force-routed --steps 30 --warmup 10 --cpu-seconds 0 \
                  --no-host-path --no-roofline-probe ;;
