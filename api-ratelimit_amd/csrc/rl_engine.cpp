@@ -1799,13 +1799,15 @@ int rl_resolve_device(rl_engine* e, const rl_resolve_batch* b, uint32_t* d_rule_
       e->d_res_flags = nullptr;
       e->res_flag_cap = 0;
       fe = hipMalloc(&e->d_res_flags, (size_t)cap * 4 * rl_engine::RES_FLAG_SLOTS);
+      if (fe == hipSuccess) fe = hipMemset(e->d_res_flags, 0, (size_t)cap * 4 * rl_engine::RES_FLAG_SLOTS);
     }
     if (fe != hipSuccess) return e->hip_fail(fe, "rl_resolve flags");
     e->res_flag_cap = cap;
   }
   uint32_t* flags = e->d_res_flags + (size_t)(e->res_seq++ % rl_engine::RES_FLAG_SLOTS) * e->res_flag_cap;
+  const uint32_t seq = (uint32_t)(e->res_seq % 0xFFFFFFFFull) + 1u;  // non-zero, differs from the slot's last
   e->timed(KT_RESOLVE, [&] {
-    launch_resolve(front ? e->front : e->stream, resolve_in(b), e->tree, d_rule_out, flags);
+    launch_resolve(front ? e->front : e->stream, resolve_in(b), e->tree, d_rule_out, flags, seq);
   });
   hipError_t he = hipGetLastError();
   if (he == hipSuccess && front) {

@@ -69,8 +69,10 @@ __host__ __device__ inline uint32_t tree_hash(uint32_t parent, uint32_t fold, ui
 int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint32_t names_len,
                std::vector<TreeNodeDev>& out_nodes, std::vector<uint64_t>& out_slots, uint32_t& mask, std::string& err);
 // Two launches: the level-pipelined walk, then the exact walk for the descriptors it leaves
-// (flags: resolve_flag_words(n_desc) words of scratch, no initial state).
-void launch_resolve(hipStream_t st, const ResolveIn& in, const TreeDesc2& t, uint32_t* rule_out, uint32_t* flags);
+// (flags: resolve_flag_words(n_desc) words of scratch, never holding `seq` (non-zero, this
+// launch's number) before the launch: zeroed once, then numbered launches).
+void launch_resolve(hipStream_t st, const ResolveIn& in, const TreeDesc2& t, uint32_t* rule_out, uint32_t* flags,
+                    uint32_t seq);
 uint32_t resolve_flag_words(uint32_t n_desc);
 // k_resolve's code on the host (tests/cshim): both passes, *exact = the exact walk decided
 uint32_t resolve_one_host(const ResolveIn& in, const TreeDesc2& t, uint32_t i, bool* exact = nullptr);

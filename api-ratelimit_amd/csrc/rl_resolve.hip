@@ -209,9 +209,9 @@ RL_HD uint32_t first_match(const uint64_t (&w)[TREE_PROBE], uint32_t h, bool& do
   return TREE_NONE;
 }
 RL_HD void probe_round(const TreeDesc2& t, uint32_t h, uint64_t (&w)[TREE_PROBE]) {
-  const uint32_t base = h & t.mask;
+  const uint64_t* p = t.slots + (h & t.mask);  // (one address, the slots at immediate offsets)
 #pragma unroll
-  for (int j = 0; j < TREE_PROBE; ++j) w[j] = t.slots[base + j];
+  for (int j = 0; j < TREE_PROBE; ++j) w[j] = p[j];
 }
 
 // rateLimitConfigImpl.GetLimit (config_impl.go:274-323) for one descriptor: unknown domain ->
@@ -532,19 +532,24 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, uint32_t i)
 // kept (config 4, one box): a persistent grid of 1024 / 512 blocks striding over the chunks, so
 // the pass leaves CUs to the engine stream's kernels: k_resolve 90 -> 95 / 113 us, the step
 // slower; the engine stream at a higher priority than the front stream: no change.
+// flags[gridDim.x] = seq when any block raised its flag (this launch's number: no clearing).
 __global__ __launch_bounds__(RS_NT) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_resolve(
-    ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out, uint32_t* __restrict__ flags) {
+    ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out, uint32_t* __restrict__ flags, uint32_t seq) {
   const uint32_t i = blockIdx.x * RS_NT + threadIdx.x;
   const uint32_t r = i >= in.n_desc ? 0u : in.n_entries ? resolve_fast<true>(in, t, i) : resolve_fast<false>(in, t, i);
   if (i < in.n_desc) rule_out[i] = r;
   const int any = __syncthreads_or(r == RS_EXACT);
-  if (threadIdx.x == 0) flags[blockIdx.x] = (uint32_t)any;
+  if (threadIdx.x == 0) {
+    flags[blockIdx.x] = (uint32_t)any;
+    if (any) flags[gridDim.x] = seq;
+  }
 }
 // Second pass: blocks stride over the first pass's flags; a flagged block's descriptors left
 // to the exact walk take it.
 constexpr uint32_t RS_EXACT_BLOCKS = 2048;  // (a tree of long names leaves every descriptor here)
 __global__ __launch_bounds__(RS_NT) void k_resolve_exact(ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out,
-                                                        const uint32_t* __restrict__ flags, uint32_t nblk) {
+                                                        const uint32_t* __restrict__ flags, uint32_t nblk, uint32_t seq) {
+  if (flags[nblk] != seq) return;  // no block raised its flag (one load: the common case)
   for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
     if (!flags[b]) continue;  // block-uniform
     const uint32_t i = b * RS_NT + threadIdx.x;
@@ -563,7 +568,7 @@ uint32_t resolve_one_host(const ResolveIn& in, const TreeDesc2& t, uint32_t i, b
   return r == RS_EXACT ? resolve_one(in, t, i) : r;
 }
 uint32_t resolve_exact_host(const ResolveIn& in, const TreeDesc2& t, uint32_t i) { return resolve_one(in, t, i); }
-uint32_t resolve_flag_words(uint32_t n_desc) { return (n_desc + RS_NT - 1) / RS_NT; }
+uint32_t resolve_flag_words(uint32_t n_desc) { return (n_desc + RS_NT - 1) / RS_NT + 1u; }  // + the "any" word
 
 int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint32_t names_len,
                std::vector<TreeNodeDev>& out_nodes, std::vector<uint64_t>& out_slots, uint32_t& mask,
@@ -620,12 +625,13 @@ int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint
   return 0;
 }
 
-void launch_resolve(hipStream_t st, const ResolveIn& in, const TreeDesc2& t, uint32_t* rule_out, uint32_t* flags) {
+void launch_resolve(hipStream_t st, const ResolveIn& in, const TreeDesc2& t, uint32_t* rule_out, uint32_t* flags,
+                    uint32_t seq) {
   if (!in.n_desc) return;
-  const uint32_t nblk = resolve_flag_words(in.n_desc);
-  hipLaunchKernelGGL(k_resolve, dim3(nblk), dim3(RS_NT), 0, st, in, t, rule_out, flags);
+  const uint32_t nblk = resolve_flag_words(in.n_desc) - 1u;
+  hipLaunchKernelGGL(k_resolve, dim3(nblk), dim3(RS_NT), 0, st, in, t, rule_out, flags, seq);
   hipLaunchKernelGGL(k_resolve_exact, dim3(std::min(nblk, RS_EXACT_BLOCKS)), dim3(RS_NT), 0, st, in, t, rule_out, flags,
-                     nblk);
+                     nblk, seq);
 }
 
 }  // namespace rlhip
