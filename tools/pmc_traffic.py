@@ -32,7 +32,9 @@ def load(pattern):
         recs = list(csv.DictReader(open(f)))
         recs.sort(key=lambda r: int(r.get("Dispatch_Id", 0) or 0))
         for r in recs:
-            k = r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1].replace("void ", "").strip()
+            # (k_resolve lives in an anonymous namespace: drop that before cutting at the arguments)
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
+            k = k.split("::")[-1].replace("void ", "").strip()
             rows[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return rows
 
