@@ -45,9 +45,11 @@ def mean_last(v, n):
 
 
 bench_rows = load(f"{root}/p*/run_counter_collection.csv")
+# the bench's workload generator (tools/gen/workload_gen.hip) and roofline probe: not the path
+NOT_ENGINE = ("k_keys", "k_bytes", "k_bytes4", "k_copy", "k_slot_rmw")
 kernels = {}
 for k, c in sorted(bench_rows.items()):
-    if not k.startswith(("k_", "k4_")):
+    if not k.startswith(("k_", "k4_")) or k in NOT_ENGINE:
         continue
     n = len(c.get("FETCH_SIZE", []))
     f = mean_last(c.get("FETCH_SIZE", []), steps) * 1024
