@@ -217,6 +217,8 @@ struct rl_engine {
   TreeNodeDev* d_tree_nodes = nullptr;
   uint64_t* d_tree_slots = nullptr;
   uint8_t* d_tree_names = nullptr;
+  FastNode* d_tree_fnodes = nullptr;  // the first pass's copy (build_fast_tree)
+  uint64_t* d_tree_fslots = nullptr;
   TreeDesc2 tree{};
   bool has_tree = false;
   uint8_t* d_res = nullptr;  // rl_resolve staging (grown on demand)
@@ -1106,7 +1108,7 @@ void rl_destroy(rl_engine* e) {
   for (int k = 0; k < 3; ++k) hipFree(e->v4_ctl[k]);
   for (void* p : {(void*)e->v4_hoff, (void*)e->v4_dfr, (void*)e->v4_hb,
                   (void*)e->v4_heads, (void*)e->v4_ins, e->v4_scratch, (void*)e->d_poison, (void*)e->d_tree_nodes,
-                  (void*)e->d_tree_slots, (void*)e->d_tree_names, (void*)e->d_res, (void*)e->d_res_flags, (void*)e->table, (void*)e->d_occ,
+                  (void*)e->d_tree_slots, (void*)e->d_tree_names, (void*)e->d_tree_fnodes, (void*)e->d_tree_fslots, (void*)e->d_res, (void*)e->d_res_flags, (void*)e->table, (void*)e->d_occ,
                   (void*)e->d_rules, (void*)e->keys_orig, (void*)e->keys_a, (void*)e->keys_b, (void*)e->vals_a,
                   (void*)e->vals_b, (void*)e->recs, (void*)e->srec, (void*)e->seg, (void*)e->offs,
                   (void*)e->hist_part, (void*)e->fp_part, (void*)e->fp_part2, (void*)e->tile_heads,
@@ -1741,13 +1743,21 @@ int rl_load_tree(rl_engine* e, const rl_tree_node* nodes, uint32_t n_nodes, cons
   uint32_t mask = 0;
   int rc = build_tree(nodes, n_nodes, names, names_len, hn, hs, mask, err);
   if (rc) return e->fail(rc, "%s", err.c_str());
+  std::vector<FastNode> fn;
+  std::vector<uint64_t> fs;
+  uint32_t fmask = 0;
+  build_fast_tree(hn, names, fn, fs, fmask);
   hipError_t he = hipStreamSynchronize(e->stream);  // resolutions queued on the old tree finish first
   hipFree(e->d_tree_nodes);
   hipFree(e->d_tree_slots);
   hipFree(e->d_tree_names);
+  hipFree(e->d_tree_fnodes);
+  hipFree(e->d_tree_fslots);
   e->d_tree_nodes = nullptr;
   e->d_tree_slots = nullptr;
   e->d_tree_names = nullptr;
+  e->d_tree_fnodes = nullptr;
+  e->d_tree_fslots = nullptr;
   e->has_tree = false;
   if (he == hipSuccess) he = hipMalloc(&e->d_tree_nodes, std::max<size_t>(1, hn.size()) * sizeof(TreeNodeDev));
   if (he == hipSuccess) he = hipMalloc(&e->d_tree_slots, hs.size() * 8);
@@ -1756,11 +1766,20 @@ int rl_load_tree(rl_engine* e, const rl_tree_node* nodes, uint32_t n_nodes, cons
     he = hipMemcpy(e->d_tree_nodes, hn.data(), hn.size() * sizeof(TreeNodeDev), hipMemcpyHostToDevice);
   if (he == hipSuccess) he = hipMemcpy(e->d_tree_slots, hs.data(), hs.size() * 8, hipMemcpyHostToDevice);
   if (he == hipSuccess && names_len) he = hipMemcpy(e->d_tree_names, names, names_len, hipMemcpyHostToDevice);
+  if (he == hipSuccess) he = hipMalloc(&e->d_tree_fnodes, std::max<size_t>(1, fn.size()) * sizeof(FastNode));
+  if (he == hipSuccess) he = hipMalloc(&e->d_tree_fslots, fs.size() * 8);
+  if (he == hipSuccess && !fn.empty())
+    he = hipMemcpy(e->d_tree_fnodes, fn.data(), fn.size() * sizeof(FastNode), hipMemcpyHostToDevice);
+  if (he == hipSuccess) he = hipMemcpy(e->d_tree_fslots, fs.data(), fs.size() * 8, hipMemcpyHostToDevice);
   if (he != hipSuccess) return e->hip_fail(he, "rl_load_tree");
   e->tree.nodes = e->d_tree_nodes;
   e->tree.slots = e->d_tree_slots;
   e->tree.names = e->d_tree_names;
   e->tree.mask = mask;
+  e->tree.fnodes = e->d_tree_fnodes;
+  e->tree.fslots = e->d_tree_fslots;
+  e->tree.fmask = fmask;
+  e->tree.n_fnodes = (uint32_t)fn.size();
   e->has_tree = true;
   return 0;
 }

@@ -29,12 +29,36 @@ struct __attribute__((aligned(64))) TreeNodeDev {
 };
 static_assert(sizeof(TreeNodeDev) == 64, "tree node layout");
 
+// The first pass's copy of the tree (k_resolve): nodes renumbered breadth-first so that a
+// node's children have consecutive ids, and each node carries its children's edge hashes, so
+// ONE 64-B load of a node both confirms it (parent, name) and looks the next level's names up
+// among its children. A node with more than FAST_CHILDREN children, or two children whose hashes
+// are equal, keeps its children in the fast edge table instead (FAST_OVERFLOW), as the domains
+// (the root's children) always are.
+constexpr int FAST_CHILDREN = 8;
+constexpr uint32_t FAST_OVERFLOW = 0x80000000u;  // len_flags: children in the fast edge table
+constexpr uint32_t FAST_NO_CHILD = 0xFFFFFFFFu;  // chash of an unused child slot (fast hashes are even)
+struct __attribute__((aligned(64))) FastNode {
+  uint32_t parent;       // fast id of the parent, or RL_TREE_ROOT
+  uint32_t len_flags;    // name length (low 24 bits, saturated), FAST_OVERFLOW
+  uint32_t rule;         // RL_NIL_RULE if none
+  uint32_t first_child;  // fast id of child 0 (children k = first_child + k)
+  uint32_t name[4];      // first 16 name bytes, little-endian, zero-padded
+  uint32_t chash[FAST_CHILDREN];  // fast_hash(this id, child k's name), or FAST_NO_CHILD
+};
+static_assert(sizeof(FastNode) == 64, "fast node layout");
+
 struct TreeDesc2 {
   const TreeNodeDev* nodes;
   const uint64_t* slots;  // (parent, name) edge table: hash << 32 | node id, or ~0; mask + TREE_PROBE entries
                           // (the first TREE_PROBE - 1 repeated at the end, so a probe round never wraps)
   const uint8_t* names;
   uint32_t mask;          // power-of-two table size - 1 (load <= 1/8)
+  // the first pass's tree (fast ids; same edge-table layout over fast_hash, for the domains and
+  // the children of overflow nodes)
+  const FastNode* fnodes;
+  const uint64_t* fslots;
+  uint32_t fmask, n_fnodes;
 };
 
 struct ResolveIn {
@@ -68,6 +92,14 @@ __host__ __device__ inline uint32_t tree_hash(uint32_t parent, uint32_t fold, ui
 
 int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint32_t names_len,
                std::vector<TreeNodeDev>& out_nodes, std::vector<uint64_t>& out_slots, uint32_t& mask, std::string& err);
+// The edge hash of the first pass's tree: tree_hash over fast ids, bit 0 clear (so no hash equals
+// FAST_NO_CHILD or the slots' empty word).
+__host__ __device__ inline uint32_t fast_hash(uint32_t parent, uint32_t fold, uint32_t len) {
+  return tree_hash(parent, fold, len) & ~1u;
+}
+// The first pass's tree from build_tree's nodes (and fast_id[original id] = fast id, for tests).
+void build_fast_tree(const std::vector<TreeNodeDev>& nodes, const uint8_t* names, std::vector<FastNode>& out_nodes,
+                     std::vector<uint64_t>& out_slots, uint32_t& mask, std::vector<uint32_t>* fast_id = nullptr);
 // Two launches: the level-pipelined walk, then the exact walk for the descriptors it leaves
 // (flags: resolve_flag_words(n_desc) words of scratch, never holding `seq` (non-zero, this
 // launch's number) before the launch: zeroed once, then numbered launches).

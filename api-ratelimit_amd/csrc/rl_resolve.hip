@@ -25,6 +25,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -308,19 +309,23 @@ RL_HD uint32_t resolve_one(const ResolveIn& in, const TreeDesc2& t, uint32_t i) 
 // ---- the level-pipelined walk (k_resolve's first pass) ----
 // resolve_one spends about four dependent round trips per level: the entry's words, its two
 // strings, the edge probe rounds, the candidate nodes. None of the first two depend on the
-// walk, and the node is needed only to confirm a hash match (a node's rule matters only at the
-// last entry; its child count not at all, see below). So this pass loads each level's entry
-// words two levels ahead and its strings one level ahead, hashes both names from registers,
-// takes a probe round's first hash match unconfirmed and confirms it one level later, beside
-// the next level's probe rounds: one round trip per level, plus one for the last node.
-//   * A probe chain without a hash match settles a miss exactly (equal names hash equally); a
-//     chain longer than the first round is read on slot by slot (rare at load <= 1/8). A match
-//     whose node turns out to carry another name, and any string the register path cannot hold
-//     (over 16 bytes, an unaligned blob, a load window past the blob's end) leave the descriptor
-//     to the exact walk (k_resolve_exact).
+// walk, and a node is needed only to confirm a hash match (its rule matters only at the last
+// entry). So this pass loads each level's entry words two levels ahead and its strings one
+// level ahead, hashes both names from registers and looks them up among the children hashes
+// of the node it is standing on (FastNode: the node's own 64-B load both confirms it and holds
+// its children's hashes), taking the match unconfirmed until the next level loads that node:
+// one round trip per level, plus one for the last node.
+//   * A miss is exact (equal names hash equally; siblings with equal hashes, and nodes with
+//     more than FAST_CHILDREN children, keep their children in the fast edge table, read by
+//     probe rounds). A match whose node carries another name, and any string the register path
+//     cannot hold (over 16 bytes, an unaligned blob, a load window past the blob's end) leave
+//     the descriptor to the exact walk (k_resolve_exact).
+//   * The usual batch lays each entry out as key "_" value inside the descriptor's own bytes
+//     (the cache key's prefix): one load window then holds the whole name. Other layouts load
+//     the value's window too and join the two in registers.
 //   * No child count check: the reference stops at a node without children (config_impl.go
-//     :320-325); this walk goes on and looks the next entry up under that node, which no edge
-//     has as parent, so it misses and stops there with the same (nil) result.
+//     :320-325); this walk goes on and looks the next entry up among no children, misses and
+//     stops there with the same (nil) result.
 constexpr uint32_t RS_EXACT = 0xFFFFFFFEu;  // first pass: left to the exact walk
 #ifndef RL_RESOLVE_FW
 #define RL_RESOLVE_FW 4
@@ -329,27 +334,100 @@ constexpr uint32_t RS_EXACT = 0xFFFFFFFEu;  // first pass: left to the exact wal
 // is 9). Longer ones go to the exact walk: every dword held here costs the pass occupancy.
 constexpr int FW = RL_RESOLVE_FW;
 constexpr uint32_t FB = 4 * FW;
-static_assert(FW >= 1 && FW <= SW, "first-pass name words");
+static_assert(FW == 4, "first-pass names: one 16-B node name load");
+constexpr uint32_t FWB = 4 * (FW + 1);  // bytes of a string's load window (from its aligned start)
 
-// load_str for FW dwords: the FW + 1 dwords from the string's first, unconditional and not
-// clamped, all in flight together. The caller checks they lie inside the blob (FWB bytes from
-// the string's aligned start). A load behind a condition — even a wave-uniform one, or a
-// clamped index the compiler turns into one — made it wait for every load before it: 141 us
-// for this pass at config 4 against 96 for the old walk.
-constexpr uint32_t FWB = 4 * (FW + 1);
-RL_HD void load_str_w(const uint8_t* bytes, uint32_t off, uint32_t len, uint32_t (&s)[FW]) {
-  const uint32_t sh = off & 3u;
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(bytes) + (off >> 2);
-  uint32_t d[FW + 1];
-#pragma unroll
-  for (int k = 0; k <= FW; ++k) d[k] = w[k];
-  // branch-free from the loads on (a use behind a condition lets the compiler sink its load
-  // into the branch, and the branch then waits for every load before it)
+// Raw buffer loads: a load wholly past the buffer's end returns zeros (the hardware's range
+// check; the host form does the same), so the loads a level does not need are sent past the end
+// (RS_OOB) rather than put behind a condition: a load behind a condition — even a wave-uniform
+// one — made the wave wait for every load before it (141 us for this pass against 96 for the
+// old walk). Buffers are capped below RS_OOB, and the walk never uses a load that is partly past
+// the end (windows are checked against the capped length).
+constexpr uint32_t RS_OOB = 0x80000000u;
+constexpr uint32_t RS_BUF_MAX = RS_OOB - 64u;
+struct Buf {
+#ifdef __HIP_DEVICE_COMPILE__
+  __amdgpu_buffer_rsrc_t r;
+#else
+  const uint8_t* p;
+  uint32_t n;
+#endif
+};
+RL_HD inline Buf make_buf(const void* p, uint64_t n) {
+  const uint32_t m = (uint32_t)(p ? (n < RS_BUF_MAX ? n : RS_BUF_MAX) : 0);
+  Buf b;
+#ifdef __HIP_DEVICE_COMPILE__
+  b.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)m, 0x00020000);
+#else
+  b.p = static_cast<const uint8_t*>(p);
+  b.n = m;
+#endif
+  return b;
+}
+RL_HD inline uint4 bld4(const Buf& b, uint32_t off) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(b.r, (int)off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+#else
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if ((uint64_t)off + 16 <= b.n) memcpy(&v, b.p + off, 16);
+  return v;
+#endif
+}
+RL_HD inline uint2 bld2(const Buf& b, uint32_t off) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const auto v = __builtin_amdgcn_raw_buffer_load_b64(b.r, (int)off, 0, 0);
+  return make_uint2(v[0], v[1]);
+#else
+  uint2 v = make_uint2(0, 0);
+  if ((uint64_t)off + 8 <= b.n) memcpy(&v, b.p + off, 8);
+  return v;
+#endif
+}
+RL_HD inline uint32_t bld1(const Buf& b, uint32_t off) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_raw_buffer_load_b32(b.r, (int)off, 0, 0);
+#else
+  uint32_t v = 0;
+  if ((uint64_t)off + 4 <= b.n) memcpy(&v, b.p + off, 4);
+  return v;
+#endif
+}
+struct FastBufs {
+  Buf bytes, dom, efirst, ent, ovr, fnodes, fslots;
+};
+RL_HD inline FastBufs fast_bufs(const ResolveIn& in, const TreeDesc2& t) {
+  FastBufs B;
+  B.bytes = make_buf(in.bytes, in.bytes_len);
+  B.dom = make_buf(in.domain, (uint64_t)in.n_desc * 8);
+  B.efirst = make_buf(in.entry_first, ((uint64_t)in.n_desc + 1) * 4);
+  B.ent = make_buf(in.entry, (uint64_t)in.n_entries * 16);
+  B.ovr = make_buf(in.override_rule, (uint64_t)in.n_desc * 4);
+  B.fnodes = make_buf(t.fnodes, (uint64_t)t.n_fnodes * sizeof(FastNode));
+  B.fslots = make_buf(t.fslots, ((uint64_t)t.fmask + TREE_PROBE) * 8);
+  return B;
+}
+
+// A string's load window: the FW + 1 dwords from its aligned start (RS_OOB: zeros).
+RL_HD inline void load_win(const Buf& b, uint32_t off, uint32_t (&d)[FW + 1]) {
+  const uint4 a = bld4(b, off);
+  d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
+  d[4] = bld1(b, off + 16u);
+}
+// s[k] = bytes 4k..4k+3 of the window's string at byte sh of its first dword, zero past len
+RL_HD inline void from_win(const uint32_t (&d)[FW + 1], uint32_t sh, uint32_t len, uint32_t (&s)[FW]) {
 #pragma unroll
   for (int k = 0; k < FW; ++k) {
     const int32_t rem = (int32_t)len - 4 * k;
     const uint32_t nb = rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem;
     s[k] = align_byte(d[k + 1], d[k], sh) & low_bytes_mask(nb);
+  }
+}
+RL_HD inline void mask_to(uint32_t (&s)[FW], uint32_t len) {
+#pragma unroll
+  for (int k = 0; k < FW; ++k) {
+    const int32_t rem = (int32_t)len - 4 * k;
+    s[k] &= low_bytes_mask(rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem);
   }
 }
 RL_HD uint32_t fold_w(const uint32_t (&s)[FW], uint32_t len) {  // = fold_reg for len <= FB
@@ -381,34 +459,24 @@ RL_HD void key_value_w(const uint32_t (&K)[FW], const uint32_t (&V)[FW], uint32_
     r[k] = (b ? align_byte(a[k], lo, 4u - b) : a[k]) | K[k] | us;
   }
 }
-// A node's header (parent, name length, rule) and first FW name dwords.
-struct NodeW {
-  uint32_t parent, len, rule, name[FW];
+// A fast node: header, first 16 name bytes and the children's hashes (four 16-B loads).
+struct NodeF {
+  uint32_t parent, len_flags, rule, first, name[FW], ch[FAST_CHILDREN];
 };
-RL_HD NodeW load_node_w(const TreeDesc2& t, uint32_t id) {
-  static_assert(FW % 4 == 0, "whole 16-B name loads");
-  const uint4* p = reinterpret_cast<const uint4*>(t.nodes + id);
-  const uint4 h = p[0];
-  uint4 nm[FW / 4];
-#pragma unroll
-  for (int k = 0; k < FW / 4; ++k) nm[k] = p[2 + k];
-  NodeW v;
-  v.parent = h.x;
-  v.len = h.y;
-  v.rule = h.z;
-#pragma unroll
-  for (int k = 0; k < FW / 4; ++k) {
-    v.name[4 * k] = nm[k].x;
-    v.name[4 * k + 1] = nm[k].y;
-    v.name[4 * k + 2] = nm[k].z;
-    v.name[4 * k + 3] = nm[k].w;
-  }
+RL_HD inline NodeF load_fnode(const Buf& b, uint32_t id) {
+  const uint32_t o = id * (uint32_t)sizeof(FastNode);
+  const uint4 h = bld4(b, o), n0 = bld4(b, o + 16u), c0 = bld4(b, o + 32u), c1 = bld4(b, o + 48u);
+  NodeF v;
+  v.parent = h.x; v.len_flags = h.y; v.rule = h.z; v.first = h.w;
+  v.name[0] = n0.x; v.name[1] = n0.y; v.name[2] = n0.z; v.name[3] = n0.w;
+  v.ch[0] = c0.x; v.ch[1] = c0.y; v.ch[2] = c0.z; v.ch[3] = c0.w;
+  v.ch[4] = c1.x; v.ch[5] = c1.y; v.ch[6] = c1.z; v.ch[7] = c1.w;
   return v;
 }
 // the node against (parent, len, the first len bytes of q): q may hold more bytes past len (a
 // key checked against key "_" value), masked here; len <= FB
-RL_HD bool confirm(const NodeW& nd, uint32_t parent, uint32_t len, const uint32_t (&q)[FW]) {
-  uint32_t diff = (nd.parent ^ parent) | (nd.len ^ len);
+RL_HD inline bool confirm_f(const NodeF& nd, uint32_t parent, uint32_t len, const uint32_t (&q)[FW]) {
+  uint32_t diff = (nd.parent ^ parent) | ((nd.len_flags & 0xFFFFFFu) ^ len);
 #pragma unroll
   for (int k = 0; k < FW; ++k) {
     const int32_t rem = (int32_t)len - 4 * k;
@@ -417,112 +485,134 @@ RL_HD bool confirm(const NodeW& nd, uint32_t parent, uint32_t len, const uint32_
   }
   return diff == 0;
 }
-// first_match, and when the round neither matches nor ends (a probe chain longer than one round:
-// rare at load <= 1/8), the rest of the chain slot by slot: a miss is then settled exactly here
-// instead of sending the descriptor to the exact walk.
-RL_HD uint32_t match_chain(const TreeDesc2& t, uint32_t h, const uint64_t (&w)[TREE_PROBE]) {
+// the child whose hash is h (fast id), or TREE_NONE (at most one: build_fast_tree)
+RL_HD inline uint32_t child_of(const NodeF& nd, uint32_t h) {
+  uint32_t k = TREE_NONE;
+#pragma unroll
+  for (int j = FAST_CHILDREN - 1; j >= 0; --j) k = nd.ch[j] == h ? (uint32_t)j : k;
+  return k == TREE_NONE ? TREE_NONE : nd.first + k;
+}
+// the fast edge table: a probe round (4 slots from h's home), then the chain slot by slot when
+// the round neither matches nor ends (rare at load <= 1/8)
+RL_HD inline void probe_round_f(const Buf& b, uint32_t h, uint32_t mask, uint64_t (&w)[TREE_PROBE]) {
+  const uint32_t o = (h & mask) * 8u;
+  const uint4 a = bld4(b, o), c = bld4(b, o + 16u);
+  w[0] = (uint64_t)a.y << 32 | a.x; w[1] = (uint64_t)a.w << 32 | a.z;
+  w[2] = (uint64_t)c.y << 32 | c.x; w[3] = (uint64_t)c.w << 32 | c.z;
+}
+RL_HD uint32_t match_chain_f(const Buf& b, uint32_t mask, uint32_t h, const uint64_t (&w)[TREE_PROBE]) {
   bool done;
   const uint32_t c = first_match(w, h, done);
   if (c != TREE_NONE || done) return c;
-  uint32_t s = (h + TREE_PROBE) & t.mask;
-  for (uint32_t probes = TREE_PROBE; probes <= t.mask; ++probes, s = (s + 1) & t.mask) {
-    const uint64_t x = t.slots[s];
-    if ((uint32_t)x == TREE_EMPTY) break;
-    if ((uint32_t)(x >> 32) == h) return (uint32_t)x;
+  uint32_t s = (h + TREE_PROBE) & mask;
+  for (uint32_t probes = TREE_PROBE; probes <= mask; ++probes, s = (s + 1) & mask) {
+    const uint2 x = bld2(b, s * 8u);
+    if (x.x == TREE_EMPTY) break;
+    if (x.y == h) return x.x;
   }
   return TREE_NONE;
 }
-RL_HD uint4 load_entry(const ResolveIn& in, uint32_t e) {
-  return make_uint4(in.entry[4 * e], in.entry[4 * e + 1], in.entry[4 * e + 2], in.entry[4 * e + 3]);
-}
 
 // rule id of descriptor i (exact), or RS_EXACT: the exact walk (resolve_one) decides it.
-// Every load is unconditional (entries at clamped indices; ENT: the batch has entries at all).
-template <bool ENT>
-RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, uint32_t i) {
-  const uint32_t doff = in.domain[2 * i], dlen = in.domain[2 * i + 1];
-  const uint32_t e0 = in.entry_first[i], e1 = in.entry_first[i + 1];
-  const uint32_t ov = in.override_rule ? in.override_rule[i] : RL_NIL_RULE;
+RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, const FastBufs& B, uint32_t i) {
+  const uint2 dm = bld2(B.dom, 8u * i), ef = bld2(B.efirst, 4u * i);
+  const uint32_t ov = in.override_rule ? bld1(B.ovr, 4u * i) : RL_NIL_RULE;
+  const uint32_t doff = dm.x, dlen = dm.y, e0 = ef.x, e1 = ef.y;
   const uint64_t blen = in.bytes_len;
   if (!(e0 <= e1 && e1 <= in.n_entries) || (uint64_t)doff + dlen > blen) return RL_NIL_RULE;  // as resolve_one
   const bool aligned = (reinterpret_cast<uintptr_t>(in.bytes) & 3u) == 0;
-  const uint64_t bwords = blen & ~3ull;
-  // the register path: a 4-B aligned blob, <= FB bytes, the FWB bytes load_str_w reads inside it
-  auto reg_ok = [&](uint32_t o, uint32_t l) { return aligned && l <= FB && (uint64_t)(o & ~3u) + FWB <= blen; };
+  const uint64_t wlim = blen < RS_BUF_MAX ? blen : RS_BUF_MAX;
+  auto win_ok = [&](uint32_t o) { return (uint64_t)(o & ~3u) + FWB <= wlim; };  // the window lies inside
   auto inside = [&](uint32_t o, uint32_t l) { return (uint64_t)o + l <= blen; };
-  auto str_ok = [&](const uint4& x) { return reg_ok(x.x, x.y) && reg_ok(x.z, x.w) && x.y + 1u + x.w <= FB; };
-  auto str_in = [&](const uint4& x) { return inside(x.x, x.y) && inside(x.z, x.w); };
-  if (!reg_ok(doff, dlen) || blen < FWB) return RS_EXACT;  // (so a skipped string may read offset 0)
+  if (!aligned || dlen > FB || !win_ok(doff)) return RS_EXACT;
   const uint32_t n = e1 - e0;
-  const uint32_t elast = ENT ? in.n_entries - 1u : 0u;
-  auto entry_at = [&](uint32_t e) {  // entry e (clamped: read always, used only when e < e1)
-    return ENT ? load_entry(in, min(e, elast)) : make_uint4(0, 0, 0, 0);
+  // an entry's windows: key "_" value from the key's window when the value follows the key's
+  // separator, else the value's window too
+  auto joined_at = [](const uint4& x) { return x.z == x.x + x.y + 1u; };
+  auto load_strings = [&](const uint4& x, bool ld, uint32_t (&W)[FW + 1], uint32_t (&Vw)[FW + 1]) {
+    load_win(B.bytes, ld ? x.x & ~3u : RS_OOB, W);
+    load_win(B.bytes, ld && !joined_at(x) ? x.z & ~3u : RS_OOB, Vw);
   };
-  // round trip 1: the domain's dwords and the first two entries' words
+  // round trip 1: the domain's window and the first two entries' words
   uint32_t Q[FW];  // the name to confirm: the domain, then key ["_" value] of a level
-  load_str_w(in.bytes, doff, dlen, Q);
-  uint4 E = entry_at(e0);
-  uint4 En = entry_at(e0 + 1);
-  const uint32_t hd = tree_hash(RL_TREE_ROOT, fold_w(Q, dlen), dlen);
-  // round trip 2: the domain's probe round and level 0's strings
-  uint64_t w[TREE_PROBE];
-  probe_round(t, hd, w);
-  uint32_t K[FW], V[FW];
   {
-    const bool ld = n > 0 && str_ok(E);
-    load_str_w(in.bytes, ld ? E.x : 0u, ld ? E.y : 0u, K);
-    load_str_w(in.bytes, ld ? E.z : 0u, ld ? E.w : 0u, V);
+    uint32_t D[FW + 1];
+    load_win(B.bytes, doff & ~3u, D);
+    from_win(D, doff & 3u, dlen, Q);
   }
-  uint32_t pend = match_chain(t, hd, w);  // the node to confirm (parent pp, name Q[0, pl))
+  uint4 E = bld4(B.ent, n > 0 ? 16u * e0 : RS_OOB);
+  uint4 En = bld4(B.ent, n > 1 ? 16u * (e0 + 1u) : RS_OOB);
+  const uint32_t hd = fast_hash(RL_TREE_ROOT, fold_w(Q, dlen), dlen);
+  // round trip 2: the domain's probe round and level 0's windows
+  uint64_t w[TREE_PROBE];
+  probe_round_f(B.fslots, hd, t.fmask, w);
+  uint32_t W[FW + 1], Vw[FW + 1];
+  load_strings(E, n > 0, W, Vw);
+  uint32_t pend = match_chain_f(B.fslots, t.fmask, hd, w);  // the node to confirm (parent pp, name Q[0, pl))
   if (pend == TREE_NONE) return RL_NIL_RULE;  // unknown domain (:279-284)
   uint32_t pp = RL_TREE_ROOT, pl = dlen;
   if (ov != RL_NIL_RULE || n == 0) {  // override (:286-296), or no entries: the domain alone decides
-    if (!confirm(load_node_w(t, pend), pp, pl, Q)) return RS_EXACT;
+    if (!confirm_f(load_fnode(B.fnodes, pend), pp, pl, Q)) return RS_EXACT;
     return ov;
   }
-  uint32_t parent = pend;
   for (uint32_t l = 0; l < n; ++l) {
-    // level l: K / V hold entry l's strings, E its words, En entry l+1's
-    if (!str_in(E)) return RL_NIL_RULE;  // as resolve_one: a string outside bytes ends the walk nil
-    if (!str_ok(E)) return RS_EXACT;
-    const uint32_t kl = E.y, lv = kl + 1u + E.w;
-    uint32_t Qn[FW];
-    key_value_w(K, V, kl, Qn);
-    const uint32_t hv = tree_hash(parent, fold_w(Qn, lv), lv), hk = tree_hash(parent, fold_w(K, kl), kl);
-    // one round trip: both probe rounds, the pending node, level l+1's strings, entry l+2's words
-    uint64_t wv[TREE_PROBE], wk[TREE_PROBE];
-    probe_round(t, hv, wv);
-    probe_round(t, hk, wk);
-    const NodeW pv = load_node_w(t, pend);
-    {
-      const bool ld = l + 1 < n && str_ok(En);
-      load_str_w(in.bytes, ld ? En.x : 0u, ld ? En.y : 0u, K);
-      load_str_w(in.bytes, ld ? En.z : 0u, ld ? En.w : 0u, V);
+    // level l: W / Vw hold entry l's windows, E its words, En entry l+1's
+    const uint32_t ko = E.x, kl = E.y, vo = E.z, vl = E.w;
+    if (!inside(ko, kl) || !inside(vo, vl)) return RL_NIL_RULE;  // as resolve_one: the walk ends nil
+    const uint32_t lv = kl + 1u + vl;
+    const bool jn = joined_at(E);
+    if (kl > FB || vl > FB || lv > FB || !win_ok(ko) || (!jn && !win_ok(vo))) return RS_EXACT;
+    uint32_t Qn[FW], K[FW];
+    from_win(W, ko & 3u, lv, Qn);  // joined: the key's window holds key "_" value
+#pragma unroll
+    for (int k = 0; k < FW; ++k) K[k] = Qn[k];
+    mask_to(K, kl);
+    if (jn) {
+      uint32_t sep = 0;
+#pragma unroll
+      for (int k = 0; k < FW; ++k) sep = (uint32_t)k == (kl >> 2) ? Qn[k] : sep;
+      if (((sep >> (8u * (kl & 3u))) & 0xFFu) != (uint32_t)'_') return RS_EXACT;  // (its value window was not read)
+    } else {
+      uint32_t V[FW];
+      from_win(Vw, vo & 3u, vl, V);
+      key_value_w(K, V, kl, Qn);
     }
-    const uint4 Enn = entry_at(e0 + l + 2);
-    if (!confirm(pv, pp, pl, Q)) return RS_EXACT;
-    const uint32_t cv = match_chain(t, hv, wv);
+    const uint32_t hv = fast_hash(pend, fold_w(Qn, lv), lv), hk = fast_hash(pend, fold_w(K, kl), kl);
+    // one round trip: the pending node (its children's hashes), level l+1's windows, entry l+2's words
+    const NodeF nf = load_fnode(B.fnodes, pend);
+    load_strings(En, l + 1 < n, W, Vw);
+    const uint4 Enn = bld4(B.ent, l + 2 < n ? 16u * (e0 + l + 2u) : RS_OOB);
+    if (!confirm_f(nf, pp, pl, Q)) return RS_EXACT;
+    uint32_t cv, ck;
+    if (!(nf.len_flags & FAST_OVERFLOW)) {
+      cv = child_of(nf, hv);
+      ck = child_of(nf, hk);
+    } else {  // children in the fast edge table
+      uint64_t wv[TREE_PROBE], wk[TREE_PROBE];
+      probe_round_f(B.fslots, hv, t.fmask, wv);
+      probe_round_f(B.fslots, hk, t.fmask, wk);
+      cv = match_chain_f(B.fslots, t.fmask, hv, wv);
+      ck = match_chain_f(B.fslots, t.fmask, hk, wk);
+    }
     uint32_t nd;
     if (cv != TREE_NONE) {
       nd = cv;
       pl = lv;
     } else {
-      const uint32_t ck = match_chain(t, hk, wk);
       if (ck == TREE_NONE) return RL_NIL_RULE;  // neither edge: the walk stops (:309), nil
       nd = ck;
       pl = kl;
     }
 #pragma unroll
-    for (int k = 0; k < FW; ++k) Q[k] = Qn[k];  // (confirm masks it to pl bytes)
-    pp = parent;
+    for (int k = 0; k < FW; ++k) Q[k] = Qn[k];  // (confirm masks it to pl bytes; K is its first kl)
+    pp = pend;
     pend = nd;
-    parent = nd;
     E = En;
     En = Enn;
   }
   // the last entry's node: confirmed, and its limit (:311-318)
-  const NodeW v = load_node_w(t, pend);
-  if (!confirm(v, pp, pl, Q)) return RS_EXACT;
+  const NodeF v = load_fnode(B.fnodes, pend);
+  if (!confirm_f(v, pp, pl, Q)) return RS_EXACT;
   return v.rule;
 }
 
@@ -533,10 +623,13 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, uint32_t i)
 // the pass leaves CUs to the engine stream's kernels: k_resolve 90 -> 95 / 113 us, the step
 // slower; the engine stream at a higher priority than the front stream: no change.
 // flags[gridDim.x] = seq when any block raised its flag (this launch's number: no clearing).
-__global__ __launch_bounds__(RS_NT) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_resolve(
+#ifndef RL_RESOLVE_WAVES
+#define RL_RESOLVE_WAVES 6
+#endif
+__global__ __launch_bounds__(RS_NT) __attribute__((amdgpu_waves_per_eu(RL_RESOLVE_WAVES, RL_RESOLVE_WAVES))) void k_resolve(
     ResolveIn in, TreeDesc2 t, uint32_t* __restrict__ rule_out, uint32_t* __restrict__ flags, uint32_t seq) {
   const uint32_t i = blockIdx.x * RS_NT + threadIdx.x;
-  const uint32_t r = i >= in.n_desc ? 0u : in.n_entries ? resolve_fast<true>(in, t, i) : resolve_fast<false>(in, t, i);
+  const uint32_t r = i >= in.n_desc ? 0u : resolve_fast(in, t, fast_bufs(in, t), i);
   if (i < in.n_desc) rule_out[i] = r;
   const int any = __syncthreads_or(r == RS_EXACT);
   if (threadIdx.x == 0) {
@@ -563,7 +656,7 @@ __global__ __launch_bounds__(RS_NT) void k_resolve_exact(ResolveIn in, TreeDesc2
 // device code path checked against the config oracle without a GPU): the first pass, then the
 // exact walk for what it leaves. *exact (optional) tells which pass decided.
 uint32_t resolve_one_host(const ResolveIn& in, const TreeDesc2& t, uint32_t i, bool* exact) {
-  const uint32_t r = in.n_entries ? resolve_fast<true>(in, t, i) : resolve_fast<false>(in, t, i);
+  const uint32_t r = resolve_fast(in, t, fast_bufs(in, t), i);
   if (exact) *exact = r == RS_EXACT;
   return r == RS_EXACT ? resolve_one(in, t, i) : r;
 }
@@ -623,6 +716,71 @@ int build_tree(const rl_tree_node* nodes, uint32_t n, const uint8_t* names, uint
   }
   for (int j = 0; j < TREE_PROBE - 1; ++j) out_slots[cap + j] = out_slots[j];  // probe rounds never wrap
   return 0;
+}
+
+static uint32_t name_fold(const uint8_t* names, uint32_t off, uint32_t len) {
+  uint32_t f = TREE_FOLD0, w = 0;
+  for (uint32_t k = 0; k < len; ++k) {
+    w |= (uint32_t)names[off + k] << (8 * (k & 3));
+    if ((k & 3) == 3 || k + 1 == len) {
+      f = tree_fold_word(f, w);
+      w = 0;
+    }
+  }
+  return f;
+}
+
+// Breadth-first ids (the domains first, then each node's children together, in id order), the
+// children's hashes inline, overflow children and the domains in the fast edge table.
+void build_fast_tree(const std::vector<TreeNodeDev>& nodes, const uint8_t* names, std::vector<FastNode>& out_nodes,
+                     std::vector<uint64_t>& out_slots, uint32_t& mask, std::vector<uint32_t>* fast_id) {
+  const uint32_t n = (uint32_t)nodes.size();
+  std::vector<std::vector<uint32_t>> kids(n);
+  std::vector<uint32_t> order, fid(n, TREE_NONE);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (nodes[i].parent == RL_TREE_ROOT) order.push_back(i);
+    else kids[nodes[i].parent].push_back(i);  // (build_tree: parents precede their children)
+  }
+  for (size_t q = 0; q < order.size(); ++q)
+    for (uint32_t c : kids[order[q]]) order.push_back(c);
+  for (uint32_t f = 0; f < n; ++f) fid[order[f]] = f;
+  out_nodes.assign(n, FastNode{});
+  std::vector<std::pair<uint32_t, uint32_t>> edges;  // (fast hash, fast id) for the edge table
+  for (uint32_t f = 0; f < n; ++f) {
+    const TreeNodeDev& d = nodes[order[f]];
+    FastNode& x = out_nodes[f];
+    x.parent = d.parent == RL_TREE_ROOT ? RL_TREE_ROOT : fid[d.parent];
+    x.len_flags = std::min<uint32_t>(d.name_len, 0xFFFFFFu);
+    x.rule = d.rule;
+    for (int k = 0; k < 4; ++k) x.name[k] = d.name[k];
+    for (int k = 0; k < FAST_CHILDREN; ++k) x.chash[k] = FAST_NO_CHILD;
+    const std::vector<uint32_t>& ks = kids[order[f]];
+    x.first_child = ks.empty() ? 0u : fid[ks[0]];
+    std::vector<uint32_t> hs;
+    for (uint32_t c : ks) hs.push_back(fast_hash(f, name_fold(names, nodes[c].name_off, nodes[c].name_len), nodes[c].name_len));
+    bool over = ks.size() > (size_t)FAST_CHILDREN;
+    for (size_t a = 0; a < hs.size() && !over; ++a)
+      for (size_t b = a + 1; b < hs.size(); ++b) over |= hs[a] == hs[b];
+    if (over) {
+      x.len_flags |= FAST_OVERFLOW;
+      for (size_t k = 0; k < ks.size(); ++k) edges.emplace_back(hs[k], fid[ks[k]]);
+    } else {
+      for (size_t k = 0; k < ks.size(); ++k) x.chash[k] = hs[k];
+    }
+    if (d.parent == RL_TREE_ROOT)
+      edges.emplace_back(fast_hash(RL_TREE_ROOT, name_fold(names, d.name_off, d.name_len), d.name_len), f);
+  }
+  uint32_t cap = 16;
+  while (cap < 8u * (uint32_t)edges.size()) cap <<= 1;  // load <= 1/8, as the exact walk's table
+  out_slots.assign(cap + TREE_PROBE - 1, ~0ull);
+  mask = cap - 1;
+  for (const auto& e : edges) {
+    uint32_t s = e.first & mask;
+    while ((uint32_t)out_slots[s] != TREE_EMPTY) s = (s + 1) & mask;
+    out_slots[s] = (uint64_t)e.first << 32 | e.second;
+  }
+  for (int j = 0; j < TREE_PROBE - 1; ++j) out_slots[cap + j] = out_slots[j];  // probe rounds never wrap
+  if (fast_id) *fast_id = fid;
 }
 
 void launch_resolve(hipStream_t st, const ResolveIn& in, const TreeDesc2& t, uint32_t* rule_out, uint32_t* flags,

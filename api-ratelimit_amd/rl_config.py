@@ -137,9 +137,15 @@ class RateLimitConfig:
 
 
 class ResolveBatch:
-    """One rl_resolve_batch: descriptors [(domain, [(key, value)...], override_rule or None)]."""
+    """One rl_resolve_batch: descriptors [(domain, [(key, value)...], override_rule or None)].
 
-    def __init__(self, descs: Sequence[Tuple[str, Sequence[Tuple[str, str]], Optional[int]]]):
+    layout "dedup": each distinct string once in the blob. "prefix": each descriptor's strings
+    inside its own cache-key prefix, domain "_" key "_" value "_" ... (the bytes a batch
+    submits anyway), so every entry's value follows its key's separator (sep: that separator,
+    "_" as the key format has it; tests vary it)."""
+
+    def __init__(self, descs: Sequence[Tuple[str, Sequence[Tuple[str, str]], Optional[int]]], layout: str = "dedup",
+                 sep: str = "_"):
         buf = bytearray()
         cache: Dict[str, Tuple[int, int]] = {}
 
@@ -152,11 +158,28 @@ class ResolveBatch:
                 cache[s] = r
             return r
 
+        def put_here(s: str) -> Tuple[int, int]:
+            b = s.encode()
+            r = (len(buf), len(b))
+            buf.extend(b)
+            return r
+
+        if layout not in ("dedup", "prefix"):
+            raise ValueError(f"layout {layout!r}")
         dom, first, ent, ov = [], [0], [], []
         for domain, entries, override in descs:
-            dom.extend(put(domain))
-            for k, v in entries:
-                ent.extend(put(k) + put(v))
+            if layout == "prefix":
+                dom.extend(put_here(domain))
+                for k, v in entries:
+                    buf.extend(b"_")
+                    kr = put_here(k)
+                    buf.extend(sep.encode())
+                    ent.extend(kr + put_here(v))
+                buf.extend(b"_")
+            else:
+                dom.extend(put(domain))
+                for k, v in entries:
+                    ent.extend(put(k) + put(v))
             first.append(len(ent) // 4)
             ov.append(hiprl.NIL_RULE if override is None else int(override))
         self.bytes = np.frombuffer(bytes(buf) + b"\0" * 16, np.uint8)

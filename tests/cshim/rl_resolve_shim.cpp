@@ -17,7 +17,11 @@ extern "C" int rls_resolve2(const rl_tree_node* nodes, uint32_t n_nodes, const u
   std::string err;
   const int rc = rlhip::build_tree(nodes, n_nodes, names, names_len, hn, hs, mask, err);
   if (rc) return rc;
-  const rlhip::TreeDesc2 t{hn.data(), hs.data(), names, mask};
+  std::vector<rlhip::FastNode> fn;
+  std::vector<uint64_t> fs;
+  uint32_t fmask = 0;
+  rlhip::build_fast_tree(hn, names, fn, fs, fmask);
+  const rlhip::TreeDesc2 t{hn.data(), hs.data(), names, mask, fn.data(), fs.data(), fmask, (uint32_t)fn.size()};
   const rlhip::ResolveIn in{b->n_desc, b->n_entries, b->bytes_len, b->bytes, b->domain,
                             b->entry_first, b->entry, b->override_rule};
   for (uint32_t i = 0; i < b->n_desc; ++i) {
@@ -42,4 +46,23 @@ extern "C" uint32_t rls_tree_hash(uint32_t parent, const uint8_t* name, uint32_t
     }
   }
   return rlhip::tree_hash(parent, f, len);
+}
+// fast_hash(parent, fold(name), len): the first pass's edge hash (parent = a fast id)
+extern "C" uint32_t rls_fast_hash(uint32_t parent, const uint8_t* name, uint32_t len) {
+  return rls_tree_hash(parent, name, len) & ~1u;
+}
+// The first pass's (breadth-first) id of tree node `id`, or 0xFFFFFFFF on a bad tree.
+extern "C" uint32_t rls_fast_id(const rl_tree_node* nodes, uint32_t n_nodes, const uint8_t* names, uint32_t names_len,
+                                uint32_t id) {
+  std::vector<rlhip::TreeNodeDev> hn;
+  std::vector<uint64_t> hs;
+  uint32_t mask = 0;
+  std::string err;
+  if (rlhip::build_tree(nodes, n_nodes, names, names_len, hn, hs, mask, err) || id >= n_nodes) return 0xFFFFFFFFu;
+  std::vector<rlhip::FastNode> fn;
+  std::vector<uint64_t> fs;
+  std::vector<uint32_t> fid;
+  uint32_t fmask = 0;
+  rlhip::build_fast_tree(hn, names, fn, fs, fmask, &fid);
+  return fid[id];
 }

@@ -142,7 +142,9 @@ def test_strings_outside_bytes_resolve_nil(shim):
 
 
 # ---- k_resolve's two passes: the level-pipelined walk, then the exact walk for what it leaves ----
-def _resolve2(lib, cfg, rb, mode=0):
+def _resolve2(lib, cfg, rb, mode=0, pad=0):
+    """(rules, which descriptors the exact walk decided); pad: zero bytes after the blob, so no
+    string's load window passes its end."""
     lib.rls_resolve2.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.POINTER(hiprl.RlResolveBatch),
                                  C.c_void_p, C.c_void_p, C.c_int]
     lib.rls_resolve2.restype = C.c_int
@@ -150,6 +152,9 @@ def _resolve2(lib, cfg, rb, mode=0):
     nodes = np.ascontiguousarray(nodes, np.uint32)
     nb = np.frombuffer(names or b"\0", np.uint8)
     s = rb.struct()
+    raw = np.concatenate([rb.bytes, np.zeros(pad, np.uint8)])
+    if pad:
+        s.bytes, s.bytes_len = raw.ctypes.data, s.bytes_len + pad
     out = np.zeros(max(1, rb.n_desc), np.uint32)
     ex = np.zeros(max(1, rb.n_desc), np.uint8)
     rc = lib.rls_resolve2(nodes.ctypes.data, nodes.shape[0], nb.ctypes.data, len(names), C.byref(s), out.ctypes.data,
@@ -158,15 +163,17 @@ def _resolve2(lib, cfg, rb, mode=0):
     return out[:rb.n_desc], ex[:rb.n_desc].astype(bool)
 
 
-def _colliding(lib, parent, make, count=400_000):
-    """Two distinct names make(i), make(j) with equal tree_hash under parent (a birthday search
-    over the device's 32-bit edge hash)."""
-    lib.rls_tree_hash.argtypes = [C.c_uint32, C.c_char_p, C.c_uint32]
-    lib.rls_tree_hash.restype = C.c_uint32
+def _colliding(lib, parent, make, count=400_000, fn="rls_tree_hash"):
+    """Two distinct names make(i), make(j) with equal edge hash under parent (a birthday search
+    over the device's 32-bit edge hash: the exact walk's tree_hash over tree ids, or with
+    fn="rls_fast_hash" the first pass's fast_hash over its breadth-first ids)."""
+    f = getattr(lib, fn)
+    f.argtypes = [C.c_uint32, C.c_char_p, C.c_uint32]
+    f.restype = C.c_uint32
     seen = {}
     for i in range(count):
         n = make(i).encode()
-        h = lib.rls_tree_hash(parent, n, len(n))
+        h = f(parent, n, len(n))
         if h in seen:
             return seen[h], i
         seen[h] = i
@@ -200,16 +207,30 @@ def test_config4_first_pass_decides_and_agrees(shim, seed):
         assert have == (None if w is None else (w.requests_per_unit, w.unit)), (d, e)
 
 
-def test_edge_hash_collisions_take_the_exact_walk(shim):
-    """Sibling names whose 32-bit edge hashes collide: the first pass takes a probe round's first
+def _fast_id(lib, cfg, node):
+    lib.rls_fast_id.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]
+    lib.rls_fast_id.restype = C.c_uint32
+    nodes, names = cfg.tree_arrays()
+    nodes = np.ascontiguousarray(nodes, np.uint32)
+    nb = np.frombuffer(names or b"\0", np.uint8)
+    return lib.rls_fast_id(nodes.ctypes.data, nodes.shape[0], nb.ctypes.data, len(names), node)
+
+
+@pytest.mark.parametrize("walk", ["fast", "exact"])
+def test_edge_hash_collisions_take_the_exact_walk(shim, walk):
+    """Sibling names whose 32-bit edge hashes collide. fast: under the first pass's hash, so the
+    domain keeps its children in the fast edge table; the first pass takes a probe round's first
     hash match unconfirmed, finds the other name when it confirms the node, and leaves the
-    descriptor to the exact walk; answers equal the oracle's (key/value nodes, key-only nodes, a
+    descriptor to the exact walk. exact: under the exact walk's hash, so its own probe meets the
+    collision. Either way the answers equal the oracle's (key/value nodes, key-only nodes, a
     colliding name absent from the tree, a collision one level down)."""
     probe = rl_config.RateLimitConfig([("p.yaml", "domain: dc\ndescriptors:\n  - key: a\n    value: x\n")])
     nodes, _ = probe.tree_arrays()
     dom = int(np.nonzero(nodes[:, 0] == 0xFFFFFFFF)[0][0])
-    ci, cj = _colliding(shim, dom, lambda k: f"a_{_mix(k)}")
-    cp, cq = _colliding(shim, dom, lambda k: f"k{_mix(k)}")
+    fn = "rls_fast_hash" if walk == "fast" else "rls_tree_hash"
+    par = _fast_id(shim, probe, dom) if walk == "fast" else dom
+    ci, cj = _colliding(shim, par, lambda k: f"a_{_mix(k)}", fn=fn)
+    cp, cq = _colliding(shim, par, lambda k: f"k{_mix(k)}", fn=fn)
     i, j, p, q = _mix(ci), _mix(cj), _mix(cp), _mix(cq)
     y = (
         "domain: dc\n"
@@ -232,14 +253,66 @@ def test_edge_hash_collisions_take_the_exact_walk(shim):
     orc = config_oracle.Config(files_)
     nodes2, _ = cfg.tree_arrays()
     assert int(np.nonzero(nodes2[:, 0] == 0xFFFFFFFF)[0][0]) == dom  # the hashes were searched under this parent
+    assert walk != "fast" or _fast_id(shim, cfg, dom) == par
     descs = [("dc", [("a", str(i))]), ("dc", [("a", str(j))]), ("dc", [("a", "nope")]), ("dc", [(f"k{p}", "v")]),
              ("dc", [(f"k{q}", "v")]), ("dc", [("a", str(i)), ("b", "z")]), ("dc", [("a", str(j)), ("b", "z")]),
              ("dd", [("a", str(j))]), ("dd", [("a", str(i))]), ("dc", [(f"k{q}", "v"), ("b", "z")])]
-    got, ex = _resolve2(shim, cfg, rl_config.ResolveBatch([(d, e, None) for d, e in descs]))
+    got, ex = _resolve2(shim, cfg, rl_config.ResolveBatch([(d, e, None) for d, e in descs]), pad=32)
     exact, _ = _resolve2(shim, cfg, rl_config.ResolveBatch([(d, e, None) for d, e in descs]), mode=1)
     assert np.array_equal(got, exact)
-    assert ex.any()  # at least one colliding lookup confirmed the wrong node and went to the exact walk
+    if walk == "fast":  # a colliding lookup that met the other name first went to the exact walk
+        assert ex.any()
     for (d, e), r in zip(descs, got):
         w = orc.get_limit(d, e)
         have = None if r == hiprl.NIL_RULE else (cfg.rules[int(r)].requests_per_unit, cfg.rules[int(r)].unit)
         assert have == (None if w is None else (w.requests_per_unit, w.unit)), (d, e)
+
+
+def _wide_yaml():
+    """A domain with 20 key/value children (more than a fast node holds inline: its children go
+    to the fast edge table), a node with exactly 8 children (inline), nested levels under both."""
+    lines = ["domain: wide", "descriptors:"]
+    for v in range(20):
+        lines += [f"  - key: k", f"    value: \"v{v}\"", f"    rate_limit: {{unit: second, requests_per_unit: {v + 1}}}"]
+        if v % 5 == 0:
+            lines += ["    descriptors:"]
+            for c in range(7):
+                lines += [f"      - key: s", f"        value: \"{c}\"",
+                          f"        rate_limit: {{unit: minute, requests_per_unit: {100 + 10 * v + c}}}"]
+            lines += ["      - key: s", "        rate_limit: {unit: hour, requests_per_unit: 7}"]
+    lines += ["  - key: k", "    rate_limit: {unit: day, requests_per_unit: 999}"]
+    return "\n".join(lines) + "\n"
+
+
+@pytest.mark.parametrize("layout,sep", [("prefix", "_"), ("prefix", ":"), ("dedup", "_")])
+def test_fast_tree_layouts_and_overflow(shim, layout, sep):
+    """The first pass over its breadth-first tree: a domain whose 20 children live in the fast
+    edge table, a node with 8 inline children, misses at both; descriptors laid out as cache-key
+    prefixes (key "_" value joined: one load window per entry), the same with another separator
+    (the walk must not take key ":" value for key "_" value: it leaves them to the exact walk), and
+    deduplicated strings. Answers equal the exact walk's and the oracle's; with the key format's
+    own separator the first pass decides everything."""
+    y = _wide_yaml()
+    cfg = rl_config.RateLimitConfig([("w.yaml", y)])
+    orc = config_oracle.Config([("w.yaml", y)])
+    rng = np.random.default_rng(7)
+    descs = []
+    for _ in range(3000):
+        ents = [("k", f"v{int(rng.integers(0, 24))}")]
+        if rng.random() < 0.7:
+            ents.append(("s", str(int(rng.integers(0, 10)))))
+        if rng.random() < 0.1:
+            ents.append(("t", "x"))
+        descs.append(("wide" if rng.random() < 0.97 else "narrow", ents))
+    rb = rl_config.ResolveBatch([(d, e, None) for d, e in descs], layout=layout, sep=sep)
+    got, ex = _resolve2(shim, cfg, rb, pad=32)
+    exact, _ = _resolve2(shim, cfg, rb, mode=1)
+    assert np.array_equal(got, exact)
+    for (d, e), r in zip(descs, got):
+        w = orc.get_limit(d, e)
+        have = None if r == hiprl.NIL_RULE else (cfg.rules[int(r)].requests_per_unit, cfg.rules[int(r)].unit)
+        assert have == (None if w is None else (w.requests_per_unit, w.unit)), (d, e)
+    if sep == "_":
+        assert not ex.any()
+    else:  # a joined-looking entry with another separator: left to the exact walk, never misread
+        assert ex.mean() > 0.5
