@@ -327,6 +327,12 @@ RL_HD uint32_t resolve_one(const ResolveIn& in, const TreeDesc2& t, uint32_t i) 
 //     :320-325); this walk goes on and looks the next entry up among no children, misses and
 //     stops there with the same (nil) result.
 constexpr uint32_t RS_EXACT = 0xFFFFFFFEu;  // first pass: left to the exact walk
+#ifndef RL_RESOLVE_PF
+// levels ahead that a level's string windows are loaded. Measured (config 4, one box, interleaved):
+// 2 (entries three ahead, 76 VGPRs) 55.6-56.1 us against 53.8-55.1 for 1; never reading the value
+// windows (other layouts to the exact walk) saves about 2 us more: not worth a second kernel.
+#define RL_RESOLVE_PF 1
+#endif
 #ifndef RL_RESOLVE_FW
 #define RL_RESOLVE_FW 4
 #endif
@@ -542,12 +548,19 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, const FastB
   }
   uint4 E = bld4(B.ent, n > 0 ? 16u * e0 : RS_OOB);
   uint4 En = bld4(B.ent, n > 1 ? 16u * (e0 + 1u) : RS_OOB);
+#if RL_RESOLVE_PF == 2
+  uint4 Enn = bld4(B.ent, n > 2 ? 16u * (e0 + 2u) : RS_OOB);
+#endif
   const uint32_t hd = fast_hash(RL_TREE_ROOT, fold_w(Q, dlen), dlen);
   // round trip 2: the domain's probe round and level 0's windows
   uint64_t w[TREE_PROBE];
   probe_round_f(B.fslots, hd, t.fmask, w);
   uint32_t W[FW + 1], Vw[FW + 1];
   load_strings(E, n > 0, W, Vw);
+#if RL_RESOLVE_PF == 2
+  uint32_t W2[FW + 1], Vw2[FW + 1];  // level l+1's windows
+  load_strings(En, n > 1, W2, Vw2);
+#endif
   uint32_t pend = match_chain_f(B.fslots, t.fmask, hd, w);  // the node to confirm (parent pp, name Q[0, pl))
   if (pend == TREE_NONE) return RL_NIL_RULE;  // unknown domain (:279-284)
   uint32_t pp = RL_TREE_ROOT, pl = dlen;
@@ -578,10 +591,17 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, const FastB
       key_value_w(K, V, kl, Qn);
     }
     const uint32_t hv = fast_hash(pend, fold_w(Qn, lv), lv), hk = fast_hash(pend, fold_w(K, kl), kl);
+#if RL_RESOLVE_PF == 2
+    // one round trip: the pending node (its children's hashes), level l+2's windows, entry l+3's words
+    const NodeF nf = load_fnode(B.fnodes, pend);
+    load_strings(Enn, l + 2 < n, W, Vw);
+    const uint4 Ennn = bld4(B.ent, l + 3 < n ? 16u * (e0 + l + 3u) : RS_OOB);
+#else
     // one round trip: the pending node (its children's hashes), level l+1's windows, entry l+2's words
     const NodeF nf = load_fnode(B.fnodes, pend);
     load_strings(En, l + 1 < n, W, Vw);
     const uint4 Enn = bld4(B.ent, l + 2 < n ? 16u * (e0 + l + 2u) : RS_OOB);
+#endif
     if (!confirm_f(nf, pp, pl, Q)) return RS_EXACT;
     uint32_t cv, ck;
     if (!(nf.len_flags & FAST_OVERFLOW)) {
@@ -609,6 +629,17 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, const FastB
     pend = nd;
     E = En;
     En = Enn;
+#if RL_RESOLVE_PF == 2
+    Enn = Ennn;
+#pragma unroll
+    for (int k = 0; k <= FW; ++k) {  // (W now holds level l+2's windows: rotate)
+      const uint32_t a = W[k], b = Vw[k];
+      W[k] = W2[k];
+      Vw[k] = Vw2[k];
+      W2[k] = a;
+      Vw2[k] = b;
+    }
+#endif
   }
   // the last entry's node: confirmed, and its limit (:311-318)
   const NodeF v = load_fnode(B.fnodes, pend);
