@@ -106,8 +106,6 @@ RL_HD inline uint32_t align_byte(uint32_t hi, uint32_t lo, uint32_t sh) {
   return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh));
 #endif
 }
-// the low n bytes of a word (n <= 4): one shift and a select
-RL_HD inline uint32_t low_bytes_mask(uint32_t n) { return n ? 0xFFFFFFFFu >> (32u - 8u * n) : 0u; }
 // s[k] = bytes 4k..4k+3 of the string at bytes + off (little-endian), zero past len (<= SB).
 // The blob is 4-B aligned and the string's last dword lies inside it (checked by the caller):
 // whole-dword loads at clamped indices, all in flight together.
@@ -327,12 +325,9 @@ RL_HD uint32_t resolve_one(const ResolveIn& in, const TreeDesc2& t, uint32_t i) 
 //     :320-325); this walk goes on and looks the next entry up among no children, misses and
 //     stops there with the same (nil) result.
 constexpr uint32_t RS_EXACT = 0xFFFFFFFEu;  // first pass: left to the exact walk
-#ifndef RL_RESOLVE_PF
-// levels ahead that a level's string windows are loaded. Measured (config 4, one box, interleaved):
-// 2 (entries three ahead, 76 VGPRs) 55.6-56.1 us against 53.8-55.1 for 1; never reading the value
-// windows (other layouts to the exact walk) saves about 2 us more: not worth a second kernel.
-#define RL_RESOLVE_PF 1
-#endif
+// (Measured and not kept, config 4, one box, interleaved: the string windows two levels ahead
+// instead of one, entries three ahead, 76 VGPRs: k_resolve 55.6-56.1 us against 53.8-55.1; never
+// reading value windows (other layouts to the exact walk) saves about 2 us more.)
 #ifndef RL_RESOLVE_FW
 #define RL_RESOLVE_FW 4
 #endif
@@ -420,28 +415,35 @@ RL_HD inline void load_win(const Buf& b, uint32_t off, uint32_t (&d)[FW + 1]) {
   d[0] = a.x; d[1] = a.y; d[2] = a.z; d[3] = a.w;
   d[4] = bld1(b, off + 16u);
 }
-// s[k] = bytes 4k..4k+3 of the window's string at byte sh of its first dword, zero past len
-RL_HD inline void from_win(const uint32_t (&d)[FW + 1], uint32_t sh, uint32_t len, uint32_t (&s)[FW]) {
+// s[k] = bytes 4k..4k+3 of the window from byte sh of its first dword (not masked)
+RL_HD inline void win_words(const uint32_t (&d)[FW + 1], uint32_t sh, uint32_t (&s)[FW]) {
+#pragma unroll
+  for (int k = 0; k < FW; ++k) s[k] = align_byte(d[k + 1], d[k], sh);
+}
+// m[k] = the bytes of word k that lie below len (len <= FB)
+RL_HD inline void len_masks(uint32_t len, uint32_t (&m)[FW]) {
 #pragma unroll
   for (int k = 0; k < FW; ++k) {
-    const int32_t rem = (int32_t)len - 4 * k;
-    const uint32_t nb = rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem;
-    s[k] = align_byte(d[k + 1], d[k], sh) & low_bytes_mask(nb);
+    const uint32_t b = min(max((int32_t)(8u * len) - 32 * k, 0), 32);  // bits of word k in the name
+    m[k] = b >= 32u ? 0xFFFFFFFFu : (1u << b) - 1u;
   }
 }
-RL_HD inline void mask_to(uint32_t (&s)[FW], uint32_t len) {
-#pragma unroll
-  for (int k = 0; k < FW; ++k) {
-    const int32_t rem = (int32_t)len - 4 * k;
-    s[k] &= low_bytes_mask(rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem);
-  }
+RL_HD inline bool any_lane(bool p) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __any(p);
+#else
+  return p;
+#endif
 }
-RL_HD uint32_t fold_w(const uint32_t (&s)[FW], uint32_t len) {  // = fold_reg for len <= FB
-  uint32_t h = TREE_FOLD0;
+// = fold_reg for len <= FB; a word no lane of the wave needs is skipped (config 4's keys are one
+// word, its key "_" value names three)
+RL_HD uint32_t fold_w(const uint32_t (&s)[FW], uint32_t len) {
+  uint32_t h = tree_fold_word(TREE_FOLD0, s[0]);
+  h = len ? h : TREE_FOLD0;
   const uint32_t nw = (len + 3u) >> 2;
 #pragma unroll
-  for (int k = 0; k < FW; ++k)
-    if ((uint32_t)k < nw) h = tree_fold_word(h, s[k]);
+  for (int k = 1; k < FW; ++k)
+    if (any_lane((uint32_t)k < nw)) h = (uint32_t)k < nw ? tree_fold_word(h, s[k]) : h;
   return h;
 }
 // r = K "_" V (finalKey, config_impl.go:300): V moved kl + 1 bytes up (kl + 1 <= FB), then K and
@@ -479,16 +481,11 @@ RL_HD inline NodeF load_fnode(const Buf& b, uint32_t id) {
   v.ch[4] = c1.x; v.ch[5] = c1.y; v.ch[6] = c1.z; v.ch[7] = c1.w;
   return v;
 }
-// the node against (parent, len, the first len bytes of q): q may hold more bytes past len (a
-// key checked against key "_" value), masked here; len <= FB
+// the node against (parent, len, q): q is zero past len (<= FB), as the node's inline name is
 RL_HD inline bool confirm_f(const NodeF& nd, uint32_t parent, uint32_t len, const uint32_t (&q)[FW]) {
   uint32_t diff = (nd.parent ^ parent) | ((nd.len_flags & 0xFFFFFFu) ^ len);
 #pragma unroll
-  for (int k = 0; k < FW; ++k) {
-    const int32_t rem = (int32_t)len - 4 * k;
-    const uint32_t nb = rem <= 0 ? 0u : rem >= 4 ? 4u : (uint32_t)rem;
-    diff |= nd.name[k] ^ (q[k] & low_bytes_mask(nb));
-  }
+  for (int k = 0; k < FW; ++k) diff |= nd.name[k] ^ q[k];
   return diff == 0;
 }
 // the child whose hash is h (fast id), or TREE_NONE (at most one: build_fast_tree)
@@ -524,12 +521,15 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, const FastB
   const uint2 dm = bld2(B.dom, 8u * i), ef = bld2(B.efirst, 4u * i);
   const uint32_t ov = in.override_rule ? bld1(B.ovr, 4u * i) : RL_NIL_RULE;
   const uint32_t doff = dm.x, dlen = dm.y, e0 = ef.x, e1 = ef.y;
-  const uint64_t blen = in.bytes_len;
-  if (!(e0 <= e1 && e1 <= in.n_entries) || (uint64_t)doff + dlen > blen) return RL_NIL_RULE;  // as resolve_one
+  const uint32_t blen = in.bytes_len;
+  // (32-bit bounds: o + l <= blen without the sum overflowing)
+  auto inside = [&](uint32_t o, uint32_t l) { return o <= blen && l <= blen - o; };
+  if (!(e0 <= e1 && e1 <= in.n_entries) || !inside(doff, dlen)) return RL_NIL_RULE;  // as resolve_one
   const bool aligned = (reinterpret_cast<uintptr_t>(in.bytes) & 3u) == 0;
-  const uint64_t wlim = blen < RS_BUF_MAX ? blen : RS_BUF_MAX;
-  auto win_ok = [&](uint32_t o) { return (uint64_t)(o & ~3u) + FWB <= wlim; };  // the window lies inside
-  auto inside = [&](uint32_t o, uint32_t l) { return (uint64_t)o + l <= blen; };
+  const uint32_t wlim = (blen < RS_BUF_MAX ? blen : RS_BUF_MAX);
+  const uint32_t wmax = wlim >= FWB ? wlim - FWB : 0u;  // the last aligned start whose window lies inside
+  const bool wany = wlim >= FWB;
+  auto win_ok = [&](uint32_t o) { return wany && (o & ~3u) <= wmax; };
   if (!aligned || dlen > FB || !win_ok(doff)) return RS_EXACT;
   const uint32_t n = e1 - e0;
   // an entry's windows: key "_" value from the key's window when the value follows the key's
@@ -540,28 +540,24 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, const FastB
     load_win(B.bytes, ld && !joined_at(x) ? x.z & ~3u : RS_OOB, Vw);
   };
   // round trip 1: the domain's window and the first two entries' words
-  uint32_t Q[FW];  // the name to confirm: the domain, then key ["_" value] of a level
+  uint32_t Q[FW];  // the name to confirm, zero past its length: the domain, then a level's name
   {
-    uint32_t D[FW + 1];
+    uint32_t D[FW + 1], M[FW];
     load_win(B.bytes, doff & ~3u, D);
-    from_win(D, doff & 3u, dlen, Q);
+    len_masks(dlen, M);
+    win_words(D, doff & 3u, Q);
+#pragma unroll
+    for (int k = 0; k < FW; ++k) Q[k] &= M[k];
   }
   uint4 E = bld4(B.ent, n > 0 ? 16u * e0 : RS_OOB);
   uint4 En = bld4(B.ent, n > 1 ? 16u * (e0 + 1u) : RS_OOB);
-#if RL_RESOLVE_PF == 2
-  uint4 Enn = bld4(B.ent, n > 2 ? 16u * (e0 + 2u) : RS_OOB);
-#endif
   const uint32_t hd = fast_hash(RL_TREE_ROOT, fold_w(Q, dlen), dlen);
   // round trip 2: the domain's probe round and level 0's windows
   uint64_t w[TREE_PROBE];
   probe_round_f(B.fslots, hd, t.fmask, w);
   uint32_t W[FW + 1], Vw[FW + 1];
   load_strings(E, n > 0, W, Vw);
-#if RL_RESOLVE_PF == 2
-  uint32_t W2[FW + 1], Vw2[FW + 1];  // level l+1's windows
-  load_strings(En, n > 1, W2, Vw2);
-#endif
-  uint32_t pend = match_chain_f(B.fslots, t.fmask, hd, w);  // the node to confirm (parent pp, name Q[0, pl))
+  uint32_t pend = match_chain_f(B.fslots, t.fmask, hd, w);  // the node to confirm (parent pp, name Q, length pl)
   if (pend == TREE_NONE) return RL_NIL_RULE;  // unknown domain (:279-284)
   uint32_t pp = RL_TREE_ROOT, pl = dlen;
   if (ov != RL_NIL_RULE || n == 0) {  // override (:286-296), or no entries: the domain alone decides
@@ -575,33 +571,34 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, const FastB
     const uint32_t lv = kl + 1u + vl;
     const bool jn = joined_at(E);
     if (kl > FB || vl > FB || lv > FB || !win_ok(ko) || (!jn && !win_ok(vo))) return RS_EXACT;
-    uint32_t Qn[FW], K[FW];
-    from_win(W, ko & 3u, lv, Qn);  // joined: the key's window holds key "_" value
+    // Qn = key "_" value and K = key, zero past their lengths (joined: both from the key's window)
+    uint32_t S[FW], Mk[FW], Qn[FW], K[FW];
+    win_words(W, ko & 3u, S);
+    len_masks(kl, Mk);
 #pragma unroll
-    for (int k = 0; k < FW; ++k) K[k] = Qn[k];
-    mask_to(K, kl);
+    for (int k = 0; k < FW; ++k) K[k] = S[k] & Mk[k];
     if (jn) {
-      uint32_t sep = 0;
+      uint32_t Mv[FW], sep = 0;
+      len_masks(lv, Mv);
 #pragma unroll
-      for (int k = 0; k < FW; ++k) sep = (uint32_t)k == (kl >> 2) ? Qn[k] : sep;
+      for (int k = 0; k < FW; ++k) {
+        Qn[k] = S[k] & Mv[k];
+        sep = (uint32_t)k == (kl >> 2) ? S[k] : sep;
+      }
       if (((sep >> (8u * (kl & 3u))) & 0xFFu) != (uint32_t)'_') return RS_EXACT;  // (its value window was not read)
     } else {
-      uint32_t V[FW];
-      from_win(Vw, vo & 3u, vl, V);
+      uint32_t V[FW], Mv[FW];
+      win_words(Vw, vo & 3u, V);
+      len_masks(vl, Mv);
+#pragma unroll
+      for (int k = 0; k < FW; ++k) V[k] &= Mv[k];
       key_value_w(K, V, kl, Qn);
     }
     const uint32_t hv = fast_hash(pend, fold_w(Qn, lv), lv), hk = fast_hash(pend, fold_w(K, kl), kl);
-#if RL_RESOLVE_PF == 2
-    // one round trip: the pending node (its children's hashes), level l+2's windows, entry l+3's words
-    const NodeF nf = load_fnode(B.fnodes, pend);
-    load_strings(Enn, l + 2 < n, W, Vw);
-    const uint4 Ennn = bld4(B.ent, l + 3 < n ? 16u * (e0 + l + 3u) : RS_OOB);
-#else
     // one round trip: the pending node (its children's hashes), level l+1's windows, entry l+2's words
     const NodeF nf = load_fnode(B.fnodes, pend);
     load_strings(En, l + 1 < n, W, Vw);
     const uint4 Enn = bld4(B.ent, l + 2 < n ? 16u * (e0 + l + 2u) : RS_OOB);
-#endif
     if (!confirm_f(nf, pp, pl, Q)) return RS_EXACT;
     uint32_t cv, ck;
     if (!(nf.len_flags & FAST_OVERFLOW)) {
@@ -614,32 +611,15 @@ RL_HD uint32_t resolve_fast(const ResolveIn& in, const TreeDesc2& t, const FastB
       cv = match_chain_f(B.fslots, t.fmask, hv, wv);
       ck = match_chain_f(B.fslots, t.fmask, hk, wk);
     }
-    uint32_t nd;
-    if (cv != TREE_NONE) {
-      nd = cv;
-      pl = lv;
-    } else {
-      if (ck == TREE_NONE) return RL_NIL_RULE;  // neither edge: the walk stops (:309), nil
-      nd = ck;
-      pl = kl;
-    }
+    if (cv == TREE_NONE && ck == TREE_NONE) return RL_NIL_RULE;  // neither edge: the walk stops (:309), nil
+    const bool byv = cv != TREE_NONE;  // key "_" value first (:300-309)
+    pl = byv ? lv : kl;
 #pragma unroll
-    for (int k = 0; k < FW; ++k) Q[k] = Qn[k];  // (confirm masks it to pl bytes; K is its first kl)
+    for (int k = 0; k < FW; ++k) Q[k] = byv ? Qn[k] : K[k];
     pp = pend;
-    pend = nd;
+    pend = byv ? cv : ck;
     E = En;
     En = Enn;
-#if RL_RESOLVE_PF == 2
-    Enn = Ennn;
-#pragma unroll
-    for (int k = 0; k <= FW; ++k) {  // (W now holds level l+2's windows: rotate)
-      const uint32_t a = W[k], b = Vw[k];
-      W[k] = W2[k];
-      Vw[k] = Vw2[k];
-      W2[k] = a;
-      Vw2[k] = b;
-    }
-#endif
   }
   // the last entry's node: confirmed, and its limit (:311-318)
   const NodeF v = load_fnode(B.fnodes, pend);
