@@ -25,17 +25,28 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from bench import source_sha  # noqa: E402
 
 
-def load(pattern):
-    """kernel -> counter -> [values in dispatch order]"""
+def kname(r):
+    # (k_resolve lives in an anonymous namespace: drop that before cutting at the arguments)
+    k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
+    return k.split("::")[-1].replace("void ", "").strip()
+
+
+def load(pattern, timed=0):
+    """kernel -> counter -> [values in dispatch order]. timed > 0: per pass, only the dispatches
+    after the k4_group of the batch before the last `timed` ones (the timed region: the LSD
+    pipeline's prefill fallbacks and other prefill work drop out, whatever their count)."""
     rows = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(pattern):
         recs = list(csv.DictReader(open(f)))
         recs.sort(key=lambda r: int(r.get("Dispatch_Id", 0) or 0))
+        t0 = -1
+        if timed:
+            g = sorted({int(r.get("Dispatch_Id", 0) or 0) for r in recs if kname(r) == "k4_group"})
+            if len(g) > timed:
+                t0 = g[-(timed + 1)]
         for r in recs:
-            # (k_resolve lives in an anonymous namespace: drop that before cutting at the arguments)
-            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0]
-            k = k.split("::")[-1].replace("void ", "").strip()
-            rows[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            if int(r.get("Dispatch_Id", 0) or 0) > t0:
+                rows[kname(r)][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return rows
 
 
@@ -44,7 +55,7 @@ def mean_last(v, n):
     return sum(v) / len(v) if v else 0.0
 
 
-bench_rows = load(f"{root}/p*/run_counter_collection.csv")
+bench_rows = load(f"{root}/p*/run_counter_collection.csv", steps)
 # the bench's workload generator (tools/gen/workload_gen.hip) and roofline probe: not the path
 NOT_ENGINE = ("k_keys", "k_bytes", "k_bytes4", "k_copy", "k_slot_rmw")
 kernels = {}
