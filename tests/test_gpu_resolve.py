@@ -202,3 +202,34 @@ def test_resolve_long_names_and_shifted_blob_gpu():
         eng.resolve_device(s, out.data_ptr())
         torch.cuda.synchronize()
         assert [have(r) for r in out.cpu().numpy().view(np.uint32)] == want, shift
+
+
+@pytest.mark.parametrize("layout,sep", [("prefix", "_"), ("prefix", ":"), ("dedup", "_")])
+def test_resolve_fast_tree_layouts_and_overflow_gpu(layout, sep):
+    """k_resolve's first pass on the device over its breadth-first tree: a domain whose 20
+    children live in the fast edge table, nodes with 8 inline children, misses at both levels;
+    the batch laid out as cache-key prefixes (one load window per key "_" value), with another
+    separator (left to the exact walk, never misread as key "_" value), and deduplicated
+    strings. Against GetLimit (tests/test_resolve_host.py runs the same walk on the host)."""
+    from test_resolve_host import _wide_yaml
+    y = _wide_yaml()
+    cfg = rl_config.RateLimitConfig([("w.yaml", y)])
+    orc = config_oracle.Config([("w.yaml", y)])
+    rng = np.random.default_rng(17)
+    descs = []
+    for _ in range(20_000):
+        ents = [("k", f"v{int(rng.integers(0, 24))}")]
+        if rng.random() < 0.7:
+            ents.append(("s", str(int(rng.integers(0, 10)))))
+        if rng.random() < 0.1:
+            ents.append(("t", "x"))
+        descs.append(("wide" if rng.random() < 0.97 else "narrow", ents))
+    eng = hiprl.Engine()
+    cfg.install(eng)
+    got = eng.resolve(rl_config.ResolveBatch([(d, e, None) for d, e in descs], layout=layout, sep=sep))
+    want = [_limit_tuple(orc.get_limit(d, e)) for d, e in descs]
+    have = [_rule_tuple(cfg, r) for r in got]
+    bad = [i for i, (a, b) in enumerate(zip(have, want)) if a != b]
+    assert not bad, f"{len(bad)} differ; first {descs[bad[0]]}: {have[bad[0]]} vs {want[bad[0]]}"
+    assert sum(w is not None for w in want) > 5_000
+
