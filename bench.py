@@ -603,11 +603,19 @@ def main():
         pend = 0
         hprev = 0.0
         rdepth = RDEPTH if depth is None else depth
+        # config 4: every batch's rule ids resolved on the device inside the step, one batch ahead
+        # (batch k+1's right after batch k's submit, so it can run beside k's kernels; each batch
+        # has its own rule array, and the engine orders a submit after the resolves before it)
+        # (RL_BENCH_RESOLVE_LATE=1, diagnostics: each batch resolved just before its own submit)
+        late = os.environ.get("RL_BENCH_RESOLVE_LATE") == "1"
+        resolve4 = args.config == 4 and nrt is None and rtr is None and not late
+        if resolve4 and dbs:
+            eng.resolve_device(gen.resolve_struct(dbs[0]), dbs[0].rule.data_ptr())
         for j, db in enumerate(dbs):
             if rtr is not None:
                 rtr.step(db)
                 continue
-            if args.config == 4 and nrt is None:
+            if late and args.config == 4 and nrt is None:
                 eng.resolve_device(gen.resolve_struct(db), db.rule.data_ptr())
             sb = hiprl.Engine.device_batch(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs())
             o, t = outs[(first + j) % len(outs)].data_ptr(), thrs[(first + j) % len(thrs)].data_ptr()
@@ -628,6 +636,8 @@ def main():
                     host_t["step"].append(h0 - hprev)
                 hprev = h0
                 eng.submit_pipelined_batch(sb, o, t)
+                if resolve4 and j + 1 < len(dbs):
+                    eng.resolve_device(gen.resolve_struct(dbs[j + 1]), dbs[j + 1].rule.data_ptr())
                 h1 = time.perf_counter()
                 host_t["submit"].append(h1 - h0)
                 pend += 1
@@ -637,6 +647,8 @@ def main():
                     pend -= 1
             else:
                 eng.submit_device_async(db.n_desc, db.n_req, db.blob_bytes(), db.ptrs(), o, t)
+                if resolve4 and j + 1 < len(dbs):
+                    eng.resolve_device(gen.resolve_struct(dbs[j + 1]), dbs[j + 1].rule.data_ptr())
                 eng.wait()
         for _ in range(pend):
             if nrt is not None:
