@@ -547,8 +547,9 @@ def main():
         tree = rl_config.RateLimitConfig([("config4.yaml", workload.config4_yaml(4))])
         rules = [(r[0], r[1], k % 2 == 0) for k, r in enumerate(tree.rule_table())]  # every other rule shadow
         wl = ("config4: 1e9 keys Zipf s=1.1, 4-entry descriptors (a, b, c, d) resolved on the device in every step "
-              "(rl_resolve_device) by a 4-level descriptor tree (workload.config4_yaml(4)), local over-limit cache on, "
-              "every other rule in shadow mode, 1 descriptor/request")
+              "(rl_resolve_device; batch k+1's right after batch k's submit) by a 4-level descriptor tree "
+              "(workload.config4_yaml(4)), local over-limit cache on, every other rule in shadow mode, "
+              "1 descriptor/request")
     elif args.config == 5:
         rules, log2 = workload.CONFIG5_RULES, (lg, lg, lg, 12)
         wl = (f"config5: 60 simulated seconds ({K} batches per second, 59 s of prefill), 1e8 keys Zipf s=1.1, "
