@@ -16,8 +16,9 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 n_show = int(sys.argv[2]) if len(sys.argv) > 2 else 16
 ks = []
 for r in rows:
-    name = r["Kernel_Name"].split("(")[0].split("<")[0].split("::")[-1].replace("void ", "").strip()
-    if name.startswith("k4_"):
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("<")[0].split("::")[-1]
+    name = name.replace("void ", "").strip()
+    if name.startswith("k4_") or name == "k_resolve":  # (config 4: the resolve of each batch too)
         q = r.get("Queue_Id") or r.get("Stream_Id") or "?"
         ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, q))
 ks.sort()
